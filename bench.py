@@ -1,0 +1,209 @@
+"""Headline benchmark: simulated peer-rounds/s and HBM GB/s of a 10M-peer
+Plumtree broadcast to convergence (BASELINE.json `metric`).
+
+A step = one heartbeat broadcast from a fresh tree to quiescence:
+  psim_plumtree_reset_trees (an update with new members, Q2)
+  -> psim_plumtree_broadcast(root)  (origin eager push, round 0)
+  -> psim_run                       (rounds until nothing is in flight and no
+                                      outstanding i_have row to a live peer)
+value = n_peers * rounds / step time, summed over ranks.  The overlay is
+resident in HBM before the timed region; nothing crosses PCIe inside it
+except the per-chunk 8 KB counter read-back the round driver needs.
+
+Roofline: dominant kernel pt_round_kernel, HBM-bound; achieved = SURVEY 8(d)
+algorithmic bytes of the timed rounds / their summed hipEvent durations
+(events on the library's own stream).  cpu_baseline: the C oracle (a
+scalar port of the reference modules) on a bounded sample of the same
+workload, rank 0 only.
+
+Multi-GPU (round 1): every rank runs an independent replica of the workload
+on its own GPU ("parallelism": "replicas"); the vertex-sharded RCCL exchange
+is the next step (DESIGN.md "Multi-GPU").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "simulated peer-rounds/sec + HBM GB/s at 10M-peer plumtree broadcast, 1–8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--n", type=int, default=10_000_000)
+    p.add_argument("--peers", type=int, default=5)
+    p.add_argument("--seed", type=int, default=0x5EED0001)
+    p.add_argument("--lazy-tick-rounds", type=int, default=1)
+    p.add_argument("--cpu-sample-n", type=int, default=1_000_000)
+    p.add_argument("--cpu-sample-reps", type=int, default=3)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="per-launch HBM bytes measured by tools/pmc_traffic.py for this workload")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+        pg = dist
+    return rank, local, world, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def max_over_ranks(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def one_step(sim, root):
+    sim.reset_trees()
+    sim.broadcast(root)
+    return sim.run()
+
+
+def cpu_baseline(args):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from partisan_amd import overlay
+    rp, col = overlay.random_regular(args.cpu_sample_n, args.peers, args.seed)
+    tot_t, tot_pr = 0.0, 0
+    rounds = 0
+    for _ in range(args.cpu_sample_reps):
+        orc = O.Plumtree(rp, col, args.lazy_tick_rounds)
+        t0 = time.perf_counter()
+        orc.heartbeat(0)
+        _, rounds = orc.run()
+        tot_t += time.perf_counter() - t0
+        tot_pr += args.cpu_sample_n * rounds
+        orc.close()
+    return {
+        "value": tot_pr / tot_t, "unit": "peer-rounds/s", "cores": 1, "kind": "port",
+        "sample": (f"C oracle (oracle/plumtree.c), {args.cpu_sample_reps} floods of a "
+                   f"{args.cpu_sample_n}-peer random {args.peers}-peer overlay to quiescence "
+                   f"({rounds} rounds each), single thread, {tot_t:.1f} s"),
+    }
+
+
+def main():
+    args = parse()
+    rank, local, world, pg = dist_setup(args)
+    import numpy as np  # noqa: F401
+
+    import partisan_amd as pa
+
+    rp, col = pa.overlay.random_regular(args.n, args.peers, args.seed)
+    sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
+    sim.load_overlay(rp, col)
+    del rp, col
+    root = 0
+
+    for _ in range(args.warmup):
+        one_step(sim, root)
+
+    algo_bytes = 0
+    round_ms = 0.0
+    rounds_per_step = []
+    barrier(pg)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stats, rounds = one_step(sim, root)
+        rounds_per_step.append(rounds)
+        algo_bytes += sum(s["algo_bytes"] for s in stats)
+        round_ms += sum(s["kernel_ms"] for s in stats)
+    # psim_run returns after hipStreamSynchronize on the library stream
+    barrier(pg)
+    t1 = time.perf_counter()
+
+    step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
+    peer_rounds = sum_over_ranks(pg, float(args.n) * sum(rounds_per_step) / args.steps)
+    value = peer_rounds / step_s
+    # per-launch figures over the rounds up to quiescence (the no-op tail of a
+    # step's last chunk is not counted): hipEvent durations of each launch
+    counted = sum(rounds_per_step)
+    avg_launch_ms = round_ms / max(1, counted)
+    achieved_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("n") == args.n and tj.get("peers") == args.peers:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "peer-rounds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": step_s * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"{args.n}-peer Plumtree broadcast to convergence: heartbeat from a fresh "
+                             f"tree (reset_peers), flood + prune, lazy tick every "
+                             f"{args.lazy_tick_rounds} round(s)"),
+                "n_peers": args.n,
+                "overlay": f"random symmetric, {args.peers} peers per vertex (HyParView active view)",
+                "rounds_to_convergence": rounds_per_step[-1],
+                "parallelism": "replicas" if world > 1 else "single",
+                "device": sim.device_info(),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "pt_round_kernel",
+                "avg_launch_us": avg_launch_ms * 1e3,
+                "algo_bytes_per_launch": algo_bytes / max(1, counted),
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    sim.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

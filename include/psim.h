@@ -1,0 +1,139 @@
+/*
+ * psim.h -- C ABI of libpsim.so, the MI355X-native round-synchronous
+ * simulator of Partisan's gossip hot path (loong/partisan).
+ *
+ * This is the drop-in boundary: the Erlang NIF `partisan_gpu_sim`
+ * (erl/c_src/partisan_gpu_sim_nif.c) and the Python
+ * host mirror (partisan_amd/) both bind exactly these symbols.  Plain
+ * pointers and sizes only; no exceptions cross the ABI.
+ *
+ * Ownership: a handle owns all device memory it allocates; callers own
+ * every host buffer they pass in or out (inputs are copied).
+ * Threading: one handle is single-threaded (callers serialise, the NIF
+ * holds a per-resource mutex); distinct handles may run concurrently.
+ * Errors: 0 = PSIM_OK, negative PSIM_E* otherwise; psim_strerror() names
+ * them and psim_last_error() returns a per-handle detail string.
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef PSIM_H
+#define PSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSIM_ABI_VERSION 1u
+
+#define PSIM_OK         0
+#define PSIM_EINVAL    (-1)   /* bad argument / shape                        */
+#define PSIM_ENOMEM    (-2)   /* device or host allocation failed            */
+#define PSIM_EHIP      (-3)   /* HIP runtime error                           */
+#define PSIM_ERCCL     (-4)   /* RCCL error (sharded handles)                */
+#define PSIM_ESTATE    (-5)   /* call not valid in the current state         */
+#define PSIM_EOVERFLOW (-6)   /* a fixed-capacity structure overflowed       */
+#define PSIM_EBUSY     (-7)   /* previous broadcast has not reached quiescence */
+#define PSIM_ENODEV    (-8)   /* no HIP device / kernel image for this GPU   */
+
+/* Message kinds of the Plumtree protocol (partisan_plumtree_broadcast.erl
+ * send sites); index of psim_round_stats.sent[]. */
+#define PSIM_MSG_BROADCAST 1  /* {broadcast, Id, Payload, Mod, Round, Root, From} :965-969, :893-897 */
+#define PSIM_MSG_PRUNE     2  /* {prune, Root, From}                   :849      */
+#define PSIM_MSG_IHAVE     3  /* {i_have, Id, Mod, Round, Root, From}  :1030     */
+#define PSIM_MSG_IGNORED   4  /* {ignored_i_have, ...}                 :863-867  */
+#define PSIM_MSG_GRAFT     5  /* {graft, ...}                          :873-875  */
+
+typedef struct psim_handle psim_handle;
+
+/* Simulation parameters.  Timer periods are in rounds; the reference's
+ * millisecond periods map onto rounds keeping their ratios (DESIGN.md
+ * "Schedule"): lazy_tick_period 1000 ms (partisan.hrl:280),
+ * exchange_tick_period 10000 ms (partisan.hrl:281). */
+typedef struct psim_config {
+    uint32_t abi_version;          /* must be PSIM_ABI_VERSION                 */
+    int32_t  device;               /* HIP device ordinal; -1 = current device  */
+    uint32_t lazy_tick_rounds;     /* lazy tick every k rounds (>= 1)          */
+    uint32_t exchange_tick_rounds; /* accepted for config parity; no effect */
+    uint32_t flags;                /* reserved, 0                              */
+    uint32_t _reserved;
+    uint64_t seed;                 /* Philox key for the protocols that draw   */
+} psim_config;
+
+/* Per-round counters, reduced on device (psim_step / psim_run). */
+typedef struct psim_round_stats {
+    uint64_t sent[6];              /* messages emitted, by PSIM_MSG_* kind     */
+    uint64_t delivered_new;        /* Mod:merge/2 returned true                */
+    uint64_t active;               /* vertices that processed messages/ticks  */
+    uint64_t senders;              /* vertices that emitted >= 1 message       */
+    uint64_t sender_degree_sum;    /* sum of deg(v) over senders               */
+    uint64_t outstanding_vertices; /* vertices holding outstanding i_have rows */
+    uint64_t algo_bytes;           /* SURVEY 8(d) bytes: 16N + sum(8+4deg) + 32 msgs */
+    double   kernel_ms;            /* device time of this round's kernel (hipEvent) */
+} psim_round_stats;
+
+/* --- lifecycle -------------------------------------------------------- */
+/* Replaces gen_server:start_link of partisan_plumtree_broadcast
+ * (partisan_plumtree_broadcast.erl:234-260, init/1 :487-515). */
+int  psim_create(const psim_config* cfg, psim_handle** out);
+int  psim_destroy(psim_handle* h);
+const char* psim_strerror(int code);
+const char* psim_last_error(const psim_handle* h);
+/* Writes the device name and arch (e.g. "gfx950") into buf. */
+int  psim_device_info(const psim_handle* h, char* buf, size_t cap);
+
+/* --- overlay / membership ------------------------------------------- */
+/* Loads every vertex's membership list (the peer service's members minus
+ * self: partisan_peer_service:members/0, consumed by start_link/0 :234-260)
+ * as a CSR: row_ptr[n+1], col[row_ptr[n]].  Copied.  Plumtree's peers of v
+ * are the union of v's members and of the vertices listing v (a message can
+ * only arrive over such an edge); at most 32 per vertex. */
+int  psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col);
+/* Number of peer slots (directed edges of the symmetrised overlay). */
+int  psim_num_slots(const psim_handle* h, uint64_t* out);
+/* The slot layout used by every per-vertex mask below: row_ptr[n+1], col[E]
+ * (sorted by id within a row). */
+int  psim_get_slots(const psim_handle* h, uint64_t* row_ptr, uint32_t* col);
+/* alive[n] bytes (1 = up).  A dead vertex drops its inbox and fires no timer;
+ * partisan:is_connected/1 on a dead peer is false. */
+int  psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
+
+/* --- Plumtree --------------------------------------------------------- */
+/* Every vertex handles a membership update that adds members: reset_peers/4
+ * drops all per-root eager/lazy sets (partisan_plumtree_broadcast.erl:607-639,
+ * :1320-1328).  O(1): sets are tagged with a tree epoch. */
+int  psim_plumtree_reset_trees(psim_handle* h);
+/* Heartbeat at `root`: partisan_plumtree_backend handle_info(heartbeat)
+ * (:341-368) -> partisan_plumtree_broadcast:broadcast/2 (:324-326) ->
+ * handle_cast({broadcast, Id, Payload, Mod}) (:565-569).  Emits round-0
+ * eager pushes delivered by the next step.  *mono_out = the Monotonic of
+ * the id {Root, Epoch, Monotonic}.  PSIM_EBUSY if the previous broadcast is
+ * not quiescent. */
+int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
+/* Runs exactly `rounds` rounds.  stats may be NULL; otherwise stats[cap]. */
+int  psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap);
+/* Runs until quiescent (nothing in flight and no outstanding i_have row to
+ * a live peer) or max_rounds; *rounds_run = rounds executed. */
+int  psim_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_t cap,
+              uint32_t* rounds_run);
+/* Per-vertex Plumtree state for the current root, masks over the vertex's
+ * slots (bit s = col[row_ptr[v] + s]): all_eager_peers / all_lazy_peers
+ * (:1252-1282), outstanding rows (:1215-1219), the Round of the accepted
+ * broadcast (0xFFFF: not delivered; 0xFFFE: the root).  Any pointer may be NULL. */
+int  psim_get_plumtree(const psim_handle* h, uint32_t* eager, uint32_t* lazy,
+                       uint32_t* outstanding, uint16_t* recv_round, size_t n);
+/* delivered[n] bytes: Mod:is_stale(Id) for the current heartbeat (backend :229-244). */
+int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
+/* Messages in flight (delivered by the next round), one word per slot of the
+ * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
+ * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
+int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* Totals since creation: device ms spent in round kernels and rounds run. */
+int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSIM_H */

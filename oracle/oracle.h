@@ -1,0 +1,160 @@
+/*
+ * oracle.h -- CPU restatement of Partisan's gossip hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is linked into, loaded by
+ * or called from the product library (partisan_amd/libpsim.so).  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * liboracle.so, and only as the checker / the timed CPU baseline.
+ *
+ * Every function cites the reference file:line it restates
+ * (reference = loong/partisan, Erlang; no Erlang runtime exists in this
+ * image, so the reference cannot be run: parity is pinned by the
+ * reference's own eunit known-answer tests, transcribed as data under
+ * tests/golden/, see DESIGN.md "Oracle").
+ */
+#ifndef PSIM_ORACLE_H
+#define PSIM_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ */
+/* partisan_interval_sets (src/partisan_interval_sets.erl)            */
+/* ------------------------------------------------------------------ */
+/* An element is an integer N (iv == 0, lo == hi == N) or a closed
+ * interval {lo, hi} (iv == 1).  Erlang distinguishes the term N from the
+ * term {N, N}; so do we, because the eunit KATs compare exact terms.   */
+typedef struct orc_iel {
+    int64_t lo, hi;
+    int32_t iv;
+    int32_t _pad;
+} orc_iel;
+
+#define ORC_OK      0
+#define ORC_BADARG (-1)   /* error(badarg) / error({badarg, E}) in Erlang  */
+#define ORC_NOSPACE (-2)  /* caller's output array too small             */
+
+int orc_iset_from_list(const orc_iel* in, size_t n, orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_is_element(const orc_iel* a, const orc_iel* set, size_t n);   /* 1/0, <0 error */
+int orc_iset_add_element(const orc_iel* a, const orc_iel* set, size_t n,
+                         orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_del_element(const orc_iel* a, const orc_iel* set, size_t n,
+                         orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_element_subtract(const orc_iel* a, const orc_iel* b,
+                              orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_element_precedes(const orc_iel* a, const orc_iel* b);
+int orc_iset_element_meets(const orc_iel* a, const orc_iel* b);
+int64_t orc_iset_flat_size(const orc_iel* set, size_t n);
+int64_t orc_iset_min(const orc_iel* set, size_t n);
+int64_t orc_iset_max(const orc_iel* set, size_t n);
+int orc_iset_is_type(const orc_iel* set, size_t n);
+int orc_iset_seq(const orc_iel* set, size_t n, int64_t* out, size_t cap, size_t* out_n);
+int orc_iset_union(const orc_iel* a, size_t na, const orc_iel* b, size_t nb,
+                   orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_intersection(const orc_iel* a, size_t na, const orc_iel* b, size_t nb,
+                          orc_iel* out, size_t cap, size_t* out_n);
+int orc_iset_subtract(const orc_iel* a, size_t na, const orc_iel* b, size_t nb,
+                      orc_iel* out, size_t cap, size_t* out_n);
+
+/* ------------------------------------------------------------------ */
+/* partisan_vclock (src/partisan_vclock.erl) -- sparse [{Actor, Ctr}] */
+/* ------------------------------------------------------------------ */
+typedef struct orc_dot {
+    uint32_t actor;
+    uint32_t _pad;
+    int64_t ctr;
+} orc_dot;
+
+int orc_vc_descends(const orc_dot* a, size_t na, const orc_dot* b, size_t nb);
+int orc_vc_dominates(const orc_dot* a, size_t na, const orc_dot* b, size_t nb);
+/* merge(VClocks): clocks given as a concatenation with per-clock lengths */
+int orc_vc_merge(const orc_dot* flat, const size_t* lens, size_t nclocks,
+                 orc_dot* out, size_t cap, size_t* out_n);
+int64_t orc_vc_get_counter(uint32_t actor, const orc_dot* a, size_t na);
+int orc_vc_increment(uint32_t actor, const orc_dot* a, size_t na,
+                     orc_dot* out, size_t cap, size_t* out_n);
+int orc_vc_equal(const orc_dot* a, size_t na, const orc_dot* b, size_t nb);
+int orc_vc_all_nodes(const orc_dot* a, size_t na, uint32_t* out, size_t cap, size_t* out_n);
+int orc_vc_glb(const orc_dot* a, size_t na, const orc_dot* b, size_t nb,
+               orc_dot* out, size_t cap, size_t* out_n);
+int orc_vc_subtract_dots(const orc_dot* dots, size_t nd, const orc_dot* clock, size_t nc,
+                         orc_dot* out, size_t cap, size_t* out_n);
+
+/* ------------------------------------------------------------------ */
+/* partisan_plumtree_util:build_tree/3 (src/partisan_plumtree_util.erl:43-58) */
+/* ------------------------------------------------------------------ */
+/* nodes: the list (term order == array order given); out_children is
+ * n_nodes * arity entries, out_counts[i] = number of children of the i-th
+ * node of the orddict (sorted by node value); out_keys[i] = that node.    */
+int orc_build_tree(uint32_t arity, const uint32_t* nodes, size_t n_nodes, int cycles,
+                   uint32_t* out_keys, uint32_t* out_children, uint32_t* out_counts);
+
+/* ------------------------------------------------------------------ */
+/* Plumtree broadcast + heartbeat backend, round-synchronous           */
+/* (src/partisan_plumtree_broadcast.erl, src/partisan_plumtree_backend.erl) */
+/* ------------------------------------------------------------------ */
+enum {
+    ORC_MSG_BROADCAST = 1,   /* {broadcast, Id, Payload, Mod, Round, Root, From} */
+    ORC_MSG_PRUNE     = 2,   /* {prune, Root, From}                              */
+    ORC_MSG_IHAVE     = 3,   /* {i_have, Id, Mod, Round, Root, From}             */
+    ORC_MSG_IGNORED   = 4,   /* {ignored_i_have, Id, Mod, Round, Root, From}     */
+    ORC_MSG_GRAFT     = 5    /* {graft, Id, Mod, Round, Root, From}              */
+};
+
+typedef struct orc_msg {
+    uint32_t type, src, dst, round;
+    uint32_t root;
+    uint32_t id_node;        /* heartbeat id {Node, Epoch, Monotonic}   */
+    uint32_t id_epoch;
+    uint32_t id_mono;
+    uint64_t seq;            /* per-sender emission counter             */
+} orc_msg;
+
+typedef struct orc_round_stats {
+    uint64_t sent[6];        /* indexed by ORC_MSG_*                    */
+    uint64_t delivered_new;  /* merge/2 returned true this round        */
+    uint64_t active;         /* vertices that processed >=1 msg or tick */
+    uint64_t outstanding;    /* outstanding rows after the round        */
+    uint64_t outstanding_live; /* rows whose peer is alive (connected)  */
+    uint64_t max_per_edge;   /* max msgs on one (src,dst) in the round  */
+} orc_round_stats;
+
+typedef struct orc_plumtree orc_plumtree;
+
+/* members: CSR of each vertex's membership list as the peer service hands
+ * it to plumtree (self NOT included; reset_peers removes self anyway).    */
+orc_plumtree* orc_pt_create(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
+                            uint32_t lazy_tick_rounds);
+void orc_pt_destroy(orc_plumtree* s);
+void orc_pt_set_alive(orc_plumtree* s, const uint8_t* alive);
+/* heartbeat from `root` (partisan_plumtree_backend.erl:341-368); returns the Monotonic */
+uint32_t orc_pt_heartbeat(orc_plumtree* s, uint32_t root);
+/* {update, Members} cast for vertex v (partisan_plumtree_broadcast.erl:607-639) */
+int orc_pt_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n);
+/* every vertex: reset_peers(AllMembers, CommonEagers, CommonLazys), i.e. what
+ * an {update, Members} with new members does to the per-root sets (Q2) */
+void orc_pt_reset_peers_all(orc_plumtree* s);
+/* run `rounds` rounds; stats[i] filled for each; returns rounds run */
+uint32_t orc_pt_step(orc_plumtree* s, uint32_t rounds, orc_round_stats* stats);
+/* run until quiescent: no message in flight and no outstanding row to a live
+ * peer (rows to dead peers persist until an update removes them, Q5) */
+uint32_t orc_pt_run(orc_plumtree* s, uint32_t max_rounds, orc_round_stats* stats, size_t cap);
+size_t orc_pt_pending(const orc_plumtree* s, orc_msg* out, size_t cap);
+int orc_pt_get_peers(const orc_plumtree* s, uint32_t v, uint32_t root,
+                     uint32_t* eager, size_t* ne, uint32_t* lazy, size_t* nl, size_t cap);
+/* outstanding rows of v: (peer, round) pairs for message (root, mono) */
+size_t orc_pt_get_outstanding(const orc_plumtree* s, uint32_t v, uint32_t* peers,
+                              uint32_t* rounds, uint32_t* monos, size_t cap);
+/* delivered bitmap for heartbeat (origin, mono): 1 byte per vertex */
+void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint8_t* out);
+/* Round field of the broadcast each vertex accepted for (origin, mono); 0xFFFFFFFF if none */
+void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

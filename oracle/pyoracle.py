@@ -1,0 +1,339 @@
+"""ctypes wrapper around oracle/liboracle.so.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package partisan_amd.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class IEl(C.Structure):
+    _fields_ = [("lo", C.c_int64), ("hi", C.c_int64), ("iv", C.c_int32), ("_pad", C.c_int32)]
+
+
+class Dot(C.Structure):
+    _fields_ = [("actor", C.c_uint32), ("_pad", C.c_uint32), ("ctr", C.c_int64)]
+
+
+class Msg(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("src", C.c_uint32), ("dst", C.c_uint32), ("round", C.c_uint32),
+                ("root", C.c_uint32), ("id_node", C.c_uint32), ("id_epoch", C.c_uint32),
+                ("id_mono", C.c_uint32), ("seq", C.c_uint64)]
+
+
+class RoundStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 6), ("delivered_new", C.c_uint64), ("active", C.c_uint64),
+                ("outstanding", C.c_uint64), ("outstanding_live", C.c_uint64),
+                ("max_per_edge", C.c_uint64)]
+
+
+MSG_NAMES = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        sz = C.c_size_t
+        L.orc_iset_from_list.argtypes = [P(IEl), sz, P(IEl), sz, P(sz)]
+        L.orc_iset_is_element.argtypes = [P(IEl), P(IEl), sz]
+        L.orc_iset_add_element.argtypes = [P(IEl), P(IEl), sz, P(IEl), sz, P(sz)]
+        L.orc_iset_del_element.argtypes = [P(IEl), P(IEl), sz, P(IEl), sz, P(sz)]
+        L.orc_iset_element_subtract.argtypes = [P(IEl), P(IEl), P(IEl), sz, P(sz)]
+        L.orc_iset_element_precedes.argtypes = [P(IEl), P(IEl)]
+        L.orc_iset_element_meets.argtypes = [P(IEl), P(IEl)]
+        for f in ("orc_iset_flat_size", "orc_iset_min", "orc_iset_max"):
+            getattr(L, f).argtypes = [P(IEl), sz]
+            getattr(L, f).restype = C.c_int64
+        L.orc_iset_is_type.argtypes = [P(IEl), sz]
+        L.orc_iset_seq.argtypes = [P(IEl), sz, P(C.c_int64), sz, P(sz)]
+        for f in ("orc_iset_union", "orc_iset_intersection", "orc_iset_subtract"):
+            getattr(L, f).argtypes = [P(IEl), sz, P(IEl), sz, P(IEl), sz, P(sz)]
+        L.orc_vc_descends.argtypes = [P(Dot), sz, P(Dot), sz]
+        L.orc_vc_dominates.argtypes = [P(Dot), sz, P(Dot), sz]
+        L.orc_vc_merge.argtypes = [P(Dot), P(sz), sz, P(Dot), sz, P(sz)]
+        L.orc_vc_get_counter.argtypes = [C.c_uint32, P(Dot), sz]
+        L.orc_vc_get_counter.restype = C.c_int64
+        L.orc_vc_increment.argtypes = [C.c_uint32, P(Dot), sz, P(Dot), sz, P(sz)]
+        L.orc_vc_equal.argtypes = [P(Dot), sz, P(Dot), sz]
+        L.orc_vc_all_nodes.argtypes = [P(Dot), sz, P(C.c_uint32), sz, P(sz)]
+        L.orc_vc_glb.argtypes = [P(Dot), sz, P(Dot), sz, P(Dot), sz, P(sz)]
+        L.orc_vc_subtract_dots.argtypes = [P(Dot), sz, P(Dot), sz, P(Dot), sz, P(sz)]
+        L.orc_build_tree.argtypes = [C.c_uint32, P(C.c_uint32), sz, C.c_int,
+                                     P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+        L.orc_pt_create.argtypes = [C.c_uint32, P(C.c_uint64), P(C.c_uint32), C.c_uint32]
+        L.orc_pt_create.restype = C.c_void_p
+        L.orc_pt_destroy.argtypes = [C.c_void_p]
+        L.orc_pt_set_alive.argtypes = [C.c_void_p, P(C.c_uint8)]
+        L.orc_pt_heartbeat.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_pt_heartbeat.restype = C.c_uint32
+        L.orc_pt_update.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), sz]
+        L.orc_pt_reset_peers_all.argtypes = [C.c_void_p]
+        L.orc_pt_step.argtypes = [C.c_void_p, C.c_uint32, P(RoundStats)]
+        L.orc_pt_step.restype = C.c_uint32
+        L.orc_pt_run.argtypes = [C.c_void_p, C.c_uint32, P(RoundStats), sz]
+        L.orc_pt_run.restype = C.c_uint32
+        L.orc_pt_pending.argtypes = [C.c_void_p, P(Msg), sz]
+        L.orc_pt_pending.restype = sz
+        L.orc_pt_get_peers.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32), P(sz),
+                                       P(C.c_uint32), P(sz), sz]
+        L.orc_pt_get_outstanding.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32),
+                                             P(C.c_uint32), sz]
+        L.orc_pt_get_outstanding.restype = sz
+        L.orc_pt_get_delivered.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint8)]
+        L.orc_pt_get_recv_round.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------- interval sets
+def _to_iels(terms):
+    arr = (IEl * max(1, len(terms)))()
+    for i, t in enumerate(terms):
+        if isinstance(t, (list, tuple)):
+            arr[i].lo, arr[i].hi, arr[i].iv = t[0], t[1], 1
+        else:
+            arr[i].lo, arr[i].hi, arr[i].iv = t, t, 0
+    return arr
+
+
+def _from_iels(arr, n):
+    out = []
+    for i in range(n):
+        e = arr[i]
+        out.append([e.lo, e.hi] if e.iv else e.lo)
+    return out
+
+
+def _iset_call(fn, *args, cap=256):
+    out = (IEl * cap)()
+    n = C.c_size_t(0)
+    rc = fn(*args, out, cap, C.byref(n))
+    if rc < 0:
+        raise ValueError("badarg")
+    return _from_iels(out, n.value)
+
+
+def iset_from_list(terms):
+    return _iset_call(lib().orc_iset_from_list, _to_iels(terms), len(terms))
+
+
+def iset_is_element(el, s):
+    rc = lib().orc_iset_is_element(_to_iels([el]), _to_iels(s), len(s))
+    if rc < 0:
+        raise ValueError("badarg")
+    return bool(rc)
+
+
+def iset_add_element(el, s):
+    return _iset_call(lib().orc_iset_add_element, _to_iels([el]), _to_iels(s), len(s))
+
+
+def iset_del_element(el, s):
+    return _iset_call(lib().orc_iset_del_element, _to_iels([el]), _to_iels(s), len(s))
+
+
+def iset_element_subtract(a, b):
+    return _iset_call(lib().orc_iset_element_subtract, _to_iels([a]), _to_iels([b]))
+
+
+def iset_element_precedes(a, b):
+    return bool(lib().orc_iset_element_precedes(_to_iels([a]), _to_iels([b])))
+
+
+def iset_element_meets(a, b):
+    return bool(lib().orc_iset_element_meets(_to_iels([a]), _to_iels([b])))
+
+
+def iset_flat_size(s):
+    return lib().orc_iset_flat_size(_to_iels(s), len(s))
+
+
+def iset_min(s):
+    return lib().orc_iset_min(_to_iels(s), len(s))
+
+
+def iset_max(s):
+    return lib().orc_iset_max(_to_iels(s), len(s))
+
+
+def iset_is_type(s):
+    return bool(lib().orc_iset_is_type(_to_iels(s), len(s)))
+
+
+def iset_seq(s, cap=4096):
+    out = (C.c_int64 * cap)()
+    n = C.c_size_t(0)
+    lib().orc_iset_seq(_to_iels(s), len(s), out, cap, C.byref(n))
+    return list(out[: n.value])
+
+
+def iset_union(a, b):
+    return _iset_call(lib().orc_iset_union, _to_iels(a), len(a), _to_iels(b), len(b))
+
+
+def iset_subtract(a, b):
+    return _iset_call(lib().orc_iset_subtract, _to_iels(a), len(a), _to_iels(b), len(b))
+
+
+# ---------------------------------------------------------------- vclock
+def _to_dots(clock):
+    arr = (Dot * max(1, len(clock)))()
+    for i, (a, c) in enumerate(clock):
+        arr[i].actor, arr[i].ctr = a, c
+    return arr
+
+
+def _from_dots(arr, n):
+    return [[arr[i].actor, arr[i].ctr] for i in range(n)]
+
+
+def vc_descends(a, b):
+    return bool(lib().orc_vc_descends(_to_dots(a), len(a), _to_dots(b), len(b)))
+
+
+def vc_dominates(a, b):
+    return bool(lib().orc_vc_dominates(_to_dots(a), len(a), _to_dots(b), len(b)))
+
+
+def vc_merge(clocks):
+    flat = [d for c in clocks for d in c]
+    lens = (C.c_size_t * max(1, len(clocks)))(*[len(c) for c in clocks])
+    cap = max(1, len(flat))
+    out = (Dot * cap)()
+    n = C.c_size_t(0)
+    lib().orc_vc_merge(_to_dots(flat), lens, len(clocks), out, cap, C.byref(n))
+    return _from_dots(out, n.value)
+
+
+def vc_get_counter(actor, clock):
+    return lib().orc_vc_get_counter(actor, _to_dots(clock), len(clock))
+
+
+def vc_increment(actor, clock):
+    cap = len(clock) + 1
+    out = (Dot * cap)()
+    n = C.c_size_t(0)
+    lib().orc_vc_increment(actor, _to_dots(clock), len(clock), out, cap, C.byref(n))
+    return _from_dots(out, n.value)
+
+
+def vc_equal(a, b):
+    return bool(lib().orc_vc_equal(_to_dots(a), len(a), _to_dots(b), len(b)))
+
+
+def vc_all_nodes(clock):
+    cap = max(1, len(clock))
+    out = (C.c_uint32 * cap)()
+    n = C.c_size_t(0)
+    lib().orc_vc_all_nodes(_to_dots(clock), len(clock), out, cap, C.byref(n))
+    return list(out[: n.value])
+
+
+# ---------------------------------------------------------------- build_tree
+def build_tree(arity, nodes, cycles):
+    n = len(nodes)
+    keys = (C.c_uint32 * n)()
+    ch = (C.c_uint32 * (n * arity))()
+    cnt = (C.c_uint32 * n)()
+    lib().orc_build_tree(arity, (C.c_uint32 * n)(*nodes), n, 1 if cycles else 0, keys, ch, cnt)
+    return [[keys[i], list(ch[i * arity: i * arity + cnt[i]])] for i in range(n)]
+
+
+# ---------------------------------------------------------------- plumtree
+def _u64p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+def _u32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+class Plumtree:
+    """Round-synchronous plumtree + heartbeat backend over a membership CSR."""
+
+    def __init__(self, row_ptr, col, lazy_tick_rounds=1):
+        self.row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        self.col = np.ascontiguousarray(col, dtype=np.uint32)
+        self.n = len(self.row_ptr) - 1
+        self._h = lib().orc_pt_create(self.n, _u64p(self.row_ptr), _u32p(self.col), lazy_tick_rounds)
+
+    def close(self):
+        if self._h:
+            lib().orc_pt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        lib().orc_pt_set_alive(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def heartbeat(self, root):
+        return lib().orc_pt_heartbeat(self._h, root)
+
+    def update(self, v, members):
+        m = np.ascontiguousarray(members, dtype=np.uint32)
+        lib().orc_pt_update(self._h, v, _u32p(m), len(m))
+
+    def reset_peers_all(self):
+        lib().orc_pt_reset_peers_all(self._h)
+
+    def step(self, rounds=1):
+        st = (RoundStats * rounds)()
+        lib().orc_pt_step(self._h, rounds, st)
+        return [stats_dict(s) for s in st]
+
+    def run(self, max_rounds=100000, cap=4096):
+        st = (RoundStats * cap)()
+        r = lib().orc_pt_run(self._h, max_rounds, st, cap)
+        return [stats_dict(st[i]) for i in range(min(r, cap))], r
+
+    def pending(self):
+        n = lib().orc_pt_pending(self._h, None, 0)
+        arr = (Msg * max(1, n))()
+        lib().orc_pt_pending(self._h, arr, n)
+        return [(m.src, m.dst, m.type, m.round) for m in arr[:n]]
+
+    def peers(self, v, root, cap=4096):
+        e = (C.c_uint32 * cap)()
+        l_ = (C.c_uint32 * cap)()
+        ne, nl = C.c_size_t(0), C.c_size_t(0)
+        lib().orc_pt_get_peers(self._h, v, root, e, C.byref(ne), l_, C.byref(nl), cap)
+        return list(e[: ne.value]), list(l_[: nl.value])
+
+    def outstanding(self, v, cap=4096):
+        p = (C.c_uint32 * cap)()
+        r = (C.c_uint32 * cap)()
+        m = (C.c_uint32 * cap)()
+        n = lib().orc_pt_get_outstanding(self._h, v, p, r, m, cap)
+        return [(p[i], r[i], m[i]) for i in range(min(n, cap))]
+
+    def delivered(self, origin, mono):
+        out = np.zeros(self.n, dtype=np.uint8)
+        lib().orc_pt_get_delivered(self._h, origin, mono, out.ctypes.data_as(C.POINTER(C.c_uint8)))
+        return out
+
+    def recv_round(self, origin, mono):
+        out = np.zeros(self.n, dtype=np.uint32)
+        lib().orc_pt_get_recv_round(self._h, origin, mono, _u32p(out))
+        return out
+
+
+def stats_dict(s):
+    d = {MSG_NAMES[t]: int(s.sent[t]) for t in range(1, 6)}
+    d.update(delivered_new=int(s.delivered_new), active=int(s.active),
+             outstanding=int(s.outstanding), outstanding_live=int(s.outstanding_live),
+             max_per_edge=int(s.max_per_edge))
+    return d

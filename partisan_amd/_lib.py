@@ -1,0 +1,95 @@
+"""ctypes binding of libpsim.so (include/psim.h).
+
+The library is the product: there is no CPU fallback anywhere in this
+package.  If libpsim.so is missing or no gfx950 device is usable, the calls
+raise.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpsim.so")
+
+PSIM_ABI_VERSION = 1
+ERRORS = {
+    0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EHIP", -4: "PSIM_ERCCL",
+    -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV",
+}
+MSG_KINDS = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
+
+
+class PsimError(RuntimeError):
+    def __init__(self, code, detail=""):
+        self.code = code
+        self.name = ERRORS.get(code, str(code))
+        super().__init__(f"{self.name}: {detail}" if detail else self.name)
+
+
+class Config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("lazy_tick_rounds", C.c_uint32),
+                ("exchange_tick_rounds", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32),
+                ("seed", C.c_uint64)]
+
+
+class RoundStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 6), ("delivered_new", C.c_uint64), ("active", C.c_uint64),
+                ("senders", C.c_uint64), ("sender_degree_sum", C.c_uint64),
+                ("outstanding_vertices", C.c_uint64), ("algo_bytes", C.c_uint64), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        d = {MSG_KINDS[t]: int(self.sent[t]) for t in range(1, 6)}
+        d.update(delivered_new=int(self.delivered_new), active=int(self.active), senders=int(self.senders),
+                 sender_degree_sum=int(self.sender_degree_sum),
+                 outstanding_vertices=int(self.outstanding_vertices), algo_bytes=int(self.algo_bytes),
+                 kernel_ms=float(self.kernel_ms))
+        return d
+
+
+# every entry point of include/psim.h: name -> (restype, argtypes)
+_P = C.POINTER
+_H = C.c_void_p
+SIGNATURES = {
+    "psim_create": (C.c_int, [_P(Config), _P(C.c_void_p)]),
+    "psim_destroy": (C.c_int, [_H]),
+    "psim_strerror": (C.c_char_p, [C.c_int]),
+    "psim_last_error": (C.c_char_p, [_H]),
+    "psim_device_info": (C.c_int, [_H, C.c_char_p, C.c_size_t]),
+    "psim_load_csr": (C.c_int, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32)]),
+    "psim_num_slots": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_get_slots": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint32)]),
+    "psim_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
+    "psim_plumtree_reset_trees": (C.c_int, [_H]),
+    "psim_plumtree_broadcast": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
+    "psim_step": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t]),
+    "psim_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32)]),
+    "psim_get_plumtree": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint16),
+                                    C.c_size_t]),
+    "psim_get_delivered": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
+    "psim_get_inflight": (C.c_int, [_H, _P(C.c_uint32), C.c_uint64]),
+    "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libpsim.so once; raise loudly if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (hipcc --offload-arch=gfx950)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, h=None):
+    if rc != 0:
+        detail = lib().psim_last_error(h).decode() if h else ""
+        raise PsimError(rc, detail)
+    return rc

@@ -1,0 +1,519 @@
+// psim_host.hip -- the C ABI of libpsim.so (include/psim.h): handle
+// lifecycle, overlay upload, the round driver and the getters.
+// Device work is in plumtree.hip; nothing here computes protocol state on
+// the CPU.  There is no fallback: without a usable gfx950 device every
+// entry point that needs one returns PSIM_ENODEV / PSIM_EHIP.
+#include "psim_internal.h"
+#include "../../include/psim.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace psim;
+
+namespace {
+constexpr int kChunk = 4;   // rounds launched between host synchronisations
+constexpr size_t kStatsRow = size_t(kStatShards) * kNStat;
+}  // namespace
+
+struct psim_handle {
+    psim_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    uint32_t n = 0;
+    uint64_t E = 0;
+    std::vector<uint64_t> h_rowp;   // slot layout
+    std::vector<uint32_t> h_col;
+    std::vector<uint32_t> h_memb;
+
+    uint32_t* rowp = nullptr;
+    uint32_t* col = nullptr;
+    uint32_t* rev = nullptr;
+    uint32_t* memb = nullptr;
+    uint32_t* alive = nullptr;
+    uint4* vs = nullptr;
+    uint32_t* in[2] = {nullptr, nullptr};
+    uint8_t* pend[2] = {nullptr, nullptr};
+    uint8_t* ost = nullptr;
+    unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
+    unsigned long long* h_stats = nullptr;   // pinned mirror
+    unsigned long long* scratch = nullptr;   // 1 counter
+    hipEvent_t ev[2 * kChunk] = {};
+
+    uint32_t par = 0;          // inbox buffer the next round reads
+    uint64_t round = 0;        // rounds completed (lazy-tick schedule)
+    uint32_t serial = 0;       // heartbeat serial (device tag, low 8 bits)
+    uint32_t epoch = 1;        // tree epoch (device tag, low 8 bits)
+    uint32_t root = 0;
+    bool have_root = false;
+    std::unordered_map<uint32_t, uint32_t> mono_of;  // backend #state.monotonic per origin
+    int64_t ost_cnt = 0;       // vertices with outstanding rows
+    int64_t live_rows = 0;     // outstanding rows to live peers
+    uint64_t inflight = 0;     // messages emitted by the last round / origin
+    double kernel_ms_total = 0;
+    uint64_t rounds_total = 0;
+};
+
+namespace {
+
+int fail(psim_handle* h, int code, const char* fmt, ...) {
+    if (h) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess)                                                            \
+            return fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+void free_graph(psim_handle* h) {
+    void* ptrs[] = {h->rowp, h->col, h->rev, h->memb, h->alive, h->vs, h->in[0], h->in[1],
+                    h->pend[0], h->pend[1], h->ost};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    h->rowp = h->col = h->rev = h->memb = h->alive = nullptr;
+    h->vs = nullptr;
+    h->in[0] = h->in[1] = nullptr;
+    h->pend[0] = h->pend[1] = h->ost = nullptr;
+    h->n = 0;
+    h->E = 0;
+}
+
+PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
+    PtArgs a{};
+    a.n = h->n;
+    a.rowp = h->rowp;
+    a.col = h->col;
+    a.rev = h->rev;
+    a.memb = h->memb;
+    a.alive = h->alive;
+    a.vs = h->vs;
+    a.in_cur = h->in[par];
+    a.in_nxt = h->in[par ^ 1];
+    a.pend_cur = h->pend[par];
+    a.pend_nxt = h->pend[par ^ 1];
+    a.ost = h->ost;
+    a.stats = stats;
+    a.tick = tick;
+    a.mono8 = h->serial & 0xFFu;
+    a.epoch8 = h->epoch & 0xFFu;
+    a.root = h->root;
+    return a;
+}
+
+void reduce_row(const unsigned long long* row, unsigned long long* out) {
+    for (int i = 0; i < kNStat; i++) out[i] = 0;
+    for (int s = 0; s < kStatShards; s++)
+        for (int i = 0; i < kNStat; i++) {
+            if (i == S_OVERFLOW) out[i] |= row[s * kNStat + i];
+            else out[i] += row[s * kNStat + i];
+        }
+}
+
+bool quiescent(const psim_handle* h) { return h->inflight == 0 && h->live_rows == 0; }
+
+int renorm_if_needed(psim_handle* h) {
+    PtArgs a = make_args(h, h->par, 0, h->stats);
+    HIPCHK(h, launch_pt_renorm(a, h->stream));
+    return PSIM_OK;
+}
+
+// Launch up to max_rounds rounds in chunks; with stop_q, stop after the first
+// round that leaves the system quiescent (trailing rounds of the chunk were
+// no-ops and are not counted: they change no state).
+int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+          uint32_t* ran_out) {
+    uint32_t ran = 0;
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    bool done = stop_q && quiescent(h);
+    while (!done && ran < max_rounds) {
+        const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
+        HIPCHK(h, hipMemsetAsync(h->stats, 0, k * kStatsRow * sizeof(unsigned long long), h->stream));
+        uint32_t par = h->par;
+        for (uint32_t i = 0; i < k; i++) {
+            const uint32_t tick = ((h->round + i + 1) % L) == 0;
+            PtArgs a = make_args(h, par, tick, h->stats + i * kStatsRow);
+            HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+            HIPCHK(h, launch_pt_round(a, h->stream));
+            HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
+            par ^= 1u;
+        }
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * kStatsRow * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->par = par;
+        for (uint32_t i = 0; i < k; i++) {
+            unsigned long long r[kNStat];
+            reduce_row(h->h_stats + i * kStatsRow, r);
+            float ms = 0.f;
+            HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
+            if (r[S_OVERFLOW])
+                return fail(h, PSIM_EOVERFLOW,
+                            "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 65535, "
+                            "4: outstanding rows of an older heartbeat)",
+                            (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
+            uint64_t msgs = 0;
+            for (int t = 1; t <= 5; t++) msgs += r[t];
+            h->round++;
+            h->ost_cnt += (int64_t)r[S_OST_DELTA];
+            h->live_rows += (int64_t)r[S_LIVE_DELTA];
+            h->inflight = msgs;
+            h->kernel_ms_total += ms;
+            h->rounds_total++;
+            if (out && ran < cap) {
+                psim_round_stats& o = out[ran];
+                memset(&o, 0, sizeof o);
+                for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
+                o.delivered_new = r[S_DELIV];
+                o.active = r[S_ACTIVE];
+                o.senders = r[S_SENDERS];
+                o.sender_degree_sum = r[S_DEGSUM];
+                o.outstanding_vertices = (uint64_t)h->ost_cnt;
+                o.algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+                o.kernel_ms = ms;
+            }
+            ran++;
+            if (stop_q && quiescent(h)) { done = true; break; }
+        }
+    }
+    if (ran_out) *ran_out = ran;
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* psim_strerror(int code) {
+    switch (code) {
+    case PSIM_OK: return "ok";
+    case PSIM_EINVAL: return "invalid argument";
+    case PSIM_ENOMEM: return "out of memory";
+    case PSIM_EHIP: return "HIP runtime error";
+    case PSIM_ERCCL: return "RCCL error";
+    case PSIM_ESTATE: return "invalid state";
+    case PSIM_EOVERFLOW: return "fixed-capacity structure overflowed";
+    case PSIM_EBUSY: return "previous broadcast not quiescent";
+    case PSIM_ENODEV: return "no usable HIP device";
+    default: return "unknown error";
+    }
+}
+
+const char* psim_last_error(const psim_handle* h) { return h ? h->err.c_str() : ""; }
+
+int psim_create(const psim_config* cfg, psim_handle** out) {
+    if (!cfg || !out) return PSIM_EINVAL;
+    if (cfg->abi_version != PSIM_ABI_VERSION) return PSIM_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PSIM_ENODEV;
+    psim_handle* h = new (std::nothrow) psim_handle();
+    if (!h) return PSIM_ENOMEM;
+    h->cfg = *cfg;
+    if (!h->cfg.lazy_tick_rounds) h->cfg.lazy_tick_rounds = 1;
+    h->device = cfg->device >= 0 ? cfg->device : 0;
+    if (cfg->device < 0) (void)hipGetDevice(&h->device);
+    if (h->device >= ndev) { delete h; return PSIM_EINVAL; }
+    int rc = PSIM_OK;
+    do {
+        if (hipSetDevice(h->device) != hipSuccess) { rc = PSIM_ENODEV; break; }
+        if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { rc = PSIM_EHIP; break; }
+        if (hipMalloc(&h->stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipHostMalloc(&h->h_stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        for (auto& e : h->ev)
+            if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
+    } while (0);
+    if (rc != PSIM_OK) { psim_destroy(h); return rc; }
+    *out = h;
+    return PSIM_OK;
+}
+
+int psim_destroy(psim_handle* h) {
+    if (!h) return PSIM_EINVAL;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    free_graph(h);
+    if (h->stats) (void)hipFree(h->stats);
+    if (h->h_stats) (void)hipHostFree(h->h_stats);
+    if (h->scratch) (void)hipFree(h->scratch);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return PSIM_OK;
+}
+
+int psim_device_info(const psim_handle* h, char* buf, size_t cap) {
+    if (!h || !buf || !cap) return PSIM_EINVAL;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, h->device) != hipSuccess) return PSIM_EHIP;
+    snprintf(buf, cap, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+    return PSIM_OK;
+}
+
+int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col) {
+    if (!h || !row_ptr || (!col && row_ptr[n])) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    free_graph(h);
+    // symmetrise: peers(v) = members(v) U {u : v in members(u)}, minus self
+    std::vector<uint64_t> cnt(size_t(n) + 1, 0);
+    for (uint32_t v = 0; v < n; v++) {
+        if (row_ptr[v + 1] < row_ptr[v]) return fail(h, PSIM_EINVAL, "row_ptr not monotone at %u", v);
+        for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
+            const uint32_t u = col[e];
+            if (u >= n) return fail(h, PSIM_EINVAL, "col[%llu]=%u >= n", (unsigned long long)e, u);
+            if (u == v) continue;
+            cnt[v + 1]++;
+            cnt[u + 1]++;
+        }
+    }
+    for (uint32_t v = 0; v < n; v++) cnt[v + 1] += cnt[v];
+    std::vector<uint32_t> tmp(cnt[n]);
+    {
+        std::vector<uint64_t> fill(cnt.begin(), cnt.end() - 1);
+        for (uint32_t v = 0; v < n; v++)
+            for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
+                const uint32_t u = col[e];
+                if (u == v) continue;
+                tmp[fill[v]++] = u;
+                tmp[fill[u]++] = v;
+            }
+    }
+    std::vector<uint64_t> rp(size_t(n) + 1, 0);
+    std::vector<uint32_t> cc;
+    cc.reserve(tmp.size() / 2 + 16);
+    for (uint32_t v = 0; v < n; v++) {
+        uint32_t* b = tmp.data() + cnt[v];
+        uint32_t* e = tmp.data() + cnt[v + 1];
+        std::sort(b, e);
+        uint32_t* u = std::unique(b, e);
+        const uint64_t d = uint64_t(u - b);
+        if (d > uint64_t(kMaxDeg))
+            return fail(h, PSIM_EINVAL, "vertex %u has %llu peers (limit %d)", v, (unsigned long long)d, kMaxDeg);
+        cc.insert(cc.end(), b, u);
+        rp[v + 1] = rp[v] + d;
+    }
+    tmp.clear();
+    tmp.shrink_to_fit();
+    const uint64_t E = rp[n];
+    if (E >= 0xFFFFFFFFull) return fail(h, PSIM_EINVAL, "too many peer slots (%llu)", (unsigned long long)E);
+    std::vector<uint32_t> rp32(size_t(n) + 1), rev(E), memb(n, 0u);
+    for (uint32_t v = 0; v <= n; v++) rp32[v] = uint32_t(rp[v]);
+    for (uint32_t v = 0; v < n; v++)
+        for (uint64_t e = rp[v]; e < rp[v + 1]; e++) {
+            const uint32_t u = cc[e];
+            const uint32_t* b = cc.data() + rp[u];
+            const uint32_t* x = std::lower_bound(b, b + (rp[u + 1] - rp[u]), v);
+            rev[e] = uint32_t(x - cc.data());
+        }
+    for (uint32_t v = 0; v < n; v++)
+        for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
+            const uint32_t u = col[e];
+            if (u == v) continue;
+            const uint32_t* b = cc.data() + rp[v];
+            const uint32_t* x = std::lower_bound(b, b + (rp[v + 1] - rp[v]), u);
+            memb[v] |= 1u << uint32_t(x - b);
+        }
+    // device arrays
+    auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
+    const size_t nw = (size_t(n) + 31) / 32;
+    if (alloc((void**)&h->rowp, (size_t(n) + 1) * 4) != hipSuccess || alloc((void**)&h->col, E * 4) != hipSuccess ||
+        alloc((void**)&h->rev, E * 4) != hipSuccess || alloc((void**)&h->memb, size_t(n) * 4) != hipSuccess ||
+        alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(n) * 16) != hipSuccess ||
+        alloc((void**)&h->in[0], E * 4) != hipSuccess || alloc((void**)&h->in[1], E * 4) != hipSuccess ||
+        alloc((void**)&h->pend[0], n) != hipSuccess || alloc((void**)&h->pend[1], n) != hipSuccess ||
+        alloc((void**)&h->ost, n) != hipSuccess) {
+        free_graph(h);
+        return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", n, (unsigned long long)E);
+    }
+    h->n = n;
+    h->E = E;
+    HIPCHK(h, hipMemcpy(h->rowp, rp32.data(), (size_t(n) + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->col, cc.data(), E * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->rev, rev.data(), E * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->memb, memb.data(), size_t(n) * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
+    // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..
+    HIPCHK(h, hipMemset(h->vs, 0, size_t(n) * 16));
+    HIPCHK(h, hipMemset(h->in[0], 0, E * 4));
+    HIPCHK(h, hipMemset(h->in[1], 0, E * 4));
+    HIPCHK(h, hipMemset(h->pend[0], 0, n));
+    HIPCHK(h, hipMemset(h->pend[1], 0, n));
+    HIPCHK(h, hipMemset(h->ost, 0, n));
+    HIPCHK(h, hipDeviceSynchronize());
+    h->h_rowp = std::move(rp);
+    h->h_col = std::move(cc);
+    h->h_memb = std::move(memb);
+    h->par = 0;
+    h->round = 0;
+    h->serial = 0;
+    h->epoch = 1;
+    h->have_root = false;
+    h->mono_of.clear();
+    h->ost_cnt = h->live_rows = 0;
+    h->inflight = 0;
+    return PSIM_OK;
+}
+
+int psim_num_slots(const psim_handle* h, uint64_t* out) {
+    if (!h || !out) return PSIM_EINVAL;
+    *out = h->E;
+    return PSIM_OK;
+}
+
+int psim_get_slots(const psim_handle* h, uint64_t* row_ptr, uint32_t* col) {
+    if (!h || !h->n) return PSIM_EINVAL;
+    if (row_ptr) memcpy(row_ptr, h->h_rowp.data(), (size_t(h->n) + 1) * 8);
+    if (col) memcpy(col, h->h_col.data(), h->E * 4);
+    return PSIM_OK;
+}
+
+int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
+    if (!h || !alive || n != h->n || !h->n) return PSIM_EINVAL;
+    std::vector<uint32_t> bm((n + 31) / 32, 0u);
+    for (size_t v = 0; v < n; v++)
+        if (alive[v]) bm[v >> 5] |= 1u << (v & 31);
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(h->alive, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->scratch, 0, 8, h->stream));
+    PtArgs a = make_args(h, h->par, 0, h->stats);
+    HIPCHK(h, launch_pt_count_live(a, h->scratch, h->stream));
+    unsigned long long live = 0;
+    HIPCHK(h, hipMemcpyAsync(&live, h->scratch, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->live_rows = (int64_t)live;
+    return PSIM_OK;
+}
+
+int psim_plumtree_reset_trees(psim_handle* h) {
+    if (!h || !h->n) return PSIM_ESTATE;
+    HIPCHK(h, hipSetDevice(h->device));
+    h->epoch++;
+    if ((h->epoch & 0x7Fu) == 0) {
+        int rc = renorm_if_needed(h);
+        if (rc) return rc;
+    }
+    return PSIM_OK;
+}
+
+int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+    if (!h || !h->n) return PSIM_ESTATE;
+    if (root >= h->n) return PSIM_EINVAL;
+    if (!quiescent(h)) return fail(h, PSIM_EBUSY, "previous broadcast still in flight");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->have_root && root != h->root) {
+        // single-root engine: the previous root's per-root sets are dropped
+        // (DESIGN.md "Scope": multi-root trees are SURVEY 8(f) row 1)
+        h->epoch++;
+    }
+    h->root = root;
+    h->have_root = true;
+    h->serial++;
+    if ((h->serial & 0x7Fu) == 0 || (h->epoch & 0x7Fu) == 0) {
+        int rc = renorm_if_needed(h);
+        if (rc) return rc;
+    }
+    uint32_t& mono = h->mono_of[root];
+    mono++;
+    if (mono_out) *mono_out = mono;
+    HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+    // origin emits into the buffer the next round reads
+    PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+    HIPCHK(h, launch_pt_origin(a, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    unsigned long long r[kNStat];
+    reduce_row(h->h_stats, r);
+    if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "origin: outstanding rows of an older heartbeat");
+    h->ost_cnt += (int64_t)r[S_OST_DELTA];
+    h->live_rows += (int64_t)r[S_LIVE_DELTA];
+    h->inflight = r[PSIM_MSG_BROADCAST];
+    return PSIM_OK;
+}
+
+int psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    return drive(h, rounds, stats, cap, false, nullptr);
+}
+
+int psim_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds_run) {
+    if (!h) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    return drive(h, max_rounds, stats, cap, true, rounds_run);
+}
+
+int psim_get_plumtree(const psim_handle* h, uint32_t* eager, uint32_t* lazy, uint32_t* outstanding,
+                      uint16_t* recv_round, size_t n) {
+    if (!h || n != h->n || !h->n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    std::vector<uint4> vs(n);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    HIPCHK(hh, hipMemcpy(vs.data(), h->vs, n * 16, hipMemcpyDeviceToHost));
+    const uint32_t ep8 = h->epoch & 0xFFu, s8 = h->serial & 0xFFu;
+    for (size_t v = 0; v < n; v++) {
+        const uint4 st = vs[v];
+        const bool cur = (st.w >> 24) == ep8;
+        if (eager) eager[v] = cur ? st.x : h->h_memb[v];
+        if (lazy) lazy[v] = cur ? st.y : 0u;
+        if (outstanding) outstanding[v] = st.z;
+        if (recv_round) {
+            const bool got = h->serial && ((st.w >> 16) & 0xFFu) == s8;
+            if (!got) recv_round[v] = 0xFFFF;
+            else if (h->have_root && v == h->root) recv_round[v] = 0xFFFE;
+            else recv_round[v] = uint16_t((st.w & 0xFFFFu) - 1u);
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
+    if (!h || !delivered || n != h->n || !h->n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    std::vector<uint4> vs(n);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    HIPCHK(hh, hipMemcpy(vs.data(), h->vs, n * 16, hipMemcpyDeviceToHost));
+    const uint32_t s8 = h->serial & 0xFFu;
+    for (size_t v = 0; v < n; v++) delivered[v] = h->serial && ((vs[v].w >> 16) & 0xFFu) == s8;
+    return PSIM_OK;
+}
+
+int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
+    if (!h || !words || n_words != h->E) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
+    return PSIM_OK;
+}
+
+int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds) {
+    if (!h) return PSIM_EINVAL;
+    if (round_kernel_ms) *round_kernel_ms = h->kernel_ms_total;
+    if (rounds) *rounds = h->rounds_total;
+    return PSIM_OK;
+}
+
+}  // extern "C"

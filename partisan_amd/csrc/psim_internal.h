@@ -1,0 +1,55 @@
+// psim_internal.h -- shared between the host ABI (psim_host.hip) and the
+// Plumtree kernels (plumtree.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psim {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
+constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
+constexpr int kNStat = 16;           // counters per shard
+
+// counter indices (1..5 = PSIM_MSG_* kinds)
+enum Stat : int {
+    S_DELIV = 6,        // merge/2 returned true
+    S_ACTIVE = 7,       // vertices that processed messages or a tick
+    S_SENDERS = 8,      // vertices that emitted >= 1 message
+    S_DEGSUM = 9,       // sum of deg over senders
+    S_OST_DELTA = 10,   // change in #vertices with outstanding rows (two's complement)
+    S_LIVE_DELTA = 11,  // change in #outstanding rows to live peers (two's complement)
+    S_OVERFLOW = 12,    // bit0: per-edge FIFO > 4 ; bit1: Round > 0xFFFF ; bit2: rows of an older heartbeat
+};
+
+// Per-vertex Plumtree state, one 16-byte record (one dwordx4 load):
+//   x = eager mask, y = lazy mask, z = outstanding mask (bits = slots)
+//   w = [15:0] round pushed by this vertex (accepted Round + 1; 0 at the root)
+//       [23:16] low 8 bits of the Monotonic last delivered (Mod:merge/2)
+//       [31:24] tree epoch (a mismatch == no per-root map entry: common sets)
+struct PtArgs {
+    uint32_t n;
+    const uint32_t* __restrict__ rowp;     // [n+1] slot row pointers
+    const uint32_t* __restrict__ col;      // [E]   neighbour id per slot (sorted in a row)
+    const uint32_t* __restrict__ rev;      // [E]   index of the reverse slot
+    const uint32_t* __restrict__ memb;     // [n]   member mask = common_eagers
+    const uint32_t* __restrict__ alive;    // [ceil(n/32)] bitmap
+    uint4* __restrict__ vs;                // [n]   state records
+    uint32_t* __restrict__ in_cur;         // [E]   words read this round (receiver slots)
+    uint32_t* __restrict__ in_nxt;         // [E]   words written this round
+    uint8_t* __restrict__ pend_cur;        // [n]   1 = inbox non-empty
+    uint8_t* __restrict__ pend_nxt;
+    uint8_t* __restrict__ ost;             // [n]   1 = outstanding rows exist
+    unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
+    uint32_t tick;                         // lazy tick fires at the end of this round
+    uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
+    uint32_t epoch8;                       // current tree epoch (low 8 bits)
+    uint32_t root;                         // origin of the current heartbeat
+};
+
+hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
+hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
+
+}  // namespace psim

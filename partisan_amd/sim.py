@@ -1,0 +1,144 @@
+"""Simulator: one libpsim handle = one simulated cluster on one GPU.
+
+Thin numpy-facing wrapper over include/psim.h; every method is one ABI
+call (the HIP kernels do the protocol work).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import PSIM_ABI_VERSION, Config, RoundStats, check, lib
+
+_u8p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))    # noqa: E731
+_u16p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint16))  # noqa: E731
+_u32p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
+_u64p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
+
+
+class Simulator:
+    """Round-synchronous simulator of Partisan's gossip hot path."""
+
+    def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0):
+        cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
+                     exchange_tick_rounds=exchange_tick_rounds, flags=0, _reserved=0, seed=seed)
+        h = C.c_void_p()
+        check(lib().psim_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.n = 0
+        self.lazy_tick_rounds = lazy_tick_rounds
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().psim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _c(self, rc):
+        return check(rc, self._h)
+
+    def device_info(self):
+        buf = C.create_string_buffer(256)
+        self._c(lib().psim_device_info(self._h, buf, 256))
+        return buf.value.decode()
+
+    # ---------------------------------------------------------------- overlay
+    def load_overlay(self, row_ptr, col):
+        """Membership lists (members minus self) as CSR; see psim_load_csr."""
+        rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        cc = np.ascontiguousarray(col, dtype=np.uint32)
+        n = len(rp) - 1
+        self._c(lib().psim_load_csr(self._h, n, _u64p(rp), _u32p(cc) if len(cc) else None))
+        self.n = n
+        E = C.c_uint64()
+        self._c(lib().psim_num_slots(self._h, C.byref(E)))
+        self.slot_row_ptr = np.zeros(n + 1, dtype=np.uint64)
+        self.slot_col = np.zeros(max(1, E.value), dtype=np.uint32)
+        self._c(lib().psim_get_slots(self._h, _u64p(self.slot_row_ptr), _u32p(self.slot_col)))
+        self.slot_col = self.slot_col[: E.value]
+        self.num_slots = E.value
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        self._c(lib().psim_set_alive(self._h, _u8p(a), len(a)))
+
+    # ---------------------------------------------------------------- plumtree
+    def reset_trees(self):
+        self._c(lib().psim_plumtree_reset_trees(self._h))
+
+    def broadcast(self, root):
+        mono = C.c_uint32()
+        self._c(lib().psim_plumtree_broadcast(self._h, root, C.byref(mono)))
+        return mono.value
+
+    def step(self, rounds=1):
+        st = (RoundStats * max(1, rounds))()
+        self._c(lib().psim_step(self._h, rounds, st, rounds))
+        return [s.as_dict() for s in st[:rounds]]
+
+    def run(self, max_rounds=100000, cap=4096):
+        st = (RoundStats * cap)()
+        ran = C.c_uint32()
+        self._c(lib().psim_run(self._h, max_rounds, st, cap, C.byref(ran)))
+        return [s.as_dict() for s in st[: min(ran.value, cap)]], ran.value
+
+    def plumtree_state(self):
+        n = self.n
+        eager = np.zeros(n, np.uint32)
+        lazy = np.zeros(n, np.uint32)
+        outst = np.zeros(n, np.uint32)
+        rr = np.zeros(n, np.uint16)
+        self._c(lib().psim_get_plumtree(self._h, _u32p(eager), _u32p(lazy), _u32p(outst), _u16p(rr), n))
+        return eager, lazy, outst, rr
+
+    def delivered(self):
+        out = np.zeros(self.n, np.uint8)
+        self._c(lib().psim_get_delivered(self._h, _u8p(out), self.n))
+        return out
+
+    def inflight(self):
+        w = np.zeros(max(1, self.num_slots), np.uint32)
+        self._c(lib().psim_get_inflight(self._h, _u32p(w), self.num_slots))
+        return w[: self.num_slots]
+
+    def timing(self):
+        ms = C.c_double()
+        r = C.c_uint64()
+        self._c(lib().psim_get_timing(self._h, C.byref(ms), C.byref(r)))
+        return ms.value, r.value
+
+    # ---------------------------------------------------------------- helpers
+    def mask_to_peers(self, v, mask):
+        """Decode a per-vertex slot mask into the sorted list of peer ids."""
+        lo = int(self.slot_row_ptr[v])
+        hi = int(self.slot_row_ptr[v + 1])
+        return [int(self.slot_col[lo + s]) for s in range(hi - lo) if (int(mask) >> s) & 1]
+
+    def decode_inflight(self, words=None):
+        """In-flight messages as sorted (src, dst, kind, round) tuples; the
+        Round is reported for broadcast / i_have only (the others carry an echo
+        or nothing).  Order within a (src, dst) pair is FIFO order."""
+        if words is None:
+            words = self.inflight()
+        out = []
+        rp = self.slot_row_ptr
+        nz = np.nonzero(words)[0]
+        dst_of = np.searchsorted(rp, nz, side="right") - 1
+        for e, dst in zip(nz.tolist(), dst_of.tolist()):
+            w = int(words[e])
+            src = int(self.slot_col[e])
+            f, rnd = w & 0xFFFF, w >> 16
+            while f:
+                t = f & 0xF
+                f >>= 4
+                out.append((src, int(dst), t, rnd if t in (1, 3) else 0))
+        out.sort(key=lambda m: (m[1], m[0]))
+        return out

@@ -1,0 +1,233 @@
+"""Parity of the HIP Plumtree path (libpsim.so via the C ABI) with the CPU
+oracle (oracle/plumtree.c), round by round, bit-exact.
+
+Compared after every round: delivered set, Round of the accepted broadcast,
+eager and lazy peer sets of every vertex for the root, outstanding i_have
+rows (peer and Round), the full set of messages in flight (src, dst, kind,
+Round) in FIFO order, and the per-kind message counters.  Plumtree traces
+are not pinned by any reference test (SURVEY 8(c) "Unpinned"): the oracle is
+the reference restatement these are checked against.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
+
+
+@pytest.fixture(scope="module")
+def psim():
+    import partisan_amd
+    return partisan_amd
+
+
+def make(psim, rp, col, L=1):
+    sim = psim.Simulator(lazy_tick_rounds=L)
+    sim.load_overlay(rp, col)
+    orc = O.Plumtree(rp, col, lazy_tick_rounds=L)
+    return sim, orc
+
+
+def compare(sim, orc, root, mono):
+    n = sim.n
+    eager, lazy, outst, rr = sim.plumtree_state()
+    assert np.array_equal(sim.delivered(), orc.delivered(root, mono)), "delivered sets differ"
+    orr = orc.recv_round(root, mono)
+    for v in range(n):
+        oe, ol = orc.peers(v, root)
+        assert sim.mask_to_peers(v, eager[v]) == oe, f"eager set of {v}"
+        assert sim.mask_to_peers(v, lazy[v]) == ol, f"lazy set of {v}"
+        rows = orc.outstanding(v)
+        assert sim.mask_to_peers(v, outst[v]) == sorted({p for p, _, _ in rows}), f"outstanding of {v}"
+        if orr[v] == 0xFFFFFFFF:
+            assert rr[v] == 0xFFFF, v
+        elif orr[v] == 0xFFFFFFFE:
+            assert rr[v] == 0xFFFE, v
+        else:
+            assert rr[v] == orr[v], v
+        if rows:
+            my_round = 0 if rr[v] == 0xFFFE else int(rr[v]) + 1
+            assert {r for _, r, _ in rows} == {my_round}, v
+            assert {m for _, _, m in rows} == {mono}, v
+    want = [(s, d, t, r if t in (1, 3) else 0) for (s, d, t, r) in orc.pending()]
+    assert sim.decode_inflight() == want, "in-flight messages differ"
+
+
+def lockstep(sim, orc, root, mono, max_rounds=200):
+    rounds = 0
+    while rounds < max_rounds:
+        gs = sim.step(1)[0]
+        os_ = orc.step(1)[0]
+        rounds += 1
+        for k in KINDS:
+            assert gs[k] == os_[k], (rounds, k, gs, os_)
+        assert gs["delivered_new"] == os_["delivered_new"]
+        compare(sim, orc, root, mono)
+        if sum(gs[k] for k in KINDS) == 0 and os_["outstanding_live"] == 0:
+            break
+    return rounds
+
+
+@pytest.mark.parametrize("n,seed,L", [(40, 1, 1), (300, 2, 1), (300, 3, 2), (1500, 4, 3), (1000, 5, 1)])
+def test_flood_then_tree_lockstep(psim, n, seed, L):
+    rp, col = psim.overlay.random_regular(n, 5, seed)
+    sim, orc = make(psim, rp, col, L)
+    root = seed % n
+    for _ in range(3):          # flood, then two heartbeats over the pruned tree
+        mono_g = sim.broadcast(root)
+        mono_o = orc.heartbeat(root)
+        assert mono_g == mono_o
+        compare(sim, orc, root, mono_o)
+        lockstep(sim, orc, root, mono_o)
+
+
+def test_dead_vertices_lockstep(psim):
+    n = 800
+    rp, col = psim.overlay.random_regular(n, 5, 11)
+    sim, orc = make(psim, rp, col, 1)
+    root = 3
+    m = sim.broadcast(root)
+    orc.heartbeat(root)
+    lockstep(sim, orc, root, m)
+    rng = np.random.default_rng(7)
+    alive = np.ones(n, np.uint8)
+    alive[rng.choice(n, n // 10, replace=False)] = 0
+    alive[root] = 1
+    sim.set_alive(alive)
+    orc.set_alive(alive)
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    lockstep(sim, orc, root, m)
+
+
+def test_ring_lattice_long_rounds(psim):
+    rp, col = psim.overlay.ring_lattice(600, 2)
+    sim, orc = make(psim, rp, col, 2)
+    for _ in range(2):
+        m = sim.broadcast(0)
+        orc.heartbeat(0)
+        lockstep(sim, orc, 0, m, max_rounds=1000)
+
+
+def test_complete_graph_c1(psim):
+    # config C1: 16 nodes, full membership (degree 15)
+    rp, col = psim.overlay.complete(16)
+    sim, orc = make(psim, rp, col, 1)
+    for _ in range(3):
+        m = sim.broadcast(0)
+        orc.heartbeat(0)
+        lockstep(sim, orc, 0, m)
+
+
+def test_reset_trees_and_root_change(psim):
+    rp, col = psim.overlay.random_regular(500, 5, 21)
+    sim, orc = make(psim, rp, col, 1)
+    for root, reset in [(7, False), (7, True), (9, False), (9, False)]:
+        if reset:
+            sim.reset_trees()
+            orc.reset_peers_all()
+        if root != getattr(sim, "_last_root", root):
+            orc.reset_peers_all()      # single-root engine drops the old root's sets
+        sim._last_root = root
+        m = sim.broadcast(root)
+        assert m == orc.heartbeat(root)
+        lockstep(sim, orc, root, m)
+
+
+def test_run_matches_oracle_round_count(psim):
+    rp, col = psim.overlay.random_regular(5000, 5, 31)
+    for L in (1, 3):
+        sim, orc = make(psim, rp, col, L)
+        for _ in range(3):
+            sim.broadcast(17)
+            m = orc.heartbeat(17)
+            gst, gr = sim.run()
+            ost, orr = orc.run()
+            assert gr == orr
+            for g, o in zip(gst, ost):
+                for k in KINDS:
+                    assert g[k] == o[k]
+            compare(sim, orc, 17, m)
+
+
+def test_busy_until_quiescent(psim):
+    rp, col = psim.overlay.random_regular(200, 5, 41)
+    sim = psim.Simulator()
+    sim.load_overlay(rp, col)
+    sim.broadcast(0)
+    with pytest.raises(psim.PsimError) as ei:
+        sim.broadcast(0)
+    assert ei.value.name == "PSIM_EBUSY"
+    sim.run()
+    sim.broadcast(0)
+
+
+def test_facade_mirrors_reference_api(psim):
+    rp, col = psim.overlay.random_regular(300, 5, 51)
+    pt = psim.PlumtreeBroadcast(rp, col)
+    orc = O.Plumtree(rp, col, 1)
+    msg_id = pt.broadcast(4)
+    orc.heartbeat(4)
+    pt.run()
+    orc.run()
+    for v in (0, 4, 100, 299):
+        assert pt.get_peers(v, 4) == orc.peers(v, 4)
+        assert pt.get_eager_peers(v, 4) == orc.peers(v, 4)[0]
+        assert pt.handler(v).is_stale(msg_id)
+        assert pt.handler(v).graft(msg_id) == ("ok", msg_id)
+        assert pt.exchanges(v) == []
+    assert pt.broadcast_channel() == "partisan_membership"
+    with pytest.raises(NotImplementedError):
+        psim.PlumtreeBroadcast(rp, col, mods=[object])
+
+
+@pytest.mark.parametrize("n", [100_000])
+def test_large_final_state_parity(psim, n):
+    rp, col = psim.overlay.random_regular(n, 5, 61)
+    sim, orc = make(psim, rp, col, 1)
+    for _ in range(2):
+        sim.broadcast(0)
+        m = orc.heartbeat(0)
+        _, gr = sim.run()
+        _, orr = orc.run()
+        assert gr == orr
+    eager, lazy, outst, rr = sim.plumtree_state()
+    assert np.array_equal(sim.delivered(), orc.delivered(0, m))
+    orr = orc.recv_round(0, m)
+    got = np.where(rr == 0xFFFF, 0xFFFFFFFF, np.where(rr == 0xFFFE, 0xFFFFFFFE, rr.astype(np.int64)))
+    assert np.array_equal(got.astype(np.uint64), orr.astype(np.uint64))
+    rng = np.random.default_rng(0)
+    for v in rng.choice(n, 2000, replace=False).tolist():
+        oe, ol = orc.peers(v, 0)
+        assert sim.mask_to_peers(v, eager[v]) == oe
+        assert sim.mask_to_peers(v, lazy[v]) == ol
+
+
+def popcount32(x):
+    x = x.astype(np.uint64)
+    c = np.zeros_like(x)
+    for i in range(32):
+        c += (x >> np.uint64(i)) & np.uint64(1)
+    return c
+
+
+@pytest.mark.parametrize("n", [2_000_000])
+def test_large_flood_properties(psim, n):
+    """Size-independent properties at scale: after a flood from a fresh state
+    every vertex delivered, no row is outstanding, and the eager graph is a
+    spanning tree (2(n-1) directed eager edges, each vertex's Round = its
+    parent's + 1)."""
+    rp, col = psim.overlay.random_regular(n, 5, 71)
+    sim = psim.Simulator()
+    sim.load_overlay(rp, col)
+    sim.broadcast(0)
+    stats, rounds = sim.run()
+    assert sim.delivered().all()
+    eager, lazy, outst, rr = sim.plumtree_state()
+    assert not outst.any()
+    assert int(popcount32(eager).sum()) == 2 * (n - 1)
+    assert sum(s["delivered_new"] for s in stats) == n - 1
+    assert stats[-1]["broadcast"] == 0
