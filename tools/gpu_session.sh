@@ -1,0 +1,43 @@
+#!/usr/bin/env bash
+# Runs on the GPU box (via gpurun) from the repo root.  Each GPU step has its
+# own time limit; a crash / abort / timeout ends the session immediately,
+# a plain test failure (exit 1) does not.
+#   usage: tools/gpu_session.sh [steps...]   steps: test smoke bench prof pmc
+set -u
+mkdir -p gpurun_out
+STEPS=${*:-"test smoke bench prof"}
+export PYTHONUNBUFFERED=1
+
+run() {  # name seconds cmd...
+    local name=$1 secs=$2; shift 2
+    echo "=== $name: $*" | tee -a gpurun_out/session.log
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a gpurun_out/session.log
+    tail -5 "gpurun_out/$name.log"
+    case $rc in
+        0|1) return 0 ;;
+        *) echo "=== stopping: $name ended with $rc"; exit $rc ;;
+    esac
+}
+
+for s in $STEPS; do
+    case $s in
+        build) run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
+        test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        prof)
+            export TMPDIR=/tmp
+            run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
+                -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+        pmc)
+            export TMPDIR=/tmp
+            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv \
+                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv \
+                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $s" ;;
+    esac
+done
+echo "=== session done"
