@@ -1,0 +1,261 @@
+/*
+ * partisan_gpu_sim_nif.c -- the thin Erlang NIF over libpsim.so (include/psim.h).
+ *
+ * Built only where erl_nif.h exists (an erts host; this image has none):
+ *   cc -O2 -shared -fPIC -I"$ERTS_INCLUDE" -I../../include \
+ *      partisan_gpu_sim_nif.c -L../../partisan_amd -lpsim -Wl,-rpath,'$ORIGIN' \
+ *      -o ../priv/partisan_gpu_sim.so
+ *
+ * Every call that launches device work runs on a dirty CPU scheduler
+ * (ERL_NIF_DIRTY_JOB_CPU_BOUND).  A handle is an enif resource whose
+ * destructor calls psim_destroy; a per-resource mutex serialises calls
+ * (psim handles are single-threaded).  Errors map to {error, Atom}.
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "psim.h"
+
+typedef struct {
+    psim_handle* h;
+    ErlNifMutex* mu;
+    uint32_t n;
+    uint64_t slots;
+} sim_res;
+
+static ErlNifResourceType* SIM_RES;
+
+static ERL_NIF_TERM mk_atom(ErlNifEnv* env, const char* a) {
+    ERL_NIF_TERM t;
+    return enif_make_existing_atom(env, a, &t, ERL_NIF_LATIN1) ? t : enif_make_atom(env, a);
+}
+
+static ERL_NIF_TERM err(ErlNifEnv* env, int rc) {
+    const char* a = "psim_error";
+    switch (rc) {
+    case PSIM_EINVAL: a = "einval"; break;
+    case PSIM_ENOMEM: a = "enomem"; break;
+    case PSIM_EHIP: a = "ehip"; break;
+    case PSIM_ERCCL: a = "erccl"; break;
+    case PSIM_ESTATE: a = "estate"; break;
+    case PSIM_EOVERFLOW: a = "eoverflow"; break;
+    case PSIM_EBUSY: a = "ebusy"; break;
+    case PSIM_ENODEV: a = "enodev"; break;
+    }
+    return enif_make_tuple2(env, mk_atom(env, "error"), mk_atom(env, a));
+}
+
+static void sim_dtor(ErlNifEnv* env, void* obj) {
+    (void)env;
+    sim_res* r = (sim_res*)obj;
+    if (r->h) psim_destroy(r->h);
+    if (r->mu) enif_mutex_destroy(r->mu);
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+    (void)priv; (void)info;
+    SIM_RES = enif_open_resource_type(env, NULL, "partisan_gpu_sim", sim_dtor, ERL_NIF_RT_CREATE, NULL);
+    return SIM_RES ? 0 : -1;
+}
+
+static int get_res(ErlNifEnv* env, ERL_NIF_TERM t, sim_res** r) {
+    return enif_get_resource(env, t, SIM_RES, (void**)r) && (*r)->h;
+}
+
+static unsigned map_u32(ErlNifEnv* env, ERL_NIF_TERM m, const char* key, unsigned dflt) {
+    ERL_NIF_TERM v;
+    unsigned x;
+    if (enif_get_map_value(env, m, mk_atom(env, key), &v) && enif_get_uint(env, v, &x)) return x;
+    return dflt;
+}
+
+/* new(#{lazy_tick_rounds, exchange_tick_rounds, device, seed}) -> {ok, Sim} */
+static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    if (!enif_is_map(env, argv[0])) return enif_make_badarg(env);
+    psim_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.abi_version = PSIM_ABI_VERSION;
+    cfg.device = (int32_t)map_u32(env, argv[0], "device", (unsigned)-1);
+    cfg.lazy_tick_rounds = map_u32(env, argv[0], "lazy_tick_rounds", 1);
+    cfg.exchange_tick_rounds = map_u32(env, argv[0], "exchange_tick_rounds", 10);
+    cfg.seed = map_u32(env, argv[0], "seed", 0);
+    sim_res* r = (sim_res*)enif_alloc_resource(SIM_RES, sizeof(sim_res));
+    memset(r, 0, sizeof *r);
+    int rc = psim_create(&cfg, &r->h);
+    if (rc != PSIM_OK) { enif_release_resource(r); return err(env, rc); }
+    r->mu = enif_mutex_create("partisan_gpu_sim");
+    ERL_NIF_TERM t = enif_make_resource(env, r);
+    enif_release_resource(r);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), t);
+}
+
+/* load_csr(Sim, RowPtr :: <<u64-little>>, Col :: <<u32-little>>) -> ok */
+static ERL_NIF_TERM nif_load_csr(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary rp, col;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &rp) ||
+        !enif_inspect_binary(env, argv[2], &col) || rp.size < 8 || rp.size % 8 || col.size % 4)
+        return enif_make_badarg(env);
+    uint32_t n = (uint32_t)(rp.size / 8 - 1);
+    enif_mutex_lock(r->mu);
+    int rc = psim_load_csr(r->h, n, (const uint64_t*)rp.data, (const uint32_t*)col.data);
+    if (rc == PSIM_OK) { r->n = n; psim_num_slots(r->h, &r->slots); }
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* set_alive(Sim, <<0|1 per vertex>>) -> ok */
+static ERL_NIF_TERM nif_set_alive(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary b;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_set_alive(r->h, b.data, b.size);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* reset_trees(Sim) -> ok   (update with new members at every node) */
+static ERL_NIF_TERM nif_reset_trees(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_reset_trees(r->h);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* broadcast(Sim, Root) -> {ok, Monotonic} */
+static ERL_NIF_TERM nif_broadcast(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root)) return enif_make_badarg(env);
+    uint32_t mono = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_broadcast(r->h, root, &mono);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_uint(env, mono));
+}
+
+static ERL_NIF_TERM stats_term(ErlNifEnv* env, const psim_round_stats* s) {
+    ERL_NIF_TERM keys[9] = {mk_atom(env, "broadcast"), mk_atom(env, "prune"), mk_atom(env, "i_have"),
+                            mk_atom(env, "ignored_i_have"), mk_atom(env, "graft"), mk_atom(env, "delivered"),
+                            mk_atom(env, "senders"), mk_atom(env, "algo_bytes"), mk_atom(env, "kernel_us")};
+    ERL_NIF_TERM vals[9] = {enif_make_uint64(env, s->sent[PSIM_MSG_BROADCAST]),
+                            enif_make_uint64(env, s->sent[PSIM_MSG_PRUNE]),
+                            enif_make_uint64(env, s->sent[PSIM_MSG_IHAVE]),
+                            enif_make_uint64(env, s->sent[PSIM_MSG_IGNORED]),
+                            enif_make_uint64(env, s->sent[PSIM_MSG_GRAFT]),
+                            enif_make_uint64(env, s->delivered_new),
+                            enif_make_uint64(env, s->senders),
+                            enif_make_uint64(env, s->algo_bytes),
+                            enif_make_uint64(env, (uint64_t)(s->kernel_ms * 1000.0))};
+    ERL_NIF_TERM m;
+    enif_make_map_from_arrays(env, keys, vals, 9, &m);
+    return m;
+}
+
+/* run(Sim, MaxRounds) -> {ok, Rounds, [StatsMap]}   (to quiescence) */
+static ERL_NIF_TERM nif_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
+    enum { CAP = 4096 };
+    psim_round_stats* st = (psim_round_stats*)enif_alloc(CAP * sizeof(psim_round_stats));
+    uint32_t ran = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_run(r->h, maxr, st, CAP, &ran);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (uint32_t i = ran < CAP ? ran : CAP; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), list);
+}
+
+/* step(Sim, Rounds) -> {ok, [StatsMap]} */
+static ERL_NIF_TERM nif_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &k) || k == 0 || k > 65536)
+        return enif_make_badarg(env);
+    psim_round_stats* st = (psim_round_stats*)enif_alloc(k * sizeof(psim_round_stats));
+    enif_mutex_lock(r->mu);
+    int rc = psim_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (unsigned i = k; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* peers(Sim) -> {ok, Eager, Lazy, Outstanding, RecvRound}: binaries of
+ * u32-little masks over slots (and u16 Rounds) for every vertex */
+static ERL_NIF_TERM nif_peers(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    ERL_NIF_TERM te, tl, to, tr;
+    unsigned char* e = enif_make_new_binary(env, (size_t)r->n * 4, &te);
+    unsigned char* l = enif_make_new_binary(env, (size_t)r->n * 4, &tl);
+    unsigned char* o = enif_make_new_binary(env, (size_t)r->n * 4, &to);
+    unsigned char* rr = enif_make_new_binary(env, (size_t)r->n * 2, &tr);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_plumtree(r->h, (uint32_t*)e, (uint32_t*)l, (uint32_t*)o, (uint16_t*)rr, r->n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple5(env, mk_atom(env, "ok"), te, tl, to, tr);
+}
+
+/* slots(Sim) -> {ok, RowPtr, Col}: the slot layout the masks index */
+static ERL_NIF_TERM nif_slots(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    ERL_NIF_TERM trp, tcol;
+    unsigned char* rp = enif_make_new_binary(env, ((size_t)r->n + 1) * 8, &trp);
+    unsigned char* col = enif_make_new_binary(env, (size_t)r->slots * 4, &tcol);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_slots(r->h, (uint64_t*)rp, (uint32_t*)col);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), trp, tcol);
+}
+
+/* delivered(Sim) -> {ok, <<0|1 per vertex>>} */
+static ERL_NIF_TERM nif_delivered(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    ERL_NIF_TERM t;
+    unsigned char* d = enif_make_new_binary(env, r->n, &t);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_delivered(r->h, d, r->n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), t);
+}
+
+static ErlNifFunc funcs[] = {
+    {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"set_alive", 2, nif_set_alive, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"reset_trees", 1, nif_reset_trees, 0},
+    {"broadcast", 2, nif_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+};
+
+ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

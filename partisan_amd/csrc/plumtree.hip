@@ -63,7 +63,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 // Reduce the per-thread counters of a workgroup and add them to a shard.
-__device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long* __restrict__ stats) {
+__device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long* __restrict__ stats,
+                                               int* ost_total) {
     __shared__ unsigned long long red[kBlock / 64][kNStat];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -90,6 +91,7 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
         } else {
             for (int w = 0; w < kBlock / 64; w++) s += red[w][i];
             if (s) atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kNStat + i], s);
+            if (s && i == S_OST_DELTA && ost_total) atomicAdd(ost_total, (int)(long long)s);
         }
     }
 }
@@ -107,10 +109,19 @@ __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_
 }
 
 // One vertex, one round.  `rep` is this thread's LDS column (stride kBlock)
-// for the reply FIFOs of its slots.
-__device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, uint16_t* rep, Ctr& c) {
+// for the reply FIFOs of its slots.  `pend`: the vertex's 16-vertex group
+// was flagged (it may have words); `due`: the lazy tick fires and it holds
+// outstanding rows.
+__device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
+                                          Ctr& c) {
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
+    if (pend) {
+        uint32_t any = 0;
+        for (uint32_t s = 0; s < deg; s++) any |= a.in_cur[rs + s];
+        pend = any != 0;
+    }
+    if (!pend && !due) return;
     if (!bit_alive(a.alive, v)) {
         // a dead vertex receives nothing: the words are dropped (cleared)
         if (pend)
@@ -240,8 +251,9 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
         if (p && s < push_pos) fifo_append(fifo, n, PSIM_MSG_BROADCAST, c);
         if (ihave & b) fifo_append(fifo, n, PSIM_MSG_IHAVE, c);
         const uint32_t e = rs + s;
+        const uint32_t u = a.col[e];
         a.in_nxt[a.rev[e]] = fifo | (myround << 16);
-        a.pend_nxt[a.col[e]] = 1;
+        a.pend_nxt[u >> kGroupShift] = 1;
         sent = true;
     }
     if (sent) {
@@ -259,19 +271,55 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     c.live_delta += (uint32_t)live_delta;
 }
 
+// A workgroup owns kChunkV consecutive vertices.  Each thread looks at 4 of
+// them: their group flag (set by any sender to the group) and, on a tick
+// round while some vertex holds outstanding rows, their outstanding byte.
+// Candidates are compacted into an LDS list and spread over the threads.
 __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     __shared__ uint16_t rep[kMaxDeg * kBlock];
+    __shared__ uint32_t cand[kChunkV];
+    __shared__ uint32_t ncand;
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = blockIdx.x * kChunkV;
+    if (t == 0) ncand = 0;
+    __syncthreads();
+    const uint32_t v0 = base + 4 * t;
+    uint32_t pmask = 0, dmask = 0;
+    if (v0 < a.n) {
+        const uint32_t g = v0 >> kGroupShift;
+        if (a.pend_cur[g]) {
+            pmask = 0xFu;
+            if ((t & 3) == 0) a.pend_cur[g] = 0;   // the 4 threads of a group share the byte
+        }
+        if (a.tick && *a.ost_total > 0) {
+            uint32_t w;
+            if (v0 + 4 <= a.n) w = *reinterpret_cast<const uint32_t*>(a.ost + v0);
+            else { w = 0; for (uint32_t i = 0; v0 + i < a.n; i++) w |= uint32_t(a.ost[v0 + i]) << (8 * i); }
+            for (int i = 0; i < 4; i++) dmask |= ((w >> (8 * i)) & 0xFFu) ? (1u << i) : 0u;
+        }
+        if (v0 + 4 > a.n) {
+            const uint32_t valid = (1u << (a.n - v0)) - 1u;
+            pmask &= valid;
+            dmask &= valid;
+        }
+    }
+    const uint32_t m = pmask | dmask;
+    if (m) {
+        const uint32_t off = atomicAdd(&ncand, (uint32_t)__popc(m));
+        uint32_t k = off;
+        for (int i = 0; i < 4; i++)
+            if (m & (1u << i)) cand[k++] = ((v0 + i) << 2) | (((pmask >> i) & 1u) << 1) | ((dmask >> i) & 1u);
+    }
+    __syncthreads();
+    const uint32_t nc = ncand;
+    if (nc == 0) return;                          // uniform: idle chunk
     Ctr c;
     c.zero();
-    const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.n; v += stride) {
-        const bool pend = a.pend_cur[v] != 0;
-        const bool due = a.tick && a.ost[v];
-        if (!pend && !due) continue;
-        if (pend) a.pend_cur[v] = 0;
-        pt_vertex(a, v, pend, &rep[threadIdx.x], c);
+    for (uint32_t i = t; i < nc; i += kBlock) {
+        const uint32_t x = cand[i];
+        pt_vertex(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
-    flush_counters(c, a.stats);
+    flush_counters(c, a.stats, a.ost_total);
 }
 
 // The origin's {broadcast, Id, Payload, Mod} cast (:565-569): eager_push/4
@@ -295,7 +343,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
         const uint32_t e = rs + s;
         if (eager & b) {
             a.in_nxt[a.rev[e]] = PSIM_MSG_BROADCAST;  // Round 0
-            a.pend_nxt[a.col[e]] = 1;
+            a.pend_nxt[a.col[e] >> kGroupShift] = 1;
             nmsg++;
         }
         if ((lazy & b) && !(outst & b)) {
@@ -307,6 +355,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
     if ((outst0 != 0) != (outst != 0)) {
         a.ost[v] = 1;
         atomicAdd(&a.stats[S_OST_DELTA], 1ull);
+        atomicAdd(a.ost_total, 1);
     }
     if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
     if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);
@@ -344,6 +393,8 @@ __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
     }
 }
 
+uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }
+
 uint32_t grid_for(uint32_t n) {
     uint32_t g = (n + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;     // grid-stride beyond 32 blocks per CU
@@ -353,7 +404,7 @@ uint32_t grid_for(uint32_t n) {
 }  // namespace
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pt_round_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pt_round_kernel, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

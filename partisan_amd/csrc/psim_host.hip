@@ -45,6 +45,7 @@ struct psim_handle {
     unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
     unsigned long long* h_stats = nullptr;   // pinned mirror
     unsigned long long* scratch = nullptr;   // 1 counter
+    int* ost_total = nullptr;                // device mirror of ost_cnt
     hipEvent_t ev[2 * kChunk] = {};
 
     uint32_t par = 0;          // inbox buffer the next round reads
@@ -109,6 +110,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.pend_cur = h->pend[par];
     a.pend_nxt = h->pend[par ^ 1];
     a.ost = h->ost;
+    a.ost_total = h->ost_total;
     a.stats = stats;
     a.tick = tick;
     a.mono8 = h->serial & 0xFFu;
@@ -238,6 +240,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (hipMalloc(&h->stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipHostMalloc(&h->h_stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->ost_total, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMemset(h->ost_total, 0, 64) != hipSuccess) { rc = PSIM_EHIP; break; }
         for (auto& e : h->ev)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
     } while (0);
@@ -254,6 +258,7 @@ int psim_destroy(psim_handle* h) {
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);
+    if (h->ost_total) (void)hipFree(h->ost_total);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -336,12 +341,13 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     // device arrays
     auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
     const size_t nw = (size_t(n) + 31) / 32;
+    const size_t ng = (size_t(n) + (1u << kGroupShift) - 1) >> kGroupShift;
     if (alloc((void**)&h->rowp, (size_t(n) + 1) * 4) != hipSuccess || alloc((void**)&h->col, E * 4) != hipSuccess ||
         alloc((void**)&h->rev, E * 4) != hipSuccess || alloc((void**)&h->memb, size_t(n) * 4) != hipSuccess ||
         alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(n) * 16) != hipSuccess ||
         alloc((void**)&h->in[0], E * 4) != hipSuccess || alloc((void**)&h->in[1], E * 4) != hipSuccess ||
-        alloc((void**)&h->pend[0], n) != hipSuccess || alloc((void**)&h->pend[1], n) != hipSuccess ||
-        alloc((void**)&h->ost, n) != hipSuccess) {
+        alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess ||
+        alloc((void**)&h->ost, size_t(n) + 4) != hipSuccess) {
         free_graph(h);
         return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", n, (unsigned long long)E);
     }
@@ -356,9 +362,10 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     HIPCHK(h, hipMemset(h->vs, 0, size_t(n) * 16));
     HIPCHK(h, hipMemset(h->in[0], 0, E * 4));
     HIPCHK(h, hipMemset(h->in[1], 0, E * 4));
-    HIPCHK(h, hipMemset(h->pend[0], 0, n));
-    HIPCHK(h, hipMemset(h->pend[1], 0, n));
-    HIPCHK(h, hipMemset(h->ost, 0, n));
+    HIPCHK(h, hipMemset(h->pend[0], 0, ng));
+    HIPCHK(h, hipMemset(h->pend[1], 0, ng));
+    HIPCHK(h, hipMemset(h->ost, 0, size_t(n) + 4));
+    HIPCHK(h, hipMemset(h->ost_total, 0, 64));
     HIPCHK(h, hipDeviceSynchronize());
     h->h_rowp = std::move(rp);
     h->h_col = std::move(cc);

@@ -10,6 +10,8 @@ constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard
+constexpr int kGroupShift = 4;       // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
+constexpr uint32_t kChunkV = 1024;   // vertices owned by one round-kernel workgroup
 
 // counter indices (1..5 = PSIM_MSG_* kinds)
 enum Stat : int {
@@ -37,9 +39,10 @@ struct PtArgs {
     uint4* __restrict__ vs;                // [n]   state records
     uint32_t* __restrict__ in_cur;         // [E]   words read this round (receiver slots)
     uint32_t* __restrict__ in_nxt;         // [E]   words written this round
-    uint8_t* __restrict__ pend_cur;        // [n]   1 = inbox non-empty
+    uint8_t* __restrict__ pend_cur;        // [ceil(n/16)] 1 = some vertex of the group has words
     uint8_t* __restrict__ pend_nxt;
-    uint8_t* __restrict__ ost;             // [n]   1 = outstanding rows exist
+    uint8_t* __restrict__ ost;             // [n+3] 1 = outstanding rows exist
+    int* ost_total;                        // device count of vertices with outstanding rows
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)

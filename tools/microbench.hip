@@ -1,0 +1,78 @@
+// Micro-benchmarks of the access patterns the Plumtree round kernel uses.
+// hipcc --offload-arch=gfx950 -O3 -o /tmp/mb tools/microbench.hip && /tmp/mb
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <random>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+__global__ void scatter32(uint32_t* __restrict__ out, const uint32_t* __restrict__ idx, uint32_t m) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[idx[i]] = i | 1u;
+}
+__global__ void scatter8(uint8_t* __restrict__ out, const uint32_t* __restrict__ idx, uint32_t m, uint32_t mask) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[idx[i] & mask] = 1;
+}
+__global__ void gather32(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, const uint32_t* __restrict__ idx, uint32_t m) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = in[idx[i]];
+}
+__global__ void copy128(uint4* __restrict__ out, const uint4* __restrict__ in, uint32_t m) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = in[i];
+}
+__global__ void scan8(const uint8_t* __restrict__ in, uint32_t n, uint32_t* cnt) {
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) c += in[i];
+    if (c) atomicAdd(cnt, c);
+}
+__global__ void scan128(const uint4* __restrict__ in, uint32_t n16, uint32_t* cnt) {
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
+        uint4 x = in[i]; c += (x.x | x.y | x.z | x.w) != 0;
+    }
+    if (c) atomicAdd(cnt, c);
+}
+__global__ void empty_kernel() {}
+
+int main() {
+    const uint32_t E = 50'000'000, M = 26'000'000, N = 10'000'000;
+    std::vector<uint32_t> h(M);
+    std::mt19937 rng(1);
+    for (auto& x : h) x = rng() % E;
+    uint32_t *idx, *buf, *out, *cnt; uint8_t* flags;
+    CK(hipMalloc(&idx, M * 4)); CK(hipMalloc(&buf, E * 4ull)); CK(hipMalloc(&out, E * 4ull));
+    CK(hipMalloc(&flags, N)); CK(hipMalloc(&cnt, 4));
+    CK(hipMemcpy(idx, h.data(), M * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(buf, 0, E * 4ull)); CK(hipMemset(flags, 0, N));
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    auto T = [&](const char* name, double bytes, auto fn) {
+        for (int w = 0; w < 3; w++) fn();
+        CK(hipDeviceSynchronize());
+        const int R = 20; float ms = 0;
+        CK(hipEventRecord(a)); for (int r = 0; r < R; r++) fn(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&ms, a, b)); ms /= R;
+        printf("%-44s %9.1f us  %8.1f GB/s(useful)  %7.2f G ops/s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9, (double)M / (ms * 1e-3) / 1e9);
+        return 0;
+    };
+    dim3 g(8192), blk(256);
+    T("empty kernel", 0, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0); });
+    T("copy 128-bit 200MB->200MB", 2.0 * E * 4, [&] { hipLaunchKernelGGL(copy128, g, blk, 0, 0, (uint4*)out, (const uint4*)buf, E / 4); });
+    T("scatter 4B into 200MB (26M)", 4.0 * M, [&] { hipLaunchKernelGGL(scatter32, g, blk, 0, 0, buf, idx, M); });
+    T("gather 4B from 200MB (26M)", 4.0 * M, [&] { hipLaunchKernelGGL(gather32, g, blk, 0, 0, out, buf, idx, M); });
+    T("scatter 1B into 10MB  (26M)", 1.0 * M, [&] { hipLaunchKernelGGL(scatter8, g, blk, 0, 0, flags, idx, M, (1u << 23) - 1); });
+    T("scatter 1B into 1MB   (26M)", 1.0 * M, [&] { hipLaunchKernelGGL(scatter8, g, blk, 0, 0, flags, idx, M, (1u << 20) - 1); });
+    T("scatter 1B into 128KB (26M)", 1.0 * M, [&] { hipLaunchKernelGGL(scatter8, g, blk, 0, 0, flags, idx, M, (1u << 17) - 1); });
+    T("scan 1B/thread 10MB", 1.0 * N, [&] { hipLaunchKernelGGL(scan8, g, blk, 0, 0, flags, N, cnt); });
+    T("scan 16B/thread 10MB", 1.0 * N, [&] { hipLaunchKernelGGL(scan128, dim3(2048), blk, 0, 0, (const uint4*)flags, N / 16, cnt); });
+    T("scan 16B/thread 200MB", 4.0 * E, [&] { hipLaunchKernelGGL(scan128, g, blk, 0, 0, (const uint4*)buf, E / 4, cnt); });
+    // sorted-within-chunk scatter: idx sorted in 64K windows (locality)
+    std::vector<uint32_t> hs(h);
+    for (uint32_t i = 0; i < M; i += 65536) std::sort(hs.begin() + i, hs.begin() + std::min<uint32_t>(M, i + 65536));
+    CK(hipMemcpy(idx, hs.data(), M * 4, hipMemcpyHostToDevice));
+    T("scatter 4B into 200MB, 64K-window sorted", 4.0 * M, [&] { hipLaunchKernelGGL(scatter32, g, blk, 0, 0, buf, idx, M); });
+    std::sort(hs.begin(), hs.end());
+    CK(hipMemcpy(idx, hs.data(), M * 4, hipMemcpyHostToDevice));
+    T("scatter 4B into 200MB, fully sorted", 4.0 * M, [&] { hipLaunchKernelGGL(scatter32, g, blk, 0, 0, buf, idx, M); });
+    return 0;
+}
