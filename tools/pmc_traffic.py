@@ -1,0 +1,58 @@
+"""Per-launch HBM traffic of pt_round_kernel from rocprofv3 PMC passes.
+
+Collected as MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7 prescribe:
+two separate --pmc passes (FETCH_SIZE, WRITE_SIZE; they do not fit one
+pass), units KiB (hbm bytes = (FETCH_SIZE + WRITE_SIZE) * 1024).  The gfx950
+caveat: FETCH_SIZE counts exactly half the bytes of WIDE coalesced streaming
+reads; this kernel's reads are mostly narrow/scattered, so the raw value is
+reported and the doubled read side is given as an upper bound.
+
+usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write \
+          --n 10000000 --peers 5 --rounds-per-step 16 --steps 3 [--out profiles/pmc_traffic.json]
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def load(d, counter):
+    path = os.path.join(d, "run_counter_collection.csv")
+    rows = [r for r in csv.DictReader(open(path)) if "pt_round_kernel" in r["Kernel_Name"]
+            and r["Counter_Name"] == counter]
+    return [float(r["Counter_Value"]) * 1024.0 for r in rows]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("fetch_dir")
+    p.add_argument("write_dir")
+    p.add_argument("--n", type=int, required=True)
+    p.add_argument("--peers", type=int, required=True)
+    p.add_argument("--rounds-per-step", type=int, required=True)
+    p.add_argument("--steps", type=int, required=True, help="steps incl. warmup in the profiled run")
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    f = load(a.fetch_dir, "FETCH_SIZE")
+    w = load(a.write_dir, "WRITE_SIZE")
+    counted = a.rounds_per_step * a.steps
+    fetch = sum(f) / counted
+    write = sum(w) / counted
+    out = {
+        "n": a.n, "peers": a.peers, "kernel": "pt_round_kernel",
+        "launches_profiled": len(f), "counted_launches": counted,
+        "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+        "hbm_bytes_per_launch": fetch + write,
+        "hbm_bytes_per_launch_read_doubled": 2 * fetch + write,
+        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB*1024, "
+                  "summed over all pt_round_kernel launches / counted rounds",
+    }
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(out, fh, indent=1)
+            fh.write("\n")
+
+
+if __name__ == "__main__":
+    main()
