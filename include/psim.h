@@ -130,6 +130,22 @@ int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
  * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
  * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
 int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* --- partisan_vclock on dense lanes ----------------------------------- */
+/* A clock is PSIM_VC_LANES u32 lanes, lane i = actor i (actor ids are ranks
+ * in the sorted actor table, so lane order is the reference's term order).
+ * Lane value 0 = actor absent, c+1 = counter c: descends/2's presence rule
+ *  is then a lane-wise compare.  Batched over n clocks, one
+ * wave per clock.  Host buffers, copied. */
+#define PSIM_VC_LANES 64
+/* partisan_vclock:descends/2 (src/partisan_vclock.erl:63-73): out[i] = A_i descends B_i */
+int  psim_vclock_descends(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n);
+/* partisan_vclock:dominates/2 (:75-77) */
+int  psim_vclock_dominates(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n);
+/* partisan_vclock:merge([A, B]) (:102-129): lane-wise max */
+int  psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
+/* partisan_vclock:increment(Actor, A) (:140-153) */
+int  psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

@@ -67,6 +67,10 @@ SIGNATURES = {
     "psim_get_delivered": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_get_inflight": (C.c_int, [_H, _P(C.c_uint32), C.c_uint64]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
+    "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
+    "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
+    "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_vclock_increment": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
 }
 
 _lib = None

@@ -60,6 +60,8 @@ struct psim_handle {
     uint64_t inflight = 0;     // messages emitted by the last round / origin
     double kernel_ms_total = 0;
     uint64_t rounds_total = 0;
+    void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
+    size_t scratch_cap = 0;
 };
 
 namespace {
@@ -259,6 +261,7 @@ int psim_destroy(psim_handle* h) {
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->ost_total) (void)hipFree(h->ost_total);
+    if (h->scratch_buf) (void)hipFree(h->scratch_buf);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -514,6 +517,65 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     HIPCHK(hh, hipStreamSynchronize(h->stream));
     HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
     return PSIM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+void* scratch(psim_handle* h, size_t bytes) {
+    if (bytes > h->scratch_cap) {
+        if (h->scratch_buf) (void)hipFree(h->scratch_buf);
+        h->scratch_buf = nullptr;
+        h->scratch_cap = 0;
+        if (hipMalloc(&h->scratch_buf, bytes) != hipSuccess) return nullptr;
+        h->scratch_cap = bytes;
+    }
+    return h->scratch_buf;
+}
+
+// one batched vclock op over host buffers: A, B (or actor ids), outputs
+int vc_op(psim_handle* h, int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
+          uint8_t* outb, size_t n) {
+    if (!h || !a || n == 0) return n == 0 ? PSIM_OK : PSIM_EINVAL;
+    if ((op <= 2 && !b) || (op == 3 && !actor) || (op >= 2 && !out) || (op <= 1 && !outb)) return PSIM_EINVAL;
+    if (op == 3)
+        for (size_t i = 0; i < n; i++)
+            if (actor[i] >= PSIM_VC_LANES) return fail(h, PSIM_EINVAL, "actor %u >= %d", actor[i], PSIM_VC_LANES);
+    const size_t cb = n * PSIM_VC_LANES * 4;
+    char* base = (char*)scratch(h, 3 * cb + n * 4 + n + 64);
+    if (!base) return fail(h, PSIM_ENOMEM, "vclock scratch of %zu bytes", 3 * cb);
+    uint32_t* da = (uint32_t*)base;
+    uint32_t* db = (uint32_t*)(base + cb);
+    uint32_t* dout = (uint32_t*)(base + 2 * cb);
+    uint32_t* dact = (uint32_t*)(base + 3 * cb);
+    uint8_t* doutb = (uint8_t*)(base + 3 * cb + n * 4);
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(da, a, cb, hipMemcpyHostToDevice, h->stream));
+    if (op <= 2) HIPCHK(h, hipMemcpyAsync(db, b, cb, hipMemcpyHostToDevice, h->stream));
+    if (op == 3) HIPCHK(h, hipMemcpyAsync(dact, actor, n * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, launch_vc(op, da, db, dact, dout, doutb, n, h->stream));
+    if (op >= 2) HIPCHK(h, hipMemcpyAsync(out, dout, cb, hipMemcpyDeviceToHost, h->stream));
+    else HIPCHK(h, hipMemcpyAsync(outb, doutb, n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_vclock_descends(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n) {
+    return vc_op(h, 0, a, b, nullptr, nullptr, out, n);
+}
+int psim_vclock_dominates(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n) {
+    return vc_op(h, 1, a, b, nullptr, nullptr, out, n);
+}
+int psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
+    return vc_op(h, 2, a, b, nullptr, out, nullptr, n);
+}
+int psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n) {
+    return vc_op(h, 3, a, nullptr, actor, out, nullptr, n);
 }
 
 int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds) {

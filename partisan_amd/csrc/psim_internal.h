@@ -51,6 +51,9 @@ struct PtArgs {
 };
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
+// op: 0 descends, 1 dominates, 2 merge, 3 increment
+hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
+                     uint8_t* outb, size_t n, hipStream_t s);
 hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
