@@ -146,6 +146,35 @@ int  psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uin
 /* partisan_vclock:increment(Actor, A) (:140-153) */
 int  psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n);
 
+/* --- Demers epidemics (protocols/demers_*.erl) ------------------------ */
+typedef struct psim_demers_stats {
+    uint64_t rm_sent;              /* {broadcast, Id, ServerRef, Message, From} (rumor mongering) */
+    uint64_t push_sent;            /* {push, From, AllMessages} (anti-entropy)    */
+    uint64_t pull_sent;            /* {pull, From, AllMessages}                   */
+    uint64_t delivered_new;        /* (vertex, rumor) pairs newly stored          */
+    uint64_t complete;             /* vertices holding every rumor after the round */
+    uint64_t algo_bytes;           /* 2*N*M/8 + pushes*6*M/8 + 32*msgs */
+    double   kernel_ms;
+} psim_demers_stats;
+/* Full-membership Demers epidemic over n vertices with m <= 64 rumors whose
+ * origins are Philox draws (stream kind 1).  rm_on: rumor mongering with
+ * fanout 2 (demers_rumor_mongering.erl :92-186); ae_period: anti-entropy
+ * push-pull with fanout 2 every ae_period rounds (demers_anti_entropy.erl
+ * :118-195; 0 = off, else >= 2).  Both on share one message store.
+ * Replaces starting both gen_servers on every node (:50-76). */
+int  psim_demers_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on);
+/* handle_cast({broadcast, ServerRef, Message}) at every rumor's origin
+ * (RM :92-115; AE :95-106, which only stores: ids {Node, 0}, Q20). */
+int  psim_demers_broadcast_all(psim_handle* h);
+int  psim_demers_step(psim_handle* h, uint32_t rounds, psim_demers_stats* stats, size_t cap);
+/* Runs until every vertex stores every rumor (or max_rounds). */
+int  psim_demers_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* stats, size_t cap,
+                     uint32_t* rounds_run);
+/* seen[n]: bit i = the rumor with store id i (i = rumor index; with
+ * anti-entropy alone, rumors of one origin share the first one's id, Q20). */
+int  psim_demers_get_seen(const psim_handle* h, uint64_t* seen, size_t n);
+int  psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

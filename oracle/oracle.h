@@ -154,6 +154,35 @@ void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono,
 /* Round field of the broadcast each vertex accepted for (origin, mono); 0xFFFFFFFF if none */
 void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint32_t* out);
 
+/* ------------------------------------------------------------------ */
+/* Philox4x32-10 (Random123) -- the simulation's counter-based RNG      */
+/* ------------------------------------------------------------------ */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* select_random_sublist(usort(Members), 2) over members 0..n-1 for the
+ * Philox stream (seed, v, event, kind); returns the number of draws (<= 2) */
+int orc_dm_sample2(uint64_t seed, uint32_t v, uint32_t event, uint32_t kind, uint32_t n, uint32_t* out);
+
+/* ------------------------------------------------------------------ */
+/* Demers rumor mongering + anti-entropy (protocols/demers_*.erl)       */
+/* ------------------------------------------------------------------ */
+typedef struct orc_dm_stats {
+    uint64_t rm_sent, push_sent, pull_sent;
+    uint64_t delivered_new;     /* (vertex, rumor) pairs newly stored */
+    uint64_t complete;          /* vertices holding every rumor after the round */
+} orc_dm_stats;
+
+typedef struct orc_demers orc_demers;
+orc_demers* orc_dm_create(uint32_t n, uint32_t m, uint64_t seed, uint32_t ae_period, uint32_t rm_on);
+void orc_dm_destroy(orc_demers* s);
+uint32_t orc_dm_origin(const orc_demers* s, uint32_t m);
+uint64_t orc_dm_full_mask(const orc_demers* s);
+void orc_dm_broadcast_all(orc_demers* s);
+uint32_t orc_dm_step(orc_demers* s, uint32_t rounds, orc_dm_stats* st);
+uint32_t orc_dm_run(orc_demers* s, uint32_t max_rounds, orc_dm_stats* st, size_t cap);
+void orc_dm_get_seen(const orc_demers* s, uint64_t* out);
+size_t orc_dm_pending(const orc_demers* s, uint32_t* type, uint32_t* src, uint32_t* dst, uint32_t* m,
+                      uint64_t* payload, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

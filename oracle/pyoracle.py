@@ -32,6 +32,14 @@ class RoundStats(C.Structure):
                 ("max_per_edge", C.c_uint64)]
 
 
+class DmStats(C.Structure):
+    _fields_ = [("rm_sent", C.c_uint64), ("push_sent", C.c_uint64), ("pull_sent", C.c_uint64),
+                ("delivered_new", C.c_uint64), ("complete", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 MSG_NAMES = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
 
 _lib = None
@@ -92,6 +100,23 @@ def lib():
         L.orc_pt_get_outstanding.restype = sz
         L.orc_pt_get_delivered.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint8)]
         L.orc_pt_get_recv_round.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+        L.orc_dm_sample2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.orc_dm_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+        L.orc_dm_create.restype = C.c_void_p
+        L.orc_dm_destroy.argtypes = [C.c_void_p]
+        L.orc_dm_origin.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_dm_origin.restype = C.c_uint32
+        L.orc_dm_full_mask.argtypes = [C.c_void_p]
+        L.orc_dm_full_mask.restype = C.c_uint64
+        L.orc_dm_broadcast_all.argtypes = [C.c_void_p]
+        L.orc_dm_step.argtypes = [C.c_void_p, C.c_uint32, P(DmStats)]
+        L.orc_dm_run.argtypes = [C.c_void_p, C.c_uint32, P(DmStats), sz]
+        L.orc_dm_run.restype = C.c_uint32
+        L.orc_dm_get_seen.argtypes = [C.c_void_p, P(C.c_uint64)]
+        L.orc_dm_pending.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), P(C.c_uint32),
+                                     P(C.c_uint64), sz]
+        L.orc_dm_pending.restype = sz
         _lib = L
     return _lib
 
@@ -337,3 +362,68 @@ def stats_dict(s):
              outstanding=int(s.outstanding), outstanding_live=int(s.outstanding_live),
              max_per_edge=int(s.max_per_edge))
     return d
+
+
+# ---------------------------------------------------------------- philox / demers
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().orc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def sample2(seed, v, event, kind, n):
+    o = (C.c_uint32 * 2)()
+    k = lib().orc_dm_sample2(seed, v, event, kind, n, o)
+    return list(o[:k])
+
+
+class Demers:
+    def __init__(self, n, m, seed, ae_period=2, rm_on=True):
+        self.n, self.m = n, m
+        self._h = lib().orc_dm_create(n, m, seed, ae_period, 1 if rm_on else 0)
+        if not self._h:
+            raise ValueError("bad demers config")
+
+    def close(self):
+        if self._h:
+            lib().orc_dm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def origins(self):
+        return [lib().orc_dm_origin(self._h, i) for i in range(self.m)]
+
+    def full_mask(self):
+        return lib().orc_dm_full_mask(self._h)
+
+    def broadcast_all(self):
+        lib().orc_dm_broadcast_all(self._h)
+
+    def step(self, rounds=1):
+        st = (DmStats * rounds)()
+        lib().orc_dm_step(self._h, rounds, st)
+        return [s.as_dict() for s in st]
+
+    def run(self, max_rounds=10000, cap=4096):
+        st = (DmStats * cap)()
+        r = lib().orc_dm_run(self._h, max_rounds, st, cap)
+        return [st[i].as_dict() for i in range(min(r, cap))], r
+
+    def seen(self):
+        out = np.zeros(self.n, dtype=np.uint64)
+        lib().orc_dm_get_seen(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return out
+
+    def pending(self):
+        n = lib().orc_dm_pending(self._h, None, None, None, None, None, 0)
+        t, s, d, m = (np.zeros(max(1, n), np.uint32) for _ in range(4))
+        p = np.zeros(max(1, n), np.uint64)
+        P = C.POINTER
+        lib().orc_dm_pending(self._h, t.ctypes.data_as(P(C.c_uint32)), s.ctypes.data_as(P(C.c_uint32)),
+                             d.ctypes.data_as(P(C.c_uint32)), m.ctypes.data_as(P(C.c_uint32)),
+                             p.ctypes.data_as(P(C.c_uint64)), n)
+        return t[:n], s[:n], d[:n], m[:n], p[:n]

@@ -45,6 +45,15 @@ class RoundStats(C.Structure):
         return d
 
 
+class DemersStats(C.Structure):
+    _fields_ = [("rm_sent", C.c_uint64), ("push_sent", C.c_uint64), ("pull_sent", C.c_uint64),
+                ("delivered_new", C.c_uint64), ("complete", C.c_uint64), ("algo_bytes", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -67,6 +76,12 @@ SIGNATURES = {
     "psim_get_delivered": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_get_inflight": (C.c_int, [_H, _P(C.c_uint32), C.c_uint64]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
+    "psim_demers_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "psim_demers_broadcast_all": (C.c_int, [_H]),
+    "psim_demers_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),
+    "psim_demers_run": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t, _P(C.c_uint32)]),
+    "psim_demers_get_seen": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
+    "psim_demers_origins": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
@@ -94,6 +109,5 @@ def lib():
 
 def check(rc, h=None):
     if rc != 0:
-        detail = lib().psim_last_error(h).decode() if h else ""
-        raise PsimError(rc, detail)
+        raise PsimError(rc, lib().psim_last_error(h).decode())
     return rc

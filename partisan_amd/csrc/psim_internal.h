@@ -50,6 +50,34 @@ struct PtArgs {
     uint32_t root;                         // origin of the current heartbeat
 };
 
+// Demers rumor mongering + anti-entropy (demers.hip)
+constexpr uint32_t kDmPushCap = 24;   // AE pushes one vertex can receive per tick (Poisson(2) in-degree)
+struct DmArgs {
+    uint32_t n, m;
+    uint2 key;                            // Philox key {seed_lo, seed_hi}
+    uint32_t rm_on;
+    uint32_t tick, tick_idx, prev_tick;   // AE tick at the end of this round; tick indices
+    unsigned long long full;              // every rumor id's bit
+    unsigned long long* __restrict__ seen;       // [n] the message store
+    unsigned long long* __restrict__ snap;       // [n] AE payload taken at the tick
+    unsigned long long* __restrict__ rm_cur_reg; // [n] RM inbox read this round
+    unsigned long long* __restrict__ rm_cur_t0;
+    unsigned long long* __restrict__ rm_cur_t1;
+    unsigned long long* __restrict__ rm_nxt_reg; // [n] RM inbox written this round
+    unsigned long long* __restrict__ rm_nxt_t0;
+    unsigned long long* __restrict__ rm_nxt_t1;
+    uint32_t* __restrict__ pushcnt_cur;   // [n]
+    uint32_t* __restrict__ pushcnt_nxt;
+    uint32_t* __restrict__ pushlist_cur;  // [n][kDmPushCap]
+    uint32_t* __restrict__ pushlist_nxt;
+    unsigned long long* __restrict__ pull_cur;   // [n][2]
+    unsigned long long* __restrict__ pull_nxt;
+    unsigned long long* __restrict__ stats;      // [kStatShards][kNStat]: 1 rm, 2 push, 3 pull, 4 deliv, 5 complete, 6 overflow
+};
+hipError_t launch_dm_origins(uint2 key, uint32_t n, uint32_t m, uint32_t* origin, hipStream_t s);
+hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const uint32_t* idbit, hipStream_t s);
+hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
+
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
