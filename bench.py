@@ -16,9 +16,10 @@ algorithmic bytes of the timed rounds / their summed hipEvent durations
 scalar port of the reference modules) on a bounded sample of the same
 workload, rank 0 only.
 
-Multi-GPU (round 1): every rank runs an independent replica of the workload
-on its own GPU ("parallelism": "replicas"); the vertex-sharded RCCL exchange
-is the next step (DESIGN.md "Multi-GPU").
+Multi-GPU (N > 1): the SAME 10M-peer overlay is vertex-sharded over the N
+GPUs (strong scaling); cross-shard records move every round
+with RCCL all-to-all over xGMI (torch.distributed backend "nccl");
+--mode replicas runs N independent copies instead.
 """
 import argparse
 import json
@@ -45,6 +46,11 @@ def parse():
     p.add_argument("--cpu-sample-n", type=int, default=1_000_000)
     p.add_argument("--cpu-sample-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
+    p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
+                   help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
+    p.add_argument("--all-on-device0", action="store_true",
+                   help="test aid: put every rank on GPU 0 (needs --transport gloo)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by tools/pmc_traffic.py for this workload")
     return p.parse_args()
@@ -55,9 +61,16 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
+    if args.all_on_device0:
+        local = 0
     if world > 1:
+        import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")
+        torch.cuda.set_device(local)
+        if args.transport == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo", init_method="env://")
         pg = dist
     return rank, local, world, pg
 
@@ -67,22 +80,21 @@ def barrier(pg):
         pg.barrier()
 
 
-def max_over_ranks(pg, x):
+def _reduce(pg, x, op):
     if pg is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if pg.get_backend() == "nccl" else "cpu")
+    pg.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(pg, x):
+    return x if pg is None else _reduce(pg, x, pg.ReduceOp.MAX)
 
 
 def sum_over_ranks(pg, x):
-    if pg is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
+    return x if pg is None else _reduce(pg, x, pg.ReduceOp.SUM)
 
 
 def one_step(sim, root):
@@ -121,31 +133,52 @@ def main():
 
     import partisan_amd as pa
 
+    sharded = world > 1 and args.mode == "sharded"
     rp, col = pa.overlay.random_regular(args.n, args.peers, args.seed)
-    sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
-    sim.load_overlay(rp, col)
+    if sharded:
+        from partisan_amd.shard import ShardedPlumtree
+        sp = ShardedPlumtree(rp, col, rank, world, device=local, backend=args.transport,
+                             lazy_tick_rounds=args.lazy_tick_rounds)
+        sim = sp.sim
+    else:
+        sp = None
+        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
+        sim.load_overlay(rp, col)
     del rp, col
     root = 0
 
+    def step():
+        if sp is not None:
+            sp.reset_trees()
+            sp.broadcast(root)
+            return sp.run()
+        return one_step(sim, root)
+
     for _ in range(args.warmup):
-        one_step(sim, root)
+        step()
 
     algo_bytes = 0
     round_ms = 0.0
     rounds_per_step = []
+    if sp is not None:
+        sp.local_algo_bytes, sp.local_kernel_ms = 0, 0.0
     barrier(pg)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        stats, rounds = one_step(sim, root)
+        stats, rounds = step()
         rounds_per_step.append(rounds)
-        algo_bytes += sum(s["algo_bytes"] for s in stats)
-        round_ms += sum(s["kernel_ms"] for s in stats)
-    # psim_run returns after hipStreamSynchronize on the library stream
+        if sp is None:
+            algo_bytes += sum(s["algo_bytes"] for s in stats)
+            round_ms += sum(s["kernel_ms"] for s in stats)
+    # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
     barrier(pg)
     t1 = time.perf_counter()
+    if sp is not None:   # this GPU's own bytes and launch times
+        algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
 
     step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
-    peer_rounds = sum_over_ranks(pg, float(args.n) * sum(rounds_per_step) / args.steps)
+    n_units = args.n if sharded else args.n * world      # peers simulated by the whole job
+    peer_rounds = float(n_units) * sum(rounds_per_step) / args.steps
     value = peer_rounds / step_s
     # per-launch figures over the rounds up to quiescence (the no-op tail of a
     # step's last chunk is not counted): hipEvent durations of each launch
@@ -171,7 +204,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": step_s * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
@@ -182,7 +215,8 @@ def main():
                 "n_peers": args.n,
                 "overlay": f"random symmetric, {args.peers} peers per vertex (HyParView active view)",
                 "rounds_to_convergence": rounds_per_step[-1],
-                "parallelism": "replicas" if world > 1 else "single",
+                "parallelism": (f"vertex-sharded x{world}, RCCL all-to-all per round" if sharded
+                                else ("replicas" if world > 1 else "single")),
                 "device": sim.device_info(),
             },
             "roofline": {

@@ -130,6 +130,31 @@ int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
  * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
  * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
 int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* --- vertex sharding over several GPUs (one process per GPU) -------- */
+/* The overlay is split into `world` contiguous vertex ranges; this handle
+ * owns range `rank`.  Call before psim_load_csr, which then
+ * keeps only the local rows; getters (psim_get_plumtree, ...) return the
+ * local range, psim_set_alive still takes all n_global vertices.  Rounds are
+ * split-phase so that the transport stays the caller's (RCCL all-to-all-v
+ * via torch.distributed "nccl" on a node; gloo in tests):
+ *   psim_shard_broadcast / psim_shard_round  -> counts[d] records for shard d,
+ *       packed in the caller's device buffer at region_base[d] (uint2
+ *       {global receiver slot, word});
+ *   caller exchanges the regions;  psim_shard_ingest(received records);
+ *   the caller all-reduces the emitted-message and live-row counters and
+ *   stops at global quiescence. */
+int  psim_shard_init(psim_handle* h, int rank, int world);
+int  psim_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local, uint64_t* slot_base,
+                     uint32_t* n_global);
+/* region_base[world + 1]: record offsets of each destination's region; the
+ * last entry is the send buffer's capacity in records */
+int  psim_shard_layout(const psim_handle* h, uint64_t* region_base, size_t world);
+int  psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev, uint64_t send_cap,
+                          uint64_t* counts, int64_t* local_live);
+int  psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts,
+                      psim_round_stats* stats, int64_t* local_live);
+int  psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records);
+
 /* --- partisan_vclock on dense lanes ----------------------------------- */
 /* A clock is PSIM_VC_LANES u32 lanes, lane i = actor i (actor ids are ranks
  * in the sorted actor table, so lane order is the reference's term order).

@@ -76,6 +76,13 @@ SIGNATURES = {
     "psim_get_delivered": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_get_inflight": (C.c_int, [_H, _P(C.c_uint32), C.c_uint64]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
+    "psim_shard_init": (C.c_int, [_H, C.c_int, C.c_int]),
+    "psim_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),
+    "psim_shard_layout": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
+    "psim_shard_broadcast": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), C.c_void_p, C.c_uint64, _P(C.c_uint64),
+                                       _P(C.c_int64)]),
+    "psim_shard_round": (C.c_int, [_H, C.c_void_p, C.c_uint64, _P(C.c_uint64), _P(RoundStats), _P(C.c_int64)]),
+    "psim_shard_ingest": (C.c_int, [_H, C.c_void_p, C.c_uint64]),
     "psim_demers_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_demers_broadcast_all": (C.c_int, [_H]),
     "psim_demers_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),

@@ -108,6 +108,19 @@ __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_
     }
 }
 
+// Hand the word for sender slot e to its receiver: a local receiver slot
+// (rev[e] is a global slot id) plus its group flag, or -- receiver on another
+// shard -- the staging word of the sender slot, packed by pt_compact_kernel.
+__device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w) {
+    const uint32_t u = a.col[e] - a.v_lo;
+    if (u < a.n) {
+        a.in_nxt[a.rev[e] - a.slot_base] = w;
+        a.pend_nxt[u >> kGroupShift] = 1;
+    } else {
+        a.stage[e] = w;
+    }
+}
+
 // One vertex, one round.  `rep` is this thread's LDS column (stride kBlock)
 // for the reply FIFOs of its slots.  `pend`: the vertex's 16-vertex group
 // was flagged (it may have words); `due`: the lazy tick fires and it holds
@@ -122,7 +135,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
         pend = any != 0;
     }
     if (!pend && !due) return;
-    if (!bit_alive(a.alive, v)) {
+    if (!bit_alive(a.alive, a.v_lo + v)) {
         // a dead vertex receives nothing: the words are dropped (cleared)
         if (pend)
             for (uint32_t s = 0; s < deg; s++)
@@ -251,9 +264,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
         if (p && s < push_pos) fifo_append(fifo, n, PSIM_MSG_BROADCAST, c);
         if (ihave & b) fifo_append(fifo, n, PSIM_MSG_IHAVE, c);
         const uint32_t e = rs + s;
-        const uint32_t u = a.col[e];
-        a.in_nxt[a.rev[e]] = fifo | (myround << 16);
-        a.pend_nxt[u >> kGroupShift] = 1;
+        deliver_word(a, e, fifo | (myround << 16));
         sent = true;
     }
     if (sent) {
@@ -327,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
 // backend already did add_timestamp (backend :341-368).
 __global__ void pt_origin_kernel(PtArgs a) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const uint32_t v = a.root;
+    const uint32_t v = a.root;   // local index of the origin (only its owner launches this)
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
     const uint4 st = a.vs[v];
@@ -342,8 +353,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
         const uint32_t b = 1u << s;
         const uint32_t e = rs + s;
         if (eager & b) {
-            a.in_nxt[a.rev[e]] = PSIM_MSG_BROADCAST;  // Round 0
-            a.pend_nxt[a.col[e] >> kGroupShift] = 1;
+            deliver_word(a, e, PSIM_MSG_BROADCAST);  // Round 0
             nmsg++;
         }
         if ((lazy & b) && !(outst & b)) {
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void pt_count_live_kernel(PtArgs a, unsigne
     unsigned long long cnt = 0;
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.n; v += stride) {
-        if (!a.ost[v] || !bit_alive(a.alive, v)) continue;
+        if (!a.ost[v] || !bit_alive(a.alive, a.v_lo + v)) continue;
         uint32_t m = a.vs[v].z;
         const uint32_t rs = a.rowp[v];
         while (m) {
@@ -393,6 +403,65 @@ __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
     }
 }
 
+// Pack the staged cross-shard words into (global receiver slot, word)
+// records, one region per destination shard.  A workgroup owns <= 1024
+// entries of ONE destination's remote-slot list (blk = {rank, start, len}),
+// so it reserves its run with a single atomicAdd.  Record order inside a
+// region is irrelevant: every receiver slot has one writer per round.
+__global__ __launch_bounds__(kBlock) void pt_compact_kernel(PtArgs a, const uint32_t* __restrict__ rem,
+                                                            const uint4* __restrict__ blk,
+                                                            const uint32_t* __restrict__ send_base,
+                                                            uint32_t* __restrict__ cursor, uint2* __restrict__ out) {
+    __shared__ uint32_t wsum_[kBlock / 64];
+    __shared__ uint32_t base;
+    const uint4 b = blk[blockIdx.x];
+    const uint32_t t = threadIdx.x;
+    uint32_t e[4], w[4], cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t j = 4 * t + i;
+        w[i] = 0;
+        e[i] = 0;
+        if (j < b.z) {
+            e[i] = rem[b.y + j];
+            w[i] = a.stage[e[i]];
+            if (w[i]) { a.stage[e[i]] = 0; cnt++; }
+        }
+    }
+    // workgroup exclusive scan of cnt
+    const uint32_t lane = t & 63, wv = t >> 6;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63) wsum_[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int i = 0; i < kBlock / 64; i++) {
+        if (i < (int)wv) pre += wsum_[i];
+        tot += wsum_[i];
+    }
+    if (t == 0) base = tot ? atomicAdd(&cursor[b.x], tot) : 0u;
+    __syncthreads();
+    uint32_t pos = send_base[b.x] + base + pre + x - cnt;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (w[i]) out[pos++] = make_uint2(a.rev[e[i]], w[i]);
+}
+
+// Scatter records received from other shards into the local receiver slots.
+__global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2* __restrict__ rec, uint32_t nrec,
+                                                           const uint32_t* __restrict__ slot2v) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nrec) return;
+    const uint2 r = rec[i];
+    const uint32_t ls = r.x - a.slot_base;
+    a.in_nxt[ls] = r.y;
+    a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+}
+
 uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }
 
 uint32_t grid_for(uint32_t n) {
@@ -415,6 +484,19 @@ hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s) {
 
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s) {
     hipLaunchKernelGGL(pt_count_live_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
+                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s) {
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(pt_compact_kernel, dim3(nblk), dim3(kBlock), 0, s, a, rem, blk, send_base, cursor, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s) {
+    if (nrec == 0) return hipSuccess;
+    hipLaunchKernelGGL(pt_ingest_kernel, dim3((nrec + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a, rec, nrec, slot2v);
     return hipGetLastError();
 }
 

@@ -63,6 +63,21 @@ struct psim_handle {
     void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
     size_t scratch_cap = 0;
 
+    // vertex sharding over `world` GPUs (one process each)
+    struct Sh {
+        int rank = 0, world = 1;
+        uint32_t n_global = 0, v_lo = 0;
+        uint64_t slot_base = 0;
+        uint32_t* stage = nullptr;       // [E_local] staged cross-shard words
+        uint32_t* rem = nullptr;         // local slots whose receiver is remote, grouped by shard
+        uint4* blk = nullptr;            // compaction blocks {shard, start, len, 0}
+        uint32_t nblk = 0;
+        uint32_t* send_base_d = nullptr; // [world] region starts (records)
+        uint32_t* cursor = nullptr;      // [world] records packed per region this round
+        uint32_t* slot2v = nullptr;      // [E_local] receiver vertex of a local slot
+        std::vector<uint64_t> send_base; // host copy, world + 1 entries (last = total)
+    } sh;
+
     // Demers epidemic state (demers.hip)
     struct Dm {
         uint32_t n = 0, m = 0, ae_period = 0, rm_on = 0;
@@ -116,6 +131,14 @@ void free_graph(psim_handle* h) {
     h->vs = nullptr;
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
+    auto& sh = h->sh;
+    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v};
+    for (void* p : sp)
+        if (p) (void)hipFree(p);
+    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = nullptr;
+    sh.blk = nullptr;
+    sh.nblk = 0;
+    sh.send_base.clear();
     h->n = 0;
     h->E = 0;
 }
@@ -123,6 +146,9 @@ void free_graph(psim_handle* h) {
 PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
     PtArgs a{};
     a.n = h->n;
+    a.v_lo = h->sh.v_lo;
+    a.slot_base = (uint32_t)h->sh.slot_base;
+    a.stage = h->sh.stage;
     a.rowp = h->rowp;
     a.col = h->col;
     a.rev = h->rev;
@@ -373,38 +399,99 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
             const uint32_t* x = std::lower_bound(b, b + (rp[v + 1] - rp[v]), u);
             memb[v] |= 1u << uint32_t(x - b);
         }
+    // this process's shard: contiguous vertex range [lo, hi)
+    auto& sh = h->sh;
+    const uint32_t W = (uint32_t)sh.world;
+    const uint32_t lo = uint32_t((uint64_t(n) * sh.rank) / W), hi = uint32_t((uint64_t(n) * (sh.rank + 1)) / W);
+    const uint32_t nl = hi - lo;
+    const uint64_t sbase = rp[lo], El = rp[hi] - rp[lo];
+    auto owner = [&](uint32_t u) -> uint32_t {      // inverse of the range split
+        uint32_t d = uint32_t((uint64_t(u) * W) / n);
+        while (d + 1 < W && u >= uint32_t((uint64_t(n) * (d + 1)) / W)) d++;
+        while (d > 0 && u < uint32_t((uint64_t(n) * d) / W)) d--;
+        return d;
+    };
+    std::vector<uint32_t> rpl(size_t(nl) + 1), cl(El), rvl(El), mbl(nl), s2v(El);
+    for (uint32_t v = 0; v <= nl; v++) rpl[v] = uint32_t(rp[lo + v] - sbase);
+    for (uint64_t e = 0; e < El; e++) { cl[e] = cc[sbase + e]; rvl[e] = rev[sbase + e]; }
+    for (uint32_t v = 0; v < nl; v++) {
+        mbl[v] = memb[lo + v];
+        for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) s2v[e] = v;
+    }
+    // remote slots grouped by destination shard, and the compaction blocks
+    std::vector<std::vector<uint32_t>> remd(W);
+    if (W > 1)
+        for (uint64_t e = 0; e < El; e++) {
+            const uint32_t d = owner(cl[e]);
+            if (d != (uint32_t)sh.rank) remd[d].push_back(uint32_t(e));
+        }
+    std::vector<uint32_t> remflat;
+    std::vector<uint4> blks;
+    std::vector<uint64_t> sbases(W + 1, 0);
+    for (uint32_t d = 0; d < W; d++) {
+        sbases[d] = remflat.size();
+        for (size_t st = 0; st < remd[d].size(); st += kChunkV)
+            blks.push_back(make_uint4(d, uint32_t(remflat.size() + st),
+                                      uint32_t(std::min<size_t>(kChunkV, remd[d].size() - st)), 0u));
+        remflat.insert(remflat.end(), remd[d].begin(), remd[d].end());
+    }
+    sbases[W] = remflat.size();
     // device arrays
     auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
     const size_t nw = (size_t(n) + 31) / 32;
-    const size_t ng = (size_t(n) + (1u << kGroupShift) - 1) >> kGroupShift;
-    if (alloc((void**)&h->rowp, (size_t(n) + 1) * 4) != hipSuccess || alloc((void**)&h->col, E * 4) != hipSuccess ||
-        alloc((void**)&h->rev, E * 4) != hipSuccess || alloc((void**)&h->memb, size_t(n) * 4) != hipSuccess ||
-        alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(n) * 16) != hipSuccess ||
-        alloc((void**)&h->in[0], E * 4) != hipSuccess || alloc((void**)&h->in[1], E * 4) != hipSuccess ||
+    const size_t ng = (size_t(nl) + (1u << kGroupShift) - 1) >> kGroupShift;
+    if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, El * 4) != hipSuccess ||
+        alloc((void**)&h->rev, El * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl) * 4) != hipSuccess ||
+        alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
+        alloc((void**)&h->in[0], El * 4) != hipSuccess || alloc((void**)&h->in[1], El * 4) != hipSuccess ||
         alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess ||
-        alloc((void**)&h->ost, size_t(n) + 4) != hipSuccess) {
+        alloc((void**)&h->ost, size_t(nl) + 4) != hipSuccess ||
+        (W > 1 && (alloc((void**)&sh.stage, El * 4) != hipSuccess ||
+                   alloc((void**)&sh.rem, remflat.size() * 4) != hipSuccess ||
+                   alloc((void**)&sh.blk, blks.size() * 16) != hipSuccess ||
+                   alloc((void**)&sh.send_base_d, W * 4) != hipSuccess ||
+                   alloc((void**)&sh.cursor, W * 4) != hipSuccess ||
+                   alloc((void**)&sh.slot2v, El * 4) != hipSuccess))) {
         free_graph(h);
-        return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", n, (unsigned long long)E);
+        return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", nl, (unsigned long long)El);
     }
-    h->n = n;
-    h->E = E;
-    HIPCHK(h, hipMemcpy(h->rowp, rp32.data(), (size_t(n) + 1) * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->col, cc.data(), E * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->rev, rev.data(), E * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->memb, memb.data(), size_t(n) * 4, hipMemcpyHostToDevice));
+    h->n = nl;
+    h->E = El;
+    sh.n_global = n;
+    sh.v_lo = lo;
+    sh.slot_base = sbase;
+    HIPCHK(h, hipMemcpy(h->rowp, rpl.data(), (size_t(nl) + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->col, cl.data(), El * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->rev, rvl.data(), El * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->memb, mbl.data(), size_t(nl) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
     // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..
-    HIPCHK(h, hipMemset(h->vs, 0, size_t(n) * 16));
-    HIPCHK(h, hipMemset(h->in[0], 0, E * 4));
-    HIPCHK(h, hipMemset(h->in[1], 0, E * 4));
+    HIPCHK(h, hipMemset(h->vs, 0, size_t(nl) * 16));
+    HIPCHK(h, hipMemset(h->in[0], 0, El * 4));
+    HIPCHK(h, hipMemset(h->in[1], 0, El * 4));
     HIPCHK(h, hipMemset(h->pend[0], 0, ng));
     HIPCHK(h, hipMemset(h->pend[1], 0, ng));
-    HIPCHK(h, hipMemset(h->ost, 0, size_t(n) + 4));
+    HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
     HIPCHK(h, hipMemset(h->ost_total, 0, 64));
+    if (W > 1) {
+        std::vector<uint32_t> sb32(W);
+        for (uint32_t d = 0; d < W; d++) sb32[d] = uint32_t(sbases[d]);
+        HIPCHK(h, hipMemset(sh.stage, 0, El * 4));
+        HIPCHK(h, hipMemcpy(sh.rem, remflat.data(), remflat.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(sh.blk, blks.data(), blks.size() * 16, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(sh.send_base_d, sb32.data(), W * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(sh.slot2v, s2v.data(), El * 4, hipMemcpyHostToDevice));
+        sh.nblk = uint32_t(blks.size());
+    }
+    sh.send_base = sbases;
     HIPCHK(h, hipDeviceSynchronize());
-    h->h_rowp = std::move(rp);
-    h->h_col = std::move(cc);
-    h->h_memb = std::move(memb);
+    {
+        std::vector<uint64_t> rpl64(size_t(nl) + 1);
+        for (uint32_t v = 0; v <= nl; v++) rpl64[v] = rpl[v];
+        h->h_rowp = std::move(rpl64);
+    }
+    h->h_col = std::move(cl);
+    h->h_memb = std::move(mbl);
     h->par = 0;
     h->round = 0;
     h->serial = 0;
@@ -430,7 +517,7 @@ int psim_get_slots(const psim_handle* h, uint64_t* row_ptr, uint32_t* col) {
 }
 
 int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
-    if (!h || !alive || n != h->n || !h->n) return PSIM_EINVAL;
+    if (!h || !alive || n != h->sh.n_global || !h->n) return PSIM_EINVAL;
     std::vector<uint32_t> bm((n + 31) / 32, 0u);
     for (size_t v = 0; v < n; v++)
         if (alive[v]) bm[v >> 5] |= 1u << (v & 31);
@@ -457,14 +544,21 @@ int psim_plumtree_reset_trees(psim_handle* h) {
     return PSIM_OK;
 }
 
-int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+}  // extern "C"
+
+namespace {
+
+// Shared by psim_plumtree_broadcast and psim_shard_broadcast: every shard
+// advances the same serial / epoch / Monotonic; only the root's owner runs
+// the origin kernel.  Returns the origin's emitted-message stats row.
+int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned long long* r) {
     if (!h || !h->n) return PSIM_ESTATE;
-    if (root >= h->n) return PSIM_EINVAL;
+    if (root >= h->sh.n_global) return PSIM_EINVAL;
     if (!quiescent(h)) return fail(h, PSIM_EBUSY, "previous broadcast still in flight");
     HIPCHK(h, hipSetDevice(h->device));
     if (h->have_root && root != h->root) {
         // single-root engine: the previous root's per-root sets are dropped
-        // (DESIGN.md "Scope": multi-root trees are SURVEY 8(f) row 1)
+        // (DESIGN.md "Limitations": multi-root trees are SURVEY 8(f) row 1)
         h->epoch++;
     }
     h->root = root;
@@ -477,30 +571,158 @@ int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     uint32_t& mono = h->mono_of[root];
     mono++;
     if (mono_out) *mono_out = mono;
-    HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
-    // origin emits into the buffer the next round reads
-    PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
-    HIPCHK(h, launch_pt_origin(a, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    unsigned long long r[kNStat];
-    reduce_row(h->h_stats, r);
-    if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "origin: outstanding rows of an older heartbeat");
+    for (int i = 0; i < kNStat; i++) r[i] = 0;
+    const uint32_t lr = root - h->sh.v_lo;
+    if (lr < h->n) {
+        HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+        // origin emits into the buffer the next round reads
+        PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+        a.root = lr;
+        HIPCHK(h, launch_pt_origin(a, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        reduce_row(h->h_stats, r);
+        if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "origin: outstanding rows of an older heartbeat");
+    }
     h->ost_cnt += (int64_t)r[S_OST_DELTA];
     h->live_rows += (int64_t)r[S_LIVE_DELTA];
     h->inflight = r[PSIM_MSG_BROADCAST];
     return PSIM_OK;
 }
 
+// Pack this shard's staged cross-shard words into the caller's device buffer
+// (regions at psim_shard_layout offsets); counts[d] = records for shard d.
+int shard_pack(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts) {
+    auto& sh = h->sh;
+    const uint32_t W = (uint32_t)sh.world;
+    for (uint32_t d = 0; d < W; d++) counts[d] = 0;
+    if (W == 1) return PSIM_OK;
+    if (send_cap < sh.send_base[W] || (!send_dev && sh.send_base[W]))
+        return fail(h, PSIM_EINVAL, "send buffer holds %llu records, layout needs %llu",
+                    (unsigned long long)send_cap, (unsigned long long)sh.send_base[W]);
+    HIPCHK(h, hipMemsetAsync(sh.cursor, 0, W * 4, h->stream));
+    PtArgs a = make_args(h, h->par, 0, h->stats);
+    HIPCHK(h, launch_pt_compact(a, sh.rem, sh.blk, sh.nblk, sh.send_base_d, sh.cursor, (uint2*)send_dev, h->stream));
+    std::vector<uint32_t> c(W);
+    HIPCHK(h, hipMemcpyAsync(c.data(), sh.cursor, W * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (uint32_t d = 0; d < W; d++) counts[d] = c[d];
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+    if (h && h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast");
+    unsigned long long r[kNStat];
+    return broadcast_common(h, root, mono_out, r);
+}
+
+int psim_shard_init(psim_handle* h, int rank, int world) {
+    if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
+    if (h->n) return fail(h, PSIM_ESTATE, "psim_shard_init must precede psim_load_csr");
+    h->sh.rank = rank;
+    h->sh.world = world;
+    return PSIM_OK;
+}
+
+int psim_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local, uint64_t* slot_base,
+                    uint32_t* n_global) {
+    if (!h) return PSIM_EINVAL;
+    if (v_lo) *v_lo = h->sh.v_lo;
+    if (n_local) *n_local = h->n;
+    if (slot_base) *slot_base = h->sh.slot_base;
+    if (n_global) *n_global = h->sh.n_global;
+    return PSIM_OK;
+}
+
+int psim_shard_layout(const psim_handle* h, uint64_t* region_base, size_t world) {
+    if (!h || !region_base || world != (size_t)h->sh.world || h->sh.send_base.size() != world + 1)
+        return PSIM_EINVAL;
+    memcpy(region_base, h->sh.send_base.data(), (world + 1) * 8);
+    return PSIM_OK;
+}
+
+int psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev, uint64_t send_cap,
+                         uint64_t* counts, int64_t* local_live) {
+    if (!h || !counts) return PSIM_EINVAL;
+    unsigned long long r[kNStat];
+    int rc = broadcast_common(h, root, mono_out, r);
+    if (rc) return rc;
+    if (local_live) *local_live = h->live_rows;
+    return shard_pack(h, send_dev, send_cap, counts);
+}
+
+int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts,
+                     psim_round_stats* st, int64_t* local_live) {
+    if (!h || !counts) return PSIM_EINVAL;
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    HIPCHK(h, hipSetDevice(h->device));
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    const uint32_t tick = ((h->round + 1) % L) == 0;
+    HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+    PtArgs a = make_args(h, h->par, tick, h->stats);
+    HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
+    HIPCHK(h, launch_pt_round(a, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->par ^= 1u;   // the staged words were written for the round that reads in[par] now
+    unsigned long long r[kNStat];
+    reduce_row(h->h_stats, r);
+    float ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    if (r[S_OVERFLOW])
+        return fail(h, PSIM_EOVERFLOW, "round %llu: overflow flags 0x%llx", (unsigned long long)(h->round + 1),
+                    r[S_OVERFLOW]);
+    uint64_t msgs = 0;
+    for (int t = 1; t <= 5; t++) msgs += r[t];
+    h->round++;
+    h->ost_cnt += (int64_t)r[S_OST_DELTA];
+    h->live_rows += (int64_t)r[S_LIVE_DELTA];
+    h->inflight = msgs;
+    h->kernel_ms_total += ms;
+    h->rounds_total++;
+    if (st) {
+        memset(st, 0, sizeof *st);
+        for (int t = 1; t <= 5; t++) st->sent[t] = r[t];
+        st->delivered_new = r[S_DELIV];
+        st->active = r[S_ACTIVE];
+        st->senders = r[S_SENDERS];
+        st->sender_degree_sum = r[S_DEGSUM];
+        st->outstanding_vertices = (uint64_t)h->ost_cnt;
+        st->algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+        st->kernel_ms = ms;
+    }
+    if (local_live) *local_live = h->live_rows;
+    return shard_pack(h, send_dev, send_cap, counts);
+}
+
+int psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records) {
+    if (!h || (!recv_dev && n_records)) return PSIM_EINVAL;
+    if (n_records == 0) return PSIM_OK;
+    if (n_records > 0xFFFFFFFFull) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt/pend_nxt = the buffers the next round reads
+    HIPCHK(h, launch_pt_ingest(a, (const uint2*)recv_dev, (uint32_t)n_records, h->sh.slot2v, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
 int psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap) {
     if (!h) return PSIM_EINVAL;
+    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: drive rounds with psim_shard_round");
     HIPCHK(h, hipSetDevice(h->device));
     return drive(h, rounds, stats, cap, false, nullptr);
 }
 
 int psim_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds_run) {
     if (!h) return PSIM_EINVAL;
+    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: drive rounds with psim_shard_round");
     HIPCHK(h, hipSetDevice(h->device));
     return drive(h, max_rounds, stats, cap, true, rounds_run);
 }
@@ -523,7 +745,7 @@ int psim_get_plumtree(const psim_handle* h, uint32_t* eager, uint32_t* lazy, uin
         if (recv_round) {
             const bool got = h->serial && ((st.w >> 16) & 0xFFu) == s8;
             if (!got) recv_round[v] = 0xFFFF;
-            else if (h->have_root && v == h->root) recv_round[v] = 0xFFFE;
+            else if (h->have_root && v + h->sh.v_lo == h->root) recv_round[v] = 0xFFFE;
             else recv_round[v] = uint16_t((st.w & 0xFFFFu) - 1u);
         }
     }

@@ -30,12 +30,15 @@ enum Stat : int {
 //       [23:16] low 8 bits of the Monotonic last delivered (Mod:merge/2)
 //       [31:24] tree epoch (a mismatch == no per-root map entry: common sets)
 struct PtArgs {
-    uint32_t n;
-    const uint32_t* __restrict__ rowp;     // [n+1] slot row pointers
-    const uint32_t* __restrict__ col;      // [E]   neighbour id per slot (sorted in a row)
-    const uint32_t* __restrict__ rev;      // [E]   index of the reverse slot
+    uint32_t n;                            // vertices of this shard (all of them on one GPU)
+    uint32_t v_lo;                         // global id of local vertex 0
+    uint32_t slot_base;                    // global slot id of local slot 0
+    uint32_t* __restrict__ stage;          // [E_local] words for receivers on other shards (sharded only)
+    const uint32_t* __restrict__ rowp;     // [n+1] local slot row pointers
+    const uint32_t* __restrict__ col;      // [E]   neighbour (global) id per slot (sorted in a row)
+    const uint32_t* __restrict__ rev;      // [E]   global slot id of the reverse slot
     const uint32_t* __restrict__ memb;     // [n]   member mask = common_eagers
-    const uint32_t* __restrict__ alive;    // [ceil(n/32)] bitmap
+    const uint32_t* __restrict__ alive;    // [ceil(N/32)] bitmap over GLOBAL ids
     uint4* __restrict__ vs;                // [n]   state records
     uint32_t* __restrict__ in_cur;         // [E]   words read this round (receiver slots)
     uint32_t* __restrict__ in_nxt;         // [E]   words written this round
@@ -47,7 +50,7 @@ struct PtArgs {
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
     uint32_t epoch8;                       // current tree epoch (low 8 bits)
-    uint32_t root;                         // origin of the current heartbeat
+    uint32_t root;                         // local index of the current heartbeat's origin
 };
 
 // Demers rumor mongering + anti-entropy (demers.hip)
@@ -85,5 +88,8 @@ hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_
 hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
+                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s);
+hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s);
 
 }  // namespace psim

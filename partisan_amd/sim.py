@@ -18,7 +18,7 @@ _u64p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
 class Simulator:
     """Round-synchronous simulator of Partisan's gossip hot path."""
 
-    def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0):
+    def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0, rank=0, world=1):
         cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
                      exchange_tick_rounds=exchange_tick_rounds, flags=0, _reserved=0, seed=seed)
         h = C.c_void_p()
@@ -26,6 +26,9 @@ class Simulator:
         self._h = h
         self.n = 0
         self.lazy_tick_rounds = lazy_tick_rounds
+        self.rank, self.world = rank, world
+        if world > 1:
+            check(lib().psim_shard_init(h, rank, world), h)
 
     # ---------------------------------------------------------------- lifecycle
     def close(self):
@@ -55,9 +58,13 @@ class Simulator:
         """Membership lists (members minus self) as CSR; see psim_load_csr."""
         rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
         cc = np.ascontiguousarray(col, dtype=np.uint32)
-        n = len(rp) - 1
-        self._c(lib().psim_load_csr(self._h, n, _u64p(rp), _u32p(cc) if len(cc) else None))
-        self.n = n
+        self._c(lib().psim_load_csr(self._h, len(rp) - 1, _u64p(rp), _u32p(cc) if len(cc) else None))
+        v_lo, n_local, n_global = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        slot_base = C.c_uint64()
+        self._c(lib().psim_shard_info(self._h, C.byref(v_lo), C.byref(n_local), C.byref(slot_base),
+                                      C.byref(n_global)))
+        self.v_lo, self.n_global, self.slot_base = v_lo.value, n_global.value, slot_base.value
+        n = self.n = n_local.value
         E = C.c_uint64()
         self._c(lib().psim_num_slots(self._h, C.byref(E)))
         self.slot_row_ptr = np.zeros(n + 1, dtype=np.uint64)
@@ -123,9 +130,10 @@ class Simulator:
         return [int(self.slot_col[lo + s]) for s in range(hi - lo) if (int(mask) >> s) & 1]
 
     def decode_inflight(self, words=None):
-        """In-flight messages as sorted (src, dst, kind, round) tuples; the
-        Round is reported for broadcast / i_have only (the others carry an echo
-        or nothing).  Order within a (src, dst) pair is FIFO order."""
+        """In-flight messages as sorted (src, dst, kind, round) tuples (global
+        ids; dst = a local vertex); the Round is reported for broadcast /
+        i_have only (the others carry an echo or nothing).  Order within a
+        (src, dst) pair is FIFO order."""
         if words is None:
             words = self.inflight()
         out = []
@@ -139,6 +147,6 @@ class Simulator:
             while f:
                 t = f & 0xF
                 f >>= 4
-                out.append((src, int(dst), t, rnd if t in (1, 3) else 0))
+                out.append((src, int(dst) + self.v_lo, t, rnd if t in (1, 3) else 0))
         out.sort(key=lambda m: (m[1], m[0]))
         return out
