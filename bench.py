@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=int, default=10_000_000)
+    p.add_argument("--num-peers", dest="n", type=int, default=10_000_000)
     p.add_argument("--peers", type=int, default=5)
     p.add_argument("--seed", type=int, default=0x5EED0001)
     p.add_argument("--lazy-tick-rounds", type=int, default=1)
@@ -215,7 +215,9 @@ def main():
                 "n_peers": args.n,
                 "overlay": f"random symmetric, {args.peers} peers per vertex (HyParView active view)",
                 "rounds_to_convergence": rounds_per_step[-1],
-                "parallelism": (f"vertex-sharded x{world}, RCCL all-to-all per round" if sharded
+                "parallelism": (f"vertex-sharded x{world}, "
+                                + ("RCCL all-to-all over xGMI" if args.transport == "nccl" else "gloo host-staged")
+                                + " exchange per round" if sharded
                                 else ("replicas" if world > 1 else "single")),
                 "device": sim.device_info(),
             },

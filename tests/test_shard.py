@@ -175,3 +175,39 @@ def test_exchange_routing_gloo_cpu(world):
     res = run_world(_cpu_worker, world, timeout=120)
     for r in range(world):
         assert res[r] == "ok", res[r]
+
+
+def _nccl_world1(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        import partisan_amd as pa
+        from partisan_amd.shard import ShardedPlumtree
+        import pyoracle as O
+        rp, col = pa.overlay.random_regular(4000, 5, 3)
+        sp = ShardedPlumtree(rp, col, 0, 1, device=0, backend="nccl")
+        orc = O.Plumtree(rp, col, 1)
+        sp.broadcast(0)
+        orc.heartbeat(0)
+        gst, gr = sp.run()
+        ost, orr = orc.run()
+        assert gr == orr
+        assert [g["prune"] for g in gst] == [o["prune"] for o in ost]
+        sp.close()
+        dist.destroy_process_group()
+        q.put((0, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((0, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_nccl_transport_world1():
+    res = run_world(_nccl_world1, 1)
+    assert res[0] == "ok", res[0]
