@@ -200,6 +200,50 @@ int  psim_demers_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* sta
 int  psim_demers_get_seen(const psim_handle* h, uint64_t* seen, size_t n);
 int  psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m);
 
+/* --- HyParView view maintenance (partisan_hyparview_peer_service_manager.erl) */
+typedef struct psim_hv_config {
+    uint32_t active_max_size;      /* partisan.hrl / hyparview config: 6 (<= 8)   */
+    uint32_t active_min_size;      /* 3                                            */
+    uint32_t active_rwl;           /* 6 (<= 255)                                   */
+    uint32_t passive_max_size;     /* 30 (<= 32)                                   */
+    uint32_t passive_rwl;          /* 6                                            */
+    uint32_t shuffle_k_active;     /* 3; k_active + k_passive <= 7                 */
+    uint32_t shuffle_k_passive;    /* 4                                            */
+    uint32_t shuffle_rounds;       /* passive_view_shuffle_period (10000 ms) in rounds */
+    uint32_t promotion_rounds;     /* random_promotion_interval (5000 ms) in rounds */
+} psim_hv_config;
+typedef struct psim_hv_stats {
+    uint64_t sent[10];             /* [k] = messages of kind k emitted (1 join .. 9 shuffle_reply;
+                                      joins cast between rounds are not counted)   */
+    uint64_t draws;                /* rand draws consumed in the round             */
+    uint64_t error;                /* bit0 queue overflow, bit1 id-map overflow,
+                                      bit2 get_next_id case_clause, bit3 2-tuple
+                                      neighbor_rejected (reference crash points)  */
+    uint64_t processed;            /* messages handled                             */
+    uint64_t active;               /* vertices that ran a handler or a timer       */
+    uint64_t algo_bytes;           /* 64 B per message read or written
+                                      + 2 x 176 B per active vertex (views, head)
+                                      + 12 B per vertex (bucket count/offset)      */
+    double   kernel_ms;
+} psim_hv_stats;
+/* Fresh cluster of n vertices (init/1: Active = {self}, Passive = {},
+ * epoch 1).  Replaces starting n partisan_hyparview_peer_service_manager
+ * processes (:745-822).  Random draws use the handle's seed, stream kind 4. */
+int  psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg);
+int  psim_hv_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
+/* handle_cast({join, Peer}) (:999-1016) at v[i] toward contact[i], made
+ * between rounds (delivered by the next round).  The v[i] must be distinct. */
+int  psim_hv_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k);
+int  psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* stats, size_t cap);
+/* act[n*8], pas[n*32] padded with 0xFFFFFFFF; na/np = view sizes (active
+ * includes self, as sets:to_list(Active) does). */
+int  psim_hv_get_views(const psim_handle* h, uint32_t* act, uint8_t* na, uint32_t* pas, uint8_t* np, size_t n);
+int  psim_hv_get_draws(const psim_handle* h, uint64_t* draws, size_t n);
+/* which 0 = sent_message_map, 1 = recv_message_map of vertex v. */
+int  psim_hv_get_idmap(const psim_handle* h, uint32_t v, int which, uint32_t* peer, uint32_t* epoch, uint32_t* cnt,
+                       size_t cap, size_t* len);
+int  psim_hv_inflight(const psim_handle* h, uint64_t* messages);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

@@ -183,6 +183,34 @@ void orc_dm_get_seen(const orc_demers* s, uint64_t* out);
 size_t orc_dm_pending(const orc_demers* s, uint32_t* type, uint32_t* src, uint32_t* dst, uint32_t* m,
                       uint64_t* payload, size_t cap);
 
+/* ------------------------------------------------------------------ */
+/* HyParView (src/partisan_hyparview_peer_service_manager.erl)          */
+/* ------------------------------------------------------------------ */
+typedef struct orc_hv_config {
+    uint32_t active_max_size, active_min_size, active_rwl;     /* partisan.hrl:204-217 */
+    uint32_t passive_max_size, passive_rwl;
+    uint32_t shuffle_k_active, shuffle_k_passive;
+    uint32_t shuffle_rounds, promotion_rounds;                  /* 10000 ms, 5000 ms in rounds */
+} orc_hv_config;
+
+typedef struct orc_hv_stats {
+    uint64_t sent[10];           /* by message kind 1..9 */
+    uint64_t draws;              /* rand draws consumed in the round */
+    uint64_t error;              /* a reference crash would have happened */
+} orc_hv_stats;
+
+typedef struct orc_hyparview orc_hyparview;
+orc_hyparview* orc_hv_create(uint32_t n, uint64_t seed, const orc_hv_config* cfg);
+void orc_hv_destroy(orc_hyparview* s);
+void orc_hv_set_alive(orc_hyparview* s, const uint8_t* alive);
+void orc_hv_join(orc_hyparview* s, uint32_t v, uint32_t contact);
+uint32_t orc_hv_step(orc_hyparview* s, uint32_t rounds, orc_hv_stats* st);
+size_t orc_hv_inflight(const orc_hyparview* s);
+void orc_hv_views(const orc_hyparview* s, uint32_t v, uint32_t* act, uint32_t* na, uint32_t* pas, uint32_t* np);
+uint64_t orc_hv_draws(const orc_hyparview* s, uint32_t v);
+size_t orc_hv_idmap(const orc_hyparview* s, uint32_t v, int which, uint32_t* peer, uint32_t* ep, uint32_t* cnt,
+                    size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

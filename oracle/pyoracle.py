@@ -40,6 +40,22 @@ class DmStats(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class HvConfig(C.Structure):
+    _fields_ = [(k, C.c_uint32) for k in ("active_max_size", "active_min_size", "active_rwl", "passive_max_size",
+                                           "passive_rwl", "shuffle_k_active", "shuffle_k_passive",
+                                           "shuffle_rounds", "promotion_rounds")]
+
+
+class HvStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 10), ("draws", C.c_uint64), ("error", C.c_uint64)]
+
+    def as_dict(self):
+        return {"sent": [int(x) for x in self.sent[1:10]], "draws": int(self.draws), "error": int(self.error)}
+
+
+HV_DEFAULTS = dict(active_max_size=6, active_min_size=3, active_rwl=6, passive_max_size=30, passive_rwl=6,
+                   shuffle_k_active=3, shuffle_k_passive=4, shuffle_rounds=10, promotion_rounds=5)
+
 MSG_NAMES = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
 
 _lib = None
@@ -117,6 +133,20 @@ def lib():
         L.orc_dm_pending.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), P(C.c_uint32),
                                      P(C.c_uint64), sz]
         L.orc_dm_pending.restype = sz
+        L.orc_hv_create.argtypes = [C.c_uint32, C.c_uint64, P(HvConfig)]
+        L.orc_hv_create.restype = C.c_void_p
+        L.orc_hv_destroy.argtypes = [C.c_void_p]
+        L.orc_hv_set_alive.argtypes = [C.c_void_p, P(C.c_uint8)]
+        L.orc_hv_join.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_hv_step.argtypes = [C.c_void_p, C.c_uint32, P(HvStats)]
+        L.orc_hv_inflight.argtypes = [C.c_void_p]
+        L.orc_hv_inflight.restype = sz
+        L.orc_hv_views.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32),
+                                   P(C.c_uint32)]
+        L.orc_hv_draws.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_hv_draws.restype = C.c_uint64
+        L.orc_hv_idmap.argtypes = [C.c_void_p, C.c_uint32, C.c_int, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), sz]
+        L.orc_hv_idmap.restype = sz
         _lib = L
     return _lib
 
@@ -427,3 +457,51 @@ class Demers:
                              d.ctypes.data_as(P(C.c_uint32)), m.ctypes.data_as(P(C.c_uint32)),
                              p.ctypes.data_as(P(C.c_uint64)), n)
         return t[:n], s[:n], d[:n], m[:n], p[:n]
+
+
+# ---------------------------------------------------------------- hyparview
+class HyParView:
+    def __init__(self, n, seed, **cfg):
+        c = dict(HV_DEFAULTS)
+        c.update(cfg)
+        self.n = n
+        self.cfg = HvConfig(**c)
+        self._h = lib().orc_hv_create(n, seed, C.byref(self.cfg))
+
+    def close(self):
+        if self._h:
+            lib().orc_hv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        lib().orc_hv_set_alive(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def join(self, v, contact):
+        lib().orc_hv_join(self._h, v, contact)
+
+    def step(self, rounds=1):
+        st = (HvStats * rounds)()
+        lib().orc_hv_step(self._h, rounds, st)
+        return [s.as_dict() for s in st]
+
+    def inflight(self):
+        return lib().orc_hv_inflight(self._h)
+
+    def views(self, v):
+        a = (C.c_uint32 * 8)()
+        p = (C.c_uint32 * 32)()
+        na, np_ = C.c_uint32(), C.c_uint32()
+        lib().orc_hv_views(self._h, v, a, C.byref(na), p, C.byref(np_))
+        return list(a[:na.value]), list(p[:np_.value])
+
+    def draws(self, v):
+        return lib().orc_hv_draws(self._h, v)
+
+    def idmap(self, v, which, cap=4096):
+        pe, ep, cn = (C.c_uint32 * cap)(), (C.c_uint32 * cap)(), (C.c_uint32 * cap)()
+        k = lib().orc_hv_idmap(self._h, v, which, pe, ep, cn, cap)
+        return sorted((pe[i], ep[i], cn[i]) for i in range(min(k, cap)))

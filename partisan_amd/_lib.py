@@ -54,6 +54,26 @@ class DemersStats(C.Structure):
         return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
 
 
+class HvConfig(C.Structure):
+    _fields_ = [(k, C.c_uint32) for k in ("active_max_size", "active_min_size", "active_rwl", "passive_max_size",
+                                           "passive_rwl", "shuffle_k_active", "shuffle_k_passive",
+                                           "shuffle_rounds", "promotion_rounds")]
+
+
+HV_MSG_KINDS = {1: "join", 2: "neighbor", 3: "forward_join", 4: "disconnect", 5: "neighbor_request",
+                6: "neighbor_rejected", 7: "neighbor_accepted", 8: "shuffle", 9: "shuffle_reply"}
+
+
+class HvStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 10), ("draws", C.c_uint64), ("error", C.c_uint64), ("processed", C.c_uint64),
+                ("active", C.c_uint64), ("algo_bytes", C.c_uint64), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {"sent": [int(x) for x in self.sent[1:10]], "draws": int(self.draws), "error": int(self.error),
+                "processed": int(self.processed), "active": int(self.active), "algo_bytes": int(self.algo_bytes),
+                "kernel_ms": float(self.kernel_ms)}
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -89,6 +109,15 @@ SIGNATURES = {
     "psim_demers_run": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t, _P(C.c_uint32)]),
     "psim_demers_get_seen": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_demers_origins": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
+    "psim_hv_setup": (C.c_int, [_H, C.c_uint32, _P(HvConfig)]),
+    "psim_hv_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
+    "psim_hv_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_hv_step": (C.c_int, [_H, C.c_uint32, _P(HvStats), C.c_size_t]),
+    "psim_hv_get_views": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint8), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
+    "psim_hv_get_draws": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
+    "psim_hv_get_idmap": (C.c_int, [_H, C.c_uint32, C.c_int, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),
+                                    C.c_size_t, _P(C.c_size_t)]),
+    "psim_hv_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

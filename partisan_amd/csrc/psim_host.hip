@@ -88,6 +88,23 @@ struct psim_handle {
         uint32_t par = 0;
         uint64_t round = 0, complete = 0;
     } dm;
+
+    // HyParView state (hyparview.hip)
+    struct Hv {
+        uint32_t n = 0, cap = 0;
+        psim_hv_config cfg{};
+        HvHead* head = nullptr;
+        uint32_t *act = nullptr, *pas = nullptr, *sent = nullptr, *recv = nullptr, *alive = nullptr;
+        HvMsg* msg[2] = {nullptr, nullptr};
+        uint32_t* nmsg = nullptr;                 // [2] device queue counts
+        uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
+        uint32_t* joinbuf = nullptr;              // [2][n] staged join pairs
+        unsigned long long* stats = nullptr;      // [kHvChunk][kHvNStat]
+        unsigned long long* h_stats = nullptr;    // pinned mirror
+        hipEvent_t ev[2 * 16] = {};
+        uint32_t par = 0;                         // queue the next round reads
+        uint64_t round = 0;
+    } hv;
 };
 
 namespace {
@@ -120,6 +137,20 @@ void free_demers(psim_handle* h) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->dm = psim_handle::Dm();
+}
+
+constexpr uint32_t kHvChunk = 16;   // HyParView rounds between host synchronisations
+
+void free_hv(psim_handle* h) {
+    auto& v = h->hv;
+    void* ptrs[] = {v.head, v.act, v.pas, v.sent, v.recv, v.alive, v.msg[0], v.msg[1], v.nmsg,
+                    v.cnt, v.cur, v.off, v.idx, v.bsum, v.joinbuf, v.stats};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (v.h_stats) (void)hipHostFree(v.h_stats);
+    for (auto& e : v.ev)
+        if (e) (void)hipEventDestroy(e);
+    h->hv = psim_handle::Hv();
 }
 
 void free_graph(psim_handle* h) {
@@ -315,6 +346,7 @@ int psim_destroy(psim_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_graph(h);
     free_demers(h);
+    free_hv(h);
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);
@@ -993,6 +1025,235 @@ int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rou
     if (!h) return PSIM_EINVAL;
     if (round_kernel_ms) *round_kernel_ms = h->kernel_ms_total;
     if (rounds) *rounds = h->rounds_total;
+    return PSIM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+HvArgs make_hv_args(const psim_handle* h, uint32_t par, unsigned long long* stats) {
+    const auto& v = h->hv;
+    HvArgs a{};
+    a.n = v.n;
+    a.cfg = HvCfg{v.cfg.active_max_size, v.cfg.active_min_size, v.cfg.active_rwl, v.cfg.passive_max_size,
+                  v.cfg.passive_rwl, v.cfg.shuffle_k_active, v.cfg.shuffle_k_passive};
+    a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
+    a.alive = v.alive;
+    a.head = v.head;
+    a.act = v.act;
+    a.pas = v.pas;
+    a.sent = v.sent;
+    a.recv = v.recv;
+    a.in = v.msg[par];
+    a.nin = v.nmsg + par;
+    a.out = v.msg[par ^ 1];
+    a.nout = v.nmsg + (par ^ 1);
+    a.out_cap = v.cap;
+    a.cnt = v.cnt;
+    a.cur = v.cur;
+    a.off = v.off;
+    a.idx = v.idx;
+    a.bsum = v.bsum;
+    a.stats = stats;
+    return a;
+}
+
+int hv_check_err(psim_handle* h, unsigned long long e, uint64_t round) {
+    if (e & 1ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: message queue over %u records",
+                              (unsigned long long)round, h->hv.cap);
+    if (e & 2ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: id map over %u rows",
+                              (unsigned long long)round, kHvMapCap);
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
+    if (!h || !cfg || n < 1) return PSIM_EINVAL;
+    if (cfg->active_max_size < 2 || cfg->active_max_size > 8 || cfg->passive_max_size < 1 ||
+        cfg->passive_max_size > 32 || cfg->active_rwl > 255 || cfg->passive_rwl > 255 ||
+        cfg->shuffle_k_active + cfg->shuffle_k_passive > kHvX - 1)
+        return fail(h, PSIM_EINVAL, "hyparview config out of range (active <= 8, passive <= 32, k_a + k_p <= 7)");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    free_hv(h);
+    auto& v = h->hv;
+    const size_t N = n;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(8ull * n + 4096, 0xFFFFFFF0ull);
+    const uint32_t nb = (n + kBlock - 1) / kBlock;
+    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    bool ok = A((void**)&v.head, N * sizeof(HvHead)) && A((void**)&v.act, N * 32) && A((void**)&v.pas, N * 128) &&
+              A((void**)&v.sent, N * kHvMapCap * 12) && A((void**)&v.recv, N * kHvMapCap * 12) &&
+              A((void**)&v.alive, ((N + 31) / 32) * 4) && A((void**)&v.msg[0], size_t(cap) * sizeof(HvMsg)) &&
+              A((void**)&v.msg[1], size_t(cap) * sizeof(HvMsg)) && A((void**)&v.nmsg, 16) &&
+              A((void**)&v.cnt, N * 4) && A((void**)&v.cur, N * 4) && A((void**)&v.off, (N + 1) * 4) &&
+              A((void**)&v.idx, size_t(cap) * 4) && A((void**)&v.bsum, size_t(nb) * 4) &&
+              A((void**)&v.joinbuf, 2 * N * 4) && A((void**)&v.stats, kHvChunk * kHvNStat * 8) &&
+              hipHostMalloc((void**)&v.h_stats, kHvChunk * kHvNStat * 8, 0) == hipSuccess;
+    for (auto& e : v.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    if (!ok) {
+        free_hv(h);
+        return fail(h, PSIM_ENOMEM, "hyparview state for n=%u", n);
+    }
+    v.n = n;
+    v.cap = cap;
+    v.cfg = *cfg;
+    HIPCHK(h, hipMemset(v.alive, 0xFF, ((N + 31) / 32) * 4));
+    HIPCHK(h, launch_hv_init(make_hv_args(h, 0, v.stats), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
+int psim_hv_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
+    if (!h || !alive) return PSIM_EINVAL;
+    if (!h->hv.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
+    if (n != h->hv.n) return fail(h, PSIM_EINVAL, "alive has %zu entries, cluster has %u", n, h->hv.n);
+    std::vector<uint32_t> bm((n + 31) / 32, 0);
+    for (size_t i = 0; i < n; i++)
+        if (alive[i]) bm[i >> 5] |= 1u << (i & 31);
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(h->hv.alive, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
+int psim_hv_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k) {
+    if (!h || (k && (!v || !contact))) return PSIM_EINVAL;
+    auto& hv = h->hv;
+    if (!hv.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
+    if (k > hv.n) return fail(h, PSIM_EINVAL, "%zu joins for %u vertices", k, hv.n);
+    std::vector<uint8_t> seen(hv.n, 0);
+    for (size_t i = 0; i < k; i++) {
+        if (v[i] >= hv.n || contact[i] >= hv.n) return fail(h, PSIM_EINVAL, "join %zu: vertex out of range", i);
+        if (seen[v[i]]) return fail(h, PSIM_EINVAL, "join %zu: vertex %u joins twice in one batch", i, v[i]);
+        seen[v[i]] = 1;
+    }
+    if (!k) return PSIM_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(hv.joinbuf, v, k * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(hv.joinbuf + hv.n, contact, k * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(hv.stats, 0, kHvNStat * 8, h->stream));
+    // the join messages go to the queue the next round reads
+    HvArgs a = make_hv_args(h, hv.par ^ 1u, hv.stats);
+    HIPCHK(h, launch_hv_join(a, hv.joinbuf, hv.joinbuf + hv.n, (uint32_t)k, h->stream));
+    HIPCHK(h, hipMemcpyAsync(hv.h_stats, hv.stats, kHvNStat * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return hv_check_err(h, hv.h_stats[11], hv.round);
+}
+
+int psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* out, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    auto& v = h->hv;
+    if (!v.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
+    HIPCHK(h, hipSetDevice(h->device));
+    uint32_t done = 0;
+    while (done < rounds) {
+        const uint32_t k = std::min(kHvChunk, rounds - done);
+        HIPCHK(h, hipMemsetAsync(v.stats, 0, size_t(k) * kHvNStat * 8, h->stream));
+        for (uint32_t i = 0; i < k; i++) {
+            HvArgs a = make_hv_args(h, v.par, v.stats + size_t(i) * kHvNStat);
+            const uint64_t t = v.round + i + 1;   // 1-based round; timers fire at its end
+            a.timers = (v.cfg.promotion_rounds && t % v.cfg.promotion_rounds == 0 ? 1u : 0u) |
+                       (v.cfg.shuffle_rounds && t % v.cfg.shuffle_rounds == 0 ? 2u : 0u);
+            HIPCHK(h, hipMemsetAsync(v.nmsg + (v.par ^ 1u), 0, 4, h->stream));
+            HIPCHK(h, hipEventRecord(v.ev[2 * i], h->stream));
+            HIPCHK(h, launch_hv_round(a, h->stream));
+            HIPCHK(h, hipEventRecord(v.ev[2 * i + 1], h->stream));
+            v.par ^= 1u;
+        }
+        HIPCHK(h, hipMemcpyAsync(v.h_stats, v.stats, size_t(k) * kHvNStat * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (uint32_t i = 0; i < k; i++) {
+            const unsigned long long* r = v.h_stats + size_t(i) * kHvNStat;
+            const uint64_t t = v.round + i + 1;
+            int rc = hv_check_err(h, r[11], t);
+            if (rc != PSIM_OK) { v.round += k; return rc; }
+            float ms = 0.f;
+            HIPCHK(h, hipEventElapsedTime(&ms, v.ev[2 * i], v.ev[2 * i + 1]));
+            h->kernel_ms_total += ms;
+            h->rounds_total++;
+            const size_t j = done + i;
+            if (out && j < cap) {
+                psim_hv_stats& o = out[j];
+                memset(&o, 0, sizeof o);
+                uint64_t emitted = 0;
+                for (int q = 1; q < 10; q++) { o.sent[q] = r[q]; emitted += r[q]; }
+                o.draws = r[10];
+                o.error = r[11];
+                o.processed = r[12];
+                o.active = r[13];
+                o.algo_bytes = 64ull * (r[12] + emitted) + 2ull * 176ull * r[13] + 12ull * v.n;
+                o.kernel_ms = ms;
+            }
+        }
+        v.round += k;
+        done += k;
+    }
+    return PSIM_OK;
+}
+
+int psim_hv_get_views(const psim_handle* h, uint32_t* act, uint8_t* na, uint32_t* pas, uint8_t* np, size_t n) {
+    if (!h || n != h->hv.n || !n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    const auto& v = h->hv;
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    if (act) HIPCHK(hh, hipMemcpy(act, v.act, n * 32, hipMemcpyDeviceToHost));
+    if (pas) HIPCHK(hh, hipMemcpy(pas, v.pas, n * 128, hipMemcpyDeviceToHost));
+    if (na || np) {
+        std::vector<HvHead> hd(n);
+        HIPCHK(hh, hipMemcpy(hd.data(), v.head, n * sizeof(HvHead), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; i++) {
+            if (na) na[i] = hd[i].na;
+            if (np) np[i] = hd[i].np;
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_hv_get_draws(const psim_handle* h, uint64_t* draws, size_t n) {
+    if (!h || !draws || n != h->hv.n || !n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    std::vector<HvHead> hd(n);
+    HIPCHK(hh, hipMemcpy(hd.data(), h->hv.head, n * sizeof(HvHead), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++) draws[i] = hd[i].draws;
+    return PSIM_OK;
+}
+
+int psim_hv_get_idmap(const psim_handle* h, uint32_t v, int which, uint32_t* peer, uint32_t* epoch, uint32_t* cnt,
+                      size_t cap, size_t* len) {
+    if (!h || !len || v >= h->hv.n || (which != 0 && which != 1)) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    HvHead hd;
+    HIPCHK(hh, hipMemcpy(&hd, h->hv.head + v, sizeof hd, hipMemcpyDeviceToHost));
+    const uint32_t m = which ? hd.nrecv : hd.nsent;
+    std::vector<uint32_t> rows(size_t(kHvMapCap) * 3);
+    HIPCHK(hh, hipMemcpy(rows.data(), (which ? h->hv.recv : h->hv.sent) + size_t(v) * kHvMapCap * 3,
+                         rows.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < m && i < cap; i++) {
+        if (peer) peer[i] = rows[3 * i];
+        if (epoch) epoch[i] = rows[3 * i + 1];
+        if (cnt) cnt[i] = rows[3 * i + 2];
+    }
+    *len = m;
+    return PSIM_OK;
+}
+
+int psim_hv_inflight(const psim_handle* h, uint64_t* messages) {
+    if (!h || !messages || !h->hv.n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    uint32_t c = 0;
+    HIPCHK(hh, hipMemcpy(&c, h->hv.nmsg + h->hv.par, 4, hipMemcpyDeviceToHost));
+    *messages = c;
     return PSIM_OK;
 }
 

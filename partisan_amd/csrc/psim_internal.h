@@ -81,6 +81,54 @@ hipError_t launch_dm_origins(uint2 key, uint32_t n, uint32_t m, uint32_t* origin
 hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const uint32_t* idbit, hipStream_t s);
 hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
 
+// HyParView (hyparview.hip)
+constexpr uint32_t kHvMapCap = 128;   // rows per sent/recv id map (overflow -> PSIM_EOVERFLOW)
+constexpr uint32_t kHvX = 8;          // exchange list capacity (1 + k_active + k_passive)
+struct HvMsg {                        // one 64-byte record
+    uint8_t type, ttl, prio, nx;
+    uint32_t src, dst, seq;           // seq: emission index at src (schedule order key)
+    uint32_t peer, epoch, did_e, did_c;
+    uint32_t x[kHvX];
+};
+static_assert(sizeof(HvMsg) == 64, "HvMsg is one 64-byte record");
+struct HvHead {                       // per-vertex scalars
+    uint8_t na, np;
+    uint16_t nsent, nrecv;
+    uint32_t seq;
+    unsigned long long draws;
+};
+struct HvCfg {
+    uint32_t active_max_size, active_min_size, active_rwl, passive_max_size, passive_rwl;
+    uint32_t shuffle_k_active, shuffle_k_passive;
+};
+constexpr int kHvNStat = 16;          // [1..9] sent by kind, 10 draws, 11 error bits, 12 msgs processed, 13 active
+struct HvArgs {
+    uint32_t n;
+    HvCfg cfg;
+    uint2 key;
+    uint32_t timers;                      // bit0 random_promotion, bit1 passive_view_maintenance
+    const uint32_t* __restrict__ alive;   // [ceil(n/32)]
+    HvHead* __restrict__ head;            // [n]
+    uint32_t* __restrict__ act;           // [n][8], 0xFFFFFFFF padded
+    uint32_t* __restrict__ pas;           // [n][32]
+    uint32_t* __restrict__ sent;          // [n][kHvMapCap][3]
+    uint32_t* __restrict__ recv;
+    const HvMsg* __restrict__ in;         // messages delivered this round
+    const uint32_t* nin;                  // device count of `in`
+    HvMsg* __restrict__ out;              // messages emitted this round
+    uint32_t* nout;                       // device count of `out` (atomicAdd)
+    uint32_t out_cap;
+    uint32_t* __restrict__ cnt;           // [n] bucket sizes
+    uint32_t* __restrict__ cur;           // [n] bucket cursors
+    uint32_t* __restrict__ off;           // [n+1] bucket starts
+    uint32_t* __restrict__ idx;           // [cap] message indices bucketed by destination
+    uint32_t* __restrict__ bsum;          // [ceil(n/256)] scan partials
+    unsigned long long* __restrict__ stats;  // [kHvNStat] for this round
+};
+hipError_t launch_hv_init(const HvArgs& a, hipStream_t s);
+hipError_t launch_hv_join(const HvArgs& a, const uint32_t* v, const uint32_t* contact, uint32_t k, hipStream_t s);
+hipError_t launch_hv_round(const HvArgs& a, hipStream_t s);
+
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,

@@ -2,7 +2,7 @@
 # Runs on the GPU box (via gpurun) from the repo root.  Each GPU step has its
 # own time limit; a crash / abort / timeout ends the session immediately,
 # a plain test failure (exit 1) does not.
-#   usage: tools/gpu_session.sh [steps...]   steps: test smoke bench prof pmc
+#   usage: tools/gpu_session.sh [steps...]   steps: build test t:<name> smoke bench prof pmc
 set -u
 mkdir -p gpurun_out
 STEPS=${*:-"test smoke bench prof"}
@@ -25,6 +25,7 @@ for s in $STEPS; do
     case $s in
         build) run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
         test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        t:*)   f=${s#t:}; run "pytest_${f}" 900 python -m pytest "tests/test_${f}.py" -m gpu -x -q ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         prof)
