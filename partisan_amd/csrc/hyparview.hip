@@ -67,24 +67,44 @@ __device__ __forceinline__ void sdel(uint32_t* s, uint32_t& n, uint32_t x) {
     n = k;
 }
 
-// id maps (sent_message_map / recv_message_map): rows {peer, epoch, cnt}
-__device__ __forceinline__ int mfind(const uint32_t* m, uint32_t n, uint32_t p) {
-    for (uint32_t i = 0; i < n; i++)
-        if (m[3 * i] == p) return (int)i;
-    return -1;
+// id maps (sent_message_map / recv_message_map, unbounded maps in the
+// reference): one global open-addressing table per map, key (v << 32 | peer),
+// value {epoch, cnt}.  Only vertex v inserts or reads keys of v, so a key is
+// never raced; distinct vertices share probe chains through atomicCAS on the
+// empty key.  Nothing is ever deleted, so a find that meets an empty slot is
+// a definite miss.
+constexpr unsigned long long kEmpty = ~0ull;
+constexpr uint32_t kProbeMax = 256;
+struct IdMap { unsigned long long* key; uint2* val; uint32_t mask; };
+__device__ __forceinline__ uint32_t hslot(unsigned long long k, uint32_t mask) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
+    return (uint32_t)k & mask;
 }
-__device__ void mput(Ctx& c, uint32_t* m, uint32_t& n, uint32_t p, uint32_t e, uint32_t cnt) {
-    int i = mfind(m, n, p);
-    if (i < 0) {
-        if (n >= kHvMapCap) { c.err |= 2u; return; }
-        i = (int)n++;
-        m[3 * i] = p;
+__device__ bool mget(const IdMap& m, uint32_t v, uint32_t p, uint2& out) {
+    const unsigned long long k = ((unsigned long long)v << 32) | p;
+    uint32_t i = hslot(k, m.mask);
+    for (uint32_t t = 0; t < kProbeMax; t++, i = (i + 1) & m.mask) {
+        const unsigned long long x = m.key[i];
+        if (x == k) { out = m.val[i]; return true; }
+        if (x == kEmpty) return false;
     }
-    m[3 * i + 1] = e;
-    m[3 * i + 2] = cnt;
+    return false;
 }
-__device__ __forceinline__ uint32_t* sent_map(const Ctx& c) { return c.a->sent + (size_t)c.v * kHvMapCap * 3; }
-__device__ __forceinline__ uint32_t* recv_map(const Ctx& c) { return c.a->recv + (size_t)c.v * kHvMapCap * 3; }
+__device__ void mput(Ctx& c, const IdMap& m, uint32_t& n, uint32_t p, uint32_t e, uint32_t cnt) {
+    const unsigned long long k = ((unsigned long long)c.v << 32) | p;
+    uint32_t i = hslot(k, m.mask);
+    for (uint32_t t = 0; t < kProbeMax; t++, i = (i + 1) & m.mask) {
+        unsigned long long x = m.key[i];
+        if (x == kEmpty) {
+            x = atomicCAS(&m.key[i], kEmpty, k);
+            if (x == kEmpty) { n++; x = k; }
+        }
+        if (x == k) { m.val[i] = make_uint2(e, cnt); return; }
+    }
+    c.err |= 2u;
+}
+__device__ __forceinline__ IdMap sent_map(const Ctx& c) { return IdMap{c.a->skey, c.a->sval, c.a->map_mask}; }
+__device__ __forceinline__ IdMap recv_map(const Ctx& c) { return IdMap{c.a->rkey, c.a->rval, c.a->map_mask}; }
 
 __device__ HvMsg* emit(Ctx& c, uint32_t dst, uint32_t type) {
     const uint32_t pos = atomicAdd(c.a->nout, 1u);
@@ -125,31 +145,26 @@ __device__ uint32_t select_exchange(Ctx& c, uint32_t* out) {
 }
 
 __device__ void get_current_id(Ctx& c, uint32_t p, uint32_t& e, uint32_t& cnt) {   // :2618-2627
-    const uint32_t* m = recv_map(c);
-    const int i = mfind(m, c.nrecv, p);
-    if (i >= 0) { e = m[3 * i + 1]; cnt = m[3 * i + 2]; }
+    uint2 r;
+    if (mget(recv_map(c), c.v, p, r)) { e = r.x; cnt = r.y; }
     else { e = 1; cnt = 0; }
 }
 __device__ bool is_addable_did(Ctx& c, uint32_t ie, uint32_t ic, uint32_t p) {       // :2652-2665
-    const uint32_t* m = sent_map(c);
-    const int i = mfind(m, c.nsent, p);
-    if (i < 0) return true;
-    const uint32_t e = m[3 * i + 1], cnt = m[3 * i + 2];
-    if (ie > e) return true;
-    if (ie == e) return ic >= cnt;
+    uint2 r;
+    if (!mget(sent_map(c), c.v, p, r)) return true;
+    if (ie > r.x) return true;
+    if (ie == r.x) return ic >= r.y;
     return false;
 }
 __device__ bool is_addable_epoch(Ctx& c, uint32_t pe, uint32_t p) {                  // :2667-2674
-    const uint32_t* m = sent_map(c);
-    const int i = mfind(m, c.nsent, p);
-    return i < 0 || pe >= m[3 * i + 1];
+    uint2 r;
+    return !mget(sent_map(c), c.v, p, r) || pe >= r.x;
 }
 __device__ bool is_valid_disconnect(Ctx& c, uint32_t ie, uint32_t ic, uint32_t p) {  // :2639-2650
-    const uint32_t* m = recv_map(c);
-    const int i = mfind(m, c.nrecv, p);
-    if (i < 0) return true;
-    if (ie > m[3 * i + 1]) return true;
-    return ic > m[3 * i + 2];
+    uint2 r;
+    if (!mget(recv_map(c), c.v, p, r)) return true;
+    if (ie > r.x) return true;
+    return ic > r.y;
 }
 
 __device__ void add_to_passive(Ctx& c, uint32_t p) {                                 // :2418-2449
@@ -168,12 +183,12 @@ __device__ void drop_random_active(Ctx& c) {                                    
     if (!pick_random(c, c.act, c.na, om, 1, r)) return;
     sdel(c.act, c.na, r);
     add_to_passive(c, r);
-    uint32_t* m = sent_map(c);
-    const int i = mfind(m, c.nsent, r);                                              // get_next_id/3
+    const IdMap m = sent_map(c);
+    uint2 prev;
     uint32_t ne = 1, nc = 1;
-    if (i >= 0) {
-        if (m[3 * i + 1] != 1u) { c.err |= 4u; return; }                             // case_clause
-        nc = m[3 * i + 2] + 1;
+    if (mget(m, c.v, r, prev)) {                                                     // get_next_id/3
+        if (prev.x != 1u) { c.err |= 4u; return; }                                    // case_clause
+        nc = prev.y + 1;
     }
     mput(c, m, c.nsent, r, ne, nc);
     if (alive_of(*c.a, r)) {

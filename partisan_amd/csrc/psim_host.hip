@@ -94,7 +94,10 @@ struct psim_handle {
         uint32_t n = 0, cap = 0;
         psim_hv_config cfg{};
         HvHead* head = nullptr;
-        uint32_t *act = nullptr, *pas = nullptr, *sent = nullptr, *recv = nullptr, *alive = nullptr;
+        uint32_t *act = nullptr, *pas = nullptr, *alive = nullptr;
+        unsigned long long *skey = nullptr, *rkey = nullptr;   // id-map hash tables
+        uint2 *sval = nullptr, *rval = nullptr;
+        uint32_t map_cap = 0;
         HvMsg* msg[2] = {nullptr, nullptr};
         uint32_t* nmsg = nullptr;                 // [2] device queue counts
         uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
@@ -143,7 +146,7 @@ constexpr uint32_t kHvChunk = 16;   // HyParView rounds between host synchronisa
 
 void free_hv(psim_handle* h) {
     auto& v = h->hv;
-    void* ptrs[] = {v.head, v.act, v.pas, v.sent, v.recv, v.alive, v.msg[0], v.msg[1], v.nmsg,
+    void* ptrs[] = {v.head, v.act, v.pas, v.skey, v.sval, v.rkey, v.rval, v.alive, v.msg[0], v.msg[1], v.nmsg,
                     v.cnt, v.cur, v.off, v.idx, v.bsum, v.joinbuf, v.stats};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1043,8 +1046,11 @@ HvArgs make_hv_args(const psim_handle* h, uint32_t par, unsigned long long* stat
     a.head = v.head;
     a.act = v.act;
     a.pas = v.pas;
-    a.sent = v.sent;
-    a.recv = v.recv;
+    a.skey = v.skey;
+    a.sval = v.sval;
+    a.rkey = v.rkey;
+    a.rval = v.rval;
+    a.map_mask = v.map_cap - 1;
     a.in = v.msg[par];
     a.nin = v.nmsg + par;
     a.out = v.msg[par ^ 1];
@@ -1062,8 +1068,8 @@ HvArgs make_hv_args(const psim_handle* h, uint32_t par, unsigned long long* stat
 int hv_check_err(psim_handle* h, unsigned long long e, uint64_t round) {
     if (e & 1ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: message queue over %u records",
                               (unsigned long long)round, h->hv.cap);
-    if (e & 2ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: id map over %u rows",
-                              (unsigned long long)round, kHvMapCap);
+    if (e & 2ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: id-map table (%u slots) too full",
+                              (unsigned long long)round, h->hv.map_cap);
     return PSIM_OK;
 }
 
@@ -1084,9 +1090,12 @@ int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
     const size_t N = n;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(8ull * n + 4096, 0xFFFFFFF0ull);
     const uint32_t nb = (n + kBlock - 1) / kBlock;
+    uint32_t mcap = 1u << 16;                  // id-map tables: >= 16 rows per vertex, power of two
+    while (mcap < 16ull * n && mcap < (1u << 31)) mcap <<= 1;
     auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
     bool ok = A((void**)&v.head, N * sizeof(HvHead)) && A((void**)&v.act, N * 32) && A((void**)&v.pas, N * 128) &&
-              A((void**)&v.sent, N * kHvMapCap * 12) && A((void**)&v.recv, N * kHvMapCap * 12) &&
+              A((void**)&v.skey, size_t(mcap) * 8) && A((void**)&v.sval, size_t(mcap) * 8) &&
+              A((void**)&v.rkey, size_t(mcap) * 8) && A((void**)&v.rval, size_t(mcap) * 8) &&
               A((void**)&v.alive, ((N + 31) / 32) * 4) && A((void**)&v.msg[0], size_t(cap) * sizeof(HvMsg)) &&
               A((void**)&v.msg[1], size_t(cap) * sizeof(HvMsg)) && A((void**)&v.nmsg, 16) &&
               A((void**)&v.cnt, N * 4) && A((void**)&v.cur, N * 4) && A((void**)&v.off, (N + 1) * 4) &&
@@ -1100,7 +1109,10 @@ int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
     }
     v.n = n;
     v.cap = cap;
+    v.map_cap = mcap;
     v.cfg = *cfg;
+    HIPCHK(h, hipMemset(v.skey, 0xFF, size_t(mcap) * 8));
+    HIPCHK(h, hipMemset(v.rkey, 0xFF, size_t(mcap) * 8));
     HIPCHK(h, hipMemset(v.alive, 0xFF, ((N + 31) / 32) * 4));
     HIPCHK(h, launch_hv_init(make_hv_args(h, 0, v.stats), h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1234,14 +1246,22 @@ int psim_hv_get_idmap(const psim_handle* h, uint32_t v, int which, uint32_t* pee
     HvHead hd;
     HIPCHK(hh, hipMemcpy(&hd, h->hv.head + v, sizeof hd, hipMemcpyDeviceToHost));
     const uint32_t m = which ? hd.nrecv : hd.nsent;
-    std::vector<uint32_t> rows(size_t(kHvMapCap) * 3);
-    HIPCHK(hh, hipMemcpy(rows.data(), (which ? h->hv.recv : h->hv.sent) + size_t(v) * kHvMapCap * 3,
-                         rows.size() * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < m && i < cap; i++) {
-        if (peer) peer[i] = rows[3 * i];
-        if (epoch) epoch[i] = rows[3 * i + 1];
-        if (cnt) cnt[i] = rows[3 * i + 2];
+    const size_t M = h->hv.map_cap;
+    std::vector<unsigned long long> keys(M);
+    std::vector<uint2> vals(M);
+    HIPCHK(hh, hipMemcpy(keys.data(), which ? h->hv.rkey : h->hv.skey, M * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hh, hipMemcpy(vals.data(), which ? h->hv.rval : h->hv.sval, M * 8, hipMemcpyDeviceToHost));
+    size_t k = 0;
+    for (size_t i = 0; i < M; i++) {
+        if (keys[i] == ~0ull || (uint32_t)(keys[i] >> 32) != v) continue;
+        if (k < cap) {
+            if (peer) peer[k] = (uint32_t)keys[i];
+            if (epoch) epoch[k] = vals[i].x;
+            if (cnt) cnt[k] = vals[i].y;
+        }
+        k++;
     }
+    if (k != m) return fail(hh, PSIM_ESTATE, "id map of %u: %zu rows in the table, head says %u", v, k, m);
     *len = m;
     return PSIM_OK;
 }

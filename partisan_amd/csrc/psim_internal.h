@@ -82,7 +82,6 @@ hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const ui
 hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
 
 // HyParView (hyparview.hip)
-constexpr uint32_t kHvMapCap = 128;   // rows per sent/recv id map (overflow -> PSIM_EOVERFLOW)
 constexpr uint32_t kHvX = 8;          // exchange list capacity (1 + k_active + k_passive)
 struct HvMsg {                        // one 64-byte record
     uint8_t type, ttl, prio, nx;
@@ -111,8 +110,11 @@ struct HvArgs {
     HvHead* __restrict__ head;            // [n]
     uint32_t* __restrict__ act;           // [n][8], 0xFFFFFFFF padded
     uint32_t* __restrict__ pas;           // [n][32]
-    uint32_t* __restrict__ sent;          // [n][kHvMapCap][3]
-    uint32_t* __restrict__ recv;
+    unsigned long long* skey;             // sent_message_map table: keys (v << 32 | peer)
+    uint2* sval;                          //   values {epoch, cnt}
+    unsigned long long* rkey;             // recv_message_map table
+    uint2* rval;
+    uint32_t map_mask;                    // table size - 1 (power of two)
     const HvMsg* __restrict__ in;         // messages delivered this round
     const uint32_t* nin;                  // device count of `in`
     HvMsg* __restrict__ out;              // messages emitted this round
