@@ -19,8 +19,10 @@
 typedef struct {
     psim_handle* h;
     ErlNifMutex* mu;
-    uint32_t n;
+    uint32_t n;          /* plumtree vertices (load_csr) */
     uint64_t slots;
+    uint32_t hv_n;       /* hyparview vertices (hv_setup) */
+    uint32_t dm_n;       /* demers vertices (demers_setup) */
 } sim_res;
 
 static ErlNifResourceType* SIM_RES;
@@ -79,7 +81,12 @@ static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[])
     cfg.device = (int32_t)map_u32(env, argv[0], "device", (unsigned)-1);
     cfg.lazy_tick_rounds = map_u32(env, argv[0], "lazy_tick_rounds", 1);
     cfg.exchange_tick_rounds = map_u32(env, argv[0], "exchange_tick_rounds", 10);
-    cfg.seed = map_u32(env, argv[0], "seed", 0);
+    {
+        ERL_NIF_TERM v;
+        ErlNifUInt64 seed = 0;
+        if (enif_get_map_value(env, argv[0], mk_atom(env, "seed"), &v)) enif_get_uint64(env, v, &seed);
+        cfg.seed = (uint64_t)seed;
+    }
     sim_res* r = (sim_res*)enif_alloc_resource(SIM_RES, sizeof(sim_res));
     memset(r, 0, sizeof *r);
     int rc = psim_create(&cfg, &r->h);
@@ -245,6 +252,174 @@ static ERL_NIF_TERM nif_delivered(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     return enif_make_tuple2(env, mk_atom(env, "ok"), t);
 }
 
+/* ---- HyParView --------------------------------------------------------- */
+
+/* hv_setup(Sim, N, #{active_max_size, ..., promotion_rounds}) -> ok */
+static ERL_NIF_TERM nif_hv_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_is_map(env, argv[2]))
+        return enif_make_badarg(env);
+    psim_hv_config c;
+    c.active_max_size = map_u32(env, argv[2], "active_max_size", 6);
+    c.active_min_size = map_u32(env, argv[2], "active_min_size", 3);
+    c.active_rwl = map_u32(env, argv[2], "active_rwl", 6);
+    c.passive_max_size = map_u32(env, argv[2], "passive_max_size", 30);
+    c.passive_rwl = map_u32(env, argv[2], "passive_rwl", 6);
+    c.shuffle_k_active = map_u32(env, argv[2], "shuffle_k_active", 3);
+    c.shuffle_k_passive = map_u32(env, argv[2], "shuffle_k_passive", 4);
+    c.shuffle_rounds = map_u32(env, argv[2], "shuffle_rounds", 10);
+    c.promotion_rounds = map_u32(env, argv[2], "promotion_rounds", 5);
+    enif_mutex_lock(r->mu);
+    int rc = psim_hv_setup(r->h, n, &c);
+    if (rc == PSIM_OK) r->hv_n = n;
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* hv_join(Sim, Joiners :: <<u32-little>>, Contacts :: <<u32-little>>) -> ok
+ * (one handle_cast({join, Contact}) per joiner, between two rounds) */
+static ERL_NIF_TERM nif_hv_join(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary v, c;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &v) ||
+        !enif_inspect_binary(env, argv[2], &c) || v.size != c.size || v.size % 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_hv_join(r->h, (const uint32_t*)v.data, (const uint32_t*)c.data, v.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+static ERL_NIF_TERM hv_stats_term(ErlNifEnv* env, const psim_hv_stats* s) {
+    static const char* names[10] = {"", "join", "neighbor", "forward_join", "disconnect", "neighbor_request",
+                                    "neighbor_rejected", "neighbor_accepted", "shuffle", "shuffle_reply"};
+    ERL_NIF_TERM keys[13], vals[13];
+    for (int k = 1; k < 10; k++) {
+        keys[k - 1] = mk_atom(env, names[k]);
+        vals[k - 1] = enif_make_uint64(env, s->sent[k]);
+    }
+    keys[9] = mk_atom(env, "draws");      vals[9] = enif_make_uint64(env, s->draws);
+    keys[10] = mk_atom(env, "error");     vals[10] = enif_make_uint64(env, s->error);
+    keys[11] = mk_atom(env, "processed"); vals[11] = enif_make_uint64(env, s->processed);
+    keys[12] = mk_atom(env, "kernel_us"); vals[12] = enif_make_uint64(env, (uint64_t)(s->kernel_ms * 1000.0));
+    ERL_NIF_TERM m;
+    enif_make_map_from_arrays(env, keys, vals, 13, &m);
+    return m;
+}
+
+/* hv_step(Sim, Rounds) -> {ok, [StatsMap]} */
+static ERL_NIF_TERM nif_hv_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &k) || k == 0 || k > 65536)
+        return enif_make_badarg(env);
+    psim_hv_stats* st = (psim_hv_stats*)enif_alloc(k * sizeof(psim_hv_stats));
+    enif_mutex_lock(r->mu);
+    int rc = psim_hv_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (unsigned i = k; i > 0; i--) list = enif_make_list_cell(env, hv_stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* hv_views(Sim) -> {ok, Active, ActiveLen, Passive, PassiveLen}: u32-little
+ * rows of 8 / 32 ids padded with 16#FFFFFFFF, and u8 lengths */
+static ERL_NIF_TERM nif_hv_views(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r) || !r->hv_n) return enif_make_badarg(env);
+    const size_t n = r->hv_n;
+    ERL_NIF_TERM ta, tna, tp, tnp;
+    unsigned char* a = enif_make_new_binary(env, n * 32, &ta);
+    unsigned char* na = enif_make_new_binary(env, n, &tna);
+    unsigned char* p = enif_make_new_binary(env, n * 128, &tp);
+    unsigned char* np = enif_make_new_binary(env, n, &tnp);
+    enif_mutex_lock(r->mu);
+    int rc = psim_hv_get_views(r->h, (uint32_t*)a, na, (uint32_t*)p, np, n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    ERL_NIF_TERM out[5] = {mk_atom(env, "ok"), ta, tna, tp, tnp};
+    return enif_make_tuple_from_array(env, out, 5);
+}
+
+/* ---- Demers --------------------------------------------------------------- */
+
+/* demers_setup(Sim, N, M, AePeriod, RumorMongering :: boolean()) -> ok */
+static ERL_NIF_TERM nif_demers_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, m, ae;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &m) ||
+        !enif_get_uint(env, argv[3], &ae))
+        return enif_make_badarg(env);
+    const int rm = enif_is_identical(argv[4], mk_atom(env, "true"));
+    enif_mutex_lock(r->mu);
+    int rc = psim_demers_setup(r->h, n, m, ae, rm ? 1u : 0u);
+    if (rc == PSIM_OK) rc = psim_demers_broadcast_all(r->h);
+    if (rc == PSIM_OK) r->dm_n = n;
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* demers_run(Sim, MaxRounds) -> {ok, Rounds, Seen :: <<u64-little per vertex>>} */
+static ERL_NIF_TERM nif_demers_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr) || !r->dm_n) return enif_make_badarg(env);
+    ERL_NIF_TERM t;
+    unsigned char* seen = enif_make_new_binary(env, (size_t)r->dm_n * 8, &t);
+    uint32_t ran = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_demers_run(r->h, maxr, NULL, 0, &ran);
+    if (rc == PSIM_OK) rc = psim_demers_get_seen(r->h, (uint64_t*)seen, r->dm_n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), t);
+}
+
+/* ---- vclock (dense 64-lane clocks, u32-little lanes, 0 = absent) ----------- */
+
+/* vclock(Sim, Op :: descends | dominates | merge | increment, A, B) ->
+ *   {ok, <<0|1 per clock>>} | {ok, Clocks}   (B = actor ids for increment) */
+static ERL_NIF_TERM nif_vclock(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary a, b;
+    const size_t cb = PSIM_VC_LANES * 4;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[2], &a) ||
+        !enif_inspect_binary(env, argv[3], &b) || a.size % cb)
+        return enif_make_badarg(env);
+    const size_t n = a.size / cb;
+    const int inc = enif_is_identical(argv[1], mk_atom(env, "increment"));
+    if (inc ? b.size != n * 4 : b.size != a.size) return enif_make_badarg(env);
+    ERL_NIF_TERM t;
+    int rc;
+    if (enif_is_identical(argv[1], mk_atom(env, "descends")) || enif_is_identical(argv[1], mk_atom(env, "dominates"))) {
+        unsigned char* o = enif_make_new_binary(env, n, &t);
+        enif_mutex_lock(r->mu);
+        rc = enif_is_identical(argv[1], mk_atom(env, "descends"))
+                 ? psim_vclock_descends(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, o, n)
+                 : psim_vclock_dominates(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, o, n);
+        enif_mutex_unlock(r->mu);
+    } else if (inc || enif_is_identical(argv[1], mk_atom(env, "merge"))) {
+        unsigned char* o = enif_make_new_binary(env, a.size, &t);
+        enif_mutex_lock(r->mu);
+        rc = inc ? psim_vclock_increment(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, (uint32_t*)o, n)
+                 : psim_vclock_merge(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, (uint32_t*)o, n);
+        enif_mutex_unlock(r->mu);
+    } else {
+        return enif_make_badarg(env);
+    }
+    return rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"), t) : err(env, rc);
+}
+
 static ErlNifFunc funcs[] = {
     {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -256,6 +431,13 @@ static ErlNifFunc funcs[] = {
     {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"hv_step", 2, nif_hv_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"hv_views", 1, nif_hv_views, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"demers_setup", 5, nif_demers_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"demers_run", 2, nif_demers_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"vclock", 4, nif_vclock, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

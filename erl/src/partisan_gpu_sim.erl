@@ -1,0 +1,103 @@
+%% partisan_gpu_sim -- Erlang binding of libpsim.so through the NIF in
+%% ../c_src/partisan_gpu_sim_nif.c.  Every function is replaced by the NIF
+%% at load time; the bodies below only run if the NIF failed to load.
+%%
+%% Binary conventions: vertex ids and masks are little-endian u32, row
+%% pointers u64, byte maps one byte per vertex (see include/psim.h).
+-module(partisan_gpu_sim).
+
+-export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
+         peers/1, slots/1, delivered/1,
+         hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
+         demers_setup/5, demers_run/2,
+         vclock/4]).
+-export([active_views/1, csr_from_views/1]).
+
+-on_load(init/0).
+
+-type sim() :: reference().
+-type error() :: {error, einval | enomem | ehip | erccl | estate | eoverflow | ebusy | enodev | psim_error}.
+-export_type([sim/0]).
+
+init() ->
+    Dir = case code:priv_dir(partisan) of
+              {error, bad_name} -> filename:join(filename:dirname(code:which(?MODULE)), "../priv");
+              D -> D
+          end,
+    erlang:load_nif(filename:join(Dir, "partisan_gpu_sim"), 0).
+
+-spec new(#{device => integer(), seed => non_neg_integer(), lazy_tick_rounds => pos_integer(),
+            exchange_tick_rounds => pos_integer()}) -> {ok, sim()} | error().
+new(_Opts) -> erlang:nif_error(nif_not_loaded).
+
+-spec load_csr(sim(), binary(), binary()) -> ok | error().
+load_csr(_Sim, _RowPtr, _Col) -> erlang:nif_error(nif_not_loaded).
+
+-spec set_alive(sim(), binary()) -> ok | error().
+set_alive(_Sim, _Alive) -> erlang:nif_error(nif_not_loaded).
+
+-spec reset_trees(sim()) -> ok | error().
+reset_trees(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+-spec broadcast(sim(), non_neg_integer()) -> {ok, non_neg_integer()} | error().
+broadcast(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
+
+-spec step(sim(), pos_integer()) -> {ok, [map()]} | error().
+step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+
+-spec run(sim(), pos_integer()) -> {ok, non_neg_integer(), [map()]} | error().
+run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
+
+-spec peers(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
+peers(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+-spec slots(sim()) -> {ok, binary(), binary()} | error().
+slots(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+-spec delivered(sim()) -> {ok, binary()} | error().
+delivered(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+-spec hv_setup(sim(), pos_integer(), map()) -> ok | error().
+hv_setup(_Sim, _N, _Config) -> erlang:nif_error(nif_not_loaded).
+
+-spec hv_join(sim(), binary(), binary()) -> ok | error().
+hv_join(_Sim, _Joiners, _Contacts) -> erlang:nif_error(nif_not_loaded).
+
+-spec hv_step(sim(), pos_integer()) -> {ok, [map()]} | error().
+hv_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+
+-spec hv_views(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
+hv_views(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+-spec demers_setup(sim(), pos_integer(), 1..64, non_neg_integer(), boolean()) -> ok | error().
+demers_setup(_Sim, _N, _M, _AePeriod, _RumorMongering) -> erlang:nif_error(nif_not_loaded).
+
+-spec demers_run(sim(), pos_integer()) -> {ok, non_neg_integer(), binary()} | error().
+demers_run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
+
+-spec vclock(sim(), descends | dominates | merge | increment, binary(), binary()) -> {ok, binary()} | error().
+vclock(_Sim, _Op, _A, _B) -> erlang:nif_error(nif_not_loaded).
+
+%% Active views (self excluded) as a list of id lists, vertex order.
+-spec active_views(sim()) -> {ok, [[non_neg_integer()]]} | error().
+active_views(Sim) ->
+    case hv_views(Sim) of
+        {ok, Act, Len, _Pas, _PLen} -> {ok, rows(Act, Len, 0, [])};
+        Err -> Err
+    end.
+
+rows(<<>>, <<>>, _V, Acc) ->
+    lists:reverse(Acc);
+rows(<<Row:32/binary, RestA/binary>>, <<L, RestL/binary>>, V, Acc) ->
+    Ids = [I || <<I:32/little>> <= binary:part(Row, 0, L * 4), I =/= V],
+    rows(RestA, RestL, V + 1, [Ids | Acc]).
+
+%% The active views as the membership CSR load_csr/3 takes (the peer
+%% service feeding partisan_plumtree_broadcast).
+-spec csr_from_views([[non_neg_integer()]]) -> {binary(), binary()}.
+csr_from_views(Views) ->
+    {RowPtr, _} = lists:foldl(fun(Ids, {Acc, Off}) -> Next = Off + length(Ids),
+                                                      {<<Acc/binary, Next:64/little>>, Next} end,
+                              {<<0:64/little>>, 0}, Views),
+    Col = << <<I:32/little>> || Ids <- Views, I <- Ids >>,
+    {RowPtr, Col}.

@@ -75,3 +75,23 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "pyoracle" not in src and "liboracle" not in src and "oracle.h" not in src, f
+
+
+def test_nif_shim_typechecks():
+    """erl/c_src/partisan_gpu_sim_nif.c against include/psim.h (erl_nif.h is a
+    declarations-only stand-in: this image has no erts)."""
+    import subprocess
+    src = os.path.join(ROOT, "erl", "c_src", "partisan_gpu_sim_nif.c")
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-std=c11",
+                        "-I" + os.path.join(ROOT, "tests", "nif_mock"), "-I" + os.path.join(ROOT, "include"), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_nif_calls_only_declared_symbols():
+    import re
+    hdr = open(os.path.join(ROOT, "include", "psim.h")).read()
+    declared = set(re.findall(r"\b(psim_\w+)\s*\(", hdr))
+    nif = open(os.path.join(ROOT, "erl", "c_src", "partisan_gpu_sim_nif.c")).read()
+    used = set(re.findall(r"\b(psim_\w+)\s*\(", nif))
+    assert used and used <= declared, used - declared

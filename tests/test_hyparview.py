@@ -180,9 +180,10 @@ def test_failures_disconnect_and_promotion():
 
 
 @pytest.mark.gpu
-def test_c2_sequential_10k_final_state():
-    """SURVEY 8 config C2's overlay: 10k sequential joins (one per round), then
-    100 rounds; final views, draws and counters equal the oracle's."""
+def test_c2_hyparview_overlay_then_plumtree():
+    """10k sequential joins (one per round), S = 10
+    shuffle periods (100 rounds), then one Plumtree broadcast from vertex 0
+    over the resulting active views; every stage equals the oracle's."""
     n = 10000
     sim, g, o = _pair(n)
     c = contacts(n)
@@ -197,6 +198,23 @@ def test_c2_sequential_10k_final_state():
     _compare(g, o, n, maps=False)
     act, na, _, _ = g.views()
     check_invariants([act[v, :na[v]].tolist() for v in range(n)], n)
+    # ... then one Plumtree broadcast from vertex 0 over the active views:
+    # per-round counters and the final tree equal the oracle's
+    rp, col = g.overlay()
+    sim.load_overlay(rp, col)
+    pt = O.Plumtree(rp, col, 1)
+    assert sim.broadcast(0) == pt.heartbeat(0)
+    gst, gr = sim.run()
+    ost, orr = pt.run()
+    assert gr == orr
+    for a, b in zip(gst, ost):
+        for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft"):
+            assert a[k] == b[k], (k, a, b)
+    assert sim.delivered().all()
+    eager, lazy, _, _ = sim.plumtree_state()
+    for v in range(0, n, 97):
+        oe, ol = pt.peers(v, 0)
+        assert sim.mask_to_peers(v, eager[v]) == oe and sim.mask_to_peers(v, lazy[v]) == ol, v
     sim.close()
 
 
