@@ -244,6 +244,34 @@ int  psim_hv_get_idmap(const psim_handle* h, uint32_t v, int which, uint32_t* pe
                        size_t cap, size_t* len);
 int  psim_hv_inflight(const psim_handle* h, uint64_t* messages);
 
+/* --- causal delivery (partisan_causality_backend.erl) ------------------ */
+typedef struct psim_causal_stats {
+    uint64_t emitted;              /* emit/4 calls at the end of the round      */
+    uint64_t received;             /* receive_message/2 calls                   */
+    uint64_t delivered;            /* deliver/5 calls                           */
+    uint64_t checks;               /* dominates evaluations                     */
+    uint64_t buffered;             /* buffered messages after the round         */
+    uint64_t algo_bytes;           /* 1024 B per delivery + 256 B per
+                                      dominates check + 32 B per message        */
+    double   kernel_ms;
+} psim_causal_stats;
+/* Causal delivery among n vertices with m <= 64 emitters e_k = floor(k n / m)
+ * (clock lanes = emitter actors; a non-emitter's own entry is its `self`
+ * counter).  At the end of round t emitter k broadcasts -- emit/4 to every
+ * other vertex in id order (:172-201) -- iff t % period == k % period; the
+ * message to v lands in round t + 1 + mulhi(Philox({v, t, 6, k}), dmax).
+ * Round t at v: receive_message/2 per arrival in (src, seq) order (:205-220),
+ * then handle_info(deliver) if t % redeliver == 0 (:233-248). */
+int  psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax, uint32_t redeliver);
+int  psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* stats, size_t cap);
+/* lanes[n*64] (lane k = counter of emitter k's actor, 0 = absent), self[n]. */
+int  psim_causal_get_clocks(const psim_handle* h, uint32_t* lanes, uint32_t* self, size_t n);
+/* buffered_messages of v in list order, as (emitter index, emission round). */
+int  psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uint32_t* round, size_t cap,
+                              size_t* len);
+int  psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t n);
+int  psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

@@ -211,6 +211,32 @@ uint64_t orc_hv_draws(const orc_hyparview* s, uint32_t v);
 size_t orc_hv_idmap(const orc_hyparview* s, uint32_t v, int which, uint32_t* peer, uint32_t* ep, uint32_t* cnt,
                     size_t cap);
 
+/* ------------------------------------------------------------------ */
+/* Causal delivery (src/partisan_causality_backend.erl)                */
+/* ------------------------------------------------------------------ */
+typedef struct orc_causal_stats {
+    uint64_t emitted;            /* emit calls (end of the round) */
+    uint64_t received;           /* receive_message calls */
+    uint64_t delivered;          /* deliver/5 calls */
+    uint64_t checks;             /* dominates evaluations */
+    uint64_t buffered;           /* messages buffered after the round */
+} orc_causal_stats;
+typedef struct orc_causal orc_causal;
+/* m = 0: primitive API only (emit/receive/tick by hand, delivery logs kept) */
+orc_causal* orc_causal_create(uint32_t n, uint32_t m, uint32_t period, uint32_t dmax, uint32_t redeliver,
+                              uint64_t seed);
+void orc_causal_destroy(orc_causal* s);
+uint32_t orc_causal_emit(orc_causal* s, uint32_t node, uint32_t dest);
+void orc_causal_receive(orc_causal* s, uint32_t node, uint32_t msg);
+void orc_causal_tick(orc_causal* s, uint32_t node);
+size_t orc_causal_log(const orc_causal* s, uint32_t node, uint32_t* msgs, size_t cap);
+void orc_causal_reset_handles(void);
+uint32_t orc_causal_step(orc_causal* s, uint32_t rounds, orc_causal_stats* st);
+size_t orc_causal_clock(const orc_causal* s, uint32_t v, orc_dot* out, size_t cap);
+size_t orc_causal_buffered(const orc_causal* s, uint32_t v, uint32_t* k, uint32_t* round, size_t cap);
+uint64_t orc_causal_delivered(const orc_causal* s, uint32_t v);
+uint32_t orc_causal_emitter(const orc_causal* s, uint32_t k);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,13 @@ class HvStats(C.Structure):
         return {"sent": [int(x) for x in self.sent[1:10]], "draws": int(self.draws), "error": int(self.error)}
 
 
+class CausalStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("emitted", "received", "delivered", "checks", "buffered")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 HV_DEFAULTS = dict(active_max_size=6, active_min_size=3, active_rwl=6, passive_max_size=30, passive_rwl=6,
                    shuffle_k_active=3, shuffle_k_passive=4, shuffle_rounds=10, promotion_rounds=5)
 
@@ -147,6 +154,24 @@ def lib():
         L.orc_hv_draws.restype = C.c_uint64
         L.orc_hv_idmap.argtypes = [C.c_void_p, C.c_uint32, C.c_int, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), sz]
         L.orc_hv_idmap.restype = sz
+        L.orc_causal_create.argtypes = [C.c_uint32] * 5 + [C.c_uint64]
+        L.orc_causal_create.restype = C.c_void_p
+        L.orc_causal_destroy.argtypes = [C.c_void_p]
+        L.orc_causal_emit.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_causal_emit.restype = C.c_uint32
+        L.orc_causal_receive.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_causal_tick.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_causal_log.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), sz]
+        L.orc_causal_log.restype = sz
+        L.orc_causal_step.argtypes = [C.c_void_p, C.c_uint32, P(CausalStats)]
+        L.orc_causal_clock.argtypes = [C.c_void_p, C.c_uint32, P(Dot), sz]
+        L.orc_causal_clock.restype = sz
+        L.orc_causal_buffered.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32), sz]
+        L.orc_causal_buffered.restype = sz
+        L.orc_causal_delivered.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_causal_delivered.restype = C.c_uint64
+        L.orc_causal_emitter.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_causal_emitter.restype = C.c_uint32
         _lib = L
     return _lib
 
@@ -505,3 +530,57 @@ class HyParView:
         pe, ep, cn = (C.c_uint32 * cap)(), (C.c_uint32 * cap)(), (C.c_uint32 * cap)()
         k = lib().orc_hv_idmap(self._h, v, which, pe, ep, cn, cap)
         return sorted((pe[i], ep[i], cn[i]) for i in range(min(k, cap)))
+
+
+class Causal:
+    """Causal delivery backend.  m = 0: the primitive API (emit/receive/tick);
+    m > 0: the round workload of DESIGN.md "Causal delivery"."""
+
+    def __init__(self, n, m=0, period=1, dmax=1, redeliver=1, seed=0):
+        self.n, self.m = n, m
+        if m == 0:
+            lib().orc_causal_reset_handles()
+        self._h = lib().orc_causal_create(n, m, period, dmax, redeliver, seed)
+
+    def close(self):
+        if self._h:
+            lib().orc_causal_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def emit(self, node, dest):
+        return lib().orc_causal_emit(self._h, node, dest)
+
+    def receive(self, node, msg):
+        lib().orc_causal_receive(self._h, node, msg)
+
+    def tick(self, node):
+        lib().orc_causal_tick(self._h, node)
+
+    def log(self, node, cap=4096):
+        out = (C.c_uint32 * cap)()
+        k = lib().orc_causal_log(self._h, node, out, cap)
+        return list(out[:min(k, cap)])
+
+    def step(self, rounds=1):
+        st = (CausalStats * rounds)()
+        lib().orc_causal_step(self._h, rounds, st)
+        return [x.as_dict() for x in st]
+
+    def clock(self, v, cap=4096):
+        out = (Dot * cap)()
+        k = lib().orc_causal_clock(self._h, v, out, cap)
+        return [(out[i].actor, out[i].ctr) for i in range(min(k, cap))]
+
+    def buffered(self, v, cap=4096):
+        k_, r_ = (C.c_uint32 * cap)(), (C.c_uint32 * cap)()
+        k = lib().orc_causal_buffered(self._h, v, k_, r_, cap)
+        return [(k_[i], r_[i]) for i in range(min(k, cap))]
+
+    def delivered(self, v):
+        return lib().orc_causal_delivered(self._h, v)
+
+    def emitter(self, k):
+        return lib().orc_causal_emitter(self._h, k)

@@ -74,6 +74,15 @@ class HvStats(C.Structure):
                 "kernel_ms": float(self.kernel_ms)}
 
 
+class CausalStats(C.Structure):
+    _fields_ = [("emitted", C.c_uint64), ("received", C.c_uint64), ("delivered", C.c_uint64),
+                ("checks", C.c_uint64), ("buffered", C.c_uint64), ("algo_bytes", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -118,6 +127,13 @@ SIGNATURES = {
     "psim_hv_get_idmap": (C.c_int, [_H, C.c_uint32, C.c_int, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),
                                     C.c_size_t, _P(C.c_size_t)]),
     "psim_hv_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_causal_setup": (C.c_int, [_H] + [C.c_uint32] * 5),
+    "psim_causal_step": (C.c_int, [_H, C.c_uint32, _P(CausalStats), C.c_size_t]),
+    "psim_causal_get_clocks": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_causal_get_buffered": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t,
+                                           _P(C.c_size_t)]),
+    "psim_causal_get_delivered": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
+    "psim_causal_emitters": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

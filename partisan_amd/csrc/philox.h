@@ -7,7 +7,7 @@
 
 namespace psim {
 
-enum RngKind : uint32_t { KIND_WORKLOAD = 1, KIND_RM = 2, KIND_AE = 3, KIND_HV = 4, KIND_SCAMP = 5 };
+enum RngKind : uint32_t { KIND_WORKLOAD = 1, KIND_RM = 2, KIND_AE = 3, KIND_HV = 4, KIND_SCAMP = 5, KIND_CAUSAL = 6 };
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll

@@ -108,6 +108,14 @@ struct psim_handle {
         uint32_t par = 0;                         // queue the next round reads
         uint64_t round = 0;
     } hv;
+
+    // causal delivery state (causal.hip)
+    struct Cs {
+        uint32_t n = 0, m = 0, period = 1, dmax = 1, redeliver = 1;
+        uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr;
+        unsigned long long *delivered = nullptr, *stats = nullptr, *h_stats = nullptr;
+        uint64_t round = 0;
+    } cs;
 };
 
 namespace {
@@ -154,6 +162,15 @@ void free_hv(psim_handle* h) {
     for (auto& e : v.ev)
         if (e) (void)hipEventDestroy(e);
     h->hv = psim_handle::Hv();
+}
+
+void free_cs(psim_handle* h) {
+    auto& c = h->cs;
+    void* ptrs[] = {c.clk, c.self, c.buf, c.nbuf, c.base, c.delivered, c.stats};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (c.h_stats) (void)hipHostFree(c.h_stats);
+    h->cs = psim_handle::Cs();
 }
 
 void free_graph(psim_handle* h) {
@@ -350,6 +367,7 @@ int psim_destroy(psim_handle* h) {
     free_graph(h);
     free_demers(h);
     free_hv(h);
+    free_cs(h);
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);
@@ -1274,6 +1292,157 @@ int psim_hv_inflight(const psim_handle* h, uint64_t* messages) {
     uint32_t c = 0;
     HIPCHK(hh, hipMemcpy(&c, h->hv.nmsg + h->hv.par, 4, hipMemcpyDeviceToHost));
     *messages = c;
+    return PSIM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
+    const auto& c = h->cs;
+    CsArgs a{};
+    a.n = c.n;
+    a.m = c.m;
+    a.period = c.period;
+    a.dmax = c.dmax;
+    a.redeliver = c.redeliver;
+    a.v_lo = 0;
+    a.n_global = c.n;
+    a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
+    a.t = t;
+    a.clk = c.clk;
+    a.self = c.self;
+    a.buf = c.buf;
+    a.nbuf = c.nbuf;
+    a.delivered = c.delivered;
+    a.base = c.base;
+    a.stats = c.stats;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax, uint32_t redeliver) {
+    if (!h) return PSIM_EINVAL;
+    if (n < 2 || m < 1 || m > kCsLanes || m > n || period < 1 || dmax < 1 || dmax > 30 ||
+        dmax + 2 * redeliver + period + 2 >= kCsWindow)
+        return fail(h, PSIM_EINVAL, "causal: need 2 <= n, 1 <= m <= min(64, n), period >= 1, 1 <= dmax <= 30, "
+                                    "dmax + 2 redeliver + period + 2 < %u", kCsWindow);
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    free_cs(h);
+    auto& c = h->cs;
+    const size_t N = n;
+    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    const bool ok = A((void**)&c.clk, N * kCsLanes * 4) && A((void**)&c.self, N * 4) &&
+                    A((void**)&c.buf, N * kCsBufCap * 4) && A((void**)&c.nbuf, N * 4) &&
+                    A((void**)&c.base, size_t(kCsWindow) * kCsLanes * kCsLanes * 4) &&
+                    A((void**)&c.delivered, N * 8) && A((void**)&c.stats, kStatShards * kCsNStat * 8) &&
+                    hipHostMalloc((void**)&c.h_stats, kStatShards * kCsNStat * 8, 0) == hipSuccess;
+    if (!ok) {
+        free_cs(h);
+        return fail(h, PSIM_ENOMEM, "causal state for n=%u", n);
+    }
+    c.n = n;
+    c.m = m;
+    c.period = period;
+    c.dmax = dmax;
+    c.redeliver = redeliver;
+    return PSIM_OK;
+}
+
+int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    auto& c = h->cs;
+    if (!c.n) return fail(h, PSIM_ESTATE, "psim_causal_setup not called");
+    HIPCHK(h, hipSetDevice(h->device));
+    for (uint32_t i = 0; i < rounds; i++) {
+        const uint64_t t = c.round + 1;
+        if (t >= (1u << 24)) return fail(h, PSIM_EOVERFLOW, "causal: round %llu exceeds 2^24", (unsigned long long)t);
+        CsArgs a = make_cs_args(h, (uint32_t)t);
+        HIPCHK(h, hipMemsetAsync(c.stats, 0, kStatShards * kCsNStat * 8, h->stream));
+        HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
+        HIPCHK(h, launch_cs_round(a, h->stream));
+        HIPCHK(h, launch_cs_broadcast(a, h->stream));
+        HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
+        HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        c.round = t;
+        unsigned long long r[kCsNStat] = {0};
+        unsigned long long err = 0;
+        for (int sh = 0; sh < kStatShards; sh++)
+            for (int q = 0; q < kCsNStat; q++) {
+                if (q == 5) err |= c.h_stats[sh * kCsNStat + q];
+                else r[q] += c.h_stats[sh * kCsNStat + q];
+            }
+        if (err & 1ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
+                                    (unsigned long long)t, kCsBufCap);
+        if (err & 2ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
+                                    "clock window", (unsigned long long)t, kCsWindow);
+        if (err & 4ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a u32 clock entry overflowed",
+                                    (unsigned long long)t);
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        h->kernel_ms_total += ms;
+        h->rounds_total++;
+        if (out && i < cap) {
+            psim_causal_stats& o = out[i];
+            memset(&o, 0, sizeof o);
+            o.emitted = r[6];
+            o.received = r[1];
+            o.delivered = r[2];
+            o.checks = r[3];
+            o.buffered = r[4];
+            o.algo_bytes = 1024ull * r[2] + 256ull * r[3] + 32ull * r[1];
+            o.kernel_ms = ms;
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_causal_get_clocks(const psim_handle* h, uint32_t* lanes, uint32_t* self, size_t n) {
+    if (!h || n != h->cs.n || !n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    if (lanes) HIPCHK(hh, hipMemcpy(lanes, h->cs.clk, n * kCsLanes * 4, hipMemcpyDeviceToHost));
+    if (self) HIPCHK(hh, hipMemcpy(self, h->cs.self, n * 4, hipMemcpyDeviceToHost));
+    return PSIM_OK;
+}
+
+int psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uint32_t* round, size_t cap,
+                             size_t* len) {
+    if (!h || !len || v >= h->cs.n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    uint32_t nb = 0;
+    HIPCHK(hh, hipMemcpy(&nb, h->cs.nbuf + v, 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> e(nb);
+    if (nb) HIPCHK(hh, hipMemcpy(e.data(), h->cs.buf + size_t(v) * kCsBufCap, nb * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nb && i < cap; i++) {
+        if (k) k[i] = e[i] >> 24;
+        if (round) round[i] = e[i] & 0xFFFFFFu;
+    }
+    *len = nb;
+    return PSIM_OK;
+}
+
+int psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t n) {
+    if (!h || !delivered || n != h->cs.n || !n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    HIPCHK(hh, hipMemcpy(delivered, h->cs.delivered, n * 8, hipMemcpyDeviceToHost));
+    return PSIM_OK;
+}
+
+int psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m) {
+    if (!h || !emitters || m != h->cs.m || !m) return PSIM_EINVAL;
+    for (size_t k = 0; k < m; k++) emitters[k] = (uint32_t)((uint64_t(k) * h->cs.n) / h->cs.m);
     return PSIM_OK;
 }
 

