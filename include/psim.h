@@ -272,6 +272,40 @@ int  psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uin
 int  psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t n);
 int  psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m);
 
+/* --- full-membership strategy (partisan_full_membership_strategy.erl) --
+ * Nodes 0..n-1; node v's #full_v1{} membership (a state_orset,
+ * partisan_membership_set.erl:113-237) is two bitmaps over the cluster's
+ * token universe: known tokens and removed tokens (token v = v's own
+ * init/1 add; a self-leave allocates the next free token).  Schedule of a
+ * round: leave calls, then join calls (made since the previous round, in
+ * call order; RemoteState = the peer's state at the end of the previous
+ * round), then the inbox in (src, seq) order, then periodic/1 every
+ * `periodic_rounds` rounds.  n <= 2048, max_tokens <= 2048. */
+typedef struct psim_fm_stats {
+    uint64_t sent;                 /* {membership_strategy, {Spec, State}} emitted */
+    uint64_t processed;            /* handle_message/2 calls                      */
+    uint64_t merges;               /* merges by join/3 or handle_message/2        */
+    uint64_t updates;              /* membership changes (peer_service_events:update) */
+    uint64_t inflight;             /* messages the next round delivers            */
+    uint64_t member_sum;           /* sum over live nodes of |members|            */
+    uint64_t algo_bytes;           /* bytes the round's kernels must move */
+    double   kernel_ms;
+} psim_fm_stats;
+/* Replaces init/1 on n nodes (:70-74, new_state/1 :288-294). */
+int  psim_fm_setup(psim_handle* h, uint32_t n, uint32_t periodic_rounds, uint32_t max_tokens);
+int  psim_fm_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
+/* partisan_peer_service:join(Peer) at v[i] -> {connected, ...} -> join/3 (:85-96) */
+int  psim_fm_join(psim_handle* h, const uint32_t* v, const uint32_t* peer, size_t k);
+/* partisan_peer_service:leave(Leaving) at v[i] -> leave/2 (:177-214) */
+int  psim_fm_leave(psim_handle* h, const uint32_t* v, const uint32_t* leaving, size_t k);
+int  psim_fm_step(psim_handle* h, uint32_t rounds, psim_fm_stats* stats, size_t cap);
+/* known[n*words], removed[n*words] token bitmaps (words = ceil(max_tokens/64)), alive[n] */
+int  psim_fm_get_state(const psim_handle* h, uint64_t* known, uint64_t* removed, uint8_t* alive, size_t n,
+                       size_t words);
+/* token_node[t] = the node token t adds; *used = tokens allocated so far */
+int  psim_fm_tokens(const psim_handle* h, uint32_t* token_node, size_t ntok, uint32_t* used);
+int  psim_fm_inflight(const psim_handle* h, uint64_t* messages);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

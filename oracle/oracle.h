@@ -237,6 +237,41 @@ size_t orc_causal_buffered(const orc_causal* s, uint32_t v, uint32_t* k, uint32_
 uint64_t orc_causal_delivered(const orc_causal* s, uint32_t v);
 uint32_t orc_causal_emitter(const orc_causal* s, uint32_t k);
 
+/* ------------------------------------------------------------------ */
+/* OR-set (state_orset, types 0.1.8) behind partisan_membership_set, and */
+/* the full-membership strategy (src/partisan_full_membership_strategy.erl) */
+/* ------------------------------------------------------------------ */
+typedef struct orc_orset orc_orset;
+orc_orset* orc_orset_new(void);
+orc_orset* orc_orset_clone(const orc_orset* s);
+void orc_orset_free(orc_orset* s);
+int orc_orset_add(orc_orset* s, uint32_t elem, uint64_t token);
+int orc_orset_remove(orc_orset* s, uint32_t elem);          /* ORC_BADARG if absent */
+orc_orset* orc_orset_merge(const orc_orset* a, const orc_orset* b);
+int orc_orset_equal(const orc_orset* a, const orc_orset* b);
+size_t orc_orset_to_list(const orc_orset* s, uint32_t* out, size_t cap);
+size_t orc_orset_dump(const orc_orset* s, uint32_t* elem, uint64_t* tok, uint8_t* act, size_t cap);
+
+typedef struct orc_fm_stats {
+    uint64_t sent;               /* {membership_strategy, {Spec, State}} messages emitted */
+    uint64_t processed;          /* handle_message/2 calls */
+    uint64_t merges;             /* states changed by a merge (join or message) */
+    uint64_t updates;            /* membership changes (peer_service_events:update) */
+    uint64_t inflight;           /* messages delivered by the next round */
+    uint64_t member_sum;         /* sum over live vertices of |members| */
+} orc_fm_stats;
+typedef struct orc_fullmem orc_fullmem;
+orc_fullmem* orc_fm_create(uint32_t n, uint32_t periodic_rounds);
+void orc_fm_destroy(orc_fullmem* s);
+void orc_fm_set_alive(orc_fullmem* s, const uint8_t* alive);
+void orc_fm_join(orc_fullmem* s, uint32_t v, uint32_t peer);
+void orc_fm_leave(orc_fullmem* s, uint32_t v, uint32_t leaving);
+uint32_t orc_fm_step(orc_fullmem* s, uint32_t rounds, orc_fm_stats* st);
+size_t orc_fm_inflight(const orc_fullmem* s);
+size_t orc_fm_members(const orc_fullmem* s, uint32_t v, uint32_t* out, size_t cap);
+const orc_orset* orc_fm_state(const orc_fullmem* s, uint32_t v);
+int orc_fm_alive(const orc_fullmem* s, uint32_t v);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,13 @@ class CausalStats(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class FmStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("sent", "processed", "merges", "updates", "inflight", "member_sum")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 HV_DEFAULTS = dict(active_max_size=6, active_min_size=3, active_rwl=6, passive_max_size=30, passive_rwl=6,
                    shuffle_k_active=3, shuffle_k_passive=4, shuffle_rounds=10, promotion_rounds=5)
 
@@ -172,6 +179,33 @@ def lib():
         L.orc_causal_delivered.restype = C.c_uint64
         L.orc_causal_emitter.argtypes = [C.c_void_p, C.c_uint32]
         L.orc_causal_emitter.restype = C.c_uint32
+        L.orc_orset_new.restype = C.c_void_p
+        L.orc_orset_clone.argtypes = [C.c_void_p]
+        L.orc_orset_clone.restype = C.c_void_p
+        L.orc_orset_free.argtypes = [C.c_void_p]
+        L.orc_orset_add.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64]
+        L.orc_orset_remove.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_orset_merge.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_orset_merge.restype = C.c_void_p
+        L.orc_orset_equal.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_orset_to_list.argtypes = [C.c_void_p, P(C.c_uint32), sz]
+        L.orc_orset_to_list.restype = sz
+        L.orc_orset_dump.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint64), P(C.c_uint8), sz]
+        L.orc_orset_dump.restype = sz
+        L.orc_fm_create.argtypes = [C.c_uint32, C.c_uint32]
+        L.orc_fm_create.restype = C.c_void_p
+        L.orc_fm_destroy.argtypes = [C.c_void_p]
+        L.orc_fm_set_alive.argtypes = [C.c_void_p, P(C.c_uint8)]
+        L.orc_fm_join.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_fm_leave.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_fm_step.argtypes = [C.c_void_p, C.c_uint32, P(FmStats)]
+        L.orc_fm_inflight.argtypes = [C.c_void_p]
+        L.orc_fm_inflight.restype = sz
+        L.orc_fm_members.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), sz]
+        L.orc_fm_members.restype = sz
+        L.orc_fm_state.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_fm_state.restype = C.c_void_p
+        L.orc_fm_alive.argtypes = [C.c_void_p, C.c_uint32]
         _lib = L
     return _lib
 
@@ -584,3 +618,94 @@ class Causal:
 
     def emitter(self, k):
         return lib().orc_causal_emitter(self._h, k)
+
+
+# ---------------------------------------------------------------- OR-set / full membership
+class ORSet:
+    """state_orset (types 0.1.8) as partisan_membership_set wraps it; tokens
+    are supplied by the caller (unique ints)."""
+
+    def __init__(self, handle=None):
+        self._h = handle if handle is not None else lib().orc_orset_new()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_orset_free(self._h)
+            self._h = None
+
+    def add(self, elem, token):
+        c = ORSet(lib().orc_orset_clone(self._h))
+        lib().orc_orset_add(c._h, elem, token)
+        return c
+
+    def remove(self, elem):
+        c = ORSet(lib().orc_orset_clone(self._h))
+        if lib().orc_orset_remove(c._h, elem) < 0:
+            raise KeyError(f"precondition: {elem} not present")
+        return c
+
+    def merge(self, other):
+        return ORSet(lib().orc_orset_merge(self._h, other._h))
+
+    def equal(self, other):
+        return bool(lib().orc_orset_equal(self._h, other._h))
+
+    def to_list(self, cap=65536):
+        out = (C.c_uint32 * cap)()
+        k = lib().orc_orset_to_list(self._h, out, cap)
+        return list(out[:min(k, cap)])
+
+    def dump(self, cap=65536):
+        e, t, a = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_uint8 * cap)()
+        k = lib().orc_orset_dump(self._h, e, t, a, cap)
+        return [(e[i], t[i], bool(a[i])) for i in range(min(k, cap))]
+
+
+class FullMembership:
+    """Round-synchronous full-membership strategy (oracle/fullmem.c)."""
+
+    def __init__(self, n, periodic_rounds=0):
+        self.n = n
+        self._h = lib().orc_fm_create(n, periodic_rounds)
+
+    def close(self):
+        if self._h:
+            lib().orc_fm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        lib().orc_fm_set_alive(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def join(self, v, peer):
+        lib().orc_fm_join(self._h, v, peer)
+
+    def leave(self, v, leaving):
+        lib().orc_fm_leave(self._h, v, leaving)
+
+    def step(self, rounds=1):
+        st = (FmStats * rounds)()
+        lib().orc_fm_step(self._h, rounds, st)
+        return [x.as_dict() for x in st]
+
+    def inflight(self):
+        return lib().orc_fm_inflight(self._h)
+
+    def members(self, v, cap=65536):
+        out = (C.c_uint32 * cap)()
+        k = lib().orc_fm_members(self._h, v, out, cap)
+        return list(out[:min(k, cap)])
+
+    def alive(self, v):
+        return bool(lib().orc_fm_alive(self._h, v))
+
+    def payload(self, v):
+        """(elem, token, active) rows of node v's state_orset."""
+        h = lib().orc_fm_state(self._h, v)
+        cap = 65536
+        e, t, a = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_uint8 * cap)()
+        k = lib().orc_orset_dump(h, e, t, a, cap)
+        return [(e[i], t[i], bool(a[i])) for i in range(min(k, cap))]

@@ -83,6 +83,14 @@ class CausalStats(C.Structure):
         return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
 
 
+class FmStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("sent", "processed", "merges", "updates", "inflight", "member_sum",
+                                           "algo_bytes")] + [("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -134,6 +142,14 @@ SIGNATURES = {
                                            _P(C.c_size_t)]),
     "psim_causal_get_delivered": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_causal_emitters": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
+    "psim_fm_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "psim_fm_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
+    "psim_fm_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_fm_leave": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_fm_step": (C.c_int, [_H, C.c_uint32, _P(FmStats), C.c_size_t]),
+    "psim_fm_get_state": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint64), _P(C.c_uint8), C.c_size_t, C.c_size_t]),
+    "psim_fm_tokens": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t, _P(C.c_uint32)]),
+    "psim_fm_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

@@ -109,6 +109,8 @@ struct psim_handle {
         uint64_t round = 0;
     } hv;
 
+    psim::ModuleState* mods[psim::MOD_COUNT] = {};   // fullmem / scamp host state
+
     // causal delivery state (causal.hip)
     struct Cs {
         uint32_t n = 0, m = 0, period = 1, dmax = 1, redeliver = 1;
@@ -302,6 +304,32 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
 
 }  // namespace
 
+namespace psim {
+
+ModuleState*& handle_module(psim_handle* h, int slot) { return h->mods[slot]; }
+const ModuleState* handle_module(const psim_handle* h, int slot) { return h->mods[slot]; }
+hipStream_t handle_stream(const psim_handle* h) { return h->stream; }
+int handle_device(const psim_handle* h) { return h->device; }
+uint64_t handle_seed(const psim_handle* h) { return h->cfg.seed; }
+int handle_fail(psim_handle* h, int code, const char* fmt, ...) {
+    if (h) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return code;
+}
+void handle_add_round(psim_handle* h, double kernel_ms) {
+    h->kernel_ms_total += kernel_ms;
+    h->rounds_total++;
+}
+hipEvent_t handle_event(psim_handle* h, int i) { return h->ev[i]; }
+
+}  // namespace psim
+
 extern "C" {
 
 const char* psim_strerror(int code) {
@@ -368,6 +396,10 @@ int psim_destroy(psim_handle* h) {
     free_demers(h);
     free_hv(h);
     free_cs(h);
+    for (auto& m : h->mods) {
+        delete m;
+        m = nullptr;
+    }
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);

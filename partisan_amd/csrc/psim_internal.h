@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+typedef struct psim_handle psim_handle;
+
 namespace psim {
 
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
@@ -152,6 +154,53 @@ struct CsArgs {
 };
 hipError_t launch_cs_round(const CsArgs& a, hipStream_t s);
 hipError_t launch_cs_broadcast(const CsArgs& a, hipStream_t s);
+
+// Full-membership strategy over the state_orset membership set (fullmem.hip)
+constexpr uint32_t kFmMaxNW = 32;     // node bitmap words: <= 2048 nodes
+constexpr uint32_t kFmMaxW = 32;      // token bitmap words: <= 2048 tokens
+struct FmArgs {
+    uint32_t n, W, NW;                    // nodes, token words, node words
+    uint32_t S;                           // snapshots delivered this round
+    uint32_t pass;                        // 0: count emissions, 1: emit and store
+    uint32_t periodic;                    // periodic/1 fires at the end of this round
+    const uint32_t* __restrict__ elem;    // [64 W] node of each token
+    const unsigned long long* st_cur;     // [n][2W] {K words, R words} at the start of the round
+    unsigned long long* st_nxt;           // [n][2W] after the round
+    const uint8_t* __restrict__ alive0;   // [n] alive at the start of the round
+    uint8_t* __restrict__ alive_nxt;      // [n] after the round
+    const unsigned long long* __restrict__ alive0_bm;  // [NW]
+    const unsigned long long* __restrict__ snap_st;    // [S][2W] delivered states, (src, seq) order
+    const unsigned long long* __restrict__ snap_p;     // [S][NW] recipients
+    unsigned long long* __restrict__ out_st;           // emitted this round
+    unsigned long long* __restrict__ out_p;
+    uint32_t* __restrict__ out_src;
+    uint32_t* __restrict__ cnt;           // [n] emissions of each node (pass 0)
+    const uint32_t* __restrict__ base;    // [n+1] emission offsets (pass 1)
+    const uint32_t* __restrict__ jo;      // [n+1] join calls of each node
+    const uint32_t* __restrict__ jp;      //   peers, in call order
+    const uint32_t* __restrict__ lo;      // [n+1] leave calls of each node
+    const uint32_t* __restrict__ lw;      //   leaving node
+    const uint32_t* __restrict__ lt;      //   fresh token of a self-leave
+    unsigned long long* __restrict__ stats;   // [8] 0 sent 1 processed 2 merges 3 updates 4 inflight 5 member_sum
+};
+hipError_t launch_fm_round(const FmArgs& a, hipStream_t s);
+hipError_t launch_fm_scan(const uint32_t* cnt, uint32_t* base, uint32_t n, hipStream_t s);
+hipError_t launch_fm_alive_bm(const uint8_t* alive, uint32_t n, unsigned long long* bm, uint32_t nw, hipStream_t s);
+
+// Protocol modules that keep their host state outside psim_host.hip: the
+// handle owns one slot per module and deletes it on psim_destroy.
+struct ModuleState {
+    virtual ~ModuleState() {}
+};
+enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_COUNT = 4 };
+ModuleState*& handle_module(psim_handle* h, int slot);
+const ModuleState* handle_module(const psim_handle* h, int slot);
+hipStream_t handle_stream(const psim_handle* h);
+int handle_device(const psim_handle* h);
+uint64_t handle_seed(const psim_handle* h);
+int handle_fail(psim_handle* h, int code, const char* fmt, ...);
+void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing totals
+hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment

@@ -7,6 +7,7 @@ blocks (inputs and expected outputs only; no reference code is copied):
   * src/partisan_vclock.erl:206-257            -> vclock_kat.json
   * src/partisan_plumtree_util.erl:102-261     -> build_tree_kat.json
   * test/partisan_SUITE.erl:500-586 (causal_test scenario) -> causal_kat.json
+  * src/partisan_membership_set.erl:269-522   -> membership_set_kat.json
 
 Term encoding: an interval-set element N is the JSON int N and {H, T} is the
 list [H, T].  vclock actors are mapped to integers preserving Erlang term
@@ -244,9 +245,64 @@ causal = {
 }
 
 
+# partisan_membership_set eunit (:269-522) as op scripts over named states.
+# Elements are node_spec() maps, numbered in Erlang term order (maps compare
+# channels, then listen_addrs, then name; here the specs differ only by ip):
+#   1 = node1@127.0.0.1 ip {127,0,0,1}; 2 = node1@127.0.0.1 ip {192,168,0,1};
+#   11, 12, 13 = node1/2/3 with ips {192,168,0,1..3} (compare_test).
+# Actors a, b, c = 1, 2, 3.  Every add draws a fresh unique token (the
+# reference's tokens are random; no assertion depends on their values).
+#   ["new", X] | ["add", X, Elem, Actor, Y] (X = add(Elem, Actor, Y))
+#   ["remove", X, Elem, Actor, Y] | ["merge", X, Y, Z] (X = merge(Y, Z))
+#   ["alias", X, Y] | ["to_list", X, [Elems]] | ["same_term", X, Y]
+#   ["equal", Bool, X, Y] | ["compare", [List], X, [Joiners], [Leavers]]
+membership_set = {
+    "source": "src/partisan_membership_set.erl:269-522",
+    "tests": {
+        "add_remove_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["to_list", "A", [1]],
+                            ["remove", "A1", 1, 1, "A"], ["to_list", "A1", []]],
+        "one_side_updates_test": [["new", "A"], ["alias", "B", "A"], ["add", "A1", 1, 1, "A"],
+                                  ["to_list", "A1", [1]], ["merge", "M", "A1", "B"], ["to_list", "M", [1]]],
+        "concurrent_updates_test": [["new", "A"], ["alias", "B", "A"], ["add", "A1", 1, 1, "A"],
+                                    ["add", "B1", 2, 2, "B"], ["to_list", "A1", [1]], ["to_list", "B1", [2]],
+                                    ["merge", "M", "A1", "B1"], ["to_list", "M", [1, 2]]],
+        "compare_test": [["new", "S0"], ["add", "S1", 11, 1, "S0"], ["add", "S2", 12, 1, "S1"],
+                         ["compare", [], "S2", [], []], ["compare", [11, 12], "S2", [], []],
+                         ["compare", [11, 12, 13], "S2", [13], []], ["compare", [11, 13], "S2", [13], [12]]],
+        "concurrent_remove_update_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["remove", "A1", 1, 1, "A"],
+                                          ["alias", "B", "A"], ["add", "B1", 2, 2, "B"], ["to_list", "A", [1]],
+                                          ["to_list", "A1", []], ["to_list", "B1", [1, 2]],
+                                          ["merge", "M", "A1", "B1"], ["to_list", "M", [2]]],
+        "assoc_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["add", "B", 1, 2, "N"], ["remove", "B2", 1, 2, "B"],
+                       ["alias", "C", "A"], ["remove", "C3", 1, 3, "C"],
+                       ["merge", "L1", "B2", "C3"], ["merge", "L", "A", "L1"],
+                       ["merge", "R1", "A", "B2"], ["merge", "R", "R1", "C3"], ["same_term", "L", "R"],
+                       ["merge", "P1", "A", "C3"], ["merge", "P", "P1", "B2"],
+                       ["to_list", "P", None], ["same_list", "P", "R"], ["same_term", "P", "R"]],
+        "clock_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["alias", "B", "A"], ["add", "B2", 2, 2, "B"],
+                       ["remove", "A2", 1, 1, "A"], ["add", "A4", 2, 1, "A2"], ["merge", "AB", "A4", "B2"],
+                       ["to_list", "AB", [2]]],
+        "remfield_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["alias", "B", "A"], ["remove", "A2", 1, 1, "A"],
+                          ["add", "A4", 2, 1, "A2"], ["merge", "AB", "A4", "B"], ["to_list", "AB", [2]]],
+        "present_but_removed_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["alias", "C", "A"],
+                                     ["remove", "A2", 1, 1, "A"], ["add", "B", 2, 2, "N"],
+                                     ["merge", "A3", "B", "A2"], ["remove", "B2", 2, 2, "B"],
+                                     ["merge", "M1", "C", "A3"], ["merge", "M", "B2", "M1"], ["to_list", "M", []]],
+        "no_dots_left_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["add", "B", 2, 2, "N"], ["alias", "C", "A"],
+                              ["remove", "A2", 1, 1, "A"], ["merge", "A3", "A2", "B"], ["remove", "B2", 2, 2, "B"],
+                              ["merge", "B3", "B2", "C"], ["merge", "M1", "B3", "A3"], ["merge", "M", "C", "M1"],
+                              ["to_list", "M", []]],
+        "equals_test": [["new", "N"], ["add", "A", 1, 1, "N"], ["add", "B", 1, 2, "N"], ["equal", False, "A", "B"],
+                        ["merge", "C", "A", "B"], ["merge", "D", "B", "A"], ["equal", True, "C", "D"],
+                        ["equal", True, "A", "A"]],
+    },
+}
+
+
 def main():
     for name, obj in [("interval_sets_kat.json", interval_sets), ("vclock_kat.json", vclock),
-                      ("build_tree_kat.json", build_tree), ("causal_kat.json", causal)]:
+                      ("build_tree_kat.json", build_tree), ("causal_kat.json", causal),
+                      ("membership_set_kat.json", membership_set)]:
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")

@@ -1,0 +1,186 @@
+"""Full-membership strategy over the state_orset membership set.
+
+Oracle (CPU): the OR-set restatement is pinned by every eunit test of
+src/partisan_membership_set.erl:269-522 (tests/golden/membership_set_kat.json);
+the strategy round simulation (oracle/fullmem.c) is checked for the
+convergence the reference's connectivity_test expects
+(test/partisan_SUITE.erl:1296-1341: every node ends up knowing every node).
+
+GPU (-m gpu): csrc/fullmem.hip through the C ABI, bit-exact against the
+oracle round by round: per-round counters, every node's known/removed token
+bitmaps (= its state_orset payload) and liveness.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+
+def _kat(golden_dir):
+    with open(os.path.join(golden_dir, "membership_set_kat.json")) as f:
+        return json.load(f)
+
+
+def run_script(ops):
+    env, tok = {}, [0]
+
+    def fresh():
+        tok[0] += 1
+        return tok[0]
+
+    for op in ops:
+        k = op[0]
+        if k == "new":
+            env[op[1]] = O.ORSet()
+        elif k == "alias":
+            env[op[1]] = env[op[2]]
+        elif k == "add":
+            env[op[1]] = env[op[4]].add(op[2], fresh())
+        elif k == "remove":
+            env[op[1]] = env[op[4]].remove(op[2])
+        elif k == "merge":
+            env[op[1]] = env[op[2]].merge(env[op[3]])
+        elif k == "to_list":
+            if op[2] is not None:
+                assert env[op[1]].to_list() == op[2], op
+        elif k == "same_list":
+            assert env[op[1]].to_list() == env[op[2]].to_list(), op
+        elif k == "same_term":
+            assert env[op[1]].dump() == env[op[2]].dump(), op
+        elif k == "equal":
+            assert env[op[2]].equal(env[op[3]]) is op[1], op
+        elif k == "compare":
+            lst, members = set(op[1]), set(env[op[2]].to_list())
+            if lst:   # compare([], _) -> {[], []} (:151-152)
+                joiners, leavers = sorted(lst - members), sorted(members - lst)
+            else:
+                joiners, leavers = [], []
+            assert joiners == op[3] and leavers == op[4], op
+        else:
+            raise ValueError(op)
+    return env
+
+
+@pytest.mark.parametrize("name", sorted(json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                                                      "membership_set_kat.json")))["tests"]))
+def test_membership_set_kat(golden_dir, name):
+    run_script(_kat(golden_dir)["tests"][name])
+
+
+def test_orset_remove_absent_is_precondition_error():
+    with pytest.raises(KeyError):
+        O.ORSet().remove(7)
+
+
+def cluster_joins(f, n):
+    """partisan_support:cluster/4: every node joins every other node."""
+    for v in range(n):
+        for u in range(n):
+            if u != v:
+                f.join(v, u)
+
+
+def test_c1_full_membership_converges():
+    n = 16
+    f = O.FullMembership(n, periodic_rounds=10)
+    cluster_joins(f, n)
+    st = f.step(12)
+    assert all(f.members(v) == list(range(n)) for v in range(n))
+    assert st[-1]["member_sum"] == n * n
+    # converged: after the join waves only periodic gossip remains, all equal
+    assert st[3]["sent"] == 0 and st[9]["sent"] == n * (n - 1) and st[10]["merges"] == 0
+
+
+def test_leave_removes_and_stops_the_leaver():
+    n = 8
+    f = O.FullMembership(n, periodic_rounds=0)
+    cluster_joins(f, n)
+    f.step(4)
+    f.leave(0, 5)                    # node 0 removes node 5; 5 learns it and stops (:1791-1803)
+    f.step(4)
+    assert not f.alive(5)
+    for v in range(n):
+        if v != 5:
+            assert f.members(v) == [u for u in range(n) if u != 5]
+
+
+# ------------------------------------------------------------------ GPU parity
+def oracle_bitmaps(f, n, words):
+    K = np.zeros((n, words), np.uint64)
+    R = np.zeros((n, words), np.uint64)
+    for v in range(n):
+        for _, t, act in f.payload(v):
+            K[v, t >> 6] |= np.uint64(1 << (t & 63))
+            if not act:
+                R[v, t >> 6] |= np.uint64(1 << (t & 63))
+    return K, R
+
+
+def check_round(g, f, n):
+    K, R, alive = g.state()
+    oK, oR = oracle_bitmaps(f, n, g.words)
+    assert np.array_equal(alive.astype(bool), np.array([f.alive(v) for v in range(n)]))
+    assert np.array_equal(K, oK) and np.array_equal(R, oR)
+
+
+def _drive(n, periodic, script, rounds):
+    import partisan_amd as pa
+    sim = pa.Simulator(device=0)
+    g = pa.fullmem.FullMembershipCluster(sim, n, periodic_rounds=periodic, max_tokens=n + 64)
+    f = O.FullMembership(n, periodic_rounds=periodic)
+    for r in range(rounds):
+        for kind, a, b in script.get(r, []):
+            if kind == "join":
+                g.join([a], [b]); f.join(a, b)
+            elif kind == "leave":
+                g.leave([a], [b]); f.leave(a, b)
+            elif kind == "alive":
+                g.set_alive(a); f.set_alive(a)
+        gs = g.step(1)[0]
+        os_ = f.step(1)[0]
+        for k in os_:
+            assert gs[k] == os_[k], (r, k, gs, os_)
+        check_round(g, f, n)
+    return g, f
+
+
+@pytest.mark.gpu
+def test_gpu_c1_parity():
+    n = 16
+    script = {0: [("join", v, u) for v in range(n) for u in range(n) if u != v]}
+    g, f = _drive(n, 5, script, 14)
+    assert all(g.members(v) == list(range(n)) for v in range(n))
+
+
+@pytest.mark.gpu
+def test_gpu_random_joins_leaves_failures_parity():
+    n = 150
+    rng = np.random.default_rng(7)
+    script = {}
+    for r in range(30):
+        ev = []
+        for _ in range(rng.integers(0, 12)):
+            ev.append(("join", int(rng.integers(n)), int(rng.integers(n))))
+        if r in (12, 20):
+            ev.append(("leave", int(rng.integers(n)), int(rng.integers(n))))
+        if r == 16:
+            v = int(rng.integers(n))
+            ev.append(("leave", v, v))             # self-leave: new_state with a fresh token
+        if r == 18:
+            a = np.ones(n, np.uint8)
+            a[rng.choice(n, 10, replace=False)] = 0
+            ev.append(("alive", a, None))
+        script[r] = ev
+    _drive(n, 4, script, 36)
+
+
+@pytest.mark.gpu
+def test_gpu_two_words_of_nodes():
+    """n > 64: node and token bitmaps span several words."""
+    n = 130
+    script = {0: [("join", v, (v * 7 + 3) % n) for v in range(n)],
+              3: [("join", v, (v * 11 + 1) % n) for v in range(n)]}
+    _drive(n, 3, script, 12)
