@@ -306,6 +306,49 @@ int  psim_fm_get_state(const psim_handle* h, uint64_t* known, uint64_t* removed,
 int  psim_fm_tokens(const psim_handle* h, uint32_t* token_node, size_t ntok, uint32_t* used);
 int  psim_fm_inflight(const psim_handle* h, uint64_t* messages);
 
+/* --- SCAMP membership (partisan_scamp_v{1,2}_membership_strategy.erl) ----
+ * Nodes 0..n-1 run the strategy inside the pluggable peer service manager.
+ * Round: leave calls, then join calls made since the last round (call
+ * order), then the inbox in (src, seq) order with the manager's stop check,
+ * then periodic/1 every `periodic_rounds`.  A handler at u reaches t iff
+ * t != u, t was up at the start of the round and t is one of u's members
+ * before or after the handler (DESIGN.md "SCAMP").  Views are rows of
+ * PSIM_SCAMP_PV_CAP / PSIM_SCAMP_IV_CAP ids in the reference's list order;
+ * overflowing one is PSIM_EOVERFLOW.  Draws: Philox stream (seed, v, kind 5,
+ * incarnation). */
+#define PSIM_SCAMP_PV_CAP 128
+#define PSIM_SCAMP_IV_CAP 64
+typedef struct psim_scamp_stats {
+    uint64_t sent[7];              /* [k] queued messages of kind k: 1 forward_subscription, 2 keep_subscription,
+                                      3 ping, 4 remove_subscription, 5 replace_subscription,
+                                      6 bootstrap_remove_subscription                          */
+    uint64_t dropped;              /* emitted to self, a dead or a non-connected node          */
+    uint64_t processed;            /* handle_message/2 calls                                   */
+    uint64_t draws;                /* rand draws                                               */
+    uint64_t stopped;              /* managers that stopped this round                         */
+    uint64_t error;                /* bit2: v2 bootstrap_remove lists:nth crash (Q18), bit3: v1 Q17 */
+    uint64_t pv_sum;               /* sum over live nodes of |partial view| (self included)    */
+    uint64_t inview_sum;           /* sum of |in-view|                                          */
+    uint64_t resub;                /* isolated periodic re-subscriptions (Q19)                 */
+    uint64_t algo_bytes;           /* bytes the round's kernels must move          */
+    double   kernel_ms;
+} psim_scamp_stats;
+/* init/1 on n nodes (v2 :75-85, v1 :56-66); version 1 or 2; c = scamp_c (SCAMP_C_VALUE 5) */
+int  psim_scamp_setup(psim_handle* h, uint32_t n, uint32_t version, uint32_t c, uint32_t periodic_rounds);
+int  psim_scamp_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
+/* partisan_peer_service:join(Contact) at v[i] -> {connected, ...} -> join/3 */
+int  psim_scamp_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k);
+/* partisan_peer_service:leave(Node) at v[i] -> leave/2 */
+int  psim_scamp_leave(psim_handle* h, const uint32_t* v, const uint32_t* node, size_t k);
+/* v[i] crash and restart now: init/1 state, new incarnation, in-flight messages to them lost */
+int  psim_scamp_crash(psim_handle* h, const uint32_t* v, size_t k);
+int  psim_scamp_step(psim_handle* h, uint32_t rounds, psim_scamp_stats* stats, size_t cap);
+/* pv[n*PSIM_SCAMP_PV_CAP], iv[n*PSIM_SCAMP_IV_CAP] in list order, npv/niv = lengths; any may be NULL */
+int  psim_scamp_get_views(const psim_handle* h, uint32_t* pv, uint32_t* npv, uint32_t* iv, uint32_t* niv, size_t n);
+/* draws of the current incarnation, round of the last ping handled (-1 none), alive */
+int  psim_scamp_get_nodes(const psim_handle* h, uint64_t* draws, int32_t* last_ping, uint8_t* alive, size_t n);
+int  psim_scamp_inflight(const psim_handle* h, uint64_t* messages);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

@@ -272,6 +272,36 @@ size_t orc_fm_members(const orc_fullmem* s, uint32_t v, uint32_t* out, size_t ca
 const orc_orset* orc_fm_state(const orc_fullmem* s, uint32_t v);
 int orc_fm_alive(const orc_fullmem* s, uint32_t v);
 
+/* ------------------------------------------------------------------ */
+/* SCAMP v1 / v2 membership strategies (partisan_scamp_v{1,2}_membership_strategy.erl) */
+/* ------------------------------------------------------------------ */
+typedef struct orc_scamp_stats {
+    uint64_t sent[7];            /* [k]: delivered-to-queue messages of kind k: 1 forward_subscription,
+                                    2 keep_subscription, 3 ping, 4 remove_subscription,
+                                    5 replace_subscription, 6 bootstrap_remove_subscription */
+    uint64_t dropped;            /* emitted to self / a non-connected / dead node */
+    uint64_t processed;          /* handle_message/2 calls */
+    uint64_t draws;              /* rand draws */
+    uint64_t stopped;            /* managers that stopped (members lost self, or a reference crash point) */
+    uint64_t error;              /* bit2: v2 bootstrap_remove lists:nth crash (Q18); bit3: v1 Q17 */
+    uint64_t pv_sum;             /* sum over live vertices of |partial view| */
+    uint64_t inview_sum;         /* sum of |in-view| (v2) */
+    uint64_t resub;              /* isolated periodic re-subscriptions */
+} orc_scamp_stats;
+typedef struct orc_scamp orc_scamp;
+orc_scamp* orc_scamp_create(uint32_t n, uint32_t version, uint32_t c, uint32_t periodic_rounds, uint64_t seed);
+void orc_scamp_destroy(orc_scamp* s);
+void orc_scamp_set_alive(orc_scamp* s, const uint8_t* alive);
+void orc_scamp_join(orc_scamp* s, uint32_t v, uint32_t contact);
+void orc_scamp_leave(orc_scamp* s, uint32_t v, uint32_t node);
+void orc_scamp_crash(orc_scamp* s, uint32_t v);
+uint32_t orc_scamp_step(orc_scamp* s, uint32_t rounds, orc_scamp_stats* st);
+size_t orc_scamp_inflight(const orc_scamp* s);
+size_t orc_scamp_view(const orc_scamp* s, uint32_t v, int which, uint32_t* out, size_t cap);
+uint64_t orc_scamp_draws(const orc_scamp* s, uint32_t v);
+int orc_scamp_alive(const orc_scamp* s, uint32_t v);
+int64_t orc_scamp_last_ping(const orc_scamp* s, uint32_t v);
+
 #ifdef __cplusplus
 }
 #endif

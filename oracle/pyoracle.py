@@ -67,6 +67,16 @@ class FmStats(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class ScampStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 7)] + [(k, C.c_uint64) for k in (
+        "dropped", "processed", "draws", "stopped", "error", "pv_sum", "inview_sum", "resub")]
+
+    def as_dict(self):
+        d = {"sent": [int(x) for x in self.sent[1:7]]}
+        d.update({k: int(getattr(self, k)) for k, _ in self._fields_[1:]})
+        return d
+
+
 HV_DEFAULTS = dict(active_max_size=6, active_min_size=3, active_rwl=6, passive_max_size=30, passive_rwl=6,
                    shuffle_k_active=3, shuffle_k_passive=4, shuffle_rounds=10, promotion_rounds=5)
 
@@ -206,6 +216,23 @@ def lib():
         L.orc_fm_state.argtypes = [C.c_void_p, C.c_uint32]
         L.orc_fm_state.restype = C.c_void_p
         L.orc_fm_alive.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_scamp_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.orc_scamp_create.restype = C.c_void_p
+        L.orc_scamp_destroy.argtypes = [C.c_void_p]
+        L.orc_scamp_set_alive.argtypes = [C.c_void_p, P(C.c_uint8)]
+        L.orc_scamp_join.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_scamp_leave.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_scamp_crash.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_scamp_step.argtypes = [C.c_void_p, C.c_uint32, P(ScampStats)]
+        L.orc_scamp_inflight.argtypes = [C.c_void_p]
+        L.orc_scamp_inflight.restype = sz
+        L.orc_scamp_view.argtypes = [C.c_void_p, C.c_uint32, C.c_int, P(C.c_uint32), sz]
+        L.orc_scamp_view.restype = sz
+        L.orc_scamp_draws.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_scamp_draws.restype = C.c_uint64
+        L.orc_scamp_alive.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_scamp_last_ping.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_scamp_last_ping.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -709,3 +736,57 @@ class FullMembership:
         e, t, a = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_uint8 * cap)()
         k = lib().orc_orset_dump(h, e, t, a, cap)
         return [(e[i], t[i], bool(a[i])) for i in range(min(k, cap))]
+
+
+# ---------------------------------------------------------------- SCAMP
+class Scamp:
+    """Round-synchronous SCAMP v1/v2 membership (oracle/scamp.c)."""
+
+    def __init__(self, n, version=2, c=5, periodic_rounds=10, seed=0):
+        self.n = n
+        self._h = lib().orc_scamp_create(n, version, c, periodic_rounds, seed)
+        if not self._h:
+            raise ValueError("bad scamp config")
+
+    def close(self):
+        if self._h:
+            lib().orc_scamp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        lib().orc_scamp_set_alive(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def join(self, v, contact):
+        lib().orc_scamp_join(self._h, v, contact)
+
+    def leave(self, v, node):
+        lib().orc_scamp_leave(self._h, v, node)
+
+    def crash(self, v):
+        lib().orc_scamp_crash(self._h, v)
+
+    def step(self, rounds=1):
+        st = (ScampStats * rounds)()
+        lib().orc_scamp_step(self._h, rounds, st)
+        return [x.as_dict() for x in st]
+
+    def inflight(self):
+        return lib().orc_scamp_inflight(self._h)
+
+    def view(self, v, which=0, cap=4096):
+        out = (C.c_uint32 * cap)()
+        k = lib().orc_scamp_view(self._h, v, which, out, cap)
+        return list(out[:min(k, cap)])
+
+    def draws(self, v):
+        return lib().orc_scamp_draws(self._h, v)
+
+    def alive(self, v):
+        return bool(lib().orc_scamp_alive(self._h, v))
+
+    def last_ping(self, v):
+        return lib().orc_scamp_last_ping(self._h, v)

@@ -91,6 +91,22 @@ class FmStats(C.Structure):
         return {k: (float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))) for k, _ in self._fields_}
 
 
+SCAMP_MSG_KINDS = {1: "forward_subscription", 2: "keep_subscription", 3: "ping", 4: "remove_subscription",
+                   5: "replace_subscription", 6: "bootstrap_remove_subscription"}
+
+
+class ScampStats(C.Structure):
+    _fields_ = [("sent", C.c_uint64 * 7)] + [(k, C.c_uint64) for k in (
+        "dropped", "processed", "draws", "stopped", "error", "pv_sum", "inview_sum", "resub", "algo_bytes")] + \
+        [("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        d = {"sent": [int(x) for x in self.sent[1:7]]}
+        for k, _ in self._fields_[1:]:
+            d[k] = float(getattr(self, k)) if k == "kernel_ms" else int(getattr(self, k))
+        return d
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -150,6 +166,16 @@ SIGNATURES = {
     "psim_fm_get_state": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint64), _P(C.c_uint8), C.c_size_t, C.c_size_t]),
     "psim_fm_tokens": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t, _P(C.c_uint32)]),
     "psim_fm_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_scamp_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "psim_scamp_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
+    "psim_scamp_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_scamp_leave": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_scamp_crash": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
+    "psim_scamp_step": (C.c_int, [_H, C.c_uint32, _P(ScampStats), C.c_size_t]),
+    "psim_scamp_get_views": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),
+                                       C.c_size_t]),
+    "psim_scamp_get_nodes": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_int32), _P(C.c_uint8), C.c_size_t]),
+    "psim_scamp_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

@@ -187,6 +187,41 @@ hipError_t launch_fm_round(const FmArgs& a, hipStream_t s);
 hipError_t launch_fm_scan(const uint32_t* cnt, uint32_t* base, uint32_t n, hipStream_t s);
 hipError_t launch_fm_alive_bm(const uint8_t* alive, uint32_t n, unsigned long long* bm, uint32_t nw, hipStream_t s);
 
+// SCAMP v1 / v2 membership strategies (scamp.hip)
+constexpr uint32_t kScPv = 128;       // partial view capacity per vertex
+constexpr uint32_t kScIv = 64;        // in-view capacity per vertex
+struct ScMsg {                        // one 24-byte record
+    uint32_t type, src, dst, seq;     // seq: emission index at src (schedule order key)
+    uint32_t a, b;                    // node / replacement
+};
+struct ScHead {
+    uint32_t npv, niv;
+    uint32_t draws, inc;              // Philox counter {v, draws, KIND_SCAMP, inc}
+    uint32_t seq;
+    int32_t last_ping;                // round of the last ping handled, -1 = undefined
+    uint32_t fresh, _pad;             // restarted since the last round
+};
+struct ScArgs {
+    uint32_t n, ver, c, round, periodic;
+    uint2 key;
+    const uint8_t* __restrict__ alive0;   // [n] up at the start of the round
+    uint8_t* __restrict__ alive;          // [n] cleared when a manager stops
+    ScHead* __restrict__ head;
+    uint32_t* __restrict__ pv;            // [n][kScPv]
+    uint32_t* __restrict__ iv;            // [n][kScIv]
+    const ScMsg* __restrict__ in;
+    const uint32_t* nin;
+    ScMsg* __restrict__ out;
+    uint32_t* nout;
+    uint32_t out_cap;
+    uint32_t *cnt, *cur, *off, *idx, *bsum;
+    const uint32_t* __restrict__ call_off;    // [n+1] calls of each vertex
+    const uint32_t* __restrict__ calls;       // bit31 = leave, low bits = node / contact
+    unsigned long long* __restrict__ stats;   // [16]
+};
+hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
+hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
+
 // Protocol modules that keep their host state outside psim_host.hip: the
 // handle owns one slot per module and deletes it on psim_destroy.
 struct ModuleState {

@@ -1,0 +1,695 @@
+// scamp.hip -- SCAMP v1 / v2 membership strategies
+// (src/partisan_scamp_v{1,2}_membership_strategy.erl) as run by the
+// pluggable peer service manager, one gfx950 thread per vertex and round.
+//
+// Same round shape as the HyParView engine: fixed 24-byte message records
+// in an HBM queue, bucketed by destination (count, 3-phase scan, scatter),
+// then one thread per vertex sorts its bucket by (src, emission seq) -- the
+// schedule's order, so the atomicAdd slot a message landed in never
+// matters -- and runs, in order: the leave and join calls made since the
+// last round, the handle_message/2 clauses with the manager's stop check,
+// and periodic/1.  Views live in HBM as fixed-capacity rows (partial view
+// kScPv ids, in-view kScIv ids) in the reference's list order (v2: prepend;
+// v1: sets in id order, Q28) and are edited in place.
+//
+// The connection rule of DESIGN.md "SCAMP" (a handler at u reaches t iff
+// t != u, t was up at the start of the round and t is a member before or
+// after the handler) is evaluated against the live row: every handler's
+// membership change is a single add (join, keep), a map (replace) or a
+// single removal (v1 leave, v2 remove -- `extra` re-admits the removed
+// node), and bootstrap_remove sends before it clears the row.
+#include "psim_internal.h"
+#include "philox.h"
+#include "../../include/psim.h"
+
+namespace psim {
+
+namespace {
+
+enum { SC_FWD = 1, SC_KEEP, SC_PING, SC_REMOVE, SC_REPLACE, SC_BOOT };
+constexpr uint32_t kScStrideBlocks = 2048;
+constexpr uint32_t kScMaxSel = 16;   // select_random_sublist sizes (c, c - 1)
+
+struct Ctx {
+    const ScArgs* a;
+    uint32_t v;
+    ScHead h;
+    uint32_t* pv;      // row in HBM
+    uint32_t* iv;
+    uint32_t sent[7];
+    uint32_t dropped, ndraw, err, resub;
+};
+
+__device__ uint64_t draw64(Ctx& c) {
+    const uint4 r = philox4x32_10(make_uint4(c.v, c.h.draws, KIND_SCAMP, c.h.inc), c.a->key);
+    c.h.draws++;
+    c.ndraw++;
+    return (uint64_t)r.x | ((uint64_t)r.y << 32);
+}
+
+__device__ __forceinline__ bool in_pv(const Ctx& c, uint32_t t) {
+    for (uint32_t i = 0; i < c.h.npv; i++)
+        if (c.pv[i] == t) return true;
+    return false;
+}
+
+// select_random_sublist(L, K) = lists:sublist(shuffle(L), K): one uniform()
+// per element in list order, then the K smallest (r >> 11, N) in order
+__device__ uint32_t select_sublist(Ctx& c, uint32_t k, uint32_t* out) {
+    const uint32_t m = c.h.npv;
+    unsigned long long key[kScMaxSel];
+    uint32_t val[kScMaxSel];
+    uint32_t got = 0;
+    for (uint32_t i = 0; i < m; i++) {
+        const unsigned long long r = draw64(c) >> 11;
+        const uint32_t e = c.pv[i];
+        // insert (r, e) into the sorted top-k
+        uint32_t j = got < k ? got : k;
+        if (j == k && !(r < key[k - 1] || (r == key[k - 1] && e < val[k - 1]))) continue;
+        if (j == k) j = k - 1;
+        while (j > 0 && (r < key[j - 1] || (r == key[j - 1] && e < val[j - 1]))) {
+            key[j] = key[j - 1];
+            val[j] = val[j - 1];
+            j--;
+        }
+        key[j] = r;
+        val[j] = e;
+        if (got < k) got++;
+    }
+    for (uint32_t i = 0; i < got; i++) out[i] = val[i];
+    return got;
+}
+
+__device__ void emit(Ctx& c, uint32_t t, uint32_t type, uint32_t x, uint32_t y, uint32_t extra) {
+    const ScArgs& a = *c.a;
+    const bool conn = t != c.v && a.alive0[t] && (t == extra || in_pv(c, t));
+    if (!conn) { c.dropped++; return; }
+    const uint32_t pos = atomicAdd(a.nout, 1u);
+    c.sent[type]++;
+    if (pos >= a.out_cap) { c.err |= 1u; return; }
+    ScMsg m;
+    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.a = x; m.b = y;
+    a.out[pos] = m;
+}
+
+__device__ void pv_push_front(Ctx& c, uint32_t x) {
+    if (c.h.npv >= kScPv) { c.err |= 2u; return; }
+    for (uint32_t i = c.h.npv; i > 0; i--) c.pv[i] = c.pv[i - 1];
+    c.pv[0] = x;
+    c.h.npv++;
+}
+__device__ void pv_set_add(Ctx& c, uint32_t x) {     // v1: sets, id order
+    if (in_pv(c, x)) return;
+    if (c.h.npv >= kScPv) { c.err |= 2u; return; }
+    uint32_t i = c.h.npv;
+    while (i > 0 && c.pv[i - 1] > x) { c.pv[i] = c.pv[i - 1]; i--; }
+    c.pv[i] = x;
+    c.h.npv++;
+}
+__device__ void pv_del_first(Ctx& c, uint32_t x) {
+    for (uint32_t i = 0; i < c.h.npv; i++)
+        if (c.pv[i] == x) {
+            for (uint32_t j = i + 1; j < c.h.npv; j++) c.pv[j - 1] = c.pv[j];
+            c.h.npv--;
+            return;
+        }
+}
+
+// join/3 (v2 :89-137, v1 :69-119)
+__device__ void do_join(Ctx& c, uint32_t node) {
+    const uint32_t k = c.a->ver == 2 ? c.a->c - 1 : c.a->c;   // Q15
+    uint32_t sel[kScMaxSel];
+    const uint32_t ns = select_sublist(c, k, sel);            // over the members before the add
+    const uint32_t n0 = c.h.npv;
+    if (c.a->ver == 2) pv_push_front(c, node);
+    else pv_set_add(c, node);
+    emit(c, node, SC_FWD, c.v, 0, node);                      // forward_subscription(Myself)
+    // to each member known before (v2: list order; v1: sets:fold = id order):
+    // v2 prepended one element, v1 inserted `node` unless present
+    for (uint32_t i = 0; i < c.h.npv; i++) {
+        const uint32_t t = c.pv[i];
+        if (c.a->ver == 2) { if (i == 0) continue; }
+        else if (t == node && c.h.npv != n0) continue;
+        emit(c, t, SC_FWD, node, 0, node);
+    }
+    for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, node);
+}
+
+// leave/2 (v2 :140-146, v1 :122-142)
+__device__ void do_leave(Ctx& c, uint32_t node) {
+    if (c.a->ver == 2) {
+        for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_BOOT, node, 0, 0xFFFFFFFFu);
+        return;
+    }
+    // members(State0) in id order, `node` deleted from the set first
+    const bool had = in_pv(c, node);
+    uint32_t snap[kScPv];
+    const uint32_t n0 = c.h.npv;
+    for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
+    if (had) pv_del_first(c, node);
+    for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu);
+}
+
+// periodic/1 (v2 :180-221, v1 :174-216); isolation per Q19
+__device__ void do_periodic(Ctx& c) {
+    const bool isolated = c.h.last_ping >= 0 && (uint32_t)c.h.last_ping < c.a->round;
+    if (isolated) {
+        uint32_t sel[1];
+        const uint32_t ns = select_sublist(c, 1, sel);
+        c.resub++;
+        for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, c.v, 0, 0xFFFFFFFFu);
+    }
+    for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_PING, c.v, 0, 0xFFFFFFFFu);
+}
+
+// handle_message/2; returns false when the manager stops (:1791-1803)
+__device__ bool do_message(Ctx& c, const ScMsg& m) {
+    const ScArgs& a = *c.a;
+    switch (m.type) {
+    case SC_PING:                                             // v2 :224-229, v1 :219-227
+        c.h.last_ping = (int32_t)a.round;
+        break;
+    case SC_FWD: {                                            // v2 :313-341, v1 :264-297
+        const uint32_t node = m.a;
+        const uint32_t r10 = 1u + (uint32_t)__umul64hi(draw64(c), 10ull);   // random_0_or_1: uniform(10) >= 5
+        const bool keep = r10 < 5 && !in_pv(c, node);
+        if (keep) {
+            if (a.ver == 2) {
+                pv_push_front(c, node);
+                emit(c, node, SC_KEEP, c.v, 0, node);
+            } else {
+                pv_set_add(c, node);
+            }
+        } else {
+            uint32_t sel[1];
+            const uint32_t ns = select_sublist(c, 1, sel);
+            for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, 0xFFFFFFFFu);
+        }
+        break;
+    }
+    case SC_KEEP:                                             // v2 :342-347
+        if (c.h.niv >= kScIv) { c.err |= 2u; break; }
+        for (uint32_t i = c.h.niv; i > 0; i--) c.iv[i] = c.iv[i - 1];
+        c.iv[0] = m.a;
+        c.h.niv++;
+        break;
+    case SC_REMOVE: {                                         // v2 :295-312, v1 :230-262
+        const uint32_t node = m.a;
+        if (!in_pv(c, node)) break;
+        if (a.ver == 1) { c.err |= 8u; return false; }       // Q17: the manager stops
+        uint32_t snap[kScPv];
+        const uint32_t n0 = c.h.npv;
+        for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
+        pv_del_first(c, node);
+        for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, node);
+        break;
+    }
+    case SC_REPLACE:                                          // v2 :275-294
+        for (uint32_t i = 0; i < c.h.npv; i++)
+            if (c.pv[i] == m.a) c.pv[i] = m.b;
+        break;
+    case SC_BOOT: {                                           // v2 :230-274
+        if (m.a != c.v) break;
+        const int32_t L = (int32_t)c.h.niv, P = (int32_t)c.h.npv;
+        const int32_t num = L - (int32_t)(a.c - 1), rem = L - num;
+        bool crash = false;                                   // lists:nth/2 out of range (Q18)
+        if (num > 0)
+            for (int32_t N = 1; N <= num && !crash; N++)
+                if (P == 0 || N / P < 1 || N / P > P) crash = true;
+        if (!crash && rem > L) crash = true;
+        if (crash) { c.err |= 4u; return false; }
+        if (num > 0)
+            for (int32_t N = 1; N <= num; N++) emit(c, c.iv[N - 1], SC_REPLACE, c.v, c.pv[N / P - 1], 0xFFFFFFFFu);
+        if (rem > 0)
+            for (int32_t N = 1; N <= rem; N++) emit(c, c.iv[N - 1], SC_REMOVE, c.v, 0, 0xFFFFFFFFu);
+        c.h.npv = 0;
+        c.h.niv = 0;
+        break;
+    }
+    default:
+        break;
+    }
+    return in_pv(c, c.v);
+}
+
+__device__ __forceinline__ bool msg_less(const ScMsg& x, const ScMsg& y) {
+    return x.src < y.src || (x.src == y.src && x.seq < y.seq);
+}
+
+__device__ __forceinline__ uint32_t n_in(const ScArgs& a) { return *a.nin < a.out_cap ? *a.nin : a.out_cap; }
+
+__global__ __launch_bounds__(kBlock) void sc_count(ScArgs a) {
+    const uint32_t k = n_in(a);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kScStrideBlocks * kBlock)
+        atomicAdd(&a.cnt[a.in[i].dst], 1u);
+}
+__global__ __launch_bounds__(kBlock) void sc_scan_blocks(ScArgs a) {
+    __shared__ uint32_t ws[kBlock / 64];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t x0 = i < a.n ? a.cnt[i] : 0u;
+    uint32_t x = x0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wv; w++) pre += ws[w];
+    if (i < a.n) a.off[i] = pre + x - x0;
+    if (threadIdx.x == kBlock - 1) a.bsum[blockIdx.x] = pre + x;
+}
+__global__ __launch_bounds__(1024) void sc_scan_sums(ScArgs a, uint32_t nb) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024;
+    const uint32_t lo = t * per, hi = min(nb, lo + per);
+    uint32_t s = 0;
+    for (uint32_t b = lo; b < hi; b++) s += a.bsum[b];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t y = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += y;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (uint32_t b = lo; b < hi; b++) { const uint32_t x = a.bsum[b]; a.bsum[b] = run; run += x; }
+    if (t == 1023) a.off[a.n] = part[1023];
+}
+__global__ __launch_bounds__(kBlock) void sc_scan_add(ScArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < a.n) a.off[i] += a.bsum[blockIdx.x];
+}
+__global__ __launch_bounds__(kBlock) void sc_scatter(ScArgs a) {
+    const uint32_t k = n_in(a);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kScStrideBlocks * kBlock) {
+        const uint32_t d = a.in[i].dst;
+        a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
+    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t sent[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t dropped = 0, ndraw = 0, err = 0, resub = 0, nproc = 0, stopped = 0, npv = 0, niv = 0;
+    if (v < a.n && !a.alive0[v] && a.head[v].fresh) a.head[v].fresh = 0;
+    if (v < a.n && a.alive0[v]) {
+        Ctx c;
+        c.a = &a;
+        c.v = v;
+        c.h = a.head[v];
+        c.pv = a.pv + (size_t)v * kScPv;
+        c.iv = a.iv + (size_t)v * kScIv;
+        for (int i = 0; i < 7; i++) c.sent[i] = 0;
+        c.dropped = c.ndraw = c.err = c.resub = 0;
+        const bool fresh = c.h.fresh != 0;
+        c.h.fresh = 0;
+        bool up = true;
+        // leave calls, then join calls (made since the last round, in call order)
+        for (uint32_t i = a.call_off[v]; i < a.call_off[v + 1]; i++) {
+            const uint32_t x = a.calls[i];
+            if (x >> 31) do_leave(c, x & 0x7FFFFFFFu);
+            else if (x != v && a.alive0[x]) do_join(c, x);   // connect/1 succeeds iff the peer is up
+        }
+        // inbox in (src, seq) order; a restarted vertex drops what was sent to its old incarnation
+        const uint32_t lo = a.off[v], hi = a.off[v + 1];
+        if (!fresh && hi > lo) {
+            for (uint32_t i = lo + 1; i < hi; i++) {
+                const uint32_t x = a.idx[i];
+                const ScMsg mx = a.in[x];
+                uint32_t j = i;
+                while (j > lo && msg_less(mx, a.in[a.idx[j - 1]])) { a.idx[j] = a.idx[j - 1]; j--; }
+                a.idx[j] = x;
+            }
+            for (uint32_t i = lo; i < hi && up; i++) {
+                nproc++;
+                if (!do_message(c, a.in[a.idx[i]])) up = false;
+            }
+        }
+        if (up && a.periodic) do_periodic(c);
+        if (!up) {
+            a.alive[v] = 0;
+            stopped = 1;
+        } else {
+            npv = c.h.npv;
+            niv = c.h.niv;
+        }
+        a.head[v] = c.h;
+        for (int i = 0; i < 7; i++) sent[i] = c.sent[i];
+        dropped = c.dropped; ndraw = c.ndraw; err = c.err; resub = c.resub;
+    }
+    // counters: [1..6] sent by kind, 7 dropped, 8 processed, 9 draws, 10 stopped,
+    // 11 error bits (OR), 12 pv_sum, 13 inview_sum, 14 resub
+    unsigned long long vals[15];
+    for (int i = 1; i < 7; i++) vals[i] = sent[i];
+    vals[7] = dropped; vals[8] = nproc; vals[9] = ndraw; vals[10] = stopped; vals[11] = 0;
+    vals[12] = npv; vals[13] = niv; vals[14] = resub;
+    for (int i = 1; i <= 14; i++) {
+        if (i == 11) continue;
+        unsigned long long x = vals[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[i], x);
+    }
+    unsigned long long e = err;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) e |= __shfl_xor(e, o, 64);
+    if ((threadIdx.x & 63) == 0 && e) atomicOr(&a.stats[11], e);
+}
+
+// init/1 (v2 :75-85, v1 :56-66) for every vertex, or crash-restart of a list
+__global__ __launch_bounds__(kBlock) void sc_init(ScArgs a, const uint32_t* __restrict__ list, uint32_t k) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (list ? k : a.n)) return;
+    const uint32_t v = list ? list[i] : i;
+    ScHead h = list ? a.head[v] : ScHead{};
+    h.npv = 1;
+    h.niv = 0;
+    h.draws = 0;
+    h.last_ping = -1;
+    if (list) {
+        h.inc++;
+        h.fresh = 1;
+        a.alive[v] = 1;
+    } else {
+        h.inc = 0;
+        h.seq = 0;
+        h.fresh = 0;
+    }
+    a.head[v] = h;
+    a.pv[(size_t)v * kScPv] = v;
+}
+
+inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+
+}  // namespace
+
+hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s) {
+    const uint32_t m = list ? k : a.n;
+    if (m) hipLaunchKernelGGL(sc_init, dim3(nblk(m)), dim3(kBlock), 0, s, a, list, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_sc_round(const ScArgs& a, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(sc_count, dim3(kScStrideBlocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sc_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sc_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
+    hipLaunchKernelGGL(sc_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sc_scatter, dim3(kScStrideBlocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sc_process, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace psim
+
+// ---------------------------------------------------------------------------
+// host side: the psim_scamp_* entry points of include/psim.h
+// ---------------------------------------------------------------------------
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+using namespace psim;
+
+namespace {
+
+struct ScState : ModuleState {
+    uint32_t n = 0, ver = 2, c = 5, periodic = 0, cap = 0;
+    ScHead* head = nullptr;
+    uint32_t *pv = nullptr, *iv = nullptr;
+    uint8_t *alive = nullptr, *alive0 = nullptr;
+    ScMsg* msg[2] = {nullptr, nullptr};
+    uint32_t* nmsg = nullptr;
+    uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
+    uint32_t *call_off = nullptr, *calls = nullptr, *list = nullptr;
+    size_t calls_cap = 0, list_cap = 0;
+    unsigned long long* stats = nullptr;
+    uint32_t par = 0;
+    uint64_t round = 0;
+    std::vector<uint32_t> cv, cx;   // calls since the last round: vertex, (bit31 = leave) | target
+    ~ScState() override {
+        void* p[] = {head, pv, iv, alive, alive0, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, call_off, calls,
+                     list, stats};
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+};
+
+ScState* sc_of(psim_handle* h) { return static_cast<ScState*>(handle_module(h, MOD_SCAMP)); }
+const ScState* sc_of(const psim_handle* h) { return static_cast<const ScState*>(handle_module(h, MOD_SCAMP)); }
+
+#define SCCHK(h, x)                                                                         \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            return handle_fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+bool sc_alloc(void** p, size_t bytes) {
+    return hipMalloc(p, bytes ? bytes : 8) == hipSuccess && hipMemset(*p, 0, bytes ? bytes : 8) == hipSuccess;
+}
+
+ScArgs sc_args(const psim_handle* h, const ScState& s) {
+    ScArgs a{};
+    a.n = s.n; a.ver = s.ver; a.c = s.c;
+    a.round = (uint32_t)(s.round + 1);
+    a.periodic = s.periodic && ((s.round + 1) % s.periodic) == 0;
+    const uint64_t seed = handle_seed(h);
+    a.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+    a.alive0 = s.alive0; a.alive = s.alive;
+    a.head = s.head; a.pv = s.pv; a.iv = s.iv;
+    a.in = s.msg[s.par]; a.nin = s.nmsg + s.par;
+    a.out = s.msg[s.par ^ 1]; a.nout = s.nmsg + (s.par ^ 1);
+    a.out_cap = s.cap;
+    a.cnt = s.cnt; a.cur = s.cur; a.off = s.off; a.idx = s.idx; a.bsum = s.bsum;
+    a.call_off = s.call_off; a.calls = s.calls;
+    a.stats = s.stats;
+    return a;
+}
+
+int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
+    const hipStream_t st = handle_stream(h);
+    // calls grouped by vertex: leaves first, then joins, each in call order
+    std::vector<uint32_t> off(s.n + 1, 0);
+    for (uint32_t v : s.cv) off[v + 1]++;
+    for (uint32_t v = 0; v < s.n; v++) off[v + 1] += off[v];
+    std::vector<uint32_t> lst(s.cv.size());
+    {
+        std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+        for (int pass = 0; pass < 2; pass++)
+            for (size_t i = 0; i < s.cv.size(); i++)
+                if ((s.cx[i] >> 31) == (pass == 0 ? 1u : 0u)) lst[fill[s.cv[i]]++] = s.cx[i];
+    }
+    if (lst.size() > s.calls_cap) {
+        if (s.calls) (void)hipFree(s.calls);
+        s.calls = nullptr;
+        s.calls_cap = std::max<size_t>(lst.size(), 2 * s.calls_cap);
+        if (!sc_alloc((void**)&s.calls, s.calls_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "scamp: call list");
+    }
+    SCCHK(h, hipMemcpyAsync(s.call_off, off.data(), (s.n + 1) * 4, hipMemcpyHostToDevice, st));
+    if (!lst.empty()) SCCHK(h, hipMemcpyAsync(s.calls, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, st));
+    s.cv.clear();
+    s.cx.clear();
+    SCCHK(h, hipMemcpyAsync(s.alive0, s.alive, s.n, hipMemcpyDeviceToDevice, st));
+    SCCHK(h, hipMemsetAsync(s.stats, 0, 16 * 8, st));
+    SCCHK(h, hipMemsetAsync(s.nmsg + (s.par ^ 1), 0, 4, st));
+    ScArgs a = sc_args(h, s);
+    SCCHK(h, hipEventRecord(handle_event(h, 0), st));
+    SCCHK(h, launch_sc_round(a, st));
+    SCCHK(h, hipEventRecord(handle_event(h, 1), st));
+    unsigned long long r[16];
+    SCCHK(h, hipMemcpyAsync(r, s.stats, sizeof r, hipMemcpyDeviceToHost, st));
+    SCCHK(h, hipStreamSynchronize(st));
+    float ms = 0.f;
+    SCCHK(h, hipEventElapsedTime(&ms, handle_event(h, 0), handle_event(h, 1)));
+    handle_add_round(h, ms);
+    s.round++;
+    s.par ^= 1u;
+    if (r[11] & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: message queue over %u records",
+                                         (unsigned long long)s.round, s.cap);
+    if (r[11] & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: a view exceeded %u / %u entries",
+                                         (unsigned long long)s.round, kScPv, kScIv);
+    if (out) {
+        memset(out, 0, sizeof *out);
+        uint64_t emitted = 0;
+        for (int k = 1; k < 7; k++) { out->sent[k] = r[k]; emitted += r[k]; }
+        out->dropped = r[7]; out->processed = r[8]; out->draws = r[9]; out->stopped = r[10];
+        out->error = r[11]; out->pv_sum = r[12]; out->inview_sum = r[13]; out->resub = r[14];
+        // records read (bucket + handler) and written, bucket counts/offsets, and
+        // one pass over each live vertex's head and partial-view row
+        out->algo_bytes = 48ull * r[8] + 28ull * emitted + 12ull * s.n + 64ull * s.n + 4ull * r[12];
+        out->kernel_ms = ms;
+    }
+    return PSIM_OK;
+}
+
+int sc_upload_list(psim_handle* h, ScState& s, const uint32_t* v, size_t k) {
+    if (k > s.list_cap) {
+        if (s.list) (void)hipFree(s.list);
+        s.list = nullptr;
+        s.list_cap = std::max<size_t>(k, 2 * s.list_cap);
+        if (!sc_alloc((void**)&s.list, s.list_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "scamp: vertex list");
+    }
+    SCCHK(h, hipMemcpyAsync(s.list, v, k * 4, hipMemcpyHostToDevice, handle_stream(h)));
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_scamp_setup(psim_handle* h, uint32_t n, uint32_t version, uint32_t c, uint32_t periodic_rounds) {
+    if (!h) return PSIM_EINVAL;
+    if (n < 1 || n >= 0x7FFFFFFFu || (version != 1 && version != 2) || c < 1 || c > kScMaxSel)
+        return handle_fail(h, PSIM_EINVAL, "scamp: need n >= 1, version 1 or 2, 1 <= c <= %u", kScMaxSel);
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    SCCHK(h, hipStreamSynchronize(handle_stream(h)));
+    ModuleState*& slot = handle_module(h, MOD_SCAMP);
+    delete slot;
+    slot = nullptr;
+    ScState* s = new ScState();
+    s->n = n; s->ver = version; s->c = c; s->periodic = periodic_rounds;
+    s->cap = (uint32_t)std::min<uint64_t>(8ull * n + 4096, 0xFFFFFFF0ull);
+    const size_t N = n;
+    const uint32_t nb = (n + kBlock - 1) / kBlock;
+    const bool ok = sc_alloc((void**)&s->head, N * sizeof(ScHead)) && sc_alloc((void**)&s->pv, N * kScPv * 4) &&
+                    sc_alloc((void**)&s->iv, N * kScIv * 4) && sc_alloc((void**)&s->alive, N) &&
+                    sc_alloc((void**)&s->alive0, N) && sc_alloc((void**)&s->msg[0], size_t(s->cap) * sizeof(ScMsg)) &&
+                    sc_alloc((void**)&s->msg[1], size_t(s->cap) * sizeof(ScMsg)) && sc_alloc((void**)&s->nmsg, 16) &&
+                    sc_alloc((void**)&s->cnt, N * 4) && sc_alloc((void**)&s->cur, N * 4) &&
+                    sc_alloc((void**)&s->off, (N + 1) * 4) && sc_alloc((void**)&s->idx, size_t(s->cap) * 4) &&
+                    sc_alloc((void**)&s->bsum, size_t(nb) * 4) && sc_alloc((void**)&s->call_off, (N + 1) * 4) &&
+                    sc_alloc((void**)&s->stats, 16 * 8);
+    if (!ok) {
+        delete s;
+        return handle_fail(h, PSIM_ENOMEM, "scamp state for n=%u", n);
+    }
+    slot = s;
+    SCCHK(h, hipMemset(s->alive, 1, N));
+    SCCHK(h, launch_sc_init(sc_args(h, *s), nullptr, 0, handle_stream(h)));
+    SCCHK(h, hipStreamSynchronize(handle_stream(h)));
+    return PSIM_OK;
+}
+
+int psim_scamp_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
+    if (!h || !alive) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    if (n != s->n) return handle_fail(h, PSIM_EINVAL, "alive has %zu entries, cluster has %u", n, s->n);
+    std::vector<uint8_t> a(n);
+    for (size_t i = 0; i < n; i++) a[i] = alive[i] ? 1 : 0;
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    SCCHK(h, hipMemcpy(s->alive, a.data(), n, hipMemcpyHostToDevice));
+    return PSIM_OK;
+}
+
+static int sc_calls(psim_handle* h, const uint32_t* v, const uint32_t* x, size_t k, uint32_t leave_bit) {
+    if (!h || (k && (!v || !x))) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    for (size_t i = 0; i < k; i++)
+        if (v[i] >= s->n || x[i] >= s->n) return handle_fail(h, PSIM_EINVAL, "call %zu: vertex out of range", i);
+    for (size_t i = 0; i < k; i++) {
+        s->cv.push_back(v[i]);
+        s->cx.push_back(x[i] | leave_bit);
+    }
+    return PSIM_OK;
+}
+
+int psim_scamp_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k) {
+    return sc_calls(h, v, contact, k, 0u);
+}
+
+int psim_scamp_leave(psim_handle* h, const uint32_t* v, const uint32_t* node, size_t k) {
+    return sc_calls(h, v, node, k, 0x80000000u);
+}
+
+int psim_scamp_crash(psim_handle* h, const uint32_t* v, size_t k) {
+    if (!h || (k && !v)) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    std::vector<uint8_t> seen(s->n, 0);
+    for (size_t i = 0; i < k; i++) {
+        if (v[i] >= s->n) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex out of range", i);
+        if (seen[v[i]]) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex %u listed twice", i, v[i]);
+        seen[v[i]] = 1;
+    }
+    if (!k) return PSIM_OK;
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    int rc = sc_upload_list(h, *s, v, k);
+    if (rc) return rc;
+    SCCHK(h, launch_sc_init(sc_args(h, *s), s->list, (uint32_t)k, handle_stream(h)));
+    SCCHK(h, hipStreamSynchronize(handle_stream(h)));
+    return PSIM_OK;
+}
+
+int psim_scamp_step(psim_handle* h, uint32_t rounds, psim_scamp_stats* stats, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    for (uint32_t i = 0; i < rounds; i++) {
+        const int rc = sc_round(h, *s, stats && i < cap ? &stats[i] : nullptr);
+        if (rc) return rc;
+    }
+    return PSIM_OK;
+}
+
+int psim_scamp_get_views(const psim_handle* h, uint32_t* pv, uint32_t* npv, uint32_t* iv, uint32_t* niv, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    const ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    if (n != s->n) return handle_fail(hh, PSIM_EINVAL, "want n=%u", s->n);
+    SCCHK(hh, hipSetDevice(handle_device(h)));
+    SCCHK(hh, hipStreamSynchronize(handle_stream(h)));
+    if (pv) SCCHK(hh, hipMemcpy(pv, s->pv, n * kScPv * 4, hipMemcpyDeviceToHost));
+    if (iv) SCCHK(hh, hipMemcpy(iv, s->iv, n * kScIv * 4, hipMemcpyDeviceToHost));
+    if (npv || niv) {
+        std::vector<ScHead> hd(n);
+        SCCHK(hh, hipMemcpy(hd.data(), s->head, n * sizeof(ScHead), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; i++) {
+            if (npv) npv[i] = hd[i].npv;
+            if (niv) niv[i] = hd[i].niv;
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_scamp_get_nodes(const psim_handle* h, uint64_t* draws, int32_t* last_ping, uint8_t* alive, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    const ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    if (n != s->n) return handle_fail(hh, PSIM_EINVAL, "want n=%u", s->n);
+    SCCHK(hh, hipSetDevice(handle_device(h)));
+    SCCHK(hh, hipStreamSynchronize(handle_stream(h)));
+    std::vector<ScHead> hd(n);
+    SCCHK(hh, hipMemcpy(hd.data(), s->head, n * sizeof(ScHead), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++) {
+        if (draws) draws[i] = hd[i].draws;
+        if (last_ping) last_ping[i] = hd[i].last_ping;
+    }
+    if (alive) SCCHK(hh, hipMemcpy(alive, s->alive, n, hipMemcpyDeviceToHost));
+    return PSIM_OK;
+}
+
+int psim_scamp_inflight(const psim_handle* h, uint64_t* messages) {
+    if (!h || !messages) return PSIM_EINVAL;
+    const ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    SCCHK(hh, hipSetDevice(handle_device(h)));
+    SCCHK(hh, hipStreamSynchronize(handle_stream(h)));
+    uint32_t c = 0;
+    SCCHK(hh, hipMemcpy(&c, s->nmsg + s->par, 4, hipMemcpyDeviceToHost));
+    *messages = c;
+    return PSIM_OK;
+}
+
+}  // extern "C"
