@@ -57,3 +57,37 @@ def ring_lattice(n, k=2):
     a = np.repeat(np.arange(n, dtype=np.int64), k)
     b = (a + np.tile(np.arange(1, k + 1, dtype=np.int64), n)) % n
     return from_edges(n, a, b)
+
+
+# ---------------------------------------------------------------- workload draws
+_PHILOX_M0, _PHILOX_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_PHILOX_W0, _PHILOX_W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+
+
+def philox4x32_10(c0, c1, c2, c3, seed):
+    """Vectorised Philox4x32-10 (Random123), the simulation's RNG, for host-side
+    workload generation (crash lists, contacts).  Arrays of uint32 counters."""
+    m = np.uint64(0xFFFFFFFF)
+    x = [np.asarray(c, dtype=np.uint64) & m for c in (c0, c1, c2, c3)]
+    x = list(np.broadcast_arrays(*x))
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for r in range(10):
+        p0 = _PHILOX_M0 * x[0]
+        p1 = _PHILOX_M1 * x[2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m
+        x = [(hi1 ^ x[1] ^ k0) & m, lo1, (hi0 ^ x[3] ^ k1) & m, lo0]
+        k0 = (k0 + np.uint64(_PHILOX_W0)) & m
+        k1 = (k1 + np.uint64(_PHILOX_W1)) & m
+    return [a.astype(np.uint32) for a in x]
+
+
+def philox_uniform(seed, ctr, kind, n):
+    """floor(r * n / 2^64) for the 64-bit draw r of counter {ctr, 0, kind, 0}."""
+    ctr = np.asarray(ctr, dtype=np.uint64)
+    r = philox4x32_10(ctr, 0, kind, 0, seed)
+    lo, hi = r[0].astype(np.uint64), r[1].astype(np.uint64)
+    n64 = np.uint64(n)
+    # mulhi(hi:lo * n) without 128-bit ints: (hi*n + (lo*n >> 32)) >> 32
+    t = hi * n64 + ((lo * n64) >> np.uint64(32))
+    return (t >> np.uint64(32)).astype(np.uint32)

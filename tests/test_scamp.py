@@ -1,0 +1,214 @@
+"""SCAMP v1 / v2 membership strategies (src/partisan_scamp_v{1,2}_membership_strategy.erl).
+
+Oracle (CPU, oracle/scamp.c): protocol properties -- a live manager's members
+contain itself (else it stops, pluggable :1791-1803); joins keep the overlay
+weakly connected through the contact edges; a kept v2 subscription puts the
+keeper in the subscriber's in-view; the v1 remove_subscription bug (Q17) and
+the v2 bootstrap_remove_subscription index crash (Q18) surface as stops.
+Trajectories are parity unpinned by reference vectors.
+
+GPU (-m gpu, csrc/scamp.hip through the C ABI): bit-exact against the oracle
+round by round -- per-round counters, every partial view and in-view in list
+order, draw counters, last-ping rounds, liveness -- through join waves,
+periodic isolation re-subscriptions, 5 % crash/rejoin churn and leaves.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from partisan_amd.overlay import philox_uniform
+
+SEED = 0x5EED0003
+
+
+def waves(n, seed=SEED):
+    out, k = [], 1
+    while k < n:
+        v = np.arange(k, min(2 * k, n), dtype=np.uint32)
+        out.append((v, philox_uniform(seed, v, 0x5CA0, k)))
+        k *= 2
+    return out
+
+
+def churn(n, rnd, frac=0.05, seed=SEED):
+    k = max(1, int(n * frac))
+    cand = philox_uniform(seed, np.arange(k, dtype=np.uint32) + np.uint32(rnd * 7919), 0xC4A5, n)
+    v = np.unique(cand).astype(np.uint32)
+    c = philox_uniform(seed, v, 0xC0A0 + (rnd & 0xFFF), n - 1)
+    c = np.where(c >= v, c + 1, c).astype(np.uint32)
+    return v, c
+
+
+def build(n, version=2, periodic=5, seed=SEED):
+    s = O.Scamp(n, version, 5, periodic, seed)
+    for v, c in waves(n, seed):
+        for a, b in zip(v, c):
+            s.join(int(a), int(b))
+        s.step(3)
+    return s
+
+
+def test_join_waves_properties():
+    n = 3000
+    s = build(n)
+    s.step(12)
+    for v in range(n):
+        assert s.alive(v)
+        assert v in s.view(v)                      # members contain self
+    # weak connectivity of the partial-view graph
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+    for v in range(n):
+        for u in s.view(v):
+            parent[find(u)] = find(v)
+    assert len({find(v) for v in range(n)}) == 1
+    # v2: u in in-view(v)  =>  v in partial view(u)  (no removals, no crashes)
+    for v in range(n):
+        for u in s.view(v, 1):
+            assert v in s.view(u), (v, u)
+
+
+def test_isolation_resubscription_q19():
+    n = 200
+    s = build(n, periodic=4)
+    st = s.step(12)
+    # after the first pings, every periodic finds the node isolated (no ping in the same round)
+    assert any(x["resub"] > 0 for x in st)
+    assert max(x["resub"] for x in st) <= n
+
+
+def test_crash_restart_drops_inbox_and_rejoins():
+    n = 500
+    s = build(n)
+    s.step(5)
+    v, c = churn(n, 1)
+    for a in v:
+        s.crash(int(a))
+    for a, b in zip(v, c):
+        s.join(int(a), int(b))
+    s.step(3)
+    for a, b in zip(v, c):
+        pv = s.view(int(a))
+        assert int(a) in pv and int(b) in pv
+
+
+def test_v1_remove_subscription_q17_stops_members():
+    n = 64
+    s = build(n, version=1)
+    s.step(6)
+    # node 0 asks to remove node 1: remove_subscription(1) to members(State0);
+    # every receiver holding 1 hits the swapped sets:del_element and stops
+    holders = [u for u in range(n) if 1 in s.view(u) and u != 0 and u in s.view(0)]
+    s.leave(0, 1)
+    st = s.step(2)
+    assert any(x["error"] & 8 for x in st) or not holders
+    for u in holders:
+        assert not s.alive(u)
+
+
+def test_v2_bootstrap_remove_q18():
+    n = 64
+    s = build(n)
+    s.step(6)
+    # leave(Node) gossips bootstrap_remove_subscription(Node); only Node acts,
+    # and its index arithmetic crashes unless |in-view| == c - 1 (Q18)
+    target = next(u for u in range(1, n) if u in s.view(0))
+    niv = len(s.view(target, 1))
+    s.leave(0, target)
+    st = s.step(2)
+    assert not s.alive(target)
+    if niv != 4:
+        assert st[0]["error"] & 4 or st[1]["error"] & 4
+
+
+# ------------------------------------------------------------------ GPU parity
+def _check(g, s, n):
+    pv, npv, iv, niv = g.views()
+    draws, lp, al = g.nodes()
+    for v in range(n):
+        assert bool(al[v]) == s.alive(v), v
+        assert list(pv[v, :npv[v]]) == s.view(v), (v, list(pv[v, :npv[v]]), s.view(v))
+        assert list(iv[v, :niv[v]]) == s.view(v, 1), v
+        assert int(draws[v]) == s.draws(v), v
+        assert int(lp[v]) == s.last_ping(v), v
+
+
+def _step_both(g, s, r):
+    gs = g.step(1)[0]
+    os_ = s.step(1)[0]
+    for k in os_:
+        assert gs[k] == os_[k], (r, k, gs[k], os_[k])
+    return gs
+
+
+def _gpu_run(n, version, periodic, churn_rounds, leaves=()):
+    import partisan_amd as pa
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.scamp.ScampCluster(sim, n, version=version, c=5, periodic_rounds=periodic)
+    s = O.Scamp(n, version, 5, periodic, SEED)
+    r = 0
+    for v, c in waves(n):
+        g.join(v, c)
+        for a, b in zip(v, c):
+            s.join(int(a), int(b))
+        for _ in range(3):
+            _step_both(g, s, r)
+            r += 1
+        _check(g, s, n)
+    for i in range(churn_rounds):
+        v, c = churn(n, i)
+        g.crash(v)
+        g.join(v, c)
+        for a, b in zip(v, c):
+            s.crash(int(a))
+            s.join(int(a), int(b))
+        for a, b in leaves:
+            if i == 3:
+                g.leave([a], [b])
+                s.leave(a, b)
+        _step_both(g, s, r)
+        r += 1
+        _check(g, s, n)
+    return g, s
+
+
+@pytest.mark.gpu
+def test_gpu_scamp_v2_parity_churn():
+    _gpu_run(4000, 2, 5, 25, leaves=[(7, 9), (100, 100)])
+
+
+@pytest.mark.gpu
+def test_gpu_scamp_v1_parity():
+    _gpu_run(1500, 1, 4, 12, leaves=[(3, 5)])
+
+
+@pytest.mark.gpu
+def test_gpu_scamp_c3_scale():
+    """C3 shape at 1M peers: join waves, then 5 % crash/rejoin churn per round;
+    view invariants checked on device results (oracle parity is covered above)."""
+    import partisan_amd as pa
+    n = 1_000_000
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.scamp.ScampCluster(sim, n, version=2, c=5, periodic_rounds=10)
+    for v, c in waves(n):
+        g.join(v, c)
+        g.step(3)
+    st = []
+    for i in range(10):
+        v, c = churn(n, i)
+        g.crash(v)
+        g.join(v, c)
+        st += g.step(1)
+    pv, npv, iv, niv = g.views()
+    _, _, al = g.nodes()
+    live = al.astype(bool)
+    assert live.sum() > 0.99 * n
+    idx = np.nonzero(live)[0]
+    # every live manager's members contain itself
+    assert all(v in pv[v, :npv[v]] for v in idx[:: max(1, len(idx) // 5000)])
+    assert all(x["error"] == 0 for x in st)
