@@ -926,6 +926,9 @@ DmArgs make_dm_args(const psim_handle* h, uint32_t par, unsigned long long* stat
     DmArgs a{};
     a.n = d.n;
     a.m = d.m;
+    a.v_lo = 0;
+    a.n_global = d.n;
+    a.sharded = 0;
     a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
     a.rm_on = d.rm_on;
     a.full = d.full;

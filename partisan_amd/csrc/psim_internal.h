@@ -58,17 +58,19 @@ struct PtArgs {
 // Demers rumor mongering + anti-entropy (demers.hip)
 constexpr uint32_t kDmPushCap = 24;   // AE pushes one vertex can receive per tick (Poisson(2) in-degree)
 struct DmArgs {
-    uint32_t n, m;
+    uint32_t n, m;                        // n = vertices of this shard (all of them on one GPU)
+    uint32_t v_lo, n_global;              // global id of local vertex 0; membership size
+    uint32_t sharded;                     // 1: AE pushes are listed by dm_pushscan after the snapshot all-gather
     uint2 key;                            // Philox key {seed_lo, seed_hi}
     uint32_t rm_on;
     uint32_t tick, tick_idx, prev_tick;   // AE tick at the end of this round; tick indices
     unsigned long long full;              // every rumor id's bit
     unsigned long long* __restrict__ seen;       // [n] the message store
-    unsigned long long* __restrict__ snap;       // [n] AE payload taken at the tick
+    unsigned long long* __restrict__ snap;       // [n_global] AE payload taken at the tick (global ids)
     unsigned long long* __restrict__ rm_cur_reg; // [n] RM inbox read this round
     unsigned long long* __restrict__ rm_cur_t0;
     unsigned long long* __restrict__ rm_cur_t1;
-    unsigned long long* __restrict__ rm_nxt_reg; // [n] RM inbox written this round
+    unsigned long long* __restrict__ rm_nxt_reg; // [n_global] RM inbox written this round (global ids)
     unsigned long long* __restrict__ rm_nxt_t0;
     unsigned long long* __restrict__ rm_nxt_t1;
     uint32_t* __restrict__ pushcnt_cur;   // [n]
@@ -76,12 +78,15 @@ struct DmArgs {
     uint32_t* __restrict__ pushlist_cur;  // [n][kDmPushCap]
     uint32_t* __restrict__ pushlist_nxt;
     unsigned long long* __restrict__ pull_cur;   // [n][2]
-    unsigned long long* __restrict__ pull_nxt;
+    unsigned long long* __restrict__ pull_nxt;   // [n_global][2]
     unsigned long long* __restrict__ stats;      // [kStatShards][kNStat]: 1 rm, 2 push, 3 pull, 4 deliv, 5 complete, 6 overflow
 };
 hipError_t launch_dm_origins(uint2 key, uint32_t n, uint32_t m, uint32_t* origin, hipStream_t s);
 hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const uint32_t* idbit, hipStream_t s);
 hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
+hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s);
+hipError_t launch_dm_ingest(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
+                            uint32_t world, uint32_t chunk, hipStream_t s);
 
 // HyParView (hyparview.hip)
 constexpr uint32_t kHvX = 8;          // exchange list capacity (1 + k_active + k_passive)
@@ -227,7 +232,7 @@ hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
 struct ModuleState {
     virtual ~ModuleState() {}
 };
-enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_COUNT = 4 };
+enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_CSSHARD = 3, MOD_COUNT = 4 };
 ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);
 hipStream_t handle_stream(const psim_handle* h);

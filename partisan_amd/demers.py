@@ -43,3 +43,127 @@ class DemersEpidemic:
         out = np.zeros(self.n, np.uint64)
         self._c(lib().psim_demers_get_seen(self.sim._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), self.n))
         return out
+
+
+class ShardedDemers:
+    """Demers epidemic vertex-sharded over `world` processes, one GPU each
+    (SURVEY 8(e)); include/psim.h "vertex-sharded Demers".  The exchange per
+    round: all-to-all of the RM inbox slices (OR-merged by the receiver),
+    reduce-scatter of the pull slots, all-gather of the AE snapshots after a
+    tick -- RCCL over xGMI with backend "nccl", host-staged with "gloo"."""
+
+    def __init__(self, n, m, rank, world, device=0, backend="nccl", ae_period=2, rumor_mongering=True, seed=0):
+        import torch
+
+        from .sim import Simulator
+        self.torch = torch
+        self.n, self.m, self.rank, self.world, self.backend = n, m, rank, world, backend
+        self.dev = torch.device("cuda", device)
+        self.sim = Simulator(device=device, seed=seed)
+        self._h = self.sim._h
+        chunk = C.c_uint64()
+        check(lib().psim_demers_shard_setup(self._h, n, m, ae_period, 1 if rumor_mongering else 0, rank, world,
+                                            C.byref(chunk)), self._h)
+        self.chunk = Cn = chunk.value
+        vlo, nl = C.c_uint32(), C.c_uint32()
+        check(lib().psim_demers_shard_info(self._h, C.byref(vlo), C.byref(nl), None), self._h)
+        self.v_lo, self.n_local = vlo.value, nl.value
+        G = world
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=self.dev)  # noqa: E731
+        self.rm_shadow, self.rm_recv = z(3, G * Cn), z(3, G * Cn)
+        self.pull_shadow, self.pull_recv = z(2 * G * Cn), z(2 * Cn)
+        self.snap_all = z(G * Cn)
+        self.local_kernel_ms = 0.0
+        self.local_algo_bytes = 0
+
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr())
+
+    # -------------------------------------------------------------- exchange
+    def _exchange(self, tick):
+        dist, torch = self._dist(), self.torch
+        G, Cn, r = self.world, self.chunk, self.rank
+        if self.backend == "nccl":
+            for k in range(3):
+                dist.all_to_all_single(self.rm_recv[k], self.rm_shadow[k])
+            dist.reduce_scatter_tensor(self.pull_recv, self.pull_shadow, op=dist.ReduceOp.SUM)
+            if tick:
+                mine = self.snap_all[r * Cn:(r + 1) * Cn].clone()
+                dist.all_gather_into_tensor(self.snap_all, mine)
+            torch.cuda.synchronize(self.dev)
+        else:   # gloo: host-staged all-gather of the shadows, each rank keeps its slices
+            rm = self.rm_shadow.cpu()
+            pull = self.pull_shadow.cpu()
+            rm_all = [torch.zeros_like(rm) for _ in range(G)]
+            pull_all = [torch.zeros_like(pull) for _ in range(G)]
+            dist.all_gather(rm_all, rm)
+            dist.all_gather(pull_all, pull)
+            recv = torch.stack([x[:, r * Cn:(r + 1) * Cn] for x in rm_all], dim=1).reshape(3, G * Cn)
+            self.rm_recv.copy_(recv.to(self.dev))
+            ps = torch.zeros(2 * Cn, dtype=torch.int64)
+            for x in pull_all:
+                ps += x[2 * r * Cn:2 * (r + 1) * Cn]
+            self.pull_recv.copy_(ps.to(self.dev))
+            if tick:
+                snap = self.snap_all.cpu()
+                snap_all = [torch.zeros_like(snap) for _ in range(G)]
+                dist.all_gather(snap_all, snap)
+                full = torch.cat([snap_all[g][g * Cn:(g + 1) * Cn] for g in range(G)])
+                self.snap_all.copy_(full.to(self.dev))
+            torch.cuda.synchronize(self.dev)
+        self.rm_shadow.zero_()
+        self.pull_shadow.zero_()
+        check(lib().psim_demers_shard_ingest(self._h, self._p(self.rm_recv), self._p(self.pull_recv),
+                                             1 if tick else 0), self._h)
+
+    @staticmethod
+    def _dist():
+        import torch.distributed as dist
+        return dist
+
+    def _allreduce(self, vals):
+        t = self.torch.tensor(vals, dtype=self.torch.int64, device=self.dev if self.backend == "nccl" else "cpu")
+        self._dist().all_reduce(t)
+        return t.tolist()
+
+    # -------------------------------------------------------------- protocol
+    def broadcast(self):
+        check(lib().psim_demers_shard_broadcast_all(self._h, self._p(self.rm_shadow)), self._h)
+        self._exchange(False)
+
+    def step(self, rounds=1):
+        """Rounds; returns per-round GLOBAL stats (summed over shards)."""
+        out = []
+        for _ in range(rounds):
+            st = DemersStats()
+            tick = C.c_uint32()
+            check(lib().psim_demers_shard_round(self._h, self._p(self.rm_shadow), self._p(self.pull_shadow),
+                                                self._p(self.snap_all), C.byref(st), C.byref(tick)), self._h)
+            d = st.as_dict()
+            self.local_kernel_ms += d["kernel_ms"]
+            self.local_algo_bytes += d["algo_bytes"]
+            self._exchange(bool(tick.value))
+            keys = ["rm_sent", "push_sent", "pull_sent", "delivered_new", "complete", "algo_bytes"]
+            g = dict(zip(keys, self._allreduce([d[k] for k in keys])))
+            g["kernel_ms"] = d["kernel_ms"]
+            out.append(g)
+        return out
+
+    def run(self, max_rounds=10000):
+        out = []
+        while len(out) < max_rounds:
+            out += self.step(1)
+            if out[-1]["complete"] == self.n:
+                break
+        return out, len(out)
+
+    def seen(self):
+        """This shard's stores, global ids [v_lo, v_lo + n_local)."""
+        out = np.zeros(self.n_local, np.uint64)
+        check(lib().psim_demers_shard_get_seen(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), self.n_local),
+              self._h)
+        return out
+
+    def close(self):
+        self.sim.close()
