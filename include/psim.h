@@ -292,6 +292,20 @@ int  psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uin
                               size_t* len);
 int  psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t n);
 int  psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m);
+/* Vertex-sharded causal delivery (one process per GPU): this
+ * handle owns global ids [floor(n rank/world), floor(n (rank+1)/world)); the
+ * getters above then address that range (index 0 = its first vertex).  A
+ * round is split-phase: psim_causal_shard_round runs the local round and the
+ * broadcasts of the shard's emitters, writing their clocks into the caller's
+ * device `slab` (64 x 64 u32, zero elsewhere); the caller sum-all-reduces
+ * the slab (RCCL on a node) and hands it to psim_causal_shard_ingest.
+ * Messages are never materialised, so that 16 KB is the whole
+ * exchange. */
+int  psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax,
+                             uint32_t redeliver, int rank, int world);
+int  psim_causal_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local);
+int  psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* stats);
+int  psim_causal_shard_ingest(psim_handle* h, const void* slab);
 
 /* --- full-membership strategy (partisan_full_membership_strategy.erl) --
  * Nodes 0..n-1; node v's #full_v1{} membership (a state_orset,

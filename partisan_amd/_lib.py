@@ -165,6 +165,10 @@ SIGNATURES = {
                                            _P(C.c_size_t)]),
     "psim_causal_get_delivered": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_causal_emitters": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
+    "psim_causal_shard_setup": (C.c_int, [_H] + [C.c_uint32] * 5 + [C.c_int, C.c_int]),
+    "psim_causal_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32)]),
+    "psim_causal_shard_round": (C.c_int, [_H, C.c_void_p, _P(CausalStats)]),
+    "psim_causal_shard_ingest": (C.c_int, [_H, C.c_void_p]),
     "psim_fm_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_fm_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_fm_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

@@ -58,3 +58,86 @@ class CausalCluster:
         out = np.zeros(self.n, np.uint64)
         self._c(lib().psim_causal_get_delivered(self.sim._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), self.n))
         return out
+
+
+class ShardedCausal:
+    """Causal delivery vertex-sharded over `world` processes, one GPU each
+    (SURVEY 8(e), config C5).  Receivers enumerate their own arrivals, so the
+    only exchange per round is the 64 x 64 clock slab of the emitters that
+    broadcast: sum-all-reduced (RCCL with backend "nccl", gloo in tests)."""
+
+    def __init__(self, n, rank, world, m=64, period=1, dmax=4, redeliver=1, device=0, backend="nccl", seed=0):
+        import torch
+
+        from .sim import Simulator
+        self.torch, self.n, self.m, self.rank, self.world, self.backend = torch, n, m, rank, world, backend
+        self.dev = torch.device("cuda", device)
+        self.sim = Simulator(device=device, seed=seed)
+        self._h = self.sim._h
+        check(lib().psim_causal_shard_setup(self._h, n, m, period, dmax, redeliver, rank, world), self._h)
+        lo, nl = C.c_uint32(), C.c_uint32()
+        check(lib().psim_causal_shard_info(self._h, C.byref(lo), C.byref(nl)), self._h)
+        self.v_lo, self.n_local = lo.value, nl.value
+        self.emitters = np.zeros(m, np.uint32)
+        check(lib().psim_causal_emitters(self._h, _u32p(self.emitters), m), self._h)
+        self.slab = torch.zeros(64 * 64, dtype=torch.int32, device=self.dev)
+        self.local_kernel_ms = 0.0
+
+    def _allreduce(self, vals):
+        import torch.distributed as dist
+        t = self.torch.tensor(vals, dtype=self.torch.int64, device=self.dev if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        return t.tolist()
+
+    def step(self, rounds=1):
+        """Rounds; per-round GLOBAL stats (summed over shards)."""
+        import torch.distributed as dist
+        out = []
+        keys = ["emitted", "received", "delivered", "checks", "buffered", "algo_bytes"]
+        for _ in range(rounds):
+            st = CausalStats()
+            check(lib().psim_causal_shard_round(self._h, C.c_void_p(self.slab.data_ptr()), C.byref(st)), self._h)
+            if self.backend == "nccl":
+                dist.all_reduce(self.slab)
+                self.torch.cuda.synchronize(self.dev)
+            else:
+                h = self.slab.cpu()
+                dist.all_reduce(h)
+                self.slab.copy_(h.to(self.dev))
+                self.torch.cuda.synchronize(self.dev)
+            check(lib().psim_causal_shard_ingest(self._h, C.c_void_p(self.slab.data_ptr())), self._h)
+            d = st.as_dict()
+            self.local_kernel_ms += d["kernel_ms"]
+            g = dict(zip(keys, self._allreduce([d[k] for k in keys])))
+            g["kernel_ms"] = d["kernel_ms"]
+            out.append(g)
+        return out
+
+    def clocks(self):
+        lanes = np.zeros((max(1, self.n_local), 64), np.uint32)
+        slf = np.zeros(max(1, self.n_local), np.uint32)
+        check(lib().psim_causal_get_clocks(self._h, _u32p(lanes), _u32p(slf), self.n_local), self._h)
+        return lanes, slf
+
+    def clock(self, lv, lanes, slf):
+        """local_clock of global vertex v_lo + lv as sorted (actor, counter) pairs."""
+        out = [(int(self.emitters[k]), int(lanes[lv, k])) for k in range(self.m) if lanes[lv, k]]
+        if slf[lv]:
+            out.append((self.v_lo + lv, int(slf[lv])))
+        return sorted(out)
+
+    def buffered(self, lv, cap=512):
+        k = np.zeros(cap, np.uint32)
+        r = np.zeros(cap, np.uint32)
+        ln = C.c_size_t()
+        check(lib().psim_causal_get_buffered(self._h, lv, _u32p(k), _u32p(r), cap, C.byref(ln)), self._h)
+        return [(int(k[i]), int(r[i])) for i in range(min(ln.value, cap))]
+
+    def delivered(self):
+        out = np.zeros(max(1, self.n_local), np.uint64)
+        check(lib().psim_causal_get_delivered(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), self.n_local),
+              self._h)
+        return out[:self.n_local]
+
+    def close(self):
+        self.sim.close()

@@ -114,6 +114,7 @@ struct psim_handle {
     // causal delivery state (causal.hip)
     struct Cs {
         uint32_t n = 0, m = 0, period = 1, dmax = 1, redeliver = 1;
+        uint32_t n_global = 0, v_lo = 0, rank = 0, world = 1;   // vertex shard [v_lo, v_lo + n) of n_global
         uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr;
         unsigned long long *delivered = nullptr, *stats = nullptr, *h_stats = nullptr;
         uint64_t round = 0;
@@ -1342,8 +1343,8 @@ CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
     a.period = c.period;
     a.dmax = c.dmax;
     a.redeliver = c.redeliver;
-    a.v_lo = 0;
-    a.n_global = c.n;
+    a.v_lo = c.v_lo;
+    a.n_global = c.n_global;
     a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
     a.t = t;
     a.clk = c.clk;
@@ -1361,7 +1362,12 @@ CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
 extern "C" {
 
 int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax, uint32_t redeliver) {
-    if (!h) return PSIM_EINVAL;
+    return psim_causal_shard_setup(h, n, m, period, dmax, redeliver, 0, 1);
+}
+
+int psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax,
+                            uint32_t redeliver, int rank, int world) {
+    if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
     if (n < 2 || m < 1 || m > kCsLanes || m > n || period < 1 || dmax < 1 || dmax > 30 ||
         dmax + 2 * redeliver + period + 2 >= kCsWindow)
         return fail(h, PSIM_EINVAL, "causal: need 2 <= n, 1 <= m <= min(64, n), period >= 1, 1 <= dmax <= 30, "
@@ -1370,7 +1376,8 @@ int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, u
     HIPCHK(h, hipStreamSynchronize(h->stream));
     free_cs(h);
     auto& c = h->cs;
-    const size_t N = n;
+    const uint32_t lo = uint32_t((uint64_t(n) * rank) / world), hi = uint32_t((uint64_t(n) * (rank + 1)) / world);
+    const size_t N = std::max<uint32_t>(hi - lo, 1);
     auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
     const bool ok = A((void**)&c.clk, N * kCsLanes * 4) && A((void**)&c.self, N * 4) &&
                     A((void**)&c.buf, N * kCsBufCap * 4) && A((void**)&c.nbuf, N * 4) &&
@@ -1381,7 +1388,11 @@ int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, u
         free_cs(h);
         return fail(h, PSIM_ENOMEM, "causal state for n=%u", n);
     }
-    c.n = n;
+    c.n = hi - lo;
+    c.n_global = n;
+    c.v_lo = lo;
+    c.rank = (uint32_t)rank;
+    c.world = (uint32_t)world;
     c.m = m;
     c.period = period;
     c.dmax = dmax;
@@ -1392,7 +1403,8 @@ int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, u
 int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, size_t cap) {
     if (!h) return PSIM_EINVAL;
     auto& c = h->cs;
-    if (!c.n) return fail(h, PSIM_ESTATE, "psim_causal_setup not called");
+    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_setup not called");
+    if (c.world > 1) return fail(h, PSIM_ESTATE, "sharded causal handle: use psim_causal_shard_round");
     HIPCHK(h, hipSetDevice(h->device));
     for (uint32_t i = 0; i < rounds; i++) {
         const uint64_t t = c.round + 1;
@@ -1438,6 +1450,77 @@ int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, si
     return PSIM_OK;
 }
 
+// Split-phase sharded round: the local round and the broadcasts of this
+// shard's emitters; their base-clock rows go to the caller's `slab`
+// (64 x 64 u32, zero elsewhere) to be sum-all-reduced, then
+// psim_causal_shard_ingest installs the reduced slab for every receiver.
+int psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* out) {
+    if (!h || !slab) return PSIM_EINVAL;
+    auto& c = h->cs;
+    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_shard_setup not called");
+    HIPCHK(h, hipSetDevice(h->device));
+    const uint64_t t = c.round + 1;
+    if (t >= (1u << 24)) return fail(h, PSIM_EOVERFLOW, "causal: round %llu exceeds 2^24", (unsigned long long)t);
+    CsArgs a = make_cs_args(h, (uint32_t)t);
+    uint32_t* sl = c.base + size_t(t % kCsWindow) * kCsLanes * kCsLanes;
+    HIPCHK(h, hipMemsetAsync(c.stats, 0, kStatShards * kCsNStat * 8, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
+    if (c.n) HIPCHK(h, launch_cs_round(a, h->stream));
+    HIPCHK(h, hipMemsetAsync(sl, 0, kCsLanes * kCsLanes * 4, h->stream));
+    HIPCHK(h, launch_cs_broadcast(a, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
+    HIPCHK(h, hipMemcpyAsync(slab, sl, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    c.round = t;
+    unsigned long long r[kCsNStat] = {0};
+    unsigned long long err = 0;
+    for (int sh = 0; sh < kStatShards; sh++)
+        for (int q = 0; q < kCsNStat; q++) {
+            if (q == 5) err |= c.h_stats[sh * kCsNStat + q];
+            else r[q] += c.h_stats[sh * kCsNStat + q];
+        }
+    if (err & 1ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
+                                (unsigned long long)t, kCsBufCap);
+    if (err & 2ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
+                                "clock window", (unsigned long long)t, kCsWindow);
+    if (err & 4ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a u32 clock entry overflowed",
+                                (unsigned long long)t);
+    float ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    h->kernel_ms_total += ms;
+    h->rounds_total++;
+    if (out) {
+        memset(out, 0, sizeof *out);
+        out->emitted = r[6];
+        out->received = r[1];
+        out->delivered = r[2];
+        out->checks = r[3];
+        out->buffered = r[4];
+        out->algo_bytes = 1024ull * r[2] + 256ull * r[3] + 32ull * r[1];
+        out->kernel_ms = ms;
+    }
+    return PSIM_OK;
+}
+
+int psim_causal_shard_ingest(psim_handle* h, const void* slab) {
+    if (!h || !slab) return PSIM_EINVAL;
+    auto& c = h->cs;
+    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_shard_setup not called");
+    HIPCHK(h, hipSetDevice(h->device));
+    uint32_t* sl = c.base + size_t(c.round % kCsWindow) * kCsLanes * kCsLanes;
+    HIPCHK(h, hipMemcpyAsync(sl, slab, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
+int psim_causal_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local) {
+    if (!h) return PSIM_EINVAL;
+    if (v_lo) *v_lo = h->cs.v_lo;
+    if (n_local) *n_local = h->cs.n;
+    return PSIM_OK;
+}
+
 int psim_causal_get_clocks(const psim_handle* h, uint32_t* lanes, uint32_t* self, size_t n) {
     if (!h || n != h->cs.n || !n) return PSIM_EINVAL;
     psim_handle* hh = const_cast<psim_handle*>(h);
@@ -1450,7 +1533,7 @@ int psim_causal_get_clocks(const psim_handle* h, uint32_t* lanes, uint32_t* self
 
 int psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uint32_t* round, size_t cap,
                              size_t* len) {
-    if (!h || !len || v >= h->cs.n) return PSIM_EINVAL;
+    if (!h || !len || v >= h->cs.n) return PSIM_EINVAL;   // v: index in this shard's range
     psim_handle* hh = const_cast<psim_handle*>(h);
     HIPCHK(hh, hipSetDevice(h->device));
     HIPCHK(hh, hipStreamSynchronize(h->stream));
@@ -1477,7 +1560,7 @@ int psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t 
 
 int psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m) {
     if (!h || !emitters || m != h->cs.m || !m) return PSIM_EINVAL;
-    for (size_t k = 0; k < m; k++) emitters[k] = (uint32_t)((uint64_t(k) * h->cs.n) / h->cs.m);
+    for (size_t k = 0; k < m; k++) emitters[k] = (uint32_t)((uint64_t(k) * h->cs.n_global) / h->cs.m);
     return PSIM_OK;
 }
 

@@ -1,0 +1,71 @@
+"""Vertex-sharded causal delivery (SURVEY 8(e), config C5's exchange).
+
+GPU: world = 2 and 4 processes on ONE GPU (gloo) and world = 1 over RCCL;
+every rank checks its range's clocks, buffers and delivery counts against
+the oracle (oracle/causality.c) after every few rounds, and the per-round
+counters summed over ranks against the oracle's.
+"""
+import os
+import sys
+
+import pytest
+
+from test_shard import run_world
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = ("emitted", "received", "delivered", "checks", "buffered")
+
+
+def _worker(rank, world, port, n, m, period, dmax, redeliver, backend, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        if backend == "nccl":
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        from partisan_amd.causal import ShardedCausal
+        import pyoracle as O
+        seed = 0x5EED0005
+        g = ShardedCausal(n, rank, world, m=m, period=period, dmax=dmax, redeliver=redeliver, device=0,
+                          backend=backend, seed=seed)
+        o = O.Causal(n, m, period=period, dmax=dmax, redeliver=redeliver, seed=seed)
+        assert g.emitters.tolist() == [o.emitter(k) for k in range(m)]
+        for _ in range(5):
+            gs, os_ = g.step(4), o.step(4)
+            for a, b in zip(gs, os_):
+                for k in KEYS:
+                    assert a[k] == b[k], (k, a, b)
+            lanes, slf = g.clocks()
+            dl = g.delivered()
+            for lv in range(g.n_local):
+                v = g.v_lo + lv
+                assert g.clock(lv, lanes, slf) == sorted(o.clock(v)), v
+                assert g.buffered(lv) == o.buffered(v), v
+                assert int(dl[lv]) == o.delivered(v), v
+        g.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,m,period,dmax,redeliver", [(2, 600, 16, 1, 4, 1), (4, 1001, 64, 2, 5, 2),
+                                                              (3, 500, 7, 3, 6, 1)])
+def test_sharded_causal_matches_oracle(world, n, m, period, dmax, redeliver):
+    res = run_world(_worker, world, n, m, period, dmax, redeliver, "gloo")
+    for r in range(world):
+        assert res[r] == "ok", res[r]
+
+
+@pytest.mark.gpu
+def test_sharded_causal_nccl_world1():
+    res = run_world(_worker, 1, 800, 64, 1, 4, 1, "nccl")
+    assert res[0] == "ok", res[0]

@@ -15,6 +15,15 @@ __global__ void scatter32(uint32_t* __restrict__ out, const uint32_t* __restrict
 __global__ void scatter8(uint8_t* __restrict__ out, const uint32_t* __restrict__ idx, uint32_t m, uint32_t mask) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[idx[i] & mask] = 1;
 }
+__global__ void scatter16(uint16_t* __restrict__ out, const uint32_t* __restrict__ idx, uint32_t m, uint32_t mod) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[idx[i] % mod] = (uint16_t)i;
+}
+__global__ void scatter8m(uint8_t* __restrict__ out, const uint32_t* __restrict__ idx, uint32_t m, uint32_t mod) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[idx[i] % mod] = (uint8_t)i;
+}
+__global__ void gather128(uint4* __restrict__ out, const uint4* __restrict__ in, const uint32_t* __restrict__ idx, uint32_t m, uint32_t mod) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i & 1023] = in[idx[i] % mod];
+}
 __global__ void gather32(uint32_t* __restrict__ out, const uint32_t* __restrict__ in, const uint32_t* __restrict__ idx, uint32_t m) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = in[idx[i]];
 }
@@ -66,6 +75,28 @@ int main() {
     T("scan 1B/thread 10MB", 1.0 * N, [&] { hipLaunchKernelGGL(scan8, g, blk, 0, 0, flags, N, cnt); });
     T("scan 16B/thread 10MB", 1.0 * N, [&] { hipLaunchKernelGGL(scan128, dim3(2048), blk, 0, 0, (const uint4*)flags, N / 16, cnt); });
     T("scan 16B/thread 200MB", 4.0 * E, [&] { hipLaunchKernelGGL(scan128, g, blk, 0, 0, (const uint4*)buf, E / 4, cnt); });
+    // working-set sizes for a narrower inbox (u8 / u16 words) and sender-state gathers
+    uint8_t* b8; CK(hipMalloc(&b8, E));
+    T("scatter 1B into 50MB  (26M)", 1.0 * M, [&] { hipLaunchKernelGGL(scatter8m, g, blk, 0, 0, b8, idx, M, E); });
+    T("scatter 2B into 100MB (26M)", 2.0 * M, [&] { hipLaunchKernelGGL(scatter16, g, blk, 0, 0, (uint16_t*)buf, idx, M, E); });
+    T("scatter 4B into 50MB  (26M)", 4.0 * M, [&] { hipLaunchKernelGGL(scatter16, g, blk, 0, 0, (uint16_t*)buf, idx, M, E / 2); });
+    T("gather 16B from 160MB (26M)", 16.0 * M, [&] { hipLaunchKernelGGL(gather128, g, blk, 0, 0, (uint4*)out, (const uint4*)buf, idx, M, N); });
+    // region-grouped: targets grouped by 256 KB region, random inside it
+    {
+        std::vector<uint32_t> hr(h);
+        std::stable_sort(hr.begin(), hr.end(), [](uint32_t x, uint32_t y) { return (x >> 16) < (y >> 16); });
+        std::vector<uint32_t> tmp(hr);
+        // shuffle inside each region so the writes are not sequential
+        for (size_t i = 0; i < hr.size();) {
+            size_t j = i;
+            while (j < hr.size() && (hr[j] >> 16) == (hr[i] >> 16)) j++;
+            std::shuffle(hr.begin() + i, hr.begin() + j, rng);
+            i = j;
+        }
+        CK(hipMemcpy(idx, hr.data(), M * 4, hipMemcpyHostToDevice));
+        T("scatter 4B into 200MB, 256KB-region grouped", 4.0 * M, [&] { hipLaunchKernelGGL(scatter32, g, blk, 0, 0, buf, idx, M); });
+        CK(hipMemcpy(idx, h.data(), M * 4, hipMemcpyHostToDevice));
+    }
     // sorted-within-chunk scatter: idx sorted in 64K windows (locality)
     std::vector<uint32_t> hs(h);
     for (uint32_t i = 0; i < M; i += 65536) std::sort(hs.begin() + i, hs.begin() + std::min<uint32_t>(M, i + 65536));
