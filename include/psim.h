@@ -154,6 +154,25 @@ int  psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, voi
 int  psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts,
                       psim_round_stats* stats, int64_t* local_live);
 int  psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records);
+/* Dense, host-sync-free exchange (what bench.py drives over RCCL): every
+ * remote slot has a fixed word position in the send buffer (region d of
+ * psim_shard_layout, in this shard's slot order; 0 = nothing sent), so the
+ * caller moves fixed-size regions (all-to-all with static split sizes; the
+ * receive regions are psim_shard_recv_layout) with no count exchange.
+ * psim_set_stream puts the handle's work on the caller's stream (e.g. torch's
+ * current stream, so kernels and RCCL are stream-ordered); rounds are
+ * enqueued by psim_shard_round_async and their stats fetched, with one sync,
+ * by psim_shard_collect (<= 16 pending). local_live[i] = this shard's
+ * outstanding rows to live peers after pending round i. */
+int  psim_set_stream(psim_handle* h, void* hip_stream);
+int  psim_shard_recv_layout(const psim_handle* h, uint64_t* recv_base, size_t world);
+int  psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_words);
+int  psim_shard_round_async(psim_handle* h, void* send_words);
+int  psim_shard_ingest_dense(psim_handle* h, const void* recv_words);
+int  psim_shard_collect(psim_handle* h, psim_round_stats* stats, size_t cap, uint32_t* n_rounds, int64_t* local_live);
+/* The last `rounds` collected rounds ran after global quiescence (no-ops):
+ * they do not advance the timer schedule (lazy tick phase), as in psim_run. */
+int  psim_shard_uncount(psim_handle* h, uint32_t rounds);
 
 /* --- partisan_vclock on dense lanes ----------------------------------- */
 /* A clock is PSIM_VC_LANES u32 lanes, lane i = actor i (actor ids are ranks

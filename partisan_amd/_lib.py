@@ -136,6 +136,13 @@ SIGNATURES = {
                                        _P(C.c_int64)]),
     "psim_shard_round": (C.c_int, [_H, C.c_void_p, C.c_uint64, _P(C.c_uint64), _P(RoundStats), _P(C.c_int64)]),
     "psim_shard_ingest": (C.c_int, [_H, C.c_void_p, C.c_uint64]),
+    "psim_set_stream": (C.c_int, [_H, C.c_void_p]),
+    "psim_shard_recv_layout": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
+    "psim_shard_broadcast_dense": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), C.c_void_p]),
+    "psim_shard_round_async": (C.c_int, [_H, C.c_void_p]),
+    "psim_shard_ingest_dense": (C.c_int, [_H, C.c_void_p]),
+    "psim_shard_collect": (C.c_int, [_H, _P(RoundStats), C.c_size_t, _P(C.c_uint32), _P(C.c_int64)]),
+    "psim_shard_uncount": (C.c_int, [_H, C.c_uint32]),
     "psim_demers_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_demers_broadcast_all": (C.c_int, [_H]),
     "psim_demers_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),

@@ -462,6 +462,34 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2
     a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
 }
 
+// Dense exchange (no counts, no host sync): word i of the send buffer is the
+// staged word of the i-th remote slot in the static order of psim_shard_layout
+// (zero when nothing was sent over that slot this round).
+__global__ __launch_bounds__(kBlock) void pt_pack_dense_kernel(PtArgs a, const uint32_t* __restrict__ rem, uint32_t nrem,
+                                                               uint32_t* __restrict__ send) {
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrem; i += stride) {
+        const uint32_t e = rem[i];
+        const uint32_t w = a.stage[e];
+        send[i] = w;
+        if (w) a.stage[e] = 0;
+    }
+}
+
+// ... and word i of the receive buffer feeds local receiver slot recv_map[i].
+__global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const uint32_t* __restrict__ recv,
+                                                                 const uint32_t* __restrict__ recv_map, uint32_t nrecv,
+                                                                 const uint32_t* __restrict__ slot2v) {
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrecv; i += stride) {
+        const uint32_t w = recv[i];
+        if (!w) continue;
+        const uint32_t ls = recv_map[i];
+        a.in_nxt[ls] = w;
+        a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+    }
+}
+
 uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }
 
 uint32_t grid_for(uint32_t n) {
@@ -497,6 +525,20 @@ hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* 
 hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s) {
     if (nrec == 0) return hipSuccess;
     hipLaunchKernelGGL(pt_ingest_kernel, dim3((nrec + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a, rec, nrec, slot2v);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_pack_dense(const PtArgs& a, const uint32_t* rem, uint32_t nrem, uint32_t* send, hipStream_t s) {
+    if (nrem == 0) return hipSuccess;
+    hipLaunchKernelGGL(pt_pack_dense_kernel, dim3(grid_for(nrem)), dim3(kBlock), 0, s, a, rem, nrem, send);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_ingest_dense(const PtArgs& a, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,
+                                  const uint32_t* slot2v, hipStream_t s) {
+    if (nrecv == 0) return hipSuccess;
+    hipLaunchKernelGGL(pt_ingest_dense_kernel, dim3(grid_for(nrecv)), dim3(kBlock), 0, s, a, recv, recv_map, nrecv,
+                       slot2v);
     return hipGetLastError();
 }
 

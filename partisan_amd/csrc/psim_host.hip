@@ -76,7 +76,16 @@ struct psim_handle {
         uint32_t* cursor = nullptr;      // [world] records packed per region this round
         uint32_t* slot2v = nullptr;      // [E_local] receiver vertex of a local slot
         std::vector<uint64_t> send_base; // host copy, world + 1 entries (last = total)
+        // dense exchange: word i of the receive buffer feeds local slot recv_map[i];
+        // the region of source s is [recv_base[s], recv_base[s+1]) in that source's slot order
+        uint32_t* recv_map = nullptr;
+        std::vector<uint64_t> recv_base;
+        // async rounds (psim_shard_round_async): per-round stats + events ring
+        unsigned long long* ring = nullptr;   // [kRing][kStatShards][kNStat]
+        hipEvent_t rev_[2 * 16] = {};
+        uint32_t pending = 0;
     } sh;
+    hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
 
     // Demers epidemic state (demers.hip)
     struct Dm {
@@ -186,10 +195,12 @@ void free_graph(psim_handle* h) {
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
     auto& sh = h->sh;
-    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v};
+    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map};
     for (void* p : sp)
         if (p) (void)hipFree(p);
-    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = nullptr;
+    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = nullptr;
+    sh.recv_base.clear();
+    sh.pending = 0;
     sh.blk = nullptr;
     sh.nblk = 0;
     sh.send_base.clear();
@@ -376,6 +387,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             break;
         }
         if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { rc = PSIM_EHIP; break; }
+        h->own_stream = h->stream;
+        if (hipMalloc(&h->sh.ring, 16 * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        for (auto& e : h->sh.rev_)
+            if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
         if (hipMalloc(&h->stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipHostMalloc(&h->h_stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
@@ -393,6 +408,7 @@ int psim_destroy(psim_handle* h) {
     if (!h) return PSIM_EINVAL;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
     free_graph(h);
     free_demers(h);
     free_hv(h);
@@ -408,7 +424,11 @@ int psim_destroy(psim_handle* h) {
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    for (auto& e : h->sh.rev_)
+        if (e) (void)hipEventDestroy(e);
+    if (h->sh.ring) (void)hipFree(h->sh.ring);
+    if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return PSIM_OK;
 }
@@ -522,6 +542,19 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         remflat.insert(remflat.end(), remd[d].begin(), remd[d].end());
     }
     sbases[W] = remflat.size();
+    // receive side: for each source shard in order, the local slots it feeds,
+    // in the source's own slot order (= the order of its region for us)
+    std::vector<uint32_t> recvflat;
+    std::vector<uint64_t> rbases(W + 1, 0);
+    if (W > 1)
+        for (uint32_t src = 0; src < W; src++) {
+            rbases[src] = recvflat.size();
+            if (src == (uint32_t)sh.rank) continue;
+            const uint32_t slo = uint32_t((uint64_t(n) * src) / W), shi = uint32_t((uint64_t(n) * (src + 1)) / W);
+            for (uint64_t e = rp[slo]; e < rp[shi]; e++)
+                if (cc[e] >= lo && cc[e] < hi) recvflat.push_back(uint32_t(rev[e] - sbase));
+        }
+    rbases[W] = recvflat.size();
     // device arrays
     auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
     const size_t nw = (size_t(n) + 31) / 32;
@@ -537,7 +570,8 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
                    alloc((void**)&sh.blk, blks.size() * 16) != hipSuccess ||
                    alloc((void**)&sh.send_base_d, W * 4) != hipSuccess ||
                    alloc((void**)&sh.cursor, W * 4) != hipSuccess ||
-                   alloc((void**)&sh.slot2v, El * 4) != hipSuccess))) {
+                   alloc((void**)&sh.slot2v, El * 4) != hipSuccess ||
+                   alloc((void**)&sh.recv_map, recvflat.size() * 4) != hipSuccess))) {
         free_graph(h);
         return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", nl, (unsigned long long)El);
     }
@@ -567,9 +601,12 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         HIPCHK(h, hipMemcpy(sh.blk, blks.data(), blks.size() * 16, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(sh.send_base_d, sb32.data(), W * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(sh.slot2v, s2v.data(), El * 4, hipMemcpyHostToDevice));
+        if (!recvflat.empty())
+            HIPCHK(h, hipMemcpy(sh.recv_map, recvflat.data(), recvflat.size() * 4, hipMemcpyHostToDevice));
         sh.nblk = uint32_t(blks.size());
     }
     sh.send_base = sbases;
+    sh.recv_base = rbases;
     HIPCHK(h, hipDeviceSynchronize());
     {
         std::vector<uint64_t> rpl64(size_t(nl) + 1);
@@ -786,6 +823,114 @@ int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t
     }
     if (local_live) *local_live = h->live_rows;
     return shard_pack(h, send_dev, send_cap, counts);
+}
+
+int psim_set_stream(psim_handle* h, void* stream) {
+    if (!h) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    return PSIM_OK;
+}
+
+int psim_shard_recv_layout(const psim_handle* h, uint64_t* recv_base, size_t world) {
+    if (!h || !recv_base || world != (size_t)h->sh.world || h->sh.recv_base.size() != world + 1) return PSIM_EINVAL;
+    memcpy(recv_base, h->sh.recv_base.data(), (world + 1) * 8);
+    return PSIM_OK;
+}
+
+int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev) {
+    if (!h) return PSIM_EINVAL;
+    if (h->sh.world > 1 && !send_dev) return PSIM_EINVAL;
+    if (h->sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
+    unsigned long long r[kNStat];
+    int rc = broadcast_common(h, root, mono_out, r);
+    if (rc) return rc;
+    PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+    HIPCHK(h, launch_pt_pack_dense(a, h->sh.rem, (uint32_t)h->sh.send_base[h->sh.world], (uint32_t*)send_dev,
+                                   h->stream));
+    return PSIM_OK;
+}
+
+int psim_shard_round_async(psim_handle* h, void* send_dev) {
+    if (!h) return PSIM_EINVAL;
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    auto& sh = h->sh;
+    if (sh.world > 1 && !send_dev) return PSIM_EINVAL;
+    if (sh.pending >= 16) return fail(h, PSIM_ESTATE, "16 async rounds pending: call psim_shard_collect");
+    HIPCHK(h, hipSetDevice(h->device));
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    const uint32_t tick = ((h->round + 1) % L) == 0;
+    unsigned long long* row = sh.ring + size_t(sh.pending) * kStatsRow;
+    HIPCHK(h, hipMemsetAsync(row, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+    PtArgs a = make_args(h, h->par, tick, row);
+    HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
+    HIPCHK(h, launch_pt_round(a, h->stream));
+    HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending + 1], h->stream));
+    if (sh.world > 1)
+        HIPCHK(h, launch_pt_pack_dense(a, sh.rem, (uint32_t)sh.send_base[sh.world], (uint32_t*)send_dev, h->stream));
+    h->par ^= 1u;
+    h->round++;
+    sh.pending++;
+    return PSIM_OK;
+}
+
+int psim_shard_ingest_dense(psim_handle* h, const void* recv_dev) {
+    if (!h) return PSIM_EINVAL;
+    auto& sh = h->sh;
+    const uint64_t nr = sh.recv_base.empty() ? 0 : sh.recv_base[sh.world];
+    if (nr == 0) return PSIM_OK;
+    if (!recv_dev) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
+    HIPCHK(h, launch_pt_ingest_dense(a, (const uint32_t*)recv_dev, sh.recv_map, (uint32_t)nr, sh.slot2v, h->stream));
+    return PSIM_OK;
+}
+
+int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32_t* n_out, int64_t* local_live) {
+    if (!h) return PSIM_EINVAL;
+    auto& sh = h->sh;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint32_t k = sh.pending;
+    std::vector<unsigned long long> hs(size_t(k) * kStatsRow);
+    if (k) HIPCHK(h, hipMemcpy(hs.data(), sh.ring, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    sh.pending = 0;
+    for (uint32_t i = 0; i < k; i++) {
+        unsigned long long r[kNStat];
+        reduce_row(hs.data() + size_t(i) * kStatsRow, r);
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, sh.rev_[2 * i], sh.rev_[2 * i + 1]));
+        if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "async round: overflow flags 0x%llx", r[S_OVERFLOW]);
+        uint64_t msgs = 0;
+        for (int t = 1; t <= 5; t++) msgs += r[t];
+        h->ost_cnt += (int64_t)r[S_OST_DELTA];
+        h->live_rows += (int64_t)r[S_LIVE_DELTA];
+        h->inflight = msgs;
+        h->kernel_ms_total += ms;
+        h->rounds_total++;
+        if (out && i < cap) {
+            psim_round_stats& o = out[i];
+            memset(&o, 0, sizeof o);
+            for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
+            o.delivered_new = r[S_DELIV];
+            o.active = r[S_ACTIVE];
+            o.senders = r[S_SENDERS];
+            o.sender_degree_sum = r[S_DEGSUM];
+            o.outstanding_vertices = (uint64_t)h->ost_cnt;
+            o.algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+            o.kernel_ms = ms;
+        }
+        if (local_live && i < cap) local_live[i] = h->live_rows;
+    }
+    if (n_out) *n_out = k;
+    return PSIM_OK;
+}
+
+int psim_shard_uncount(psim_handle* h, uint32_t rounds) {
+    if (!h || rounds > h->round || h->sh.pending) return PSIM_EINVAL;
+    h->round -= rounds;
+    return PSIM_OK;
 }
 
 int psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records) {

@@ -252,5 +252,8 @@ hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
                              const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s);
 hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s);
+hipError_t launch_pt_pack_dense(const PtArgs& a, const uint32_t* rem, uint32_t nrem, uint32_t* send, hipStream_t s);
+hipError_t launch_pt_ingest_dense(const PtArgs& a, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,
+                                  const uint32_t* slot2v, hipStream_t s);
 
 }  // namespace psim

@@ -35,6 +35,18 @@ class ShardedPlumtree:
         self.counts = (C.c_uint64 * world)()
         self.local_algo_bytes = 0      # this GPU's SURVEY 8(d) bytes over the rounds run
         self.local_kernel_ms = 0.0     # this GPU's pt_round_kernel time (hipEvent)
+        # dense exchange: fixed word positions per remote slot, static split sizes
+        rb = (C.c_uint64 * (world + 1))()
+        check(lib().psim_shard_recv_layout(self._h, rb, world), self._h)
+        self.rbase = [int(x) for x in rb]
+        self.in_splits = [self.base[d + 1] - self.base[d] for d in range(world)]
+        self.out_splits = [self.rbase[s + 1] - self.rbase[s] for s in range(world)]
+        self.send_w = torch.zeros(max(1, self.base[world]), dtype=torch.int32, device=self.dev)
+        self.recv_w = torch.zeros(max(1, self.rbase[world]), dtype=torch.int32, device=self.dev)
+        self.chunk_rounds = 4
+        if backend == "nccl":   # kernels and RCCL ordered on torch's current stream: no host sync per round
+            check(lib().psim_set_stream(self._h, C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)),
+                  self._h)
 
     # -------------------------------------------------------------- exchange
     def _allreduce(self, vals):
@@ -78,6 +90,22 @@ class ShardedPlumtree:
         if total:
             check(lib().psim_shard_ingest(self._h, C.c_void_p(self.recv.data_ptr()), total), self._h)
 
+    def _exchange_dense(self):
+        W = self.world
+        if W == 1:
+            return
+        if self.backend == "nccl":
+            dist.all_to_all_single(self.recv_w[:self.rbase[W]], self.send_w[:self.base[W]],
+                                   self.out_splits, self.in_splits)
+        else:
+            torch.cuda.synchronize(self.dev)
+            hs = self.send_w[:self.base[W]].cpu()
+            hr = torch.zeros(self.rbase[W], dtype=torch.int32)
+            dist.all_to_all_single(hr, hs, self.out_splits, self.in_splits)
+            self.recv_w[:self.rbase[W]].copy_(hr.to(self.dev))
+            torch.cuda.synchronize(self.dev)
+        check(lib().psim_shard_ingest_dense(self._h, C.c_void_p(self.recv_w.data_ptr())), self._h)
+
     # -------------------------------------------------------------- protocol
     def reset_trees(self):
         self.sim.reset_trees()
@@ -87,33 +115,55 @@ class ShardedPlumtree:
 
     def broadcast(self, root):
         mono = C.c_uint32()
-        live = C.c_int64()
-        check(lib().psim_shard_broadcast(self._h, root, C.byref(mono), C.c_void_p(self.send.data_ptr()), self.cap,
-                                         self.counts, C.byref(live)), self._h)
-        self._exchange()
+        check(lib().psim_shard_broadcast_dense(self._h, root, C.byref(mono), C.c_void_p(self.send_w.data_ptr())),
+              self._h)
+        self._exchange_dense()
         return mono.value
 
+    KEYS = ["broadcast", "prune", "i_have", "ignored_i_have", "graft", "delivered_new", "senders",
+            "sender_degree_sum", "algo_bytes"]
+
     def run(self, max_rounds=100000):
-        """Rounds until global quiescence; returns (per-round GLOBAL stats, rounds)."""
+        """Rounds until global quiescence; returns (per-round GLOBAL stats, rounds).
+
+        Rounds are enqueued in chunks of `chunk_rounds` (kernel -> all-to-all ->
+        ingest, stream-ordered) and their counters collected with one sync and
+        one all-reduce per chunk; rounds after the first globally quiescent one
+        changed nothing and are not counted (as in psim_run)."""
         out, rounds = [], 0
-        st = RoundStats()
-        live = C.c_int64()
+        K = self.chunk_rounds
+        keys = self.KEYS
         while rounds < max_rounds:
-            check(lib().psim_shard_round(self._h, C.c_void_p(self.send.data_ptr()), self.cap, self.counts,
-                                         C.byref(st), C.byref(live)), self._h)
-            self._exchange()
-            d = st.as_dict()
-            self.local_algo_bytes += d["algo_bytes"]
-            self.local_kernel_ms += d["kernel_ms"]
-            keys = ["broadcast", "prune", "i_have", "ignored_i_have", "graft", "delivered_new", "senders",
-                    "sender_degree_sum", "algo_bytes"]
-            g = self._allreduce([d[k] for k in keys] + [int(live.value)])
-            gd = dict(zip(keys, g[:-1]))
-            gd["kernel_ms"] = d["kernel_ms"]
-            gd["live_rows"] = g[-1]
-            out.append(gd)
-            rounds += 1
-            if sum(gd[k] for k in keys[:5]) == 0 and g[-1] == 0:
+            k = min(K, max_rounds - rounds)
+            for _ in range(k):
+                check(lib().psim_shard_round_async(self._h, C.c_void_p(self.send_w.data_ptr())), self._h)
+                self._exchange_dense()
+            st = (RoundStats * k)()
+            live = (C.c_int64 * k)()
+            got = C.c_uint32()
+            check(lib().psim_shard_collect(self._h, st, k, C.byref(got), live), self._h)
+            loc = [s.as_dict() for s in st[:got.value]]
+            flat = []
+            for d, lv in zip(loc, live):
+                flat += [d[x] for x in keys] + [int(lv)]
+            g = self._allreduce(flat)
+            done = False
+            for i, d in enumerate(loc):
+                row = g[i * (len(keys) + 1):(i + 1) * (len(keys) + 1)]
+                gd = dict(zip(keys, row[:-1]))
+                gd["kernel_ms"] = d["kernel_ms"]
+                gd["live_rows"] = row[-1]
+                out.append(gd)
+                rounds += 1
+                self.local_algo_bytes += d["algo_bytes"]
+                self.local_kernel_ms += d["kernel_ms"]
+                if sum(gd[x] for x in keys[:5]) == 0 and row[-1] == 0:
+                    done = True
+                    extra = len(loc) - (i + 1)
+                    if extra:
+                        check(lib().psim_shard_uncount(self._h, extra), self._h)
+                    break
+            if done:
                 break
         return out, rounds
 
