@@ -403,6 +403,41 @@ int  psim_scamp_get_views(const psim_handle* h, uint32_t* pv, uint32_t* npv, uin
 int  psim_scamp_get_nodes(const psim_handle* h, uint64_t* draws, int32_t* last_ping, uint8_t* alive, size_t n);
 int  psim_scamp_inflight(const psim_handle* h, uint64_t* messages);
 
+/* --- C3: Plumtree repair over churning SCAMP v2 ------------------------
+ * The pluggable manager runs SCAMP v2 (the psim_scamp_* state of this
+ * handle) and the Plumtree server reacts to its {update, Members} casts
+ * (partisan_plumtree_broadcast.erl:607-639); Plumtree sends need a
+ * connection, i.e. the destination in the sender's partial view.  A round:
+ * the SCAMP round, then the Plumtree round (the round's updates in order,
+ * the inbox in (src, seq) order, the lazy tick).  A crash restarts both
+ * processes (start_link/0 with members = {self}).  psim_scamp_get_views /
+ * _get_nodes read the membership side. */
+typedef struct psim_c3_stats {
+    psim_scamp_stats scamp;        /* the membership round                      */
+    uint64_t pt_sent[6];           /* [k] Plumtree messages of PSIM_MSG_* kind k */
+    uint64_t pt_dropped;           /* Plumtree sends without a connection        */
+    uint64_t delivered_new;        /* Mod:merge/2 returned true                  */
+    uint64_t active;               /* vertices that handled messages             */
+    uint64_t updates;              /* {update, Members} casts applied            */
+    uint64_t delivered_live;       /* live vertices holding the current heartbeat */
+    uint64_t live;                 /* live vertices                              */
+    uint64_t outstanding_live;     /* outstanding rows to connected live peers   */
+    uint64_t pt_algo_bytes;        /* bytes the Plumtree round must move */
+    double   pt_kernel_ms;
+} psim_c3_stats;
+int  psim_c3_setup(psim_handle* h, uint32_t n, uint32_t c, uint32_t periodic_rounds);
+int  psim_c3_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k);
+int  psim_c3_crash(psim_handle* h, const uint32_t* v, size_t k);
+/* heartbeat at `root` (backend :341-368 -> broadcast :565-569) */
+int  psim_c3_heartbeat(psim_handle* h, uint32_t root, uint32_t* mono_out);
+int  psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* stats, size_t cap);
+/* vertex v's Plumtree state: all_eager_peers / all_lazy_peers / outstanding
+ * rows (sorted ids, up to cap each), the heartbeat serial it delivered (0 =
+ * none) and its pushed Round */
+int  psim_c3_get_plumtree(const psim_handle* h, uint32_t v, uint32_t* eager, size_t* ne, uint32_t* lazy, size_t* nl,
+                          uint32_t* outstanding, size_t* no, size_t cap, uint32_t* delivered_mono,
+                          uint32_t* recv_round);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

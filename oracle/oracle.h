@@ -301,6 +301,41 @@ size_t orc_scamp_view(const orc_scamp* s, uint32_t v, int which, uint32_t* out, 
 uint64_t orc_scamp_draws(const orc_scamp* s, uint32_t v);
 int orc_scamp_alive(const orc_scamp* s, uint32_t v);
 int64_t orc_scamp_last_ping(const orc_scamp* s, uint32_t v);
+int orc_scamp_has_member(const orc_scamp* s, uint32_t v, uint32_t t);
+/* called after every handler that fires partisan_peer_service_events:update(Members) */
+typedef void (*orc_scamp_update_fn)(void* ctx, uint32_t v, const uint32_t* members, size_t n);
+void orc_scamp_set_update_hook(orc_scamp* s, orc_scamp_update_fn fn, void* ctx);
+
+/* ------------------------------------------------------------------ */
+/* C3: Plumtree repair over churning SCAMP v2 views                      */
+/* ------------------------------------------------------------------ */
+/* Plumtree hooks used by the composition: a connection predicate for sends
+ * (default: every peer), a node restart (start_link/0 with members = {self},
+ * the backend's timestamps lost, in-flight messages to it dropped), and
+ * {update, Members} casts applied at the start of the next round in order. */
+typedef int (*orc_pt_conn_fn)(void* ctx, uint32_t u, uint32_t t);
+void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx);
+void orc_pt_restart(orc_plumtree* s, uint32_t v);
+void orc_pt_queue_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n);
+uint64_t orc_pt_dropped(const orc_plumtree* s);
+
+typedef struct orc_c3 orc_c3;
+typedef struct orc_c3_stats {
+    orc_scamp_stats scamp;
+    orc_round_stats pt;
+    uint64_t updates;            /* {update, Members} casts delivered to plumtree */
+    uint64_t pt_dropped;         /* plumtree sends to a non-connected peer */
+    uint64_t delivered_live;     /* live vertices holding the current heartbeat after the round */
+    uint64_t live;               /* live vertices */
+} orc_c3_stats;
+orc_c3* orc_c3_create(uint32_t n, uint32_t c, uint32_t periodic_rounds, uint64_t seed);
+void orc_c3_destroy(orc_c3* s);
+orc_scamp* orc_c3_scamp(orc_c3* s);
+orc_plumtree* orc_c3_plumtree(orc_c3* s);
+void orc_c3_join(orc_c3* s, uint32_t v, uint32_t contact);
+void orc_c3_crash(orc_c3* s, uint32_t v);            /* crash + restart now (both processes) */
+uint32_t orc_c3_heartbeat(orc_c3* s, uint32_t root);
+uint32_t orc_c3_step(orc_c3* s, uint32_t rounds, orc_c3_stats* st);
 
 #ifdef __cplusplus
 }

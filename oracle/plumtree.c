@@ -104,6 +104,8 @@ typedef struct {
     recvrec* rr; size_t nrr, caprr;
     uint32_t hb_epoch, hb_monotonic;      /* backend #state{epoch, monotonic} */
     uint64_t seq;                         /* emission counter (FIFO order)    */
+    uint32_t* upd; size_t nupd, capupd;   /* queued {update, Members}: [len, ids...] records */
+    uint8_t fresh;                        /* restarted since the last round: inbox dropped */
 } node_t;
 
 struct orc_plumtree {
@@ -114,11 +116,21 @@ struct orc_plumtree {
     orc_msg* cur; size_t ncur, capcur;    /* being processed this round */
     orc_msg* nxt; size_t nnxt, capnxt;    /* emitted, delivered next round */
     orc_round_stats* st;                   /* stats of the running round */
+    orc_pt_conn_fn conn;                   /* partisan:cast_message needs a connection (C3) */
+    void* conn_ctx;
+    uint64_t dropped;                      /* sends to a non-connected peer */
 };
+
+void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx) { s->conn = fn; s->conn_ctx = ctx; }
+uint64_t orc_pt_dropped(const orc_plumtree* s) { return s->dropped; }
 
 /* ---------------- message emission: partisan:cast_message via send/3 ---- */
 static void emit(orc_plumtree* s, uint32_t src, uint32_t dst, uint32_t type,
                  uint32_t round, uint32_t root, uint32_t idn, uint32_t ide, uint32_t idm) {
+    if (s->conn && !s->conn(s->conn_ctx, src, dst)) {    /* do_send_message: no connection, dropped */
+        s->dropped++;
+        return;
+    }
     if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? s->capnxt * 2 : 1024; s->nxt = (orc_msg*)realloc(s->nxt, s->capnxt * sizeof(orc_msg)); }
     orc_msg* m = &s->nxt[s->nnxt++];
     m->type = type; m->src = src; m->dst = dst; m->round = round; m->root = root;
@@ -298,6 +310,7 @@ static void send_lazy(orc_plumtree* s, uint32_t v) {
     for (size_t i = 0; i < nd->nout; i++) {
         outrow r = nd->out[i];
         if (!s->alive[r.peer]) continue;           /* partisan:is_connected(Peer) (Q5, Q30) */
+        if (s->conn && !s->conn(s->conn_ctx, v, r.peer)) continue;
         emit(s, v, r.peer, ORC_MSG_IHAVE, r.round, r.root, r.id_node, r.id_epoch, r.id_mono);
     }
 }
@@ -331,7 +344,7 @@ void orc_pt_destroy(orc_plumtree* s) {
         free(nd->eager_sets.e); free(nd->lazy_sets.e);
         free(nd->out);
         for (size_t i = 0; i < nd->nts; i++) free(nd->ts[i].is);
-        free(nd->ts); free(nd->rr);
+        free(nd->ts); free(nd->rr); free(nd->upd);
     }
     free(s->nodes); free(s->alive); free(s->cur); free(s->nxt);
     free(s);
@@ -382,6 +395,33 @@ int orc_pt_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n
     return 0;
 }
 
+/* crash + restart: start_link/0 with the peer service's members = {self};
+ * the backend's timestamp table is lost (a new node) */
+void orc_pt_restart(orc_plumtree* s, uint32_t v) {
+    node_t* nd = &s->nodes[v];
+    oset self = {0}, empty = {0};
+    os_add(&self, v);
+    reset_peers(nd, v, &self, &self, &empty);
+    os_free(&self);
+    nd->nout = 0;
+    for (size_t i = 0; i < nd->nts; i++) free(nd->ts[i].is);
+    nd->nts = 0;
+    nd->nrr = 0;
+    nd->nupd = 0;
+    nd->fresh = 1;
+}
+
+void orc_pt_queue_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n) {
+    node_t* nd = &s->nodes[v];
+    if (nd->nupd + n + 1 > nd->capupd) {
+        nd->capupd = (nd->nupd + n + 1) * 2;
+        nd->upd = (uint32_t*)realloc(nd->upd, nd->capupd * 4);
+    }
+    nd->upd[nd->nupd++] = (uint32_t)n;
+    memcpy(nd->upd + nd->nupd, members, n * 4);
+    nd->nupd += n;
+}
+
 void orc_pt_reset_peers_all(orc_plumtree* s) {
     for (uint32_t v = 0; v < s->n; v++) {
         node_t* nd = &s->nodes[v];
@@ -408,16 +448,28 @@ static void one_round(orc_plumtree* s, orc_round_stats* st) {
     s->cur = s->nxt; s->ncur = s->nnxt; s->capcur = s->capnxt;
     s->nxt = t; s->nnxt = 0; s->capnxt = tc;
     qsort(s->cur, s->ncur, sizeof(orc_msg), msg_cmp);
+    /* {update, Members} casts queued since the last round, in order (C3) */
+    for (uint32_t v = 0; v < s->n; v++) {
+        node_t* nd = &s->nodes[v];
+        size_t i = 0;
+        while (i < nd->nupd) {
+            const uint32_t k = nd->upd[i];
+            if (s->alive[v]) orc_pt_update(s, v, nd->upd + i + 1, k);
+            i += 1 + k;
+        }
+        nd->nupd = 0;
+    }
     uint64_t maxe = 0, run = 0;
     uint32_t last_dst = 0xFFFFFFFFu;
     for (size_t i = 0; i < s->ncur; i++) {
         const orc_msg* m = &s->cur[i];
         if (i > 0 && s->cur[i - 1].dst == m->dst && s->cur[i - 1].src == m->src) run++; else run = 1;
         if (run > maxe) maxe = run;
-        if (!s->alive[m->dst]) continue;            /* lost on the wire */
+        if (!s->alive[m->dst] || s->nodes[m->dst].fresh) continue;   /* lost on the wire */
         if (m->dst != last_dst) { st->active++; last_dst = m->dst; }
         handle(s, m->dst, m);
     }
+    for (uint32_t v = 0; v < s->n; v++) s->nodes[v].fresh = 0;
     s->round++;
     if (s->round % s->lazy_tick_rounds == 0) {      /* handle_info(lazy_tick) */
         for (uint32_t v = 0; v < s->n; v++) {

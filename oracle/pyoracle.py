@@ -77,6 +77,16 @@ class ScampStats(C.Structure):
         return d
 
 
+class C3Stats(C.Structure):
+    _fields_ = [("scamp", ScampStats), ("pt", RoundStats)] + [(k, C.c_uint64) for k in (
+        "updates", "pt_dropped", "delivered_live", "live")]
+
+    def as_dict(self):
+        d = {"scamp": self.scamp.as_dict(), "pt": stats_dict(self.pt)}
+        d.update({k: int(getattr(self, k)) for k, _ in self._fields_[2:]})
+        return d
+
+
 HV_DEFAULTS = dict(active_max_size=6, active_min_size=3, active_rwl=6, passive_max_size=30, passive_rwl=6,
                    shuffle_k_active=3, shuffle_k_passive=4, shuffle_rounds=10, promotion_rounds=5)
 
@@ -233,6 +243,18 @@ def lib():
         L.orc_scamp_alive.argtypes = [C.c_void_p, C.c_uint32]
         L.orc_scamp_last_ping.argtypes = [C.c_void_p, C.c_uint32]
         L.orc_scamp_last_ping.restype = C.c_int64
+        L.orc_c3_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.orc_c3_create.restype = C.c_void_p
+        L.orc_c3_destroy.argtypes = [C.c_void_p]
+        L.orc_c3_scamp.argtypes = [C.c_void_p]
+        L.orc_c3_scamp.restype = C.c_void_p
+        L.orc_c3_plumtree.argtypes = [C.c_void_p]
+        L.orc_c3_plumtree.restype = C.c_void_p
+        L.orc_c3_join.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_c3_crash.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_c3_heartbeat.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_c3_heartbeat.restype = C.c_uint32
+        L.orc_c3_step.argtypes = [C.c_void_p, C.c_uint32, P(C3Stats)]
         _lib = L
     return _lib
 
@@ -790,3 +812,40 @@ class Scamp:
 
     def last_ping(self, v):
         return lib().orc_scamp_last_ping(self._h, v)
+
+
+# ---------------------------------------------------------------- C3
+class C3:
+    """Plumtree over churning SCAMP v2 (oracle/c3.c)."""
+
+    def __init__(self, n, c=5, periodic_rounds=10, seed=0):
+        self.n = n
+        self._h = lib().orc_c3_create(n, c, periodic_rounds, seed)
+        self.scamp = Scamp.__new__(Scamp)
+        self.scamp.n, self.scamp._h = n, lib().orc_c3_scamp(self._h)
+        self.pt = Plumtree.__new__(Plumtree)
+        self.pt.n, self.pt._h = n, lib().orc_c3_plumtree(self._h)
+
+    def close(self):
+        if self._h:
+            self.scamp._h = None   # owned by the composition
+            self.pt._h = None
+            lib().orc_c3_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def join(self, v, contact):
+        lib().orc_c3_join(self._h, v, contact)
+
+    def crash(self, v):
+        lib().orc_c3_crash(self._h, v)
+
+    def heartbeat(self, root):
+        return lib().orc_c3_heartbeat(self._h, root)
+
+    def step(self, rounds=1):
+        st = (C3Stats * rounds)()
+        lib().orc_c3_step(self._h, rounds, st)
+        return [x.as_dict() for x in st]

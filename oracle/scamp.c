@@ -105,7 +105,21 @@ struct orc_scamp {
     sccall* calls; size_t ncalls, capcalls;
     orc_scamp_stats* st;
     ulist before;             /* members of the vertex before the running handler */
+    orc_scamp_update_fn upd;  /* partisan_peer_service_events:update/1 listener (Plumtree, C3) */
+    void* upd_ctx;
 };
+
+void orc_scamp_set_update_hook(orc_scamp* s, orc_scamp_update_fn fn, void* ctx) { s->upd = fn; s->upd_ctx = ctx; }
+
+/* the manager fires update(Members) when the members list changed after a
+ * join (:1574-1579) or a membership message (:1756-1761), and always after a
+ * leave (:2107) */
+static void fire_update(orc_scamp* s, uint32_t v, int always) {
+    if (!s->upd) return;
+    const ulist* pv = &s->nd[v].pv;
+    int same = pv->n == s->before.n && memcmp(pv->a, s->before.a, pv->n * 4) == 0;
+    if (!same || always) s->upd(s->upd_ctx, v, pv->a, pv->n);
+}
 
 static void node_init(scnode* x, uint32_t v) {      /* init/1: [Myself] / sets {Myself} */
     x->pv.n = 0;
@@ -341,8 +355,11 @@ static void one_round(orc_scamp* s) {
         for (size_t i = 0; i < s->ncalls; i++) {
             sccall* c = &s->calls[i];
             if ((int)c->kind != kind || !s->alive[c->v]) continue;
-            if (kind == 1) do_leave(s, c->v, c->x);
-            else if (c->x != c->v && s->alive0[c->x]) do_join(s, c->v, c->x);   /* connect/1 to a live peer */
+            if (kind == 1) { do_leave(s, c->v, c->x); fire_update(s, c->v, 1); }
+            else if (c->x != c->v && s->alive0[c->x]) {                        /* connect/1 to a live peer */
+                do_join(s, c->v, c->x);
+                fire_update(s, c->v, 0);
+            }
         }
     s->ncalls = 0;
 
@@ -351,7 +368,9 @@ static void one_round(orc_scamp* s) {
         uint32_t v = m->dst;
         if (!s->alive[v] || s->nd[v].fresh) continue;
         if (s->st) s->st->processed++;
-        if (!do_message(s, v, m)) {
+        const int up = do_message(s, v, m);
+        fire_update(s, v, 0);
+        if (!up) {
             s->alive[v] = 0;
             if (s->st) s->st->stopped++;
         }
@@ -386,3 +405,4 @@ size_t orc_scamp_view(const orc_scamp* s, uint32_t v, int which, uint32_t* out, 
 uint64_t orc_scamp_draws(const orc_scamp* s, uint32_t v) { return s->nd[v].draws; }
 int orc_scamp_alive(const orc_scamp* s, uint32_t v) { return s->alive[v]; }
 int64_t orc_scamp_last_ping(const orc_scamp* s, uint32_t v) { return s->nd[v].last_ping; }
+int orc_scamp_has_member(const orc_scamp* s, uint32_t v, uint32_t t) { return lhas(&s->nd[v].pv, t); }

@@ -107,6 +107,18 @@ class ScampStats(C.Structure):
         return d
 
 
+class C3Stats(C.Structure):
+    _fields_ = [("scamp", ScampStats), ("pt_sent", C.c_uint64 * 6)] + [(k, C.c_uint64) for k in (
+        "pt_dropped", "delivered_new", "active", "updates", "delivered_live", "live", "outstanding_live",
+        "pt_algo_bytes")] + [("pt_kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        d = {"scamp": self.scamp.as_dict(), "pt_sent": {MSG_KINDS[t]: int(self.pt_sent[t]) for t in range(1, 6)}}
+        for k, _ in self._fields_[2:]:
+            d[k] = float(getattr(self, k)) if k == "pt_kernel_ms" else int(getattr(self, k))
+        return d
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 _P = C.POINTER
 _H = C.c_void_p
@@ -194,6 +206,14 @@ SIGNATURES = {
                                        C.c_size_t]),
     "psim_scamp_get_nodes": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_int32), _P(C.c_uint8), C.c_size_t]),
     "psim_scamp_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_c3_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "psim_c3_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_c3_crash": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
+    "psim_c3_heartbeat": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
+    "psim_c3_step": (C.c_int, [_H, C.c_uint32, _P(C3Stats), C.c_size_t]),
+    "psim_c3_get_plumtree": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), _P(C.c_size_t), _P(C.c_uint32),
+                                       _P(C.c_size_t), _P(C.c_uint32), _P(C.c_size_t), C.c_size_t,
+                                       _P(C.c_uint32), _P(C.c_uint32)]),
     "psim_vclock_descends": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 typedef struct psim_handle psim_handle;
+typedef struct psim_scamp_stats psim_scamp_stats;
 
 namespace psim {
 
@@ -223,16 +224,65 @@ struct ScArgs {
     const uint32_t* __restrict__ call_off;    // [n+1] calls of each vertex
     const uint32_t* __restrict__ calls;       // bit31 = leave, low bits = node / contact
     unsigned long long* __restrict__ stats;   // [16]
+    // partisan_peer_service_events:update(Members) as set deltas, per vertex in
+    // firing order (C3: consumed by the Plumtree engine); null = not recorded
+    uint32_t* __restrict__ ev_cnt;            // [n]
+    uint2* __restrict__ ev;                   // [n][kScEv] {new member, removed member}, 0xFFFFFFFF = none
 };
+constexpr uint32_t kScEv = 32;                // update events per vertex and round
+
+// The SCAMP engine's device state, for the C3 Plumtree engine (ptdyn.hip)
+struct ScView {
+    uint32_t n;
+    const uint32_t* pv;                   // [n][kScPv]
+    const ScHead* head;
+    uint8_t* alive;
+    uint32_t* ev_cnt;
+    uint2* ev;
+};
+int scamp_view(psim_handle* h, ScView* out, bool want_events);   // PSIM_ESTATE without psim_scamp_setup
+int scamp_round(psim_handle* h, psim_scamp_stats* out);          // one SCAMP round (calls made so far)
+int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k);
 hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
+
+// C3: Plumtree over the SCAMP engine's changing views (ptdyn.hip)
+constexpr uint32_t kPdTab = 64;       // peer-table ids per vertex (u64 masks)
+constexpr int kPdNStat = 16;
+struct PdHead {
+    uint32_t ntab, flags;             // flags: bit0 root's eager/lazy map entries exist, bit1 restarted
+    uint32_t myround, seq;            // pushed Round; emission counter
+    uint32_t mono, _pad[3];           // heartbeat serial delivered (0 = none)
+};
+struct PdMsg { uint32_t type, src, dst, seq, round, pad; };   // 24 B
+struct PdArgs {
+    uint32_t n, mono, tick;
+    const uint8_t* __restrict__ alive;        // SCAMP's (a stopped manager takes its node down)
+    const uint32_t* __restrict__ pv;          // SCAMP partial views: the connections
+    const ScHead* __restrict__ sch;
+    const uint32_t* __restrict__ ev_cnt;      // SCAMP update events of this round
+    const uint2* __restrict__ ev;
+    PdHead* __restrict__ head;
+    uint32_t* __restrict__ tab;               // [n][kPdTab]
+    unsigned long long* __restrict__ mask;    // [n][6]
+    const PdMsg* __restrict__ in;
+    const uint32_t* nin;
+    PdMsg* __restrict__ out;
+    uint32_t* nout;
+    uint32_t out_cap;
+    uint32_t *cnt, *cur, *off, *idx, *bsum;
+    unsigned long long* __restrict__ stats;   // [kPdNStat]
+};
+hipError_t launch_pd_init(const PdArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
+hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s);
+hipError_t launch_pd_round(const PdArgs& a, hipStream_t s);
 
 // Protocol modules that keep their host state outside psim_host.hip: the
 // handle owns one slot per module and deletes it on psim_destroy.
 struct ModuleState {
     virtual ~ModuleState() {}
 };
-enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_CSSHARD = 3, MOD_COUNT = 4 };
+enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_COUNT = 4 };
 ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);
 hipStream_t handle_stream(const psim_handle* h);

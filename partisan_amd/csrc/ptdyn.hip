@@ -1,0 +1,626 @@
+// ptdyn.hip -- configuration C3: the Plumtree server
+// (src/partisan_plumtree_broadcast.erl) with the heartbeat handler, over the
+// churning SCAMP v2 membership of scamp.hip, one gfx950 thread per vertex.
+//
+// Unlike the static-overlay engine (plumtree.hip), a vertex's peers change
+// every round, so its Plumtree state is a small peer table (<= kPdTab ids)
+// with one 64-bit mask per set over it: all_members, common_eagers,
+// common_lazys, the root's eager and lazy sets (present iff the root's map
+// entry exists) and the outstanding i_have rows (one heartbeat in flight, so
+// a row is a peer).  Messages are 24 B records in a queue bucketed by
+// destination and sorted by (src, seq) per vertex, as in the SCAMP engine.
+// A round, after the SCAMP round it follows:
+//   1. the {update, Members} casts the manager fired this round
+//      (partisan_plumtree_broadcast.erl:607-639), in order, as the set
+//      deltas scamp.hip recorded: a new member -> common_eagers U New and
+//      reset_peers/4 (:1320-1328); a removed one -> neighbors_down/2
+//      (:910-951), which also deletes its outstanding rows;
+//   2. the inbox (handle_cast clauses :565-605);
+//   3. the lazy tick (every round): i_have to every outstanding peer that
+//      is connected (:992-1030).
+// A send needs a connection (partisan:cast_message -> do_send_message):
+// the destination must be a member of the sender (its SCAMP partial view);
+// otherwise it is dropped.
+#include "psim_internal.h"
+#include "../../include/psim.h"
+
+namespace psim {
+
+namespace {
+
+enum { PD_BROADCAST = 1, PD_PRUNE, PD_IHAVE, PD_IGNORED, PD_GRAFT };
+enum { S_MEM = 0, S_CE, S_CL, S_EAG, S_LAZ, S_OUT, S_NSET };
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kPdStrideBlocks = 2048;
+
+struct Ctx {
+    const PdArgs* a;
+    uint32_t v;
+    PdHead h;
+    uint32_t* tab;                 // row in HBM
+    unsigned long long m[S_NSET];     // masks over the row
+    const uint32_t* pv;            // SCAMP partial view row
+    uint32_t npv;
+    uint32_t sent[6], dropped, deliv, err;
+};
+
+__device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
+    if (t == c.v) return false;
+    for (uint32_t i = 0; i < c.npv; i++)
+        if (c.pv[i] == t) return true;
+    return false;
+}
+
+__device__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t round) {
+    if (!connected(c, t)) { c.dropped++; return; }
+    const PdArgs& a = *c.a;
+    const uint32_t pos = atomicAdd(a.nout, 1u);
+    c.sent[type]++;
+    if (pos >= a.out_cap) { c.err |= 1u; return; }
+    PdMsg m;
+    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.pad = 0;
+    a.out[pos] = m;
+}
+
+__device__ int tab_find(const Ctx& c, uint32_t x) {
+    for (uint32_t i = 0; i < c.h.ntab; i++)
+        if (c.tab[i] == x) return (int)i;
+    return -1;
+}
+
+// drop ids no set refers to (keeps the masks aligned with the row)
+__device__ void tab_compact(Ctx& c) {
+    unsigned long long any = 0;
+    for (int k = 0; k < S_NSET; k++) any |= c.m[k];
+    uint32_t w = 0;
+    unsigned long long nm[S_NSET] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < c.h.ntab; i++) {
+        if (!((any >> i) & 1ull)) continue;
+        c.tab[w] = c.tab[i];
+        for (int k = 0; k < S_NSET; k++) nm[k] |= ((c.m[k] >> i) & 1ull) << w;
+        w++;
+    }
+    c.h.ntab = w;
+    for (int k = 0; k < S_NSET; k++) c.m[k] = nm[k];
+}
+
+__device__ int tab_insert(Ctx& c, uint32_t x) {
+    const int f = tab_find(c, x);
+    if (f >= 0) return f;
+    if (c.h.ntab >= kPdTab) tab_compact(c);
+    if (c.h.ntab >= kPdTab) { c.err |= 2u; return -1; }
+    c.tab[c.h.ntab] = x;
+    return (int)c.h.ntab++;
+}
+
+__device__ __forceinline__ unsigned long long bit(int i) { return i < 0 ? 0ull : (1ull << i); }
+
+// all_peers/3 materialised: set_peers/4 creates the root's map entries
+__device__ __forceinline__ void ensure_root_sets(Ctx& c) {
+    if (c.h.flags & 1u) return;
+    c.m[S_EAG] = c.m[S_CE];
+    c.m[S_LAZ] = c.m[S_CL];
+    c.h.flags |= 1u;
+}
+__device__ void add_eager(Ctx& c, unsigned long long b) {
+    ensure_root_sets(c);
+    c.m[S_EAG] |= b;
+    c.m[S_LAZ] &= ~b;
+}
+__device__ void add_lazy(Ctx& c, unsigned long long b) {
+    ensure_root_sets(c);
+    c.m[S_EAG] &= ~b;
+    c.m[S_LAZ] |= b;
+}
+__device__ __forceinline__ unsigned long long eager_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_EAG] : c.m[S_CE]; }
+__device__ __forceinline__ unsigned long long lazy_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_LAZ] : c.m[S_CL]; }
+
+// eager_push/7 (:962-970) to eager peers -- From, schedule_lazy_push/6 (:974-988)
+__device__ void push(Ctx& c, unsigned long long from_bit, uint32_t round) {
+    unsigned long long e = eager_now(c) & ~from_bit;
+    while (e) {
+        const int i = __ffsll(e) - 1;
+        e &= e - 1;
+        send(c, c.tab[i], PD_BROADCAST, round);
+    }
+    c.m[S_OUT] |= lazy_now(c) & ~from_bit;
+}
+
+__device__ void handle(Ctx& c, const PdMsg& m) {
+    const PdArgs& a = *c.a;
+    const bool delivered = c.h.mono == a.mono;
+    switch (m.type) {
+    case PD_BROADCAST: {                           // :571-578 -> handle_broadcast/8 :843-857
+        const unsigned long long b = bit(tab_insert(c, m.src));
+        if (!delivered) {                          // merge/2: not stale -> add_timestamp
+            c.h.mono = a.mono;
+            c.h.myround = m.round + 1;
+            c.deliv++;
+            add_eager(c, b);
+            push(c, b, c.h.myround);
+        } else {
+            add_lazy(c, b);
+            send(c, m.src, PD_PRUNE, 0);
+        }
+        break;
+    }
+    case PD_PRUNE:                                 // :580-584
+        add_lazy(c, bit(tab_insert(c, m.src)));
+        break;
+    case PD_IHAVE:                                 // :586-590 -> handle_ihave/7 :861-876
+        if (delivered) {
+            send(c, m.src, PD_IGNORED, m.round);
+        } else {
+            send(c, m.src, PD_GRAFT, m.round);
+            add_eager(c, bit(tab_insert(c, m.src)));
+        }
+        break;
+    case PD_IGNORED: {                             // :592-598 ack_outstanding/5: the row {From, {Id, Mod, Round, Root}}
+        const int i = tab_find(c, m.src);
+        if (i >= 0 && m.round == c.h.myround && delivered) c.m[S_OUT] &= ~bit(i);
+        break;
+    }
+    case PD_GRAFT:                                 // :600-605 -> handle_graft/7 :880-906
+        if (delivered) {                           // Mod:graft -> {ok, M}
+            add_eager(c, bit(tab_insert(c, m.src)));
+            send(c, m.src, PD_BROADCAST, m.round);
+        }                                          // {error, not_found}: logged only
+        break;
+    default:
+        break;
+    }
+}
+
+// {update, Members} as a set delta (:607-639)
+__device__ void apply_update(Ctx& c, uint32_t added, uint32_t removed) {
+    if (added != kNone) {
+        const unsigned long long b = bit(tab_insert(c, added));
+        c.m[S_MEM] |= b;
+        if (added != c.v) c.m[S_CE] |= b;          // common_eagers U New, minus self (reset_peers)
+        c.m[S_EAG] = 0;                              // reset_peers: the per-root maps are dropped
+        c.m[S_LAZ] = 0;
+        c.h.flags &= ~1u;
+    }
+    if (removed != kNone) {                        // neighbors_down/2
+        const int i = tab_find(c, removed);
+        if (i >= 0)
+            for (int k = 0; k < S_NSET; k++) c.m[k] &= ~bit(i);
+    }
+}
+
+__device__ __forceinline__ bool msg_less(const PdMsg& x, const PdMsg& y) {
+    return x.src < y.src || (x.src == y.src && x.seq < y.seq);
+}
+__device__ __forceinline__ uint32_t n_in(const PdArgs& a) { return *a.nin < a.out_cap ? *a.nin : a.out_cap; }
+
+__global__ __launch_bounds__(kBlock) void pd_count(PdArgs a) {
+    const uint32_t k = n_in(a);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock)
+        atomicAdd(&a.cnt[a.in[i].dst], 1u);
+}
+__global__ __launch_bounds__(kBlock) void pd_scan_blocks(PdArgs a) {
+    __shared__ uint32_t ws[kBlock / 64];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t x0 = i < a.n ? a.cnt[i] : 0u;
+    uint32_t x = x0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wv; w++) pre += ws[w];
+    if (i < a.n) a.off[i] = pre + x - x0;
+    if (threadIdx.x == kBlock - 1) a.bsum[blockIdx.x] = pre + x;
+}
+__global__ __launch_bounds__(1024) void pd_scan_sums(PdArgs a, uint32_t nb) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024;
+    const uint32_t lo = t * per, hi = min(nb, lo + per);
+    uint32_t s = 0;
+    for (uint32_t b = lo; b < hi; b++) s += a.bsum[b];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t y = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += y;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (uint32_t b = lo; b < hi; b++) { const uint32_t x = a.bsum[b]; a.bsum[b] = run; run += x; }
+    if (t == 1023) a.off[a.n] = part[1023];
+}
+__global__ __launch_bounds__(kBlock) void pd_scan_add(PdArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < a.n) a.off[i] += a.bsum[blockIdx.x];
+}
+__global__ __launch_bounds__(kBlock) void pd_scatter(PdArgs a) {
+    const uint32_t k = n_in(a);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock) {
+        const uint32_t d = a.in[i].dst;
+        a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
+    }
+}
+
+__device__ void load(Ctx& c, const PdArgs& a, uint32_t v) {
+    c.a = &a;
+    c.v = v;
+    c.h = a.head[v];
+    c.tab = a.tab + (size_t)v * kPdTab;
+    for (int k = 0; k < S_NSET; k++) c.m[k] = a.mask[(size_t)v * S_NSET + k];
+    c.pv = a.pv + (size_t)v * kScPv;
+    c.npv = a.sch[v].npv;
+    for (int i = 0; i < 6; i++) c.sent[i] = 0;
+    c.dropped = c.deliv = c.err = 0;
+}
+__device__ void store(const Ctx& c) {
+    const PdArgs& a = *c.a;
+    a.head[c.v] = c.h;
+    for (int k = 0; k < S_NSET; k++) a.mask[(size_t)c.v * S_NSET + k] = c.m[k];
+}
+
+__device__ void reduce_stats(const PdArgs& a, const unsigned long long* vals) {
+    for (int i = 1; i < kPdNStat; i++) {
+        unsigned long long x = vals[i];
+        if (i == 9) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
+            if ((threadIdx.x & 63) == 0 && x) atomicOr(&a.stats[i], x);
+            continue;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[i], x);
+    }
+}
+
+// stats: [1..5] sent by kind, 6 dropped, 7 delivered_new, 8 active, 9 error bits,
+// 10 updates applied, 11 delivered_live, 12 live, 13 outstanding rows to connected live peers
+__global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
+    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    unsigned long long vals[kPdNStat];
+    for (int i = 0; i < kPdNStat; i++) vals[i] = 0;
+    if (v < a.n && a.alive[v]) {
+        Ctx c;
+        load(c, a, v);
+        const bool fresh = (c.h.flags & 2u) != 0;
+        c.h.flags &= ~2u;
+        // 1. the manager's update casts of this round, in order
+        const uint32_t ne = a.ev_cnt ? a.ev_cnt[v] : 0u;
+        for (uint32_t i = 0; i < ne; i++) {
+            const uint2 e = a.ev[(size_t)v * kScEv + i];
+            apply_update(c, e.x, e.y);
+        }
+        vals[10] = ne;
+        // 2. the inbox in (src, seq) order (a restarted vertex drops it)
+        const uint32_t lo = a.off[v], hi = a.off[v + 1];
+        if (!fresh && hi > lo) {
+            for (uint32_t i = lo + 1; i < hi; i++) {
+                const uint32_t x = a.idx[i];
+                const PdMsg mx = a.in[x];
+                uint32_t j = i;
+                while (j > lo && msg_less(mx, a.in[a.idx[j - 1]])) { a.idx[j] = a.idx[j - 1]; j--; }
+                a.idx[j] = x;
+            }
+            for (uint32_t i = lo; i < hi; i++) handle(c, a.in[a.idx[i]]);
+            vals[8] = 1;
+        }
+        // 3. handle_info(lazy_tick): send_lazy/0, rows persist
+        unsigned long long o = c.m[S_OUT], live_rows = 0;
+        while (o) {
+            const int i = __ffsll(o) - 1;
+            o &= o - 1;
+            const uint32_t t = c.tab[i];
+            if (!a.alive[t] || !connected(c, t)) continue;
+            live_rows++;
+            if (a.tick) send(c, t, PD_IHAVE, c.h.myround);
+        }
+        if (c.h.ntab > kPdTab - 8) tab_compact(c);
+        store(c);
+        for (int i = 1; i <= 5; i++) vals[i] = c.sent[i];
+        vals[6] = c.dropped;
+        vals[7] = c.deliv;
+        vals[9] = c.err;
+        vals[11] = c.h.mono == a.mono && a.mono != 0;
+        vals[12] = 1;
+        vals[13] = live_rows;
+    }
+    reduce_stats(a, vals);
+}
+
+// heartbeat at the root: the backend's add_timestamp + the plumtree cast
+// {broadcast, Id, Payload, Mod} (:565-569) -> eager_push/4, schedule_lazy_push/3
+__global__ void pd_origin(PdArgs a, uint32_t root) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long vals[kPdNStat];
+    Ctx c;
+    load(c, a, root);
+    c.h.mono = a.mono;
+    c.h.myround = 0;
+    push(c, 0ull, 0u);
+    store(c);
+    (void)vals;
+    if (c.err) atomicOr(&a.stats[9], (unsigned long long)c.err);
+    atomicAdd(&a.stats[6], (unsigned long long)c.dropped);
+}
+
+// start_link/0 with members = {self}: fresh state (every vertex, or a crash list)
+__global__ __launch_bounds__(kBlock) void pd_init(PdArgs a, const uint32_t* __restrict__ list, uint32_t k) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (list ? k : a.n)) return;
+    const uint32_t v = list ? list[i] : i;
+    PdHead h = list ? a.head[v] : PdHead{};
+    h.ntab = 1;
+    h.flags = list ? 2u : 0u;        // restarted: its inbox holds messages for the old incarnation
+    h.myround = 0;
+    h.mono = 0;
+    if (!list) h.seq = 0;
+    a.head[v] = h;
+    a.tab[(size_t)v * kPdTab] = v;
+    a.mask[(size_t)v * S_NSET + S_MEM] = 1ull;   // all_members = {self}
+    for (int m = 1; m < S_NSET; m++) a.mask[(size_t)v * S_NSET + m] = 0ull;
+}
+
+inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+
+}  // namespace
+
+hipError_t launch_pd_init(const PdArgs& a, const uint32_t* list, uint32_t k, hipStream_t s) {
+    const uint32_t m = list ? k : a.n;
+    if (m) hipLaunchKernelGGL(pd_init, dim3(nblk(m)), dim3(kBlock), 0, s, a, list, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s) {
+    hipLaunchKernelGGL(pd_origin, dim3(1), dim3(64), 0, s, a, root);
+    return hipGetLastError();
+}
+
+hipError_t launch_pd_round(const PdArgs& a, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(pd_count, dim3(kPdStrideBlocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pd_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pd_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
+    hipLaunchKernelGGL(pd_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pd_scatter, dim3(kPdStrideBlocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(pd_process, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace psim
+
+// ---------------------------------------------------------------------------
+// host side: the psim_c3_* entry points of include/psim.h
+// ---------------------------------------------------------------------------
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+using namespace psim;
+
+namespace {
+
+struct PdState : ModuleState {
+    uint32_t n = 0, cap = 0, mono = 0, root = 0;
+    PdHead* head = nullptr;
+    uint32_t* tab = nullptr;
+    unsigned long long *mask = nullptr, *stats = nullptr;
+    PdMsg* msg[2] = {nullptr, nullptr};
+    uint32_t* nmsg = nullptr;
+    uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr, *list = nullptr;
+    size_t list_cap = 0;
+    uint32_t par = 0;
+    uint64_t round = 0;
+    ~PdState() override {
+        void* p[] = {head, tab, mask, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, list};
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+};
+
+PdState* pd_of(psim_handle* h) { return static_cast<PdState*>(handle_module(h, MOD_PTDYN)); }
+
+#define PDCHK(h, x)                                                                         \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            return handle_fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+bool pd_alloc(void** p, size_t bytes) {
+    return hipMalloc(p, bytes ? bytes : 8) == hipSuccess && hipMemset(*p, 0, bytes ? bytes : 8) == hipSuccess;
+}
+
+int pd_args(psim_handle* h, const PdState& s, PdArgs& a) {
+    ScView sv;
+    const int rc = scamp_view(h, &sv, true);
+    if (rc) return rc;
+    a = PdArgs{};
+    a.n = s.n; a.mono = s.mono; a.tick = 1;
+    a.alive = sv.alive; a.pv = sv.pv; a.sch = sv.head; a.ev_cnt = sv.ev_cnt; a.ev = sv.ev;
+    a.head = s.head; a.tab = s.tab; a.mask = s.mask;
+    a.in = s.msg[s.par]; a.nin = s.nmsg + s.par;
+    a.out = s.msg[s.par ^ 1]; a.nout = s.nmsg + (s.par ^ 1);
+    a.out_cap = s.cap;
+    a.cnt = s.cnt; a.cur = s.cur; a.off = s.off; a.idx = s.idx; a.bsum = s.bsum;
+    a.stats = s.stats;
+    return PSIM_OK;
+}
+
+int pd_check(psim_handle* h, unsigned long long err, uint64_t round) {
+    if (err & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: plumtree message queue full", (unsigned long long)round);
+    if (err & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a peer table exceeded %u ids",
+                                       (unsigned long long)round, kPdTab);
+    return PSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_c3_setup(psim_handle* h, uint32_t n, uint32_t c, uint32_t periodic_rounds) {
+    if (!h) return PSIM_EINVAL;
+    int rc = psim_scamp_setup(h, n, 2, c, periodic_rounds);
+    if (rc) return rc;
+    ScView sv;
+    rc = scamp_view(h, &sv, true);
+    if (rc) return rc;
+    ModuleState*& slot = handle_module(h, MOD_PTDYN);
+    delete slot;
+    slot = nullptr;
+    PdState* s = new PdState();
+    s->n = n;
+    s->cap = (uint32_t)std::min<uint64_t>(16ull * n + 4096, 0xFFFFFFF0ull);
+    const size_t N = n;
+    const uint32_t nb = (n + kBlock - 1) / kBlock;
+    const bool ok = pd_alloc((void**)&s->head, N * sizeof(PdHead)) && pd_alloc((void**)&s->tab, N * kPdTab * 4) &&
+                    pd_alloc((void**)&s->mask, N * 6 * 8) && pd_alloc((void**)&s->stats, kPdNStat * 8) &&
+                    pd_alloc((void**)&s->msg[0], size_t(s->cap) * sizeof(PdMsg)) &&
+                    pd_alloc((void**)&s->msg[1], size_t(s->cap) * sizeof(PdMsg)) && pd_alloc((void**)&s->nmsg, 16) &&
+                    pd_alloc((void**)&s->cnt, N * 4) && pd_alloc((void**)&s->cur, N * 4) &&
+                    pd_alloc((void**)&s->off, (N + 1) * 4) && pd_alloc((void**)&s->idx, size_t(s->cap) * 4) &&
+                    pd_alloc((void**)&s->bsum, size_t(nb) * 4);
+    if (!ok) {
+        delete s;
+        return handle_fail(h, PSIM_ENOMEM, "c3 plumtree state for n=%u", n);
+    }
+    slot = s;
+    PdArgs a;
+    rc = pd_args(h, *s, a);
+    if (rc) return rc;
+    PDCHK(h, launch_pd_init(a, nullptr, 0, handle_stream(h)));
+    PDCHK(h, hipStreamSynchronize(handle_stream(h)));
+    return PSIM_OK;
+}
+
+int psim_c3_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k) {
+    return psim_scamp_join(h, v, contact, k);
+}
+
+int psim_c3_crash(psim_handle* h, const uint32_t* v, size_t k) {
+    if (!h || (k && !v)) return PSIM_EINVAL;
+    PdState* s = pd_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
+    int rc = scamp_crash_list(h, v, k);     // validates the list, restarts the SCAMP side
+    if (rc || !k) return rc;
+    if (k > s->list_cap) {
+        if (s->list) (void)hipFree(s->list);
+        s->list = nullptr;
+        s->list_cap = std::max<size_t>(k, 2 * s->list_cap);
+        if (!pd_alloc((void**)&s->list, s->list_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "c3 crash list");
+    }
+    PDCHK(h, hipMemcpyAsync(s->list, v, k * 4, hipMemcpyHostToDevice, handle_stream(h)));
+    PdArgs a;
+    rc = pd_args(h, *s, a);
+    if (rc) return rc;
+    PDCHK(h, launch_pd_init(a, s->list, (uint32_t)k, handle_stream(h)));
+    PDCHK(h, hipStreamSynchronize(handle_stream(h)));
+    return PSIM_OK;
+}
+
+int psim_c3_heartbeat(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+    if (!h) return PSIM_EINVAL;
+    PdState* s = pd_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
+    if (root >= s->n) return PSIM_EINVAL;
+    s->mono++;
+    s->root = root;
+    PdArgs a;
+    int rc = pd_args(h, *s, a);
+    if (rc) return rc;
+    a.out = s->msg[s->par];          // the origin's pushes are read by the next round
+    a.nout = s->nmsg + s->par;
+    PDCHK(h, hipMemsetAsync(s->stats, 0, kPdNStat * 8, handle_stream(h)));
+    PDCHK(h, launch_pd_origin(a, root, handle_stream(h)));
+    unsigned long long r[kPdNStat];
+    PDCHK(h, hipMemcpyAsync(r, s->stats, sizeof r, hipMemcpyDeviceToHost, handle_stream(h)));
+    PDCHK(h, hipStreamSynchronize(handle_stream(h)));
+    if (mono_out) *mono_out = s->mono;
+    return pd_check(h, r[9], s->round);
+}
+
+int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    PdState* s = pd_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
+    const hipStream_t st = handle_stream(h);
+    for (uint32_t i = 0; i < rounds; i++) {
+        psim_c3_stats* o = out && i < cap ? &out[i] : nullptr;
+        int rc = scamp_round(h, o ? &o->scamp : nullptr);
+        if (rc) return rc;
+        PdArgs a;
+        rc = pd_args(h, *s, a);
+        if (rc) return rc;
+        PDCHK(h, hipMemsetAsync(s->stats, 0, kPdNStat * 8, st));
+        PDCHK(h, hipMemsetAsync(s->nmsg + (s->par ^ 1), 0, 4, st));
+        PDCHK(h, hipEventRecord(handle_event(h, 2), st));
+        PDCHK(h, launch_pd_round(a, st));
+        PDCHK(h, hipEventRecord(handle_event(h, 3), st));
+        unsigned long long r[kPdNStat];
+        PDCHK(h, hipMemcpyAsync(r, s->stats, sizeof r, hipMemcpyDeviceToHost, st));
+        PDCHK(h, hipStreamSynchronize(st));
+        float ms = 0.f;
+        PDCHK(h, hipEventElapsedTime(&ms, handle_event(h, 2), handle_event(h, 3)));
+        s->par ^= 1u;
+        s->round++;
+        rc = pd_check(h, r[9], s->round);
+        if (rc) return rc;
+        if (o) {
+            for (int k = 1; k <= 5; k++) o->pt_sent[k] = r[k];
+            o->pt_sent[0] = 0;
+            o->pt_dropped = r[6];
+            o->delivered_new = r[7];
+            o->active = r[8];
+            o->updates = r[10];
+            o->delivered_live = r[11];
+            o->live = r[12];
+            o->outstanding_live = r[13];
+            uint64_t msgs = 0;
+            for (int k = 1; k <= 5; k++) msgs += r[k];
+            o->pt_algo_bytes = 48ull * msgs + 24ull * msgs + 12ull * s->n + 64ull * r[12];
+            o->pt_kernel_ms = ms;
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_c3_get_plumtree(const psim_handle* h, uint32_t v, uint32_t* eager, size_t* ne, uint32_t* lazy, size_t* nl,
+                         uint32_t* outstanding, size_t* no, size_t cap, uint32_t* delivered_mono,
+                         uint32_t* recv_round) {
+    if (!h) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    PdState* s = pd_of(hh);
+    if (!s) return PSIM_ESTATE;
+    if (v >= s->n) return PSIM_EINVAL;
+    PDCHK(hh, hipStreamSynchronize(handle_stream(h)));
+    PdHead hd;
+    uint32_t tab[kPdTab];
+    unsigned long long m[6];
+    PDCHK(hh, hipMemcpy(&hd, s->head + v, sizeof hd, hipMemcpyDeviceToHost));
+    PDCHK(hh, hipMemcpy(tab, s->tab + size_t(v) * kPdTab, sizeof tab, hipMemcpyDeviceToHost));
+    PDCHK(hh, hipMemcpy(m, s->mask + size_t(v) * 6, sizeof m, hipMemcpyDeviceToHost));
+    const bool sets = hd.flags & 1u;
+    const unsigned long long E = sets ? m[3] : m[1], L = sets ? m[4] : m[2];
+    auto out = [&](unsigned long long mk, uint32_t* dst, size_t* n) {
+        std::vector<uint32_t> ids;
+        for (uint32_t i = 0; i < hd.ntab && i < kPdTab; i++)
+            if ((mk >> i) & 1ull) ids.push_back(tab[i]);
+        std::sort(ids.begin(), ids.end());
+        if (dst)
+            for (size_t i = 0; i < ids.size() && i < cap; i++) dst[i] = ids[i];
+        if (n) *n = ids.size();
+    };
+    out(E, eager, ne);
+    out(L, lazy, nl);
+    out(m[5], outstanding, no);
+    if (delivered_mono) *delivered_mono = hd.mono;
+    if (recv_round) *recv_round = hd.myround;
+    return PSIM_OK;
+}
+
+}  // extern "C"

@@ -38,7 +38,17 @@ struct Ctx {
     uint32_t* iv;
     uint32_t sent[7];
     uint32_t dropped, ndraw, err, resub;
+    uint32_t nev;      // update events recorded this round
 };
+
+// partisan_peer_service_events:update(Members) after a handler that changed
+// the members' set: {added, removed} (each handler adds or removes at most one)
+__device__ void record_update(Ctx& c, uint32_t added, uint32_t removed) {
+    if (!c.a->ev_cnt || (added == 0xFFFFFFFFu && removed == 0xFFFFFFFFu)) return;
+    if (c.nev >= kScEv) { c.err |= 16u; return; }
+    c.a->ev[(size_t)c.v * kScEv + c.nev] = make_uint2(added, removed);
+    c.nev++;
+}
 
 __device__ uint64_t draw64(Ctx& c) {
     const uint4 r = philox4x32_10(make_uint4(c.v, c.h.draws, KIND_SCAMP, c.h.inc), c.a->key);
@@ -121,8 +131,10 @@ __device__ void do_join(Ctx& c, uint32_t node) {
     uint32_t sel[kScMaxSel];
     const uint32_t ns = select_sublist(c, k, sel);            // over the members before the add
     const uint32_t n0 = c.h.npv;
+    const bool had = in_pv(c, node);
     if (c.a->ver == 2) pv_push_front(c, node);
     else pv_set_add(c, node);
+    if (!had) record_update(c, node, 0xFFFFFFFFu);
     emit(c, node, SC_FWD, c.v, 0, node);                      // forward_subscription(Myself)
     // to each member known before (v2: list order; v1: sets:fold = id order):
     // v2 prepended one element, v1 inserted `node` unless present
@@ -147,6 +159,7 @@ __device__ void do_leave(Ctx& c, uint32_t node) {
     const uint32_t n0 = c.h.npv;
     for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
     if (had) pv_del_first(c, node);
+    if (had) record_update(c, 0xFFFFFFFFu, node);
     for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu);
 }
 
@@ -176,9 +189,11 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         if (keep) {
             if (a.ver == 2) {
                 pv_push_front(c, node);
+                record_update(c, node, 0xFFFFFFFFu);
                 emit(c, node, SC_KEEP, c.v, 0, node);
             } else {
                 pv_set_add(c, node);
+                record_update(c, node, 0xFFFFFFFFu);
             }
         } else {
             uint32_t sel[1];
@@ -201,13 +216,18 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         const uint32_t n0 = c.h.npv;
         for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
         pv_del_first(c, node);
+        if (!in_pv(c, node)) record_update(c, 0xFFFFFFFFu, node);   // a duplicate keeps it a member
         for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, node);
         break;
     }
-    case SC_REPLACE:                                          // v2 :275-294
+    case SC_REPLACE: {                                        // v2 :275-294
+        if (m.a == m.b || !in_pv(c, m.a)) break;
+        const bool had_b = in_pv(c, m.b);
         for (uint32_t i = 0; i < c.h.npv; i++)
             if (c.pv[i] == m.a) c.pv[i] = m.b;
+        record_update(c, had_b ? 0xFFFFFFFFu : m.b, m.a);
         break;
+    }
     case SC_BOOT: {                                           // v2 :230-274
         if (m.a != c.v) break;
         const int32_t L = (int32_t)c.h.niv, P = (int32_t)c.h.npv;
@@ -304,6 +324,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         c.iv = a.iv + (size_t)v * kScIv;
         for (int i = 0; i < 7; i++) c.sent[i] = 0;
         c.dropped = c.ndraw = c.err = c.resub = 0;
+        c.nev = 0;
         const bool fresh = c.h.fresh != 0;
         c.h.fresh = 0;
         bool up = true;
@@ -337,6 +358,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
             niv = c.h.niv;
         }
         a.head[v] = c.h;
+        if (a.ev_cnt) a.ev_cnt[v] = c.nev;
         for (int i = 0; i < 7; i++) sent[i] = c.sent[i];
         dropped = c.dropped; ndraw = c.ndraw; err = c.err; resub = c.resub;
     }
@@ -429,12 +451,14 @@ struct ScState : ModuleState {
     uint32_t *call_off = nullptr, *calls = nullptr, *list = nullptr;
     size_t calls_cap = 0, list_cap = 0;
     unsigned long long* stats = nullptr;
+    uint32_t* ev_cnt = nullptr;     // update events (C3), allocated on demand
+    uint2* ev = nullptr;
     uint32_t par = 0;
     uint64_t round = 0;
     std::vector<uint32_t> cv, cx;   // calls since the last round: vertex, (bit31 = leave) | target
     ~ScState() override {
         void* p[] = {head, pv, iv, alive, alive0, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, call_off, calls,
-                     list, stats};
+                     list, stats, ev_cnt, ev};
         for (void* x : p)
             if (x) (void)hipFree(x);
     }
@@ -469,6 +493,8 @@ ScArgs sc_args(const psim_handle* h, const ScState& s) {
     a.cnt = s.cnt; a.cur = s.cur; a.off = s.off; a.idx = s.idx; a.bsum = s.bsum;
     a.call_off = s.call_off; a.calls = s.calls;
     a.stats = s.stats;
+    a.ev_cnt = s.ev_cnt;
+    a.ev = s.ev;
     return a;
 }
 
@@ -496,6 +522,7 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     s.cv.clear();
     s.cx.clear();
     SCCHK(h, hipMemcpyAsync(s.alive0, s.alive, s.n, hipMemcpyDeviceToDevice, st));
+    if (s.ev_cnt) SCCHK(h, hipMemsetAsync(s.ev_cnt, 0, size_t(s.n) * 4, st));
     SCCHK(h, hipMemsetAsync(s.stats, 0, 16 * 8, st));
     SCCHK(h, hipMemsetAsync(s.nmsg + (s.par ^ 1), 0, 4, st));
     ScArgs a = sc_args(h, s);
@@ -514,6 +541,8 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
                                          (unsigned long long)s.round, s.cap);
     if (r[11] & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: a view exceeded %u / %u entries",
                                          (unsigned long long)s.round, kScPv, kScIv);
+    if (r[11] & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: > %u membership updates at a vertex",
+                                          (unsigned long long)s.round, kScEv);
     if (out) {
         memset(out, 0, sizeof *out);
         uint64_t emitted = 0;
@@ -540,6 +569,34 @@ int sc_upload_list(psim_handle* h, ScState& s, const uint32_t* v, size_t k) {
 }
 
 }  // namespace
+
+namespace psim {
+
+int scamp_view(psim_handle* h, ScView* out, bool want_events) {
+    ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    if (want_events && !s->ev_cnt) {
+        if (!sc_alloc((void**)&s->ev_cnt, size_t(s->n) * 4) || !sc_alloc((void**)&s->ev, size_t(s->n) * kScEv * 8))
+            return handle_fail(h, PSIM_ENOMEM, "scamp: update event arrays");
+    }
+    out->n = s->n;
+    out->pv = s->pv;
+    out->head = s->head;
+    out->alive = s->alive;
+    out->ev_cnt = s->ev_cnt;
+    out->ev = s->ev;
+    return PSIM_OK;
+}
+
+int scamp_round(psim_handle* h, psim_scamp_stats* out) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    return sc_round(h, *s, out);
+}
+
+int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k) { return psim_scamp_crash(h, v, k); }
+
+}  // namespace psim
 
 extern "C" {
 

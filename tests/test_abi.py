@@ -16,7 +16,7 @@ LIB = os.path.join(ROOT, "partisan_amd", "libpsim.so")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(psim_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(psim_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_entry_points():

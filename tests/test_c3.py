@@ -1,0 +1,150 @@
+"""Configuration C3: Plumtree broadcast repaired by graft/prune over churning
+SCAMP v2 membership (oracle/c3.c composes the two restatements; csrc/ptdyn.hip
++ csrc/scamp.hip on the device).
+
+CPU: the composition's behaviour -- the flood prunes redundant links and
+announces lazy rows (i_have); restarted vertices lose the heartbeat.
+GPU: bit-exact against the oracle round by round (both protocols' counters,
+SCAMP views, every vertex's eager / lazy / outstanding sets, delivery and
+pushed Round) through join waves, a heartbeat and 5 % crash/rejoin churn;
+and the 1M-peer C3 shape.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from test_scamp import churn, waves
+
+SEED = 0x5EED0003
+
+
+def build_oracle(n, periodic, warm):
+    c = O.C3(n, 5, periodic, SEED)
+    for v, cc in waves(n):
+        for a, b in zip(v, cc):
+            c.join(int(a), int(b))
+        c.step(3)
+    c.step(warm)
+    return c
+
+
+def test_c3_oracle_repair_and_churn():
+    n = 2000
+    c = build_oracle(n, 10, 5)
+    st = []
+    for _ in range(3):                  # later heartbeats find lazy links: i_have / graft repair
+        mono = c.heartbeat(0)
+        st.append(c.step(9))
+    assert sum(x["pt"]["prune"] for x in st[0]) > 0
+    assert sum(x["pt"]["i_have"] for x in st[2]) > 0
+    assert sum(x["pt"]["graft"] for x in st[2]) > 0
+    assert sum(x["pt"]["ignored_i_have"] for x in st[2]) > 0
+    assert st[2][-1]["delivered_live"] > n // 2
+    v, cc = churn(n, 3)
+    keep = v != 0
+    v, cc = v[keep], cc[keep]
+    for a in v:
+        c.crash(int(a))
+    d = c.pt.delivered(0, mono)
+    assert not any(d[int(a)] for a in v)     # the restarted nodes lost the heartbeat
+    for a, b in zip(v, cc):
+        c.join(int(a), int(b))
+    c.step(3)
+
+
+def _compare(g, o, n, root, mono):
+    pv, npv, iv, niv = g.scamp.views()
+    od = o.pt.delivered(root, mono) if mono else np.zeros(n, np.uint8)
+    orr = o.pt.recv_round(root, mono) if mono else None
+    for v in range(n):
+        assert list(pv[v, :npv[v]]) == o.scamp.view(v), v
+        if not o.scamp.alive(v):
+            continue
+        ge, gl, go, gm, gr = g.plumtree(v)
+        oe, ol = o.pt.peers(v, root)
+        assert ge == oe and gl == ol, (v, ge, oe, gl, ol)
+        assert go == sorted({p for p, _, _ in o.pt.outstanding(v)}), v
+        assert (gm == mono and mono != 0) == bool(od[v]), v
+        if mono and od[v]:
+            want = 0 if orr[v] == 0xFFFFFFFE else int(orr[v]) + 1
+            assert gr == want, (v, gr, want)
+
+
+def _step(g, o, r):
+    gs, os_ = g.step(1)[0], o.step(1)[0]
+    for k in ("sent", "dropped", "processed", "draws", "stopped", "pv_sum", "inview_sum", "resub"):
+        assert gs["scamp"][k] == os_["scamp"][k], (r, "scamp", k)
+    for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft"):
+        assert gs["pt_sent"][k] == os_["pt"][k], (r, k, gs["pt_sent"], os_["pt"])
+    assert gs["pt_dropped"] == os_["pt_dropped"], r
+    assert gs["delivered_new"] == os_["pt"]["delivered_new"], r
+    assert gs["active"] == os_["pt"]["active"], r
+    assert gs["delivered_live"] == os_["delivered_live"] and gs["live"] == os_["live"], r
+    return gs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,periodic,warm,churn_rounds", [(1500, 2, 16, 14), (3000, 10, 5, 10)])
+def test_gpu_c3_parity(n, periodic, warm, churn_rounds):
+    import partisan_amd as pa
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=periodic)
+    o = O.C3(n, 5, periodic, SEED)
+    r = 0
+    for v, cc in waves(n):
+        g.join(v, cc)
+        for a, b in zip(v, cc):
+            o.join(int(a), int(b))
+        for _ in range(3):
+            _step(g, o, r)
+            r += 1
+    for _ in range(warm):
+        _step(g, o, r)
+        r += 1
+    _compare(g, o, n, 0, 0)
+    for _ in range(2):                  # a settled tree first: the next heartbeats use lazy links
+        mono = g.heartbeat(0)
+        assert mono == o.heartbeat(0)
+        for _ in range(8):
+            _step(g, o, r)
+            r += 1
+        _compare(g, o, n, 0, mono)
+    for i in range(churn_rounds):
+        if i % 5 == 0:
+            mono = g.heartbeat(0)
+            assert mono == o.heartbeat(0)
+        v, cc = churn(n, i)
+        keep = v != 0
+        v, cc = v[keep], cc[keep]
+        g.crash(v)
+        g.join(v, cc)
+        for a, b in zip(v, cc):
+            o.crash(int(a))
+            o.join(int(a), int(b))
+        _step(g, o, r)
+        r += 1
+        _compare(g, o, n, 0, mono)
+
+
+@pytest.mark.gpu
+def test_gpu_c3_1m():
+    """C3 at 1M peers: join waves, heartbeat, 5 % churn per round; sanity of
+    the device counters (oracle parity is covered above)."""
+    import partisan_amd as pa
+    n = 1_000_000
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=10)
+    for v, cc in waves(n):
+        g.join(v, cc)
+        g.step(3)
+    g.step(5)
+    g.heartbeat(0)
+    st = g.step(10)
+    for i in range(10):
+        v, cc = churn(n, i)
+        keep = v != 0
+        g.crash(v[keep])
+        g.join(v[keep], cc[keep])
+        st += g.step(1)
+    assert st[5]["delivered_live"] > 0
+    assert all(x["live"] > 0.99 * n for x in st)
