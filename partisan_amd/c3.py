@@ -48,7 +48,7 @@ class C3Cluster:
         self._c(lib().psim_c3_step(self.sim._h, rounds, st, rounds))
         return [s.as_dict() for s in st]
 
-    def plumtree(self, v, cap=64):
+    def plumtree(self, v, cap=128):
         """(eager, lazy, outstanding) sorted ids, delivered heartbeat serial, pushed Round."""
         e, l_, o = (C.c_uint32 * cap)(), (C.c_uint32 * cap)(), (C.c_uint32 * cap)()
         ne, nl, no = C.c_size_t(), C.c_size_t(), C.c_size_t()

@@ -247,14 +247,35 @@ hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hip
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
 
 // C3: Plumtree over the SCAMP engine's changing views (ptdyn.hip)
-constexpr uint32_t kPdTab = 64;       // peer-table ids per vertex (u64 masks)
+constexpr uint32_t kPdTab = 128;      // peer-table ids per vertex (PdBits masks)
+constexpr uint32_t kPdRows = 64;      // outstanding i_have rows per vertex
+constexpr uint32_t kPdSets = 5;       // masks per vertex: members, common eager/lazy, root eager/lazy
 constexpr int kPdNStat = 16;
 struct PdHead {
     uint32_t ntab, flags;             // flags: bit0 root's eager/lazy map entries exist, bit1 restarted
-    uint32_t myround, seq;            // pushed Round; emission counter
-    uint32_t mono, _pad[3];           // heartbeat serial delivered (0 = none)
+    uint32_t myround, seq;            // pushed Round of the current heartbeat; emission counter
+    uint32_t dbase, nrow;             // delivered window top (heartbeat serial); outstanding rows
+    unsigned long long dmask;         // bit k: heartbeat dbase-k delivered (the backend's ISet)
 };
-struct PdMsg { uint32_t type, src, dst, seq, round, pad; };   // 24 B
+// a set over a vertex's peer table: bit i <-> tab[i]
+struct PdBits {
+    unsigned long long w[2];
+    __host__ __device__ static PdBits none() { return PdBits{{0ull, 0ull}}; }
+    __host__ __device__ static PdBits one(int i) {
+        PdBits b = none();
+        if (i >= 0) b.w[i >> 6] = 1ull << (i & 63);
+        return b;
+    }
+    __host__ __device__ bool test(uint32_t i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
+    __host__ __device__ bool any() const { return (w[0] | w[1]) != 0ull; }
+    __host__ __device__ PdBits operator|(const PdBits& o) const { return PdBits{{w[0] | o.w[0], w[1] | o.w[1]}}; }
+    __host__ __device__ PdBits operator&(const PdBits& o) const { return PdBits{{w[0] & o.w[0], w[1] & o.w[1]}}; }
+    __host__ __device__ PdBits operator~() const { return PdBits{{~w[0], ~w[1]}}; }
+    __host__ __device__ PdBits& operator|=(const PdBits& o) { w[0] |= o.w[0]; w[1] |= o.w[1]; return *this; }
+    __host__ __device__ PdBits& operator&=(const PdBits& o) { w[0] &= o.w[0]; w[1] &= o.w[1]; return *this; }
+};
+struct PdRow { uint32_t peer, mono, round; };                   // {Peer, {Id, Mod, Round, Root}}
+struct PdMsg { uint32_t type, src, dst, seq, round, mono; };   // 24 B
 struct PdArgs {
     uint32_t n, mono, tick;
     const uint8_t* __restrict__ alive;        // SCAMP's (a stopped manager takes its node down)
@@ -264,7 +285,8 @@ struct PdArgs {
     const uint2* __restrict__ ev;
     PdHead* __restrict__ head;
     uint32_t* __restrict__ tab;               // [n][kPdTab]
-    unsigned long long* __restrict__ mask;    // [n][6]
+    PdBits* __restrict__ mask;                // [n][kPdSets]
+    PdRow* __restrict__ rows;                 // [n][kPdRows], insertion order
     const PdMsg* __restrict__ in;
     const uint32_t* nin;
     PdMsg* __restrict__ out;

@@ -4,10 +4,12 @@
 //
 // Unlike the static-overlay engine (plumtree.hip), a vertex's peers change
 // every round, so its Plumtree state is a small peer table (<= kPdTab ids)
-// with one 64-bit mask per set over it: all_members, common_eagers,
-// common_lazys, the root's eager and lazy sets (present iff the root's map
-// entry exists) and the outstanding i_have rows (one heartbeat in flight, so
-// a row is a peer).  Messages are 24 B records in a queue bucketed by
+// with one 128-bit mask per set over it: all_members, common_eagers,
+// common_lazys and the root's eager and lazy sets (present iff the root's map
+// entry exists).  The outstanding ETS rows {Peer, {Id, Mod, Round, Root}} are
+// a per-vertex list in insertion order (several heartbeats may be in flight:
+// a row of an older one is still re-announced), and the backend's timestamp
+// ISet for the root is a 64-heartbeat window bitmap.  Messages are 24 B records in a queue bucketed by
 // destination and sorted by (src, seq) per vertex, as in the SCAMP engine.
 // A round, after the SCAMP round it follows:
 //   1. the {update, Members} casts the manager fired this round
@@ -29,7 +31,8 @@ namespace psim {
 namespace {
 
 enum { PD_BROADCAST = 1, PD_PRUNE, PD_IHAVE, PD_IGNORED, PD_GRAFT };
-enum { S_MEM = 0, S_CE, S_CL, S_EAG, S_LAZ, S_OUT, S_NSET };
+enum { S_MEM = 0, S_CE, S_CL, S_EAG, S_LAZ, S_NSET };
+static_assert(S_NSET == kPdSets, "mask layout");
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kPdStrideBlocks = 2048;
 
@@ -38,7 +41,8 @@ struct Ctx {
     uint32_t v;
     PdHead h;
     uint32_t* tab;                 // row in HBM
-    unsigned long long m[S_NSET];     // masks over the row
+    PdBits m[S_NSET];              // masks over the row
+    PdRow* rows;                   // outstanding rows in HBM
     const uint32_t* pv;            // SCAMP partial view row
     uint32_t npv;
     uint32_t sent[6], dropped, deliv, err;
@@ -51,14 +55,14 @@ __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
     return false;
 }
 
-__device__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t round) {
+__device__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     if (!connected(c, t)) { c.dropped++; return; }
     const PdArgs& a = *c.a;
     const uint32_t pos = atomicAdd(a.nout, 1u);
     c.sent[type]++;
     if (pos >= a.out_cap) { c.err |= 1u; return; }
     PdMsg m;
-    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.pad = 0;
+    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.mono = mono;
     a.out[pos] = m;
 }
 
@@ -70,14 +74,16 @@ __device__ int tab_find(const Ctx& c, uint32_t x) {
 
 // drop ids no set refers to (keeps the masks aligned with the row)
 __device__ void tab_compact(Ctx& c) {
-    unsigned long long any = 0;
+    PdBits any = PdBits::none();
     for (int k = 0; k < S_NSET; k++) any |= c.m[k];
     uint32_t w = 0;
-    unsigned long long nm[S_NSET] = {0, 0, 0, 0, 0, 0};
+    PdBits nm[S_NSET];
+    for (int k = 0; k < S_NSET; k++) nm[k] = PdBits::none();
     for (uint32_t i = 0; i < c.h.ntab; i++) {
-        if (!((any >> i) & 1ull)) continue;
+        if (!any.test(i)) continue;
         c.tab[w] = c.tab[i];
-        for (int k = 0; k < S_NSET; k++) nm[k] |= ((c.m[k] >> i) & 1ull) << w;
+        for (int k = 0; k < S_NSET; k++)
+            if (c.m[k].test(i)) nm[k] |= PdBits::one((int)w);
         w++;
     }
     c.h.ntab = w;
@@ -93,7 +99,12 @@ __device__ int tab_insert(Ctx& c, uint32_t x) {
     return (int)c.h.ntab++;
 }
 
-__device__ __forceinline__ unsigned long long bit(int i) { return i < 0 ? 0ull : (1ull << i); }
+__device__ __forceinline__ PdBits bit(int i) { return PdBits::one(i); }
+// pop the lowest member of b (b non-empty)
+__device__ __forceinline__ int pop_low(PdBits& b) {
+    if (b.w[0]) { const int i = __ffsll(b.w[0]) - 1; b.w[0] &= b.w[0] - 1; return i; }
+    const int i = __ffsll(b.w[1]) - 1; b.w[1] &= b.w[1] - 1; return 64 + i;
+}
 
 // all_peers/3 materialised: set_peers/4 creates the root's map entries
 __device__ __forceinline__ void ensure_root_sets(Ctx& c) {
@@ -102,45 +113,72 @@ __device__ __forceinline__ void ensure_root_sets(Ctx& c) {
     c.m[S_LAZ] = c.m[S_CL];
     c.h.flags |= 1u;
 }
-__device__ void add_eager(Ctx& c, unsigned long long b) {
+__device__ void add_eager(Ctx& c, const PdBits& b) {
     ensure_root_sets(c);
     c.m[S_EAG] |= b;
     c.m[S_LAZ] &= ~b;
 }
-__device__ void add_lazy(Ctx& c, unsigned long long b) {
+__device__ void add_lazy(Ctx& c, const PdBits& b) {
     ensure_root_sets(c);
     c.m[S_EAG] &= ~b;
     c.m[S_LAZ] |= b;
 }
-__device__ __forceinline__ unsigned long long eager_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_EAG] : c.m[S_CE]; }
-__device__ __forceinline__ unsigned long long lazy_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_LAZ] : c.m[S_CL]; }
+__device__ __forceinline__ PdBits eager_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_EAG] : c.m[S_CE]; }
+__device__ __forceinline__ PdBits lazy_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_LAZ] : c.m[S_CL]; }
+
+// the backend's timestamp ISet for the root (partisan_plumtree_backend.erl
+// is_stale/1 :229-244, add_timestamp): heartbeat serials dbase-63..dbase
+__device__ __forceinline__ bool delivered(Ctx& c, uint32_t mono) {
+    const uint32_t k = c.h.dbase - mono;
+    if (mono > c.h.dbase || mono == 0) return false;
+    if (k >= 64) { c.err |= 8u; return true; }
+    return (c.h.dmask >> k) & 1ull;
+}
+__device__ __forceinline__ void mark_delivered(Ctx& c, uint32_t mono) {
+    const uint32_t k = c.h.dbase - mono;
+    if (k >= 64) { c.err |= 8u; return; }
+    c.h.dmask |= 1ull << k;
+}
+
+// add_all_outstanding/5 (:1215-1219)
+__device__ void add_row(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
+    if (c.h.nrow >= kPdRows) { c.err |= 4u; return; }
+    c.rows[c.h.nrow++] = PdRow{peer, mono, round};
+}
+// ack_outstanding/5 (:1207-1211): ets:delete_object removes every identical row
+__device__ void ack_rows(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
+    uint32_t w = 0;
+    for (uint32_t i = 0; i < c.h.nrow; i++) {
+        const PdRow r = c.rows[i];
+        if (r.peer == peer && r.mono == mono && r.round == round) continue;
+        if (w != i) c.rows[w] = r;
+        w++;
+    }
+    c.h.nrow = w;
+}
 
 // eager_push/7 (:962-970) to eager peers -- From, schedule_lazy_push/6 (:974-988)
-__device__ void push(Ctx& c, unsigned long long from_bit, uint32_t round) {
-    unsigned long long e = eager_now(c) & ~from_bit;
-    while (e) {
-        const int i = __ffsll(e) - 1;
-        e &= e - 1;
-        send(c, c.tab[i], PD_BROADCAST, round);
-    }
-    c.m[S_OUT] |= lazy_now(c) & ~from_bit;
+__device__ void push(Ctx& c, const PdBits& from_bit, uint32_t mono, uint32_t round) {
+    PdBits e = eager_now(c) & ~from_bit;
+    while (e.any()) send(c, c.tab[pop_low(e)], PD_BROADCAST, mono, round);
+    PdBits l = lazy_now(c) & ~from_bit;
+    while (l.any()) add_row(c, c.tab[pop_low(l)], mono, round);
 }
 
 __device__ void handle(Ctx& c, const PdMsg& m) {
     const PdArgs& a = *c.a;
-    const bool delivered = c.h.mono == a.mono;
     switch (m.type) {
     case PD_BROADCAST: {                           // :571-578 -> handle_broadcast/8 :843-857
-        const unsigned long long b = bit(tab_insert(c, m.src));
-        if (!delivered) {                          // merge/2: not stale -> add_timestamp
-            c.h.mono = a.mono;
-            c.h.myround = m.round + 1;
+        const PdBits b = bit(tab_insert(c, m.src));
+        if (!delivered(c, m.mono)) {               // merge/2: not stale -> add_timestamp
+            mark_delivered(c, m.mono);
+            if (m.mono == a.mono) c.h.myround = m.round + 1;
             c.deliv++;
             add_eager(c, b);
-            push(c, b, c.h.myround);
+            push(c, b, m.mono, m.round + 1);
         } else {
             add_lazy(c, b);
-            send(c, m.src, PD_PRUNE, 0);
+            send(c, m.src, PD_PRUNE, 0, 0);
         }
         break;
     }
@@ -148,22 +186,20 @@ __device__ void handle(Ctx& c, const PdMsg& m) {
         add_lazy(c, bit(tab_insert(c, m.src)));
         break;
     case PD_IHAVE:                                 // :586-590 -> handle_ihave/7 :861-876
-        if (delivered) {
-            send(c, m.src, PD_IGNORED, m.round);
+        if (delivered(c, m.mono)) {
+            send(c, m.src, PD_IGNORED, m.mono, m.round);
         } else {
-            send(c, m.src, PD_GRAFT, m.round);
+            send(c, m.src, PD_GRAFT, m.mono, m.round);
             add_eager(c, bit(tab_insert(c, m.src)));
         }
         break;
-    case PD_IGNORED: {                             // :592-598 ack_outstanding/5: the row {From, {Id, Mod, Round, Root}}
-        const int i = tab_find(c, m.src);
-        if (i >= 0 && m.round == c.h.myround && delivered) c.m[S_OUT] &= ~bit(i);
+    case PD_IGNORED:                               // :592-598 ack_outstanding/5
+        ack_rows(c, m.src, m.mono, m.round);
         break;
-    }
     case PD_GRAFT:                                 // :600-605 -> handle_graft/7 :880-906
-        if (delivered) {                           // Mod:graft -> {ok, M}
+        if (delivered(c, m.mono)) {                // Mod:graft -> {ok, M} (one epoch: never stale)
             add_eager(c, bit(tab_insert(c, m.src)));
-            send(c, m.src, PD_BROADCAST, m.round);
+            send(c, m.src, PD_BROADCAST, m.mono, m.round);
         }                                          // {error, not_found}: logged only
         break;
     default:
@@ -174,17 +210,25 @@ __device__ void handle(Ctx& c, const PdMsg& m) {
 // {update, Members} as a set delta (:607-639)
 __device__ void apply_update(Ctx& c, uint32_t added, uint32_t removed) {
     if (added != kNone) {
-        const unsigned long long b = bit(tab_insert(c, added));
+        const PdBits b = bit(tab_insert(c, added));
         c.m[S_MEM] |= b;
         if (added != c.v) c.m[S_CE] |= b;          // common_eagers U New, minus self (reset_peers)
-        c.m[S_EAG] = 0;                              // reset_peers: the per-root maps are dropped
-        c.m[S_LAZ] = 0;
+        c.m[S_EAG] = PdBits::none();                 // reset_peers: the per-root maps are dropped
+        c.m[S_LAZ] = PdBits::none();
         c.h.flags &= ~1u;
     }
     if (removed != kNone) {                        // neighbors_down/2
         const int i = tab_find(c, removed);
         if (i >= 0)
             for (int k = 0; k < S_NSET; k++) c.m[k] &= ~bit(i);
+        uint32_t w = 0;                            // ... and deletes the outstanding rows to it
+        for (uint32_t j = 0; j < c.h.nrow; j++) {
+            const PdRow r = c.rows[j];
+            if (r.peer == removed) continue;
+            if (w != j) c.rows[w] = r;
+            w++;
+        }
+        c.h.nrow = w;
     }
 }
 
@@ -251,6 +295,12 @@ __device__ void load(Ctx& c, const PdArgs& a, uint32_t v) {
     c.h = a.head[v];
     c.tab = a.tab + (size_t)v * kPdTab;
     for (int k = 0; k < S_NSET; k++) c.m[k] = a.mask[(size_t)v * S_NSET + k];
+    c.rows = a.rows + (size_t)v * kPdRows;
+    if (a.mono > c.h.dbase) {                      // slide the delivered window to the newest serial
+        const uint32_t d = a.mono - c.h.dbase;
+        c.h.dmask = d >= 64 ? 0ull : c.h.dmask << d;
+        c.h.dbase = a.mono;
+    }
     c.pv = a.pv + (size_t)v * kScPv;
     c.npv = a.sch[v].npv;
     for (int i = 0; i < 6; i++) c.sent[i] = 0;
@@ -309,14 +359,13 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
             vals[8] = 1;
         }
         // 3. handle_info(lazy_tick): send_lazy/0, rows persist
-        unsigned long long o = c.m[S_OUT], live_rows = 0;
-        while (o) {
-            const int i = __ffsll(o) - 1;
-            o &= o - 1;
-            const uint32_t t = c.tab[i];
-            if (!a.alive[t] || !connected(c, t)) continue;
+        unsigned long long live_rows = 0;
+        const uint32_t nr = c.h.nrow;
+        for (uint32_t i = 0; i < nr; i++) {
+            const PdRow r = c.rows[i];
+            if (!a.alive[r.peer] || !connected(c, r.peer)) continue;
             live_rows++;
-            if (a.tick) send(c, t, PD_IHAVE, c.h.myround);
+            if (a.tick) send(c, r.peer, PD_IHAVE, r.mono, r.round);
         }
         if (c.h.ntab > kPdTab - 8) tab_compact(c);
         store(c);
@@ -324,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
         vals[6] = c.dropped;
         vals[7] = c.deliv;
         vals[9] = c.err;
-        vals[11] = c.h.mono == a.mono && a.mono != 0;
+        vals[11] = delivered(c, a.mono);
         vals[12] = 1;
         vals[13] = live_rows;
     }
@@ -338,9 +387,9 @@ __global__ void pd_origin(PdArgs a, uint32_t root) {
     unsigned long long vals[kPdNStat];
     Ctx c;
     load(c, a, root);
-    c.h.mono = a.mono;
+    mark_delivered(c, a.mono);
     c.h.myround = 0;
-    push(c, 0ull, 0u);
+    push(c, PdBits::none(), a.mono, 0u);
     store(c);
     (void)vals;
     if (c.err) atomicOr(&a.stats[9], (unsigned long long)c.err);
@@ -356,12 +405,14 @@ __global__ __launch_bounds__(kBlock) void pd_init(PdArgs a, const uint32_t* __re
     h.ntab = 1;
     h.flags = list ? 2u : 0u;        // restarted: its inbox holds messages for the old incarnation
     h.myround = 0;
-    h.mono = 0;
+    h.dbase = a.mono;
+    h.dmask = 0;
+    h.nrow = 0;
     if (!list) h.seq = 0;
     a.head[v] = h;
     a.tab[(size_t)v * kPdTab] = v;
-    a.mask[(size_t)v * S_NSET + S_MEM] = 1ull;   // all_members = {self}
-    for (int m = 1; m < S_NSET; m++) a.mask[(size_t)v * S_NSET + m] = 0ull;
+    a.mask[(size_t)v * S_NSET + S_MEM] = PdBits::one(0);   // all_members = {self}
+    for (int m = 1; m < S_NSET; m++) a.mask[(size_t)v * S_NSET + m] = PdBits::none();
 }
 
 inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
@@ -409,7 +460,9 @@ struct PdState : ModuleState {
     uint32_t n = 0, cap = 0, mono = 0, root = 0;
     PdHead* head = nullptr;
     uint32_t* tab = nullptr;
-    unsigned long long *mask = nullptr, *stats = nullptr;
+    PdBits* mask = nullptr;
+    unsigned long long* stats = nullptr;
+    PdRow* rows = nullptr;
     PdMsg* msg[2] = {nullptr, nullptr};
     uint32_t* nmsg = nullptr;
     uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr, *list = nullptr;
@@ -417,7 +470,7 @@ struct PdState : ModuleState {
     uint32_t par = 0;
     uint64_t round = 0;
     ~PdState() override {
-        void* p[] = {head, tab, mask, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, list};
+        void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, list};
         for (void* x : p)
             if (x) (void)hipFree(x);
     }
@@ -443,7 +496,7 @@ int pd_args(psim_handle* h, const PdState& s, PdArgs& a) {
     a = PdArgs{};
     a.n = s.n; a.mono = s.mono; a.tick = 1;
     a.alive = sv.alive; a.pv = sv.pv; a.sch = sv.head; a.ev_cnt = sv.ev_cnt; a.ev = sv.ev;
-    a.head = s.head; a.tab = s.tab; a.mask = s.mask;
+    a.head = s.head; a.tab = s.tab; a.mask = s.mask; a.rows = s.rows;
     a.in = s.msg[s.par]; a.nin = s.nmsg + s.par;
     a.out = s.msg[s.par ^ 1]; a.nout = s.nmsg + (s.par ^ 1);
     a.out_cap = s.cap;
@@ -456,6 +509,10 @@ int pd_check(psim_handle* h, unsigned long long err, uint64_t round) {
     if (err & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: plumtree message queue full", (unsigned long long)round);
     if (err & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a peer table exceeded %u ids",
                                        (unsigned long long)round, kPdTab);
+    if (err & 4ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a vertex exceeded %u outstanding rows",
+                                       (unsigned long long)round, kPdRows);
+    if (err & 8ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a heartbeat older than 64 serials is still in flight",
+                                       (unsigned long long)round);
     return PSIM_OK;
 }
 
@@ -479,7 +536,8 @@ int psim_c3_setup(psim_handle* h, uint32_t n, uint32_t c, uint32_t periodic_roun
     const size_t N = n;
     const uint32_t nb = (n + kBlock - 1) / kBlock;
     const bool ok = pd_alloc((void**)&s->head, N * sizeof(PdHead)) && pd_alloc((void**)&s->tab, N * kPdTab * 4) &&
-                    pd_alloc((void**)&s->mask, N * 6 * 8) && pd_alloc((void**)&s->stats, kPdNStat * 8) &&
+                    pd_alloc((void**)&s->mask, N * kPdSets * sizeof(PdBits)) &&
+                    pd_alloc((void**)&s->rows, N * kPdRows * sizeof(PdRow)) && pd_alloc((void**)&s->stats, kPdNStat * 8) &&
                     pd_alloc((void**)&s->msg[0], size_t(s->cap) * sizeof(PdMsg)) &&
                     pd_alloc((void**)&s->msg[1], size_t(s->cap) * sizeof(PdMsg)) && pd_alloc((void**)&s->nmsg, 16) &&
                     pd_alloc((void**)&s->cnt, N * 4) && pd_alloc((void**)&s->cur, N * 4) &&
@@ -600,26 +658,35 @@ int psim_c3_get_plumtree(const psim_handle* h, uint32_t v, uint32_t* eager, size
     PDCHK(hh, hipStreamSynchronize(handle_stream(h)));
     PdHead hd;
     uint32_t tab[kPdTab];
-    unsigned long long m[6];
+    PdBits m[kPdSets];
+    PdRow rows[kPdRows];
     PDCHK(hh, hipMemcpy(&hd, s->head + v, sizeof hd, hipMemcpyDeviceToHost));
     PDCHK(hh, hipMemcpy(tab, s->tab + size_t(v) * kPdTab, sizeof tab, hipMemcpyDeviceToHost));
-    PDCHK(hh, hipMemcpy(m, s->mask + size_t(v) * 6, sizeof m, hipMemcpyDeviceToHost));
+    PDCHK(hh, hipMemcpy(m, s->mask + size_t(v) * kPdSets, sizeof m, hipMemcpyDeviceToHost));
+    PDCHK(hh, hipMemcpy(rows, s->rows + size_t(v) * kPdRows, sizeof rows, hipMemcpyDeviceToHost));
     const bool sets = hd.flags & 1u;
-    const unsigned long long E = sets ? m[3] : m[1], L = sets ? m[4] : m[2];
-    auto out = [&](unsigned long long mk, uint32_t* dst, size_t* n) {
-        std::vector<uint32_t> ids;
-        for (uint32_t i = 0; i < hd.ntab && i < kPdTab; i++)
-            if ((mk >> i) & 1ull) ids.push_back(tab[i]);
+    const PdBits E = sets ? m[3] : m[1], L = sets ? m[4] : m[2];
+    auto emit = [&](std::vector<uint32_t>& ids, uint32_t* dst, size_t* n) {
         std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
         if (dst)
             for (size_t i = 0; i < ids.size() && i < cap; i++) dst[i] = ids[i];
         if (n) *n = ids.size();
     };
+    auto out = [&](const PdBits& mk, uint32_t* dst, size_t* n) {
+        std::vector<uint32_t> ids;
+        for (uint32_t i = 0; i < hd.ntab && i < kPdTab; i++)
+            if (mk.test(i)) ids.push_back(tab[i]);
+        emit(ids, dst, n);
+    };
     out(E, eager, ne);
     out(L, lazy, nl);
-    out(m[5], outstanding, no);
-    if (delivered_mono) *delivered_mono = hd.mono;
-    if (recv_round) *recv_round = hd.myround;
+    std::vector<uint32_t> peers;
+    for (uint32_t i = 0; i < hd.nrow && i < kPdRows; i++) peers.push_back(rows[i].peer);
+    emit(peers, outstanding, no);
+    const bool cur = s->mono && hd.dbase == s->mono && (hd.dmask & 1ull);   // a lagging window top: not seen
+    if (delivered_mono) *delivered_mono = cur ? s->mono : 0;
+    if (recv_round) *recv_round = cur ? hd.myround : 0;
     return PSIM_OK;
 }
 

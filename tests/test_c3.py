@@ -91,6 +91,7 @@ def test_gpu_c3_parity(n, periodic, warm, churn_rounds):
     g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=periodic)
     o = O.C3(n, 5, periodic, SEED)
     r = 0
+    seen = []
     for v, cc in waves(n):
         g.join(v, cc)
         for a, b in zip(v, cc):
@@ -106,7 +107,7 @@ def test_gpu_c3_parity(n, periodic, warm, churn_rounds):
         mono = g.heartbeat(0)
         assert mono == o.heartbeat(0)
         for _ in range(8):
-            _step(g, o, r)
+            seen.append(_step(g, o, r))
             r += 1
         _compare(g, o, n, 0, mono)
     for i in range(churn_rounds):
@@ -121,9 +122,12 @@ def test_gpu_c3_parity(n, periodic, warm, churn_rounds):
         for a, b in zip(v, cc):
             o.crash(int(a))
             o.join(int(a), int(b))
-        _step(g, o, r)
+        seen.append(_step(g, o, r))
         r += 1
         _compare(g, o, n, 0, mono)
+    for k in ("prune", "i_have", "ignored_i_have", "graft"):    # the repair paths were exercised
+        assert sum(x["pt_sent"][k] for x in seen) > 0, k
+    assert sum(x["pt_dropped"] for x in seen) > 0
 
 
 @pytest.mark.gpu
