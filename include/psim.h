@@ -57,10 +57,17 @@ typedef struct psim_config {
     int32_t  device;               /* HIP device ordinal; -1 = current device  */
     uint32_t lazy_tick_rounds;     /* lazy tick every k rounds (>= 1)          */
     uint32_t exchange_tick_rounds; /* accepted for config parity; no effect */
-    uint32_t flags;                /* reserved, 0                              */
+    uint32_t flags;                /* PSIM_CFG_* bits                          */
     uint32_t _reserved;
     uint64_t seed;                 /* Philox key for the protocols that draw   */
 } psim_config;
+
+/* psim_config.flags: PSIM_CFG_BINNED routes a single-GPU handle's Plumtree
+ * messages as {receiver slot, word} records through coarse then fine
+ * receiver bins instead of scattering one HBM word per
+ * receiver slot (the default, and what sharded handles always run).  Both
+ * give identical results; the binned engine is the slower one on MI355X today. */
+#define PSIM_CFG_BINNED 1u
 
 /* Per-round counters, reduced on device (psim_step / psim_run). */
 typedef struct psim_round_stats {

@@ -96,15 +96,16 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
     }
 }
 
-// Append the nibble FIFO `f` holding `k` messages to (fifo, n); count kinds.
+// Append the nibble FIFO `f` to (fifo, n); count kinds (kCount).
+template <bool kCount>
 __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_t f, Ctr& c) {
     while (f) {
         const uint32_t t = f & 0xFu;
         f >>= 4;
         if (n < 4) fifo |= t << (4 * n);
-        else c.overflow |= 1u;
+        else if (kCount) c.overflow |= 1u;
         n++;
-        c.kind(t);
+        if (kCount) c.kind(t);
     }
 }
 
@@ -121,10 +122,158 @@ __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32
     }
 }
 
-// One vertex, one round.  `rep` is this thread's LDS column (stride kBlock)
-// for the reply FIFOs of its slots.  `pend`: the vertex's 16-vertex group
-// was flagged (it may have words); `due`: the lazy tick fires and it holds
-// outstanding rows.
+// A vertex's Plumtree state while it handles one round (both engines).
+struct VSt {
+    uint32_t eager, lazy, outst, outst0, myround, rseq, ep;
+    uint32_t push_mask, push_pos;   // eager_push of this round: targets, delivering slot
+    int32_t live_delta;
+    bool rcv;
+};
+
+__device__ __forceinline__ void vst_load(const PtArgs& a, uint32_t v, const uint4& st, VSt& x) {
+    x.eager = st.x;
+    x.lazy = st.y;
+    x.outst = x.outst0 = st.z;
+    x.myround = st.w & 0xFFFFu;
+    x.rseq = (st.w >> 16) & 0xFFu;
+    x.ep = st.w >> 24;
+    if (x.ep != a.epoch8) {     // all_peers/3 (:1278-1282): no map entry -> common sets
+        x.eager = a.memb[v];    // common_eagers = Members -- self
+        x.lazy = 0;             // common_lazys = [] (start_link/0 :253-254)
+        x.ep = a.epoch8;
+    }
+    x.rcv = x.rseq == a.mono8;
+    x.push_mask = 0;
+    x.push_pos = 0xFFFFFFFFu;
+    x.live_delta = 0;
+}
+
+// handle_cast of the messages of one inbox word (slot s of the vertex whose
+// row starts at rs); returns the FIFO of replies sent back over s.
+__device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32_t s, uint32_t w, VSt& x, Ctr& c) {
+    const uint32_t b = 1u << s;
+    uint32_t f = w & 0xFFFFu;
+    const uint32_t rnd = w >> 16;
+    uint32_t r = 0, rn = 0;
+    while (f) {
+        const uint32_t t = f & 0xFu;
+        f >>= 4;
+        uint32_t reply = 0;
+        switch (t) {
+        case PSIM_MSG_BROADCAST:           // handle_cast :571-578
+            if (!x.rcv) {                  // merge/2 -> true; handle_broadcast(true) :852-857
+                x.rcv = true;
+                x.rseq = a.mono8;
+                x.myround = rnd + 1;
+                if (x.myround > 0xFFFFu) { c.overflow |= 2u; x.myround = 0xFFFFu; }
+                c.deliv++;
+                x.eager |= b;              // add_eager(From, Root)
+                x.lazy &= ~b;
+                x.push_mask = x.eager & ~b;  // eager_push(.., Round+1, Root, From)
+                x.push_pos = s;
+                if (x.outst) c.overflow |= 4u;
+                {                          // schedule_lazy_push(.., Round+1, Root, From)
+                    uint32_t add = x.lazy & ~b & ~x.outst;
+                    x.outst |= x.lazy & ~b;
+                    while (add) {
+                        const uint32_t q = __ffs(add) - 1;
+                        add &= add - 1;
+                        x.live_delta += bit_alive(a.alive, a.col[rs + q]);
+                    }
+                }
+            } else {                       // handle_broadcast(false) :843-850
+                x.eager &= ~b;             // add_lazy(From, Root)
+                x.lazy |= b;
+                reply = PSIM_MSG_PRUNE;
+            }
+            break;
+        case PSIM_MSG_PRUNE:               // :580-584
+            x.eager &= ~b;
+            x.lazy |= b;
+            break;
+        case PSIM_MSG_IHAVE:               // :586-590 -> handle_ihave/7 :861-876
+            if (x.rcv) {
+                reply = PSIM_MSG_IGNORED;
+            } else {
+                reply = PSIM_MSG_GRAFT;
+                x.eager |= b;
+                x.lazy &= ~b;
+            }
+            break;
+        case PSIM_MSG_IGNORED:             // :592-598 ack_outstanding/5
+            if (x.outst & b) {
+                x.outst &= ~b;
+                x.live_delta -= bit_alive(a.alive, a.col[rs + s]);
+            }
+            break;
+        case PSIM_MSG_GRAFT:               // :600-605 -> handle_graft/7 :880-906
+            if (x.rcv) {                   // Mod:graft -> {ok, M}
+                x.eager |= b;
+                x.lazy &= ~b;
+                reply = PSIM_MSG_BROADCAST;  // same Round (Q3)
+            }                              // {error, not_found}: logged only
+            break;
+        default:
+            break;
+        }
+        if (reply) {
+            if (rn < 4) r |= reply << (4 * rn);
+            else c.overflow |= 1u;
+            rn++;
+        }
+    }
+    return r;
+}
+
+// lazy tick: send_lazy/0 (:992-1019), connected peers only, rows persist
+__device__ __forceinline__ uint32_t pt_ihave(const PtArgs& a, uint32_t rs, const VSt& x) {
+    uint32_t ihave = 0;
+    if (a.tick && x.outst) {
+        uint32_t m = x.outst;
+        while (m) {
+            const uint32_t q = __ffs(m) - 1;
+            m &= m - 1;
+            if (bit_alive(a.alive, a.col[rs + q])) ihave |= 1u << q;
+        }
+    }
+    return ihave;
+}
+
+// The word sent over slot s this round (0 = nothing): the replies r to s's
+// messages and the eager push -- before them when s comes after the slot
+// that delivered the heartbeat, after them otherwise -- then the i_have.
+template <bool kCount>
+__device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x, uint32_t ihave, Ctr& c) {
+    const uint32_t b = 1u << s;
+    if (!r && !((x.push_mask | ihave) & b)) return 0u;
+    uint32_t fifo = 0, n = 0;
+    const bool p = (x.push_mask & b) != 0;
+    if (p && s > x.push_pos) fifo_append<kCount>(fifo, n, PSIM_MSG_BROADCAST, c);
+    fifo_append<kCount>(fifo, n, r, c);
+    if (p && s < x.push_pos) fifo_append<kCount>(fifo, n, PSIM_MSG_BROADCAST, c);
+    if (ihave & b) fifo_append<kCount>(fifo, n, PSIM_MSG_IHAVE, c);
+    return fifo | (x.myround << 16);
+}
+
+// Write back the state record and the outstanding flag; returns the change
+// in "holds outstanding rows" (-1, 0, +1).
+__device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint4& st, const VSt& x, Ctr& c) {
+    const uint32_t nw = x.myround | (x.rseq << 16) | (x.ep << 24);
+    if (x.eager != st.x || x.lazy != st.y || x.outst != st.z || nw != st.w)
+        a.vs[v] = make_uint4(x.eager, x.lazy, x.outst, nw);
+    c.live_delta += (uint32_t)x.live_delta;
+    if ((x.outst0 != 0) != (x.outst != 0)) {
+        a.ost[v] = x.outst != 0;
+        c.ost_delta += x.outst != 0 ? 1u : 0xFFFFFFFFu;
+        return x.outst != 0 ? 1 : -1;
+    }
+    return 0;
+}
+
+// Slot-scatter engine: one vertex, one round.  `rep` is this thread's LDS
+// column (stride kBlock) for the reply FIFOs of its slots.  `pend`: the
+// vertex's 16-vertex group was flagged (it may have words); `due`: the lazy
+// tick fires and it holds outstanding rows.
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
     const uint32_t rs = a.rowp[v];
@@ -144,142 +293,32 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     }
     c.active++;
     const uint4 st = a.vs[v];
-    uint32_t eager = st.x, lazy = st.y, outst = st.z;
-    uint32_t myround = st.w & 0xFFFFu;
-    uint32_t rseq = (st.w >> 16) & 0xFFu;
-    uint32_t ep = st.w >> 24;
-    if (ep != a.epoch8) {       // all_peers/3 (:1278-1282): no map entry -> common sets
-        eager = a.memb[v];      // common_eagers = Members -- self
-        lazy = 0;               // common_lazys = [] (start_link/0 :253-254)
-        ep = a.epoch8;
-    }
-    bool rcv = rseq == a.mono8;
-    const uint32_t outst0 = outst;
-    uint32_t push_mask = 0, push_pos = 0xFFFFFFFFu;
-    int32_t live_delta = 0;
-
+    VSt x;
+    vst_load(a, v, st, x);
     if (pend) {
         for (uint32_t s = 0; s < deg; s++) {
             const uint32_t w = a.in_cur[rs + s];
-            uint32_t r = 0, rn = 0;
+            uint32_t r = 0;
             if (w) {
                 a.in_cur[rs + s] = 0;
-                const uint32_t b = 1u << s;
-                uint32_t f = w & 0xFFFFu;
-                const uint32_t rnd = w >> 16;
-                while (f) {
-                    const uint32_t t = f & 0xFu;
-                    f >>= 4;
-                    uint32_t reply = 0;
-                    switch (t) {
-                    case PSIM_MSG_BROADCAST:           // handle_cast :571-578
-                        if (!rcv) {                    // merge/2 -> true; handle_broadcast(true) :852-857
-                            rcv = true;
-                            rseq = a.mono8;
-                            myround = rnd + 1;
-                            if (myround > 0xFFFFu) { c.overflow |= 2u; myround = 0xFFFFu; }
-                            c.deliv++;
-                            eager |= b;                // add_eager(From, Root)
-                            lazy &= ~b;
-                            push_mask = eager & ~b;    // eager_push(.., Round+1, Root, From)
-                            push_pos = s;
-                            if (outst) c.overflow |= 4u;
-                            {                          // schedule_lazy_push(.., Round+1, Root, From)
-                                uint32_t add = lazy & ~b & ~outst;
-                                outst |= lazy & ~b;
-                                while (add) {
-                                    const uint32_t q = __ffs(add) - 1;
-                                    add &= add - 1;
-                                    live_delta += bit_alive(a.alive, a.col[rs + q]);
-                                }
-                            }
-                        } else {                       // handle_broadcast(false) :843-850
-                            eager &= ~b;               // add_lazy(From, Root)
-                            lazy |= b;
-                            reply = PSIM_MSG_PRUNE;
-                        }
-                        break;
-                    case PSIM_MSG_PRUNE:               // :580-584
-                        eager &= ~b;
-                        lazy |= b;
-                        break;
-                    case PSIM_MSG_IHAVE:               // :586-590 -> handle_ihave/7 :861-876
-                        if (rcv) {
-                            reply = PSIM_MSG_IGNORED;
-                        } else {
-                            reply = PSIM_MSG_GRAFT;
-                            eager |= b;
-                            lazy &= ~b;
-                        }
-                        break;
-                    case PSIM_MSG_IGNORED:             // :592-598 ack_outstanding/5
-                        if (outst & b) {
-                            outst &= ~b;
-                            live_delta -= bit_alive(a.alive, a.col[rs + s]);
-                        }
-                        break;
-                    case PSIM_MSG_GRAFT:               // :600-605 -> handle_graft/7 :880-906
-                        if (rcv) {                     // Mod:graft -> {ok, M}
-                            eager |= b;
-                            lazy &= ~b;
-                            reply = PSIM_MSG_BROADCAST;  // same Round (Q3)
-                        }                              // {error, not_found}: logged only
-                        break;
-                    default:
-                        break;
-                    }
-                    if (reply) {
-                        if (rn < 4) r |= reply << (4 * rn);
-                        else c.overflow |= 1u;
-                        rn++;
-                    }
-                }
+                r = pt_word(a, rs, s, w, x, c);
             }
             rep[s * kBlock] = (uint16_t)r;
         }
     }
-
-    // lazy tick: send_lazy/0 (:992-1019), connected peers only, rows persist
-    uint32_t ihave = 0;
-    if (a.tick && outst) {
-        uint32_t m = outst;
-        while (m) {
-            const uint32_t q = __ffs(m) - 1;
-            m &= m - 1;
-            if (bit_alive(a.alive, a.col[rs + q])) ihave |= 1u << q;
-        }
-    }
-
-    // compose and scatter the outgoing words
-    const uint32_t any = push_mask | ihave;
+    const uint32_t ihave = pt_ihave(a, rs, x);
     bool sent = false;
     for (uint32_t s = 0; s < deg; s++) {
-        const uint32_t r = pend ? rep[s * kBlock] : 0u;
-        const uint32_t b = 1u << s;
-        if (!r && !(any & b)) continue;
-        uint32_t fifo = 0, n = 0;
-        const bool p = (push_mask & b) != 0;
-        if (p && s > push_pos) fifo_append(fifo, n, PSIM_MSG_BROADCAST, c);
-        fifo_append(fifo, n, r, c);
-        if (p && s < push_pos) fifo_append(fifo, n, PSIM_MSG_BROADCAST, c);
-        if (ihave & b) fifo_append(fifo, n, PSIM_MSG_IHAVE, c);
-        const uint32_t e = rs + s;
-        deliver_word(a, e, fifo | (myround << 16));
+        const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, c);
+        if (!w) continue;
+        deliver_word(a, rs + s, w);
         sent = true;
     }
     if (sent) {
         c.senders++;
         c.degsum += deg;
     }
-
-    const uint32_t nw = myround | (rseq << 16) | (ep << 24);
-    if (eager != st.x || lazy != st.y || outst != st.z || nw != st.w)
-        a.vs[v] = make_uint4(eager, lazy, outst, nw);
-    if ((outst0 != 0) != (outst != 0)) {
-        a.ost[v] = outst != 0;
-        c.ost_delta += outst != 0 ? 1u : 0xFFFFFFFFu;
-    }
-    c.live_delta += (uint32_t)live_delta;
+    vst_store(a, v, st, x, c);
 }
 
 // A workgroup owns kChunkV consecutive vertices.  Each thread looks at 4 of
@@ -333,6 +372,219 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     flush_counters(c, a.stats, a.ost_total);
 }
 
+// ---------------------------------------------------------------------------
+// Binned engine (single GPU).  A round is two launches:
+//   pb_route_kernel: the records emitted last round sit in coarse receiver
+//     bins (2^cv_shift vertices); each workgroup moves <= kRouteK of one
+//     coarse bin's records into its fine bins (2^fv_shift vertices) --
+//     an LDS histogram, one atomicAdd per fine bin, contiguous runs out;
+//   pb_round_kernel: a workgroup owns one fine bin: it drops the bin's
+//     records into an LDS copy of the bin's receiver slots (the same words
+//     the slot-scatter engine keeps in HBM), runs every vertex of the bin
+//     through the shared handlers, and appends its outgoing words as
+//     {receiver slot, word} records to the coarse bins of the next round
+//     (histogram, one atomicAdd per coarse bin, contiguous runs).
+// Each bin region is the bin's receiver-slot range, which bounds its record
+// count (a receiver slot has one sender and gets <= 1 word per round), so no
+// region can overflow.  Random 4-byte scatters into HBM become appends of
+// 8-byte records in runs plus LDS scatters.
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void pb_route_kernel(PtArgs a) {
+    __shared__ uint32_t fsb[kCoarseMax + 1];
+    __shared__ uint32_t hist[kCoarseMax];
+    __shared__ uint32_t base[kCoarseMax];
+    constexpr uint32_t kPer = kRouteK / kBlock;
+    const uint32_t t = threadIdx.x;
+    const uint32_t G = 1u << (a.cv_shift - a.fv_shift);
+    const uint32_t total = a.nc * kCoarseShards * a.chunks;
+    for (uint32_t blk = blockIdx.x; blk < total; blk += gridDim.x) {
+        const uint32_t cs = blk / a.chunks, j = blk - cs * a.chunks;
+        const uint32_t c = cs / kCoarseShards;
+        const uint32_t nrec = a.cnt_c_cur[cs];
+        const uint32_t lo = j * kRouteK;
+        if (lo >= nrec) continue;                     // uniform
+        const uint32_t hi = min(nrec, lo + kRouteK);
+        const uint32_t f0 = c * G;
+        const uint32_t ng = min(G, a.nf - f0);
+        for (uint32_t g = t; g <= ng; g += kBlock) fsb[g] = a.fslot[f0 + g];
+        for (uint32_t g = t; g < ng; g += kBlock) hist[g] = 0;
+        const uint32_t cb = a.csub[cs];
+        uint2 r[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) {
+            const uint32_t i = lo + t + q * kBlock;
+            if (i < hi) r[q] = a.rec_c[cb + i];
+        }
+        __syncthreads();
+        uint32_t fb[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) {
+            const uint32_t i = lo + t + q * kBlock;
+            fb[q] = 0xFFFFFFFFu;
+            if (i < hi) {
+                uint32_t l = 0, h = ng;               // fsb[l] <= slot < fsb[h]
+                while (h - l > 1) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (fsb[m] <= r[q].x) l = m; else h = m;
+                }
+                fb[q] = l;
+                atomicAdd(&hist[l], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t g = t; g < ng; g += kBlock) {
+            const uint32_t k = hist[g];
+            if (k) base[g] = fsb[g] + atomicAdd(&a.cnt_f[f0 + g], k);
+            hist[g] = 0;
+        }
+        __syncthreads();
+        bool bad = false;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++)
+            if (fb[q] != 0xFFFFFFFFu) {
+                const uint32_t pos = base[fb[q]] + atomicAdd(&hist[fb[q]], 1u);
+                if (pos < fsb[fb[q] + 1]) a.rec_f[pos] = r[q];   // a region holds its slots' words
+                else bad = true;
+            }
+        if (bad) atomicOr(&a.stats[S_OVERFLOW], 8ull);
+        __syncthreads();                              // LDS reuse by the next chunk
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
+    constexpr uint32_t kVPer = kBinVMax / kBlock;
+    __shared__ uint32_t words[kBinSlots];            // the bin's receiver slots, then the replies
+    __shared__ uint32_t rpc[kBinVMax + 1];           // row starts of the bin's vertices
+    __shared__ uint16_t cand[kBinVMax];              // bin-local vertex | 0x8000 = has words
+    __shared__ uint32_t hist[kCoarseMax];
+    __shared__ uint32_t base[kCoarseMax];
+    __shared__ uint32_t ncand;
+    __shared__ int obd;
+    const uint32_t t = threadIdx.x;
+    // the coarse counts route read this round are free for the round after next
+    for (uint32_t i = blockIdx.x * kBlock + t; i < a.nc * kCoarseShards; i += gridDim.x * kBlock)
+        a.cnt_c_cur[i] = 0;
+    Ctr c;
+    c.zero();
+    bool any_bin = false;
+    for (uint32_t f = blockIdx.x; f < a.nf; f += gridDim.x) {
+        uint32_t nrec = a.cnt_f[f];
+        const bool due = a.tick && a.obin[f] != 0;
+        if (nrec == 0 && !due) continue;              // uniform: idle bin
+        any_bin = true;
+        const uint32_t v0 = f << a.fv_shift;
+        const uint32_t nv = min(1u << a.fv_shift, a.n - v0);
+        const uint32_t sb = a.fslot[f], ns = a.fslot[f + 1] - sb;
+        for (uint32_t i = t; i <= nv; i += kBlock) rpc[i] = a.rowp[v0 + i] - sb;
+        for (uint32_t i = t; i < ns; i += kBlock) words[i] = 0;
+        for (uint32_t i = t; i < a.nc; i += kBlock) hist[i] = 0;
+        if (t == 0) { obd = 0; ncand = 0; }
+        if (nrec > ns) {                              // cannot happen: one word per receiver slot
+            nrec = ns;
+            c.overflow |= 8u;
+        }
+        uint2 rr[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)              // the first records are in flight during the zeroing
+            if (t + q * kBlock < nrec) rr[q] = a.rec_f[sb + t + q * kBlock];
+        __syncthreads();
+        if (t == 0 && nrec) a.cnt_f[f] = 0;           // consumed (route of the next round adds again)
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+            if (t + q * kBlock < nrec) words[rr[q].x - sb] = rr[q].y;
+        for (uint32_t i = t + 4 * kBlock; i < nrec; i += kBlock) {
+            const uint2 r = a.rec_f[sb + i];
+            words[r.x - sb] = r.y;
+        }
+        __syncthreads();
+        // candidates: vertices with words, and (tick) vertices holding rows
+#pragma unroll
+        for (uint32_t k = 0; k < kVPer; k++) {
+            const uint32_t lv = t + k * kBlock;
+            if (lv >= nv) continue;
+            uint32_t any = 0;
+            for (uint32_t i = rpc[lv]; i < rpc[lv + 1]; i++) any |= words[i];
+            if (any || (due && a.ost[v0 + lv]))
+                cand[atomicAdd(&ncand, 1u)] = (uint16_t)(lv | (any ? 0x8000u : 0u));
+        }
+        __syncthreads();
+        const uint32_t nk = ncand;
+        // handle: replies are written over the words
+        VSt x[kVPer];
+        uint32_t ihave[kVPer], lvk[kVPer];
+        bool send[kVPer];
+        int od = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kVPer; k++) {
+            send[k] = false;
+            ihave[k] = 0;
+            lvk[k] = 0;
+            const uint32_t i = t + k * kBlock;
+            if (i >= nk) continue;
+            const uint32_t cv = cand[i];
+            const uint32_t lv = cv & 0x7FFFu;
+            const bool pend = (cv & 0x8000u) != 0;
+            const uint32_t v = v0 + lv;
+            lvk[k] = lv;
+            if (!bit_alive(a.alive, v)) continue;     // a dead vertex drops its words
+            c.active++;
+            const uint32_t ls = rpc[lv], deg = rpc[lv + 1] - ls, rs = sb + ls;
+            const uint4 st = a.vs[v];
+            vst_load(a, v, st, x[k]);
+            if (pend)
+                for (uint32_t s = 0; s < deg; s++) {
+                    const uint32_t w = words[ls + s];
+                    if (w) words[ls + s] = pt_word(a, rs, s, w, x[k], c);
+                }
+            ihave[k] = pt_ihave(a, rs, x[k]);
+            od += vst_store(a, v, st, x[k], c);
+            send[k] = true;
+        }
+        if (od) atomicAdd(&obd, od);
+        // emit, pass 1: records per coarse bin of the next round
+#pragma unroll
+        for (uint32_t k = 0; k < kVPer; k++) {
+            if (!send[k]) continue;
+            const uint32_t ls = rpc[lvk[k]], deg = rpc[lvk[k] + 1] - ls, rs = sb + ls;
+            for (uint32_t s = 0; s < deg; s++)
+                if (pt_out<false>(s, words[ls + s], x[k], ihave[k], c))
+                    atomicAdd(&hist[a.col[rs + s] >> a.cv_shift], 1u);
+        }
+        __syncthreads();
+        const uint32_t sh = f & (kCoarseShards - 1);     // this bin's sub-region of every coarse bin
+        for (uint32_t i = t; i < a.nc; i += kBlock) {
+            const uint32_t k = hist[i];
+            if (k) base[i] = a.csub[i * kCoarseShards + sh] + atomicAdd(&a.cnt_c_nxt[i * kCoarseShards + sh], k);
+            hist[i] = 0;
+        }
+        if (t == 0 && obd) a.obin[f] += (uint32_t)obd;
+        __syncthreads();
+        // pass 2: the records
+#pragma unroll
+        for (uint32_t k = 0; k < kVPer; k++) {
+            if (!send[k]) continue;
+            const uint32_t ls = rpc[lvk[k]], deg = rpc[lvk[k] + 1] - ls, rs = sb + ls;
+            bool sent = false;
+            for (uint32_t s = 0; s < deg; s++) {
+                const uint32_t w = pt_out<true>(s, words[ls + s], x[k], ihave[k], c);
+                if (!w) continue;
+                const uint32_t cb = a.col[rs + s] >> a.cv_shift;
+                const uint32_t pos = base[cb] + atomicAdd(&hist[cb], 1u);
+                if (pos < a.csub[cb * kCoarseShards + sh + 1]) a.rec_c[pos] = make_uint2(a.rev[rs + s], w);
+                else c.overflow |= 8u;
+                sent = true;
+            }
+            if (sent) {
+                c.senders++;
+                c.degsum += deg;
+            }
+        }
+        __syncthreads();                              // LDS reuse by the next bin
+    }
+    if (__syncthreads_or(any_bin)) flush_counters(c, a.stats, a.ost_total);
+}
+
 // The origin's {broadcast, Id, Payload, Mod} cast (:565-569): eager_push/4
 // and schedule_lazy_push/3 with Round 0, Root = From = the origin; the
 // backend already did add_timestamp (backend :341-368).
@@ -353,7 +605,12 @@ __global__ void pt_origin_kernel(PtArgs a) {
         const uint32_t b = 1u << s;
         const uint32_t e = rs + s;
         if (eager & b) {
-            deliver_word(a, e, PSIM_MSG_BROADCAST);  // Round 0
+            if (a.rec_c) {                           // binned: a record for the next route
+                const uint32_t cs = (a.col[e] >> a.cv_shift) * kCoarseShards + ((v >> a.fv_shift) & (kCoarseShards - 1));
+                a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] = make_uint2(a.rev[e], PSIM_MSG_BROADCAST);
+            } else {
+                deliver_word(a, e, PSIM_MSG_BROADCAST);  // Round 0
+            }
             nmsg++;
         }
         if ((lazy & b) && !(outst & b)) {
@@ -364,6 +621,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
     a.vs[v] = make_uint4(eager, lazy, outst, 0u | (a.mono8 << 16) | (ep << 24));
     if ((outst0 != 0) != (outst != 0)) {
         a.ost[v] = 1;
+        if (a.obin) a.obin[v >> a.fv_shift] += 1u;
         atomicAdd(&a.stats[S_OST_DELTA], 1ull);
         atomicAdd(a.ost_total, 1);
     }
@@ -501,6 +759,12 @@ uint32_t grid_for(uint32_t n) {
 }  // namespace
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
+    if (a.rec_c) {
+        const uint32_t nr = a.nc * kCoarseShards * a.chunks;
+        hipLaunchKernelGGL(pb_route_kernel, dim3(nr < 2048u ? nr : 2048u), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(pb_round_kernel, dim3(a.nf < 4096u ? a.nf : 4096u), dim3(kBlock), 0, s, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(pt_round_kernel, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }

@@ -42,6 +42,13 @@ struct psim_handle {
     uint32_t* in[2] = {nullptr, nullptr};
     uint8_t* pend[2] = {nullptr, nullptr};
     uint8_t* ost = nullptr;
+    // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
+    struct Bin {
+        uint2 *rec_c = nullptr, *rec_f = nullptr;
+        uint32_t *cnt_c[2] = {nullptr, nullptr}, *cnt_f = nullptr, *csub = nullptr, *fslot = nullptr, *obin = nullptr;
+        uint32_t fv_shift = 0, cv_shift = 0, nf = 0, nc = 0, chunks = 0;
+        std::vector<uint32_t> h_csub, h_fslot;
+    } bin;
     unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
     unsigned long long* h_stats = nullptr;   // pinned mirror
     unsigned long long* scratch = nullptr;   // 1 counter
@@ -194,6 +201,13 @@ void free_graph(psim_handle* h) {
     h->vs = nullptr;
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
+    {
+        auto& b = h->bin;
+        void* bp[] = {b.rec_c, b.rec_f, b.cnt_c[0], b.cnt_c[1], b.cnt_f, b.csub, b.fslot, b.obin};
+        for (void* p : bp)
+            if (p) (void)hipFree(p);
+        b = psim_handle::Bin();
+    }
     auto& sh = h->sh;
     void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map};
     for (void* p : sp)
@@ -231,7 +245,49 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.mono8 = h->serial & 0xFFu;
     a.epoch8 = h->epoch & 0xFFu;
     a.root = h->root;
+    if (h->bin.rec_c) {
+        const auto& b = h->bin;
+        a.rec_c = b.rec_c;
+        a.rec_f = b.rec_f;
+        a.cnt_c_cur = b.cnt_c[par];
+        a.cnt_c_nxt = b.cnt_c[par ^ 1];
+        a.cnt_f = b.cnt_f;
+        a.csub = b.csub;
+        a.fslot = b.fslot;
+        a.obin = b.obin;
+        a.fv_shift = b.fv_shift;
+        a.cv_shift = b.cv_shift;
+        a.nf = b.nf;
+        a.nc = b.nc;
+        a.chunks = b.chunks;
+    }
     return a;
+}
+
+// Binned engine geometry: fine bins of 2^fv vertices whose slots fit the LDS
+// inbox, coarse bins of 2^cv vertices with about sqrt(#fine) fine bins each.
+bool bin_geometry(const std::vector<uint32_t>& rp, uint32_t n, uint32_t& fv, uint32_t& cv, uint32_t& nf,
+                  uint32_t& nc) {
+    fv = 0;
+    while ((1u << (fv + 1)) <= kBinVMax) fv++;
+    for (;; fv--) {
+        uint32_t mx = 0;
+        for (uint64_t v = 0; v < n; v += (1u << fv)) {
+            const uint64_t e = std::min<uint64_t>(n, v + (1u << fv));
+            mx = std::max(mx, rp[e] - rp[v]);
+        }
+        if (mx <= kBinSlots) break;
+        if (fv == 0) return false;
+    }
+    nf = uint32_t((uint64_t(n) + (1u << fv) - 1) >> fv);
+    uint32_t g = 0;                                   // fine bins per coarse bin = 2^g ~ sqrt(nf)
+    while ((1ull << (2 * g)) < nf) g++;
+    while (g > 0 && (1u << g) > kCoarseMax) g--;
+    while (((uint64_t(nf) + (1u << g) - 1) >> g) > kCoarseMax) g++;
+    if ((1u << g) > kCoarseMax) return false;
+    cv = fv + g;
+    nc = uint32_t((uint64_t(nf) + (1u << g) - 1) >> g);
+    return true;
 }
 
 void reduce_row(const unsigned long long* row, unsigned long long* out) {
@@ -284,7 +340,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             if (r[S_OVERFLOW])
                 return fail(h, PSIM_EOVERFLOW,
                             "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 65535, "
-                            "4: outstanding rows of an older heartbeat)",
+                            "4: outstanding rows of an older heartbeat, 8: a bin region overran)",
                             (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
             uint64_t msgs = 0;
             for (int t = 1; t <= 5; t++) msgs += r[t];
@@ -559,11 +615,41 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
     const size_t nw = (size_t(n) + 31) / 32;
     const size_t ng = (size_t(nl) + (1u << kGroupShift) - 1) >> kGroupShift;
+    const bool binned = W == 1 && (h->cfg.flags & PSIM_CFG_BINNED);
+    auto& bn = h->bin;
+    if (binned) {
+        if (!bin_geometry(rpl, nl, bn.fv_shift, bn.cv_shift, bn.nf, bn.nc))
+            return fail(h, PSIM_EINVAL, "overlay does not fit the binned engine (drop PSIM_CFG_BINNED)");
+        // sub-region (c, s) holds the records fine bins f = s (mod kCoarseShards)
+        // send into coarse bin c: at most their slots whose peer lies in c
+        const size_t NS = size_t(bn.nc) * kCoarseShards;
+        std::vector<uint32_t> cap(NS, 0u);
+        for (uint32_t v = 0; v < nl; v++) {
+            const uint32_t sh = (v >> bn.fv_shift) & (kCoarseShards - 1);
+            for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) cap[size_t(cl[e] >> bn.cv_shift) * kCoarseShards + sh]++;
+        }
+        bn.h_csub.assign(NS + 1, 0u);
+        uint32_t mx = 0;
+        for (size_t i = 0; i < NS; i++) {
+            bn.h_csub[i + 1] = bn.h_csub[i] + cap[i];
+            mx = std::max(mx, cap[i]);
+        }
+        bn.chunks = std::max<uint32_t>(1u, (mx + kRouteK - 1) / kRouteK);
+        bn.h_fslot.resize(size_t(bn.nf) + 1);
+        for (uint32_t f = 0; f <= bn.nf; f++) bn.h_fslot[f] = rpl[std::min<uint64_t>(nl, uint64_t(f) << bn.fv_shift)];
+    }
     if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, El * 4) != hipSuccess ||
         alloc((void**)&h->rev, El * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl) * 4) != hipSuccess ||
         alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
-        alloc((void**)&h->in[0], El * 4) != hipSuccess || alloc((void**)&h->in[1], El * 4) != hipSuccess ||
-        alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess ||
+        (!binned && (alloc((void**)&h->in[0], El * 4) != hipSuccess || alloc((void**)&h->in[1], El * 4) != hipSuccess ||
+                     alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess)) ||
+        (binned && (alloc((void**)&bn.rec_c, El * 8) != hipSuccess || alloc((void**)&bn.rec_f, El * 8) != hipSuccess ||
+                    alloc((void**)&bn.cnt_c[0], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
+                    alloc((void**)&bn.cnt_c[1], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
+                    alloc((void**)&bn.cnt_f, size_t(bn.nf) * 4) != hipSuccess ||
+                    alloc((void**)&bn.csub, bn.h_csub.size() * 4) != hipSuccess ||
+                    alloc((void**)&bn.fslot, (size_t(bn.nf) + 1) * 4) != hipSuccess ||
+                    alloc((void**)&bn.obin, size_t(bn.nf) * 4) != hipSuccess)) ||
         alloc((void**)&h->ost, size_t(nl) + 4) != hipSuccess ||
         (W > 1 && (alloc((void**)&sh.stage, El * 4) != hipSuccess ||
                    alloc((void**)&sh.rem, remflat.size() * 4) != hipSuccess ||
@@ -587,10 +673,19 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
     // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..
     HIPCHK(h, hipMemset(h->vs, 0, size_t(nl) * 16));
-    HIPCHK(h, hipMemset(h->in[0], 0, El * 4));
-    HIPCHK(h, hipMemset(h->in[1], 0, El * 4));
-    HIPCHK(h, hipMemset(h->pend[0], 0, ng));
-    HIPCHK(h, hipMemset(h->pend[1], 0, ng));
+    if (binned) {
+        HIPCHK(h, hipMemset(bn.cnt_c[0], 0, size_t(bn.nc) * kCoarseShards * 4));
+        HIPCHK(h, hipMemset(bn.cnt_c[1], 0, size_t(bn.nc) * kCoarseShards * 4));
+        HIPCHK(h, hipMemset(bn.cnt_f, 0, size_t(bn.nf) * 4));
+        HIPCHK(h, hipMemset(bn.obin, 0, size_t(bn.nf) * 4));
+        HIPCHK(h, hipMemcpy(bn.csub, bn.h_csub.data(), bn.h_csub.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(bn.fslot, bn.h_fslot.data(), (size_t(bn.nf) + 1) * 4, hipMemcpyHostToDevice));
+    } else {
+        HIPCHK(h, hipMemset(h->in[0], 0, El * 4));
+        HIPCHK(h, hipMemset(h->in[1], 0, El * 4));
+        HIPCHK(h, hipMemset(h->pend[0], 0, ng));
+        HIPCHK(h, hipMemset(h->pend[1], 0, ng));
+    }
     HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
     HIPCHK(h, hipMemset(h->ost_total, 0, 64));
     if (W > 1) {
@@ -1000,7 +1095,24 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     psim_handle* hh = const_cast<psim_handle*>(h);
     HIPCHK(hh, hipSetDevice(h->device));
     HIPCHK(hh, hipStreamSynchronize(h->stream));
-    HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
+    if (!h->bin.rec_c) {
+        HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
+        return PSIM_OK;
+    }
+    // binned: the records waiting in the coarse bins the next round routes
+    const auto& b = h->bin;
+    const size_t NS = size_t(b.nc) * kCoarseShards;
+    std::vector<uint32_t> cnt(NS);
+    std::vector<uint2> rec(h->E);
+    HIPCHK(hh, hipMemcpy(cnt.data(), b.cnt_c[h->par], NS * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hh, hipMemcpy(rec.data(), b.rec_c, h->E * 8, hipMemcpyDeviceToHost));
+    memset(words, 0, h->E * 4);
+    for (size_t c = 0; c < NS; c++)
+        for (uint32_t i = 0; i < cnt[c]; i++) {
+            const uint2 r = rec[size_t(b.h_csub[c]) + i];
+            if (r.x >= h->E) return fail(hh, PSIM_ESTATE, "corrupt in-flight record");
+            words[r.x] = r.y;
+        }
     return PSIM_OK;
 }
 

@@ -15,6 +15,14 @@ constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread
 constexpr int kNStat = 16;           // counters per shard
 constexpr int kGroupShift = 4;       // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
 constexpr uint32_t kChunkV = 1024;   // vertices owned by one round-kernel workgroup
+// binned engine (single GPU): messages travel as {receiver
+// slot, word} records through coarse then fine receiver bins
+constexpr uint32_t kBinSlots = 4096;   // LDS inbox words of one fine bin (16 KB)
+constexpr uint32_t kBinVMax = 512;     // vertices of a fine bin (2 per thread)
+constexpr uint32_t kCoarseMax = 512;   // coarse bins; also fine bins per coarse bin
+constexpr uint32_t kRouteK = 4096;     // records one route workgroup moves (16 per thread)
+constexpr uint32_t kCoarseShards = 32; // sub-regions per coarse bin (fine bin f appends to f % 32):
+                                       // spreads the reservation atomics over 32 counters
 
 // counter indices (1..5 = PSIM_MSG_* kinds)
 enum Stat : int {
@@ -54,6 +62,17 @@ struct PtArgs {
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
     uint32_t epoch8;                       // current tree epoch (low 8 bits)
     uint32_t root;                         // local index of the current heartbeat's origin
+    // binned engine (null for the slot-scatter engine)
+    uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}
+    uint2* __restrict__ rec_f;             // [E] fine-bin regions
+    uint32_t* __restrict__ cnt_c_cur;      // [nc][kCoarseShards] records per sub-region, routed this round
+    uint32_t* __restrict__ cnt_c_nxt;      // ... emitted this round
+    uint32_t* __restrict__ cnt_f;          // [nf] records per fine region
+    const uint32_t* __restrict__ csub;     // [nc*kCoarseShards+1] sub-region starts (record index)
+    const uint32_t* __restrict__ fslot;    // [nf+1] first slot of each fine bin
+    uint32_t* __restrict__ obin;           // [nf] vertices of the fine bin holding outstanding rows
+    uint32_t fv_shift, cv_shift;           // fine bin = 2^fv_shift vertices, coarse = 2^cv_shift
+    uint32_t nf, nc, chunks;               // bins; route chunks per sub-region
 };
 
 // Demers rumor mongering + anti-entropy (demers.hip)
@@ -314,7 +333,7 @@ int handle_fail(psim_handle* h, int code, const char* fmt, ...);
 void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing totals
 hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
 
-hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);   // binned when a.rec_c is set
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
                      uint8_t* outb, size_t n, hipStream_t s);

@@ -18,10 +18,18 @@ pytestmark = pytest.mark.gpu
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-@pytest.fixture(scope="module")
-def psim():
+@pytest.fixture(scope="module", params=["slot_scatter", "binned"])
+def psim(request):
+    """partisan_amd with Simulator bound to one Plumtree engine: the
+    slot-scatter engine (the default, also what sharded handles run) and the
+    binned one (PSIM_CFG_BINNED) must both match the oracle."""
+    import functools
+    import types
+
     import partisan_amd
-    return partisan_amd
+    ns = types.SimpleNamespace(**{k: getattr(partisan_amd, k) for k in dir(partisan_amd) if not k.startswith("__")})
+    ns.Simulator = functools.partial(partisan_amd.Simulator, binned=request.param == "binned")
+    return ns
 
 
 def make(psim, rp, col, L=1):

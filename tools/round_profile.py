@@ -10,10 +10,11 @@ p = argparse.ArgumentParser()
 p.add_argument("--n", type=int, default=10_000_000)
 p.add_argument("--peers", type=int, default=5)
 p.add_argument("--steps", type=int, default=3)
+p.add_argument("--binned", action="store_true")
 a = p.parse_args()
 
 rp, col = pa.overlay.random_regular(a.n, a.peers, 0x5EED0001)
-sim = pa.Simulator()
+sim = pa.Simulator(binned=a.binned)
 sim.load_overlay(rp, col)
 for step in range(a.steps):
     sim.reset_trees()
