@@ -252,6 +252,21 @@ static ERL_NIF_TERM nif_delivered(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     return enif_make_tuple2(env, mk_atom(env, "ok"), t);
 }
 
+/* trace_hash(Sim) -> {ok, {StateDigest, InflightDigest, Delivered, Rounds}} (psim_trace_hash) */
+static ERL_NIF_TERM nif_trace_hash(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    uint64_t h[4];
+    enif_mutex_lock(r->mu);
+    int rc = psim_trace_hash(r->h, h);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    ERL_NIF_TERM t[4];
+    for (int i = 0; i < 4; i++) t[i] = enif_make_uint64(env, h[i]);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_tuple_from_array(env, t, 4));
+}
+
 /* ---- HyParView --------------------------------------------------------- */
 
 /* hv_setup(Sim, N, #{active_max_size, ..., promotion_rounds}) -> ok */
@@ -431,6 +446,7 @@ static ErlNifFunc funcs[] = {
     {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"trace_hash", 1, nif_trace_hash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_step", 2, nif_hv_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -137,6 +137,20 @@ int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
  * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
  * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
 int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* Order-independent digest of the Plumtree state, to compare runs (the two
+ * engines, shard counts, replays) at full size without copying state out.
+ * With mix = the splitmix64 finaliser (z += 0x9E3779B97F4A7C15;
+ * z = (z ^ z>>30) * 0xBF58476D1CE4E5B9; z = (z ^ z>>27) * 0x94D049BB133111EB;
+ * z ^ z>>31) and sums mod 2^64:
+ *   out[0] = sum over this handle's vertices (global id g) of
+ *            mix(mix(mix(O) ^ (E<<32 | L)) ^ (g<<32 | R)), with E, L, O, R
+ *            the psim_get_plumtree eager / lazy / outstanding masks and recv_round;
+ *   out[1] = sum over in-flight words w != 0 (psim_get_inflight) at global
+ *            receiver slot e of mix(e<<32 | w);
+ *   out[2] = delivered vertices;  out[3] = rounds completed.
+ * Shards' out[0..2] add up to the whole overlay's (SURVEY 8(b) psim_trace_hash). */
+int  psim_trace_hash(const psim_handle* h, uint64_t* out);
+
 /* --- vertex sharding over several GPUs (one process per GPU) -------- */
 /* The overlay is split into `world` contiguous vertex ranges; this handle
  * owns range `rank`.  Call before psim_load_csr, which then

@@ -648,6 +648,64 @@ __global__ __launch_bounds__(kBlock) void pt_count_live_kernel(PtArgs a, unsigne
     if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, cnt);
 }
 
+// psim_trace_hash: order-independent digests (sums of splitmix64 mixes).
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Per vertex: the psim_get_plumtree view (eager / lazy resolved through the
+// tree epoch, outstanding mask, recv_round) -> out[0]; delivered -> out[2].
+__global__ __launch_bounds__(kBlock) void pt_hash_state_kernel(PtArgs a, uint32_t has_serial, uint32_t root_local,
+                                                               unsigned long long* out) {
+    unsigned long long sum = 0, cnt = 0;
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.n; v += stride) {
+        const uint4 st = a.vs[v];
+        const bool cur = (st.w >> 24) == a.epoch8;
+        const uint32_t e = cur ? st.x : a.memb[v], l = cur ? st.y : 0u;
+        const bool got = has_serial && ((st.w >> 16) & 0xFFu) == a.mono8;
+        const uint32_t rr = !got ? 0xFFFFu : (v == root_local ? 0xFFFEu : ((st.w & 0xFFFFu) - 1u) & 0xFFFFu);
+        const unsigned long long g = a.v_lo + v;
+        sum += mix64(mix64(mix64(st.z) ^ ((unsigned long long)e << 32 | l)) ^ (g << 32 | rr));
+        cnt += got;
+    }
+    sum = wave_sum(sum);
+    cnt = wave_sum(cnt);
+    if ((threadIdx.x & 63) == 0) {
+        if (sum) atomicAdd(&out[0], sum);
+        if (cnt) atomicAdd(&out[2], cnt);
+    }
+}
+
+// In-flight words of the slot-scatter engine (one per receiver slot) -> out[1].
+__global__ __launch_bounds__(kBlock) void pt_hash_words_kernel(PtArgs a, unsigned long long E, unsigned long long* out) {
+    unsigned long long sum = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+    for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < E; i += stride) {
+        const uint32_t w = a.in_cur[i];
+        if (w) sum += mix64(((a.slot_base + i) << 32) | w);
+    }
+    sum = wave_sum(sum);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&out[1], sum);
+}
+
+// ... and of the binned engine (records waiting in the coarse sub-regions).
+__global__ __launch_bounds__(kBlock) void pb_hash_records_kernel(PtArgs a, unsigned long long* out) {
+    unsigned long long sum = 0;
+    for (uint32_t cs = blockIdx.x; cs < a.nc * kCoarseShards; cs += gridDim.x) {
+        const uint32_t k = a.cnt_c_cur[cs], b = a.csub[cs];
+        for (uint32_t i = threadIdx.x; i < k; i += kBlock) {
+            const uint2 r = a.rec_c[b + i];
+            sum += mix64(((unsigned long long)r.x << 32) | r.y);
+        }
+    }
+    sum = wave_sum(sum);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&out[1], sum);
+}
+
 // Re-base the 8-bit Monotonic / epoch tags so they cannot alias after wrap.
 __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
     const uint32_t stride = gridDim.x * kBlock;
@@ -803,6 +861,16 @@ hipError_t launch_pt_ingest_dense(const PtArgs& a, const uint32_t* recv, const u
     if (nrecv == 0) return hipSuccess;
     hipLaunchKernelGGL(pt_ingest_dense_kernel, dim3(grid_for(nrecv)), dim3(kBlock), 0, s, a, recv, recv_map, nrecv,
                        slot2v);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_local, unsigned long long E,
+                          unsigned long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(pt_hash_state_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a, has_serial, root_local, out);
+    if (a.rec_c)
+        hipLaunchKernelGGL(pb_hash_records_kernel, dim3(1024), dim3(kBlock), 0, s, a, out);
+    else if (E)
+        hipLaunchKernelGGL(pt_hash_words_kernel, dim3(2048), dim3(kBlock), 0, s, a, E, out);
     return hipGetLastError();
 }
 

@@ -1335,6 +1335,25 @@ int psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m) {
     return PSIM_OK;
 }
 
+int psim_trace_hash(const psim_handle* h, uint64_t* out) {
+    if (!h || !out || !h->n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    PtArgs a = make_args(h, h->par, 0, h->stats);
+    const uint32_t rl = h->have_root ? h->root - h->sh.v_lo : 0xFFFFFFFFu;
+    HIPCHK(hh, hipMemsetAsync(h->scratch, 0, 32, h->stream));
+    HIPCHK(hh, launch_pt_hash(a, h->serial != 0, rl < h->n ? rl : 0xFFFFFFFFu, h->bin.rec_c ? 0ull : h->E,
+                              h->scratch, h->stream));
+    unsigned long long r[4];
+    HIPCHK(hh, hipMemcpyAsync(r, h->scratch, 32, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    out[0] = r[0];
+    out[1] = r[1];
+    out[2] = r[2];
+    out[3] = h->round;
+    return PSIM_OK;
+}
+
 int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds) {
     if (!h) return PSIM_EINVAL;
     if (round_kernel_ms) *round_kernel_ms = h->kernel_ms_total;

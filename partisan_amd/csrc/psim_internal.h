@@ -340,6 +340,8 @@ hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_
 hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_local, unsigned long long E,
+                          unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
                              const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s);
 hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s);

@@ -121,6 +121,12 @@ class Simulator:
         self._c(lib().psim_get_inflight(self._h, _u32p(w), self.num_slots))
         return w[: self.num_slots]
 
+    def trace_hash(self):
+        """psim_trace_hash: (state digest, in-flight digest, delivered, rounds)."""
+        out = (C.c_uint64 * 4)()
+        self._c(lib().psim_trace_hash(self._h, out))
+        return tuple(int(x) for x in out)
+
     def timing(self):
         ms = C.c_double()
         r = C.c_uint64()
