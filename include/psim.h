@@ -222,8 +222,12 @@ typedef struct psim_demers_stats {
     double   kernel_ms;
 } psim_demers_stats;
 /* Full-membership Demers epidemic over n vertices with m <= 64 rumors whose
- * origins are Philox draws (stream kind 1).  rm_on: rumor mongering with
- * fanout 2 (demers_rumor_mongering.erl :92-186); ae_period: anti-entropy
+ * origins are Philox draws (stream kind 1).  rm_on: 1 = rumor mongering with
+ * fanout 2 (demers_rumor_mongering.erl :92-186); 2 = direct mail, the
+ * baseline: the origin sends to every other member, receivers only store
+ * (demers_direct_mail.erl :91-143; not in psim_demers_shard_setup; the
+ * origins' n-1 sends, like rumor mongering's, are not in the round stats);
+ * 0 = off.  ae_period: anti-entropy
  * push-pull with fanout 2 every ae_period rounds (demers_anti_entropy.erl
  * :118-195; 0 = off, else >= 2).  Both on share one message store.
  * Replaces starting both gen_servers on every node (:50-76). */

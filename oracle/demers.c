@@ -124,12 +124,18 @@ uint64_t orc_dm_full_mask(const orc_demers* s) { return s->full; }
 
 /* handle_cast({broadcast, ServerRef, Message}) at every origin, rumor order.
  * RM (:92-115): deliver, store, forward to select_random_sublist(..) -- [MyNode].
- * AE (:95-106): deliver and store only. */
+ * AE (:95-106): deliver and store only.
+ * Direct mail (rm_on == 2, demers_direct_mail.erl:91-121): deliver, store,
+ * forward to every member but MyNode. */
 void orc_dm_broadcast_all(orc_demers* s) {
     for (uint32_t i = 0; i < s->m; i++) {
         uint32_t o = s->origin[i];
         s->seen[o] |= 1ull << s->idbit[i];
         if (!s->rm_on) continue;
+        if (s->rm_on == 2) {
+            for (uint32_t t = 0; t < s->n; t++) if (t != o) emit(s, DM_RM, o, t, i, 0);
+            continue;
+        }
         uint32_t t[2];
         int k = sample2(s->seed, o, i, KIND_RM, s->n, t);
         for (int j = 0; j < k; j++) if (t[j] != o) emit(s, DM_RM, o, t[j], i, 0);
@@ -158,7 +164,7 @@ static void one_round(orc_demers* s, orc_dm_stats* st) {
     /* class of an RM message: is the sender one of the receiver's own targets */
     for (size_t i = 0; i < s->ncur; i++) {
         dmsg* x = &s->cur[i];
-        if (x->type != DM_RM) continue;
+        if (x->type != DM_RM || s->rm_on == 2) continue;
         uint32_t tg[2];
         int k = sample2(s->seed, x->dst, x->m, KIND_RM, s->n, tg);
         x->cls = 0;
@@ -173,6 +179,7 @@ static void one_round(orc_demers* s, orc_dm_stats* st) {
             if (s->seen[v] & b) continue;            /* ets:lookup -> [_] */
             s->seen[v] |= b;                         /* deliver + ets:insert */
             st->delivered_new++;
+            if (s->rm_on == 2) continue;             /* direct mail :127-143: store only */
             uint32_t tg[2];
             int k = sample2(s->seed, v, x->m, KIND_RM, s->n, tg);
             for (int j = 0; j < k; j++)              /* AntiEntropyMembers -- [MyNode, FromNode] */

@@ -520,7 +520,8 @@ def sample2(seed, v, event, kind, n):
 class Demers:
     def __init__(self, n, m, seed, ae_period=2, rm_on=True):
         self.n, self.m = n, m
-        self._h = lib().orc_dm_create(n, m, seed, ae_period, 1 if rm_on else 0)
+        mode = 2 if rm_on == "direct_mail" else (1 if rm_on else 0)   # direct mail: demers_direct_mail.erl
+        self._h = lib().orc_dm_create(n, m, seed, ae_period, mode)
         if not self._h:
             raise ValueError("bad demers config")
 

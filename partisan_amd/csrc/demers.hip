@@ -78,6 +78,9 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
         const uint32_t v = a.v_lo + i;   // global id; i indexes this shard's arrays
         unsigned long long s = a.seen[i];
         const unsigned long long s0 = s;
+        // ---- direct mail: handle_info({broadcast, Id, ...}) stores only
+        // (demers_direct_mail.erl:127-143); the origins sent to every other member
+        s |= a.dm_mail;
 
         // ---- rumor mongering: handle_info({broadcast, Id, ..., FromNode}) :127-158
         if (a.rm_on) {
@@ -355,7 +358,7 @@ extern "C" {
 
 int psim_demers_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on, int rank,
                             int world, uint64_t* chunk_out) {
-    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1 || world < 1 || rank < 0 || rank >= world)
+    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1 || rm_on > 1 || world < 1 || rank < 0 || rank >= world)
         return PSIM_EINVAL;
     DMCHK(h, hipSetDevice(handle_device(h)));
     DMCHK(h, hipStreamSynchronize(handle_stream(h)));

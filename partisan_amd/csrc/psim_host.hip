@@ -96,8 +96,9 @@ struct psim_handle {
 
     // Demers epidemic state (demers.hip)
     struct Dm {
-        uint32_t n = 0, m = 0, ae_period = 0, rm_on = 0;
+        uint32_t n = 0, m = 0, ae_period = 0, rm_on = 0;   // rm_on: 0 off, 1 rumor mongering, 2 direct mail
         unsigned long long full = 0;
+        unsigned long long dm_pending = 0;                 // direct-mail ids the next round delivers
         unsigned long long *seen = nullptr, *snap = nullptr, *rm[2][3] = {}, *pull[2] = {};
         uint32_t *pushcnt[2] = {}, *pushlist[2] = {}, *origin = nullptr, *idbit = nullptr;
         std::vector<uint32_t> h_origin;
@@ -1188,7 +1189,7 @@ DmArgs make_dm_args(const psim_handle* h, uint32_t par, unsigned long long* stat
     a.n_global = d.n;
     a.sharded = 0;
     a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
-    a.rm_on = d.rm_on;
+    a.rm_on = d.rm_on == 1u;
     a.full = d.full;
     a.seen = d.seen;
     a.snap = d.snap;
@@ -1219,6 +1220,8 @@ int dm_drive(psim_handle* h, uint32_t max_rounds, psim_demers_stats* out, size_t
         a.tick = d.ae_period && (t % d.ae_period) == 0;
         a.tick_idx = d.ae_period ? (uint32_t)(t / d.ae_period) : 0;
         a.prev_tick = d.ae_period ? (uint32_t)(d.round / d.ae_period) : 0;
+        a.dm_mail = d.dm_pending;
+        d.dm_pending = 0;
         HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
         HIPCHK(h, launch_dm_round(a, h->stream));
         HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
@@ -1258,7 +1261,7 @@ int dm_drive(psim_handle* h, uint32_t max_rounds, psim_demers_stats* out, size_t
 extern "C" {
 
 int psim_demers_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on) {
-    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1) return PSIM_EINVAL;
+    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1 || rm_on > 2) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     free_demers(h);
@@ -1279,7 +1282,8 @@ int psim_demers_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period
     d.n = n;
     d.m = m;
     d.ae_period = ae_period;
-    d.rm_on = rm_on ? 1u : 0u;
+    d.rm_on = rm_on;
+    d.dm_pending = 0;
     const uint2 key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
     HIPCHK(h, launch_dm_origins(key, n, m, d.origin, h->stream));
     d.h_origin.assign(m, 0);
@@ -1305,6 +1309,7 @@ int psim_demers_broadcast_all(psim_handle* h) {
     DmArgs a = make_dm_args(h, h->dm.par ^ 1u, h->stats);   // writes the inbox the next round reads
     HIPCHK(h, launch_dm_broadcast(a, h->dm.origin, h->dm.idbit, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->dm.rm_on == 2u) h->dm.dm_pending |= h->dm.full;   // every other member receives every rumor
     return PSIM_OK;
 }
 

@@ -84,6 +84,7 @@ struct DmArgs {
     uint2 key;                            // Philox key {seed_lo, seed_hi}
     uint32_t rm_on;
     uint32_t tick, tick_idx, prev_tick;   // AE tick at the end of this round; tick indices
+    unsigned long long dm_mail;           // direct mail: rumor ids every vertex receives this round
     unsigned long long full;              // every rumor id's bit
     unsigned long long* __restrict__ seen;       // [n] the message store
     unsigned long long* __restrict__ snap;       // [n_global] AE payload taken at the tick (global ids)

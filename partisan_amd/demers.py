@@ -14,8 +14,11 @@ from ._lib import DemersStats, check, lib
 
 class DemersEpidemic:
     def __init__(self, sim, n, m=64, ae_period=2, rumor_mongering=True):
+        """rumor_mongering: True (demers_rumor_mongering), False (anti-entropy
+        alone) or "direct_mail" (demers_direct_mail, the baseline)."""
         self.sim, self.n, self.m = sim, n, m
-        check(lib().psim_demers_setup(sim._h, n, m, ae_period, 1 if rumor_mongering else 0), sim._h)
+        mode = 2 if rumor_mongering == "direct_mail" else (1 if rumor_mongering else 0)
+        check(lib().psim_demers_setup(sim._h, n, m, ae_period, mode), sim._h)
 
     def _c(self, rc):
         return check(rc, self.sim._h)

@@ -32,12 +32,15 @@ def test_sample2_is_uniform_pair():
     assert off.min() > 0.7 * off.mean() and off.max() < 1.3 * off.mean()
 
 
-@pytest.mark.parametrize("rm,ae", [(True, 2), (True, 0), (False, 2), (True, 3)])
+@pytest.mark.parametrize("rm,ae", [(True, 2), (True, 0), (False, 2), (True, 3), ("direct_mail", 0)])
 def test_oracle_modes_converge_or_residue(rm, ae):
     d = O.Demers(3000, 64, 0x5EED0004, ae_period=ae, rm_on=rm)
     d.broadcast_all()
     st, r = d.run(300)
-    if ae:
+    if rm == "direct_mail":                         # one hop to every member
+        assert r == 1 and st[0]["complete"] == 3000 and st[0]["rm_sent"] == 0
+        assert st[0]["delivered_new"] == 64 * 2999      # each rumor reaches the n - 1 others
+    elif ae:
         assert st[-1]["complete"] == 3000          # anti-entropy guarantees delivery
     else:
         assert r == 300 and st[-1]["complete"] < 3000   # rumor mongering leaves a residue
@@ -66,7 +69,8 @@ def lockstep(pa, n, m, seed, ae, rm, max_rounds=200):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,ae,rm,seed", [
     (500, 64, 2, True, 1), (3000, 64, 2, True, 2), (2000, 17, 3, True, 3),
-    (1500, 64, 2, False, 4), (800, 64, 0, True, 5), (20000, 64, 2, True, 0x5EED0004)])
+    (1500, 64, 2, False, 4), (800, 64, 0, True, 5), (20000, 64, 2, True, 0x5EED0004),
+    (3000, 64, 0, "direct_mail", 6), (2500, 64, 2, "direct_mail", 7)])
 def test_lockstep(n, m, ae, rm, seed):
     import partisan_amd as pa
     lockstep(pa, n, m, seed, ae, rm, max_rounds=60 if ae == 0 else 200)
