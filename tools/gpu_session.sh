@@ -24,7 +24,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
     case $s in
         build) run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
-        test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        test)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
         t:*)   f=${s#t:}; run "pytest_${f}" 900 python -m pytest "tests/test_${f}.py" -m gpu -x -q ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
