@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--cpu-sample-n", type=int, default=1_000_000)
     p.add_argument("--cpu-sample-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-workers", type=int, default=16,
+                   help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
     p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
@@ -123,6 +125,31 @@ def cpu_baseline(args):
         "sample": (f"C oracle (oracle/plumtree.c), {args.cpu_sample_reps} floods of a "
                    f"{args.cpu_sample_n}-peer random {args.peers}-peer overlay to quiescence "
                    f"({rounds} rounds each), single thread, {tot_t:.1f} s"),
+    }
+
+
+def cpu_baseline_allcores(args):
+    """W single-thread oracle floods at once, one spawned process each (no
+    fork of this GPU-initialised process); value = the sum of the workers'
+    own rates (peer-rounds / time inside their floods, which overlap)."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_flood
+    w = args.cpu_workers
+    jobs = [(args.cpu_sample_n, args.peers, args.seed + i, args.cpu_sample_reps, args.lazy_tick_rounds)
+            for i in range(w)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(w) as pool:
+        pool.map(cpu_flood.flood, [(1000, args.peers, 1, 1, 1)] * w)   # interpreters up, oracle loaded
+        t0 = time.perf_counter()
+        res = pool.map(cpu_flood.flood, jobs)
+        wall = time.perf_counter() - t0
+    rate = sum(r[0] / r[1] for r in res)
+    return {
+        "value": rate, "unit": "peer-rounds/s", "cores": w, "kind": "port",
+        "sample": (f"{w} processes at once, each the single-thread C oracle running {args.cpu_sample_reps} "
+                   f"floods of its own {args.cpu_sample_n}-peer random {args.peers}-peer overlay "
+                   f"({res[0][2]} rounds); sum of per-process rates, {wall:.1f} s wall incl. overlay builds"),
     }
 
 
@@ -235,6 +262,8 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)
+            if args.cpu_workers > 1:
+                out["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
         print(json.dumps(out), flush=True)
     sim.close()
     if pg is not None:
