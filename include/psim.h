@@ -137,6 +137,14 @@ int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
  * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
  * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
 int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* Omission faults (test/prop_partisan_crash_fault_model.erl:117-196, send /
+ * receive omission interposition funs): every Plumtree message over a
+ * directed pair (src[i], dst[i]) is sent -- counted, the sender moves on --
+ * and lost.  Replaces the whole set; k = 0 heals all ("resolve all faults").
+ * Pairs that are not overlay edges are ignored; a partition is the set of
+ * its cross edges (partisan_amd.Simulator.inject_partition). */
+int  psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst, size_t k);
+
 /* Order-independent digest of the Plumtree state, to compare runs (the two
  * engines, shard counts, replays) at full size without copying state out.
  * With mix = the splitmix64 finaliser (z += 0x9E3779B97F4A7C15;

@@ -318,6 +318,10 @@ void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx);
 void orc_pt_restart(orc_plumtree* s, uint32_t v);
 void orc_pt_queue_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n);
 uint64_t orc_pt_dropped(const orc_plumtree* s);
+/* omission faults: the directed pairs (src[i], dst[i]) lose every message
+ * (prop_partisan_crash_fault_model.erl:117-196); k = 0 heals */
+void orc_pt_set_omissions(orc_plumtree* s, const uint32_t* src, const uint32_t* dst, size_t k);
+uint64_t orc_pt_omitted(const orc_plumtree* s);
 
 typedef struct orc_c3 orc_c3;
 typedef struct orc_c3_stats {

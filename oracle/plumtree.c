@@ -119,16 +119,50 @@ struct orc_plumtree {
     orc_pt_conn_fn conn;                   /* partisan:cast_message needs a connection (C3) */
     void* conn_ctx;
     uint64_t dropped;                      /* sends to a non-connected peer */
+    uint64_t* omit; size_t nomit;          /* omission faults: sorted (src << 32 | dst) keys */
+    uint64_t omitted;                      /* messages they dropped */
 };
 
 void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx) { s->conn = fn; s->conn_ctx = ctx; }
 uint64_t orc_pt_dropped(const orc_plumtree* s) { return s->dropped; }
+
+static int cmp_u64(const void* x, const void* y) {
+    const uint64_t a = *(const uint64_t*)x, b = *(const uint64_t*)y;
+    return a < b ? -1 : a > b;
+}
+/* Send / receive omission faults (test/prop_partisan_crash_fault_model.erl
+ * :117-196): an interposition fun in the manager's forward_message (sender
+ * side) or receive_message (receiver side) path returns undefined for the
+ * directed pair, so the message is sent -- counted, the sender's state moves
+ * on -- and lost.  Replaces the whole set; k = 0 heals every fault. */
+void orc_pt_set_omissions(orc_plumtree* s, const uint32_t* src, const uint32_t* dst, size_t k) {
+    free(s->omit);
+    s->omit = NULL;
+    s->nomit = 0;
+    if (!k) return;
+    s->omit = (uint64_t*)malloc(k * sizeof(uint64_t));
+    for (size_t i = 0; i < k; i++) s->omit[i] = ((uint64_t)src[i] << 32) | dst[i];
+    qsort(s->omit, k, sizeof(uint64_t), cmp_u64);
+    s->nomit = k;
+}
+uint64_t orc_pt_omitted(const orc_plumtree* s) { return s->omitted; }
+static int omitted(const orc_plumtree* s, uint32_t src, uint32_t dst) {
+    if (!s->nomit) return 0;
+    const uint64_t key = ((uint64_t)src << 32) | dst;
+    return bsearch(&key, s->omit, s->nomit, sizeof(uint64_t), cmp_u64) != NULL;
+}
 
 /* ---------------- message emission: partisan:cast_message via send/3 ---- */
 static void emit(orc_plumtree* s, uint32_t src, uint32_t dst, uint32_t type,
                  uint32_t round, uint32_t root, uint32_t idn, uint32_t ide, uint32_t idm) {
     if (s->conn && !s->conn(s->conn_ctx, src, dst)) {    /* do_send_message: no connection, dropped */
         s->dropped++;
+        return;
+    }
+    if (omitted(s, src, dst)) {                         /* interposition: sent, then lost */
+        s->nodes[src].seq++;
+        if (s->st) s->st->sent[type]++;
+        s->omitted++;
         return;
     }
     if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? s->capnxt * 2 : 1024; s->nxt = (orc_msg*)realloc(s->nxt, s->capnxt * sizeof(orc_msg)); }
@@ -337,6 +371,7 @@ orc_plumtree* orc_pt_create(uint32_t n, const uint64_t* row_ptr, const uint32_t*
 
 void orc_pt_destroy(orc_plumtree* s) {
     if (!s) return;
+    free(s->omit);
     for (uint32_t v = 0; v < s->n; v++) {
         node_t* nd = &s->nodes[v];
         os_free(&nd->all_members); os_free(&nd->common_eagers); os_free(&nd->common_lazys);

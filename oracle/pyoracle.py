@@ -150,6 +150,9 @@ def lib():
         L.orc_pt_get_outstanding.restype = sz
         L.orc_pt_get_delivered.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint8)]
         L.orc_pt_get_recv_round.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.orc_pt_set_omissions.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), sz]
+        L.orc_pt_omitted.argtypes = [C.c_void_p]
+        L.orc_pt_omitted.restype = C.c_uint64
         L.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         L.orc_dm_sample2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
         L.orc_dm_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
@@ -452,6 +455,15 @@ class Plumtree:
 
     def reset_peers_all(self):
         lib().orc_pt_reset_peers_all(self._h)
+
+    def set_omissions(self, pairs):
+        """Omission faults on directed (src, dst) pairs; [] heals."""
+        p = np.asarray(pairs, dtype=np.uint32).reshape(-1, 2)
+        s, d = np.ascontiguousarray(p[:, 0]), np.ascontiguousarray(p[:, 1])
+        lib().orc_pt_set_omissions(self._h, _u32p(s), _u32p(d), len(p))
+
+    def omitted(self):
+        return int(lib().orc_pt_omitted(self._h))
 
     def step(self, rounds=1):
         st = (RoundStats * rounds)()

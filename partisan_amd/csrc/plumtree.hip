@@ -112,7 +112,14 @@ __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_
 // Hand the word for sender slot e to its receiver: a local receiver slot
 // (rev[e] is a global slot id) plus its group flag, or -- receiver on another
 // shard -- the staging word of the sender slot, packed by pt_compact_kernel.
+// Omission faults (prop_partisan_crash_fault_model.erl:117-196): the word
+// over sender slot e is sent (counted) and lost.
+__device__ __forceinline__ bool omitted(const PtArgs& a, uint32_t e) {
+    return a.omit && ((a.omit[e >> 5] >> (e & 31)) & 1u);
+}
+
 __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w) {
+    if (omitted(a, e)) return;
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
         a.in_nxt[a.rev[e] - a.slot_base] = w;
@@ -548,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
             if (!send[k]) continue;
             const uint32_t ls = rpc[lvk[k]], deg = rpc[lvk[k] + 1] - ls, rs = sb + ls;
             for (uint32_t s = 0; s < deg; s++)
-                if (pt_out<false>(s, words[ls + s], x[k], ihave[k], c))
+                if (pt_out<false>(s, words[ls + s], x[k], ihave[k], c) && !omitted(a, rs + s))
                     atomicAdd(&hist[a.col[rs + s] >> a.cv_shift], 1u);
         }
         __syncthreads();
@@ -569,11 +576,12 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
             for (uint32_t s = 0; s < deg; s++) {
                 const uint32_t w = pt_out<true>(s, words[ls + s], x[k], ihave[k], c);
                 if (!w) continue;
+                sent = true;
+                if (omitted(a, rs + s)) continue;
                 const uint32_t cb = a.col[rs + s] >> a.cv_shift;
                 const uint32_t pos = base[cb] + atomicAdd(&hist[cb], 1u);
                 if (pos < a.csub[cb * kCoarseShards + sh + 1]) a.rec_c[pos] = make_uint2(a.rev[rs + s], w);
                 else c.overflow |= 8u;
-                sent = true;
             }
             if (sent) {
                 c.senders++;
@@ -605,7 +613,9 @@ __global__ void pt_origin_kernel(PtArgs a) {
         const uint32_t b = 1u << s;
         const uint32_t e = rs + s;
         if (eager & b) {
-            if (a.rec_c) {                           // binned: a record for the next route
+            if (omitted(a, e)) {
+                // sent and lost
+            } else if (a.rec_c) {                    // binned: a record for the next route
                 const uint32_t cs = (a.col[e] >> a.cv_shift) * kCoarseShards + ((v >> a.fv_shift) & (kCoarseShards - 1));
                 a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] = make_uint2(a.rev[e], PSIM_MSG_BROADCAST);
             } else {

@@ -42,6 +42,7 @@ struct psim_handle {
     uint32_t* in[2] = {nullptr, nullptr};
     uint8_t* pend[2] = {nullptr, nullptr};
     uint8_t* ost = nullptr;
+    uint32_t* omit = nullptr;       // omission faults: bitmap over local sender slots (psim_set_omissions)
     // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
     struct Bin {
         uint2 *rec_c = nullptr, *rec_f = nullptr;
@@ -202,6 +203,8 @@ void free_graph(psim_handle* h) {
     h->vs = nullptr;
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
+    if (h->omit) (void)hipFree(h->omit);
+    h->omit = nullptr;
     {
         auto& b = h->bin;
         void* bp[] = {b.rec_c, b.rec_f, b.cnt_c[0], b.cnt_c[1], b.cnt_f, b.csub, b.fslot, b.obin};
@@ -246,6 +249,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.mono8 = h->serial & 0xFFu;
     a.epoch8 = h->epoch & 0xFFu;
     a.root = h->root;
+    a.omit = h->omit;
     if (h->bin.rec_c) {
         const auto& b = h->bin;
         a.rec_c = b.rec_c;
@@ -1337,6 +1341,32 @@ int psim_demers_get_seen(const psim_handle* h, uint64_t* seen, size_t n) {
 int psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m) {
     if (!h || !origins || m != h->dm.m || !m) return PSIM_EINVAL;
     memcpy(origins, h->dm.h_origin.data(), m * 4);
+    return PSIM_OK;
+}
+
+int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst, size_t k) {
+    if (!h || !h->n || (k && (!src || !dst))) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::vector<uint32_t> bm((h->E + 31) / 32, 0u);
+    size_t hit = 0;
+    for (size_t i = 0; i < k; i++) {
+        if (src[i] >= h->sh.n_global || dst[i] >= h->sh.n_global)
+            return fail(h, PSIM_EINVAL, "omission pair (%u, %u) out of range", src[i], dst[i]);
+        const uint32_t u = src[i] - h->sh.v_lo;
+        if (u >= h->n) continue;                       // another shard's sender
+        const auto b = h->h_col.begin() + h->h_rowp[u], e = h->h_col.begin() + h->h_rowp[u + 1];
+        const auto it = std::lower_bound(b, e, dst[i]);
+        if (it == e || *it != dst[i]) continue;        // not an overlay edge: nothing ever flows
+        const size_t s = size_t(it - h->h_col.begin());
+        bm[s >> 5] |= 1u << (s & 31);
+        hit++;
+    }
+    if (h->omit) (void)hipFree(h->omit);
+    h->omit = nullptr;
+    if (!hit) return PSIM_OK;                          // healed (or no local edge affected)
+    if (hipMalloc((void**)&h->omit, bm.size() * 4) != hipSuccess) return fail(h, PSIM_ENOMEM, "omission bitmap");
+    HIPCHK(h, hipMemcpy(h->omit, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
     return PSIM_OK;
 }
 

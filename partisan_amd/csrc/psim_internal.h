@@ -62,6 +62,7 @@ struct PtArgs {
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
     uint32_t epoch8;                       // current tree epoch (low 8 bits)
     uint32_t root;                         // local index of the current heartbeat's origin
+    const uint32_t* __restrict__ omit;     // [ceil(E/32)] omission faults over sender slots, or null
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}
     uint2* __restrict__ rec_f;             // [E] fine-bin regions

@@ -121,6 +121,30 @@ class Simulator:
         self._c(lib().psim_get_inflight(self._h, _u32p(w), self.num_slots))
         return w[: self.num_slots]
 
+    def set_omissions(self, pairs):
+        """Omission faults on directed (src, dst) pairs (psim_set_omissions); [] heals."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        s, d = np.ascontiguousarray(p[:, 0]), np.ascontiguousarray(p[:, 1])
+        self._c(lib().psim_set_omissions(self._h, s.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         d.ctypes.data_as(C.POINTER(C.c_uint32)), len(p)))
+
+    def partition_pairs(self, group):
+        """Directed overlay edges (of this handle's vertices) whose ends lie in
+        different groups: group[v] = partition of global vertex v."""
+        group = np.asarray(group)
+        rp = np.asarray(self.slot_row_ptr, dtype=np.int64)
+        col = np.asarray(self.slot_col, dtype=np.int64)
+        src = np.repeat(np.arange(len(rp) - 1, dtype=np.int64) + self.v_lo, np.diff(rp))
+        cut = group[src] != group[col]
+        return np.stack([src[cut], col[cut]], axis=1)
+
+    def inject_partition(self, group):
+        """partisan's inject_partition: messages across groups are lost."""
+        self.set_omissions(self.partition_pairs(group))
+
+    def resolve_partition(self):
+        self.set_omissions(np.zeros((0, 2), np.uint32))
+
     def trace_hash(self):
         """psim_trace_hash: (state digest, in-flight digest, delivered, rounds)."""
         out = (C.c_uint64 * 4)()

@@ -297,3 +297,62 @@ def test_trace_hash_engines_agree_at_scale():
                 break
     a.close()
     b.close()
+
+
+def _omit_step(sim, orc, root, mono, rounds):
+    for r in range(rounds):
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (r, k, gs, os_)
+        assert gs["delivered_new"] == os_["delivered_new"], r
+        compare(sim, orc, root, mono)
+
+
+def test_omission_faults_lockstep(psim):
+    """Send/receive omission faults (prop_partisan_crash_fault_model.erl
+    :117-196) on 10 % of the directed edges during a flood, then healed: the
+    omitted messages are counted as sent and lost, round by round as in the
+    oracle; after the heal the lazy ticks' i_have/graft repair the tree."""
+    rp, col = psim.overlay.random_regular(1500, 5, 101)
+    sim, orc = make(psim, rp, col, 1)
+    rng = np.random.default_rng(5)
+    src = np.repeat(np.arange(sim.n), np.diff(sim.slot_row_ptr.astype(np.int64)))
+    pick = rng.random(len(src)) < 0.10
+    pairs = np.stack([src[pick], sim.slot_col[pick]], axis=1)
+    sim.set_omissions(pairs)
+    orc.set_omissions(pairs)
+    sim.broadcast(3)
+    mono = orc.heartbeat(3)
+    _omit_step(sim, orc, 3, mono, 14)
+    assert orc.omitted() > 0
+    sim.set_omissions([])
+    orc.set_omissions([])
+    lockstep(sim, orc, 3, mono)
+    assert sim.delivered().all()
+
+
+def test_partition_then_heal(psim):
+    """inject_partition: a flood from vertex 0 stays on its side while the
+    partition holds (same delivered sets as the oracle).  Eager pushes lost on
+    the cut leave no outstanding row (only lazy peers get rows), so after the
+    heal only i_have over lazy links crosses -- as in the oracle; the next
+    heartbeat then reaches every vertex (the reliable-broadcast postcondition,
+    prop_partisan_reliable_broadcast.erl:127-172, holds from there)."""
+    rp, col = psim.overlay.random_regular(2000, 5, 111)
+    sim, orc = make(psim, rp, col, 1)
+    group = (np.arange(2000) >= 1000).astype(np.int64)
+    pairs = sim.partition_pairs(group)
+    sim.inject_partition(group)
+    orc.set_omissions(pairs)
+    sim.broadcast(0)
+    mono = orc.heartbeat(0)
+    _omit_step(sim, orc, 0, mono, 20)
+    d = sim.delivered()
+    assert not d[1000:].any() and d[:1000].sum() > 900   # side 0 minus vertices cut off inside it
+    sim.resolve_partition()
+    orc.set_omissions([])
+    lockstep(sim, orc, 0, mono)
+    sim.broadcast(0)
+    mono = orc.heartbeat(0)
+    lockstep(sim, orc, 0, mono)
+    assert sim.delivered().all()
