@@ -119,6 +119,17 @@ int  psim_plumtree_reset_trees(psim_handle* h);
  * the id {Root, Epoch, Monotonic}.  PSIM_EBUSY if the previous broadcast is
  * not quiescent. */
 int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
+/* Several roots: on one GPU without PSIM_CFG_BINNED each
+ * heartbeat root gets a lane of its own (per-root eager / lazy sets, rows,
+ * delivered serials, in-flight words; up to 16 lanes, then the least
+ * recently used quiescent lane is reused and its root's sets forgotten), so
+ * heartbeats of different roots run concurrently and PSIM_EBUSY is per
+ * root; rounds advance every lane and their stats are summed.  Sharded and
+ * binned handles keep one lane: a heartbeat from a new root drops the old
+ * root's sets.  The per-vertex getters (psim_get_plumtree, _delivered,
+ * _inflight, psim_trace_hash) read the focused root: the last broadcast one,
+ * or the one chosen here (PSIM_EINVAL if it has no lane). */
+int  psim_plumtree_focus(psim_handle* h, uint32_t root);
 /* Runs exactly `rounds` rounds.  stats may be NULL; otherwise stats[cap]. */
 int  psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap);
 /* Runs until quiescent (nothing in flight and no outstanding i_have row to

@@ -18,6 +18,7 @@ using namespace psim;
 
 namespace {
 constexpr int kChunk = 4;   // rounds launched between host synchronisations
+constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-scatter engine)
 constexpr size_t kStatsRow = size_t(kStatShards) * kNStat;
 }  // namespace
 
@@ -53,7 +54,8 @@ struct psim_handle {
     unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
     unsigned long long* h_stats = nullptr;   // pinned mirror
     unsigned long long* scratch = nullptr;   // 1 counter
-    int* ost_total = nullptr;                // device mirror of ost_cnt
+    int* ost_total = nullptr;                // device mirror of ost_cnt (the focused lane's)
+    int* ost_total_base = nullptr;           // [kMaxLanes] allocation
     hipEvent_t ev[2 * kChunk] = {};
 
     uint32_t par = 0;          // inbox buffer the next round reads
@@ -68,6 +70,26 @@ struct psim_handle {
     uint64_t inflight = 0;     // messages emitted by the last round / origin
     double kernel_ms_total = 0;
     uint64_t rounds_total = 0;
+
+    // Multi-root heartbeat trees: on one
+    // GPU with the slot-scatter engine each heartbeat root gets a lane --
+    // its own vertex states, inbox and counters; the fields above (vs, in,
+    // pend, ost, ost_total, par, serial, root, have_root, ost_cnt, live_rows,
+    // inflight) are the focused lane's, the others wait in `lanes`.
+    struct Lane {
+        uint4* vs = nullptr;
+        uint32_t* in[2] = {nullptr, nullptr};
+        uint8_t* pend[2] = {nullptr, nullptr};
+        uint8_t* ost = nullptr;
+        int* ost_total = nullptr;
+        uint32_t par = 0, serial = 0, root = 0;
+        bool have_root = false;
+        int64_t ost_cnt = 0, live_rows = 0;
+        uint64_t inflight = 0, last_use = 0;
+    };
+    std::vector<Lane> lanes;
+    int cur_lane = 0;
+    uint64_t use_clock = 0;
     void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
     size_t scratch_cap = 0;
 
@@ -194,7 +216,20 @@ void free_cs(psim_handle* h) {
     h->cs = psim_handle::Cs();
 }
 
+void swap_lane(psim_handle* h, int j);
+
 void free_graph(psim_handle* h) {
+    if (!h->lanes.empty()) {
+        swap_lane(h, 0);
+        for (size_t j = 1; j < h->lanes.size(); j++) {
+            auto& l = h->lanes[j];
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
+            for (void* p : lp)
+                if (p) (void)hipFree(p);
+        }
+        h->lanes.clear();
+        h->cur_lane = 0;
+    }
     void* ptrs[] = {h->rowp, h->col, h->rev, h->memb, h->alive, h->vs, h->in[0], h->in[1],
                     h->pend[0], h->pend[1], h->ost};
     for (void* p : ptrs)
@@ -269,6 +304,28 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     return a;
 }
 
+// ---- heartbeat-root lanes ------------------------------------------------
+void save_lane(psim_handle* h) {
+    auto& l = h->lanes[h->cur_lane];
+    l.vs = h->vs; l.in[0] = h->in[0]; l.in[1] = h->in[1]; l.pend[0] = h->pend[0]; l.pend[1] = h->pend[1];
+    l.ost = h->ost; l.ost_total = h->ost_total; l.par = h->par; l.serial = h->serial; l.root = h->root;
+    l.have_root = h->have_root; l.ost_cnt = h->ost_cnt; l.live_rows = h->live_rows; l.inflight = h->inflight;
+}
+void load_lane(psim_handle* h, int j) {
+    const auto& l = h->lanes[j];
+    h->vs = l.vs; h->in[0] = l.in[0]; h->in[1] = l.in[1]; h->pend[0] = l.pend[0]; h->pend[1] = l.pend[1];
+    h->ost = l.ost; h->ost_total = l.ost_total; h->par = l.par; h->serial = l.serial; h->root = l.root;
+    h->have_root = l.have_root; h->ost_cnt = l.ost_cnt; h->live_rows = l.live_rows; h->inflight = l.inflight;
+    h->cur_lane = j;
+}
+void swap_lane(psim_handle* h, int j) {
+    if (h->lanes.empty() || j == h->cur_lane) return;
+    save_lane(h);
+    load_lane(h, j);
+}
+bool lanes_enabled(const psim_handle* h) { return h->sh.world == 1 && !h->bin.rec_c; }
+bool lane_quiescent(const psim_handle::Lane& l) { return l.inflight == 0 && l.live_rows == 0; }
+
 // Binned engine geometry: fine bins of 2^fv vertices whose slots fit the LDS
 // inbox, coarse bins of 2^cv vertices with about sqrt(#fine) fine bins each.
 bool bin_geometry(const std::vector<uint32_t>& rp, uint32_t n, uint32_t& fv, uint32_t& cv, uint32_t& nf,
@@ -307,8 +364,74 @@ void reduce_row(const unsigned long long* row, unsigned long long* out) {
 bool quiescent(const psim_handle* h) { return h->inflight == 0 && h->live_rows == 0; }
 
 int renorm_if_needed(psim_handle* h) {
-    PtArgs a = make_args(h, h->par, 0, h->stats);
-    HIPCHK(h, launch_pt_renorm(a, h->stream));
+    const int focus = h->cur_lane;
+    for (int j = 0; j < (int)h->lanes.size(); j++) {   // every lane's tags
+        swap_lane(h, j);
+        PtArgs a = make_args(h, h->par, 0, h->stats);
+        HIPCHK(h, launch_pt_renorm(a, h->stream));
+    }
+    swap_lane(h, focus);
+    return PSIM_OK;
+}
+
+// Focus the lane of heartbeat root `root`; with `create`, give a new root a
+// lane (a fresh one while fewer than kMaxLanes exist, else the least recently
+// used quiescent lane, whose root's per-root sets are then forgotten).
+int focus_root(psim_handle* h, uint32_t root, bool create) {
+    save_lane(h);
+    auto& L = h->lanes;
+    int pick = -1;
+    for (int j = 0; j < (int)L.size() && pick < 0; j++)
+        if (L[j].have_root && L[j].root == root) pick = j;
+    if (pick < 0 && !create) return fail(h, PSIM_EINVAL, "root %u has no heartbeat lane", root);
+    for (int j = 0; j < (int)L.size() && pick < 0; j++)
+        if (!L[j].have_root) pick = j;
+    bool fresh = false;
+    if (pick < 0 && (int)L.size() < kMaxLanes) {
+        psim_handle::Lane l;
+        const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+        if (hipMalloc((void**)&l.vs, size_t(h->n) * 16) != hipSuccess ||
+            hipMalloc((void**)&l.in[0], h->E * 4) != hipSuccess || hipMalloc((void**)&l.in[1], h->E * 4) != hipSuccess ||
+            hipMalloc((void**)&l.pend[0], ng) != hipSuccess || hipMalloc((void**)&l.pend[1], ng) != hipSuccess ||
+            hipMalloc((void**)&l.ost, size_t(h->n) + 4) != hipSuccess) {
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
+            for (void* p : lp)
+                if (p) (void)hipFree(p);
+            return fail(h, PSIM_ENOMEM, "heartbeat lane %zu for n=%u", L.size(), h->n);
+        }
+        l.ost_total = h->ost_total_base + L.size();
+        L.push_back(l);
+        pick = (int)L.size() - 1;
+        fresh = true;
+    }
+    if (pick < 0) {                                 // evict the least recently used quiescent lane
+        for (int j = 0; j < (int)L.size(); j++)
+            if (lane_quiescent(L[j]) && (pick < 0 || L[j].last_use < L[pick].last_use)) pick = j;
+        if (pick < 0) return fail(h, PSIM_EBUSY, "all %d heartbeat lanes are in flight", kMaxLanes);
+        fresh = true;
+    }
+    if (fresh) {                                    // start_link/0 state for this lane
+        auto& l = L[pick];
+        const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+        HIPCHK(h, hipMemsetAsync(l.vs, 0, size_t(h->n) * 16, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.in[0], 0, h->E * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.in[1], 0, h->E * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.pend[0], 0, ng, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.pend[1], 0, ng, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.ost, 0, size_t(h->n) + 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.ost_total, 0, sizeof(int), h->stream));
+        l.par = 0;
+        l.serial = 0;
+        l.have_root = false;
+        l.ost_cnt = l.live_rows = 0;
+        l.inflight = 0;
+        load_lane(h, pick);
+        PtArgs a = make_args(h, h->par, 0, h->stats);   // tags that match no serial / epoch
+        HIPCHK(h, launch_pt_renorm(a, h->stream));
+    } else {
+        load_lane(h, pick);
+    }
+    L[pick].last_use = ++h->use_clock;
     return PSIM_OK;
 }
 
@@ -320,57 +443,83 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     uint32_t ran = 0;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
-    bool done = stop_q && quiescent(h);
+    const int focus = h->cur_lane;
+    save_lane(h);
+    auto all_quiet = [&]() {
+        for (const auto& l : h->lanes)
+            if (!lane_quiescent(l)) return false;
+        return true;
+    };
+    bool done = stop_q && all_quiet();
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
-        HIPCHK(h, hipMemsetAsync(h->stats, 0, k * kStatsRow * sizeof(unsigned long long), h->stream));
-        uint32_t par = h->par;
+        // a quiescent lane's round changes nothing: only the others run (the
+        // focused lane always runs, so a plain psim_step still launches)
+        std::vector<int> act;
+        for (int j = 0; j < (int)h->lanes.size(); j++)
+            if (j == focus || !lane_quiescent(h->lanes[j])) act.push_back(j);
+        const size_t A = act.size();
+        HIPCHK(h, hipMemsetAsync(h->stats, 0, k * A * kStatsRow * sizeof(unsigned long long), h->stream));
         for (uint32_t i = 0; i < k; i++) {
             const uint32_t tick = ((h->round + i + 1) % L) == 0;
-            PtArgs a = make_args(h, par, tick, h->stats + i * kStatsRow);
             HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-            HIPCHK(h, launch_pt_round(a, h->stream));
+            for (size_t q = 0; q < A; q++) {
+                load_lane(h, act[q]);
+                PtArgs a = make_args(h, h->par, tick, h->stats + (i * A + q) * kStatsRow);
+                HIPCHK(h, launch_pt_round(a, h->stream));
+                h->lanes[act[q]].par ^= 1u;
+            }
             HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
-            par ^= 1u;
         }
-        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * kStatsRow * sizeof(unsigned long long),
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        h->par = par;
         for (uint32_t i = 0; i < k; i++) {
-            unsigned long long r[kNStat];
-            reduce_row(h->h_stats + i * kStatsRow, r);
             float ms = 0.f;
             HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
-            if (r[S_OVERFLOW])
-                return fail(h, PSIM_EOVERFLOW,
-                            "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 65535, "
-                            "4: outstanding rows of an older heartbeat, 8: a bin region overran)",
-                            (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
+            unsigned long long tot[kNStat] = {0};
             uint64_t msgs = 0;
-            for (int t = 1; t <= 5; t++) msgs += r[t];
+            for (size_t q = 0; q < A; q++) {
+                unsigned long long r[kNStat];
+                reduce_row(h->h_stats + (i * A + q) * kStatsRow, r);
+                if (r[S_OVERFLOW]) {
+                    load_lane(h, focus);
+                    return fail(h, PSIM_EOVERFLOW,
+                                "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 65535, "
+                                "4: outstanding rows of an older heartbeat, 8: a bin region overran)",
+                                (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
+                }
+                auto& l = h->lanes[act[q]];
+                uint64_t lm = 0;
+                for (int t = 1; t <= 5; t++) lm += r[t];
+                l.ost_cnt += (int64_t)r[S_OST_DELTA];
+                l.live_rows += (int64_t)r[S_LIVE_DELTA];
+                l.inflight = lm;
+                msgs += lm;
+                for (int t = 0; t < kNStat; t++) tot[t] += r[t];
+            }
             h->round++;
-            h->ost_cnt += (int64_t)r[S_OST_DELTA];
-            h->live_rows += (int64_t)r[S_LIVE_DELTA];
-            h->inflight = msgs;
             h->kernel_ms_total += ms;
             h->rounds_total++;
             if (out && ran < cap) {
                 psim_round_stats& o = out[ran];
                 memset(&o, 0, sizeof o);
-                for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
-                o.delivered_new = r[S_DELIV];
-                o.active = r[S_ACTIVE];
-                o.senders = r[S_SENDERS];
-                o.sender_degree_sum = r[S_DEGSUM];
-                o.outstanding_vertices = (uint64_t)h->ost_cnt;
-                o.algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+                for (int t = 1; t <= 5; t++) o.sent[t] = tot[t];
+                o.delivered_new = tot[S_DELIV];
+                o.active = tot[S_ACTIVE];
+                o.senders = tot[S_SENDERS];
+                o.sender_degree_sum = tot[S_DEGSUM];
+                int64_t ov = 0;
+                for (const auto& l : h->lanes) ov += l.ost_cnt;
+                o.outstanding_vertices = (uint64_t)ov;
+                o.algo_bytes = 16ull * h->n * A + 8ull * tot[S_SENDERS] + 4ull * tot[S_DEGSUM] + 32ull * msgs;
                 o.kernel_ms = ms;
             }
             ran++;
-            if (stop_q && quiescent(h)) { done = true; break; }
+            if (stop_q && all_quiet()) { done = true; break; }
         }
     }
+    load_lane(h, focus);
     if (ran_out) *ran_out = ran;
     return PSIM_OK;
 }
@@ -452,11 +601,12 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (hipMalloc(&h->sh.ring, 16 * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         for (auto& e : h->sh.rev_)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
-        if (hipMalloc(&h->stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipHostMalloc(&h->h_stats, kChunk * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMalloc(&h->ost_total, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMemset(h->ost_total, 0, 64) != hipSuccess) { rc = PSIM_EHIP; break; }
+        if (hipMalloc(&h->ost_total_base, kMaxLanes * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)) != hipSuccess) { rc = PSIM_EHIP; break; }
+        h->ost_total = h->ost_total_base;
         for (auto& e : h->ev)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
     } while (0);
@@ -481,7 +631,7 @@ int psim_destroy(psim_handle* h) {
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
     if (h->scratch) (void)hipFree(h->scratch);
-    if (h->ost_total) (void)hipFree(h->ost_total);
+    if (h->ost_total_base) (void)hipFree(h->ost_total_base);
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -692,7 +842,10 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         HIPCHK(h, hipMemset(h->pend[1], 0, ng));
     }
     HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
-    HIPCHK(h, hipMemset(h->ost_total, 0, 64));
+    HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)));
+    h->ost_total = h->ost_total_base;
+    h->lanes.assign(1, psim_handle::Lane());
+    h->cur_lane = 0;
     if (W > 1) {
         std::vector<uint32_t> sb32(W);
         for (uint32_t d = 0; d < W; d++) sb32[d] = uint32_t(sbases[d]);
@@ -746,13 +899,18 @@ int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
         if (alive[v]) bm[v >> 5] |= 1u << (v & 31);
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemcpyAsync(h->alive, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemsetAsync(h->scratch, 0, 8, h->stream));
-    PtArgs a = make_args(h, h->par, 0, h->stats);
-    HIPCHK(h, launch_pt_count_live(a, h->scratch, h->stream));
-    unsigned long long live = 0;
-    HIPCHK(h, hipMemcpyAsync(&live, h->scratch, 8, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    h->live_rows = (int64_t)live;
+    const int focus = h->cur_lane;
+    for (int j = 0; j < (int)h->lanes.size(); j++) {   // outstanding rows to live peers, per lane
+        swap_lane(h, j);
+        HIPCHK(h, hipMemsetAsync(h->scratch, 0, 8, h->stream));
+        PtArgs a = make_args(h, h->par, 0, h->stats);
+        HIPCHK(h, launch_pt_count_live(a, h->scratch, h->stream));
+        unsigned long long live = 0;
+        HIPCHK(h, hipMemcpyAsync(&live, h->scratch, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->live_rows = (int64_t)live;
+    }
+    swap_lane(h, focus);
     return PSIM_OK;
 }
 
@@ -777,9 +935,13 @@ namespace {
 int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned long long* r) {
     if (!h || !h->n) return PSIM_ESTATE;
     if (root >= h->sh.n_global) return PSIM_EINVAL;
-    if (!quiescent(h)) return fail(h, PSIM_EBUSY, "previous broadcast still in flight");
     HIPCHK(h, hipSetDevice(h->device));
-    if (h->have_root && root != h->root) {
+    if (lanes_enabled(h)) {                 // each root heartbeats over its own lane
+        const int rc = focus_root(h, root, true);
+        if (rc) return rc;
+    }
+    if (!quiescent(h)) return fail(h, PSIM_EBUSY, "previous broadcast of this root still in flight");
+    if (!lanes_enabled(h) && h->have_root && root != h->root) {
         // single-root engine: the previous root's per-root sets are dropped
         // (DESIGN.md "Limitations": multi-root trees are SURVEY 8(f) row 1)
         h->epoch++;
@@ -1342,6 +1504,12 @@ int psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m) {
     if (!h || !origins || m != h->dm.m || !m) return PSIM_EINVAL;
     memcpy(origins, h->dm.h_origin.data(), m * 4);
     return PSIM_OK;
+}
+
+int psim_plumtree_focus(psim_handle* h, uint32_t root) {
+    if (!h || !h->n) return PSIM_ESTATE;
+    if (!lanes_enabled(h)) return h->have_root && h->root == root ? PSIM_OK : PSIM_EINVAL;
+    return focus_root(h, root, false);
 }
 
 int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst, size_t k) {

@@ -121,6 +121,10 @@ class Simulator:
         self._c(lib().psim_get_inflight(self._h, _u32p(w), self.num_slots))
         return w[: self.num_slots]
 
+    def focus(self, root):
+        """Point the per-vertex getters at heartbeat root `root`'s lane (psim_plumtree_focus)."""
+        self._c(lib().psim_plumtree_focus(self._h, root))
+
     def set_omissions(self, pairs):
         """Omission faults on directed (src, dst) pairs (psim_set_omissions); [] heals."""
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))

@@ -29,6 +29,7 @@ def psim(request):
     import partisan_amd
     ns = types.SimpleNamespace(**{k: getattr(partisan_amd, k) for k in dir(partisan_amd) if not k.startswith("__")})
     ns.Simulator = functools.partial(partisan_amd.Simulator, binned=request.param == "binned")
+    ns.engine = request.param
     return ns
 
 
@@ -137,8 +138,8 @@ def test_reset_trees_and_root_change(psim):
         if reset:
             sim.reset_trees()
             orc.reset_peers_all()
-        if root != getattr(sim, "_last_root", root):
-            orc.reset_peers_all()      # single-root engine drops the old root's sets
+        if root != getattr(sim, "_last_root", root) and psim.engine == "binned":
+            orc.reset_peers_all()      # one lane: a new root drops the old root's sets
         sim._last_root = root
         m = sim.broadcast(root)
         assert m == orc.heartbeat(root)
@@ -356,3 +357,74 @@ def test_partition_then_heal(psim):
     mono = orc.heartbeat(0)
     lockstep(sim, orc, 0, mono)
     assert sim.delivered().all()
+
+
+def _multi_compare(sim, orc, monos):
+    """Per root: delivered set, Round, eager / lazy sets; all roots together:
+    outstanding peers per vertex and the in-flight messages (as a multiset:
+    lanes keep no FIFO order across roots, which no per-root state depends on)."""
+    n = sim.n
+    outst_all = [set() for _ in range(n)]
+    inflight = []
+    for root, mono in monos.items():
+        sim.focus(root)
+        eager, lazy, outst, rr = sim.plumtree_state()
+        assert np.array_equal(sim.delivered(), orc.delivered(root, mono)), root
+        orr = orc.recv_round(root, mono)
+        got = np.where(rr == 0xFFFF, 0xFFFFFFFF, np.where(rr == 0xFFFE, 0xFFFFFFFE, rr.astype(np.int64)))
+        assert np.array_equal(got.astype(np.uint64), orr.astype(np.uint64)), root
+        for v in range(n):
+            oe, ol = orc.peers(v, root)
+            assert sim.mask_to_peers(v, eager[v]) == oe, (root, v)
+            assert sim.mask_to_peers(v, lazy[v]) == ol, (root, v)
+            outst_all[v] |= set(sim.mask_to_peers(v, outst[v]))
+        inflight += sim.decode_inflight()
+    for v in range(n):
+        assert outst_all[v] == {p for p, _, _ in orc.outstanding(v)}, v
+    want = [(s_, d, t, r if t in (1, 3) else 0) for (s_, d, t, r) in orc.pending()]
+    assert sorted(inflight) == sorted(want)
+
+
+def test_multi_root_heartbeats_lockstep():
+    """heartbeats of several roots in flight at once (and
+    a root heartbeating again while others are in flight), each root's tree
+    kept -- round by round against the oracle, whose state is per root."""
+    import partisan_amd as pa
+    rp, col = pa.overlay.random_regular(1200, 5, 121)
+    sim = pa.Simulator()
+    sim.load_overlay(rp, col)
+    orc = O.Plumtree(rp, col, lazy_tick_rounds=1)
+    monos = {}
+    schedule = {0: [0, 7], 2: [500], 5: [1100], 12: [7]}   # round -> roots heartbeating before it
+    for rnd in range(40):
+        for root in schedule.get(rnd, []):
+            m = sim.broadcast(root)
+            assert m == orc.heartbeat(root)
+            monos[root] = m
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (rnd, k, gs, os_)
+        assert gs["delivered_new"] == os_["delivered_new"], rnd
+        _multi_compare(sim, orc, monos)
+    sim.focus(7)
+    assert sim.delivered().all()
+    with pytest.raises(pa.PsimError):
+        sim.focus(3)                 # never heartbeated: no lane
+    sim.close()
+
+
+def test_multi_root_lane_reuse():
+    """More roots than lanes: the least recently used quiescent lane is reused
+    (its root's sets forgotten, as after reset_peers for that root)."""
+    import partisan_amd as pa
+    rp, col = pa.overlay.random_regular(400, 5, 131)
+    sim = pa.Simulator()
+    sim.load_overlay(rp, col)
+    for root in range(20):
+        sim.broadcast(root)
+        sim.run()
+        assert sim.delivered().all()
+    sim.focus(19)
+    with pytest.raises(pa.PsimError):
+        sim.focus(0)                 # evicted
+    sim.close()
