@@ -376,7 +376,7 @@ int psim_demers_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_
     d->v_lo = std::min<uint32_t>(n, d->chunk * (uint32_t)rank);
     d->n = std::min<uint32_t>(n, d->v_lo + d->chunk) - d->v_lo;
     const size_t N = std::max<uint32_t>(d->n, 1);
-    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
     bool ok = A((void**)&d->seen, N * 8) && A((void**)&d->pull, N * 16) && A((void**)&d->stats, kStatShards * kNStat * 8) &&
               A((void**)&d->origin, 64 * 4) && A((void**)&d->idbit, 64 * 4);
     for (int k = 0; k < 3 && ok; k++) ok = A((void**)&d->rm[k], N * 8);

@@ -271,7 +271,7 @@ const FmState* fm_of(const psim_handle* h) { return static_cast<const FmState*>(
     } while (0)
 
 bool fm_alloc(void** p, size_t bytes) {
-    return hipMalloc(p, bytes ? bytes : 8) == hipSuccess && hipMemset(*p, 0, bytes ? bytes : 8) == hipSuccess;
+    return alloc_zero(p, bytes);
 }
 
 // grow the snapshot buffer `which` to hold k records

@@ -605,7 +605,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->ost_total_base, kMaxLanes * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)) != hipSuccess) { rc = PSIM_EHIP; break; }
+        if (hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) { rc = PSIM_EHIP; break; }
         h->ost_total = h->ost_total_base;
         for (auto& e : h->ev)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
@@ -1433,7 +1434,7 @@ int psim_demers_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period
     free_demers(h);
     auto& d = h->dm;
     const size_t N = n;
-    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
     bool ok = A((void**)&d.seen, N * 8) && A((void**)&d.snap, N * 8) && A((void**)&d.origin, 64 * 4) &&
               A((void**)&d.idbit, 64 * 4);
     for (int p = 0; p < 2 && ok; p++) {
@@ -1625,7 +1626,7 @@ int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
     const uint32_t nb = (n + kBlock - 1) / kBlock;
     uint32_t mcap = 1u << 16;                  // id-map tables: >= 16 rows per vertex, power of two
     while (mcap < 16ull * n && mcap < (1u << 31)) mcap <<= 1;
-    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
     bool ok = A((void**)&v.head, N * sizeof(HvHead)) && A((void**)&v.act, N * 32) && A((void**)&v.pas, N * 128) &&
               A((void**)&v.skey, size_t(mcap) * 8) && A((void**)&v.sval, size_t(mcap) * 8) &&
               A((void**)&v.rkey, size_t(mcap) * 8) && A((void**)&v.rval, size_t(mcap) * 8) &&
@@ -1644,9 +1645,9 @@ int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
     v.cap = cap;
     v.map_cap = mcap;
     v.cfg = *cfg;
-    HIPCHK(h, hipMemset(v.skey, 0xFF, size_t(mcap) * 8));
-    HIPCHK(h, hipMemset(v.rkey, 0xFF, size_t(mcap) * 8));
-    HIPCHK(h, hipMemset(v.alive, 0xFF, ((N + 31) / 32) * 4));
+    HIPCHK(h, hipMemsetAsync(v.skey, 0xFF, size_t(mcap) * 8, h->stream));
+    HIPCHK(h, hipMemsetAsync(v.rkey, 0xFF, size_t(mcap) * 8, h->stream));
+    HIPCHK(h, hipMemsetAsync(v.alive, 0xFF, ((N + 31) / 32) * 4, h->stream));
     HIPCHK(h, launch_hv_init(make_hv_args(h, 0, v.stats), h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PSIM_OK;
@@ -1857,7 +1858,7 @@ int psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t per
     auto& c = h->cs;
     const uint32_t lo = uint32_t((uint64_t(n) * rank) / world), hi = uint32_t((uint64_t(n) * (rank + 1)) / world);
     const size_t N = std::max<uint32_t>(hi - lo, 1);
-    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess; };
+    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
     const bool ok = A((void**)&c.clk, N * kCsLanes * 4) && A((void**)&c.self, N * 4) &&
                     A((void**)&c.buf, N * kCsBufCap * 4) && A((void**)&c.nbuf, N * 4) &&
                     A((void**)&c.base, size_t(kCsWindow) * kCsLanes * kCsLanes * 4) &&

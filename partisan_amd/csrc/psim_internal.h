@@ -9,6 +9,16 @@ typedef struct psim_scamp_stats psim_scamp_stats;
 
 namespace psim {
 
+// hipMalloc + zero fill, finished before returning.  hipMemset runs on the
+// null stream, which does not order with the handles' non-blocking streams:
+// without the device sync a fill could land after work the handle's stream
+// enqueues next (e.g. an upload into a freshly grown buffer).
+inline bool alloc_zero(void** p, size_t bytes) {
+    if (!bytes) bytes = 8;
+    return hipMalloc(p, bytes) == hipSuccess && hipMemset(*p, 0, bytes) == hipSuccess &&
+           hipDeviceSynchronize() == hipSuccess;
+}
+
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics

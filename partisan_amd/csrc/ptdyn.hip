@@ -486,7 +486,7 @@ PdState* pd_of(psim_handle* h) { return static_cast<PdState*>(handle_module(h, M
     } while (0)
 
 bool pd_alloc(void** p, size_t bytes) {
-    return hipMalloc(p, bytes ? bytes : 8) == hipSuccess && hipMemset(*p, 0, bytes ? bytes : 8) == hipSuccess;
+    return alloc_zero(p, bytes);
 }
 
 int pd_args(psim_handle* h, const PdState& s, PdArgs& a) {

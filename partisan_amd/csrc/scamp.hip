@@ -475,7 +475,7 @@ const ScState* sc_of(const psim_handle* h) { return static_cast<const ScState*>(
     } while (0)
 
 bool sc_alloc(void** p, size_t bytes) {
-    return hipMalloc(p, bytes ? bytes : 8) == hipSuccess && hipMemset(*p, 0, bytes ? bytes : 8) == hipSuccess;
+    return alloc_zero(p, bytes);
 }
 
 ScArgs sc_args(const psim_handle* h, const ScState& s) {
@@ -627,7 +627,7 @@ int psim_scamp_setup(psim_handle* h, uint32_t n, uint32_t version, uint32_t c, u
         return handle_fail(h, PSIM_ENOMEM, "scamp state for n=%u", n);
     }
     slot = s;
-    SCCHK(h, hipMemset(s->alive, 1, N));
+    SCCHK(h, hipMemsetAsync(s->alive, 1, N, handle_stream(h)));
     SCCHK(h, launch_sc_init(sc_args(h, *s), nullptr, 0, handle_stream(h)));
     SCCHK(h, hipStreamSynchronize(handle_stream(h)));
     return PSIM_OK;

@@ -152,3 +152,31 @@ def test_gpu_c3_1m():
         st += g.step(1)
     assert st[5]["delivered_live"] > 0
     assert all(x["live"] > 0.99 * n for x in st)
+
+
+@pytest.mark.gpu
+def test_gpu_large_crash_list_resets_every_vertex():
+    """A crash list larger than any before grows the device list buffer; the
+    upload must land after the buffer's zero fill (regression: the fill ran
+    on the null stream, unordered with the handle's stream, and could wipe
+    the list).  Every listed vertex must come back in its start_link state."""
+    import partisan_amd as pa
+    n = 1_000_000
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=10)
+    for v, cc in waves(n)[:12]:
+        g.join(v, cc)
+        g.step(3)
+    pv0, npv0, _, _ = g.scamp.views()
+    fresh = pa.Simulator(device=0, seed=SEED)
+    f = pa.c3.C3Cluster(fresh, n, c=5, periodic_rounds=10)
+    fpv, fnpv, _, _ = f.scamp.views()
+    for k in (2_000, 60_000, 200_000):          # growing lists
+        v, _ = churn(n, k, frac=k / n)
+        v = v[v != 0]
+        g.crash(v)
+        pv, npv, _, _ = g.scamp.views()
+        assert np.array_equal(npv[v], fnpv[v])
+        assert all(pv[x, :npv[x]].tolist() == fpv[x, :fnpv[x]].tolist() for x in v[:2000])
+    sim.close()
+    fresh.close()

@@ -1,0 +1,100 @@
+"""Throughput of the SURVEY 8(d) configurations other than the headline one
+(bench.py measures the 10M-peer Plumtree broadcast).  One JSON line per
+config: device time from the engines' hipEvents, the 8(d) algorithmic bytes
+and their fraction of the 8 TB/s HBM roofline.  Synthetic inputs; run on the
+GPU box:  python tools/config_bench.py > profiles/rNN/configs.jsonl
+  C2  10k-peer HyParView overlay (sequential joins, 10 shuffle periods) + one Plumtree broadcast
+  C3  1M-peer SCAMP v2, 5 % churn per round + Plumtree repair (tools/probe_engines.py c3)
+  C4  10M-peer Demers rumor mongering (fanout 2) + anti-entropy (fanout 2, every 2 rounds), 64 rumors, 1 GPU
+  C5  1M-peer causal broadcast, 64 emitters with 64-lane vclocks, 1 GPU
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+import partisan_amd as pa  # noqa: E402
+
+HBM = 8000.0   # GB/s, MI355X peak (MI355X_MICROARCH.md)
+
+
+def line(cfg, **kw):
+    print(json.dumps(dict(config=cfg, **kw)), flush=True)
+
+
+def c2():
+    n = 10_000
+    sim = pa.Simulator(seed=0x5EED0002)
+    hv = pa.hyparview.HyParViewCluster(sim, n)
+    from partisan_amd.overlay import philox_uniform
+    t0 = time.time()
+    st = []
+    for v in range(1, n):                        # vertex v joins a Philox contact in [0, v)
+        c = philox_uniform(0x5EED0002, np.array([v], np.uint32), 0xC200, v)
+        hv.join_many(np.array([v], np.uint32), np.asarray(c, np.uint32))
+        st += hv.step(1)
+    st += hv.step(10 * 10)                       # 10 shuffle periods (shuffle every 10 rounds)
+    wall = time.time() - t0
+    rp, col = hv.overlay()
+    sim.load_overlay(rp, col)
+    sim.broadcast(0)
+    pst, rounds = sim.run()
+    hv_ms = sum(s["kernel_ms"] for s in st)
+    pt_ms = sum(s["kernel_ms"] for s in pst)
+    line("C2", n=n, hyparview_rounds=len(st), hyparview_kernel_ms=round(hv_ms, 3),
+         hyparview_ms_per_round=round(hv_ms / len(st), 4), hyparview_wall_s=round(wall, 2),
+         plumtree_rounds=rounds, plumtree_kernel_ms=round(pt_ms, 3), delivered=int(sim.delivered().sum()),
+         note="latency-bound at 10k peers: one join per round, as the sequential-join schedule prescribes")
+    sim.close()
+
+
+def c4(n=10_000_000, m=64):
+    sim = pa.Simulator(seed=0x5EED0004)
+    dm = pa.demers.DemersEpidemic(sim, n, m, 2, True)
+    dm.broadcast()
+    t0 = time.time()
+    st, r = dm.run(400)
+    wall = time.time() - t0
+    ms = sum(s["kernel_ms"] for s in st)
+    b = sum(s["algo_bytes"] for s in st)
+    gbs = b / 1e6 / ms
+    line("C4", n=n, rumors=m, rounds=r, complete=int(st[-1]["complete"]), kernel_ms=round(ms, 3),
+         ms_per_round=round(ms / r, 4), wall_s=round(wall, 3), peer_rounds_per_s=n * r / (ms / 1e3),
+         algo_GBps=round(gbs, 1), hbm_frac=round(gbs / HBM, 4),
+         messages=int(sum(s["rm_sent"] + s["push_sent"] + s["pull_sent"] for s in st)))
+    sim.close()
+
+
+def c5(n=1_000_000, m=64, rounds=16):
+    sim = pa.Simulator(seed=0x5EED0005)
+    g = pa.causal.CausalCluster(sim, n, m=m, period=1, dmax=4, redeliver=1)
+    st = g.step(rounds)
+    last = st[4:]
+    ms = sum(s["kernel_ms"] for s in last)
+    b = sum(s["algo_bytes"] for s in last)
+    gbs = b / 1e6 / ms
+    line("C5", n=n, emitters=m, rounds=rounds, ms_per_round=round(ms / len(last), 4),
+         deliveries_per_round=sum(s["delivered"] for s in last) / len(last),
+         deliveries_per_s=sum(s["delivered"] for s in last) / (ms / 1e3),
+         algo_GBps=round(gbs, 1), hbm_frac=round(gbs / HBM, 4))
+    sim.close()
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["C2", "C3", "C4", "C5"]
+    for w in which:
+        if w == "C2":
+            c2()
+        elif w == "C3":
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            import probe_engines
+            r = probe_engines.c3(1_000_000, 30)
+            line("C3", **r)
+        elif w == "C4":
+            c4()
+        elif w == "C5":
+            c5()
