@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpsim.so")
+LIB_PATH = os.environ.get("PSIM_LIB_PATH") or os.path.join(HERE, "libpsim.so")   # override: kernel experiments
 
 PSIM_ABI_VERSION = 1
 PSIM_CFG_BINNED = 1   # psim_config.flags: binned Plumtree engine on one GPU
@@ -236,6 +236,8 @@ def lib():
                               f"g.build()'` (hipcc --offload-arch=gfx950)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PSIM_LIB_PATH") and not hasattr(L, name):
+                continue            # an older experiment build: bind what it exports
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

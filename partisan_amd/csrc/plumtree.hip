@@ -118,11 +118,16 @@ __device__ __forceinline__ bool omitted(const PtArgs& a, uint32_t e) {
     return a.omit && ((a.omit[e >> 5] >> (e & 31)) & 1u);
 }
 
+template <bool kOmit = true>
 __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w) {
-    if (omitted(a, e)) return;
+    if (kOmit && omitted(a, e)) return;
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
+#ifdef PT_NT_STORE
+        __builtin_nontemporal_store(w, &a.in_nxt[a.rev[e] - a.slot_base]);
+#else
         a.in_nxt[a.rev[e] - a.slot_base] = w;
+#endif
         a.pend_nxt[u >> kGroupShift] = 1;
     } else {
         a.stage[e] = w;
@@ -281,6 +286,7 @@ __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint
 // column (stride kBlock) for the reply FIFOs of its slots.  `pend`: the
 // vertex's 16-vertex group was flagged (it may have words); `due`: the lazy
 // tick fires and it holds outstanding rows.
+template <bool kOmit>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
     const uint32_t rs = a.rowp[v];
@@ -318,7 +324,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, c);
         if (!w) continue;
-        deliver_word(a, rs + s, w);
+        deliver_word<kOmit>(a, rs + s, w);
         sent = true;
     }
     if (sent) {
@@ -332,6 +338,9 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 // them: their group flag (set by any sender to the group) and, on a tick
 // round while some vertex holds outstanding rows, their outstanding byte.
 // Candidates are compacted into an LDS list and spread over the threads.
+// kOmit: omission faults installed (psim_set_omissions); the common case
+// compiles without the per-word bitmap test.
+template <bool kOmit>
 __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     __shared__ uint16_t rep[kMaxDeg * kBlock];
     __shared__ uint32_t cand[kChunkV];
@@ -374,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
+        pt_vertex<kOmit>(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
     flush_counters(c, a.stats, a.ost_total);
 }
@@ -833,7 +842,10 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(pb_round_kernel, dim3(a.nf < 4096u ? a.nf : 4096u), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(pt_round_kernel, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
+    if (a.omit)
+        hipLaunchKernelGGL(pt_round_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(pt_round_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
