@@ -267,6 +267,33 @@ static ERL_NIF_TERM nif_trace_hash(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
     return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_tuple_from_array(env, t, 4));
 }
 
+/* focus(Sim, Root) -> ok: the per-vertex getters read Root's heartbeat lane */
+static ERL_NIF_TERM nif_focus(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_focus(r->h, root);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* set_omissions(Sim, SrcU32s, DstU32s) -> ok: omission faults on the directed
+ * pairs (native-endian u32 binaries of equal length; <<>> heals) */
+static ERL_NIF_TERM nif_set_omissions(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary s, d;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &s) ||
+        !enif_inspect_binary(env, argv[2], &d) || s.size != d.size || s.size % 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_set_omissions(r->h, (const uint32_t*)s.data, (const uint32_t*)d.data, s.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
 /* ---- HyParView --------------------------------------------------------- */
 
 /* hv_setup(Sim, N, #{active_max_size, ..., promotion_rounds}) -> ok */
@@ -447,6 +474,8 @@ static ErlNifFunc funcs[] = {
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"trace_hash", 1, nif_trace_hash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"focus", 2, nif_focus, 0},
+    {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_step", 2, nif_hv_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},

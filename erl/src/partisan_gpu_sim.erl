@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
-         peers/1, slots/1, delivered/1, trace_hash/1,
+         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
          vclock/4]).
@@ -56,6 +56,14 @@ slots(_Sim) -> erlang:nif_error(nif_not_loaded).
 
 -spec delivered(sim()) -> {ok, binary()} | error().
 delivered(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% Point the per-vertex getters at Root's heartbeat lane (psim_plumtree_focus).
+-spec focus(sim(), non_neg_integer()) -> ok | error().
+focus(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
+
+%% Omission faults on directed pairs: native-endian u32 binaries (psim_set_omissions).
+-spec set_omissions(sim(), binary(), binary()) -> ok | error().
+set_omissions(_Sim, _Src, _Dst) -> erlang:nif_error(nif_not_loaded).
 
 %% Order-independent digest of the Plumtree state (psim_trace_hash).
 -spec trace_hash(sim()) -> {ok, {non_neg_integer(), non_neg_integer(), non_neg_integer(), non_neg_integer()}} | error().
