@@ -64,7 +64,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 
 // Reduce the per-thread counters of a workgroup and add them to a shard.
 __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long* __restrict__ stats,
-                                               int* ost_total) {
+                                               int* ost_total, int* msgs = nullptr) {
     __shared__ unsigned long long red[kBlock / 64][kNStat];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -93,6 +93,12 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
             if (s) atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kNStat + i], s);
             if (s && i == S_OST_DELTA && ost_total) atomicAdd(ost_total, (int)(long long)s);
         }
+    }
+    if (msgs && threadIdx.x == 0) {          // "this round sent something" for the next round's early exit:
+        unsigned long long m = 0;            // a plain store of 1 (an atomic per workgroup on one
+        for (int k = 1; k <= 5; k++)         // address serialises at ~12 ns each)
+            for (int w = 0; w < kBlock / 64; w++) m += red[w][k];
+        if (m) *msgs = 1;
     }
 }
 
@@ -346,6 +352,12 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     __shared__ uint32_t cand[kChunkV];
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
+    if (a.msgs3) {
+        if (blockIdx.x == 0 && t == 0) a.msgs3[a.mnext] = 0;   // the next round's counter starts empty
+        // nothing was sent last round and no row is due: every vertex is idle
+        // (no inbox flag can be set), so the whole round is a no-op
+        if (a.msgs3[a.mprev] == 0 && !(a.tick && *a.ost_total > 0)) return;
+    }
     const uint32_t base = blockIdx.x * kChunkV;
     if (t == 0) ncand = 0;
     __syncthreads();
@@ -385,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
         const uint32_t x = cand[i];
         pt_vertex<kOmit>(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
-    flush_counters(c, a.stats, a.ost_total);
+    flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -646,6 +658,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
     }
     if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
     if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);
+    if (nmsg && a.msgs3) a.msgs3[a.mprev] = 1;   // read by the next round
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
 }
 

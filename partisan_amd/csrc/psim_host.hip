@@ -17,7 +17,7 @@
 using namespace psim;
 
 namespace {
-constexpr int kChunk = 4;   // rounds launched between host synchronisations
+constexpr int kChunk = 16;  // rounds launched between host synchronisations (no-op rounds exit early)
 constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-scatter engine)
 constexpr size_t kStatsRow = size_t(kStatShards) * kNStat;
 }  // namespace
@@ -304,6 +304,19 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     return a;
 }
 
+// Early exit of no-op rounds (psim_step / psim_run on one GPU with the
+// slot-scatter engine): round R reads the messages emitted by round R-1 (or
+// the origin) from msgs3[(R-1) mod 3], adds its own into msgs3[R mod 3] and
+// clears msgs3[(R+1) mod 3]; lane-local, next to the lane's ost_total.
+void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
+    if (h->sh.world != 1 || h->bin.rec_c) return;
+    a.msgs3 = h->ost_total + 1;
+    const uint32_t r = uint32_t(R % 3);
+    a.mprev = (r + 2) % 3;
+    a.mcur = r;
+    a.mnext = (r + 1) % 3;
+}
+
 // ---- heartbeat-root lanes ------------------------------------------------
 void save_lane(psim_handle* h) {
     auto& l = h->lanes[h->cur_lane];
@@ -399,7 +412,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
                 if (p) (void)hipFree(p);
             return fail(h, PSIM_ENOMEM, "heartbeat lane %zu for n=%u", L.size(), h->n);
         }
-        l.ost_total = h->ost_total_base + L.size();
+        l.ost_total = h->ost_total_base + 4 * L.size();     // {ost_total, msgs3[3]} per lane
         L.push_back(l);
         pick = (int)L.size() - 1;
         fresh = true;
@@ -419,7 +432,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         HIPCHK(h, hipMemsetAsync(l.pend[0], 0, ng, h->stream));
         HIPCHK(h, hipMemsetAsync(l.pend[1], 0, ng, h->stream));
         HIPCHK(h, hipMemsetAsync(l.ost, 0, size_t(h->n) + 4, h->stream));
-        HIPCHK(h, hipMemsetAsync(l.ost_total, 0, sizeof(int), h->stream));
+        HIPCHK(h, hipMemsetAsync(l.ost_total, 0, 4 * sizeof(int), h->stream));
         l.par = 0;
         l.serial = 0;
         l.have_root = false;
@@ -466,6 +479,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             for (size_t q = 0; q < A; q++) {
                 load_lane(h, act[q]);
                 PtArgs a = make_args(h, h->par, tick, h->stats + (i * A + q) * kStatsRow);
+                set_round_slots(h, a, h->round + i + 1);
                 HIPCHK(h, launch_pt_round(a, h->stream));
                 h->lanes[act[q]].par ^= 1u;
             }
@@ -604,8 +618,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (hipMalloc(&h->stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMalloc(&h->ost_total_base, kMaxLanes * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)) != hipSuccess ||
+        if (hipMalloc(&h->ost_total_base, kMaxLanes * 4 * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) { rc = PSIM_EHIP; break; }
         h->ost_total = h->ost_total_base;
         for (auto& e : h->ev)
@@ -843,7 +857,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         HIPCHK(h, hipMemset(h->pend[1], 0, ng));
     }
     HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
-    HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * sizeof(int)));
+    HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)));
     h->ost_total = h->ost_total_base;
     h->lanes.assign(1, psim_handle::Lane());
     h->cur_lane = 0;
@@ -963,6 +977,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
         // origin emits into the buffer the next round reads
         PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+        set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
         a.root = lr;
         HIPCHK(h, launch_pt_origin(a, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),

@@ -67,6 +67,8 @@ struct PtArgs {
     uint8_t* __restrict__ pend_nxt;
     uint8_t* __restrict__ ost;             // [n+3] 1 = outstanding rows exist
     int* ost_total;                        // device count of vertices with outstanding rows
+    int* msgs3;                            // [3] "round r mod 3 sent messages" flags (null: no early exit)
+    uint32_t mprev, mcur, mnext;           // this round r: (r-1) mod 3, r mod 3, (r+1) mod 3
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
