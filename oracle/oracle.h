@@ -341,6 +341,28 @@ void orc_c3_crash(orc_c3* s, uint32_t v);            /* crash + restart now (bot
 uint32_t orc_c3_heartbeat(orc_c3* s, uint32_t root);
 uint32_t orc_c3_step(orc_c3* s, uint32_t rounds, orc_c3_stats* st);
 
+/* ------------------------------------------------------------------ */
+/* Transitive relay over Plumtree out-links (relay.c) */
+/* partisan_hyparview_peer_service_manager.erl:1800-1832, 2220-2290,  */
+/* 2796-2870.                                                          */
+/* ------------------------------------------------------------------ */
+typedef struct orc_relay_round {
+    uint64_t direct;   /* copies of Message sent to Node (connected)     */
+    uint64_t relay;    /* relay_message copies sent                      */
+    uint64_t dropped;  /* relay_message copies dropped at TTL 0          */
+    uint64_t lost;     /* out-links not connected: send failed           */
+    uint64_t arrived;  /* copies of Message arriving at Node this round  */
+} orc_relay_round;
+/* k sends src[i] -> dst[i] with transitive => true, all handled by their
+ * origins in round 0; runs to quiescence.  act = active views (members),
+ * ol = out_links per vertex.  delivered[k] copies, first_round[k] arrival
+ * round (UINT32_MAX: never).  Returns the rounds run (stats[0..]), or
+ * ORC_BADARG / ORC_NOSPACE (more than max_copies copies in one round). */
+int64_t orc_relay_run(uint32_t n, const uint64_t* act_ptr, const uint32_t* act, const uint64_t* ol_ptr,
+                      const uint32_t* ol, const uint8_t* alive, uint32_t k, const uint32_t* src,
+                      const uint32_t* dst, uint32_t relay_ttl, uint64_t* delivered, uint32_t* first_round,
+                      orc_relay_round* stats, size_t cap, size_t max_copies);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,6 +95,10 @@ MSG_NAMES = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "g
 _lib = None
 
 
+class RelayRound(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("direct", "relay", "dropped", "lost", "arrived")]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -153,6 +157,10 @@ def lib():
         L.orc_pt_set_omissions.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), sz]
         L.orc_pt_omitted.argtypes = [C.c_void_p]
         L.orc_pt_omitted.restype = C.c_uint64
+        L.orc_relay_run.argtypes = [C.c_uint32, P(C.c_uint64), P(C.c_uint32), P(C.c_uint64), P(C.c_uint32),
+                                    P(C.c_uint8), C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
+                                    P(C.c_uint64), P(C.c_uint32), P(RelayRound), sz, sz]
+        L.orc_relay_run.restype = C.c_int64
         L.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         L.orc_dm_sample2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
         L.orc_dm_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
@@ -862,3 +870,26 @@ class C3:
         st = (C3Stats * rounds)()
         lib().orc_c3_step(self._h, rounds, st)
         return [x.as_dict() for x in st]
+
+
+def relay_run(act_ptr, act, ol_ptr, ol, alive, src, dst, relay_ttl=5, max_copies=50_000_000, cap=64):
+    """Transitive relay (oracle/relay.c): returns (per-round stats dicts, delivered[k], first_round[k])."""
+    ap = np.ascontiguousarray(act_ptr, dtype=np.uint64)
+    ai = np.ascontiguousarray(act, dtype=np.uint32)
+    op = np.ascontiguousarray(ol_ptr, dtype=np.uint64)
+    oi = np.ascontiguousarray(ol, dtype=np.uint32)
+    al = np.ascontiguousarray(alive, dtype=np.uint8)
+    s = np.ascontiguousarray(src, dtype=np.uint32)
+    d = np.ascontiguousarray(dst, dtype=np.uint32)
+    k = len(s)
+    n = len(ap) - 1
+    dv = np.zeros(k, dtype=np.uint64)
+    fr = np.zeros(k, dtype=np.uint32)
+    st = (RelayRound * cap)()
+    r = lib().orc_relay_run(n, _u64p(ap), _u32p(ai), _u64p(op), _u32p(oi),
+                            al.ctypes.data_as(C.POINTER(C.c_uint8)), k, _u32p(s), _u32p(d), relay_ttl,
+                            dv.ctypes.data_as(C.POINTER(C.c_uint64)), _u32p(fr), st, cap, max_copies)
+    if r < 0:
+        raise ValueError(f"orc_relay_run: {r}")
+    rows = [{f: int(getattr(st[i], f)) for f, _ in RelayRound._fields_} for i in range(min(r, cap))]
+    return rows, dv, fr
