@@ -482,6 +482,33 @@ int  psim_c3_get_plumtree(const psim_handle* h, uint32_t v, uint32_t* eager, siz
                           uint32_t* outstanding, size_t* no, size_t cap, uint32_t* delivered_mono,
                           uint32_t* recv_round);
 
+/* ---- Transitive relay over Plumtree out-links -------
+ * Replaces, for a batch of k sends with `transitive => true`:
+ *   do_send_message/3 (src/partisan_hyparview_peer_service_manager.erl:2220-2290),
+ *   do_tree_forward/4 (:2796-2842), handle_message({relay_message, ..}) (:1800-1832),
+ *   retrieve_outlinks/1 (:2846-2870).
+ * act = active views (CSR, the members handle_message checks), ol = each
+ * vertex's out_links (its eager peers in its own tree), alive = 1 per live
+ * vertex.  "Connected to P" = P live and a peer of the sender (a member of its
+ * view or a vertex whose view lists it).  Round 0: origins handle their sends;
+ * a copy sent in round r is handled in round r + 1; runs to quiescence.
+ * Outputs delivered[k] (copies of Message that reached dst[k]),
+ * first_round[k] (arrival round, UINT32_MAX = never) and per-round stats
+ * (up to cap rows).  Returns the rounds run, PSIM_EOVERFLOW when one round
+ * holds more than max_copies copies, PSIM_EINVAL for bad shapes (src == dst,
+ * ids >= n, relay_ttl 0 or > 127, k >= 2^24). */
+typedef struct psim_relay_stats {
+    uint64_t direct;    /* copies of Message sent to Node (connected)      */
+    uint64_t relay;     /* relay_message copies sent                       */
+    uint64_t dropped;   /* relay_message copies dropped at TTL 0           */
+    uint64_t lost;      /* out-links not connected: the send fails         */
+    uint64_t arrived;   /* copies of Message arriving at Node this round   */
+} psim_relay_stats;
+int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, const uint32_t* act,
+                       const uint64_t* ol_ptr, const uint32_t* ol, const uint8_t* alive, uint32_t k,
+                       const uint32_t* src, const uint32_t* dst, uint32_t relay_ttl, uint64_t* delivered,
+                       uint32_t* first_round, psim_relay_stats* stats, size_t cap, size_t max_copies);
+
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
 

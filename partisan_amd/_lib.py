@@ -121,6 +121,13 @@ class C3Stats(C.Structure):
 
 
 # every entry point of include/psim.h: name -> (restype, argtypes)
+class RelayStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("direct", "relay", "dropped", "lost", "arrived")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 _P = C.POINTER
 _H = C.c_void_p
 SIGNATURES = {
@@ -222,6 +229,9 @@ SIGNATURES = {
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_vclock_increment": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_relay_run": (C.c_int64, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32),
+                                   _P(C.c_uint8), C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), C.c_uint32,
+                                   _P(C.c_uint64), _P(C.c_uint32), _P(RelayStats), C.c_size_t, C.c_size_t]),
 }
 
 _lib = None

@@ -337,7 +337,7 @@ hipError_t launch_pd_round(const PdArgs& a, hipStream_t s);
 struct ModuleState {
     virtual ~ModuleState() {}
 };
-enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_COUNT = 4 };
+enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_RELAY = 4, MOD_COUNT = 5 };
 ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);
 hipStream_t handle_stream(const psim_handle* h);
