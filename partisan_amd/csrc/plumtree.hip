@@ -292,11 +292,88 @@ __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint
 // column (stride kBlock) for the reply FIFOs of its slots.  `pend`: the
 // vertex's 16-vertex group was flagged (it may have words); `due`: the lazy
 // tick fires and it holds outstanding rows.
+// Fast path for rows of <= kFastDeg slots (every HyParView active view):
+// the same clauses in the same slot order, with the row held in registers so
+// that a vertex costs three dependent global round trips (row pointers ->
+// inbox words -> state + neighbour ids + reverse slots), not one or two per
+// slot.  The sparse and middle rounds of a flood are bound by exactly that
+// chain (a workgroup holds few active vertices, each walked by one thread).
+constexpr uint32_t kFastDeg = 8;
+
+template <bool kOmit>
+__device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
+                                               bool due, Ctr& c) {
+    uint32_t w[kFastDeg];
+    uint32_t any = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kFastDeg; s++) {
+        w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
+        any |= w[s];
+    }
+    pend = any != 0;
+    if (!pend && !due) return;
+    const uint32_t aw = a.alive[(a.v_lo + v) >> 5];
+    const uint4 st = a.vs[v];
+    uint32_t cl[kFastDeg], rv[kFastDeg];
+#pragma unroll
+    for (uint32_t s = 0; s < kFastDeg; s++) {
+        cl[s] = s < deg ? a.col[rs + s] : 0u;
+        rv[s] = s < deg ? a.rev[rs + s] : 0u;
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < kFastDeg; s++)
+        if (w[s]) a.in_cur[rs + s] = 0;
+    if (!((aw >> ((a.v_lo + v) & 31)) & 1u)) return;   // a dead vertex receives nothing
+    c.active++;
+    VSt x;
+    vst_load(a, v, st, x);
+    uint32_t r[kFastDeg];
+#pragma unroll
+    for (uint32_t s = 0; s < kFastDeg; s++) r[s] = w[s] ? pt_word(a, rs, s, w[s], x, c) : 0u;
+    uint32_t ihave = 0;                                  // pt_ihave over the registers
+    if (a.tick && x.outst) {
+#pragma unroll
+        for (uint32_t s = 0; s < kFastDeg; s++)
+            if ((x.outst >> s) & 1u) ihave |= (bit_alive(a.alive, cl[s]) ? 1u : 0u) << s;
+    }
+    bool sent = false;
+#pragma unroll
+    for (uint32_t s = 0; s < kFastDeg; s++) {
+        if (s >= deg) break;
+        const uint32_t wo = pt_out<true>(s, r[s], x, ihave, c);
+        if (!wo) continue;
+        sent = true;
+        if (kOmit && omitted(a, rs + s)) continue;
+        const uint32_t u = cl[s] - a.v_lo;
+        if (u < a.n) {
+#ifdef PT_NT_STORE
+            __builtin_nontemporal_store(wo, &a.in_nxt[rv[s] - a.slot_base]);
+#else
+            a.in_nxt[rv[s] - a.slot_base] = wo;
+#endif
+            a.pend_nxt[u >> kGroupShift] = 1;
+        } else {
+            a.stage[rs + s] = wo;
+        }
+    }
+    if (sent) {
+        c.senders++;
+        c.degsum += deg;
+    }
+    vst_store(a, v, st, x, c);
+}
+
 template <bool kOmit>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
+#ifndef PT_NO_FAST
+    if (deg <= kFastDeg) {
+        pt_vertex_fast<kOmit>(a, v, rs, deg, pend, due, c);
+        return;
+    }
+#endif
     if (pend) {
         uint32_t any = 0;
         for (uint32_t s = 0; s < deg; s++) any |= a.in_cur[rs + s];
