@@ -294,6 +294,52 @@ static ERL_NIF_TERM nif_set_omissions(ErlNifEnv* env, int argc, const ERL_NIF_TE
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
 }
 
+/* relay_run(Sim, ActPtr, Act, OlPtr, Ol, Alive, Src, Dst, RelayTTL, MaxCopies)
+ *   -> {ok, Rounds, [{Direct, Relay, Dropped, Lost, Arrived}], Delivered, FirstRound}
+ * Transitive relay over out-links (psim_relay_run).  Pointer binaries are
+ * native-endian u64, id binaries u32, Alive one byte per vertex; Delivered is
+ * a u64 binary and FirstRound a u32 binary, one entry per send. */
+static ERL_NIF_TERM nif_relay_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary ap, ac, op, ol, al, s, d;
+    unsigned ttl;
+    ErlNifUInt64 maxc;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &ap) ||
+        !enif_inspect_binary(env, argv[2], &ac) || !enif_inspect_binary(env, argv[3], &op) ||
+        !enif_inspect_binary(env, argv[4], &ol) || !enif_inspect_binary(env, argv[5], &al) ||
+        !enif_inspect_binary(env, argv[6], &s) || !enif_inspect_binary(env, argv[7], &d) ||
+        !enif_get_uint(env, argv[8], &ttl) || !enif_get_uint64(env, argv[9], &maxc))
+        return enif_make_badarg(env);
+    if (ap.size % 8 || ap.size < 16 || op.size != ap.size || ac.size % 4 || ol.size % 4 || s.size % 4 ||
+        s.size != d.size || al.size != ap.size / 8 - 1)
+        return enif_make_badarg(env);
+    const size_t k = s.size / 4;
+    enum { kCap = 256 };
+    psim_relay_stats st[kCap];
+    ERL_NIF_TERM dv_t, fr_t;   /* env-owned: dropped with the env on an error return */
+    unsigned char* dv = enif_make_new_binary(env, k * 8, &dv_t);
+    unsigned char* fr = enif_make_new_binary(env, k * 4, &fr_t);
+    if (!dv || !fr) return err(env, PSIM_ENOMEM);
+    enif_mutex_lock(r->mu);
+    int64_t rc = psim_relay_run(r->h, (uint32_t)(al.size), (const uint64_t*)ap.data, (const uint32_t*)ac.data,
+                                (const uint64_t*)op.data, (const uint32_t*)ol.data, (const uint8_t*)al.data,
+                                (uint32_t)k, (const uint32_t*)s.data, (const uint32_t*)d.data, ttl,
+                                (uint64_t*)dv, (uint32_t*)fr, st, kCap, (size_t)maxc);
+    enif_mutex_unlock(r->mu);
+    if (rc < 0) return err(env, (int)rc);
+    ERL_NIF_TERM rows = enif_make_list(env, 0);
+    for (int64_t i = (rc < kCap ? rc : kCap) - 1; i >= 0; i--)
+        rows = enif_make_list_cell(env,
+                                   enif_make_tuple5(env, enif_make_uint64(env, st[i].direct),
+                                                    enif_make_uint64(env, st[i].relay),
+                                                    enif_make_uint64(env, st[i].dropped),
+                                                    enif_make_uint64(env, st[i].lost),
+                                                    enif_make_uint64(env, st[i].arrived)),
+                                   rows);
+    return enif_make_tuple5(env, mk_atom(env, "ok"), enif_make_uint64(env, (ErlNifUInt64)rc), rows, dv_t, fr_t);
+}
+
 /* ---- HyParView --------------------------------------------------------- */
 
 /* hv_setup(Sim, N, #{active_max_size, ..., promotion_rounds}) -> ok */
@@ -476,6 +522,7 @@ static ErlNifFunc funcs[] = {
     {"trace_hash", 1, nif_trace_hash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"focus", 2, nif_focus, 0},
     {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"relay_run", 10, nif_relay_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_step", 2, nif_hv_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},

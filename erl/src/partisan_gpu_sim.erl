@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
-         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3,
+         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
          vclock/4]).
@@ -64,6 +64,17 @@ focus(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
 %% Omission faults on directed pairs: native-endian u32 binaries (psim_set_omissions).
 -spec set_omissions(sim(), binary(), binary()) -> ok | error().
 set_omissions(_Sim, _Src, _Dst) -> erlang:nif_error(nif_not_loaded).
+
+%% Transitive relay (psim_relay_run): forward_message(Node, Message,
+%% #{transitive => true}) for a batch of sends over active views (ActPtr u64 /
+%% Act u32 binaries) and out-links (OlPtr / Ol), Alive one byte per vertex.
+%% Returns the rounds run, per-round {Direct, Relay, Dropped, Lost, Arrived},
+%% copies delivered per send (u64 binary) and first arrival rounds (u32).
+-spec relay_run(sim(), binary(), binary(), binary(), binary(), binary(), binary(), binary(),
+                pos_integer(), pos_integer()) ->
+    {ok, non_neg_integer(), [tuple()], binary(), binary()} | error().
+relay_run(_Sim, _ActPtr, _Act, _OlPtr, _Ol, _Alive, _Src, _Dst, _RelayTTL, _MaxCopies) ->
+    erlang:nif_error(nif_not_loaded).
 
 %% Order-independent digest of the Plumtree state (psim_trace_hash).
 -spec trace_hash(sim()) -> {ok, {non_neg_integer(), non_neg_integer(), non_neg_integer(), non_neg_integer()}} | error().
