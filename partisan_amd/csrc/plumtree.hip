@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
         const uint32_t g = v0 >> kGroupShift;
         if (a.pend_cur[g]) {
             pmask = 0xFu;
-            if ((t & 3) == 0) a.pend_cur[g] = 0;   // the 4 threads of a group share the byte
+            if ((t & ((1u << (kGroupShift - 2)) - 1)) == 0) a.pend_cur[g] = 0;   // threads of a group share the byte
         }
         if (a.tick && *a.ost_total > 0) {
             uint32_t w;

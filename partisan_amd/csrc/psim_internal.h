@@ -23,7 +23,11 @@ constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard
-constexpr int kGroupShift = 4;       // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
+#ifndef PT_GROUP_SHIFT
+#define PT_GROUP_SHIFT 4
+#endif
+constexpr int kGroupShift = PT_GROUP_SHIFT;   // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
+static_assert(kGroupShift >= 2 && kGroupShift <= 8, "a group spans whole 4-vertex thread quads");
 constexpr uint32_t kChunkV = 1024;   // vertices owned by one round-kernel workgroup
 // binned engine (single GPU): messages travel as {receiver
 // slot, word} records through coarse then fine receiver bins

@@ -23,6 +23,7 @@
 #include "psim_internal.h"
 #include "../../include/psim.h"
 
+#include <algorithm>
 #include <vector>
 
 namespace psim {
@@ -35,6 +36,8 @@ constexpr uint32_t kRlMaxOl = 64;         // out-links per vertex (u64 mask)
 struct RlArgs {
     const uint32_t *act_ptr, *act, *peer_ptr, *peer, *ol_ptr, *ol;
     const uint8_t* alive;
+    const unsigned long long* olmask;     // [n] out-links that are connected (bit j = ol[ol_ptr[v] + j])
+    const uint8_t* nlost;                 // [n] out-links (minus self) that are not
     const uint32_t *src, *dst;
     unsigned long long* delivered;
     uint32_t* first_round;
@@ -109,18 +112,10 @@ __global__ __launch_bounds__(kBlock) void rl_round_kernel(RlArgs a) {
                 c_direct = 1;
             } else if (!origin && ttl == 0) {
                 c_drop = 1;                     // TTL expired: dropped
-            } else {
-                const uint32_t b = a.ol_ptr[v], e = a.ol_ptr[v + 1];
-                for (uint32_t j = b; j < e; j++) {       // do_tree_forward: OutLinks -- [MyNode]
-                    const uint32_t p = a.ol[j];
-                    if (p == v) continue;
-                    if (a.alive[p] && member(a.peer_ptr, a.peer, v, p)) {
-                        mask |= 1ull << (j - b);
-                        nemit++;
-                    } else {
-                        c_lost++;               // not connected: the send fails, no retry
-                    }
-                }
+            } else {                            // do_tree_forward: OutLinks -- [MyNode]
+                mask = a.olmask[v];             // connectivity is fixed during a run (rl_prep_kernel)
+                nemit = __popcll(mask);
+                c_lost = a.nlost[v];            // not connected: the send fails, no retry
                 c_relay = nemit;
             }
         }
@@ -164,10 +159,30 @@ __global__ __launch_bounds__(kBlock) void rl_round_kernel(RlArgs a) {
     }
 }
 
+// Per vertex, once per run: which out-links are connected (live and a peer)
+// -- views and liveness do not change while a batch is relayed, so every copy
+// at v reuses the mask instead of rescanning v's peer row per out-link.
+__global__ __launch_bounds__(kBlock) void rl_prep_kernel(RlArgs a, uint32_t n, unsigned long long* olmask,
+                                                         uint8_t* nlost) {
+    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= n) return;
+    const uint32_t b = a.ol_ptr[v], e = a.ol_ptr[v + 1];
+    unsigned long long m = 0;
+    uint32_t lost = 0;
+    for (uint32_t j = b; j < e; j++) {
+        const uint32_t p = a.ol[j];
+        if (p == v) continue;
+        if (a.alive[p] && member(a.peer_ptr, a.peer, v, p)) m |= 1ull << (j - b);
+        else lost++;
+    }
+    olmask[v] = m;
+    nlost[v] = (uint8_t)lost;
+}
+
 // Device buffers kept on the handle between runs (grown on demand).
 struct RelayState : ModuleState {
-    void* buf[16] = {};
-    size_t cap[16] = {};
+    void* buf[18] = {};
+    size_t cap[18] = {};
     ~RelayState() override {
         for (void* p : buf)
             if (p) (void)hipFree(p);
@@ -247,6 +262,19 @@ extern "C" int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* ac
             pe[pp[v] + fill[v]++] = act[i];
             pe[pp[act[i]] + fill[act[i]]++] = v;
         }
+    {   // a symmetric pair lists each peer twice: sort + unique every row (shorter member scans)
+        uint32_t out = 0;
+        for (uint32_t v = 0; v < n; v++) {
+            const uint32_t b = pp[v], e = pp[v + 1];
+            std::sort(pe.begin() + b, pe.begin() + e);
+            const uint32_t start = out;
+            for (uint32_t i = b; i < e; i++)
+                if (i == b || pe[i] != pe[i - 1]) pe[out++] = pe[i];
+            pp[v] = start;
+        }
+        pp[n] = out;
+        pe.resize(out ? out : 1);
+    }
 
     ModuleState*& slot = handle_module(h, MOD_RELAY);
     if (!slot) slot = new RelayState();
@@ -265,13 +293,15 @@ extern "C" int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* ac
     unsigned long long* d_deliv = (unsigned long long*)st->get(9, (size_t)k * 8);
     uint2 *d_q0 = (uint2*)st->get(11, max_copies * 8), *d_q1 = (uint2*)st->get(12, max_copies * 8);
     unsigned long long* d_stats = (unsigned long long*)st->get(14, nrounds_max * stat_row * 8);
+    unsigned long long* d_olmask = (unsigned long long*)st->get(15, (size_t)n * 8);
+    uint8_t* d_nlost = (uint8_t*)st->get(16, n);
     if (!d_ap || !d_act || !d_pp || !d_pe || !d_op || !d_ol || !d_src || !d_dst || !d_first || !d_cnt || !d_alive ||
-        !d_deliv || !d_q0 || !d_q1 || !d_stats)
+        !d_deliv || !d_q0 || !d_q1 || !d_stats || !d_olmask || !d_nlost)
         return handle_fail(h, PSIM_ENOMEM, "relay buffers (%zu copies per round)", max_copies);
     RL_HIP(h, hipMemcpyAsync(d_ap, ap.data(), ap.size() * 4, hipMemcpyHostToDevice, s));
     if (na) RL_HIP(h, hipMemcpyAsync(d_act, act, na * 4, hipMemcpyHostToDevice, s));
     RL_HIP(h, hipMemcpyAsync(d_pp, pp.data(), pp.size() * 4, hipMemcpyHostToDevice, s));
-    if (na) RL_HIP(h, hipMemcpyAsync(d_pe, pe.data(), pe.size() * 4, hipMemcpyHostToDevice, s));
+    if (pp[n]) RL_HIP(h, hipMemcpyAsync(d_pe, pe.data(), (size_t)pp[n] * 4, hipMemcpyHostToDevice, s));
     RL_HIP(h, hipMemcpyAsync(d_op, op.data(), op.size() * 4, hipMemcpyHostToDevice, s));
     if (no) RL_HIP(h, hipMemcpyAsync(d_ol, ol, no * 4, hipMemcpyHostToDevice, s));
     RL_HIP(h, hipMemcpyAsync(d_alive, alive, n, hipMemcpyHostToDevice, s));
@@ -288,6 +318,10 @@ extern "C" int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* ac
     a.ovf = d_cnt + 8;
     a.cap = (uint32_t)max_copies;
     a.relay_ttl = relay_ttl;
+    hipLaunchKernelGGL(rl_prep_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a, n, d_olmask, d_nlost);
+    RL_HIP(h, hipGetLastError());
+    a.olmask = d_olmask;
+    a.nlost = d_nlost;
 
     hipEvent_t e0 = handle_event(h, 0), e1 = handle_event(h, 1);
     uint2* q[2] = {d_q0, d_q1};

@@ -7,6 +7,8 @@ GPU box:  python tools/config_bench.py > profiles/rNN/configs.jsonl
   C3  1M-peer SCAMP v2, 5 % churn per round + Plumtree repair (tools/probe_engines.py c3)
   C4  10M-peer Demers rumor mongering (fanout 2) + anti-entropy (fanout 2, every 2 rounds), 64 rumors, 1 GPU
   C5  1M-peer causal broadcast, 64 emitters with 64-lane vclocks, 1 GPU
+  RELAY  10M-peer transitive relay: 100k random sends, relay_ttl 3,
+         5-peer views, out-links = members (no per-root entry), 1 GPU
 """
 import json
 import os
@@ -84,6 +86,30 @@ def c5(n=1_000_000, m=64, rounds=16):
     sim.close()
 
 
+def relay(n=10_000_000, k=100_000, ttl=3):
+    rp, col = pa.overlay.random_regular(n, 5, 0x5EED0006)
+    rng = np.random.default_rng(6)
+    src = rng.integers(0, n, size=k).astype(np.uint32)
+    dst = rng.integers(0, n - 1, size=k).astype(np.uint32)
+    dst = np.where(dst >= src, dst + 1, dst).astype(np.uint32)
+    alive = np.ones(n, np.uint8)
+    sim = pa.Simulator(seed=0x5EED0006)
+    out = []
+    for rep in range(3):                         # the first run also allocates the handle's buffers
+        ms0, _ = sim.timing()
+        t0 = time.time()
+        rows, dv, fr = pa.relay.relay_run(sim, rp, col, rp, col, alive, src, dst, relay_ttl=ttl)
+        wall = time.time() - t0
+        ms = sim.timing()[0] - ms0
+        out.append((ms, wall))
+    ms, wall = out[-1]
+    copies = sum(r["relay"] + r["direct"] for r in rows) + k
+    line("RELAY", n=n, sends=k, relay_ttl=ttl, rounds=len(rows), copies_handled=int(copies),
+         kernel_ms=round(ms, 3), copies_per_s=copies / (ms / 1e3), wall_s_incl_host_setup=round(wall, 3),
+         delivered_sends=int((dv > 0).sum()), per_round=rows)
+    sim.close()
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["C2", "C3", "C4", "C5"]
     for w in which:
@@ -98,3 +124,5 @@ if __name__ == "__main__":
             c4()
         elif w == "C5":
             c5()
+        elif w == "RELAY":
+            relay()
