@@ -424,7 +424,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 // kOmit: omission faults installed (psim_set_omissions); the common case
 // compiles without the per-word bitmap test.
 template <bool kOmit>
-__global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
+__device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     __shared__ uint16_t rep[kMaxDeg * kBlock];
     __shared__ uint32_t cand[kChunkV];
     __shared__ uint32_t ncand;
@@ -475,6 +475,20 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
         pt_vertex<kOmit>(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
     flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+}
+
+template <bool kOmit>
+__global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
+    pt_round_body<kOmit>(a);
+}
+
+// Multi-root rounds: one launch runs the round of every
+// non-quiescent heartbeat lane, blockIdx.y = lane, each lane's arguments in
+// device memory -- the lanes' sparse rounds share the chip instead of
+// following each other launch by launch.
+template <bool kOmit>
+__global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __restrict__ args) {
+    pt_round_body<kOmit>(args[blockIdx.y]);
 }
 
 // ---------------------------------------------------------------------------
@@ -936,6 +950,15 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(pt_round_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     else
         hipLaunchKernelGGL(pt_round_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s) {
+    const dim3 grid(grid_chunks(a0.n), nlanes);
+    if (a0.omit)
+        hipLaunchKernelGGL(pt_round_lanes_kernel<true>, grid, dim3(kBlock), 0, s, d_args);
+    else
+        hipLaunchKernelGGL(pt_round_lanes_kernel<false>, grid, dim3(kBlock), 0, s, d_args);
     return hipGetLastError();
 }
 

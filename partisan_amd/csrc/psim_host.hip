@@ -53,6 +53,8 @@ struct psim_handle {
     } bin;
     unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
     unsigned long long* h_stats = nullptr;   // pinned mirror
+    psim::PtArgs* lane_args = nullptr;       // [kChunk][kMaxLanes] per-round lane arguments (device)
+    psim::PtArgs* h_lane_args = nullptr;     // pinned staging
     unsigned long long* scratch = nullptr;   // 1 counter
     int* ost_total = nullptr;                // device mirror of ost_cnt (the focused lane's)
     int* ost_total_base = nullptr;           // [kMaxLanes] allocation
@@ -473,6 +475,28 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             if (j == focus || !lane_quiescent(h->lanes[j])) act.push_back(j);
         const size_t A = act.size();
         HIPCHK(h, hipMemsetAsync(h->stats, 0, k * A * kStatsRow * sizeof(unsigned long long), h->stream));
+#ifndef PT_LANE_LAUNCHES
+        if (A > 1) {
+            // several lanes: one launch per round over all of them (blockIdx.y = lane)
+            for (uint32_t i = 0; i < k; i++) {
+                const uint32_t tick = ((h->round + i + 1) % L) == 0;
+                for (size_t q = 0; q < A; q++) {
+                    load_lane(h, act[q]);
+                    PtArgs a = make_args(h, h->par, tick, h->stats + (i * A + q) * kStatsRow);
+                    set_round_slots(h, a, h->round + i + 1);
+                    h->h_lane_args[i * A + q] = a;
+                    h->lanes[act[q]].par ^= 1u;
+                }
+            }
+            HIPCHK(h, hipMemcpyAsync(h->lane_args, h->h_lane_args, k * A * sizeof(PtArgs), hipMemcpyHostToDevice,
+                                     h->stream));
+            for (uint32_t i = 0; i < k; i++) {
+                HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+                HIPCHK(h, launch_pt_round_lanes(h->lane_args + i * A, h->h_lane_args[i * A], (uint32_t)A, h->stream));
+                HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
+            }
+        } else
+#endif
         for (uint32_t i = 0; i < k; i++) {
             const uint32_t tick = ((h->round + i + 1) % L) == 0;
             HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
@@ -617,6 +641,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
         if (hipMalloc(&h->stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess ||
+            hipHostMalloc(&h->h_lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->ost_total_base, kMaxLanes * 4 * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)) != hipSuccess ||
@@ -645,6 +671,8 @@ int psim_destroy(psim_handle* h) {
     }
     if (h->stats) (void)hipFree(h->stats);
     if (h->h_stats) (void)hipHostFree(h->h_stats);
+    if (h->lane_args) (void)hipFree(h->lane_args);
+    if (h->h_lane_args) (void)hipHostFree(h->h_lane_args);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->ost_total_base) (void)hipFree(h->ost_total_base);
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);

@@ -352,6 +352,8 @@ void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing to
 hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);   // binned when a.rec_c is set
+// one slot-scatter round for nlanes heartbeat lanes (d_args[0..nlanes) on device; a0 = d_args[0] on host)
+hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
                      uint8_t* outb, size_t n, hipStream_t s);
