@@ -114,6 +114,37 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
             const uint32_t cnt = np < kDmPushCap ? np : kDmPushCap;
             if (np > kDmPushCap) c.overflow |= 1u;
             const uint32_t* lst = a.pushlist_cur + (size_t)i * kDmPushCap;
+#ifndef DM_NO_FAST_AE
+            if (cnt <= kDmFastPush) {
+                // the usual case (Poisson(2) in-degree): the list in registers,
+                // sorted there, and every pusher's snapshot requested at once --
+                // one dependent round trip instead of one per pusher
+                uint32_t x[kDmFastPush];
+#pragma unroll
+                for (uint32_t j = 0; j < kDmFastPush; j++) x[j] = j < cnt ? lst[j] : 0xFFFFFFFFu;
+#pragma unroll
+                for (uint32_t j = 1; j < kDmFastPush; j++)          // sorting network over 8 lanes
+#pragma unroll
+                    for (uint32_t q = j; q > 0; q--) {
+                        const uint32_t lo = x[q - 1] < x[q] ? x[q - 1] : x[q];
+                        const uint32_t hi = x[q - 1] < x[q] ? x[q] : x[q - 1];
+                        x[q - 1] = lo;
+                        x[q] = hi;
+                    }
+                unsigned long long P[kDmFastPush];
+#pragma unroll
+                for (uint32_t j = 0; j < kDmFastPush; j++) P[j] = j < cnt ? a.snap[x[j]] : 0ull;
+#pragma unroll
+                for (uint32_t j = 0; j < kDmFastPush; j++) {
+                    if (j >= cnt) break;
+                    s |= P[j];
+                    const uint2 sp = sample2(a.key, x[j], a.prev_tick, KIND_AE, a.n_global);
+                    a.pull_nxt[2 * (size_t)x[j] + (sp.x == v ? 0u : 1u)] = s;   // {pull, MyNode, OurMessages}
+                    c.pull++;
+                }
+            } else
+#endif
+            {
             uint32_t last = 0;
             bool first = true;
             for (uint32_t k = 0; k < cnt; k++) {                     // senders in id order
@@ -130,6 +161,7 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
                 const uint32_t slot = sp.x == v ? 0u : 1u;
                 a.pull_nxt[2 * (size_t)best + slot] = s;             // {pull, MyNode, OurMessages}
                 c.pull++;
+            }
             }
         }
 

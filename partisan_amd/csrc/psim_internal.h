@@ -94,6 +94,7 @@ struct PtArgs {
 
 // Demers rumor mongering + anti-entropy (demers.hip)
 constexpr uint32_t kDmPushCap = 24;   // AE pushes one vertex can receive per tick (Poisson(2) in-degree)
+constexpr uint32_t kDmFastPush = 8;   // pushes handled in registers (the rest: the generic walk)
 struct DmArgs {
     uint32_t n, m;                        // n = vertices of this shard (all of them on one GPU)
     uint32_t v_lo, n_global;              // global id of local vertex 0; membership size
