@@ -426,7 +426,8 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 template <bool kOmit>
 __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     __shared__ uint16_t rep[kMaxDeg * kBlock];
-    __shared__ uint32_t cand[kChunkV];
+    __shared__ uint16_t cand[kChunkV];           // (vertex - base) << 2 | pend << 1 | due: 12 bits
+    static_assert(kChunkV == 4 * kBlock && (kChunkV << 2) <= 65536, "candidate encoding");
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
     if (a.msgs3) {
@@ -463,7 +464,7 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
         const uint32_t off = atomicAdd(&ncand, (uint32_t)__popc(m));
         uint32_t k = off;
         for (int i = 0; i < 4; i++)
-            if (m & (1u << i)) cand[k++] = ((v0 + i) << 2) | (((pmask >> i) & 1u) << 1) | ((dmask >> i) & 1u);
+            if (m & (1u << i)) cand[k++] = (uint16_t)(((4 * t + i) << 2) | (((pmask >> i) & 1u) << 1) | ((dmask >> i) & 1u));
     }
     __syncthreads();
     const uint32_t nc = ncand;
@@ -472,7 +473,7 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex<kOmit>(a, x >> 2, (x >> 1) & 1u, x & 1u, &rep[t], c);
+        pt_vertex<kOmit>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
     flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
 }
