@@ -105,6 +105,25 @@ def one_step(sim, root):
     return sim.run()
 
 
+def verify(sim, pg, n, rounds_per_step):
+    """After the timed region (outside it): the last step converged.  Every
+    vertex delivered the heartbeat (the reliable-broadcast postcondition,
+    test/prop_partisan_reliable_broadcast.erl:127-172), no outstanding i_have
+    row is left, and the eager links form a spanning tree: 2(n-1) directed
+    eager entries over all shards.  Every step ran the same number of rounds."""
+    import numpy as np
+    eager, _lazy, outst, _rr = sim.plumtree_state()
+    local = [int(sim.delivered().sum()), int(np.count_nonzero(outst)),
+             int(np.bitwise_count(eager).sum(dtype=np.int64))]
+    tot = [int(sum_over_ranks(pg, float(x))) for x in local]
+    ok = {"delivered": tot[0] == n, "no_outstanding": tot[1] == 0, "spanning_tree": tot[2] == 2 * (n - 1),
+          "same_rounds_every_step": len(set(rounds_per_step)) == 1}
+    if not all(ok.values()):
+        raise SystemExit(f"bench: the timed steps did not converge: {ok} (delivered {tot[0]} of {n}, "
+                         f"outstanding vertices {tot[1]}, eager entries {tot[2]}, rounds {rounds_per_step})")
+    return ok
+
+
 def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
@@ -203,6 +222,8 @@ def main():
     if sp is not None:   # this GPU's own bytes and launch times
         algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
 
+    verified = verify(sim, pg, args.n, rounds_per_step)
+
     step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
     n_units = args.n if sharded else args.n * world      # peers simulated by the whole job
     peer_rounds = float(n_units) * sum(rounds_per_step) / args.steps
@@ -242,6 +263,7 @@ def main():
                 "n_peers": args.n,
                 "overlay": f"random symmetric, {args.peers} peers per vertex (HyParView active view)",
                 "rounds_to_convergence": rounds_per_step[-1],
+                "verified_after_timing": verified,
                 "parallelism": (f"vertex-sharded x{world}, "
                                 + ("RCCL all-to-all over xGMI" if args.transport == "nccl" else "gloo host-staged")
                                 + " exchange per round" if sharded

@@ -105,9 +105,23 @@ static ERL_NIF_TERM nif_load_csr(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
     if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &rp) ||
         !enif_inspect_binary(env, argv[2], &col) || rp.size < 8 || rp.size % 8 || col.size % 4)
         return enif_make_badarg(env);
+    if (rp.size / 8 - 1 > 0xFFFFFFFFu) return enif_make_badarg(env);
     uint32_t n = (uint32_t)(rp.size / 8 - 1);
+    /* binary data carries no alignment guarantee: copy the row pointers
+     * (and ids) out; the library checks row_ptr against col's length */
+    uint64_t* rpa = (uint64_t*)enif_alloc(rp.size);
+    uint32_t* cola = (uint32_t*)enif_alloc(col.size ? col.size : 4);
+    if (!rpa || !cola) {
+        if (rpa) enif_free(rpa);
+        if (cola) enif_free(cola);
+        return err(env, PSIM_ENOMEM);
+    }
+    memcpy(rpa, rp.data, rp.size);
+    memcpy(cola, col.data, col.size);
     enif_mutex_lock(r->mu);
-    int rc = psim_load_csr(r->h, n, (const uint64_t*)rp.data, (const uint32_t*)col.data);
+    int rc = psim_load_csr(r->h, n, rpa, cola, col.size / 4);
+    enif_free(rpa);
+    enif_free(cola);
     if (rc == PSIM_OK) { r->n = n; psim_num_slots(r->h, &r->slots); }
     enif_mutex_unlock(r->mu);
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
@@ -322,10 +336,35 @@ static ERL_NIF_TERM nif_relay_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     unsigned char* fr = enif_make_new_binary(env, k * 4, &fr_t);
     if (!dv || !fr) return err(env, PSIM_ENOMEM);
     enif_mutex_lock(r->mu);
-    int64_t rc = psim_relay_run(r->h, (uint32_t)(al.size), (const uint64_t*)ap.data, (const uint32_t*)ac.data,
-                                (const uint64_t*)op.data, (const uint32_t*)ol.data, (const uint8_t*)al.data,
-                                (uint32_t)k, (const uint32_t*)s.data, (const uint32_t*)d.data, ttl,
-                                (uint64_t*)dv, (uint32_t*)fr, st, kCap, (size_t)maxc);
+    /* copies: binary data carries no alignment guarantee */
+    uint64_t* apc = (uint64_t*)enif_alloc(ap.size);
+    uint64_t* opc = (uint64_t*)enif_alloc(op.size);
+    uint32_t* acc = (uint32_t*)enif_alloc(ac.size + 4);
+    uint32_t* olc = (uint32_t*)enif_alloc(ol.size + 4);
+    uint32_t* sc = (uint32_t*)enif_alloc(s.size + 4);
+    uint32_t* dc = (uint32_t*)enif_alloc(d.size + 4);
+    int64_t rc = PSIM_ENOMEM;
+    if (apc && opc && acc && olc && sc && dc) {
+        memcpy(apc, ap.data, ap.size);
+        memcpy(opc, op.data, op.size);
+        memcpy(acc, ac.data, ac.size);
+        memcpy(olc, ol.data, ol.size);
+        memcpy(sc, s.data, s.size);
+        memcpy(dc, d.data, d.size);
+        uint64_t* dva = (uint64_t*)enif_alloc(k * 8 + 8);
+        uint32_t* fra = (uint32_t*)enif_alloc(k * 4 + 4);
+        if (dva && fra) {
+            rc = psim_relay_run(r->h, (uint32_t)(al.size), apc, acc, ac.size / 4, opc, olc, ol.size / 4,
+                                (const uint8_t*)al.data, (uint32_t)k, sc, dc, ttl, dva, fra, st, kCap, (size_t)maxc);
+            memcpy(dv, dva, k * 8);
+            memcpy(fr, fra, k * 4);
+        }
+        if (dva) enif_free(dva);
+        if (fra) enif_free(fra);
+    }
+    void* tmp[] = {apc, opc, acc, olc, sc, dc};
+    for (int i = 0; i < 6; i++)
+        if (tmp[i]) enif_free(tmp[i]);
     enif_mutex_unlock(r->mu);
     if (rc < 0) return err(env, (int)rc);
     ERL_NIF_TERM rows = enif_make_list(env, 0);

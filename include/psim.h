@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 1u
+#define PSIM_ABI_VERSION 2u   /* 2: psim_load_csr takes the col length */
 
 #define PSIM_OK         0
 #define PSIM_EINVAL    (-1)   /* bad argument / shape                        */
@@ -94,10 +94,13 @@ int  psim_device_info(const psim_handle* h, char* buf, size_t cap);
 /* --- overlay / membership ------------------------------------------- */
 /* Loads every vertex's membership list (the peer service's members minus
  * self: partisan_peer_service:members/0, consumed by start_link/0 :234-260)
- * as a CSR: row_ptr[n+1], col[row_ptr[n]].  Copied.  Plumtree's peers of v
+ * as a CSR: row_ptr[n+1], col[col_len].  Copied.  Plumtree's peers of v
  * are the union of v's members and of the vertices listing v (a message can
- * only arrive over such an edge); at most 32 per vertex. */
-int  psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col);
+ * only arrive over such an edge); at most 32 per vertex.  PSIM_EINVAL unless
+ * row_ptr[0] == 0, row_ptr is monotone, row_ptr[n] == col_len and every id
+ * is < n (nothing is read past col[col_len - 1]).  Neither array needs any
+ * alignment beyond its element type's. */
+int  psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col, uint64_t col_len);
 /* Number of peer slots (directed edges of the symmetrised overlay). */
 int  psim_num_slots(const psim_handle* h, uint64_t* out);
 /* The slot layout used by every per-vertex mask below: row_ptr[n+1], col[E]
@@ -496,7 +499,8 @@ int  psim_c3_get_plumtree(const psim_handle* h, uint32_t v, uint32_t* eager, siz
  * first_round[k] (arrival round, UINT32_MAX = never) and per-round stats
  * (up to cap rows).  Returns the rounds run, PSIM_EOVERFLOW when one round
  * holds more than max_copies copies, PSIM_EINVAL for bad shapes (src == dst,
- * ids >= n, relay_ttl 0 or > 127, k >= 2^24). */
+ * ids >= n, relay_ttl 0 or > 127, k >= 2^24, a CSR whose row pointers do not
+ * start at 0 and end at its id array's length act_len / ol_len). */
 typedef struct psim_relay_stats {
     uint64_t direct;    /* copies of Message sent to Node (connected)      */
     uint64_t relay;     /* relay_message copies sent                       */
@@ -504,8 +508,8 @@ typedef struct psim_relay_stats {
     uint64_t lost;      /* out-links not connected: the send fails         */
     uint64_t arrived;   /* copies of Message arriving at Node this round   */
 } psim_relay_stats;
-int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, const uint32_t* act,
-                       const uint64_t* ol_ptr, const uint32_t* ol, const uint8_t* alive, uint32_t k,
+int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, const uint32_t* act, uint64_t act_len,
+                       const uint64_t* ol_ptr, const uint32_t* ol, uint64_t ol_len, const uint8_t* alive, uint32_t k,
                        const uint32_t* src, const uint32_t* dst, uint32_t relay_ttl, uint64_t* delivered,
                        uint32_t* first_round, psim_relay_stats* stats, size_t cap, size_t max_copies);
 

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSIM_LIB_PATH") or os.path.join(HERE, "libpsim.so")   # override: kernel experiments
 
-PSIM_ABI_VERSION = 1
+PSIM_ABI_VERSION = 2
 PSIM_CFG_BINNED = 1   # psim_config.flags: binned Plumtree engine on one GPU
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EHIP", -4: "PSIM_ERCCL",
@@ -136,7 +136,7 @@ SIGNATURES = {
     "psim_strerror": (C.c_char_p, [C.c_int]),
     "psim_last_error": (C.c_char_p, [_H]),
     "psim_device_info": (C.c_int, [_H, C.c_char_p, C.c_size_t]),
-    "psim_load_csr": (C.c_int, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32)]),
+    "psim_load_csr": (C.c_int, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32), C.c_uint64]),
     "psim_num_slots": (C.c_int, [_H, _P(C.c_uint64)]),
     "psim_get_slots": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint32)]),
     "psim_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
@@ -229,8 +229,8 @@ SIGNATURES = {
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_vclock_increment": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
-    "psim_relay_run": (C.c_int64, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32),
-                                   _P(C.c_uint8), C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), C.c_uint32,
+    "psim_relay_run": (C.c_int64, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32), C.c_uint64, _P(C.c_uint64),
+                                   _P(C.c_uint32), C.c_uint64, _P(C.c_uint8), C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), C.c_uint32,
                                    _P(C.c_uint64), _P(C.c_uint32), _P(RelayStats), C.c_size_t, C.c_size_t]),
 }
 

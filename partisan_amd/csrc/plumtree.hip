@@ -32,18 +32,19 @@ __device__ __forceinline__ bool bit_alive(const uint32_t* __restrict__ alive, ui
 }
 
 // Per-thread counters.  Message kinds are packed 12 bits each into one
-// 64-bit word (a thread emits < 4096 messages per round) so that no counter
-// is indexed at run time (that would spill the array to scratch).
+// 64-bit word (a thread emits < 4096 messages per round: <= 4 candidate
+// vertices x 32 slots x 4 messages) so that no counter is indexed at run
+// time (that would spill the array to scratch).
 struct Ctr {
-    unsigned long long kinds;   // field t (t = 1..5) at bits [12t, 12t+12)
+    unsigned long long kinds;   // field t (t = 1..5) at bits [12(t-1), 12t): 60 bits, no field truncated
     uint32_t deliv, active, senders, degsum, ost_delta, live_delta, overflow;
     __device__ __forceinline__ void zero() {
         kinds = 0; deliv = active = senders = degsum = ost_delta = live_delta = overflow = 0;
     }
-    __device__ __forceinline__ void kind(uint32_t t) { kinds += 1ull << (12 * t); }
+    __device__ __forceinline__ void kind(uint32_t t) { kinds += 1ull << (12 * (t - 1)); }
     __device__ __forceinline__ unsigned long long get(int i) const {
         switch (i) {
-        case 1: case 2: case 3: case 4: case 5: return (kinds >> (12 * i)) & 0xFFFull;
+        case 1: case 2: case 3: case 4: case 5: return (kinds >> (12 * (i - 1))) & 0xFFFull;
         case S_DELIV: return deliv;
         case S_ACTIVE: return active;
         case S_SENDERS: return senders;

@@ -460,6 +460,13 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
     const int focus = h->cur_lane;
     save_lane(h);
+    // every return (HIP error paths included) leaves the handle focused on
+    // the lane it was focused on; lane fields are only changed in h->lanes
+    struct Refocus {
+        psim_handle* h;
+        int f;
+        ~Refocus() { load_lane(h, f); }
+    } refocus{h, focus};
     auto all_quiet = [&]() {
         for (const auto& l : h->lanes)
             if (!lane_quiescent(l)) return false;
@@ -474,19 +481,24 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         for (int j = 0; j < (int)h->lanes.size(); j++)
             if (j == focus || !lane_quiescent(h->lanes[j])) act.push_back(j);
         const size_t A = act.size();
+        // inbox parities advance on a copy, committed once every launch of the
+        // chunk is enqueued (a failed launch leaves the lanes' parities alone)
+        std::vector<uint32_t> par(A);
+        for (size_t q = 0; q < A; q++) par[q] = h->lanes[act[q]].par;
+        auto lane_args = [&](size_t q, uint32_t i, uint32_t tick) {
+            load_lane(h, act[q]);
+            PtArgs a = make_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
+            set_round_slots(h, a, h->round + i + 1);
+            par[q] ^= 1u;
+            return a;
+        };
         HIPCHK(h, hipMemsetAsync(h->stats, 0, k * A * kStatsRow * sizeof(unsigned long long), h->stream));
 #ifndef PT_LANE_LAUNCHES
         if (A > 1) {
             // several lanes: one launch per round over all of them (blockIdx.y = lane)
             for (uint32_t i = 0; i < k; i++) {
                 const uint32_t tick = ((h->round + i + 1) % L) == 0;
-                for (size_t q = 0; q < A; q++) {
-                    load_lane(h, act[q]);
-                    PtArgs a = make_args(h, h->par, tick, h->stats + (i * A + q) * kStatsRow);
-                    set_round_slots(h, a, h->round + i + 1);
-                    h->h_lane_args[i * A + q] = a;
-                    h->lanes[act[q]].par ^= 1u;
-                }
+                for (size_t q = 0; q < A; q++) h->h_lane_args[i * A + q] = lane_args(q, i, tick);
             }
             HIPCHK(h, hipMemcpyAsync(h->lane_args, h->h_lane_args, k * A * sizeof(PtArgs), hipMemcpyHostToDevice,
                                      h->stream));
@@ -500,15 +512,10 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         for (uint32_t i = 0; i < k; i++) {
             const uint32_t tick = ((h->round + i + 1) % L) == 0;
             HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-            for (size_t q = 0; q < A; q++) {
-                load_lane(h, act[q]);
-                PtArgs a = make_args(h, h->par, tick, h->stats + (i * A + q) * kStatsRow);
-                set_round_slots(h, a, h->round + i + 1);
-                HIPCHK(h, launch_pt_round(a, h->stream));
-                h->lanes[act[q]].par ^= 1u;
-            }
+            for (size_t q = 0; q < A; q++) HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
             HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
         }
+        for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -695,15 +702,19 @@ int psim_device_info(const psim_handle* h, char* buf, size_t cap) {
     return PSIM_OK;
 }
 
-int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col) {
-    if (!h || !row_ptr || (!col && row_ptr[n])) return PSIM_EINVAL;
+int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uint32_t* col, uint64_t col_len) {
+    if (!h || !row_ptr || (!col && col_len)) return PSIM_EINVAL;
+    if (row_ptr[0] != 0 || row_ptr[n] != col_len)
+        return fail(h, PSIM_EINVAL, "row_ptr[0]=%llu, row_ptr[n]=%llu, col_len=%llu", (unsigned long long)row_ptr[0],
+                    (unsigned long long)row_ptr[n], (unsigned long long)col_len);
+    for (uint32_t v = 0; v < n; v++)     // before any col access: every row lies inside col[0, col_len)
+        if (row_ptr[v + 1] < row_ptr[v]) return fail(h, PSIM_EINVAL, "row_ptr not monotone at %u", v);
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     free_graph(h);
     // symmetrise: peers(v) = members(v) U {u : v in members(u)}, minus self
     std::vector<uint64_t> cnt(size_t(n) + 1, 0);
     for (uint32_t v = 0; v < n; v++) {
-        if (row_ptr[v + 1] < row_ptr[v]) return fail(h, PSIM_EINVAL, "row_ptr not monotone at %u", v);
         for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
             const uint32_t u = col[e];
             if (u >= n) return fail(h, PSIM_EINVAL, "col[%llu]=%u >= n", (unsigned long long)e, u);

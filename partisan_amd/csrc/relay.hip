@@ -222,7 +222,8 @@ bool narrow(const uint64_t* p, uint32_t n, std::vector<uint32_t>& out) {
     } while (0)
 
 extern "C" int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, const uint32_t* act,
-                                  const uint64_t* ol_ptr, const uint32_t* ol, const uint8_t* alive, uint32_t k,
+                                  uint64_t act_len, const uint64_t* ol_ptr, const uint32_t* ol, uint64_t ol_len,
+                                  const uint8_t* alive, uint32_t k,
                                   const uint32_t* src, const uint32_t* dst, uint32_t relay_ttl,
                                   uint64_t* delivered, uint32_t* first_round, psim_relay_stats* stats,
                                   size_t cap, size_t max_copies) {
@@ -239,6 +240,9 @@ extern "C" int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* ac
     std::vector<uint32_t> ap, op;
     if (!narrow(act_ptr, n, ap) || !narrow(ol_ptr, n, op))
         return handle_fail(h, PSIM_EINVAL, "CSR offsets not monotone or >= 2^32");
+    if (ap[0] != 0 || ap[n] != act_len || op[0] != 0 || op[n] != ol_len || (act_len && !act) || (ol_len && !ol))
+        return handle_fail(h, PSIM_EINVAL, "CSR rows do not cover act[%llu] / ol[%llu] exactly",
+                           (unsigned long long)act_len, (unsigned long long)ol_len);
     const uint64_t na = ap[n], no = op[n];
     for (uint64_t i = 0; i < na; i++)
         if (act[i] >= n) return handle_fail(h, PSIM_EINVAL, "act[%llu] = %u >= n", (unsigned long long)i, act[i]);

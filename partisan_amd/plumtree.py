@@ -69,13 +69,19 @@ class PlumtreeBackend(PlumtreeBroadcastHandler):
         return ts, ts
 
     def is_stale(self, message_id):                       # backend :229-244
+        """Monotonic in this node's interval set for the origin: the latest
+        heartbeat's delivery is read from the device, an earlier one's from the
+        delivered set recorded when the origin heartbeated again (a heartbeat
+        runs to quiescence before its origin's next one: PSIM_EBUSY)."""
         origin, _epoch, mono = message_id
         c = self.cluster
-        if c.current_id is None or c.current_id[0] != origin:
+        cur = c.ids.get(origin)
+        if cur is None or mono > cur[2]:
             return False
-        if mono != c.current_id[2]:
-            return mono < c.current_id[2]
-        return bool(c.sim.delivered()[self.node])
+        if mono == cur[2]:
+            return bool(c._delivered(origin)[self.node])
+        past = c._hist.get(origin, {}).get(mono)   # recorded when the origin heartbeated again
+        return bool(past is not None and past[self.node])
 
     def merge(self, message_id, payload):                 # backend :205-215 (read-only view)
         return not self.is_stale(message_id)
@@ -106,25 +112,36 @@ class PlumtreeBroadcast:
         self.members_col = np.asarray(col, dtype=np.uint32)
         self.mods = mods
         self.current_id = None            # {Node, Epoch, Monotonic} of the latest heartbeat
-        self._state = None
+        self.ids = {}                     # origin -> its latest heartbeat id
+        self._hist = {}                   # origin -> {Monotonic: delivered set} of its earlier heartbeats
+        self._state = {}                  # root -> device state of its lane (cached until the next round)
+        # roots whose per-root sets the device keeps: every root on one GPU
+        # (heartbeat lanes); only the latest on a binned / sharded handle
+        self._one_lane = bool(getattr(self.sim, "binned", False)) or self.sim.world > 1
 
     # -- partisan_plumtree_broadcast API ------------------------------------
     def broadcast(self, node, mod=PlumtreeBackend):
         """Heartbeat at `node` (backend handle_info(heartbeat) :341-368 ->
         broadcast/2 :324-326).  Returns the message id."""
+        prev = self.ids.get(node)
+        if prev is not None:
+            self._hist.setdefault(node, {})[prev[2]] = self._delivered(node).astype(bool)
         mono = self.sim.broadcast(node)
+        if self._one_lane:
+            self.ids = {r: i for r, i in self.ids.items() if r == node}
         self.current_id = (node, 0, mono)
-        self._state = None
+        self.ids[node] = self.current_id
+        self._state = {}
         return self.current_id
 
     def run(self, max_rounds=100000):
         stats, rounds = self.sim.run(max_rounds)
-        self._state = None
+        self._state = {}
         return stats, rounds
 
     def step(self, rounds=1):
         st = self.sim.step(rounds)
-        self._state = None
+        self._state = {}
         return st
 
     def update(self, members_added=True):
@@ -132,15 +149,24 @@ class PlumtreeBroadcast:
         drops per-root sets (:607-639, :1320-1328)."""
         if members_added:
             self.sim.reset_trees()
-        self._state = None
+        self._state = {}
 
-    def _st(self):
-        if self._state is None:
-            self._state = self.sim.plumtree_state()
-        return self._state
+    def _st(self, root):
+        if root not in self._state:
+            self.sim.focus(root)
+            self._state[root] = (self.sim.plumtree_state(), self.sim.delivered())
+        return self._state[root]
+
+    def _delivered(self, root):
+        return self._st(root)[1]
 
     def get_peers(self, node, root):                       # :516-536
-        eager, lazy, _, _ = self._st()
+        """all_peers(Root, eager_sets, common_eagers) / (.., lazy_sets, common_lazys)
+        (:1278-1282): the root's map entries when the device holds a tree for
+        that root, else the common sets (members minus self, and [])."""
+        if root not in self.ids:
+            return [p for p in self.broadcast_members(node) if p != node], []
+        (eager, lazy, _, _), _ = self._st(root)
         return self.sim.mask_to_peers(node, eager[node]), self.sim.mask_to_peers(node, lazy[node])
 
     def get_eager_peers(self, node, root):                 # :538-542

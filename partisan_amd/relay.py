@@ -42,12 +42,14 @@ def relay_run(sim, act_ptr, act, ol_ptr, ol, alive, src, dst, relay_ttl=RELAY_TT
     n = len(ap) - 1
     if len(op) != n + 1 or len(al) != n or len(s) != len(d):
         raise ValueError("relay_run: shapes disagree")
+    if ap[0] != 0 or int(ap[-1]) != len(ai) or op[0] != 0 or int(op[-1]) != len(oi):
+        raise ValueError("relay_run: row pointers must start at 0 and end at the id array's length")
     k = len(s)
     dv = np.zeros(max(k, 1), dtype=np.uint64)
     fr = np.zeros(max(k, 1), dtype=np.uint32)
     st = (RelayStats * cap)()
-    r = lib().psim_relay_run(sim._h, n, _p(ap, C.c_uint64), _p(ai, C.c_uint32), _p(op, C.c_uint64),
-                             _p(oi, C.c_uint32), _p(al, C.c_uint8), k, _p(s, C.c_uint32), _p(d, C.c_uint32),
+    r = lib().psim_relay_run(sim._h, n, _p(ap, C.c_uint64), _p(ai, C.c_uint32), len(ai), _p(op, C.c_uint64),
+                             _p(oi, C.c_uint32), len(oi), _p(al, C.c_uint8), k, _p(s, C.c_uint32), _p(d, C.c_uint32),
                              relay_ttl, _p(dv, C.c_uint64), _p(fr, C.c_uint32), st, cap, max_copies)
     if r < 0:
         raise PsimError(int(r), lib().psim_last_error(sim._h).decode())

@@ -30,6 +30,7 @@ class Simulator:
         check(lib().psim_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.n = 0
+        self.binned = binned
         self.lazy_tick_rounds = lazy_tick_rounds
         self.rank, self.world = rank, world
         if world > 1:
@@ -63,7 +64,10 @@ class Simulator:
         """Membership lists (members minus self) as CSR; see psim_load_csr."""
         rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
         cc = np.ascontiguousarray(col, dtype=np.uint32)
-        self._c(lib().psim_load_csr(self._h, len(rp) - 1, _u64p(rp), _u32p(cc) if len(cc) else None))
+        if len(rp) < 1 or rp[0] != 0 or int(rp[-1]) != len(cc):
+            raise ValueError(f"CSR shape: row_ptr[0]={int(rp[0]) if len(rp) else None}, "
+                             f"row_ptr[n]={int(rp[-1]) if len(rp) else None}, len(col)={len(cc)}")
+        self._c(lib().psim_load_csr(self._h, len(rp) - 1, _u64p(rp), _u32p(cc) if len(cc) else None, len(cc)))
         v_lo, n_local, n_global = C.c_uint32(), C.c_uint32(), C.c_uint32()
         slot_base = C.c_uint64()
         self._c(lib().psim_shard_info(self._h, C.byref(v_lo), C.byref(n_local), C.byref(slot_base),

@@ -1,0 +1,245 @@
+"""Correctness at the sizes the numbers are quoted on (BASELINE.json configs,
+SURVEY 8(d)): the oracle finishes only up to ~1e5 peers in test time, so
+these runs check size-independent properties of the HIP path at full size,
+the reliable-broadcast postcondition of
+test/prop_partisan_reliable_broadcast.erl:127-172 (every node that was up
+receives the broadcast) among them.
+
+* bench.py's workload: a 10M-peer Plumtree flood from a fresh tree.
+* C4: 10M-peer Demers rumor mongering + anti-entropy on one GPU, and the
+  vertex-sharded engine (world 2 / 4, gloo, one GPU) at 1M against the
+  single-GPU run by digest.
+* C3: 1M-peer SCAMP v2 churn + Plumtree repair invariants.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from test_shard import run_world
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def popcount32(x):
+    x = x.astype(np.uint32)
+    c = np.zeros(x.shape, np.int64)
+    for i in range(32):
+        c += ((x >> np.uint32(i)) & np.uint32(1)).astype(np.int64)
+    return c
+
+
+def check_flood_tree(sim, root, stats, n):
+    """After one flood from a fresh tree on a static overlay: every vertex
+    delivered, no outstanding row, the eager links form a spanning tree
+    (2(n-1) directed eager entries, symmetric), every non-root vertex has
+    exactly one eager peer whose accepted Round is its own minus one (its
+    parent) and every other eager peer one more (its children)."""
+    assert sim.delivered().all()
+    eager, lazy, outst, rr = sim.plumtree_state()
+    assert not outst.any()
+    assert not (eager & lazy).any()
+    assert int(popcount32(eager).sum()) == 2 * (n - 1)
+    assert sum(s["delivered_new"] for s in stats) == n - 1
+    rp = sim.slot_row_ptr.astype(np.int64)
+    col = sim.slot_col.astype(np.int64)
+    deg = np.diff(rp)
+    owner = np.repeat(np.arange(n, dtype=np.int64), deg)
+    slot = np.arange(len(col), dtype=np.int64) - rp[owner]
+    is_e = ((eager[owner] >> slot.astype(np.uint32)) & 1).astype(bool)
+    hop = rr.astype(np.int64)
+    hop[root] = -1                                        # 0xFFFE: the root pushes Round 0
+    assert (hop[np.arange(n) != root] < 0xFFFE).all()
+    d = hop[col[is_e]] - hop[owner[is_e]]
+    assert (np.abs(d) == 1).all()
+    parents = np.bincount(owner[is_e][d == -1], minlength=n)
+    assert parents[root] == 0
+    assert (np.delete(parents, root) == 1).all()
+    # symmetric: u eager at v <=> v eager at u
+    key_fwd = np.sort(owner[is_e] * n + col[is_e])
+    key_rev = np.sort(col[is_e] * n + owner[is_e])
+    assert np.array_equal(key_fwd, key_rev)
+
+
+@pytest.mark.gpu
+def test_bench_config_10m_flood_converges():
+    """bench.py's step at its exact workload (10M peers, random 5-peer overlay,
+    seed 0x5EED0001, lazy tick every round, heartbeat from vertex 0 after
+    reset_peers): quiescent in 16 rounds with a spanning eager tree; then a
+    second heartbeat over the pruned tree delivers everywhere with one
+    broadcast per tree edge and nothing else."""
+    import partisan_amd as pa
+    n = 10_000_000
+    rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
+    sim = pa.Simulator(lazy_tick_rounds=1, device=0)
+    sim.load_overlay(rp, col)
+    del rp, col
+    sim.reset_trees()
+    sim.broadcast(0)
+    stats, rounds = sim.run()
+    assert rounds == 16, rounds
+    assert sum(s[k] for s in stats[-1:] for k in KINDS) == 0
+    check_flood_tree(sim, 0, stats, n)
+    sim.broadcast(0)
+    st2, r2 = sim.run()
+    assert sim.delivered().all()
+    assert sum(s["broadcast"] for s in st2) == n - 1
+    assert sum(s["prune"] + s["graft"] + s["i_have"] for s in st2) == 0
+    sim.close()
+
+
+@pytest.mark.gpu
+def test_bench_config_10m_engines_agree_per_round():
+    """The slot-scatter and binned engines at the bench size, round by round,
+    by psim_trace_hash (state digest, in-flight digest, delivered count)."""
+    import partisan_amd as pa
+    n = 10_000_000
+    rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
+    a = pa.Simulator(lazy_tick_rounds=1, device=0)
+    b = pa.Simulator(lazy_tick_rounds=1, device=0, binned=True)
+    a.load_overlay(rp, col)
+    b.load_overlay(rp, col)
+    del rp, col
+    for h in (a, b):
+        h.reset_trees()
+        h.broadcast(0)
+    rounds = 0
+    while True:
+        sa, sb = a.step(1)[0], b.step(1)[0]
+        rounds += 1
+        for k in KINDS + ("delivered_new", "active", "senders"):
+            assert sa[k] == sb[k], (rounds, k)
+        assert a.trace_hash() == b.trace_hash(), rounds
+        if sum(sa[k] for k in KINDS) == 0 or rounds > 40:
+            break
+    assert rounds == 17       # the 16 rounds of the flood + the silent one that shows quiescence
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_c4_10m_single_gpu():
+    """C4: 10M peers, 64 rumors from Philox origins, rumor
+    mongering fanout 2 + anti-entropy every 2 rounds: every vertex ends with
+    every rumor, each (vertex, rumor) pair is stored exactly once (the origins
+    start with theirs), in the 21 rounds profiles/r01/configs.jsonl records."""
+    import partisan_amd as pa
+    n, m = 10_000_000, 64
+    sim = pa.Simulator(seed=0x5EED0004, device=0)
+    dm = pa.demers.DemersEpidemic(sim, n, m, 2, True)
+    dm.broadcast()
+    st, rounds = dm.run(200)
+    assert st[-1]["complete"] == n
+    assert sum(s["delivered_new"] for s in st) == n * m - m
+    assert rounds == 21, rounds
+    assert (dm.seen() == M64).all()
+    sim.close()
+
+
+def _digest(seen, v_lo):
+    """sum over vertices of splitmix64(global id, store) mod 2^64 (shards add up)."""
+    with np.errstate(over="ignore"):
+        z = (np.arange(len(seen), dtype=np.uint64) + np.uint64(v_lo)) * np.uint64(0x9E3779B97F4A7C15)
+        z ^= seen.astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+        return int(z.sum(dtype=np.uint64))
+
+
+def _demers_shard_worker(rank, world, port, n, m, q):
+    try:
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from partisan_amd.demers import ShardedDemers
+        sd = ShardedDemers(n, m, rank, world, device=0, backend="gloo", ae_period=2, rumor_mongering=True,
+                           seed=0x5EED0004)
+        sd.broadcast()
+        st, rounds = sd.run(200)
+        res = (_digest(sd.seen(), sd.v_lo), rounds, [s["delivered_new"] for s in st], st[-1]["complete"])
+        sd.close()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_c4_sharded_1m_matches_single_gpu(world):
+    """C4's vertex-sharded engine at 1M peers (world processes on one GPU,
+    gloo transport): the union of the shards' stores equals the single-GPU
+    run's (digest), round count and per-round new deliveries too."""
+    import partisan_amd as pa
+    n, m = 1_000_000, 64
+    sim = pa.Simulator(seed=0x5EED0004, device=0)
+    dm = pa.demers.DemersEpidemic(sim, n, m, 2, True)
+    dm.broadcast()
+    st, rounds = dm.run(200)
+    want = _digest(dm.seen(), 0)
+    want_new = [s["delivered_new"] for s in st]
+    sim.close()
+    res = run_world(_demers_shard_worker, world, n, m, timeout=300)
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+    got = sum(res[r][0] for r in range(world)) % (1 << 64)
+    assert got == want
+    for r in range(world):
+        assert res[r][1] == rounds
+        assert res[r][2] == want_new          # run() returns global (all-reduced) stats
+        assert res[r][3] == n
+
+
+@pytest.mark.gpu
+def test_c3_1m_invariants():
+    """C3 at 1M: join waves, a heartbeat, 5 % crash/rejoin churn per round.
+    Per live vertex (20k sampled): eager and lazy disjoint and without self,
+    every outstanding row's peer a current SCAMP member (neighbors_down drops
+    removed members' rows, :910-951).  Note: eager U lazy is NOT a subset of
+    the current SCAMP view in the reference composition -- Plumtree's
+    all_members only move on {update, Members} casts, which periodic/1 never
+    fires (6706 of 40000 vertex-rounds on the oracle at n = 2000), so that is
+    not asserted.  The heartbeat reaches most live vertices."""
+    import partisan_amd as pa
+    from test_scamp import churn, waves
+    n = 1_000_000
+    sim = pa.Simulator(device=0, seed=0x5EED0003)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=10)
+    for v, cc in waves(n):
+        g.join(v, cc)
+        g.step(3)
+    g.step(5)
+    g.heartbeat(0)
+    st = g.step(10)
+    reach = st[-1]["delivered_live"] / st[-1]["live"]
+    for i in range(10):
+        v, cc = churn(n, i)
+        keep = v != 0
+        g.crash(v[keep])
+        g.join(v[keep], cc[keep])
+        st += g.step(1)
+    assert all(x["live"] > 0.99 * n for x in st)
+    assert reach > 0.5, reach
+    pv, npv, _, _ = g.scamp.views()
+    _, _, alive = g.scamp.nodes()
+    rng = np.random.default_rng(3)
+    checked = 0
+    for v in rng.choice(n, 20000, replace=False).tolist():
+        if not alive[v]:
+            continue
+        e, lz, rows, _, _ = g.plumtree(v)
+        mem = set(pv[v, :npv[v]].tolist())
+        assert not (set(e) & set(lz)), v
+        assert v not in e and v not in lz, v
+        assert set(rows) <= mem, v
+        checked += 1
+    assert checked > 19000
+    print(f"C3 1M: heartbeat reached {reach:.3f} of live vertices 9 rounds after it")
+    sim.close()

@@ -428,3 +428,66 @@ def test_multi_root_lane_reuse():
     with pytest.raises(pa.PsimError):
         sim.focus(0)                 # evicted
     sim.close()
+
+
+def test_graft_storm_counts_every_graft(psim):
+    """One vertex answers >= 16 i_haves with grafts in one round (ADVICE r1:
+    the per-thread kind counters once kept the graft count mod 16).  Complete
+    graph of 33 nodes (32 peers each, the slot limit): after two heartbeats
+    every non-root link is lazy; the third heartbeat's messages INTO vertex 17
+    are omitted, then healed, so at the next lazy tick all 31 lazy peers'
+    i_have reach 17 in the same round and it grafts each of them."""
+    n, V = 33, 17
+    rp, col = psim.overlay.complete(n)
+    sim, orc = make(psim, rp, col, 1)
+    for _ in range(2):
+        m = sim.broadcast(0)
+        orc.heartbeat(0)
+        lockstep(sim, orc, 0, m)
+    pairs = [(u, V) for u in range(n) if u != V]
+    sim.set_omissions(pairs)
+    orc.set_omissions(pairs)
+    sim.broadcast(0)
+    mono = orc.heartbeat(0)
+    _omit_step(sim, orc, 0, mono, 3)
+    sim.set_omissions([])
+    orc.set_omissions([])
+    grafts = []
+    for _ in range(10):
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (k, gs, os_)
+        compare(sim, orc, 0, mono)
+        grafts.append(gs["graft"])
+    assert max(grafts) >= 16, grafts
+    assert sim.delivered().all()
+
+
+def test_facade_get_peers_per_root():
+    """PlumtreeBroadcast.get_peers(Node, Root) answers for Root's tree
+    (all_peers/3 :1278-1282), not the last broadcast one; a root that never
+    broadcast has no map entry: the common sets (members -- self, [])."""
+    import partisan_amd as pa
+    rp, col = pa.overlay.random_regular(400, 5, 141)
+    pt = pa.PlumtreeBroadcast(rp, col)
+    orc = O.Plumtree(rp, col, 1)
+    ids = {}
+    for root in (3, 250):
+        ids[root] = pt.broadcast(root)
+        orc.heartbeat(root)
+        pt.run()
+        orc.run()
+    for root in (3, 250):
+        for v in (0, 3, 99, 250, 399):
+            assert pt.get_peers(v, root) == orc.peers(v, root), (root, v)
+            assert pt.handler(v).is_stale(ids[root])
+    for v in (0, 99):
+        assert pt.get_peers(v, 7) == orc.peers(v, 7)       # never broadcast
+    first = ids[3]
+    ids[3] = pt.broadcast(3)
+    orc.heartbeat(3)
+    pt.run()
+    orc.run()
+    assert pt.handler(99).is_stale(first) and pt.handler(99).is_stale(ids[3])
+    assert not pt.handler(99).is_stale((3, 0, ids[3][2] + 1))
+    pt.close()
