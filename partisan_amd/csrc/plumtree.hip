@@ -6,10 +6,11 @@
 //   * one thread per vertex, grid-stride; a vertex is visited when its inbox
 //     flag is set or when the lazy tick fires and it holds outstanding rows;
 //   * the inbox of v is one 32-bit word per peer slot of v: a FIFO of up to
-//     four 4-bit message kinds plus the 16-bit Round carried by broadcast /
-//     i_have.  Each word is written by exactly one sender per round, so there
-//     are no atomics on the data path and the result never depends on
-//     arrival order;
+//     four 3-bit message kinds, the reading round's tag and the 12-bit Round
+//     carried by broadcast / i_have (psim_internal.h).  Each word is written
+//     by exactly one sender per round, so there are no atomics on the data
+//     path and the result never depends on arrival order; a consumed word is
+//     left in place (its tag goes stale), so a message costs one store;
 //   * slots are sorted by peer id, so walking them in order IS the schedule's
 //     (src id, src emission seq) order; per-slot FIFO order is the sender's
 //     emission order;
@@ -21,6 +22,7 @@
 //   * counters are reduced per wave with shuffles, per workgroup in LDS, and
 //     added to one of 64 shards so atomics never pile onto one address.
 #include "psim_internal.h"
+#include <algorithm>
 #include "../../include/psim.h"
 
 namespace psim {
@@ -107,9 +109,9 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
 template <bool kCount>
 __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_t f, Ctr& c) {
     while (f) {
-        const uint32_t t = f & 0xFu;
-        f >>= 4;
-        if (n < 4) fifo |= t << (4 * n);
+        const uint32_t t = f & 7u;
+        f >>= kKindBits;
+        if (n < 4) fifo |= t << (kKindBits * n);
         else if (kCount) c.overflow |= 1u;
         n++;
         if (kCount) c.kind(t);
@@ -171,12 +173,12 @@ __device__ __forceinline__ void vst_load(const PtArgs& a, uint32_t v, const uint
 // row starts at rs); returns the FIFO of replies sent back over s.
 __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32_t s, uint32_t w, VSt& x, Ctr& c) {
     const uint32_t b = 1u << s;
-    uint32_t f = w & 0xFFFFu;
-    const uint32_t rnd = w >> 16;
+    uint32_t f = w & kFifoMask;
+    const uint32_t rnd = w >> kRoundShift;
     uint32_t r = 0, rn = 0;
     while (f) {
-        const uint32_t t = f & 0xFu;
-        f >>= 4;
+        const uint32_t t = f & 7u;
+        f >>= kKindBits;
         uint32_t reply = 0;
         switch (t) {
         case PSIM_MSG_BROADCAST:           // handle_cast :571-578
@@ -184,7 +186,7 @@ __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32
                 x.rcv = true;
                 x.rseq = a.mono8;
                 x.myround = rnd + 1;
-                if (x.myround > 0xFFFFu) { c.overflow |= 2u; x.myround = 0xFFFFu; }
+                if (x.myround > kMaxRound) { c.overflow |= 2u; x.myround = kMaxRound; }
                 c.deliv++;
                 x.eager |= b;              // add_eager(From, Root)
                 x.lazy &= ~b;
@@ -236,7 +238,7 @@ __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32
             break;
         }
         if (reply) {
-            if (rn < 4) r |= reply << (4 * rn);
+            if (rn < 4) r |= reply << (kKindBits * rn);
             else c.overflow |= 1u;
             rn++;
         }
@@ -262,7 +264,8 @@ __device__ __forceinline__ uint32_t pt_ihave(const PtArgs& a, uint32_t rs, const
 // messages and the eager push -- before them when s comes after the slot
 // that delivered the heartbeat, after them otherwise -- then the i_have.
 template <bool kCount>
-__device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x, uint32_t ihave, Ctr& c) {
+__device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x, uint32_t ihave, uint32_t wtag,
+                                           Ctr& c) {
     const uint32_t b = 1u << s;
     if (!r && !((x.push_mask | ihave) & b)) return 0u;
     uint32_t fifo = 0, n = 0;
@@ -271,7 +274,7 @@ __device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x,
     fifo_append<kCount>(fifo, n, r, c);
     if (p && s < x.push_pos) fifo_append<kCount>(fifo, n, PSIM_MSG_BROADCAST, c);
     if (ihave & b) fifo_append<kCount>(fifo, n, PSIM_MSG_IHAVE, c);
-    return fifo | (x.myround << 16);
+    return fifo | (wtag << kTagShift) | (x.myround << kRoundShift);
 }
 
 // Write back the state record and the outstanding flag; returns the change
@@ -309,6 +312,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 #pragma unroll
     for (uint32_t s = 0; s < kFastDeg; s++) {
         w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
+        if (!live_word(w[s], a.ctag)) w[s] = 0u;       // stale: consumed in an earlier round
         any |= w[s];
     }
     pend = any != 0;
@@ -321,9 +325,6 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
         cl[s] = s < deg ? a.col[rs + s] : 0u;
         rv[s] = s < deg ? a.rev[rs + s] : 0u;
     }
-#pragma unroll
-    for (uint32_t s = 0; s < kFastDeg; s++)
-        if (w[s]) a.in_cur[rs + s] = 0;
     if (!((aw >> ((a.v_lo + v) & 31)) & 1u)) return;   // a dead vertex receives nothing
     c.active++;
     VSt x;
@@ -341,7 +342,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 #pragma unroll
     for (uint32_t s = 0; s < kFastDeg; s++) {
         if (s >= deg) break;
-        const uint32_t wo = pt_out<true>(s, r[s], x, ihave, c);
+        const uint32_t wo = pt_out<true>(s, r[s], x, ihave, a.wtag, c);
         if (!wo) continue;
         sent = true;
         if (kOmit && omitted(a, rs + s)) continue;
@@ -376,18 +377,12 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     }
 #endif
     if (pend) {
-        uint32_t any = 0;
-        for (uint32_t s = 0; s < deg; s++) any |= a.in_cur[rs + s];
-        pend = any != 0;
+        bool any = false;
+        for (uint32_t s = 0; s < deg; s++) any |= live_word(a.in_cur[rs + s], a.ctag);
+        pend = any;
     }
     if (!pend && !due) return;
-    if (!bit_alive(a.alive, a.v_lo + v)) {
-        // a dead vertex receives nothing: the words are dropped (cleared)
-        if (pend)
-            for (uint32_t s = 0; s < deg; s++)
-                if (a.in_cur[rs + s]) a.in_cur[rs + s] = 0;
-        return;
-    }
+    if (!bit_alive(a.alive, a.v_lo + v)) return;   // a dead vertex receives nothing: its words go stale
     c.active++;
     const uint4 st = a.vs[v];
     VSt x;
@@ -396,17 +391,14 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
         for (uint32_t s = 0; s < deg; s++) {
             const uint32_t w = a.in_cur[rs + s];
             uint32_t r = 0;
-            if (w) {
-                a.in_cur[rs + s] = 0;
-                r = pt_word(a, rs, s, w, x, c);
-            }
+            if (live_word(w, a.ctag)) r = pt_word(a, rs, s, w, x, c);
             rep[s * kBlock] = (uint16_t)r;
         }
     }
     const uint32_t ihave = pt_ihave(a, rs, x);
     bool sent = false;
     for (uint32_t s = 0; s < deg; s++) {
-        const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, c);
+        const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
         deliver_word<kOmit>(a, rs + s, w);
         sent = true;
@@ -669,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
             if (!send[k]) continue;
             const uint32_t ls = rpc[lvk[k]], deg = rpc[lvk[k] + 1] - ls, rs = sb + ls;
             for (uint32_t s = 0; s < deg; s++)
-                if (pt_out<false>(s, words[ls + s], x[k], ihave[k], c) && !omitted(a, rs + s))
+                if (pt_out<false>(s, words[ls + s], x[k], ihave[k], a.wtag, c) && !omitted(a, rs + s))
                     atomicAdd(&hist[a.col[rs + s] >> a.cv_shift], 1u);
         }
         __syncthreads();
@@ -688,7 +680,7 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
             const uint32_t ls = rpc[lvk[k]], deg = rpc[lvk[k] + 1] - ls, rs = sb + ls;
             bool sent = false;
             for (uint32_t s = 0; s < deg; s++) {
-                const uint32_t w = pt_out<true>(s, words[ls + s], x[k], ihave[k], c);
+                const uint32_t w = pt_out<true>(s, words[ls + s], x[k], ihave[k], a.wtag, c);
                 if (!w) continue;
                 sent = true;
                 if (omitted(a, rs + s)) continue;
@@ -731,9 +723,10 @@ __global__ void pt_origin_kernel(PtArgs a) {
                 // sent and lost
             } else if (a.rec_c) {                    // binned: a record for the next route
                 const uint32_t cs = (a.col[e] >> a.cv_shift) * kCoarseShards + ((v >> a.fv_shift) & (kCoarseShards - 1));
-                a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] = make_uint2(a.rev[e], PSIM_MSG_BROADCAST);
+                a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] =
+                    make_uint2(a.rev[e], PSIM_MSG_BROADCAST | (a.wtag << kTagShift));
             } else {
-                deliver_word(a, e, PSIM_MSG_BROADCAST);  // Round 0
+                deliver_word(a, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift));  // Round 0
             }
             nmsg++;
         }
@@ -811,7 +804,7 @@ __global__ __launch_bounds__(kBlock) void pt_hash_words_kernel(PtArgs a, unsigne
     const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
     for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < E; i += stride) {
         const uint32_t w = a.in_cur[i];
-        if (w) sum += mix64(((a.slot_base + i) << 32) | w);
+        if (live_word(w, a.ctag)) sum += mix64(((a.slot_base + i) << 32) | abi_word(w));
     }
     sum = wave_sum(sum);
     if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&out[1], sum);
@@ -824,7 +817,7 @@ __global__ __launch_bounds__(kBlock) void pb_hash_records_kernel(PtArgs a, unsig
         const uint32_t k = a.cnt_c_cur[cs], b = a.csub[cs];
         for (uint32_t i = threadIdx.x; i < k; i += kBlock) {
             const uint2 r = a.rec_c[b + i];
-            sum += mix64(((unsigned long long)r.x << 32) | r.y);
+            sum += mix64(((unsigned long long)r.x << 32) | abi_word(r.y));
         }
     }
     sum = wave_sum(sum);
@@ -842,6 +835,24 @@ __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
         st.w = (st.w & 0xFFFFu) | (rseq << 16) | (ep << 24);
         a.vs[v] = st;
     }
+}
+
+// Zero inbox words whose round tag is not `keep` (stale ones, before a tag
+// could repeat): one pass over a buffer every <= 256 rounds.
+__global__ __launch_bounds__(kBlock) void pt_scrub_kernel(uint4* __restrict__ w, unsigned long long n4, uint32_t keep) {
+    const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+    for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+        uint4 x = w[i];
+        const uint4 y = make_uint4(word_tag(x.x) == keep ? x.x : 0u, word_tag(x.y) == keep ? x.y : 0u,
+                                   word_tag(x.z) == keep ? x.z : 0u, word_tag(x.w) == keep ? x.w : 0u);
+        if (y.x != x.x || y.y != x.y || y.z != x.z || y.w != x.w) w[i] = y;
+    }
+}
+
+__global__ void pt_scrub_tail_kernel(uint32_t* __restrict__ w, unsigned long long lo, unsigned long long n,
+                                     uint32_t keep) {
+    const unsigned long long i = lo + threadIdx.x;
+    if (i < n && word_tag(w[i]) != keep) w[i] = 0u;
 }
 
 // Pack the staged cross-shard words into (global receiver slot, word)
@@ -1008,6 +1019,18 @@ hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_lo
         hipLaunchKernelGGL(pb_hash_records_kernel, dim3(1024), dim3(kBlock), 0, s, a, out);
     else if (E)
         hipLaunchKernelGGL(pt_hash_words_kernel, dim3(2048), dim3(kBlock), 0, s, a, E, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, hipStream_t s) {
+    if (!words || !n) return hipSuccess;
+    const unsigned long long n4 = n / 4;    // hipMalloc'd buffers: 16-byte aligned
+    if (n4) {
+        const unsigned long long g = std::min<unsigned long long>((n4 + kBlock - 1) / kBlock, 8192ull);
+        hipLaunchKernelGGL(pt_scrub_kernel, dim3((uint32_t)g), dim3(kBlock), 0, s, reinterpret_cast<uint4*>(words),
+                           n4, keep);
+    }
+    if (n % 4) hipLaunchKernelGGL(pt_scrub_tail_kernel, dim3(1), dim3(64), 0, s, words, n4 * 4, (unsigned long long)n, keep);
     return hipGetLastError();
 }
 

@@ -62,6 +62,7 @@ struct psim_handle {
 
     uint32_t par = 0;          // inbox buffer the next round reads
     uint64_t round = 0;        // rounds completed (lazy-tick schedule)
+    uint64_t scrub = 0;        // round at which the focused lane's inbox held no word older than it
     uint32_t serial = 0;       // heartbeat serial (device tag, low 8 bits)
     uint32_t epoch = 1;        // tree epoch (device tag, low 8 bits)
     uint32_t root = 0;
@@ -87,7 +88,7 @@ struct psim_handle {
         uint32_t par = 0, serial = 0, root = 0;
         bool have_root = false;
         int64_t ost_cnt = 0, live_rows = 0;
-        uint64_t inflight = 0, last_use = 0;
+        uint64_t inflight = 0, last_use = 0, scrub = 0;
     };
     std::vector<Lane> lanes;
     int cur_lane = 0;
@@ -283,6 +284,8 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.ost_total = h->ost_total;
     a.stats = stats;
     a.tick = tick;
+    a.ctag = uint32_t(h->round + 1) & 0xFFu;   // the next round to run reads these words ...
+    a.wtag = uint32_t(h->round + 2) & 0xFFu;   // ... and writes words for the one after it
     a.mono8 = h->serial & 0xFFu;
     a.epoch8 = h->epoch & 0xFFu;
     a.root = h->root;
@@ -319,18 +322,41 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     a.mnext = (r + 1) % 3;
 }
 
+// Round tags (psim_internal.h): a slot-scatter inbox word carries the round
+// that reads it, mod 256, and consumed words stay in place.  Before a lane
+// runs round `last`, every word older than 256 rounds must be gone, or its
+// tag could alias: zero every word not tagged for the next round (both
+// buffers; the in-flight words of round h->round + 1 are kept).
+void set_round_tags(PtArgs& a, uint64_t R) {
+    a.ctag = uint32_t(R) & 0xFFu;
+    a.wtag = uint32_t(R + 1) & 0xFFu;
+}
+
+hipError_t scrub_if_needed(psim_handle* h, uint64_t last) {
+    if (h->bin.rec_c || last <= h->scrub + kTagSpan) return hipSuccess;
+    const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
+    for (int b = 0; b < 2; b++) {
+        const hipError_t e = launch_pt_scrub(h->in[b], h->E, keep, h->stream);
+        if (e != hipSuccess) return e;
+    }
+    h->scrub = h->round;
+    return hipSuccess;
+}
+
 // ---- heartbeat-root lanes ------------------------------------------------
 void save_lane(psim_handle* h) {
     auto& l = h->lanes[h->cur_lane];
     l.vs = h->vs; l.in[0] = h->in[0]; l.in[1] = h->in[1]; l.pend[0] = h->pend[0]; l.pend[1] = h->pend[1];
     l.ost = h->ost; l.ost_total = h->ost_total; l.par = h->par; l.serial = h->serial; l.root = h->root;
     l.have_root = h->have_root; l.ost_cnt = h->ost_cnt; l.live_rows = h->live_rows; l.inflight = h->inflight;
+    l.scrub = h->scrub;
 }
 void load_lane(psim_handle* h, int j) {
     const auto& l = h->lanes[j];
     h->vs = l.vs; h->in[0] = l.in[0]; h->in[1] = l.in[1]; h->pend[0] = l.pend[0]; h->pend[1] = l.pend[1];
     h->ost = l.ost; h->ost_total = l.ost_total; h->par = l.par; h->serial = l.serial; h->root = l.root;
     h->have_root = l.have_root; h->ost_cnt = l.ost_cnt; h->live_rows = l.live_rows; h->inflight = l.inflight;
+    h->scrub = l.scrub;
     h->cur_lane = j;
 }
 void swap_lane(psim_handle* h, int j) {
@@ -440,6 +466,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         l.have_root = false;
         l.ost_cnt = l.live_rows = 0;
         l.inflight = 0;
+        l.scrub = h->round;
         load_lane(h, pick);
         PtArgs a = make_args(h, h->par, 0, h->stats);   // tags that match no serial / epoch
         HIPCHK(h, launch_pt_renorm(a, h->stream));
@@ -484,11 +511,17 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         // inbox parities advance on a copy, committed once every launch of the
         // chunk is enqueued (a failed launch leaves the lanes' parities alone)
         std::vector<uint32_t> par(A);
-        for (size_t q = 0; q < A; q++) par[q] = h->lanes[act[q]].par;
+        for (size_t q = 0; q < A; q++) {
+            par[q] = h->lanes[act[q]].par;
+            load_lane(h, act[q]);
+            HIPCHK(h, scrub_if_needed(h, h->round + k));
+            h->lanes[act[q]].scrub = h->scrub;
+        }
         auto lane_args = [&](size_t q, uint32_t i, uint32_t tick) {
             load_lane(h, act[q]);
             PtArgs a = make_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
             set_round_slots(h, a, h->round + i + 1);
+            set_round_tags(a, h->round + i + 1);
             par[q] ^= 1u;
             return a;
         };
@@ -924,6 +957,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->h_memb = std::move(mbl);
     h->par = 0;
     h->round = 0;
+    h->scrub = 0;
     h->serial = 0;
     h->epoch = 1;
     h->have_root = false;
@@ -1017,6 +1051,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         // origin emits into the buffer the next round reads
         PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
         set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
+        a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
         a.root = lr;
         HIPCHK(h, launch_pt_origin(a, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),
@@ -1103,6 +1138,7 @@ int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t
     HIPCHK(h, hipSetDevice(h->device));
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
     const uint32_t tick = ((h->round + 1) % L) == 0;
+    HIPCHK(h, scrub_if_needed(h, h->round + 1));
     HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, h->stats);
     HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
@@ -1179,6 +1215,7 @@ int psim_shard_round_async(psim_handle* h, void* send_dev) {
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
     const uint32_t tick = ((h->round + 1) % L) == 0;
     unsigned long long* row = sh.ring + size_t(sh.pending) * kStatsRow;
+    HIPCHK(h, scrub_if_needed(h, h->round + 1));
     HIPCHK(h, hipMemsetAsync(row, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, row);
     HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
@@ -1319,6 +1356,8 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     HIPCHK(hh, hipStreamSynchronize(h->stream));
     if (!h->bin.rec_c) {
         HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
+        const uint32_t tag = uint32_t(h->round + 1) & 0xFFu;   // words the next round reads
+        for (uint64_t i = 0; i < h->E; i++) words[i] = live_word(words[i], tag) ? abi_word(words[i]) : 0u;
         return PSIM_OK;
     }
     // binned: the records waiting in the coarse bins the next round routes
@@ -1333,7 +1372,7 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
         for (uint32_t i = 0; i < cnt[c]; i++) {
             const uint2 r = rec[size_t(b.h_csub[c]) + i];
             if (r.x >= h->E) return fail(hh, PSIM_ESTATE, "corrupt in-flight record");
-            words[r.x] = r.y;
+            words[r.x] = abi_word(r.y);
         }
     return PSIM_OK;
 }

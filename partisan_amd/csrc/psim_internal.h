@@ -46,8 +46,30 @@ enum Stat : int {
     S_DEGSUM = 9,       // sum of deg over senders
     S_OST_DELTA = 10,   // change in #vertices with outstanding rows (two's complement)
     S_LIVE_DELTA = 11,  // change in #outstanding rows to live peers (two's complement)
-    S_OVERFLOW = 12,    // bit0: per-edge FIFO > 4 ; bit1: Round > 0xFFFF ; bit2: rows of an older heartbeat
+    S_OVERFLOW = 12,    // bit0: per-edge FIFO > 4 ; bit1: Round > 4095 ; bit2: rows of an older heartbeat
 };
+
+// Slot-scatter inbox word (one per receiver slot):
+//   [11:0]  FIFO of <= 4 message kinds, 3 bits each (PSIM_MSG_*, first in the low bits)
+//   [19:12] round tag: the round that reads the word, mod 256 -- consumed words
+//           are never cleared; a word whose tag is not the reading round's is
+//           stale (buffers are zeroed once at least every 256 rounds)
+//   [31:20] Round carried by broadcast / i_have (< 4096)
+// The ABI form (psim_get_inflight) is 4-bit kinds in [15:0], Round in [31:16].
+constexpr uint32_t kKindBits = 3;
+constexpr uint32_t kFifoMask = 0xFFFu;
+constexpr uint32_t kTagShift = 12;
+constexpr uint32_t kRoundShift = 20;
+constexpr uint32_t kMaxRound = 0xFFFu;
+constexpr uint32_t kTagSpan = 256;     // rounds before a tag repeats
+__host__ __device__ inline uint32_t word_tag(uint32_t w) { return (w >> kTagShift) & 0xFFu; }
+// a word carries messages for the round whose tag is `tag`
+__host__ __device__ inline bool live_word(uint32_t w, uint32_t tag) { return (w & kFifoMask) && word_tag(w) == tag; }
+__host__ __device__ inline uint32_t abi_word(uint32_t w) {   // inbox word -> psim_get_inflight form
+    uint32_t f = w & kFifoMask, o = 0;
+    for (uint32_t i = 0; f; i++, f >>= kKindBits) o |= (f & 7u) << (4 * i);
+    return o | ((w >> kRoundShift) << 16);
+}
 
 // Per-vertex Plumtree state, one 16-byte record (one dwordx4 load):
 //   x = eager mask, y = lazy mask, z = outstanding mask (bits = slots)
@@ -78,6 +100,7 @@ struct PtArgs {
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
     uint32_t epoch8;                       // current tree epoch (low 8 bits)
     uint32_t root;                         // local index of the current heartbeat's origin
+    uint32_t ctag, wtag;                   // round tags of the words read / written this round
     const uint32_t* __restrict__ omit;     // [ceil(E/32)] omission faults over sender slots, or null
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}
@@ -361,6 +384,8 @@ hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_
 hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
+// zero every inbox word whose round tag is not `keep` (psim_internal.h word format)
+hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, hipStream_t s);
 hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_local, unsigned long long E,
                           unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,

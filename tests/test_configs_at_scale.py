@@ -83,11 +83,17 @@ def test_bench_config_10m_flood_converges():
     assert rounds == 16, rounds
     assert sum(s[k] for s in stats[-1:] for k in KINDS) == 0
     check_flood_tree(sim, 0, stats, n)
-    sim.broadcast(0)
+    eager, lazy = sim.plumtree_state()[:2]
+    root_children = int(np.bitwise_count(eager[0]))
+    lazy_links = int(np.bitwise_count(lazy).sum(dtype=np.int64))
+    sim.broadcast(0)                     # the origin's pushes are sent before the first round
     st2, r2 = sim.run()
     assert sim.delivered().all()
-    assert sum(s["broadcast"] for s in st2) == n - 1
-    assert sum(s["prune"] + s["graft"] + s["i_have"] for s in st2) == 0
+    # the tree carries the heartbeat (BFS tree: the parent's push is first in
+    # slot order), every lazy link gets one i_have answered by ignored_i_have
+    assert root_children + sum(s["broadcast"] for s in st2) == n - 1
+    assert sum(s["prune"] + s["graft"] for s in st2) == 0
+    assert sum(s["i_have"] for s in st2) == lazy_links == sum(s["ignored_i_have"] for s in st2)
     sim.close()
 
 

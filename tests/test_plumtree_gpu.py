@@ -491,3 +491,22 @@ def test_facade_get_peers_per_root():
     assert pt.handler(99).is_stale(first) and pt.handler(99).is_stale(ids[3])
     assert not pt.handler(99).is_stale((3, 0, ids[3][2] + 1))
     pt.close()
+
+
+def test_round_tags_across_wrap(psim):
+    """Consumed inbox words are left in place with their round tag (mod 256);
+    hundreds of idle rounds between heartbeats (and a lane that sat idle)
+    must not let an old word alias a new round's tag: lockstep after 600
+    idle rounds, across several tag wraps and scrubs."""
+    rp, col = psim.overlay.random_regular(700, 5, 151)
+    sim, orc = make(psim, rp, col, 1)
+    for gap in (0, 300, 257, 43):
+        if gap:
+            gs = sim.step(gap)
+            os_ = orc.step(gap)
+            assert all(sum(g[k] for k in KINDS) == 0 for g in gs)
+            assert all(sum(o[k] for k in KINDS) == 0 for o in os_)
+        m = sim.broadcast(5)
+        assert m == orc.heartbeat(5)
+        compare(sim, orc, 5, m)
+        lockstep(sim, orc, 5, m)
