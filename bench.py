@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
+    p.add_argument("--buckets", choices=["auto", "always", "never"], default="auto",
+                   help="slot-scatter engine transport per round (DESIGN.md 5.2); auto = chosen on device")
     p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
     p.add_argument("--all-on-device0", action="store_true",
@@ -188,7 +190,7 @@ def main():
         sim = sp.sim
     else:
         sp = None
-        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
+        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local, buckets=args.buckets)
         sim.load_overlay(rp, col)
     del rp, col
     root = 0

@@ -101,31 +101,35 @@ def test_bench_config_10m_flood_converges():
 
 @pytest.mark.gpu
 def test_bench_config_10m_engines_agree_per_round():
-    """The slot-scatter and binned engines at the bench size, round by round,
-    by psim_trace_hash (state digest, in-flight digest, delivered count)."""
+    """The engines at the bench size, round by round, by psim_trace_hash
+    (state digest, in-flight digest, delivered count): the slot-scatter engine
+    with its per-round transport choice (what bench.py times), with direct
+    slot stores only, and the binned engine."""
     import partisan_amd as pa
     n = 10_000_000
     rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
-    a = pa.Simulator(lazy_tick_rounds=1, device=0)
-    b = pa.Simulator(lazy_tick_rounds=1, device=0, binned=True)
-    a.load_overlay(rp, col)
-    b.load_overlay(rp, col)
+    sims = [pa.Simulator(lazy_tick_rounds=1, device=0),                   # bench's engine (auto transport)
+            pa.Simulator(lazy_tick_rounds=1, device=0, buckets="never"),
+            pa.Simulator(lazy_tick_rounds=1, device=0, binned=True)]
+    for h in sims:
+        h.load_overlay(rp, col)
     del rp, col
-    for h in (a, b):
+    for h in sims:
         h.reset_trees()
         h.broadcast(0)
     rounds = 0
     while True:
-        sa, sb = a.step(1)[0], b.step(1)[0]
+        st = [h.step(1)[0] for h in sims]
         rounds += 1
         for k in KINDS + ("delivered_new", "active", "senders"):
-            assert sa[k] == sb[k], (rounds, k)
-        assert a.trace_hash() == b.trace_hash(), rounds
-        if sum(sa[k] for k in KINDS) == 0 or rounds > 40:
+            assert len({x[k] for x in st}) == 1, (rounds, k)
+        th = [h.trace_hash() for h in sims]
+        assert th[0] == th[1] == th[2], rounds
+        if sum(st[0][k] for k in KINDS) == 0 or rounds > 40:
             break
     assert rounds == 17       # the 16 rounds of the flood + the silent one that shows quiescence
-    a.close()
-    b.close()
+    for h in sims:
+        h.close()
 
 
 @pytest.mark.gpu

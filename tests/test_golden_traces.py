@@ -72,14 +72,17 @@ def test_oracle_replays_golden_trace(name):
     orc.close()
 
 
+ENGINES = {"direct": {"buckets": "never"}, "buckets": {"buckets": "always"}, "binned": {"binned": True}}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("binned", [False, True])
+@pytest.mark.parametrize("engine", sorted(ENGINES))
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_hip_replays_golden_trace(name, binned):
+def test_hip_replays_golden_trace(name, engine):
     import partisan_amd as pa
     c = CASES[name]
     rp, col = csr(c)
-    sim = pa.Simulator(lazy_tick_rounds=c["lazy_tick_rounds"], device=0, binned=binned)
+    sim = pa.Simulator(lazy_tick_rounds=c["lazy_tick_rounds"], device=0, **ENGINES[engine])
     sim.load_overlay(rp, col)
     n = c["n"]
     for ev in c["events"]:

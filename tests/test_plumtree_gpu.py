@@ -18,17 +18,20 @@ pytestmark = pytest.mark.gpu
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-@pytest.fixture(scope="module", params=["slot_scatter", "binned"])
+@pytest.fixture(scope="module", params=["slot_scatter", "binned", "buckets"])
 def psim(request):
     """partisan_amd with Simulator bound to one Plumtree engine: the
-    slot-scatter engine (the default, also what sharded handles run) and the
-    binned one (PSIM_CFG_BINNED) must both match the oracle."""
+    slot-scatter engine with direct slot stores (what sharded handles run),
+    the binned one (PSIM_CFG_BINNED) and the slot-scatter engine with every
+    round through the bucketed transport (PSIM_CFG_BUCKETS_ALWAYS) must all
+    match the oracle."""
     import functools
     import types
 
     import partisan_amd
     ns = types.SimpleNamespace(**{k: getattr(partisan_amd, k) for k in dir(partisan_amd) if not k.startswith("__")})
-    ns.Simulator = functools.partial(partisan_amd.Simulator, binned=request.param == "binned")
+    kw = {"slot_scatter": {"buckets": "never"}, "binned": {"binned": True}, "buckets": {"buckets": "always"}}
+    ns.Simulator = functools.partial(partisan_amd.Simulator, **kw[request.param])
     ns.engine = request.param
     return ns
 
@@ -277,27 +280,29 @@ def test_trace_hash_matches_getters(psim):
 
 
 def test_trace_hash_engines_agree_at_scale():
-    """The two engines at 2M peers, round by round, compared by digest only."""
+    """The engines at 2M peers, round by round, compared by digest only:
+    direct slot stores, the per-round transport choice (default), every round
+    bucketed, and the binned engine."""
     import partisan_amd
     rp, col = partisan_amd.overlay.random_regular(2_000_000, 5, 91)
-    a = partisan_amd.Simulator()
-    b = partisan_amd.Simulator(binned=True)
-    a.load_overlay(rp, col)
-    b.load_overlay(rp, col)
+    sims = [partisan_amd.Simulator(buckets="never"), partisan_amd.Simulator(),
+            partisan_amd.Simulator(buckets="always"), partisan_amd.Simulator(binned=True)]
+    for s in sims:
+        s.load_overlay(rp, col)
     for root in (0, 12345):
-        a.reset_trees()
-        b.reset_trees()
-        a.broadcast(root)
-        b.broadcast(root)
+        for s in sims:
+            s.reset_trees()
+            s.broadcast(root)
         for _ in range(40):
-            sa, sb = a.step(1)[0], b.step(1)[0]
+            st = [s.step(1)[0] for s in sims]
             for k in KINDS + ("delivered_new", "active", "senders"):
-                assert sa[k] == sb[k], k
-            assert a.trace_hash() == b.trace_hash()
-            if sum(sa[k] for k in KINDS) == 0:
+                assert len({x[k] for x in st}) == 1, k
+            th = [s.trace_hash() for s in sims]
+            assert all(t == th[0] for t in th), th
+            if sum(st[0][k] for k in KINDS) == 0:
                 break
-    a.close()
-    b.close()
+    for s in sims:
+        s.close()
 
 
 def _omit_step(sim, orc, root, mono, rounds):
