@@ -224,6 +224,50 @@ int  psim_shard_collect(psim_handle* h, psim_round_stats* stats, size_t cap, uin
  * they do not advance the timer schedule (lazy tick phase), as in psim_run. */
 int  psim_shard_uncount(psim_handle* h, uint32_t rounds);
 
+/* --- the exchange inside the library -------------
+ * A sharded handle can own its transport and run whole heartbeats itself:
+ * every round is enqueued as round kernel -> pack -> exchange -> ingest on the
+ * handle's stream, counters are collected (one host sync, one all-reduce)
+ * every 4 rounds, and the run stops at GLOBAL quiescence with the single-GPU
+ * engine's round count.  Transports:
+ *   psim_shard_init_rccl: one RCCL communicator per handle (ncclCommInitRank
+ *     on the handle's device), the words as one grouped ncclSend / ncclRecv
+ *     per round over the static regions of psim_shard_layout /
+ *     psim_shard_recv_layout, the counters as one int64 ncclAllReduce.  The
+ *     unique id comes from psim_rccl_unique_id on one rank, shipped to the
+ *     others by the caller (any out-of-band channel);
+ *   psim_shard_set_transport: caller callbacks over HOST buffers (tests, or a
+ *     fabric the library does not know). */
+#define PSIM_RCCL_ID_BYTES 128
+typedef struct psim_transport {
+    void* ctx;
+    /* all-to-all-v of u32 words: region d of send = send[send_off[d], send_off[d+1])
+     * goes to rank d; what rank s sends to this rank lands at recv[recv_off[s], ...).
+     * Returns 0 on success. */
+    int (*alltoallv)(void* ctx, const uint32_t* send, const uint64_t* send_off, uint32_t* recv,
+                     const uint64_t* recv_off, int world);
+    /* in-place sum over ranks of n int64 values; returns 0 on success */
+    int (*allreduce)(void* ctx, int64_t* vals, size_t n);
+} psim_transport;
+typedef struct psim_exchange_stats {
+    uint64_t rounds;               /* rounds enqueued (the uncounted quiescent tail included) */
+    uint64_t fabric_bytes;         /* bytes this rank sent to other ranks                     */
+    double   exchange_ms;          /* device time inside the exchange (hipEvents)              */
+    double   kernel_ms;            /* device time of the round kernels (hipEvents)             */
+} psim_exchange_stats;
+int  psim_rccl_unique_id(uint8_t* id_out /* PSIM_RCCL_ID_BYTES */);
+/* psim_shard_init + an RCCL communicator of `world` ranks; before psim_load_csr */
+int  psim_shard_init_rccl(psim_handle* h, int rank, int world, const uint8_t* id /* PSIM_RCCL_ID_BYTES */);
+int  psim_shard_set_transport(psim_handle* h, const psim_transport* t);
+/* heartbeat at `root` on every rank (collective): the origin's pushes are
+ * exchanged before it returns */
+int  psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out);
+/* collective: rounds until global quiescence (or max_rounds); stats are the
+ * GLOBAL per-round counters (summed over ranks; kernel_ms this rank's),
+ * *xs this rank's exchange figures (may be NULL) */
+int  psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds_run,
+                    psim_exchange_stats* xs);
+
 /* --- partisan_vclock on dense lanes ----------------------------------- */
 /* A clock is PSIM_VC_LANES u32 lanes, lane i = actor i (actor ids are ranks
  * in the sorted actor table, so lane order is the reference's term order).

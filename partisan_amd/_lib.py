@@ -122,6 +122,27 @@ class C3Stats(C.Structure):
         return d
 
 
+class ExchangeStats(C.Structure):
+    _fields_ = [("rounds", C.c_uint64), ("fabric_bytes", C.c_uint64), ("exchange_ms", C.c_double),
+                ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: (float(getattr(self, k)) if k.endswith("_ms") else int(getattr(self, k))) for k, _ in self._fields_}
+
+
+# psim_transport callbacks (include/psim.h): all-to-all-v of u32 words over host buffers, int64 sum all-reduce
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                           C.POINTER(C.c_uint64), C.c_int)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_size_t)
+
+
+class Transport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("alltoallv", ALLTOALLV_FN), ("allreduce", ALLREDUCE_FN)]
+
+
+PSIM_RCCL_ID_BYTES = 128
+
+
 # every entry point of include/psim.h: name -> (restype, argtypes)
 class RelayStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("direct", "relay", "dropped", "lost", "arrived")]
@@ -168,6 +189,11 @@ SIGNATURES = {
     "psim_shard_ingest_dense": (C.c_int, [_H, C.c_void_p]),
     "psim_shard_collect": (C.c_int, [_H, _P(RoundStats), C.c_size_t, _P(C.c_uint32), _P(C.c_int64)]),
     "psim_shard_uncount": (C.c_int, [_H, C.c_uint32]),
+    "psim_rccl_unique_id": (C.c_int, [_P(C.c_uint8)]),
+    "psim_shard_init_rccl": (C.c_int, [_H, C.c_int, C.c_int, _P(C.c_uint8)]),
+    "psim_shard_set_transport": (C.c_int, [_H, _P(Transport)]),
+    "psim_shard_broadcast_x": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
+    "psim_shard_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32), _P(ExchangeStats)]),
     "psim_demers_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_demers_broadcast_all": (C.c_int, [_H]),
     "psim_demers_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),

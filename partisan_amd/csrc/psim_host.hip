@@ -128,6 +128,10 @@ struct psim_handle {
         unsigned long long* ring = nullptr;   // [kRing][kStatShards][kNStat]
         hipEvent_t rev_[2 * 16] = {};
         uint32_t pending = 0;
+        // the exchange inside the library (psim_shard_init_rccl / _set_transport, transport.hip)
+        psim::Transport* xport = nullptr;
+        uint32_t *xsend = nullptr, *xrecv = nullptr;   // dense word regions (psim_shard_layout / _recv_layout)
+        hipEvent_t xev[2 * 16] = {};                   // exchange start / end per pending round
     } sh;
     hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
 
@@ -269,10 +273,10 @@ void free_graph(psim_handle* h) {
         b = psim_handle::Bin();
     }
     auto& sh = h->sh;
-    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map};
+    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map, sh.xsend, sh.xrecv};
     for (void* p : sp)
         if (p) (void)hipFree(p);
-    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = nullptr;
+    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = sh.xsend = sh.xrecv = nullptr;
     sh.recv_base.clear();
     sh.pending = 0;
     sh.blk = nullptr;
@@ -773,6 +777,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (hipMalloc(&h->sh.ring, 16 * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         for (auto& e : h->sh.rev_)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
+        for (auto& e : h->sh.xev)
+            if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
         if (hipMalloc(&h->stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess ||
@@ -814,7 +820,11 @@ int psim_destroy(psim_handle* h) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : h->sh.rev_)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->sh.xev)
+        if (e) (void)hipEventDestroy(e);
     if (h->sh.ring) (void)hipFree(h->sh.ring);
+    delete h->sh.xport;
+    h->sh.xport = nullptr;
     if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -1385,6 +1395,156 @@ int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32
 int psim_shard_uncount(psim_handle* h, uint32_t rounds) {
     if (!h || rounds > h->round || h->sh.pending) return PSIM_EINVAL;
     h->round -= rounds;
+    return PSIM_OK;
+}
+
+int psim_rccl_unique_id(uint8_t* id_out) {
+    if (!id_out) return PSIM_EINVAL;
+    return psim::rccl_unique_id(id_out);
+}
+
+int psim_shard_init_rccl(psim_handle* h, int rank, int world, const uint8_t* id) {
+    if (!h || !id) return PSIM_EINVAL;
+    int rc = psim_shard_init(h, rank, world);
+    if (rc) return rc;
+    delete h->sh.xport;
+    h->sh.xport = nullptr;
+    std::string err;
+    rc = psim::make_rccl_transport(h->device, rank, world, id, &h->sh.xport, &err);
+    return rc ? fail(h, rc, "%s", err.c_str()) : PSIM_OK;
+}
+
+int psim_shard_set_transport(psim_handle* h, const psim_transport* t) {
+    if (!h || !t || !t->alltoallv || !t->allreduce) return PSIM_EINVAL;
+    delete h->sh.xport;
+    h->sh.xport = psim::make_callback_transport(*t);
+    return h->sh.xport ? PSIM_OK : PSIM_ENOMEM;
+}
+
+}  // extern "C"
+
+namespace {
+
+// The dense word buffers of the in-library exchange (allocated on first use).
+int x_buffers(psim_handle* h) {
+    auto& sh = h->sh;
+    if (sh.world > 1 && !sh.xport) return fail(h, PSIM_ESTATE, "sharded handle without a transport (psim_shard_init_rccl)");
+    if (sh.xsend || sh.world == 1) return PSIM_OK;
+    const size_t ns = std::max<uint64_t>(1, sh.send_base[sh.world]), nr = std::max<uint64_t>(1, sh.recv_base[sh.world]);
+    if (hipMalloc((void**)&sh.xsend, ns * 4) != hipSuccess || hipMalloc((void**)&sh.xrecv, nr * 4) != hipSuccess)
+        return fail(h, PSIM_ENOMEM, "exchange buffers");
+    HIPCHK(h, hipMemsetAsync(sh.xsend, 0, ns * 4, h->stream));
+    HIPCHK(h, hipMemsetAsync(sh.xrecv, 0, nr * 4, h->stream));
+    return PSIM_OK;
+}
+
+// exchange the dense regions just packed into xsend, then ingest them
+int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs) {
+    auto& sh = h->sh;
+    if (sh.world == 1) return PSIM_OK;
+    std::string err;
+    HIPCHK(h, hipEventRecord(sh.xev[2 * slot], h->stream));
+    int rc = sh.xport->alltoallv(sh.xsend, sh.send_base.data(), sh.xrecv, sh.recv_base.data(), sh.rank, sh.world,
+                                 h->stream, &err);
+    if (rc) return fail(h, rc, "exchange: %s", err.c_str());
+    HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
+    if (xs) xs->fabric_bytes += 4ull * (sh.send_base[sh.world] - (sh.send_base[sh.rank + 1] - sh.send_base[sh.rank]));
+    return psim_shard_ingest_dense(h, sh.xrecv);
+}
+
+}  // namespace
+
+extern "C" {
+
+int psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+    if (!h) return PSIM_EINVAL;
+    int rc = x_buffers(h);
+    if (rc) return rc;
+    rc = psim_shard_broadcast_dense(h, root, mono_out, h->sh.xsend);
+    if (rc) return rc;
+    rc = x_exchange(h, 0, nullptr);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
+int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, uint32_t* rounds_run,
+                   psim_exchange_stats* xs) {
+    if (!h) return PSIM_EINVAL;
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    int rc = x_buffers(h);
+    if (rc) return rc;
+    if (xs) memset(xs, 0, sizeof *xs);
+    constexpr uint32_t K = 4;                  // rounds between counter collections
+    constexpr int NK = 9;                      // 5 kinds, delivered_new, senders, degree sum, live rows
+    uint32_t ran = 0;
+    bool done = false;
+    while (!done && ran < max_rounds) {
+        const uint32_t k = std::min<uint32_t>(K, max_rounds - ran);
+        for (uint32_t j = 0; j < k; j++) {
+            rc = psim_shard_round_async(h, h->sh.xsend);
+            if (rc) return rc;
+            rc = x_exchange(h, (int)j, xs);
+            if (rc) return rc;
+        }
+        psim_round_stats st[K];
+        int64_t live[K];
+        uint32_t got = 0;
+        rc = psim_shard_collect(h, st, K, &got, live);
+        if (rc) return rc;
+        if (xs) {
+            xs->rounds += got;
+            for (uint32_t j = 0; j < got; j++) {
+                xs->kernel_ms += st[j].kernel_ms;
+                float ms = 0.f;
+                if (h->sh.world > 1) HIPCHK(h, hipEventElapsedTime(&ms, h->sh.xev[2 * j], h->sh.xev[2 * j + 1]));
+                xs->exchange_ms += ms;
+            }
+        }
+        std::vector<int64_t> flat(size_t(got) * NK);
+        for (uint32_t j = 0; j < got; j++) {
+            int64_t* f = flat.data() + size_t(j) * NK;
+            for (int t = 1; t <= 5; t++) f[t - 1] = (int64_t)st[j].sent[t];
+            f[5] = (int64_t)st[j].delivered_new;
+            f[6] = (int64_t)st[j].senders;
+            f[7] = (int64_t)st[j].sender_degree_sum;
+            f[8] = live[j];
+        }
+        if (h->sh.world > 1) {
+            std::string err;
+            rc = h->sh.xport->allreduce(flat.data(), flat.size(), h->stream, &err);
+            if (rc) return fail(h, rc, "counter all-reduce: %s", err.c_str());
+        }
+        for (uint32_t j = 0; j < got; j++) {
+            const int64_t* f = flat.data() + size_t(j) * NK;
+            int64_t msgs = 0;
+            for (int t = 0; t < 5; t++) msgs += f[t];
+            if (out && ran < cap) {
+                psim_round_stats& o = out[ran];
+                const double kms = st[j].kernel_ms;
+                memset(&o, 0, sizeof o);
+                for (int t = 1; t <= 5; t++) o.sent[t] = (uint64_t)f[t - 1];
+                o.delivered_new = (uint64_t)f[5];
+                o.senders = (uint64_t)f[6];
+                o.sender_degree_sum = (uint64_t)f[7];
+                o.active = st[j].active;                        // this rank's
+                o.outstanding_vertices = st[j].outstanding_vertices;
+                o.algo_bytes = st[j].algo_bytes;                // this rank's (its kernel's bytes)
+                o.kernel_ms = kms;
+            }
+            ran++;
+            if (msgs == 0 && f[8] == 0) {                       // globally quiescent after this round
+                done = true;
+                const uint32_t extra = got - (j + 1);
+                if (extra) {
+                    rc = psim_shard_uncount(h, extra);
+                    if (rc) return rc;
+                }
+                break;
+            }
+        }
+    }
+    if (rounds_run) *rounds_run = ran;
     return PSIM_OK;
 }
 

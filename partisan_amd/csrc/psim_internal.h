@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 typedef struct psim_handle psim_handle;
 typedef struct psim_scamp_stats psim_scamp_stats;
+typedef struct psim_transport psim_transport;
 
 namespace psim {
 
@@ -364,6 +367,22 @@ struct PdArgs {
 hipError_t launch_pd_init(const PdArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s);
 hipError_t launch_pd_round(const PdArgs& a, hipStream_t s);
+
+// Cross-shard exchange owned by a handle (transport.hip).  Calls return
+// PSIM_* codes and put a detail into *err.
+struct Transport {
+    virtual ~Transport() {}
+    // u32 words, regions by rank (static offsets), on stream s (RCCL) or via
+    // host staging (callbacks); the own-rank region is empty
+    virtual int alltoallv(const uint32_t* send, const uint64_t* soff, uint32_t* recv, const uint64_t* roff, int rank,
+                          int world, hipStream_t s, std::string* err) = 0;
+    // host values, in place, summed over ranks (synchronous)
+    virtual int allreduce(int64_t* vals, size_t n, hipStream_t s, std::string* err) = 0;
+    virtual const char* name() const = 0;
+};
+int make_rccl_transport(int device, int rank, int world, const void* id, Transport** out, std::string* err);
+Transport* make_callback_transport(const psim_transport& t);
+int rccl_unique_id(void* out);
 
 // Protocol modules that keep their host state outside psim_host.hip: the
 // handle owns one slot per module and deletes it on psim_destroy.
