@@ -49,8 +49,6 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
-    p.add_argument("--buckets", choices=["auto", "always", "never"], default="auto",
-                   help="slot-scatter engine transport per round (DESIGN.md 5.2); auto = chosen on device")
     p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
     p.add_argument("--all-on-device0", action="store_true",
@@ -190,7 +188,7 @@ def main():
         sim = sp.sim
     else:
         sp = None
-        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local, buckets=args.buckets)
+        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
         sim.load_overlay(rp, col)
     del rp, col
     root = 0
@@ -210,6 +208,7 @@ def main():
     rounds_per_step = []
     if sp is not None:
         sp.local_algo_bytes, sp.local_kernel_ms = 0, 0.0
+        sp.exchange_total = {}
     barrier(pg)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -225,6 +224,16 @@ def main():
         algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
 
     verified = verify(sim, pg, args.n, rounds_per_step)
+    exchange = None
+    if sp is not None:   # the in-library exchange (psim_shard_run): fabric bytes and device time per step
+        xt = sp.exchange_total
+        exchange = {
+            "transport": sp.transport,
+            "fabric_bytes_per_step": sum_over_ranks(pg, float(xt.get("fabric_bytes", 0))) / args.steps,
+            "exchange_ms_per_step_max_rank": max_over_ranks(pg, float(xt.get("exchange_ms", 0.0))) / args.steps,
+            "kernel_ms_per_step_max_rank": max_over_ranks(pg, float(xt.get("kernel_ms", 0.0))) / args.steps,
+            "rounds_enqueued_per_step": float(xt.get("rounds", 0)) / args.steps,
+        }
 
     step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
     n_units = args.n if sharded else args.n * world      # peers simulated by the whole job
@@ -267,8 +276,8 @@ def main():
                 "rounds_to_convergence": rounds_per_step[-1],
                 "verified_after_timing": verified,
                 "parallelism": (f"vertex-sharded x{world}, "
-                                + ("RCCL all-to-all over xGMI" if args.transport == "nccl" else "gloo host-staged")
-                                + " exchange per round" if sharded
+                                + ("RCCL grouped send/recv over xGMI inside libpsim" if args.transport == "nccl"
+                                   else "gloo host-staged") + " exchange per round" if sharded
                                 else ("replicas" if world > 1 else "single")),
                 "device": sim.device_info(),
             },
@@ -284,6 +293,8 @@ def main():
                 "algo_bytes_per_launch": algo_bytes / max(1, counted),
             },
         }
+        if exchange is not None:
+            out["exchange"] = exchange
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)
             if args.cpu_workers > 1:

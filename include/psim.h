@@ -68,13 +68,6 @@ typedef struct psim_config {
  * receiver slot (the default, and what sharded handles always run).  Both
  * give identical results; the binned engine is the slower one on MI355X today. */
 #define PSIM_CFG_BINNED 1u
-/* Slot-scatter engine, single GPU: dense rounds move their words through the
- * bucketed transport (senders write words into static
- * per-(receiver bucket, sender chunk) runs, a second pass scatters each
- * L2-sized bucket into the inbox); the engine picks it per round on device.
- * These force it for every round / never (tests and A/B runs). */
-#define PSIM_CFG_BUCKETS_ALWAYS 2u
-#define PSIM_CFG_BUCKETS_NEVER  4u
 
 /* Per-round counters, reduced on device (psim_step / psim_run). */
 typedef struct psim_round_stats {

@@ -128,12 +128,8 @@ __device__ __forceinline__ bool omitted(const PtArgs& a, uint32_t e) {
 }
 
 template <bool kOmit = true>
-__device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w, bool bk = false) {
+__device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w) {
     if (kOmit && omitted(a, e)) return;
-    if (bk) {                                   // bucketed transport: the word's static run position
-        a.bk_words[a.bk_pos[e]] = w;
-        return;
-    }
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
 #ifdef PT_NT_STORE
@@ -310,7 +306,7 @@ constexpr uint32_t kFastDeg = 8;
 
 template <bool kOmit>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
-                                               bool due, bool bk, Ctr& c) {
+                                               bool due, Ctr& c) {
     uint32_t w[kFastDeg];
     uint32_t any = 0;
 #pragma unroll
@@ -327,7 +323,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 #pragma unroll
     for (uint32_t s = 0; s < kFastDeg; s++) {
         cl[s] = s < deg ? a.col[rs + s] : 0u;
-        rv[s] = s < deg ? (bk ? a.bk_pos[rs + s] : a.rev[rs + s]) : 0u;
+        rv[s] = s < deg ? a.rev[rs + s] : 0u;
     }
     if (!((aw >> ((a.v_lo + v) & 31)) & 1u)) return;   // a dead vertex receives nothing
     c.active++;
@@ -351,9 +347,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
         sent = true;
         if (kOmit && omitted(a, rs + s)) continue;
         const uint32_t u = cl[s] - a.v_lo;
-        if (bk) {
-            a.bk_words[rv[s]] = wo;                      // rv = run position (bk_pos) in bucket rounds
-        } else if (u < a.n) {
+        if (u < a.n) {
 #ifdef PT_NT_STORE
             __builtin_nontemporal_store(wo, &a.in_nxt[rv[s] - a.slot_base]);
 #else
@@ -372,13 +366,13 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 }
 
 template <bool kOmit>
-__device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, bool bk, uint16_t* rep,
+__device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
 #ifndef PT_NO_FAST
     if (deg <= kFastDeg) {
-        pt_vertex_fast<kOmit>(a, v, rs, deg, pend, due, bk, c);
+        pt_vertex_fast<kOmit>(a, v, rs, deg, pend, due, c);
         return;
     }
 #endif
@@ -406,7 +400,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
-        deliver_word<kOmit>(a, rs + s, w, bk);
+        deliver_word<kOmit>(a, rs + s, w);
         sent = true;
     }
     if (sent) {
@@ -470,10 +464,9 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     if (nc == 0) return;                          // uniform: idle chunk
     Ctr c;
     c.zero();
-    const bool bk = a.bk_words && a.bk_mode[a.bk_mode_idx];   // uniform: this round's transport
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex<kOmit>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, bk, &rep[t], c);
+        pt_vertex<kOmit>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
     flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
 }
@@ -844,43 +837,6 @@ __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
     }
 }
 
-// Bucketed transport, second pass.  Bucket b = receiver
-// slots [b 2^kBkShift, (b+1) 2^kBkShift) = 1 MB of inbox words; its words sit
-// in runs [bk_off[b], bk_off[b+1]) of bk_words (one run per sender chunk,
-// written by that chunk's workgroup: whole lines, no cross-XCD partials), with
-// the receiver slot of each position in bk_dst.  Workgroup g works on XCD
-// g % 8 (round-robin dispatch, a speed assumption only) and takes part
-// (g / 8) % kBkParts of buckets g % 8, g % 8 + 8, ...: one bucket is swept by
-// the 256 workgroups of ONE XCD, so its random inbox stores and group flags
-// land in that XCD's L2 and leave it as whole lines.  Stale words (an older
-// round tag: the slot sent nothing this round) are skipped.
-__global__ __launch_bounds__(kBlock) void pt_bucket_route_kernel(PtArgs a, const uint32_t* __restrict__ bk_dst,
-                                                                 const uint32_t* __restrict__ bk_off, uint32_t nbk,
-                                                                 const uint32_t* __restrict__ slot2v,
-                                                                 const unsigned long long* __restrict__ st,
-                                                                 int* __restrict__ mode, uint32_t next_idx,
-                                                                 unsigned long long min_bcast, int force) {
-    if (blockIdx.x == 0 && threadIdx.x < 64) {        // the next round's transport, from this round's broadcasts
-        unsigned long long b = st[threadIdx.x * kNStat + PSIM_MSG_BROADCAST];
-        b = wave_sum(b);
-        if (threadIdx.x == 0) mode[next_idx] = force == 1 ? 1 : force == 2 ? 0 : (b >= min_bcast ? 1 : 0);
-    }
-    if (!mode[a.bk_mode_idx]) return;                 // this round wrote straight into the inbox
-    const uint32_t x = blockIdx.x & 7u, part = (blockIdx.x >> 3) % kBkParts;
-    for (uint32_t b = x; b < nbk; b += 8) {
-        const uint32_t lo = bk_off[b], len = bk_off[b + 1] - lo;
-        const uint32_t p0 = lo + uint32_t((uint64_t(len) * part) / kBkParts);
-        const uint32_t p1 = lo + uint32_t((uint64_t(len) * (part + 1)) / kBkParts);
-        for (uint32_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
-            const uint32_t w = a.bk_words[i];
-            if (!live_word(w, a.wtag)) continue;
-            const uint32_t d = bk_dst[i];
-            a.in_nxt[d] = w;
-            a.pend_nxt[slot2v[d] >> kGroupShift] = 1;
-        }
-    }
-}
-
 // Zero inbox words whose round tag is not `keep` (stale ones, before a tag
 // could repeat): one pass over a buffer every <= 256 rounds.
 __global__ __launch_bounds__(kBlock) void pt_scrub_kernel(uint4* __restrict__ w, unsigned long long n4, uint32_t keep) {
@@ -1007,14 +963,6 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(pt_round_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     else
         hipLaunchKernelGGL(pt_round_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_pt_bucket_route(const PtArgs& a, const uint32_t* bk_dst, const uint32_t* bk_off, uint32_t nbk,
-                                  const uint32_t* slot2v, const unsigned long long* round_stats, int* mode_ring,
-                                  uint32_t next_idx, unsigned long long min_bcast, int force, hipStream_t s) {
-    hipLaunchKernelGGL(pt_bucket_route_kernel, dim3(8 * kBkParts), dim3(kBlock), 0, s, a, bk_dst, bk_off, nbk, slot2v,
-                       round_stats, mode_ring, next_idx, min_bcast, force);
     return hipGetLastError();
 }
 

@@ -45,16 +45,6 @@ struct psim_handle {
     uint8_t* pend[2] = {nullptr, nullptr};
     uint8_t* ost = nullptr;
     uint32_t* omit = nullptr;       // omission faults: bitmap over local sender slots (psim_set_omissions)
-    // bucketed transport of dense rounds (single GPU, slot-scatter engine): DESIGN.md 5.2
-    struct Bk {
-        uint32_t *pos = nullptr, *dst = nullptr, *off = nullptr, *words = nullptr, *slot2v = nullptr;
-        int* mode = nullptr;            // [4] transport of round R mod 4 (1 = buckets)
-        uint32_t nbk = 0;
-        uint64_t total = 0;             // bucket run positions (padded)
-        uint64_t scrub = 0;             // round at which `words` was last zeroed (round tags, see scrub_if_needed)
-        unsigned long long min_bcast = 0;
-        int force = 0;                  // 0 auto, 1 always, 2 never
-    } bk;
     // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
     struct Bin {
         uint2 *rec_c = nullptr, *rec_f = nullptr;
@@ -259,13 +249,6 @@ void free_graph(psim_handle* h) {
     if (h->omit) (void)hipFree(h->omit);
     h->omit = nullptr;
     {
-        auto& k = h->bk;
-        void* kp[] = {k.pos, k.dst, k.off, k.words, k.slot2v, k.mode};
-        for (void* p : kp)
-            if (p) (void)hipFree(p);
-        k = psim_handle::Bk();
-    }
-    {
         auto& b = h->bin;
         void* bp[] = {b.rec_c, b.rec_f, b.cnt_c[0], b.cnt_c[1], b.cnt_f, b.csub, b.fslot, b.obin};
         for (void* p : bp)
@@ -413,61 +396,6 @@ bool bin_geometry(const std::vector<uint32_t>& rp, uint32_t n, uint32_t& fv, uin
     cv = fv + g;
     nc = uint32_t((uint64_t(nf) + (1u << g) - 1) >> g);
     return true;
-}
-
-// Static layout of the bucketed transport.  Receiver slot d
-// lies in bucket d >> kBkShift; sender slot e in chunk v(e) / kChunkV (the
-// round kernel's workgroup).  bk_words holds, bucket by bucket, one run per
-// (bucket, sender chunk) padded to kBkPad words; pos[e] = the word position of
-// sender slot e, dst[p] = the receiver slot of position p.
-int build_buckets(psim_handle* h, const std::vector<uint32_t>& rpl, const std::vector<uint32_t>& rev,
-                  const std::vector<uint32_t>& s2v, uint32_t n, uint64_t E) {
-    auto& k = h->bk;
-    const uint32_t nch = (n + kChunkV - 1) / kChunkV;
-    const uint32_t nbk = uint32_t((E + (1ull << kBkShift) - 1) >> kBkShift);
-    std::vector<uint32_t> cnt(size_t(nbk) * nch, 0u);
-    for (uint32_t v = 0; v < n; v++)
-        for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) cnt[size_t(rev[e] >> kBkShift) * nch + v / kChunkV]++;
-    std::vector<uint64_t> run(cnt.size());
-    std::vector<uint32_t> boff(size_t(nbk) + 1);
-    uint64_t tot = 0;
-    for (uint32_t b = 0; b < nbk; b++) {
-        boff[b] = uint32_t(tot);
-        for (uint32_t c = 0; c < nch; c++) {
-            run[size_t(b) * nch + c] = tot;
-            tot += (cnt[size_t(b) * nch + c] + kBkPad - 1) / kBkPad * kBkPad;
-        }
-        if (tot >= 0xFFFFFFFFull) return fail(h, PSIM_EINVAL, "bucket layout exceeds 2^32 positions");
-    }
-    boff[nbk] = uint32_t(tot);
-    std::vector<uint32_t> pos(E), dst(tot, 0u);
-    for (uint32_t v = 0; v < n; v++)
-        for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) {
-            const uint64_t p = run[size_t(rev[e] >> kBkShift) * nch + v / kChunkV]++;
-            pos[e] = uint32_t(p);
-            dst[p] = rev[e];
-        }
-    if (hipMalloc((void**)&k.pos, E * 4) != hipSuccess || hipMalloc((void**)&k.dst, tot * 4) != hipSuccess ||
-        hipMalloc((void**)&k.off, (size_t(nbk) + 1) * 4) != hipSuccess ||
-        hipMalloc((void**)&k.words, tot * 4) != hipSuccess || hipMalloc((void**)&k.slot2v, E * 4) != hipSuccess ||
-        hipMalloc((void**)&k.mode, 4 * sizeof(int)) != hipSuccess)
-        return fail(h, PSIM_ENOMEM, "bucketed transport arrays (%llu positions)", (unsigned long long)tot);
-    HIPCHK(h, hipMemcpy(k.pos, pos.data(), E * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(k.dst, dst.data(), tot * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(k.off, boff.data(), (size_t(nbk) + 1) * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(k.slot2v, s2v.data(), E * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemset(k.words, 0, tot * 4));
-    k.force = (h->cfg.flags & PSIM_CFG_BUCKETS_ALWAYS) ? 1 : 0;
-    const int m0[4] = {k.force, k.force, k.force, k.force};
-    HIPCHK(h, hipMemcpy(k.mode, m0, sizeof m0, hipMemcpyHostToDevice));
-    k.nbk = nbk;
-    k.total = tot;
-    k.scrub = 0;
-    // a round that sends >= E/20 broadcasts makes the next one dense (each
-    // delivery pushes to its deg - 1 eager peers): bucket it
-    k.min_bcast = E / 20;
-    if (const char* env = getenv("PSIM_BK_MIN_BCAST")) k.min_bcast = strtoull(env, nullptr, 10);
-    return PSIM_OK;
 }
 
 void reduce_row(const unsigned long long* row, unsigned long long* out) {
@@ -619,32 +547,11 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             }
         } else
 #endif
-        {
-            const bool bk = h->bk.words && A == 1;    // bucketed transport: single-lane rounds only
-            if (bk && h->round + k > h->bk.scrub + kTagSpan) {   // stale run words must not alias a tag
-                HIPCHK(h, hipMemsetAsync(h->bk.words, 0, h->bk.total * 4, h->stream));
-                h->bk.scrub = h->round;
-            }
-            for (uint32_t i = 0; i < k; i++) {
-                const uint32_t tick = ((h->round + i + 1) % L) == 0;
-                HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-                for (size_t q = 0; q < A; q++) {
-                    PtArgs a = lane_args(q, i, tick);
-                    const uint64_t R = h->round + i + 1;
-                    if (bk) {
-                        a.bk_words = h->bk.words;
-                        a.bk_pos = h->bk.pos;
-                        a.bk_mode = h->bk.mode;
-                        a.bk_mode_idx = uint32_t(R % 4);
-                    }
-                    HIPCHK(h, launch_pt_round(a, h->stream));
-                    if (bk)
-                        HIPCHK(h, launch_pt_bucket_route(a, h->bk.dst, h->bk.off, h->bk.nbk, h->bk.slot2v, a.stats,
-                                                         h->bk.mode, uint32_t((R + 1) % 4), h->bk.min_bcast,
-                                                         h->bk.force, h->stream));
-                }
-                HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
-            }
+        for (uint32_t i = 0; i < k; i++) {
+            const uint32_t tick = ((h->round + i + 1) % L) == 0;
+            HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+            for (size_t q = 0; q < A; q++) HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
+            HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
         }
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
@@ -1051,13 +958,6 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     sh.send_base = sbases;
     sh.recv_base = rbases;
-    if (W == 1 && !binned && !(h->cfg.flags & PSIM_CFG_BUCKETS_NEVER) && El) {
-        const int rc = build_buckets(h, rpl, rvl, s2v, nl, El);
-        if (rc) {
-            free_graph(h);
-            return rc;
-        }
-    }
     HIPCHK(h, hipDeviceSynchronize());
     {
         std::vector<uint64_t> rpl64(size_t(nl) + 1);

@@ -105,11 +105,6 @@ struct PtArgs {
     uint32_t root;                         // local index of the current heartbeat's origin
     uint32_t ctag, wtag;                   // round tags of the words read / written this round
     const uint32_t* __restrict__ omit;     // [ceil(E/32)] omission faults over sender slots, or null
-    // bucketed transport of dense rounds (single GPU, slot-scatter; null = off)
-    uint32_t* __restrict__ bk_words;       // [bk_total] words by (receiver bucket, sender chunk) run
-    const uint32_t* __restrict__ bk_pos;   // [E] run position of each sender slot's word
-    const int* __restrict__ bk_mode;       // [4] 1 = round R mod 4 writes through the buckets
-    uint32_t bk_mode_idx;                  // R mod 4
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}
     uint2* __restrict__ rec_f;             // [E] fine-bin regions
@@ -400,18 +395,6 @@ void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing to
 hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);   // binned when a.rec_c is set
-// Bucketed transport (after a round kernel with a.bk_words set): if that
-// round wrote through the buckets, scatter every bucket (2^kBkShift receiver
-// slots, one XCD's workgroups per bucket) into a.in_nxt + group flags; and
-// decide the next round's transport from this round's broadcast count
-// (stats row of the round): buckets iff >= min_bcast (force: 0 auto,
-// 1 always, 2 never).
-constexpr uint32_t kBkShift = 18;        // 2^18 receiver slots = 1 MB of inbox words per bucket
-constexpr uint32_t kBkPad = 16;          // runs padded to 64 B
-constexpr uint32_t kBkParts = 256;       // workgroups per bucket (one XCD's share of the grid)
-hipError_t launch_pt_bucket_route(const PtArgs& a, const uint32_t* bk_dst, const uint32_t* bk_off, uint32_t nbk,
-                                  const uint32_t* slot2v, const unsigned long long* round_stats, int* mode_ring,
-                                  uint32_t next_idx, unsigned long long min_bcast, int force, hipStream_t s);
 // one slot-scatter round for nlanes heartbeat lanes (d_args[0..nlanes) on device; a0 = d_args[0] on host)
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment

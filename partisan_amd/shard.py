@@ -1,12 +1,22 @@
 """Vertex-sharded Plumtree over several GPUs, one process per GPU
 (SURVEY 8(e)).
 
-The library runs each round split-phase (include/psim.h, "vertex
-sharding"); this driver moves the cross-shard records with
-torch.distributed -- backend "nccl" (RCCL over xGMI, device tensors) on a
-node, or "gloo" (host-staged) in tests -- and stops at GLOBAL quiescence
-(all-reduced emitted messages and live outstanding rows), so the round
-count equals the single-GPU engine's and the oracle's.
+Transports (``transport=``):
+
+* ``"rccl"`` (default with backend "nccl"): the exchange lives in libpsim --
+  ``psim_shard_init_rccl`` gives the handle its own RCCL communicator (the
+  unique id is shipped once over torch.distributed), and ``psim_shard_run``
+  runs a whole heartbeat: round kernel -> pack -> grouped ncclSend/ncclRecv
+  -> ingest on the handle's stream, counters all-reduced every 4 rounds,
+  stop at GLOBAL quiescence;
+* ``"callback"`` (default with backend "gloo", tests): the same in-library
+  run loop, the words moved by Python callbacks (``psim_shard_set_transport``)
+  over gloo, host-staged;
+* ``"torch"``: the split-phase ABI driven from Python with torch.distributed
+  collectives (the round-1 path, kept for A/B).
+
+All stop at global quiescence, so the round count equals the single-GPU
+engine's and the oracle's.
 """
 import ctypes as C
 
@@ -14,17 +24,64 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ._lib import RoundStats, check, lib
+from ._lib import (ALLREDUCE_FN, ALLTOALLV_FN, PSIM_RCCL_ID_BYTES, ExchangeStats, RoundStats, Transport, check,
+                   lib)
 from .sim import Simulator
 
 
+def gloo_transport():
+    """psim_transport callbacks over the default torch.distributed group
+    (host buffers).  Returns (Transport struct, keep-alive refs)."""
+    def a2a(_ctx, send, soff, recv, roff, world):
+        try:
+            so = [int(soff[i]) for i in range(world + 1)]
+            ro = [int(roff[i]) for i in range(world + 1)]
+            sb = np.ctypeslib.as_array(send, shape=(max(so[-1], 1),))[:so[-1]].view(np.int32)
+            rb = np.ctypeslib.as_array(recv, shape=(max(ro[-1], 1),))[:ro[-1]].view(np.int32)
+            tr = torch.from_numpy(rb)
+            dist.all_to_all_single(tr, torch.from_numpy(sb.copy()), [ro[i + 1] - ro[i] for i in range(world)],
+                                   [so[i + 1] - so[i] for i in range(world)])
+            return 0
+        except Exception as e:  # noqa: BLE001 -- must not unwind through C
+            print("psim gloo transport alltoallv:", repr(e), flush=True)
+            return 1
+
+    def ared(_ctx, vals, n):
+        try:
+            v = np.ctypeslib.as_array(vals, shape=(max(n, 1),))[:n]
+            t = torch.from_numpy(v)
+            dist.all_reduce(t)
+            return 0
+        except Exception as e:  # noqa: BLE001
+            print("psim gloo transport allreduce:", repr(e), flush=True)
+            return 1
+
+    fa, fr = ALLTOALLV_FN(a2a), ALLREDUCE_FN(ared)
+    return Transport(None, fa, fr), (fa, fr)
+
+
 class ShardedPlumtree:
-    def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1):
+    def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None):
         self.rank, self.world, self.backend = rank, world, backend
+        self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
         self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world)
-        self.sim.load_overlay(row_ptr, col)
         self._h = self.sim._h
+        self.last_exchange = {}
+        self.exchange_total = {}      # psim_exchange_stats summed over runs (this rank)
+        if self.transport == "rccl":
+            uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES)()
+            if rank == 0:
+                check(lib().psim_rccl_unique_id(uid))
+            if world > 1:
+                box = [bytes(uid)]
+                dist.broadcast_object_list(box, src=0)
+                uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES).from_buffer_copy(box[0])
+            check(lib().psim_shard_init_rccl(self._h, rank, world, uid), self._h)
+        elif self.transport == "callback":
+            self._tp, self._keep = gloo_transport()
+            check(lib().psim_shard_set_transport(self._h, C.byref(self._tp)), self._h)
+        self.sim.load_overlay(row_ptr, col)
         base = (C.c_uint64 * (world + 1))()
         check(lib().psim_shard_layout(self._h, base, world), self._h)
         self.base = [int(x) for x in base]
@@ -44,7 +101,7 @@ class ShardedPlumtree:
         self.send_w = torch.zeros(max(1, self.base[world]), dtype=torch.int32, device=self.dev)
         self.recv_w = torch.zeros(max(1, self.rbase[world]), dtype=torch.int32, device=self.dev)
         self.chunk_rounds = 4
-        if backend == "nccl":   # kernels and RCCL ordered on torch's current stream: no host sync per round
+        if backend == "nccl" and self.transport == "torch":   # kernels and RCCL on torch's stream: no host sync per round
             check(lib().psim_set_stream(self._h, C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)),
                   self._h)
 
@@ -115,6 +172,9 @@ class ShardedPlumtree:
 
     def broadcast(self, root):
         mono = C.c_uint32()
+        if self.transport != "torch":
+            check(lib().psim_shard_broadcast_x(self._h, root, C.byref(mono)), self._h)
+            return mono.value
         check(lib().psim_shard_broadcast_dense(self._h, root, C.byref(mono), C.c_void_p(self.send_w.data_ptr())),
               self._h)
         self._exchange_dense()
@@ -130,6 +190,8 @@ class ShardedPlumtree:
         ingest, stream-ordered) and their counters collected with one sync and
         one all-reduce per chunk; rounds after the first globally quiescent one
         changed nothing and are not counted (as in psim_run)."""
+        if self.transport != "torch":
+            return self._run_in_library(max_rounds)
         out, rounds = [], 0
         K = self.chunk_rounds
         keys = self.KEYS
@@ -166,6 +228,22 @@ class ShardedPlumtree:
             if done:
                 break
         return out, rounds
+
+    def _run_in_library(self, max_rounds, cap=4096):
+        st = (RoundStats * cap)()
+        ran = C.c_uint32()
+        xs = ExchangeStats()
+        check(lib().psim_shard_run(self._h, max_rounds, st, cap, C.byref(ran), C.byref(xs)), self._h)
+        out = []
+        for s_ in st[:min(ran.value, cap)]:
+            d = s_.as_dict()
+            self.local_algo_bytes += d["algo_bytes"]
+            self.local_kernel_ms += d["kernel_ms"]
+            out.append(d)
+        self.last_exchange = xs.as_dict()
+        for k, v in self.last_exchange.items():
+            self.exchange_total[k] = self.exchange_total.get(k, 0) + v
+        return out, ran.value
 
     def close(self):
         self.sim.close()

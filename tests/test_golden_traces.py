@@ -72,7 +72,7 @@ def test_oracle_replays_golden_trace(name):
     orc.close()
 
 
-ENGINES = {"direct": {"buckets": "never"}, "buckets": {"buckets": "always"}, "binned": {"binned": True}}
+ENGINES = {"slot_scatter": {}, "binned": {"binned": True}}
 
 
 @pytest.mark.gpu

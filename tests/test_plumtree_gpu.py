@@ -18,19 +18,17 @@ pytestmark = pytest.mark.gpu
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-@pytest.fixture(scope="module", params=["slot_scatter", "binned", "buckets"])
+@pytest.fixture(scope="module", params=["slot_scatter", "binned"])
 def psim(request):
     """partisan_amd with Simulator bound to one Plumtree engine: the
-    slot-scatter engine with direct slot stores (what sharded handles run),
-    the binned one (PSIM_CFG_BINNED) and the slot-scatter engine with every
-    round through the bucketed transport (PSIM_CFG_BUCKETS_ALWAYS) must all
-    match the oracle."""
+    slot-scatter engine (the default, also what sharded handles run) and the
+    binned one (PSIM_CFG_BINNED) must both match the oracle."""
     import functools
     import types
 
     import partisan_amd
     ns = types.SimpleNamespace(**{k: getattr(partisan_amd, k) for k in dir(partisan_amd) if not k.startswith("__")})
-    kw = {"slot_scatter": {"buckets": "never"}, "binned": {"binned": True}, "buckets": {"buckets": "always"}}
+    kw = {"slot_scatter": {}, "binned": {"binned": True}}
     ns.Simulator = functools.partial(partisan_amd.Simulator, **kw[request.param])
     ns.engine = request.param
     return ns
@@ -280,13 +278,10 @@ def test_trace_hash_matches_getters(psim):
 
 
 def test_trace_hash_engines_agree_at_scale():
-    """The engines at 2M peers, round by round, compared by digest only:
-    direct slot stores, the per-round transport choice (default), every round
-    bucketed, and the binned engine."""
+    """The engines at 2M peers, round by round, compared by digest only."""
     import partisan_amd
     rp, col = partisan_amd.overlay.random_regular(2_000_000, 5, 91)
-    sims = [partisan_amd.Simulator(buckets="never"), partisan_amd.Simulator(),
-            partisan_amd.Simulator(buckets="always"), partisan_amd.Simulator(binned=True)]
+    sims = [partisan_amd.Simulator(), partisan_amd.Simulator(binned=True)]
     for s in sims:
         s.load_overlay(rp, col)
     for root in (0, 12345):

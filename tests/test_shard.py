@@ -39,7 +39,7 @@ def _init(rank, world, port):
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-def _gpu_worker(rank, world, port, n, seed, L, q):
+def _gpu_worker(rank, world, port, n, seed, L, transport, q):
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -48,7 +48,7 @@ def _gpu_worker(rank, world, port, n, seed, L, q):
         from partisan_amd.shard import ShardedPlumtree
         import pyoracle as O
         rp, col = pa.overlay.random_regular(n, 5, seed)
-        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L, transport=transport)
         orc = O.Plumtree(rp, col, L)
         sim = sp.sim
         root = 7
@@ -108,9 +108,12 @@ def run_world(target, world, *args, timeout=600):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["callback", "torch"])
 @pytest.mark.parametrize("world,n,seed,L", [(2, 3000, 1, 1), (4, 5000, 2, 2)])
-def test_sharded_matches_oracle(world, n, seed, L):
-    res = run_world(_gpu_worker, world, n, seed, L)
+def test_sharded_matches_oracle(world, n, seed, L, transport):
+    """callback: psim_shard_run's in-library loop (exchange through the
+    psim_transport hook, gloo); torch: the split-phase ABI driven from Python."""
+    res = run_world(_gpu_worker, world, n, seed, L, transport)
     for r in range(world):
         assert res[r] == "ok", res[r]
 
@@ -211,3 +214,45 @@ def _nccl_world1(rank, world, port, q):
 def test_nccl_transport_world1():
     res = run_world(_nccl_world1, 1)
     assert res[0] == "ok", res[0]
+
+
+# ------------------------------------------------------------------ CPU: psim_transport callbacks
+def _cb_worker(rank, world, port, q):
+    """The gloo psim_transport callbacks, called as libpsim would call them
+    (ctypes function pointers, host buffers): region d of rank r's send goes
+    to rank d and lands at recv[recv_off[r]]; the all-reduce sums in place."""
+    try:
+        sys.path.insert(0, ROOT)
+        _init(rank, world, port)
+        import ctypes as C
+        from partisan_amd.shard import gloo_transport
+        tp, _keep = gloo_transport()
+        # rank r sends (r+1)*(d+1) words valued 100r+d to rank d != r
+        scnt = [0 if d == rank else (rank + 1) * (d + 1) for d in range(world)]
+        rcnt = [0 if s == rank else (s + 1) * (rank + 1) for s in range(world)]
+        soff = np.concatenate([[0], np.cumsum(scnt)]).astype(np.uint64)
+        roff = np.concatenate([[0], np.cumsum(rcnt)]).astype(np.uint64)
+        send = np.concatenate([np.full(c, 100 * rank + d, np.uint32) for d, c in enumerate(scnt)] + [np.zeros(1, np.uint32)])
+        recv = np.zeros(int(roff[-1]) + 1, np.uint32)
+        P32, P64 = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+        rc = tp.alltoallv(None, send.ctypes.data_as(P32), soff.ctypes.data_as(P64), recv.ctypes.data_as(P32),
+                          roff.ctypes.data_as(P64), world)
+        assert rc == 0
+        for s in range(world):
+            assert (recv[int(roff[s]):int(roff[s + 1])] == 100 * s + rank).all()
+        vals = np.array([rank + 1, 10 * rank], np.int64)
+        assert tp.allreduce(None, vals.ctypes.data_as(C.POINTER(C.c_int64)), 2) == 0
+        assert vals.tolist() == [sum(range(1, world + 1)), 10 * sum(range(world))]
+        import torch.distributed as dist
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_transport_callbacks_cpu(world):
+    res = run_world(_cb_worker, world, timeout=120)
+    for r in range(world):
+        assert res[r] == "ok", res[r]
