@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
+    p.add_argument("--csr", action="store_true", help="A/B: CSR slot rows instead of ELL rows (DESIGN.md 4)")
     p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
     p.add_argument("--all-on-device0", action="store_true",
@@ -188,7 +189,7 @@ def main():
         sim = sp.sim
     else:
         sp = None
-        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local)
+        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local, csr=args.csr)
         sim.load_overlay(rp, col)
     del rp, col
     root = 0

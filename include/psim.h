@@ -68,6 +68,11 @@ typedef struct psim_config {
  * receiver slot (the default, and what sharded handles always run).  Both
  * give identical results; the binned engine is the slower one on MI355X today. */
 #define PSIM_CFG_BINNED 1u
+/* The slot-scatter engine on one GPU keeps each vertex's slots as a fixed-width
+ * row (ELL, width = the maximum degree) when every degree is <= 8, so a
+ * vertex's inbox words are found without reading row pointers;
+ * PSIM_CFG_CSR keeps the CSR layout instead (same results; A/B and tests). */
+#define PSIM_CFG_CSR 2u
 
 /* Per-round counters, reduced on device (psim_step / psim_run). */
 typedef struct psim_round_stats {

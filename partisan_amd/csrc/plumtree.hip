@@ -304,6 +304,10 @@ __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint
 // chain (a workgroup holds few active vertices, each walked by one thread).
 constexpr uint32_t kFastDeg = 8;
 
+// ELL layout (a.ell = row width W <= kFastDeg, single GPU): slot s of v is
+// v*W + s, so the inbox words are loaded without first reading rowp -- two
+// dependent round trips per vertex instead of three; padding slots (col =
+// kNoPeer) never carry a word, a mask bit or an outgoing message.
 template <bool kOmit>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
                                                bool due, Ctr& c) {
@@ -360,7 +364,13 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
     }
     if (sent) {
         c.senders++;
-        c.degsum += deg;
+        uint32_t d = deg;
+        if (a.ell) {                                     // true degree: the non-padding slots
+            d = 0;
+#pragma unroll
+            for (uint32_t s = 0; s < kFastDeg; s++) d += (s < deg && cl[s] != kNoPeer) ? 1u : 0u;
+        }
+        c.degsum += d;
     }
     vst_store(a, v, st, x, c);
 }
@@ -368,6 +378,10 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 template <bool kOmit>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
+    if (a.ell) {
+        pt_vertex_fast<kOmit>(a, v, v * a.ell, a.ell, pend, due, c);
+        return;
+    }
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
 #ifndef PT_NO_FAST
@@ -705,8 +719,8 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
 __global__ void pt_origin_kernel(PtArgs a) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint32_t v = a.root;   // local index of the origin (only its owner launches this)
-    const uint32_t rs = a.rowp[v];
-    const uint32_t deg = a.rowp[v + 1] - rs;
+    const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
+    const uint32_t deg = a.ell ? a.ell : a.rowp[v + 1] - rs;   // ELL padding: no mask bits
     const uint4 st = a.vs[v];
     uint32_t eager = st.x, lazy = st.y, outst = st.z;
     uint32_t ep = st.w >> 24;
@@ -755,7 +769,7 @@ __global__ __launch_bounds__(kBlock) void pt_count_live_kernel(PtArgs a, unsigne
     for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.n; v += stride) {
         if (!a.ost[v] || !bit_alive(a.alive, a.v_lo + v)) continue;
         uint32_t m = a.vs[v].z;
-        const uint32_t rs = a.rowp[v];
+        const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
         while (m) {
             const uint32_t q = __ffs(m) - 1;
             m &= m - 1;
@@ -798,13 +812,16 @@ __global__ __launch_bounds__(kBlock) void pt_hash_state_kernel(PtArgs a, uint32_
     }
 }
 
-// In-flight words of the slot-scatter engine (one per receiver slot) -> out[1].
+// In-flight words of the slot-scatter engine (one per receiver slot) -> out[1],
+// keyed by the ABI (CSR) slot id in both layouts.
 __global__ __launch_bounds__(kBlock) void pt_hash_words_kernel(PtArgs a, unsigned long long E, unsigned long long* out) {
     unsigned long long sum = 0;
     const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
     for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < E; i += stride) {
         const uint32_t w = a.in_cur[i];
-        if (live_word(w, a.ctag)) sum += mix64(((a.slot_base + i) << 32) | abi_word(w));
+        if (!live_word(w, a.ctag)) continue;
+        const unsigned long long e = a.ell ? a.rowp[i / a.ell] + i % a.ell : i;   // ELL -> CSR slot id
+        sum += mix64(((a.slot_base + e) << 32) | abi_word(w));
     }
     sum = wave_sum(sum);
     if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&out[1], sum);

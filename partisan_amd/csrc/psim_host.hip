@@ -30,7 +30,9 @@ struct psim_handle {
     std::string err;
 
     uint32_t n = 0;
-    uint64_t E = 0;
+    uint64_t E = 0;                 // ABI (CSR) peer slots of this handle's vertices
+    uint64_t Ed = 0;                // device slots: E (CSR) or n * ell (ELL rows)
+    uint32_t ell = 0;               // ELL row width (single GPU, max degree <= kEllMax), 0 = CSR
     std::vector<uint64_t> h_rowp;   // slot layout
     std::vector<uint32_t> h_col;
     std::vector<uint32_t> h_memb;
@@ -267,6 +269,8 @@ void free_graph(psim_handle* h) {
     sh.send_base.clear();
     h->n = 0;
     h->E = 0;
+    h->Ed = 0;
+    h->ell = 0;
 }
 
 PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
@@ -295,6 +299,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.epoch8 = h->epoch & 0xFFu;
     a.root = h->root;
     a.omit = h->omit;
+    a.ell = h->ell;
     if (h->bin.rec_c) {
         const auto& b = h->bin;
         a.rec_c = b.rec_c;
@@ -341,7 +346,7 @@ hipError_t scrub_if_needed(psim_handle* h, uint64_t last) {
     if (h->bin.rec_c || last <= h->scrub + kTagSpan) return hipSuccess;
     const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
     for (int b = 0; b < 2; b++) {
-        const hipError_t e = launch_pt_scrub(h->in[b], h->E, keep, h->stream);
+        const hipError_t e = launch_pt_scrub(h->in[b], h->Ed, keep, h->stream);
         if (e != hipSuccess) return e;
     }
     h->scrub = h->round;
@@ -437,7 +442,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         psim_handle::Lane l;
         const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
         if (hipMalloc((void**)&l.vs, size_t(h->n) * 16) != hipSuccess ||
-            hipMalloc((void**)&l.in[0], h->E * 4) != hipSuccess || hipMalloc((void**)&l.in[1], h->E * 4) != hipSuccess ||
+            hipMalloc((void**)&l.in[0], h->Ed * 4) != hipSuccess || hipMalloc((void**)&l.in[1], h->Ed * 4) != hipSuccess ||
             hipMalloc((void**)&l.pend[0], ng) != hipSuccess || hipMalloc((void**)&l.pend[1], ng) != hipSuccess ||
             hipMalloc((void**)&l.ost, size_t(h->n) + 4) != hipSuccess) {
             void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
@@ -460,8 +465,8 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         auto& l = L[pick];
         const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
         HIPCHK(h, hipMemsetAsync(l.vs, 0, size_t(h->n) * 16, h->stream));
-        HIPCHK(h, hipMemsetAsync(l.in[0], 0, h->E * 4, h->stream));
-        HIPCHK(h, hipMemsetAsync(l.in[1], 0, h->E * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.in[0], 0, h->Ed * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(l.in[1], 0, h->Ed * 4, h->stream));
         HIPCHK(h, hipMemsetAsync(l.pend[0], 0, ng, h->stream));
         HIPCHK(h, hipMemsetAsync(l.pend[1], 0, ng, h->stream));
         HIPCHK(h, hipMemsetAsync(l.ost, 0, size_t(h->n) + 4, h->stream));
@@ -826,7 +831,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         while (d > 0 && u < uint32_t((uint64_t(n) * d) / W)) d--;
         return d;
     };
-    std::vector<uint32_t> rpl(size_t(nl) + 1), cl(El), rvl(El), mbl(nl), s2v(El);
+    std::vector<uint32_t> rpl(size_t(nl) + 1), cl(El), rvl(El), mbl(nl), s2v(El), cl_dev, rv_dev;
     for (uint32_t v = 0; v <= nl; v++) rpl[v] = uint32_t(rp[lo + v] - sbase);
     for (uint64_t e = 0; e < El; e++) { cl[e] = cc[sbase + e]; rvl[e] = rev[sbase + e]; }
     for (uint32_t v = 0; v < nl; v++) {
@@ -864,6 +869,30 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
                 if (cc[e] >= lo && cc[e] < hi) recvflat.push_back(uint32_t(rev[e] - sbase));
         }
     rbases[W] = recvflat.size();
+    // ELL rows: on one GPU with the slot-scatter engine and every
+    // degree <= kEllMax, slot s of v is v*W + s (W = the maximum degree), so
+    // the round kernel finds a vertex's inbox words without reading rowp
+    uint32_t ell = 0;
+    if (W == 1 && !(h->cfg.flags & (PSIM_CFG_BINNED | PSIM_CFG_CSR))) {
+        uint32_t mx = 0;
+        for (uint32_t v = 0; v < nl; v++) mx = std::max(mx, rpl[v + 1] - rpl[v]);
+        if (mx >= 1 && mx <= kEllMax) ell = mx;
+    }
+    const uint64_t Ed = ell ? uint64_t(nl) * ell : El;
+    if (ell) {
+        if (Ed >= 0xFFFFFFFFull) return fail(h, PSIM_EINVAL, "too many ELL slots (%llu)", (unsigned long long)Ed);
+        std::vector<uint32_t> ce(Ed, kNoPeer), re(Ed, 0u);
+        for (uint32_t v = 0; v < nl; v++)
+            for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) {
+                const uint32_t u = s2v[rvl[e]];                  // owner of the reverse slot
+                ce[uint64_t(v) * ell + (e - rpl[v])] = cl[e];
+                re[uint64_t(v) * ell + (e - rpl[v])] = u * ell + (rvl[e] - rpl[u]);
+            }
+        cl_dev.swap(ce);
+        rv_dev.swap(re);
+    }
+    const std::vector<uint32_t>& cl_up = ell ? cl_dev : cl;
+    const std::vector<uint32_t>& rv_up = ell ? rv_dev : rvl;
     // device arrays
     auto alloc = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 4); };
     const size_t nw = (size_t(n) + 31) / 32;
@@ -891,10 +920,10 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         bn.h_fslot.resize(size_t(bn.nf) + 1);
         for (uint32_t f = 0; f <= bn.nf; f++) bn.h_fslot[f] = rpl[std::min<uint64_t>(nl, uint64_t(f) << bn.fv_shift)];
     }
-    if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, El * 4) != hipSuccess ||
-        alloc((void**)&h->rev, El * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl) * 4) != hipSuccess ||
+    if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, Ed * 4) != hipSuccess ||
+        alloc((void**)&h->rev, Ed * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl) * 4) != hipSuccess ||
         alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
-        (!binned && (alloc((void**)&h->in[0], El * 4) != hipSuccess || alloc((void**)&h->in[1], El * 4) != hipSuccess ||
+        (!binned && (alloc((void**)&h->in[0], Ed * 4) != hipSuccess || alloc((void**)&h->in[1], Ed * 4) != hipSuccess ||
                      alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess)) ||
         (binned && (alloc((void**)&bn.rec_c, El * 8) != hipSuccess || alloc((void**)&bn.rec_f, El * 8) != hipSuccess ||
                     alloc((void**)&bn.cnt_c[0], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
@@ -916,12 +945,14 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     h->n = nl;
     h->E = El;
+    h->Ed = Ed;
+    h->ell = ell;
     sh.n_global = n;
     sh.v_lo = lo;
     sh.slot_base = sbase;
     HIPCHK(h, hipMemcpy(h->rowp, rpl.data(), (size_t(nl) + 1) * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->col, cl.data(), El * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->rev, rvl.data(), El * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->col, cl_up.data(), Ed * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->rev, rv_up.data(), Ed * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->memb, mbl.data(), size_t(nl) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
     // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..
@@ -934,8 +965,8 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         HIPCHK(h, hipMemcpy(bn.csub, bn.h_csub.data(), bn.h_csub.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(bn.fslot, bn.h_fslot.data(), (size_t(bn.nf) + 1) * 4, hipMemcpyHostToDevice));
     } else {
-        HIPCHK(h, hipMemset(h->in[0], 0, El * 4));
-        HIPCHK(h, hipMemset(h->in[1], 0, El * 4));
+        HIPCHK(h, hipMemset(h->in[0], 0, Ed * 4));
+        HIPCHK(h, hipMemset(h->in[1], 0, Ed * 4));
         HIPCHK(h, hipMemset(h->pend[0], 0, ng));
         HIPCHK(h, hipMemset(h->pend[1], 0, ng));
     }
@@ -1516,8 +1547,18 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     HIPCHK(hh, hipSetDevice(h->device));
     HIPCHK(hh, hipStreamSynchronize(h->stream));
     if (!h->bin.rec_c) {
-        HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
         const uint32_t tag = uint32_t(h->round + 1) & 0xFFu;   // words the next round reads
+        if (h->ell) {                                          // ELL rows -> ABI (CSR) slots
+            std::vector<uint32_t> d(h->Ed);
+            HIPCHK(hh, hipMemcpy(d.data(), h->in[h->par], h->Ed * 4, hipMemcpyDeviceToHost));
+            for (uint32_t v = 0; v < h->n; v++)
+                for (uint64_t e = h->h_rowp[v]; e < h->h_rowp[v + 1]; e++) {
+                    const uint32_t w = d[uint64_t(v) * h->ell + (e - h->h_rowp[v])];
+                    words[e] = live_word(w, tag) ? abi_word(w) : 0u;
+                }
+            return PSIM_OK;
+        }
+        HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
         for (uint64_t i = 0; i < h->E; i++) words[i] = live_word(words[i], tag) ? abi_word(words[i]) : 0u;
         return PSIM_OK;
     }
@@ -1771,7 +1812,7 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
     if (!h || !h->n || (k && (!src || !dst))) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    std::vector<uint32_t> bm((h->E + 31) / 32, 0u);
+    std::vector<uint32_t> bm((h->Ed + 31) / 32, 0u);
     size_t hit = 0;
     for (size_t i = 0; i < k; i++) {
         if (src[i] >= h->sh.n_global || dst[i] >= h->sh.n_global)
@@ -1781,7 +1822,8 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
         const auto b = h->h_col.begin() + h->h_rowp[u], e = h->h_col.begin() + h->h_rowp[u + 1];
         const auto it = std::lower_bound(b, e, dst[i]);
         if (it == e || *it != dst[i]) continue;        // not an overlay edge: nothing ever flows
-        const size_t s = size_t(it - h->h_col.begin());
+        size_t s = size_t(it - h->h_col.begin());
+        if (h->ell) s = size_t(u) * h->ell + (s - h->h_rowp[u]);   // device (ELL) slot
         bm[s >> 5] |= 1u << (s & 31);
         hit++;
     }
@@ -1800,7 +1842,7 @@ int psim_trace_hash(const psim_handle* h, uint64_t* out) {
     PtArgs a = make_args(h, h->par, 0, h->stats);
     const uint32_t rl = h->have_root ? h->root - h->sh.v_lo : 0xFFFFFFFFu;
     HIPCHK(hh, hipMemsetAsync(h->scratch, 0, 32, h->stream));
-    HIPCHK(hh, launch_pt_hash(a, h->serial != 0, rl < h->n ? rl : 0xFFFFFFFFu, h->bin.rec_c ? 0ull : h->E,
+    HIPCHK(hh, launch_pt_hash(a, h->serial != 0, rl < h->n ? rl : 0xFFFFFFFFu, h->bin.rec_c ? 0ull : h->Ed,
                               h->scratch, h->stream));
     unsigned long long r[4];
     HIPCHK(hh, hipMemcpyAsync(r, h->scratch, 32, hipMemcpyDeviceToHost, h->stream));

@@ -65,6 +65,8 @@ constexpr uint32_t kTagShift = 12;
 constexpr uint32_t kRoundShift = 20;
 constexpr uint32_t kMaxRound = 0xFFFu;
 constexpr uint32_t kTagSpan = 256;     // rounds before a tag repeats
+constexpr uint32_t kNoPeer = 0xFFFFFFFFu;   // col of an ELL padding slot
+constexpr uint32_t kEllMax = 8;              // widest ELL row (the round kernel's register-resident rows)
 __host__ __device__ inline uint32_t word_tag(uint32_t w) { return (w >> kTagShift) & 0xFFu; }
 // a word carries messages for the round whose tag is `tag`
 __host__ __device__ inline bool live_word(uint32_t w, uint32_t tag) { return (w & kFifoMask) && word_tag(w) == tag; }
@@ -104,6 +106,8 @@ struct PtArgs {
     uint32_t epoch8;                       // current tree epoch (low 8 bits)
     uint32_t root;                         // local index of the current heartbeat's origin
     uint32_t ctag, wtag;                   // round tags of the words read / written this round
+    uint32_t ell;                          // row width of the ELL slot layout (slot s of v = v*ell + s;
+                                           // padding slots: col = kNoPeer), 0 = CSR (rowp)
     const uint32_t* __restrict__ omit;     // [ceil(E/32)] omission faults over sender slots, or null
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}

@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import PSIM_ABI_VERSION, PSIM_CFG_BINNED, Config, RoundStats, check, lib
+from ._lib import PSIM_ABI_VERSION, PSIM_CFG_BINNED, PSIM_CFG_CSR, Config, RoundStats, check, lib
 
 _u8p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))    # noqa: E731
 _u16p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint16))  # noqa: E731
@@ -19,13 +19,14 @@ class Simulator:
     """Round-synchronous simulator of Partisan's gossip hot path."""
 
     def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0, rank=0, world=1,
-                 binned=False):
+                 binned=False, csr=False):
         """binned: route Plumtree messages through receiver bins on a single
         GPU instead of scattering receiver-slot words (PSIM_CFG_BINNED; same
-        results)."""
+        results).  csr: keep CSR slot rows in the slot-scatter
+        engine instead of fixed-width ELL rows (PSIM_CFG_CSR; same results)."""
+        flags = (PSIM_CFG_BINNED if binned else 0) | (PSIM_CFG_CSR if csr else 0)
         cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
-                     exchange_tick_rounds=exchange_tick_rounds, flags=PSIM_CFG_BINNED if binned else 0,
-                     _reserved=0, seed=seed)
+                     exchange_tick_rounds=exchange_tick_rounds, flags=flags, _reserved=0, seed=seed)
         h = C.c_void_p()
         check(lib().psim_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -107,7 +107,8 @@ def test_bench_config_10m_engines_agree_per_round():
     import partisan_amd as pa
     n = 10_000_000
     rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
-    sims = [pa.Simulator(lazy_tick_rounds=1, device=0),                   # bench's engine
+    sims = [pa.Simulator(lazy_tick_rounds=1, device=0),                   # bench's engine (ELL rows)
+            pa.Simulator(lazy_tick_rounds=1, device=0, csr=True),
             pa.Simulator(lazy_tick_rounds=1, device=0, binned=True)]
     for h in sims:
         h.load_overlay(rp, col)
@@ -122,7 +123,7 @@ def test_bench_config_10m_engines_agree_per_round():
         for k in KINDS + ("delivered_new", "active", "senders"):
             assert len({x[k] for x in st}) == 1, (rounds, k)
         th = [h.trace_hash() for h in sims]
-        assert th[0] == th[1], rounds
+        assert th[0] == th[1] == th[2], rounds
         if sum(st[0][k] for k in KINDS) == 0 or rounds > 40:
             break
     assert rounds == 17       # the 16 rounds of the flood + the silent one that shows quiescence

@@ -72,7 +72,7 @@ def test_oracle_replays_golden_trace(name):
     orc.close()
 
 
-ENGINES = {"slot_scatter": {}, "binned": {"binned": True}}
+ENGINES = {"slot_scatter": {}, "slot_scatter_csr": {"csr": True}, "binned": {"binned": True}}
 
 
 @pytest.mark.gpu

@@ -18,17 +18,18 @@ pytestmark = pytest.mark.gpu
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-@pytest.fixture(scope="module", params=["slot_scatter", "binned"])
+@pytest.fixture(scope="module", params=["slot_scatter", "slot_scatter_csr", "binned"])
 def psim(request):
     """partisan_amd with Simulator bound to one Plumtree engine: the
-    slot-scatter engine (the default, also what sharded handles run) and the
-    binned one (PSIM_CFG_BINNED) must both match the oracle."""
+    slot-scatter engine (the default: ELL rows when every degree is <= 8),
+    the same with CSR rows (PSIM_CFG_CSR; what sharded handles run) and the
+    binned one (PSIM_CFG_BINNED) must all match the oracle."""
     import functools
     import types
 
     import partisan_amd
     ns = types.SimpleNamespace(**{k: getattr(partisan_amd, k) for k in dir(partisan_amd) if not k.startswith("__")})
-    kw = {"slot_scatter": {}, "binned": {"binned": True}}
+    kw = {"slot_scatter": {}, "slot_scatter_csr": {"csr": True}, "binned": {"binned": True}}
     ns.Simulator = functools.partial(partisan_amd.Simulator, **kw[request.param])
     ns.engine = request.param
     return ns
@@ -281,7 +282,7 @@ def test_trace_hash_engines_agree_at_scale():
     """The engines at 2M peers, round by round, compared by digest only."""
     import partisan_amd
     rp, col = partisan_amd.overlay.random_regular(2_000_000, 5, 91)
-    sims = [partisan_amd.Simulator(), partisan_amd.Simulator(binned=True)]
+    sims = [partisan_amd.Simulator(), partisan_amd.Simulator(csr=True), partisan_amd.Simulator(binned=True)]
     for s in sims:
         s.load_overlay(rp, col)
     for root in (0, 12345):
