@@ -23,6 +23,10 @@ typedef struct {
     uint64_t slots;
     uint32_t hv_n;       /* hyparview vertices (hv_setup) */
     uint32_t dm_n;       /* demers vertices (demers_setup) */
+    uint32_t sc_n;       /* scamp / c3 vertices (scamp_setup, c3_setup) */
+    uint32_t fm_n;       /* full-membership nodes (fm_setup) */
+    uint32_t fm_words;   /* token bitmap words per node */
+    uint32_t cs_n;       /* causal vertices (causal_setup) */
 } sim_res;
 
 static ErlNifResourceType* SIM_RES;
@@ -547,6 +551,477 @@ static ERL_NIF_TERM nif_vclock(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     return rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"), t) : err(env, rc);
 }
 
+/* ---- shared helpers for the batch entry points ------------------------------ */
+
+/* A u32 binary copied to an aligned buffer (binary data has no alignment
+ * guarantee); *k = element count.  NULL on a bad size or no memory. */
+static uint32_t* u32_copy(ErlNifEnv* env, ERL_NIF_TERM t, size_t* k) {
+    ErlNifBinary b;
+    if (!enif_inspect_binary(env, t, &b) || b.size % 4) return NULL;
+    uint32_t* p = (uint32_t*)enif_alloc(b.size + 4);
+    if (p) memcpy(p, b.data, b.size);
+    *k = b.size / 4;
+    return p;
+}
+
+typedef int (*pair_fn)(psim_handle*, const uint32_t*, const uint32_t*, size_t);
+typedef int (*list_fn)(psim_handle*, const uint32_t*, size_t);
+
+/* Fn(Sim, As :: <<u32>>, Bs :: <<u32>>) -> ok, for the batched join / leave calls */
+static ERL_NIF_TERM pair_call(ErlNifEnv* env, const ERL_NIF_TERM argv[], pair_fn fn) {
+    sim_res* r;
+    size_t ka = 0, kb = 0;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    uint32_t* a = u32_copy(env, argv[1], &ka);
+    uint32_t* b = u32_copy(env, argv[2], &kb);
+    int rc = PSIM_EINVAL;
+    if (a && b && ka == kb) {
+        enif_mutex_lock(r->mu);
+        rc = fn(r->h, a, b, ka);
+        enif_mutex_unlock(r->mu);
+    }
+    if (a) enif_free(a);
+    if (b) enif_free(b);
+    if (!a || !b || ka != kb) return enif_make_badarg(env);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+static ERL_NIF_TERM list_call(ErlNifEnv* env, const ERL_NIF_TERM argv[], list_fn fn) {
+    sim_res* r;
+    size_t k = 0;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    uint32_t* a = u32_copy(env, argv[1], &k);
+    if (!a) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = fn(r->h, a, k);
+    enif_mutex_unlock(r->mu);
+    enif_free(a);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+static ERL_NIF_TERM kv_map(ErlNifEnv* env, const char* const* names, const uint64_t* vals, int n) {
+    ERL_NIF_TERM keys[24], vs[24], m;
+    for (int i = 0; i < n && i < 24; i++) {
+        keys[i] = mk_atom(env, names[i]);
+        vs[i] = enif_make_uint64(env, vals[i]);
+    }
+    enif_make_map_from_arrays(env, keys, vs, (size_t)n, &m);
+    return m;
+}
+
+static ERL_NIF_TERM stats_list(ErlNifEnv* env, ERL_NIF_TERM* maps, unsigned k) {
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (unsigned i = k; i > 0; i--) list = enif_make_list_cell(env, maps[i - 1], list);
+    return list;
+}
+
+static int get_rounds(ErlNifEnv* env, ERL_NIF_TERM t, unsigned* k) {
+    return enif_get_uint(env, t, k) && *k >= 1 && *k <= 65536;
+}
+
+/* ---- SCAMP (partisan_scamp_v{1,2}_membership_strategy) ----------------------- */
+
+/* scamp_setup(Sim, N, Version, C, PeriodicRounds) -> ok */
+static ERL_NIF_TERM nif_scamp_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, ver, c, per;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &ver) ||
+        !enif_get_uint(env, argv[3], &c) || !enif_get_uint(env, argv[4], &per))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_setup(r->h, n, ver, c, per);
+    if (rc == PSIM_OK) r->sc_n = n;
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* scamp_join(Sim, Joiners, Contacts) / scamp_leave(Sim, Vs, Leaving) -> ok; scamp_crash(Sim, Vs) -> ok */
+static ERL_NIF_TERM nif_scamp_join(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return pair_call(env, argv, psim_scamp_join);
+}
+static ERL_NIF_TERM nif_scamp_leave(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return pair_call(env, argv, psim_scamp_leave);
+}
+static ERL_NIF_TERM nif_scamp_crash(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return list_call(env, argv, psim_scamp_crash);
+}
+
+static ERL_NIF_TERM scamp_stats_term(ErlNifEnv* env, const psim_scamp_stats* s) {
+    static const char* const names[] = {"forward_subscription", "keep_subscription", "ping", "remove_subscription",
+                                        "replace_subscription", "bootstrap_remove_subscription", "dropped",
+                                        "processed", "draws", "stopped", "error", "pv_sum", "inview_sum", "resub",
+                                        "kernel_us"};
+    uint64_t v[15];
+    for (int k = 1; k <= 6; k++) v[k - 1] = s->sent[k];
+    v[6] = s->dropped; v[7] = s->processed; v[8] = s->draws; v[9] = s->stopped; v[10] = s->error;
+    v[11] = s->pv_sum; v[12] = s->inview_sum; v[13] = s->resub; v[14] = (uint64_t)(s->kernel_ms * 1000.0);
+    return kv_map(env, names, v, 15);
+}
+
+/* scamp_step(Sim, Rounds) -> {ok, [StatsMap]} */
+static ERL_NIF_TERM nif_scamp_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !get_rounds(env, argv[1], &k)) return enif_make_badarg(env);
+    psim_scamp_stats* st = (psim_scamp_stats*)enif_alloc(k * sizeof(psim_scamp_stats));
+    ERL_NIF_TERM* maps = (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM));
+    if (!st || !maps) {
+        if (st) enif_free(st);
+        if (maps) enif_free(maps);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = err(env, rc);
+    if (rc == PSIM_OK) {
+        for (unsigned i = 0; i < k; i++) maps[i] = scamp_stats_term(env, &st[i]);
+        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+    }
+    enif_free(st);
+    enif_free(maps);
+    return out;
+}
+
+/* scamp_views(Sim) -> {ok, PartialViews, PvLens, InViews, IvLens}: u32 rows of
+ * PSIM_SCAMP_PV_CAP / PSIM_SCAMP_IV_CAP ids in the reference's list order */
+static ERL_NIF_TERM nif_scamp_views(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r) || !r->sc_n) return enif_make_badarg(env);
+    const size_t n = r->sc_n;
+    ERL_NIF_TERM tp, tnp, ti, tni;
+    unsigned char* pv = enif_make_new_binary(env, n * PSIM_SCAMP_PV_CAP * 4, &tp);
+    unsigned char* npv = enif_make_new_binary(env, n * 4, &tnp);
+    unsigned char* iv = enif_make_new_binary(env, n * PSIM_SCAMP_IV_CAP * 4, &ti);
+    unsigned char* niv = enif_make_new_binary(env, n * 4, &tni);
+    uint32_t* a = (uint32_t*)enif_alloc(n * (PSIM_SCAMP_PV_CAP + PSIM_SCAMP_IV_CAP + 2) * 4);
+    if (!pv || !npv || !iv || !niv || !a) {
+        if (a) enif_free(a);
+        return err(env, PSIM_ENOMEM);
+    }
+    uint32_t *ap = a, *anp = ap + n * PSIM_SCAMP_PV_CAP, *ai = anp + n, *ani = ai + n * PSIM_SCAMP_IV_CAP;
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_get_views(r->h, ap, anp, ai, ani, n);
+    enif_mutex_unlock(r->mu);
+    if (rc == PSIM_OK) {
+        memcpy(pv, ap, n * PSIM_SCAMP_PV_CAP * 4);
+        memcpy(npv, anp, n * 4);
+        memcpy(iv, ai, n * PSIM_SCAMP_IV_CAP * 4);
+        memcpy(niv, ani, n * 4);
+    }
+    enif_free(a);
+    if (rc != PSIM_OK) return err(env, rc);
+    ERL_NIF_TERM out[5] = {mk_atom(env, "ok"), tp, tnp, ti, tni};
+    return enif_make_tuple_from_array(env, out, 5);
+}
+
+/* ---- full membership (partisan_full_membership_strategy) ---------------------- */
+
+/* fm_setup(Sim, N, PeriodicRounds, MaxTokens) -> ok */
+static ERL_NIF_TERM nif_fm_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, per, tok;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &per) ||
+        !enif_get_uint(env, argv[3], &tok))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_setup(r->h, n, per, tok);
+    if (rc == PSIM_OK) { r->fm_n = n; r->fm_words = (tok + 63) / 64; }
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+static ERL_NIF_TERM nif_fm_join(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return pair_call(env, argv, psim_fm_join);
+}
+static ERL_NIF_TERM nif_fm_leave(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return pair_call(env, argv, psim_fm_leave);
+}
+
+/* fm_step(Sim, Rounds) -> {ok, [StatsMap]} */
+static ERL_NIF_TERM nif_fm_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !get_rounds(env, argv[1], &k)) return enif_make_badarg(env);
+    psim_fm_stats* st = (psim_fm_stats*)enif_alloc(k * sizeof(psim_fm_stats));
+    ERL_NIF_TERM* maps = (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM));
+    if (!st || !maps) {
+        if (st) enif_free(st);
+        if (maps) enif_free(maps);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = err(env, rc);
+    if (rc == PSIM_OK) {
+        static const char* const names[] = {"sent", "processed", "merges", "updates", "inflight", "member_sum",
+                                            "kernel_us"};
+        for (unsigned i = 0; i < k; i++) {
+            const uint64_t v[7] = {st[i].sent, st[i].processed, st[i].merges, st[i].updates, st[i].inflight,
+                                   st[i].member_sum, (uint64_t)(st[i].kernel_ms * 1000.0)};
+            maps[i] = kv_map(env, names, v, 7);
+        }
+        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+    }
+    enif_free(st);
+    enif_free(maps);
+    return out;
+}
+
+/* fm_state(Sim) -> {ok, Known, Removed, Alive}: per node the u64 token
+ * bitmaps of its state_orset (known / removed) and one alive byte */
+static ERL_NIF_TERM nif_fm_state(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r) || !r->fm_n) return enif_make_badarg(env);
+    const size_t n = r->fm_n, w = r->fm_words;
+    ERL_NIF_TERM tk, trm, ta;
+    unsigned char* kb = enif_make_new_binary(env, n * w * 8, &tk);
+    unsigned char* rb = enif_make_new_binary(env, n * w * 8, &trm);
+    unsigned char* ab = enif_make_new_binary(env, n, &ta);
+    uint64_t* tmp = (uint64_t*)enif_alloc(2 * n * w * 8 + 8);
+    if (!kb || !rb || !ab || !tmp) {
+        if (tmp) enif_free(tmp);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_get_state(r->h, tmp, tmp + n * w, ab, n, w);
+    enif_mutex_unlock(r->mu);
+    if (rc == PSIM_OK) {
+        memcpy(kb, tmp, n * w * 8);
+        memcpy(rb, tmp + n * w, n * w * 8);
+    }
+    enif_free(tmp);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple4(env, mk_atom(env, "ok"), tk, trm, ta);
+}
+
+/* ---- C3: Plumtree repair over churning SCAMP v2 ------------------------------- */
+
+/* c3_setup(Sim, N, C, PeriodicRounds) -> ok */
+static ERL_NIF_TERM nif_c3_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, c, per;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &c) ||
+        !enif_get_uint(env, argv[3], &per))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_c3_setup(r->h, n, c, per);
+    if (rc == PSIM_OK) r->sc_n = n;
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+static ERL_NIF_TERM nif_c3_join(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return pair_call(env, argv, psim_c3_join);
+}
+static ERL_NIF_TERM nif_c3_crash(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return list_call(env, argv, psim_c3_crash);
+}
+
+/* c3_heartbeat(Sim, Root) -> {ok, Monotonic} */
+static ERL_NIF_TERM nif_c3_heartbeat(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root)) return enif_make_badarg(env);
+    uint32_t mono = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_c3_heartbeat(r->h, root, &mono);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_uint(env, mono));
+}
+
+/* c3_step(Sim, Rounds) -> {ok, [StatsMap]} (both protocols' counters) */
+static ERL_NIF_TERM nif_c3_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !get_rounds(env, argv[1], &k)) return enif_make_badarg(env);
+    psim_c3_stats* st = (psim_c3_stats*)enif_alloc(k * sizeof(psim_c3_stats));
+    ERL_NIF_TERM* maps = (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM));
+    if (!st || !maps) {
+        if (st) enif_free(st);
+        if (maps) enif_free(maps);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_c3_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = err(env, rc);
+    if (rc == PSIM_OK) {
+        static const char* const names[] = {"broadcast", "prune", "i_have", "ignored_i_have", "graft", "pt_dropped",
+                                            "delivered_new", "updates", "delivered_live", "live", "outstanding_live",
+                                            "pt_kernel_us"};
+        for (unsigned i = 0; i < k; i++) {
+            const psim_c3_stats* x = &st[i];
+            const uint64_t v[12] = {x->pt_sent[1], x->pt_sent[2], x->pt_sent[3], x->pt_sent[4], x->pt_sent[5],
+                                    x->pt_dropped, x->delivered_new, x->updates, x->delivered_live, x->live,
+                                    x->outstanding_live, (uint64_t)(x->pt_kernel_ms * 1000.0)};
+            maps[i] = enif_make_tuple2(env, kv_map(env, names, v, 12), scamp_stats_term(env, &x->scamp));
+        }
+        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+    }
+    enif_free(st);
+    enif_free(maps);
+    return out;
+}
+
+/* ---- causal delivery (partisan_causality_backend) ----------------------------- */
+
+/* causal_setup(Sim, N, M, Period, DMax, Redeliver) -> ok */
+static ERL_NIF_TERM nif_causal_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, m, per, dmax, red;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &m) ||
+        !enif_get_uint(env, argv[3], &per) || !enif_get_uint(env, argv[4], &dmax) || !enif_get_uint(env, argv[5], &red))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_causal_setup(r->h, n, m, per, dmax, red);
+    if (rc == PSIM_OK) r->cs_n = n;
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* causal_step(Sim, Rounds) -> {ok, [StatsMap]} */
+static ERL_NIF_TERM nif_causal_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !get_rounds(env, argv[1], &k)) return enif_make_badarg(env);
+    psim_causal_stats* st = (psim_causal_stats*)enif_alloc(k * sizeof(psim_causal_stats));
+    ERL_NIF_TERM* maps = (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM));
+    if (!st || !maps) {
+        if (st) enif_free(st);
+        if (maps) enif_free(maps);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_causal_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = err(env, rc);
+    if (rc == PSIM_OK) {
+        static const char* const names[] = {"emitted", "received", "delivered", "checks", "buffered", "kernel_us"};
+        for (unsigned i = 0; i < k; i++) {
+            const uint64_t v[6] = {st[i].emitted, st[i].received, st[i].delivered, st[i].checks, st[i].buffered,
+                                   (uint64_t)(st[i].kernel_ms * 1000.0)};
+            maps[i] = kv_map(env, names, v, 6);
+        }
+        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+    }
+    enif_free(st);
+    enif_free(maps);
+    return out;
+}
+
+/* causal_clocks(Sim) -> {ok, Lanes :: <<u32 x 64 per vertex>>, Self :: <<u32 per vertex>>} */
+static ERL_NIF_TERM nif_causal_clocks(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r) || !r->cs_n) return enif_make_badarg(env);
+    const size_t n = r->cs_n;
+    ERL_NIF_TERM tl, ts;
+    unsigned char* lb = enif_make_new_binary(env, n * PSIM_VC_LANES * 4, &tl);
+    unsigned char* sb = enif_make_new_binary(env, n * 4, &ts);
+    uint32_t* tmp = (uint32_t*)enif_alloc(n * (PSIM_VC_LANES + 1) * 4);
+    if (!lb || !sb || !tmp) {
+        if (tmp) enif_free(tmp);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_causal_get_clocks(r->h, tmp, tmp + n * PSIM_VC_LANES, n);
+    enif_mutex_unlock(r->mu);
+    if (rc == PSIM_OK) {
+        memcpy(lb, tmp, n * PSIM_VC_LANES * 4);
+        memcpy(sb, tmp + n * PSIM_VC_LANES, n * 4);
+    }
+    enif_free(tmp);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), tl, ts);
+}
+
+/* ---- vertex sharding with the exchange inside the library (RCCL) ------------- */
+
+/* rccl_unique_id() -> {ok, <<_:1024>>}: on one rank; ship it to the others */
+static ERL_NIF_TERM nif_rccl_unique_id(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    (void)argv;
+    ERL_NIF_TERM t;
+    unsigned char* b = enif_make_new_binary(env, PSIM_RCCL_ID_BYTES, &t);
+    if (!b) return err(env, PSIM_ENOMEM);
+    int rc = psim_rccl_unique_id(b);
+    return rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"), t) : err(env, rc);
+}
+
+/* shard_init_rccl(Sim, Rank, World, UniqueId) -> ok   (before load_csr) */
+static ERL_NIF_TERM nif_shard_init_rccl(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned rank, world;
+    ErlNifBinary id;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &rank) || !enif_get_uint(env, argv[2], &world) ||
+        !enif_inspect_binary(env, argv[3], &id) || id.size != PSIM_RCCL_ID_BYTES)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_shard_init_rccl(r->h, (int)rank, (int)world, id.data);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* shard_broadcast(Sim, Root) -> {ok, Monotonic}   (collective over the ranks) */
+static ERL_NIF_TERM nif_shard_broadcast(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root)) return enif_make_badarg(env);
+    uint32_t mono = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_shard_broadcast_x(r->h, root, &mono);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_uint(env, mono));
+}
+
+/* shard_run(Sim, MaxRounds) -> {ok, Rounds, [StatsMap], {FabricBytes, ExchangeUs, KernelUs}}
+ * (collective: global counters, stops at global quiescence) */
+static ERL_NIF_TERM nif_shard_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
+    enum { CAP = 4096 };
+    psim_round_stats* st = (psim_round_stats*)enif_alloc(CAP * sizeof(psim_round_stats));
+    if (!st) return err(env, PSIM_ENOMEM);
+    uint32_t ran = 0;
+    psim_exchange_stats xs;
+    enif_mutex_lock(r->mu);
+    int rc = psim_shard_run(r->h, maxr, st, CAP, &ran, &xs);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (uint32_t i = ran < CAP ? ran : CAP; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    ERL_NIF_TERM x = enif_make_tuple3(env, enif_make_uint64(env, xs.fabric_bytes),
+                                      enif_make_uint64(env, (uint64_t)(xs.exchange_ms * 1000.0)),
+                                      enif_make_uint64(env, (uint64_t)(xs.kernel_ms * 1000.0)));
+    ERL_NIF_TERM out[4] = {mk_atom(env, "ok"), enif_make_uint(env, ran), list, x};
+    return enif_make_tuple_from_array(env, out, 4);
+}
+
 static ErlNifFunc funcs[] = {
     {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -569,6 +1044,29 @@ static ErlNifFunc funcs[] = {
     {"demers_setup", 5, nif_demers_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"demers_run", 2, nif_demers_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"vclock", 4, nif_vclock, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_setup", 5, nif_scamp_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_join", 3, nif_scamp_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_leave", 3, nif_scamp_leave, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_crash", 2, nif_scamp_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_step", 2, nif_scamp_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_views", 1, nif_scamp_views, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_setup", 4, nif_fm_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_join", 3, nif_fm_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_leave", 3, nif_fm_leave, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_step", 2, nif_fm_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_state", 1, nif_fm_state, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_setup", 4, nif_c3_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_join", 3, nif_c3_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_crash", 2, nif_c3_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_heartbeat", 2, nif_c3_heartbeat, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_step", 2, nif_c3_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"causal_setup", 6, nif_causal_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"causal_step", 2, nif_causal_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"causal_clocks", 1, nif_causal_clocks, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"rccl_unique_id", 0, nif_rccl_unique_id, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"shard_init_rccl", 4, nif_shard_init_rccl, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"shard_broadcast", 2, nif_shard_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"shard_run", 2, nif_shard_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

@@ -308,15 +308,21 @@ constexpr uint32_t kFastDeg = 8;
 // v*W + s, so the inbox words are loaded without first reading rowp -- two
 // dependent round trips per vertex instead of three; padding slots (col =
 // kNoPeer) never carry a word, a mask bit or an outgoing message.
-template <bool kOmit>
+// kLdsWords: the round kernel already gathered the vertex's live inbox words
+// into LDS (pt_round_ell_body) and `lw` points at them.
+template <bool kOmit, bool kLdsWords = false>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
-                                               bool due, Ctr& c) {
+                                               bool due, Ctr& c, const uint32_t* lw = nullptr) {
     uint32_t w[kFastDeg];
     uint32_t any = 0;
 #pragma unroll
     for (uint32_t s = 0; s < kFastDeg; s++) {
-        w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
-        if (!live_word(w[s], a.ctag)) w[s] = 0u;       // stale: consumed in an earlier round
+        if (kLdsWords) {
+            w[s] = (pend && s < deg) ? lw[s] : 0u;
+        } else {
+            w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
+            if (!live_word(w[s], a.ctag)) w[s] = 0u;   // stale: consumed in an earlier round
+        }
         any |= w[s];
     }
     pend = any != 0;
@@ -490,6 +496,94 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
     pt_round_body<kOmit>(a);
 }
 
+// ELL rows (a.ell = W): the workgroup first reads the inbox words of every
+// flagged 16-vertex group of its chunk with ALL its threads -- consecutive
+// words, one coalesced sweep (a group's words are 16 W consecutive words) --
+// keeps the live ones in LDS and marks the vertices that have any; only those
+// (and, on a tick round, the vertices holding outstanding rows) are handed to
+// threads, which then need one round trip (state, peer ids, reverse slots)
+// instead of a per-vertex dependent load of words that are mostly stale
+// (a flagged group typically has one or two receivers in the sparse rounds).
+template <bool kOmit>
+__device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
+    extern __shared__ uint32_t wbuf[];                 // [kChunkV * W] the chunk's live words (flagged groups)
+    __shared__ uint32_t actm[kChunkV / 32];            // vertices with live words
+    __shared__ uint32_t duem[kChunkV / 32];            // vertices holding outstanding rows on a tick round
+    __shared__ uint16_t cand[kChunkV];
+    __shared__ uint8_t glist[kChunkV >> kGroupShift];
+    __shared__ uint32_t ncand, ngrp;
+    constexpr uint32_t kGroups = kChunkV >> kGroupShift, kGV = 1u << kGroupShift;
+    const uint32_t t = threadIdx.x;
+    if (a.msgs3) {
+        if (blockIdx.x == 0 && t == 0) a.msgs3[a.mnext] = 0;
+        if (a.msgs3[a.mprev] == 0 && !(a.tick && *a.ost_total > 0)) return;
+    }
+    const uint32_t W = a.ell, base = blockIdx.x * kChunkV;
+    const uint32_t nv = min(kChunkV, a.n - base);
+    if (t < kChunkV / 32) {
+        actm[t] = 0;
+        duem[t] = 0;
+    }
+    if (t == 0) ncand = ngrp = 0;
+    __syncthreads();
+    if (t < kGroups && t * kGV < nv) {
+        const uint32_t g = (base >> kGroupShift) + t;
+        if (a.pend_cur[g]) {
+            a.pend_cur[g] = 0;
+            glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
+        }
+    }
+    if (a.tick && *a.ost_total > 0 && 4 * t < nv) {
+        uint32_t w;
+        const uint32_t v0 = base + 4 * t;
+        if (v0 + 4 <= a.n) w = *reinterpret_cast<const uint32_t*>(a.ost + v0);
+        else { w = 0; for (uint32_t i = 0; v0 + i < a.n; i++) w |= uint32_t(a.ost[v0 + i]) << (8 * i); }
+        uint32_t d = 0;
+        for (int i = 0; i < 4; i++) d |= ((w >> (8 * i)) & 0xFFu) ? (1u << i) : 0u;
+        if (d) atomicOr(&duem[(4 * t) >> 5], d << ((4 * t) & 31));
+    }
+    __syncthreads();
+    const uint32_t ng = ngrp, gw = kGV * W;
+    const uint32_t lim = nv * W;                        // chunk-local words that exist
+    for (uint32_t i = t; i < ng * gw; i += kBlock) {
+        const uint32_t lwi = glist[i / gw] * gw + i % gw;   // chunk-local word = local vertex * W + slot
+        if (lwi >= lim) continue;
+        uint32_t w = a.in_cur[base * W + lwi];
+        if (!live_word(w, a.ctag)) w = 0u;
+        wbuf[lwi] = w;
+        if (w) {
+            const uint32_t lv = lwi / W;
+            atomicOr(&actm[lv >> 5], 1u << (lv & 31));
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t v4 = 4 * t;
+        const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & 0xFu, dm = (duem[v4 >> 5] >> (v4 & 31)) & 0xFu;
+        const uint32_t m = am | dm;
+        if (m) {
+            uint32_t k = atomicAdd(&ncand, (uint32_t)__popc(m));
+            for (uint32_t i = 0; i < 4; i++)
+                if (m & (1u << i)) cand[k++] = (uint16_t)(((v4 + i) << 2) | (((am >> i) & 1u) << 1) | ((dm >> i) & 1u));
+        }
+    }
+    __syncthreads();
+    const uint32_t nc = ncand;
+    if (nc == 0) return;                                // uniform: idle chunk
+    Ctr c;
+    c.zero();
+    for (uint32_t i = t; i < nc; i += kBlock) {
+        const uint32_t x = cand[i], lv = x >> 2;
+        pt_vertex_fast<kOmit, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W]);
+    }
+    flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+}
+
+template <bool kOmit>
+__global__ __launch_bounds__(kBlock) void pt_round_ell_kernel(PtArgs a) {
+    pt_round_ell_body<kOmit>(a);
+}
+
 // Multi-root rounds: one launch runs the round of every
 // non-quiescent heartbeat lane, blockIdx.y = lane, each lane's arguments in
 // device memory -- the lanes' sparse rounds share the chip instead of
@@ -497,6 +591,11 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
 template <bool kOmit>
 __global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __restrict__ args) {
     pt_round_body<kOmit>(args[blockIdx.y]);
+}
+
+template <bool kOmit>
+__global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs* __restrict__ args) {
+    pt_round_ell_body<kOmit>(args[blockIdx.y]);
 }
 
 // ---------------------------------------------------------------------------
@@ -976,6 +1075,14 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(pb_round_kernel, dim3(a.nf < 4096u ? a.nf : 4096u), dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
+    if (a.ell) {
+        const size_t lds = size_t(kChunkV) * a.ell * 4;
+        if (a.omit)
+            hipLaunchKernelGGL(pt_round_ell_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL(pt_round_ell_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
+        return hipGetLastError();
+    }
     if (a.omit)
         hipLaunchKernelGGL(pt_round_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     else
@@ -985,6 +1092,14 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
 
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s) {
     const dim3 grid(grid_chunks(a0.n), nlanes);
+    if (a0.ell) {
+        const size_t lds = size_t(kChunkV) * a0.ell * 4;
+        if (a0.omit)
+            hipLaunchKernelGGL(pt_round_ell_lanes_kernel<true>, grid, dim3(kBlock), lds, s, d_args);
+        else
+            hipLaunchKernelGGL(pt_round_ell_lanes_kernel<false>, grid, dim3(kBlock), lds, s, d_args);
+        return hipGetLastError();
+    }
     if (a0.omit)
         hipLaunchKernelGGL(pt_round_lanes_kernel<true>, grid, dim3(kBlock), 0, s, d_args);
     else

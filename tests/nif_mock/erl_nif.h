@@ -1,7 +1,11 @@
-/* Declarations-only stand-in for erts' erl_nif.h, used by
- * tests/test_abi.py to type-check erl/c_src/partisan_gpu_sim_nif.c with
- * `gcc -fsyntax-only` in an image without erts.  Signatures follow the
- * documented erl_nif API (erts >= 2.14); nothing here is linked or run. */
+/* Stand-in for erts' erl_nif.h (this image has no erts), used two ways:
+ *   * tests/test_abi.py type-checks erl/c_src/partisan_gpu_sim_nif.c with
+ *     `gcc -fsyntax-only` against these declarations;
+ *   * tests/nif_mock/mock_erts.c implements them over a small term arena so
+ *     tests/nif_harness.c can link the real NIF shim with libpsim.so and call
+ *     its function table as the BEAM would (GPU test, tests/test_nif_harness.py).
+ * Signatures follow the documented erl_nif API (erts >= 2.14).  ERL_NIF_INIT
+ * here exposes the shim's function table and load callback to the harness. */
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -25,6 +29,7 @@ int enif_make_existing_atom(ErlNifEnv*, const char*, ERL_NIF_TERM*, ErlNifCharEn
 ERL_NIF_TERM enif_make_atom(ErlNifEnv*, const char*);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple3(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
+ERL_NIF_TERM enif_make_tuple4(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple5(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv*, const ERL_NIF_TERM[], unsigned);
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv*);
@@ -52,5 +57,10 @@ ErlNifMutex* enif_mutex_create(char*);
 void enif_mutex_destroy(ErlNifMutex*);
 void enif_mutex_lock(ErlNifMutex*);
 void enif_mutex_unlock(ErlNifMutex*);
-#define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD) \
-    const void* nif_init(void) { (void)(FUNCS); (void)(LOAD); return 0; }
+typedef int (*mock_nif_load_fn)(ErlNifEnv*, void**, ERL_NIF_TERM);
+#define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                     \
+    const ErlNifFunc* mock_nif_table(int* n, mock_nif_load_fn* load) {                  \
+        *n = (int)(sizeof(FUNCS) / sizeof((FUNCS)[0]));                                 \
+        *load = (LOAD);                                                                 \
+        return (FUNCS);                                                                 \
+    }

@@ -5,7 +5,7 @@
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -u -m pytest tests/test_plumtree_gpu.py tests/test_golden_traces.py tests/test_shard.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pt_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_plumtree_gpu.py tests/test_golden_traces.py tests/test_shard.py tests/test_configs_at_scale.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pt_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/pt_tests.log
 [ $rc -le 1 ] || exit $rc
 line() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2],round(d['ms_per_step'],3),round(d['roofline']['avg_launch_us'],1),round(d['roofline']['frac'],4))" "$@"; }
