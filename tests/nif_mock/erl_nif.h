@@ -59,8 +59,8 @@ void enif_mutex_lock(ErlNifMutex*);
 void enif_mutex_unlock(ErlNifMutex*);
 typedef int (*mock_nif_load_fn)(ErlNifEnv*, void**, ERL_NIF_TERM);
 #define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                     \
-    const ErlNifFunc* mock_nif_table(int* n, mock_nif_load_fn* load) {                  \
-        *n = (int)(sizeof(FUNCS) / sizeof((FUNCS)[0]));                                 \
-        *load = (LOAD);                                                                 \
+    const ErlNifFunc* mock_nif_table(int* nfuncs_out, mock_nif_load_fn* load_out) {    \
+        *nfuncs_out = (int)(sizeof(FUNCS) / sizeof((FUNCS)[0]));                        \
+        *load_out = (LOAD);                                                             \
         return (FUNCS);                                                                 \
     }

@@ -1,0 +1,252 @@
+/* nif_harness.c -- drives the real Erlang NIF shim (erl/c_src/partisan_gpu_sim_nif.c)
+ * as the BEAM would: load/3, then calls through its ErlNifFunc table with
+ * terms of the mock term store (tests/nif_mock/mock_erts.c), linked with
+ * libpsim.so.  TEST INFRASTRUCTURE (tests/test_nif_harness.py runs it on the
+ * GPU box and checks its JSON report against the Python path).
+ *
+ * Scenario: config C2 in small (HyParView sequential joins + shuffle
+ * periods, then a Plumtree heartbeat over the active views), Demers, SCAMP
+ * v2 join waves, full membership, C3 churn, causal delivery, vclock ops and
+ * the vertex-sharded run with the in-library RCCL exchange at world 1. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mock_erts.h"
+
+static const ErlNifFunc* g_funcs;
+static int g_nfuncs;
+static ErlNifEnv* const ENV = (ErlNifEnv*)0x1;   /* the shim never dereferences it */
+
+static ERL_NIF_TERM call(const char* name, unsigned arity, const ERL_NIF_TERM* argv) {
+    for (int i = 0; i < g_nfuncs; i++)
+        if (!strcmp(g_funcs[i].name, name) && g_funcs[i].arity == arity) return g_funcs[i].fptr(ENV, (int)arity, argv);
+    fprintf(stderr, "no NIF %s/%u\n", name, arity);
+    exit(2);
+}
+
+static void die(const char* what, ERL_NIF_TERM t) {
+    fprintf(stderr, "FAIL %s: ", what);
+    if (mock_is_badarg(t)) fprintf(stderr, "badarg\n");
+    else if (mock_tuple_arity(t) == 2 && mock_is_atom(mock_elem(t, 0), "error"))
+        fprintf(stderr, "{error, %s}\n", mock_atom_name(mock_elem(t, 1)));
+    else fprintf(stderr, "unexpected term\n");
+    exit(1);
+}
+
+static void want_ok(const char* what, ERL_NIF_TERM t) {
+    if (!mock_is_atom(t, "ok")) die(what, t);
+}
+
+/* {ok, ...} -> the tuple */
+static ERL_NIF_TERM want_ok_tuple(const char* what, ERL_NIF_TERM t) {
+    if (mock_tuple_arity(t) < 2 || !mock_is_atom(mock_elem(t, 0), "ok")) die(what, t);
+    return t;
+}
+
+#define A(...) ((const ERL_NIF_TERM[]){__VA_ARGS__})
+
+static ERL_NIF_TERM new_sim(uint64_t seed) {
+    const char* k[] = {"seed", "lazy_tick_rounds", "device"};
+    const uint64_t v[] = {seed, 1, 0};
+    ERL_NIF_TERM r = want_ok_tuple("new", call("new", 1, A(mock_map(3, k, v))));
+    return mock_elem(r, 1);
+}
+
+static ERL_NIF_TERM u32s(const uint32_t* a, size_t n) { return mock_bin(a, n * 4); }
+
+static uint32_t lcg(uint64_t* s) {
+    *s = *s * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint32_t)(*s >> 33);
+}
+
+int main(void) {
+    mock_nif_load_fn load;
+    g_funcs = mock_nif_table(&g_nfuncs, &load);
+    if (load(ENV, NULL, 0) != 0) {
+        fprintf(stderr, "FAIL load\n");
+        return 1;
+    }
+    printf("{");
+    /* ---- C2 in small: HyParView overlay, then a Plumtree heartbeat -------- */
+    {
+        const uint32_t n = 2000;
+        ERL_NIF_TERM sim = new_sim(0x5EED0002ull);
+        const char* hk[] = {"shuffle_rounds", "promotion_rounds"};
+        const uint64_t hv[] = {10, 5};
+        want_ok("hv_setup", call("hv_setup", 3, A(sim, mock_uint(n), mock_map(2, hk, hv))));
+        uint64_t s = 2;
+        for (uint32_t i = 1; i < n; i++) {       /* vertex i joins a contact in [0, i), one join per round */
+            const uint32_t c = lcg(&s) % i;
+            want_ok("hv_join", call("hv_join", 3, A(sim, u32s(&i, 1), u32s(&c, 1))));
+            want_ok_tuple("hv_step", call("hv_step", 2, A(sim, mock_uint(1))));
+        }
+        want_ok_tuple("hv_step", call("hv_step", 2, A(sim, mock_uint(100))));   /* 10 shuffle periods */
+        ERL_NIF_TERM views = want_ok_tuple("hv_views", call("hv_views", 1, A(sim)));
+        size_t na_sz, nl_sz;
+        const uint32_t* act = (const uint32_t*)mock_bin_data(mock_elem(views, 1), &na_sz);
+        const unsigned char* alen = mock_bin_data(mock_elem(views, 2), &nl_sz);
+        uint64_t* rp = (uint64_t*)calloc(n + 1, 8);
+        uint32_t* col = (uint32_t*)calloc((size_t)n * 8, 4);
+        uint64_t e = 0;
+        for (uint32_t v = 0; v < n; v++) {       /* active views minus self = the members plumtree sees */
+            for (uint32_t j = 0; j < alen[v]; j++)
+                if (act[v * 8 + j] != v) col[e++] = act[v * 8 + j];
+            rp[v + 1] = e;
+        }
+        want_ok("load_csr", call("load_csr", 3, A(sim, mock_bin(rp, (n + 1) * 8), u32s(col, e))));
+        ERL_NIF_TERM bc = want_ok_tuple("broadcast", call("broadcast", 2, A(sim, mock_uint(0))));
+        ERL_NIF_TERM run = want_ok_tuple("run", call("run", 2, A(sim, mock_uint(1000))));
+        const uint64_t rounds = mock_int(mock_elem(run, 1));
+        ERL_NIF_TERM stats = mock_elem(run, 2);
+        uint64_t bsum = 0, x;
+        for (size_t i = 0; i < mock_list_len(stats); i++)
+            if (mock_map_get(mock_list_nth(stats, i), "broadcast", &x)) bsum += x;
+        ERL_NIF_TERM dl = want_ok_tuple("delivered", call("delivered", 1, A(sim)));
+        size_t dsz;
+        const unsigned char* d = mock_bin_data(mock_elem(dl, 1), &dsz);
+        uint64_t got = 0;
+        for (size_t i = 0; i < dsz; i++) got += d[i];
+        ERL_NIF_TERM th = mock_elem(want_ok_tuple("trace_hash", call("trace_hash", 1, A(sim))), 1);
+        printf("\"c2\": {\"n\": %u, \"edges\": %llu, \"mono\": %llu, \"rounds\": %llu, \"delivered\": %llu, "
+               "\"broadcasts\": %llu, \"trace\": [\"%llu\", \"%llu\", \"%llu\", \"%llu\"]}",
+               n, (unsigned long long)e, (unsigned long long)mock_int(mock_elem(bc, 1)), (unsigned long long)rounds,
+               (unsigned long long)got, (unsigned long long)bsum, (unsigned long long)mock_int(mock_elem(th, 0)),
+               (unsigned long long)mock_int(mock_elem(th, 1)), (unsigned long long)mock_int(mock_elem(th, 2)),
+               (unsigned long long)mock_int(mock_elem(th, 3)));
+        /* the same overlay, vertex-sharded at world 1 with the library's own RCCL communicator */
+        ERL_NIF_TERM sim7 = new_sim(0x5EED0002ull);
+        ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);
+        want_ok("shard_init_rccl", call("shard_init_rccl", 4, A(sim7, mock_uint(0), mock_uint(1), id)));
+        want_ok("load_csr", call("load_csr", 3, A(sim7, mock_bin(rp, (n + 1) * 8), u32s(col, e))));
+        want_ok_tuple("shard_broadcast", call("shard_broadcast", 2, A(sim7, mock_uint(0))));
+        ERL_NIF_TERM sr = want_ok_tuple("shard_run", call("shard_run", 2, A(sim7, mock_uint(1000))));
+        ERL_NIF_TERM dl7 = want_ok_tuple("delivered", call("delivered", 1, A(sim7)));
+        d = mock_bin_data(mock_elem(dl7, 1), &dsz);
+        uint64_t got7 = 0;
+        for (size_t i = 0; i < dsz; i++) got7 += d[i];
+        printf(", \"shard_rccl_world1\": {\"rounds\": %llu, \"delivered\": %llu}",
+               (unsigned long long)mock_int(mock_elem(sr, 1)), (unsigned long long)got7);
+        free(rp);
+        free(col);
+    }
+    /* ---- Demers rumor mongering + anti-entropy --------------------------- */
+    {
+        ERL_NIF_TERM sim = new_sim(0x5EED0004ull);
+        want_ok("demers_setup", call("demers_setup", 5, A(sim, mock_uint(20000), mock_uint(64), mock_uint(2),
+                                                          mock_atom("true"))));
+        ERL_NIF_TERM r = want_ok_tuple("demers_run", call("demers_run", 2, A(sim, mock_uint(200))));
+        size_t sz;
+        const uint64_t* seen = (const uint64_t*)mock_bin_data(mock_elem(r, 2), &sz);
+        uint64_t full = 0;
+        for (size_t i = 0; i < sz / 8; i++) full += seen[i] == ~0ull;
+        printf(", \"demers\": {\"n\": 20000, \"rounds\": %llu, \"complete\": %llu}",
+               (unsigned long long)mock_int(mock_elem(r, 1)), (unsigned long long)full);
+    }
+    /* ---- SCAMP v2 join waves ---------------------------------------------- */
+    {
+        const uint32_t n = 3000;
+        ERL_NIF_TERM sim = new_sim(0x5EED0003ull);
+        want_ok("scamp_setup", call("scamp_setup", 5, A(sim, mock_uint(n), mock_uint(2), mock_uint(5), mock_uint(10))));
+        uint64_t s = 3;
+        for (uint32_t k = 1; k < n; k *= 2) {
+            const uint32_t hi = 2 * k < n ? 2 * k : n;
+            uint32_t* v = (uint32_t*)malloc((hi - k) * 4);
+            uint32_t* c = (uint32_t*)malloc((hi - k) * 4);
+            for (uint32_t i = k; i < hi; i++) {
+                v[i - k] = i;
+                c[i - k] = lcg(&s) % k;
+            }
+            want_ok("scamp_join", call("scamp_join", 3, A(sim, u32s(v, hi - k), u32s(c, hi - k))));
+            want_ok_tuple("scamp_step", call("scamp_step", 2, A(sim, mock_uint(3))));
+            free(v);
+            free(c);
+        }
+        ERL_NIF_TERM st = mock_elem(want_ok_tuple("scamp_step", call("scamp_step", 2, A(sim, mock_uint(5)))), 1);
+        uint64_t pv = 0;
+        mock_map_get(mock_list_nth(st, 4), "pv_sum", &pv);
+        ERL_NIF_TERM vw = want_ok_tuple("scamp_views", call("scamp_views", 1, A(sim)));
+        size_t sz;
+        const uint32_t* npv = (const uint32_t*)mock_bin_data(mock_elem(vw, 2), &sz);
+        uint64_t tot = 0;
+        for (size_t i = 0; i < sz / 4; i++) tot += npv[i];
+        printf(", \"scamp\": {\"n\": %u, \"pv_sum\": %llu, \"view_entries\": %llu}", n, (unsigned long long)pv,
+               (unsigned long long)tot);
+    }
+    /* ---- full membership (C1 shape: 16 nodes join node 0) ------------------ */
+    {
+        const uint32_t n = 16;
+        ERL_NIF_TERM sim = new_sim(0x5EED0001ull);
+        want_ok("fm_setup", call("fm_setup", 4, A(sim, mock_uint(n), mock_uint(10), mock_uint(64))));
+        uint32_t v[15], p[15];
+        for (uint32_t i = 1; i < n; i++) {
+            v[i - 1] = i;
+            p[i - 1] = 0;
+        }
+        want_ok("fm_join", call("fm_join", 3, A(sim, u32s(v, 15), u32s(p, 15))));
+        want_ok_tuple("fm_step", call("fm_step", 2, A(sim, mock_uint(30))));
+        ERL_NIF_TERM fs = want_ok_tuple("fm_state", call("fm_state", 1, A(sim)));
+        size_t sz;
+        const uint64_t* known = (const uint64_t*)mock_bin_data(mock_elem(fs, 1), &sz);
+        uint64_t full = 0;
+        for (uint32_t i = 0; i < n; i++) full += (known[i] & 0xFFFFull) == 0xFFFFull;
+        printf(", \"fullmem\": {\"n\": %u, \"knows_all\": %llu}", n, (unsigned long long)full);
+    }
+    /* ---- C3: SCAMP v2 churn + Plumtree repair ------------------------------- */
+    {
+        const uint32_t n = 2000;
+        ERL_NIF_TERM sim = new_sim(0x5EED0003ull);
+        want_ok("c3_setup", call("c3_setup", 4, A(sim, mock_uint(n), mock_uint(5), mock_uint(10))));
+        uint64_t s = 5;
+        for (uint32_t k = 1; k < n; k *= 2) {
+            const uint32_t hi = 2 * k < n ? 2 * k : n;
+            uint32_t* v = (uint32_t*)malloc((hi - k) * 4);
+            uint32_t* c = (uint32_t*)malloc((hi - k) * 4);
+            for (uint32_t i = k; i < hi; i++) {
+                v[i - k] = i;
+                c[i - k] = lcg(&s) % k;
+            }
+            want_ok("c3_join", call("c3_join", 3, A(sim, u32s(v, hi - k), u32s(c, hi - k))));
+            want_ok_tuple("c3_step", call("c3_step", 2, A(sim, mock_uint(3))));
+            free(v);
+            free(c);
+        }
+        want_ok_tuple("c3_heartbeat", call("c3_heartbeat", 2, A(sim, mock_uint(0))));
+        ERL_NIF_TERM st = mock_elem(want_ok_tuple("c3_step", call("c3_step", 2, A(sim, mock_uint(10)))), 1);
+        uint64_t dl = 0, live = 0;
+        ERL_NIF_TERM last = mock_elem(mock_list_nth(st, 9), 0);
+        mock_map_get(last, "delivered_live", &dl);
+        mock_map_get(last, "live", &live);
+        uint32_t crash[20];
+        for (int i = 0; i < 20; i++) crash[i] = 100 + 17 * i;
+        want_ok("c3_crash", call("c3_crash", 2, A(sim, u32s(crash, 20))));
+        want_ok_tuple("c3_step", call("c3_step", 2, A(sim, mock_uint(2))));
+        printf(", \"c3\": {\"n\": %u, \"delivered_live\": %llu, \"live\": %llu}", n, (unsigned long long)dl,
+               (unsigned long long)live);
+    }
+    /* ---- causal delivery ------------------------------------------------------ */
+    {
+        ERL_NIF_TERM sim = new_sim(0x5EED0005ull);
+        want_ok("causal_setup", call("causal_setup", 6, A(sim, mock_uint(1000), mock_uint(8), mock_uint(1), mock_uint(2),
+                                                          mock_uint(1))));
+        ERL_NIF_TERM st = mock_elem(want_ok_tuple("causal_step", call("causal_step", 2, A(sim, mock_uint(10)))), 1);
+        uint64_t delivered = 0, x;
+        for (size_t i = 0; i < mock_list_len(st); i++)
+            if (mock_map_get(mock_list_nth(st, i), "delivered", &x)) delivered += x;
+        want_ok_tuple("causal_clocks", call("causal_clocks", 1, A(sim)));
+        printf(", \"causal\": {\"n\": 1000, \"delivered\": %llu}", (unsigned long long)delivered);
+    }
+    /* ---- vclock merge on dense lanes ------------------------------------------ */
+    {
+        ERL_NIF_TERM sim = new_sim(1);
+        uint32_t a[64] = {0}, b[64] = {0};
+        a[0] = 3; a[5] = 1; b[0] = 1; b[7] = 4;
+        ERL_NIF_TERM m = want_ok_tuple("vclock", call("vclock", 4, A(sim, mock_atom("merge"), u32s(a, 64), u32s(b, 64))));
+        size_t sz;
+        const uint32_t* o = (const uint32_t*)mock_bin_data(mock_elem(m, 1), &sz);
+        printf(", \"vclock_merge\": [%u, %u, %u]", o[0], o[5], o[7]);
+    }
+    printf("}\n");
+    mock_drop_terms();      /* resource destructors: psim_destroy on every handle */
+    return 0;
+}

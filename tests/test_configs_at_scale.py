@@ -126,7 +126,7 @@ def test_bench_config_10m_engines_agree_per_round():
         assert th[0] == th[1] == th[2], rounds
         if sum(st[0][k] for k in KINDS) == 0 or rounds > 40:
             break
-    assert rounds == 17       # the 16 rounds of the flood + the silent one that shows quiescence
+    assert rounds == 16       # psim_run's round count: the 16th round sends nothing
     for h in sims:
         h.close()
 
