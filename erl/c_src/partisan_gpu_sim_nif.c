@@ -806,6 +806,31 @@ static ERL_NIF_TERM nif_fm_state(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
     return enif_make_tuple4(env, mk_atom(env, "ok"), tk, trm, ta);
 }
 
+/* fm_tokens(Sim) -> {ok, TokenNodes :: <<u32 per token>>, Used}: the node each
+ * state_orset token adds (token v = node v's init/1 add; a self-leave takes a
+ * fresh one) */
+static ERL_NIF_TERM nif_fm_tokens(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r) || !r->fm_n) return enif_make_badarg(env);
+    const size_t ntok = (size_t)r->fm_words * 64;
+    ERL_NIF_TERM tt;
+    unsigned char* tb = enif_make_new_binary(env, ntok * 4, &tt);
+    uint32_t* tmp = (uint32_t*)enif_alloc(ntok * 4 + 4);
+    uint32_t used = 0;
+    if (!tb || !tmp) {
+        if (tmp) enif_free(tmp);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_tokens(r->h, tmp, ntok, &used);
+    enif_mutex_unlock(r->mu);
+    if (rc == PSIM_OK) memcpy(tb, tmp, ntok * 4);
+    enif_free(tmp);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), tt, enif_make_uint(env, used));
+}
+
 /* ---- C3: Plumtree repair over churning SCAMP v2 ------------------------------- */
 
 /* c3_setup(Sim, N, C, PeriodicRounds) -> ok */
@@ -1055,6 +1080,7 @@ static ErlNifFunc funcs[] = {
     {"fm_leave", 3, nif_fm_leave, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_step", 2, nif_fm_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_state", 1, nif_fm_state, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_tokens", 1, nif_fm_tokens, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_setup", 4, nif_c3_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_join", 3, nif_c3_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_crash", 2, nif_c3_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},

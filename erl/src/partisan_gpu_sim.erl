@@ -10,7 +10,12 @@
          peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
-         vclock/4]).
+         vclock/4,
+         scamp_setup/5, scamp_join/3, scamp_leave/3, scamp_crash/2, scamp_step/2, scamp_views/1,
+         fm_setup/4, fm_join/3, fm_leave/3, fm_step/2, fm_state/1, fm_tokens/1,
+         c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
+         causal_setup/6, causal_step/2, causal_clocks/1,
+         rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2]).
 -export([active_views/1, csr_from_views/1]).
 
 -on_load(init/0).
@@ -100,6 +105,70 @@ demers_run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 
 -spec vclock(sim(), descends | dominates | merge | increment, binary(), binary()) -> {ok, binary()} | error().
 vclock(_Sim, _Op, _A, _B) -> erlang:nif_error(nif_not_loaded).
+
+%% ---- SCAMP v1 / v2 (psim_scamp_*): joins / leaves / crashes are u32 binaries,
+%% handled by the next round; views are rows of 128 (partial) and 64 (in-view)
+%% u32 ids in the reference's list order, with u32 lengths.
+-spec scamp_setup(sim(), pos_integer(), 1 | 2, pos_integer(), pos_integer()) -> ok | error().
+scamp_setup(_Sim, _N, _Version, _C, _PeriodicRounds) -> erlang:nif_error(nif_not_loaded).
+-spec scamp_join(sim(), binary(), binary()) -> ok | error().
+scamp_join(_Sim, _Joiners, _Contacts) -> erlang:nif_error(nif_not_loaded).
+-spec scamp_leave(sim(), binary(), binary()) -> ok | error().
+scamp_leave(_Sim, _Vs, _Leaving) -> erlang:nif_error(nif_not_loaded).
+-spec scamp_crash(sim(), binary()) -> ok | error().
+scamp_crash(_Sim, _Vs) -> erlang:nif_error(nif_not_loaded).
+-spec scamp_step(sim(), pos_integer()) -> {ok, [map()]} | error().
+scamp_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+-spec scamp_views(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
+scamp_views(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% ---- full membership (psim_fm_*): state_orset token bitmaps per node ----------
+-spec fm_setup(sim(), pos_integer(), pos_integer(), pos_integer()) -> ok | error().
+fm_setup(_Sim, _N, _PeriodicRounds, _MaxTokens) -> erlang:nif_error(nif_not_loaded).
+-spec fm_join(sim(), binary(), binary()) -> ok | error().
+fm_join(_Sim, _Vs, _Peers) -> erlang:nif_error(nif_not_loaded).
+-spec fm_leave(sim(), binary(), binary()) -> ok | error().
+fm_leave(_Sim, _Vs, _Leaving) -> erlang:nif_error(nif_not_loaded).
+-spec fm_step(sim(), pos_integer()) -> {ok, [map()]} | error().
+fm_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+-spec fm_state(sim()) -> {ok, binary(), binary(), binary()} | error().
+fm_state(_Sim) -> erlang:nif_error(nif_not_loaded).
+-spec fm_tokens(sim()) -> {ok, binary(), non_neg_integer()} | error().
+fm_tokens(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% ---- C3: Plumtree over churning SCAMP v2 (psim_c3_*) -------------------------
+-spec c3_setup(sim(), pos_integer(), pos_integer(), pos_integer()) -> ok | error().
+c3_setup(_Sim, _N, _C, _PeriodicRounds) -> erlang:nif_error(nif_not_loaded).
+-spec c3_join(sim(), binary(), binary()) -> ok | error().
+c3_join(_Sim, _Joiners, _Contacts) -> erlang:nif_error(nif_not_loaded).
+-spec c3_crash(sim(), binary()) -> ok | error().
+c3_crash(_Sim, _Vs) -> erlang:nif_error(nif_not_loaded).
+-spec c3_heartbeat(sim(), non_neg_integer()) -> {ok, non_neg_integer()} | error().
+c3_heartbeat(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
+-spec c3_step(sim(), pos_integer()) -> {ok, [{map(), map()}]} | error().
+c3_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+
+%% ---- causal delivery (psim_causal_*) ------------------------------------------
+-spec causal_setup(sim(), pos_integer(), 1..64, pos_integer(), pos_integer(), pos_integer()) -> ok | error().
+causal_setup(_Sim, _N, _M, _Period, _DMax, _Redeliver) -> erlang:nif_error(nif_not_loaded).
+-spec causal_step(sim(), pos_integer()) -> {ok, [map()]} | error().
+causal_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+-spec causal_clocks(sim()) -> {ok, binary(), binary()} | error().
+causal_clocks(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% ---- vertex sharding with the library's own RCCL communicator --------------------
+%% One BEAM per GPU: rank 0 calls rccl_unique_id/0 and ships the id to the
+%% other ranks (e.g. erpc); each calls shard_init_rccl/4 before load_csr/3;
+%% shard_broadcast/2 and shard_run/2 are collective.
+-spec rccl_unique_id() -> {ok, binary()} | error().
+rccl_unique_id() -> erlang:nif_error(nif_not_loaded).
+-spec shard_init_rccl(sim(), non_neg_integer(), pos_integer(), binary()) -> ok | error().
+shard_init_rccl(_Sim, _Rank, _World, _Id) -> erlang:nif_error(nif_not_loaded).
+-spec shard_broadcast(sim(), non_neg_integer()) -> {ok, non_neg_integer()} | error().
+shard_broadcast(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
+-spec shard_run(sim(), pos_integer()) ->
+    {ok, non_neg_integer(), [map()], {non_neg_integer(), non_neg_integer(), non_neg_integer()}} | error().
+shard_run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 
 %% Active views (self excluded) as a list of id lists, vertex order.
 -spec active_views(sim()) -> {ok, [[non_neg_integer()]]} | error().

@@ -1,0 +1,213 @@
+%% partisan_gpu_sim_cluster -- one simulated Partisan cluster of N virtual
+%% peers in HBM, driven through the partisan_gpu_sim NIF (include/psim.h).
+%%
+%% This is what the two behaviour adapters
+%% (partisan_gpu_sim_membership_strategy, partisan_gpu_sim_plumtree_handler)
+%% call: the cluster owns one libpsim handle; the strategy callbacks of the
+%% simulated nodes queue their joins / leaves on it, and the cluster runs the
+%% device rounds -- one periodic interval (`periodic_rounds' rounds, the
+%% strategy's periodic/1 inside them, src/partisan_pluggable_peer_service_manager.erl
+%% :1386-1419) once every live simulated node's periodic/1 has been called
+%% for the interval.  Membership messages never leave the device.
+%%
+%% Simulated node v is named 'nXXXXXXXX' (zero-padded v) with listen port
+%% 10000 + v, so every Erlang term order of node specs equals vertex order
+%% (SURVEY App. A Q28).
+-module(partisan_gpu_sim_cluster).
+
+-export([start/1, stop/0, sim/0, n/0,
+         node_spec/1, vertex/1, self_vertex/0, set_self/1,
+         join/2, leave/2, periodic/1, members/1, run_interval/0,
+         load_overlay/2, heartbeat/1, delivered/3]).
+
+-define(KEY, ?MODULE).
+-define(HIST, partisan_gpu_sim_heartbeats).
+
+%% Opts: n, strategy (scamp_v2 | scamp_v1 | full), seed, device,
+%% periodic_rounds (10), scamp_c (5), lazy_tick_rounds (1), max_tokens (2n).
+-spec start(map()) -> {ok, partisan_gpu_sim:sim()} | {error, term()}.
+start(#{n := N, strategy := Strategy} = Opts) ->
+    Periodic = maps:get(periodic_rounds, Opts, 10),
+    NewOpts = #{seed => maps:get(seed, Opts, 0), device => maps:get(device, Opts, 0),
+                lazy_tick_rounds => maps:get(lazy_tick_rounds, Opts, 1)},
+    case partisan_gpu_sim:new(NewOpts) of
+        {ok, Sim} ->
+            Setup = case Strategy of
+                        scamp_v2 -> partisan_gpu_sim:scamp_setup(Sim, N, 2, maps:get(scamp_c, Opts, 5), Periodic);
+                        scamp_v1 -> partisan_gpu_sim:scamp_setup(Sim, N, 1, maps:get(scamp_c, Opts, 5), Periodic);
+                        full -> partisan_gpu_sim:fm_setup(Sim, N, Periodic, maps:get(max_tokens, Opts, 2 * N))
+                    end,
+            case Setup of
+                ok ->
+                    Calls = atomics:new(1, []),
+                    catch ets:delete(?HIST),
+                    ?HIST = ets:new(?HIST, [named_table, public, set]),
+                    persistent_term:put(?KEY, #{sim => Sim, n => N, strategy => Strategy,
+                                                periodic => Periodic, calls => Calls,
+                                                live => maps:get(live, Opts, N)}),
+                    {ok, Sim};
+                Err ->
+                    Err
+            end;
+        Err ->
+            Err
+    end.
+
+-spec stop() -> ok.
+stop() ->
+    catch ets:delete(?HIST),
+    _ = persistent_term:erase(?KEY),
+    ok.
+
+sim() -> maps:get(sim, persistent_term:get(?KEY)).
+n() -> maps:get(n, persistent_term:get(?KEY)).
+
+%% ---- node identity (SURVEY Q28) ----------------------------------------------
+-spec node_spec(non_neg_integer()) -> map().
+node_spec(V) ->
+    Name = list_to_atom(lists:flatten(io_lib:format("n~8..0B", [V]))),
+    #{name => Name,
+      listen_addrs => [#{ip => {127, 0, 0, 1}, port => 10000 + V}],
+      channels => #{undefined => #{parallelism => 1}}}.
+
+-spec vertex(map() | atom()) -> non_neg_integer().
+vertex(#{name := Name}) -> vertex(Name);
+vertex(Name) when is_atom(Name) ->
+    [Base | _] = string:split(atom_to_list(Name), "@"),
+    "n" ++ Digits = Base,
+    list_to_integer(Digits).
+
+%% The simulated node the calling process acts for: set_self/1, else the
+%% node name.
+-spec self_vertex() -> non_neg_integer().
+self_vertex() ->
+    case get(partisan_gpu_sim_vertex) of
+        undefined -> vertex(node());
+        V -> V
+    end.
+
+set_self(V) -> put(partisan_gpu_sim_vertex, V), ok.
+
+%% ---- membership strategy side ---------------------------------------------------
+%% join/leave calls are queued on the device and handled by the next round
+%% (psim_scamp_join / psim_fm_join: {connected, ...} -> Strategy:join/3).
+join(V, Peer) -> batch(join, V, Peer).
+leave(V, Node) -> batch(leave, V, Node).
+
+batch(What, V, Other) ->
+    #{sim := Sim, strategy := S} = persistent_term:get(?KEY),
+    A = <<V:32/little>>,
+    B = <<Other:32/little>>,
+    case {S, What} of
+        {full, join} -> partisan_gpu_sim:fm_join(Sim, A, B);
+        {full, leave} -> partisan_gpu_sim:fm_leave(Sim, A, B);
+        {_, join} -> partisan_gpu_sim:scamp_join(Sim, A, B);
+        {_, leave} -> partisan_gpu_sim:scamp_leave(Sim, A, B)
+    end.
+
+%% periodic/1 of node V for the current interval: the last live node's call
+%% runs the interval on the device.
+periodic(_V) ->
+    #{calls := C, live := Live} = persistent_term:get(?KEY),
+    case atomics:add_get(C, 1, 1) >= Live of
+        true ->
+            atomics:put(C, 1, 0),
+            run_interval();
+        false ->
+            ok
+    end.
+
+-spec run_interval() -> ok | {error, term()}.
+run_interval() ->
+    #{sim := Sim, strategy := S, periodic := P} = persistent_term:get(?KEY),
+    Res = case S of
+              full -> partisan_gpu_sim:fm_step(Sim, P);
+              _ -> partisan_gpu_sim:scamp_step(Sim, P)
+          end,
+    case Res of
+        {ok, _Stats} -> ok;
+        Err -> Err
+    end.
+
+%% The members node V's strategy holds, as node specs in term order.
+-spec members(non_neg_integer()) -> [map()].
+members(V) ->
+    #{sim := Sim, strategy := S, n := N} = persistent_term:get(?KEY),
+    Ids = case S of
+              full ->
+                  {ok, Known, Removed, _Alive} = partisan_gpu_sim:fm_state(Sim),
+                  W = byte_size(Known) div (N * 8),
+                  K = binary:part(Known, V * W * 8, W * 8),
+                  R = binary:part(Removed, V * W * 8, W * 8),
+                  Live = [Bit || {Kw, Rw, Word} <- lists:zip3(words(K), words(R), lists:seq(0, W - 1)),
+                                 Bit <- bits(Kw band (bnot Rw), Word * 64)],
+                  {ok, TokNodes, _Used} = partisan_gpu_sim:fm_tokens(Sim),
+                  lists:usort([token_node(TokNodes, T) || T <- Live]);
+              _ ->
+                  {ok, Pv, Npv, _Iv, _Niv} = partisan_gpu_sim:scamp_views(Sim),
+                  Skip = V * 4,
+                  <<_:Skip/binary, Len:32/little, _/binary>> = Npv,
+                  Row = binary:part(Pv, V * 128 * 4, Len * 4),
+                  lists:usort([I || <<I:32/little>> <= Row])
+          end,
+    [node_spec(I) || I <- Ids].
+
+words(Bin) -> [W || <<W:64/little>> <= Bin].
+bits(0, _Base) -> [];
+bits(W, Base) -> [Base + I || I <- lists:seq(0, 63), (W bsr I) band 1 =:= 1].
+
+%% the node token T adds (psim_fm_tokens: token v is node v's init/1 add, a
+%% self-leave takes a fresh token)
+token_node(TokNodes, T) ->
+    Skip = T * 4,
+    <<_:Skip/binary, Node:32/little, _/binary>> = TokNodes,
+    Node.
+
+%% ---- plumtree side ------------------------------------------------------------------
+%% The peer service's members as Plumtree sees them (partisan_plumtree_broadcast
+%% start_link/0): row_ptr u64 / col u32 binaries.
+load_overlay(RowPtr, Col) -> partisan_gpu_sim:load_csr(sim(), RowPtr, Col).
+
+%% backend heartbeat at Root (src/partisan_plumtree_backend.erl:341-368), run to
+%% quiescence; the delivered set of the previous heartbeat of Root is kept for
+%% is_stale/1 of older ids.
+-spec heartbeat(non_neg_integer()) -> {ok, {node(), 0, non_neg_integer()}, non_neg_integer()} | {error, term()}.
+heartbeat(Root) ->
+    Sim = sim(),
+    case ets:lookup(?HIST, {latest, Root}) of
+        [{_, Prev}] ->
+            ok = partisan_gpu_sim:focus(Sim, Root),
+            {ok, D} = partisan_gpu_sim:delivered(Sim),
+            ets:insert(?HIST, {{Root, Prev}, D});
+        [] ->
+            ok
+    end,
+    case partisan_gpu_sim:broadcast(Sim, Root) of
+        {ok, Mono} ->
+            ets:insert(?HIST, {{latest, Root}, Mono}),
+            {ok, Rounds, _Stats} = partisan_gpu_sim:run(Sim, 100000),
+            {ok, {maps:get(name, node_spec(Root)), 0, Mono}, Rounds};
+        Err ->
+            Err
+    end.
+
+%% Mod:is_stale/1 at vertex V for heartbeat Mono of Origin (the backend's
+%% interval set, src/partisan_plumtree_backend.erl:229-244).
+-spec delivered(non_neg_integer(), non_neg_integer(), non_neg_integer()) -> boolean().
+delivered(V, Origin, Mono) ->
+    case ets:lookup(?HIST, {latest, Origin}) of
+        [] ->
+            false;
+        [{_, Latest}] when Mono > Latest ->
+            false;
+        [{_, Mono}] ->
+            Sim = sim(),
+            ok = partisan_gpu_sim:focus(Sim, Origin),
+            {ok, D} = partisan_gpu_sim:delivered(Sim),
+            binary:at(D, V) =:= 1;
+        [_] ->
+            case ets:lookup(?HIST, {Origin, Mono}) of
+                [{_, D}] -> binary:at(D, V) =:= 1;
+                [] -> false
+            end
+    end.

@@ -190,7 +190,13 @@ int main(void) {
         const uint64_t* known = (const uint64_t*)mock_bin_data(mock_elem(fs, 1), &sz);
         uint64_t full = 0;
         for (uint32_t i = 0; i < n; i++) full += (known[i] & 0xFFFFull) == 0xFFFFull;
-        printf(", \"fullmem\": {\"n\": %u, \"knows_all\": %llu}", n, (unsigned long long)full);
+        ERL_NIF_TERM tk = want_ok_tuple("fm_tokens", call("fm_tokens", 1, A(sim)));
+        size_t tsz;
+        const uint32_t* tn = (const uint32_t*)mock_bin_data(mock_elem(tk, 1), &tsz);
+        uint64_t ident = 0;
+        for (uint32_t i = 0; i < n; i++) ident += tn[i] == i;          /* token v = node v's init/1 add */
+        printf(", \"fullmem\": {\"n\": %u, \"knows_all\": %llu, \"tokens_used\": %llu, \"own_tokens\": %llu}", n,
+               (unsigned long long)full, (unsigned long long)mock_int(mock_elem(tk, 2)), (unsigned long long)ident);
     }
     /* ---- C3: SCAMP v2 churn + Plumtree repair ------------------------------- */
     {

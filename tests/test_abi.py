@@ -95,3 +95,34 @@ def test_nif_calls_only_declared_symbols():
     nif = open(os.path.join(ROOT, "erl", "c_src", "partisan_gpu_sim_nif.c")).read()
     used = set(re.findall(r"\b(psim_\w+)\s*\(", nif))
     assert used and used <= declared, used - declared
+
+
+def test_erlang_stubs_cover_the_nif_table():
+    """Every entry of the shim's ErlNifFunc table has an exported stub of the
+    same arity in erl/src/partisan_gpu_sim.erl (what erlang:load_nif/2
+    requires), and the behaviour adapters export every callback of the
+    reference behaviours (src/partisan_membership_strategy.erl:55-77,
+    src/partisan_plumtree_broadcast_handler.erl:47-78)."""
+    nif = open(os.path.join(ROOT, "erl", "c_src", "partisan_gpu_sim_nif.c")).read()
+    table = set(re.findall(r'\{"(\w+)", (\d+), nif_\w+,', nif))
+    erl = open(os.path.join(ROOT, "erl", "src", "partisan_gpu_sim.erl")).read()
+    exports = set()
+    for block in re.findall(r"-export\(\[(.*?)\]\)\.", erl, re.S):
+        exports |= {tuple(x.strip().split("/")) for x in block.split(",") if "/" in x}
+    assert table, "no NIF table parsed"
+    missing = {(f, a) for f, a in table if (f, a) not in exports}
+    assert not missing, missing
+    for f, _a in table:
+        assert re.search(rf"^{f}\(" + r"[^)]*\) ->\s*erlang:nif_error", erl, re.M), f
+    def exported(path):
+        src = open(os.path.join(ROOT, "erl", "src", path)).read()
+        out = set()
+        for block in re.findall(r"-export\(\[(.*?)\]\)\.", src, re.S):
+            out |= {x.strip() for x in block.split(",")}
+        return src, out
+    src, ex = exported("partisan_gpu_sim_membership_strategy.erl")
+    assert "-behaviour(partisan_membership_strategy)." in src
+    assert {"init/1", "join/3", "leave/2", "compare/2", "periodic/1", "prune/2", "handle_message/2"} <= ex
+    src, ex = exported("partisan_gpu_sim_plumtree_handler.erl")
+    assert "-behaviour(partisan_plumtree_broadcast_handler)." in src
+    assert {"broadcast_data/1", "broadcast_channel/0", "merge/2", "is_stale/1", "graft/1", "exchange/1"} <= ex
