@@ -312,6 +312,22 @@ static ERL_NIF_TERM nif_set_omissions(ErlNifEnv* env, int argc, const ERL_NIF_TE
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
 }
 
+/* set_delays(Sim, SrcU32s, DstU32s, Rounds) -> ok: delay faults on the
+ * directed pairs, Rounds one byte per pair (<<>>s: no delays) */
+static ERL_NIF_TERM nif_set_delays(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary s, d, k;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &s) ||
+        !enif_inspect_binary(env, argv[2], &d) || !enif_inspect_binary(env, argv[3], &k) || s.size != d.size ||
+        s.size % 4 || k.size != s.size / 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_set_delays(r->h, (const uint32_t*)s.data, (const uint32_t*)d.data, (const uint8_t*)k.data, k.size);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
 /* relay_run(Sim, ActPtr, Act, OlPtr, Ol, Alive, Src, Dst, RelayTTL, MaxCopies)
  *   -> {ok, Rounds, [{Direct, Relay, Dropped, Lost, Arrived}], Delivered, FirstRound}
  * Transitive relay over out-links (psim_relay_run).  Pointer binaries are
@@ -1061,6 +1077,7 @@ static ErlNifFunc funcs[] = {
     {"trace_hash", 1, nif_trace_hash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"focus", 2, nif_focus, 0},
     {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"set_delays", 4, nif_set_delays, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"relay_run", 10, nif_relay_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},

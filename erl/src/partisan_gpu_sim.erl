@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
-         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, relay_run/10,
+         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
          vclock/4,
@@ -69,6 +69,11 @@ focus(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
 %% Omission faults on directed pairs: native-endian u32 binaries (psim_set_omissions).
 -spec set_omissions(sim(), binary(), binary()) -> ok | error().
 set_omissions(_Sim, _Src, _Dst) -> erlang:nif_error(nif_not_loaded).
+
+%% Delay faults on directed pairs (psim_set_delays): Src / Dst native-endian
+%% u32 binaries, Rounds one byte per pair; refused while messages are in flight.
+-spec set_delays(sim(), binary(), binary(), binary()) -> ok | error().
+set_delays(_Sim, _Src, _Dst, _Rounds) -> erlang:nif_error(nif_not_loaded).
 
 %% Transitive relay (psim_relay_run): forward_message(Node, Message,
 %% #{transitive => true}) for a batch of sends over active views (ActPtr u64 /

@@ -163,6 +163,19 @@ int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
  * Pairs that are not overlay edges are ignored; a partition is the set of
  * its cross edges (partisan_amd.Simulator.inject_partition). */
 int  psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst, size_t k);
+/* Delay faults (test/partisan_SUITE.erl with_egress_delay /
+ * with_ingress_delay; partisan_peer_service_client.erl:148-176 and
+ * partisan_peer_service_server.erl sleep before each send / after each
+ * receipt): every Plumtree message over the directed pair (src[i], dst[i])
+ * emitted in round t is delivered in round t + 1 + rounds[i] instead of
+ * t + 1 (a fixed delay per pair keeps each pair FIFO).  rounds[i] <=
+ * PSIM_MAX_DELAY.  Replaces the whole set (k = 0: every delay 0); an egress
+ * (ingress) delay of a node is its out- (in-) edges.  PSIM_EBUSY while any
+ * message is in flight (a change could reorder a pair); PSIM_ESTATE for the
+ * binned engine and for sharded handles.  Pairs that are not overlay edges
+ * are ignored.  psim_run ends only when no delayed message is pending. */
+#define PSIM_MAX_DELAY 14u
+int  psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k);
 
 /* Order-independent digest of the Plumtree state, to compare runs (the two
  * engines, shard counts, replays) at full size without copying state out.

@@ -322,6 +322,10 @@ uint64_t orc_pt_dropped(const orc_plumtree* s);
  * (prop_partisan_crash_fault_model.erl:117-196); k = 0 heals */
 void orc_pt_set_omissions(orc_plumtree* s, const uint32_t* src, const uint32_t* dst, size_t k);
 uint64_t orc_pt_omitted(const orc_plumtree* s);
+/* delay faults: messages over (src[i], dst[i]) arrive d[i] rounds late;
+ * k = 0 removes them; ORC_BADARG while messages are in flight */
+int orc_pt_set_delays(orc_plumtree* s, const uint32_t* src, const uint32_t* dst, const uint8_t* d, size_t k);
+uint64_t orc_pt_inflight(const orc_plumtree* s);
 
 typedef struct orc_c3 orc_c3;
 typedef struct orc_c3_stats {

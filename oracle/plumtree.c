@@ -121,6 +121,9 @@ struct orc_plumtree {
     uint64_t dropped;                      /* sends to a non-connected peer */
     uint64_t* omit; size_t nomit;          /* omission faults: sorted (src << 32 | dst) keys */
     uint64_t omitted;                      /* messages they dropped */
+    uint64_t* dkey; uint8_t* dval; size_t ndly;   /* delay faults: sorted (src << 32 | dst) -> rounds */
+    orc_msg* dq; uint64_t* dqa; size_t ndq, capdq; /* delayed messages and their arrival rounds */
+    uint64_t emit_round;                   /* the round whose emissions are being made (0: before round 1) */
 };
 
 void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx) { s->conn = fn; s->conn_ctx = ctx; }
@@ -146,6 +149,44 @@ void orc_pt_set_omissions(orc_plumtree* s, const uint32_t* src, const uint32_t* 
     s->nomit = k;
 }
 uint64_t orc_pt_omitted(const orc_plumtree* s) { return s->omitted; }
+
+/* Delay faults (test/partisan_SUITE.erl groups with_egress_delay /
+ * with_ingress_delay; partisan_peer_service_client.erl:148-176 sleeps
+ * egress_delay ms before each send, partisan_peer_service_server.erl the
+ * same on receipt): in rounds, a message emitted in round t over the
+ * directed pair (src, dst) with delay d is delivered in round t + 1 + d
+ * instead of t + 1.  A fixed per-pair delay keeps every pair FIFO, which is
+ * all the reference guarantees.  Replaces the whole set (k = 0: no delays);
+ * refused with ORC_BADARG while any message is in flight, as a change could
+ * reorder a pair's messages. */
+int orc_pt_set_delays(orc_plumtree* s, const uint32_t* src, const uint32_t* dst, const uint8_t* d, size_t k) {
+    if (s->nnxt || s->ndq) return ORC_BADARG;
+    free(s->dkey); free(s->dval);
+    s->dkey = NULL; s->dval = NULL; s->ndly = 0;
+    if (!k) return ORC_OK;
+    uint64_t* kv = (uint64_t*)malloc(k * sizeof(uint64_t));   /* key << 8 | delay, sorted by key */
+    for (size_t i = 0; i < k; i++) kv[i] = ((((uint64_t)src[i] << 32) | dst[i]) << 8) | d[i];
+    qsort(kv, k, sizeof(uint64_t), cmp_u64);
+    s->dkey = (uint64_t*)malloc(k * sizeof(uint64_t));
+    s->dval = (uint8_t*)malloc(k);
+    for (size_t i = 0; i < k; i++) {           /* a repeated pair: the last listed wins */
+        const uint64_t key = kv[i] >> 8;
+        if (s->ndly && s->dkey[s->ndly - 1] == key) { s->dval[s->ndly - 1] = (uint8_t)kv[i]; continue; }
+        s->dkey[s->ndly] = key; s->dval[s->ndly] = (uint8_t)kv[i]; s->ndly++;
+    }
+    free(kv);
+    return ORC_OK;
+}
+static uint32_t delay_of(const orc_plumtree* s, uint32_t src, uint32_t dst) {
+    if (!s->ndly) return 0;
+    const uint64_t key = ((uint64_t)src << 32) | dst;
+    size_t lo = 0, hi = s->ndly;
+    while (lo < hi) { size_t m = (lo + hi) / 2; if (s->dkey[m] < key) lo = m + 1; else hi = m; }
+    return lo < s->ndly && s->dkey[lo] == key ? s->dval[lo] : 0;
+}
+/* messages in flight: delivered next round + delayed beyond it */
+uint64_t orc_pt_inflight(const orc_plumtree* s) { return s->nnxt + s->ndq; }
+
 static int omitted(const orc_plumtree* s, uint32_t src, uint32_t dst) {
     if (!s->nomit) return 0;
     const uint64_t key = ((uint64_t)src << 32) | dst;
@@ -165,8 +206,20 @@ static void emit(orc_plumtree* s, uint32_t src, uint32_t dst, uint32_t type,
         s->omitted++;
         return;
     }
-    if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? s->capnxt * 2 : 1024; s->nxt = (orc_msg*)realloc(s->nxt, s->capnxt * sizeof(orc_msg)); }
-    orc_msg* m = &s->nxt[s->nnxt++];
+    const uint32_t d = delay_of(s, src, dst);
+    orc_msg* m;
+    if (d) {                                             /* delivered in round emit_round + 1 + d */
+        if (s->ndq == s->capdq) {
+            s->capdq = s->capdq ? s->capdq * 2 : 1024;
+            s->dq = (orc_msg*)realloc(s->dq, s->capdq * sizeof(orc_msg));
+            s->dqa = (uint64_t*)realloc(s->dqa, s->capdq * sizeof(uint64_t));
+        }
+        s->dqa[s->ndq] = s->emit_round + 1 + d;
+        m = &s->dq[s->ndq++];
+    } else {
+        if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? s->capnxt * 2 : 1024; s->nxt = (orc_msg*)realloc(s->nxt, s->capnxt * sizeof(orc_msg)); }
+        m = &s->nxt[s->nnxt++];
+    }
     m->type = type; m->src = src; m->dst = dst; m->round = round; m->root = root;
     m->id_node = idn; m->id_epoch = ide; m->id_mono = idm;
     m->seq = s->nodes[src].seq++;
@@ -371,7 +424,7 @@ orc_plumtree* orc_pt_create(uint32_t n, const uint64_t* row_ptr, const uint32_t*
 
 void orc_pt_destroy(orc_plumtree* s) {
     if (!s) return;
-    free(s->omit);
+    free(s->omit); free(s->dkey); free(s->dval); free(s->dq); free(s->dqa);
     for (uint32_t v = 0; v < s->n; v++) {
         node_t* nd = &s->nodes[v];
         os_free(&nd->all_members); os_free(&nd->common_eagers); os_free(&nd->common_lazys);
@@ -482,6 +535,19 @@ static void one_round(orc_plumtree* s, orc_round_stats* st) {
     orc_msg* t = s->cur; size_t tc = s->capcur;
     s->cur = s->nxt; s->ncur = s->nnxt; s->capcur = s->capnxt;
     s->nxt = t; s->nnxt = 0; s->capnxt = tc;
+    s->emit_round = s->round + 1;
+    {                                                   /* delayed messages due this round */
+        size_t k = 0;
+        for (size_t i = 0; i < s->ndq; i++) {
+            if (s->dqa[i] == s->emit_round) {
+                if (s->ncur == s->capcur) { s->capcur = s->capcur ? s->capcur * 2 : 1024; s->cur = (orc_msg*)realloc(s->cur, s->capcur * sizeof(orc_msg)); }
+                s->cur[s->ncur++] = s->dq[i];
+            } else {
+                s->dq[k] = s->dq[i]; s->dqa[k] = s->dqa[i]; k++;
+            }
+        }
+        s->ndq = k;
+    }
     qsort(s->cur, s->ncur, sizeof(orc_msg), msg_cmp);
     /* {update, Members} casts queued since the last round, in order (C3) */
     for (uint32_t v = 0; v < s->n; v++) {
@@ -532,7 +598,7 @@ uint32_t orc_pt_run(orc_plumtree* s, uint32_t max_rounds, orc_round_stats* stats
     uint32_t r = 0;
     orc_round_stats tmp;
     while (r < max_rounds) {
-        if (s->nnxt == 0) {
+        if (s->nnxt == 0 && s->ndq == 0) {
             uint64_t live = 0;
             for (uint32_t v = 0; v < s->n && !live; v++) {
                 if (!s->alive[v]) continue;
@@ -546,11 +612,14 @@ uint32_t orc_pt_run(orc_plumtree* s, uint32_t max_rounds, orc_round_stats* stats
     return r;
 }
 
+/* the messages the next round delivers (delayed ones due then included) */
 size_t orc_pt_pending(const orc_plumtree* s, orc_msg* out, size_t cap) {
-    size_t n = s->nnxt < cap ? s->nnxt : cap;
-    memcpy(out, s->nxt, n * sizeof(orc_msg));
-    qsort(out, n, sizeof(orc_msg), msg_cmp);
-    return s->nnxt;
+    size_t n = 0;
+    for (size_t i = 0; i < s->nnxt; i++, n++) if (n < cap) out[n] = s->nxt[i];
+    for (size_t i = 0; i < s->ndq; i++)
+        if (s->dqa[i] == s->round + 1) { if (n < cap) out[n] = s->dq[i]; n++; }
+    qsort(out, n < cap ? n : cap, sizeof(orc_msg), msg_cmp);
+    return n;
 }
 
 int orc_pt_get_peers(const orc_plumtree* s, uint32_t v, uint32_t root,

@@ -157,6 +157,9 @@ def lib():
         L.orc_pt_set_omissions.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), sz]
         L.orc_pt_omitted.argtypes = [C.c_void_p]
         L.orc_pt_omitted.restype = C.c_uint64
+        L.orc_pt_set_delays.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), P(C.c_uint8), sz]
+        L.orc_pt_inflight.argtypes = [C.c_void_p]
+        L.orc_pt_inflight.restype = C.c_uint64
         L.orc_relay_run.argtypes = [C.c_uint32, P(C.c_uint64), P(C.c_uint32), P(C.c_uint64), P(C.c_uint32),
                                     P(C.c_uint8), C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
                                     P(C.c_uint64), P(C.c_uint32), P(RelayRound), sz, sz]
@@ -472,6 +475,20 @@ class Plumtree:
 
     def omitted(self):
         return int(lib().orc_pt_omitted(self._h))
+
+    def set_delays(self, pairs, delays):
+        """Delay faults: messages over directed (src, dst) arrive delays[i]
+        rounds late; [] removes them.  Refused while messages are in flight."""
+        p = np.asarray(pairs, dtype=np.uint32).reshape(-1, 2)
+        s, d = np.ascontiguousarray(p[:, 0]), np.ascontiguousarray(p[:, 1])
+        dl = np.ascontiguousarray(delays, dtype=np.uint8)
+        assert len(dl) == len(p)
+        rc = lib().orc_pt_set_delays(self._h, _u32p(s), _u32p(d), dl.ctypes.data_as(C.POINTER(C.c_uint8)), len(p))
+        if rc:
+            raise RuntimeError("orc_pt_set_delays: messages in flight")
+
+    def inflight(self):
+        return int(lib().orc_pt_inflight(self._h))
 
     def step(self, rounds=1):
         st = (RoundStats * rounds)()

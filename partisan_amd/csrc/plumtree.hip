@@ -105,6 +105,11 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
     }
 }
 
+// After flush_counters (whose barrier orders the LDS counts): the
+// workgroup's per-delay message counts into the round's stats row tail.
+template <bool kFault>
+__device__ __forceinline__ void flush_delays(const PtArgs& a);
+
 // Append the nibble FIFO `f` to (fifo, n); count kinds (kCount).
 template <bool kCount>
 __device__ __forceinline__ void fifo_append(uint32_t& fifo, uint32_t& n, uint32_t f, Ctr& c) {
@@ -127,11 +132,41 @@ __device__ __forceinline__ bool omitted(const PtArgs& a, uint32_t e) {
     return a.omit && ((a.omit[e >> 5] >> (e & 31)) & 1u);
 }
 
-template <bool kOmit = true>
-__device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w) {
-    if (kOmit && omitted(a, e)) return;
+// Delay faults (psim_set_delays): the word over sender slot e goes to the
+// ring slot of the round that reads it, 1 + dly[e] rounds on, tagged with
+// that round; `hist` counts the messages per delay (the host keeps the
+// arrivals pending, so a delayed message keeps the run from ending).
+__device__ __forceinline__ uint32_t word_msgs(uint32_t w) {
+    const uint32_t f = w & kFifoMask;
+    return __popc((f | (f >> 1) | (f >> 2)) & 0x249u);   // non-zero 3-bit kinds
+}
+
+__device__ __forceinline__ void put_delayed(const PtArgs& a, uint32_t e, uint32_t ls, uint32_t u, uint32_t w,
+                                            unsigned long long* hist) {
+    const uint32_t d = a.dly[e];
+    const uint32_t k = (a.rpos + d) & (kRing - 1);
+    w = (w & ~(0xFFu << kTagShift)) | (((a.wtag + d) & 0xFFu) << kTagShift);
+    a.ring[size_t(k) * a.ed + ls] = w;
+    a.pring[size_t(k) * a.ngrp + (u >> kGroupShift)] = 1;
+    atomicAdd(&hist[d], (unsigned long long)word_msgs(w));
+}
+
+// The round kernels' per-delay message counts (LDS, flushed once per workgroup).
+__device__ __forceinline__ unsigned long long* delay_hist() {
+    __shared__ unsigned long long dh[kRing];
+    return dh;
+}
+
+template <bool kFault = true>
+__device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w,
+                                             unsigned long long* hist = nullptr) {
+    if (kFault && omitted(a, e)) return;
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
+        if (kFault && a.dly) {
+            put_delayed(a, e, a.rev[e] - a.slot_base, u, w, hist ? hist : delay_hist());
+            return;
+        }
 #ifdef PT_NT_STORE
         __builtin_nontemporal_store(w, &a.in_nxt[a.rev[e] - a.slot_base]);
 #else
@@ -310,7 +345,7 @@ constexpr uint32_t kFastDeg = 8;
 // kNoPeer) never carry a word, a mask bit or an outgoing message.
 // kLdsWords: the round kernel already gathered the vertex's live inbox words
 // into LDS (pt_round_ell_body) and `lw` points at them.
-template <bool kOmit, bool kLdsWords = false>
+template <bool kFault, bool kLdsWords = false>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
                                                bool due, Ctr& c, const uint32_t* lw = nullptr) {
     uint32_t w[kFastDeg];
@@ -355,9 +390,11 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
         const uint32_t wo = pt_out<true>(s, r[s], x, ihave, a.wtag, c);
         if (!wo) continue;
         sent = true;
-        if (kOmit && omitted(a, rs + s)) continue;
+        if (kFault && omitted(a, rs + s)) continue;
         const uint32_t u = cl[s] - a.v_lo;
-        if (u < a.n) {
+        if (kFault && a.dly && u < a.n) {
+            put_delayed(a, rs + s, rv[s] - a.slot_base, u, wo, delay_hist());
+        } else if (u < a.n) {
 #ifdef PT_NT_STORE
             __builtin_nontemporal_store(wo, &a.in_nxt[rv[s] - a.slot_base]);
 #else
@@ -381,18 +418,28 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
     vst_store(a, v, st, x, c);
 }
 
-template <bool kOmit>
+template <bool kFault>
+__device__ __forceinline__ void flush_delays(const PtArgs& a) {
+    if (!kFault || !a.dly) return;
+    const uint32_t t = threadIdx.x;
+    if (t < kRing) {
+        const unsigned long long x = delay_hist()[t];
+        if (x) atomicAdd(&a.dhist[t], x);
+    }
+}
+
+template <bool kFault>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
                                           Ctr& c) {
     if (a.ell) {
-        pt_vertex_fast<kOmit>(a, v, v * a.ell, a.ell, pend, due, c);
+        pt_vertex_fast<kFault>(a, v, v * a.ell, a.ell, pend, due, c);
         return;
     }
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
 #ifndef PT_NO_FAST
     if (deg <= kFastDeg) {
-        pt_vertex_fast<kOmit>(a, v, rs, deg, pend, due, c);
+        pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c);
         return;
     }
 #endif
@@ -420,7 +467,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
-        deliver_word<kOmit>(a, rs + s, w);
+        deliver_word<kFault>(a, rs + s, w);
         sent = true;
     }
     if (sent) {
@@ -434,9 +481,9 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 // them: their group flag (set by any sender to the group) and, on a tick
 // round while some vertex holds outstanding rows, their outstanding byte.
 // Candidates are compacted into an LDS list and spread over the threads.
-// kOmit: omission faults installed (psim_set_omissions); the common case
+// kFault: omission faults installed (psim_set_omissions); the common case
 // compiles without the per-word bitmap test.
-template <bool kOmit>
+template <bool kFault>
 __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     __shared__ uint16_t rep[kMaxDeg * kBlock];
     __shared__ uint16_t cand[kChunkV];           // (vertex - base) << 2 | pend << 1 | due: 12 bits
@@ -451,6 +498,7 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     }
     const uint32_t base = blockIdx.x * kChunkV;
     if (t == 0) ncand = 0;
+    if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
     __syncthreads();
     const uint32_t v0 = base + 4 * t;
     uint32_t pmask = 0, dmask = 0;
@@ -486,14 +534,15 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex<kOmit>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c);
+        pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c);
     }
     flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+    flush_delays<kFault>(a);
 }
 
-template <bool kOmit>
+template <bool kFault>
 __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
-    pt_round_body<kOmit>(a);
+    pt_round_body<kFault>(a);
 }
 
 // ELL rows (a.ell = W): the workgroup first reads the inbox words of every
@@ -504,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
 // threads, which then need one round trip (state, peer ids, reverse slots)
 // instead of a per-vertex dependent load of words that are mostly stale
 // (a flagged group typically has one or two receivers in the sparse rounds).
-template <bool kOmit>
+template <bool kFault>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     extern __shared__ uint32_t wbuf[];                 // [kChunkV * W] the chunk's live words (flagged groups)
     __shared__ uint32_t actm[kChunkV / 32];            // vertices with live words
@@ -525,6 +574,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         duem[t] = 0;
     }
     if (t == 0) ncand = ngrp = 0;
+    if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
     __syncthreads();
     if (t < kGroups && t * kGV < nv) {
         const uint32_t g = (base >> kGroupShift) + t;
@@ -574,28 +624,29 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i], lv = x >> 2;
-        pt_vertex_fast<kOmit, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W]);
+        pt_vertex_fast<kFault, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W]);
     }
     flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+    flush_delays<kFault>(a);
 }
 
-template <bool kOmit>
+template <bool kFault>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_kernel(PtArgs a) {
-    pt_round_ell_body<kOmit>(a);
+    pt_round_ell_body<kFault>(a);
 }
 
 // Multi-root rounds: one launch runs the round of every
 // non-quiescent heartbeat lane, blockIdx.y = lane, each lane's arguments in
 // device memory -- the lanes' sparse rounds share the chip instead of
 // following each other launch by launch.
-template <bool kOmit>
+template <bool kFault>
 __global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __restrict__ args) {
-    pt_round_body<kOmit>(args[blockIdx.y]);
+    pt_round_body<kFault>(args[blockIdx.y]);
 }
 
-template <bool kOmit>
+template <bool kFault>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs* __restrict__ args) {
-    pt_round_ell_body<kOmit>(args[blockIdx.y]);
+    pt_round_ell_body<kFault>(args[blockIdx.y]);
 }
 
 // ---------------------------------------------------------------------------
@@ -839,7 +890,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
                 a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] =
                     make_uint2(a.rev[e], PSIM_MSG_BROADCAST | (a.wtag << kTagShift));
             } else {
-                deliver_word(a, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift));  // Round 0
+                deliver_word(a, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift), a.dhist);  // Round 0
             }
             nmsg++;
         }
@@ -953,22 +1004,29 @@ __global__ __launch_bounds__(kBlock) void pt_renorm_kernel(PtArgs a) {
     }
 }
 
-// Zero inbox words whose round tag is not `keep` (stale ones, before a tag
-// could repeat): one pass over a buffer every <= 256 rounds.
-__global__ __launch_bounds__(kBlock) void pt_scrub_kernel(uint4* __restrict__ w, unsigned long long n4, uint32_t keep) {
+// Zero inbox words whose round tag is not among the `span` rounds from
+// `keep` on (stale ones, before a tag could repeat): one pass over a buffer
+// every <= 256 rounds.  span = 1 for the double buffer, kRing - 1 for the
+// delay ring (words up to kRing - 1 rounds ahead are in flight).
+__device__ __forceinline__ uint32_t scrub_word(uint32_t x, uint32_t keep, uint32_t span) {
+    return ((word_tag(x) - keep) & 0xFFu) < span ? x : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void pt_scrub_kernel(uint4* __restrict__ w, unsigned long long n4, uint32_t keep,
+                                                          uint32_t span) {
     const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
     for (unsigned long long i = blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
         uint4 x = w[i];
-        const uint4 y = make_uint4(word_tag(x.x) == keep ? x.x : 0u, word_tag(x.y) == keep ? x.y : 0u,
-                                   word_tag(x.z) == keep ? x.z : 0u, word_tag(x.w) == keep ? x.w : 0u);
+        const uint4 y = make_uint4(scrub_word(x.x, keep, span), scrub_word(x.y, keep, span),
+                                   scrub_word(x.z, keep, span), scrub_word(x.w, keep, span));
         if (y.x != x.x || y.y != x.y || y.z != x.z || y.w != x.w) w[i] = y;
     }
 }
 
 __global__ void pt_scrub_tail_kernel(uint32_t* __restrict__ w, unsigned long long lo, unsigned long long n,
-                                     uint32_t keep) {
+                                     uint32_t keep, uint32_t span) {
     const unsigned long long i = lo + threadIdx.x;
-    if (i < n && word_tag(w[i]) != keep) w[i] = 0u;
+    if (i < n) w[i] = scrub_word(w[i], keep, span);
 }
 
 // Pack the staged cross-shard words into (global receiver slot, word)
@@ -1077,13 +1135,13 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
     }
     if (a.ell) {
         const size_t lds = size_t(kChunkV) * a.ell * 4;
-        if (a.omit)
+        if (a.omit || a.dly)
             hipLaunchKernelGGL(pt_round_ell_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
         else
             hipLaunchKernelGGL(pt_round_ell_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
         return hipGetLastError();
     }
-    if (a.omit)
+    if (a.omit || a.dly)
         hipLaunchKernelGGL(pt_round_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
     else
         hipLaunchKernelGGL(pt_round_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), 0, s, a);
@@ -1094,13 +1152,13 @@ hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_
     const dim3 grid(grid_chunks(a0.n), nlanes);
     if (a0.ell) {
         const size_t lds = size_t(kChunkV) * a0.ell * 4;
-        if (a0.omit)
+        if (a0.omit || a0.dly)
             hipLaunchKernelGGL(pt_round_ell_lanes_kernel<true>, grid, dim3(kBlock), lds, s, d_args);
         else
             hipLaunchKernelGGL(pt_round_ell_lanes_kernel<false>, grid, dim3(kBlock), lds, s, d_args);
         return hipGetLastError();
     }
-    if (a0.omit)
+    if (a0.omit || a0.dly)
         hipLaunchKernelGGL(pt_round_lanes_kernel<true>, grid, dim3(kBlock), 0, s, d_args);
     else
         hipLaunchKernelGGL(pt_round_lanes_kernel<false>, grid, dim3(kBlock), 0, s, d_args);
@@ -1154,15 +1212,16 @@ hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_lo
     return hipGetLastError();
 }
 
-hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, hipStream_t s) {
+hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, uint32_t span, hipStream_t s) {
     if (!words || !n) return hipSuccess;
     const unsigned long long n4 = n / 4;    // hipMalloc'd buffers: 16-byte aligned
     if (n4) {
         const unsigned long long g = std::min<unsigned long long>((n4 + kBlock - 1) / kBlock, 8192ull);
         hipLaunchKernelGGL(pt_scrub_kernel, dim3((uint32_t)g), dim3(kBlock), 0, s, reinterpret_cast<uint4*>(words),
-                           n4, keep);
+                           n4, keep, span);
     }
-    if (n % 4) hipLaunchKernelGGL(pt_scrub_tail_kernel, dim3(1), dim3(64), 0, s, words, n4 * 4, (unsigned long long)n, keep);
+    if (n % 4)
+        hipLaunchKernelGGL(pt_scrub_tail_kernel, dim3(1), dim3(64), 0, s, words, n4 * 4, (unsigned long long)n, keep, span);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ using namespace psim;
 namespace {
 constexpr int kChunk = 16;  // rounds launched between host synchronisations (no-op rounds exit early)
 constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-scatter engine)
-constexpr size_t kStatsRow = size_t(kStatShards) * kNStat;
+constexpr size_t kStatsRow = size_t(kStatShards) * kNStat + kDelayHist;   // shards, then messages per delay
 }  // namespace
 
 struct psim_handle {
@@ -47,6 +47,12 @@ struct psim_handle {
     uint8_t* pend[2] = {nullptr, nullptr};
     uint8_t* ost = nullptr;
     uint32_t* omit = nullptr;       // omission faults: bitmap over local sender slots (psim_set_omissions)
+    // delay faults (psim_set_delays): once installed, every lane's inbox is a
+    // ring of kRing buffers (ring, pring: the focused lane's) instead of in/pend
+    uint8_t* dly = nullptr;         // [Ed] extra rounds per device sender slot
+    uint32_t* ring = nullptr;
+    uint8_t* pring = nullptr;
+    uint64_t due[kRing] = {};       // messages pending per arrival round mod kRing (focused lane)
     // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
     struct Bin {
         uint2 *rec_c = nullptr, *rec_f = nullptr;
@@ -88,6 +94,9 @@ struct psim_handle {
         uint8_t* pend[2] = {nullptr, nullptr};
         uint8_t* ost = nullptr;
         int* ost_total = nullptr;
+        uint32_t* ring = nullptr;
+        uint8_t* pring = nullptr;
+        uint64_t due[kRing] = {};
         uint32_t par = 0, serial = 0, root = 0;
         bool have_root = false;
         int64_t ost_cnt = 0, live_rows = 0;
@@ -233,7 +242,7 @@ void free_graph(psim_handle* h) {
         swap_lane(h, 0);
         for (size_t j = 1; j < h->lanes.size(); j++) {
             auto& l = h->lanes[j];
-            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost, l.ring, l.pring};
             for (void* p : lp)
                 if (p) (void)hipFree(p);
         }
@@ -241,13 +250,16 @@ void free_graph(psim_handle* h) {
         h->cur_lane = 0;
     }
     void* ptrs[] = {h->rowp, h->col, h->rev, h->memb, h->alive, h->vs, h->in[0], h->in[1],
-                    h->pend[0], h->pend[1], h->ost};
+                    h->pend[0], h->pend[1], h->ost, h->dly, h->ring, h->pring};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->rowp = h->col = h->rev = h->memb = h->alive = nullptr;
     h->vs = nullptr;
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
+    h->dly = h->pring = nullptr;
+    h->ring = nullptr;
+    for (auto& x : h->due) x = 0;
     if (h->omit) (void)hipFree(h->omit);
     h->omit = nullptr;
     {
@@ -271,6 +283,25 @@ void free_graph(psim_handle* h) {
     h->E = 0;
     h->Ed = 0;
     h->ell = 0;
+}
+
+// Delay ring (psim_set_delays): the arguments of round R read ring slot
+// R mod kRing (tag R) and write the words of round R + 1 + d to slot
+// (R + 1 + d) mod kRing with tag R + 1 + d.
+void set_round_ring(const psim_handle* h, PtArgs& a, uint64_t R) {
+    const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+    a.dly = h->dly;
+    a.ring = h->ring;
+    a.pring = h->pring;
+    a.ed = (uint32_t)h->Ed;
+    a.ngrp = (uint32_t)ng;
+    a.rpos = uint32_t(R + 1) & (kRing - 1);
+    a.in_cur = h->ring + size_t(R & (kRing - 1)) * h->Ed;
+    a.in_nxt = h->ring + size_t(a.rpos) * h->Ed;
+    a.pend_cur = h->pring + size_t(R & (kRing - 1)) * ng;
+    a.pend_nxt = h->pring + size_t(a.rpos) * ng;
+    a.ctag = uint32_t(R) & 0xFFu;
+    a.wtag = uint32_t(R + 1) & 0xFFu;
 }
 
 PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
@@ -300,6 +331,12 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.root = h->root;
     a.omit = h->omit;
     a.ell = h->ell;
+    if (h->dly) {
+        // delay ring: `par` names the round as in[] does -- h->par reads the
+        // next round's words, h->par ^ 1 writes them (the origin)
+        set_round_ring(h, a, par == h->par ? h->round + 1 : h->round);
+        a.dhist = stats + size_t(kStatShards) * kNStat;
+    }
     if (h->bin.rec_c) {
         const auto& b = h->bin;
         a.rec_c = b.rec_c;
@@ -324,7 +361,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
 // the origin) from msgs3[(R-1) mod 3], adds its own into msgs3[R mod 3] and
 // clears msgs3[(R+1) mod 3]; lane-local, next to the lane's ost_total.
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
-    if (h->sh.world != 1 || h->bin.rec_c) return;
+    if (h->sh.world != 1 || h->bin.rec_c || h->dly) return;   // delays: a silent round may precede arrivals
     a.msgs3 = h->ost_total + 1;
     const uint32_t r = uint32_t(R % 3);
     a.mprev = (r + 2) % 3;
@@ -345,8 +382,12 @@ void set_round_tags(PtArgs& a, uint64_t R) {
 hipError_t scrub_if_needed(psim_handle* h, uint64_t last) {
     if (h->bin.rec_c || last <= h->scrub + kTagSpan) return hipSuccess;
     const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
-    for (int b = 0; b < 2; b++) {
-        const hipError_t e = launch_pt_scrub(h->in[b], h->Ed, keep, h->stream);
+    if (h->dly) {       // the ring: words for the next kRing - 1 rounds are in flight
+        const hipError_t e = launch_pt_scrub(h->ring, kRing * h->Ed, keep, kRing - 1, h->stream);
+        if (e != hipSuccess) return e;
+    }
+    for (int b = 0; b < 2 && !h->dly; b++) {
+        const hipError_t e = launch_pt_scrub(h->in[b], h->Ed, keep, 1, h->stream);
         if (e != hipSuccess) return e;
     }
     h->scrub = h->round;
@@ -360,6 +401,8 @@ void save_lane(psim_handle* h) {
     l.ost = h->ost; l.ost_total = h->ost_total; l.par = h->par; l.serial = h->serial; l.root = h->root;
     l.have_root = h->have_root; l.ost_cnt = h->ost_cnt; l.live_rows = h->live_rows; l.inflight = h->inflight;
     l.scrub = h->scrub;
+    l.ring = h->ring; l.pring = h->pring;
+    memcpy(l.due, h->due, sizeof l.due);
 }
 void load_lane(psim_handle* h, int j) {
     const auto& l = h->lanes[j];
@@ -367,6 +410,8 @@ void load_lane(psim_handle* h, int j) {
     h->ost = l.ost; h->ost_total = l.ost_total; h->par = l.par; h->serial = l.serial; h->root = l.root;
     h->have_root = l.have_root; h->ost_cnt = l.ost_cnt; h->live_rows = l.live_rows; h->inflight = l.inflight;
     h->scrub = l.scrub;
+    h->ring = l.ring; h->pring = l.pring;
+    memcpy(h->due, l.due, sizeof h->due);
     h->cur_lane = j;
 }
 void swap_lane(psim_handle* h, int j) {
@@ -425,6 +470,31 @@ int renorm_if_needed(psim_handle* h) {
     return PSIM_OK;
 }
 
+// A lane's delay ring: kRing inbox buffers and group-flag buffers, zeroed.
+int alloc_ring(psim_handle* h, uint32_t*& ring, uint8_t*& pring) {
+    const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+    ring = nullptr;
+    pring = nullptr;
+    if (hipMalloc((void**)&ring, kRing * h->Ed * 4) != hipSuccess || hipMalloc((void**)&pring, kRing * ng) != hipSuccess ||
+        hipMemset(ring, 0, kRing * h->Ed * 4) != hipSuccess || hipMemset(pring, 0, kRing * ng) != hipSuccess) {
+        if (ring) (void)hipFree(ring);
+        if (pring) (void)hipFree(pring);
+        ring = nullptr;
+        pring = nullptr;
+        return PSIM_ENOMEM;
+    }
+    return PSIM_OK;
+}
+
+// Messages of the round (or origin) `R` written per delay: pending until
+// round R + 1 + d; the lane's in-flight count is what is still pending.
+uint64_t add_due(uint64_t* due, uint64_t R, const unsigned long long* hist) {
+    for (uint32_t d = 0; d < kRing; d++) due[(R + 1 + d) & (kRing - 1)] += hist[d];
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < kRing; k++) s += due[k];
+    return s;
+}
+
 // Focus the lane of heartbeat root `root`; with `create`, give a new root a
 // lane (a fresh one while fewer than kMaxLanes exist, else the least recently
 // used quiescent lane, whose root's per-root sets are then forgotten).
@@ -450,6 +520,12 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
                 if (p) (void)hipFree(p);
             return fail(h, PSIM_ENOMEM, "heartbeat lane %zu for n=%u", L.size(), h->n);
         }
+        if (h->dly && alloc_ring(h, l.ring, l.pring) != PSIM_OK) {
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
+            for (void* p : lp)
+                if (p) (void)hipFree(p);
+            return fail(h, PSIM_ENOMEM, "delay ring of heartbeat lane %zu", L.size());
+        }
         l.ost_total = h->ost_total_base + 4 * L.size();     // {ost_total, msgs3[3]} per lane
         L.push_back(l);
         pick = (int)L.size() - 1;
@@ -471,6 +547,11 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         HIPCHK(h, hipMemsetAsync(l.pend[1], 0, ng, h->stream));
         HIPCHK(h, hipMemsetAsync(l.ost, 0, size_t(h->n) + 4, h->stream));
         HIPCHK(h, hipMemsetAsync(l.ost_total, 0, 4 * sizeof(int), h->stream));
+        if (l.ring) {
+            HIPCHK(h, hipMemsetAsync(l.ring, 0, kRing * h->Ed * 4, h->stream));
+            HIPCHK(h, hipMemsetAsync(l.pring, 0, kRing * ng, h->stream));
+        }
+        for (auto& x : l.due) x = 0;
         l.par = 0;
         l.serial = 0;
         l.have_root = false;
@@ -532,6 +613,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             PtArgs a = make_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
             set_round_slots(h, a, h->round + i + 1);
             set_round_tags(a, h->round + i + 1);
+            if (h->dly) set_round_ring(h, a, h->round + i + 1);
             par[q] ^= 1u;
             return a;
         };
@@ -583,6 +665,11 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
                 l.ost_cnt += (int64_t)r[S_OST_DELTA];
                 l.live_rows += (int64_t)r[S_LIVE_DELTA];
                 l.inflight = lm;
+                if (h->dly) {                   // round R consumed its arrivals; the sends are pending
+                    const uint64_t R = h->round + 1;
+                    l.due[R & (kRing - 1)] = 0;
+                    l.inflight = add_due(l.due, R, h->h_stats + (i * A + q) * kStatsRow + size_t(kStatShards) * kNStat);
+                }
                 msgs += lm;
                 for (int t = 0; t < kNStat; t++) tot[t] += r[t];
             }
@@ -1105,6 +1192,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
     h->ost_cnt += (int64_t)r[S_OST_DELTA];
     h->live_rows += (int64_t)r[S_LIVE_DELTA];
     h->inflight = r[PSIM_MSG_BROADCAST];
+    if (h->dly) h->inflight = lr < h->n ? add_due(h->due, h->round, h->h_stats + size_t(kStatShards) * kNStat) : 0;
     return PSIM_OK;
 }
 
@@ -1548,9 +1636,10 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     HIPCHK(hh, hipStreamSynchronize(h->stream));
     if (!h->bin.rec_c) {
         const uint32_t tag = uint32_t(h->round + 1) & 0xFFu;   // words the next round reads
+        const uint32_t* src = make_args(h, h->par, 0, h->stats).in_cur;   // in[par] or its ring slot
         if (h->ell) {                                          // ELL rows -> ABI (CSR) slots
             std::vector<uint32_t> d(h->Ed);
-            HIPCHK(hh, hipMemcpy(d.data(), h->in[h->par], h->Ed * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hh, hipMemcpy(d.data(), src, h->Ed * 4, hipMemcpyDeviceToHost));
             for (uint32_t v = 0; v < h->n; v++)
                 for (uint64_t e = h->h_rowp[v]; e < h->h_rowp[v + 1]; e++) {
                     const uint32_t w = d[uint64_t(v) * h->ell + (e - h->h_rowp[v])];
@@ -1558,7 +1647,7 @@ int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
                 }
             return PSIM_OK;
         }
-        HIPCHK(hh, hipMemcpy(words, h->in[h->par], h->E * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hh, hipMemcpy(words, src, h->E * 4, hipMemcpyDeviceToHost));
         for (uint64_t i = 0; i < h->E; i++) words[i] = live_word(words[i], tag) ? abi_word(words[i]) : 0u;
         return PSIM_OK;
     }
@@ -1832,6 +1921,46 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
     if (!hit) return PSIM_OK;                          // healed (or no local edge affected)
     if (hipMalloc((void**)&h->omit, bm.size() * 4) != hipSuccess) return fail(h, PSIM_ENOMEM, "omission bitmap");
     HIPCHK(h, hipMemcpy(h->omit, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
+    return PSIM_OK;
+}
+
+int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
+    if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
+    if (h->sh.world != 1 || h->bin.rec_c)
+        return fail(h, PSIM_ESTATE, "delay faults need the single-GPU slot-scatter engine");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    save_lane(h);
+    for (const auto& l : h->lanes)
+        if (l.inflight) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
+    std::vector<uint8_t> dl(h->Ed, 0);
+    for (size_t i = 0; i < k; i++) {
+        if (src[i] >= h->n || dst[i] >= h->n)
+            return fail(h, PSIM_EINVAL, "delay pair (%u, %u) out of range", src[i], dst[i]);
+        if (rounds[i] > kMaxDelay) return fail(h, PSIM_EINVAL, "delay %u > %u rounds", rounds[i], kMaxDelay);
+        const uint32_t u = src[i];
+        const auto b = h->h_col.begin() + h->h_rowp[u], e = h->h_col.begin() + h->h_rowp[u + 1];
+        const auto it = std::lower_bound(b, e, dst[i]);
+        if (it == e || *it != dst[i]) continue;        // not an overlay edge: nothing ever flows
+        size_t s = size_t(it - h->h_col.begin());
+        if (h->ell) s = size_t(u) * h->ell + (s - h->h_rowp[u]);   // device (ELL) slot
+        dl[s] = rounds[i];
+    }
+    if (!h->dly) {
+        // switch every lane to the ring; nothing is in flight, so no word moves
+        if (hipMalloc((void**)&h->dly, h->Ed) != hipSuccess) return fail(h, PSIM_ENOMEM, "delay table");
+        const int focus = h->cur_lane;
+        for (int j = 0; j < (int)h->lanes.size(); j++) {
+            auto& l = h->lanes[j];
+            if (alloc_ring(h, l.ring, l.pring) != PSIM_OK) {
+                load_lane(h, focus);
+                return fail(h, PSIM_ENOMEM, "delay ring of heartbeat lane %d", j);
+            }
+            for (auto& x : l.due) x = 0;
+        }
+        load_lane(h, focus);
+    }
+    HIPCHK(h, hipMemcpy(h->dly, dl.data(), h->Ed, hipMemcpyHostToDevice));
     return PSIM_OK;
 }
 

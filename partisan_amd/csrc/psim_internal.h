@@ -67,6 +67,9 @@ constexpr uint32_t kMaxRound = 0xFFFu;
 constexpr uint32_t kTagSpan = 256;     // rounds before a tag repeats
 constexpr uint32_t kNoPeer = 0xFFFFFFFFu;   // col of an ELL padding slot
 constexpr uint32_t kEllMax = 8;              // widest ELL row (the round kernel's register-resident rows)
+constexpr uint32_t kRing = 16;               // inbox ring with delay faults: a word is written <= kRing - 1
+constexpr uint32_t kMaxDelay = kRing - 2;    // rounds ahead of the round that reads the slot being written
+constexpr int kDelayHist = kRing;            // per-round stats row tail: messages per delay
 __host__ __device__ inline uint32_t word_tag(uint32_t w) { return (w >> kTagShift) & 0xFFu; }
 // a word carries messages for the round whose tag is `tag`
 __host__ __device__ inline bool live_word(uint32_t w, uint32_t tag) { return (w & kFifoMask) && word_tag(w) == tag; }
@@ -109,6 +112,14 @@ struct PtArgs {
     uint32_t ell;                          // row width of the ELL slot layout (slot s of v = v*ell + s;
                                            // padding slots: col = kNoPeer), 0 = CSR (rowp)
     const uint32_t* __restrict__ omit;     // [ceil(E/32)] omission faults over sender slots, or null
+    // delay faults (psim_set_delays; null dly: none): the inbox is a ring of
+    // kRing buffers, ring slot k holding the words read by the rounds = k mod kRing
+    const uint8_t* __restrict__ dly;       // [E] extra rounds per sender slot (<= kMaxDelay)
+    uint32_t* __restrict__ ring;           // [kRing][ed] inbox words
+    uint8_t* __restrict__ pring;           // [kRing][ngrp] group flags
+    unsigned long long* __restrict__ dhist;  // [kRing] messages written this round per delay
+    uint32_t rpos;                         // ring slot read by the round after this one
+    uint32_t ed, ngrp;                     // words per ring slot, flags per ring slot
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}
     uint2* __restrict__ rec_f;             // [E] fine-bin regions
@@ -408,7 +419,7 @@ hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
 // zero every inbox word whose round tag is not `keep` (psim_internal.h word format)
-hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, hipStream_t s);
+hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, uint32_t span, hipStream_t s);
 hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_local, unsigned long long E,
                           unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,

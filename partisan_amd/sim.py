@@ -137,6 +137,25 @@ class Simulator:
         self._c(lib().psim_set_omissions(self._h, s.ctypes.data_as(C.POINTER(C.c_uint32)),
                                          d.ctypes.data_as(C.POINTER(C.c_uint32)), len(p)))
 
+    def set_delays(self, pairs, rounds):
+        """Delay faults (psim_set_delays): messages over directed (src, dst)
+        pairs arrive rounds[i] rounds late; [] removes them.  Raises with
+        PSIM_EBUSY while messages are in flight."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        s, d = np.ascontiguousarray(p[:, 0]), np.ascontiguousarray(p[:, 1])
+        r = np.ascontiguousarray(np.asarray(rounds, dtype=np.uint8).reshape(-1))
+        if len(r) != len(p):
+            raise ValueError("one delay per pair")
+        self._c(lib().psim_set_delays(self._h, s.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      d.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      r.ctypes.data_as(C.POINTER(C.c_uint8)), len(p)))
+
+    def egress_delay(self, v, rounds):
+        """partisan's egress_delay for node v: every out-edge of v delayed."""
+        rp = np.asarray(self.slot_row_ptr, dtype=np.int64)
+        col = np.asarray(self.slot_col, dtype=np.uint32)[rp[v]:rp[v + 1]]
+        return np.stack([np.full(len(col), v, np.uint32), col], axis=1), np.full(len(col), rounds, np.uint8)
+
     def partition_pairs(self, group):
         """Directed overlay edges (of this handle's vertices) whose ends lie in
         different groups: group[v] = partition of global vertex v."""

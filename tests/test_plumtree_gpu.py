@@ -511,3 +511,145 @@ def test_round_tags_across_wrap(psim):
         assert m == orc.heartbeat(5)
         compare(sim, orc, 5, m)
         lockstep(sim, orc, 5, m)
+
+
+def _delay_pairs(sim, frac, dmax, seed):
+    rng = np.random.default_rng(seed)
+    src = np.repeat(np.arange(sim.n), np.diff(sim.slot_row_ptr.astype(np.int64)))
+    pick = rng.random(len(src)) < frac
+    pairs = np.stack([src[pick], sim.slot_col[pick]], axis=1)
+    return pairs, rng.integers(1, dmax + 1, len(pairs)).astype(np.uint8)
+
+
+def _delay_lockstep(sim, orc, root, mono, max_rounds=300):
+    """lockstep() whose end also waits for the delayed messages."""
+    for r in range(max_rounds):
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (r, k, gs, os_)
+        assert gs["delivered_new"] == os_["delivered_new"], r
+        compare(sim, orc, root, mono)
+        if orc.inflight() == 0 and os_["outstanding_live"] == 0:
+            return r + 1
+    raise AssertionError("no quiescence")
+
+
+@pytest.mark.parametrize("n,seed,L,dmax", [(600, 1, 1, 3), (1500, 2, 2, 14), (1000, 3, 1, 6)])
+def test_delay_faults_lockstep(psim, n, seed, L, dmax):
+    """Delay faults (partisan_SUITE with_egress_delay / with_ingress_delay):
+    30 % of the directed edges deliver 1..dmax rounds late.  Round by round
+    against the oracle -- every clause sees its messages in the same round and
+    order, the late eager pushes turn into prunes, lazy i_haves race the
+    delayed pushes -- over a flood and two tree heartbeats; psim_run's round
+    count (it waits for the pending delayed messages) equals the oracle's."""
+    rp, col = psim.overlay.random_regular(n, 5, 200 + seed)
+    sim, orc = make(psim, rp, col, L)
+    pairs, d = _delay_pairs(sim, 0.3, dmax, seed)
+    if psim.engine == "binned":
+        with pytest.raises(psim.PsimError):
+            sim.set_delays(pairs, d)
+        return
+    sim.set_delays(pairs, d)
+    orc.set_delays(pairs, d)
+    root = seed * 7 % n
+    for _ in range(2):
+        m = sim.broadcast(root)
+        assert m == orc.heartbeat(root)
+        compare(sim, orc, root, m)
+        _delay_lockstep(sim, orc, root, m)
+    assert sim.delivered().all()
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    gst, gr = sim.run(1000)
+    ost, orr = orc.run(1000)
+    assert gr == orr
+    assert [x["broadcast"] for x in gst] == [x["broadcast"] for x in ost]
+    assert sim.delivered().all()
+
+
+def test_delay_faults_egress_and_busy(psim):
+    """A node's egress delay (all its out-edges) on the heartbeat root, with
+    omission faults on other edges at the same time; changing delays while
+    messages are in flight is refused (PSIM_EBUSY), as it could reorder a
+    pair; removing them (k = 0) while quiescent restores next-round delivery."""
+    if psim.engine == "binned":
+        return
+    rp, col = psim.overlay.random_regular(800, 5, 211)
+    sim, orc = make(psim, rp, col, 1)
+    root = 5
+    pairs, d = sim.egress_delay(root, 4)
+    sim.set_delays(pairs, d)
+    orc.set_delays(pairs, d)
+    op, _ = _delay_pairs(sim, 0.05, 1, 9)
+    op = op[op[:, 0] != root]
+    sim.set_omissions(op)
+    orc.set_omissions(op)
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    gs, os_ = sim.step(3), orc.step(3)
+    assert sum(g["delivered_new"] for g in gs) == 0 == sum(o["delivered_new"] for o in os_)
+    with pytest.raises(psim.PsimError):
+        sim.set_delays([], [])                     # the root's pushes are still on the wire
+    with pytest.raises(RuntimeError):
+        orc.set_delays([], [])
+    _delay_lockstep(sim, orc, root, m)
+    sim.set_omissions([])
+    orc.set_omissions([])
+    sim.set_delays([], [])
+    orc.set_delays([], [])
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    _delay_lockstep(sim, orc, root, m)
+    assert sim.delivered().all()
+
+
+def test_delay_faults_multi_root():
+    """Delays with several heartbeat lanes in flight (each lane gets its own
+    ring), checked per root against the oracle."""
+    import partisan_amd as pa
+    rp, col = pa.overlay.random_regular(900, 5, 221)
+    sim = pa.Simulator()
+    sim.load_overlay(rp, col)
+    orc = O.Plumtree(rp, col, lazy_tick_rounds=1)
+    pairs, d = _delay_pairs(sim, 0.25, 5, 4)
+    sim.set_delays(pairs, d)
+    orc.set_delays(pairs, d)
+    monos = {}
+    schedule = {0: [0, 7], 3: [450]}
+    for rnd in range(45):
+        for root in schedule.get(rnd, []):
+            m = sim.broadcast(root)
+            assert m == orc.heartbeat(root)
+            monos[root] = m
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (rnd, k, gs, os_)
+        assert gs["delivered_new"] == os_["delivered_new"], rnd
+        _multi_compare(sim, orc, monos)
+    for root in monos:
+        sim.focus(root)
+        assert sim.delivered().all()
+    sim.close()
+
+
+def test_delay_faults_across_tag_wrap(psim):
+    """The delay ring's words carry their arrival round's tag: idle gaps of
+    hundreds of rounds (tag wraps, ring scrubs keeping the next 15 rounds)
+    between heartbeats whose messages are up to 14 rounds late."""
+    if psim.engine == "binned":
+        return
+    rp, col = psim.overlay.random_regular(500, 5, 231)
+    sim, orc = make(psim, rp, col, 1)
+    pairs, d = _delay_pairs(sim, 0.4, 14, 12)
+    sim.set_delays(pairs, d)
+    orc.set_delays(pairs, d)
+    for gap in (0, 300, 257, 250):
+        if gap:
+            sim.step(gap)
+            orc.step(gap)
+        m = sim.broadcast(9)
+        assert m == orc.heartbeat(9)
+        _delay_lockstep(sim, orc, 9, m)
+        sim.step(7)                                # part of the next gap with rows still acked late
+        orc.step(7)
+        compare(sim, orc, 9, m)
