@@ -60,14 +60,22 @@ static uint32_t lcg(uint64_t* s) {
     return (uint32_t)(*s >> 33);
 }
 
-int main(void) {
+/* the report goes to argv[1] (the libraries may write to stdout) */
+static FILE* g_out;
+
+int main(int argc, char** argv) {
     mock_nif_load_fn load;
+    g_out = argc > 1 ? fopen(argv[1], "w") : stdout;
+    if (!g_out) {
+        fprintf(stderr, "FAIL open %s\n", argv[1]);
+        return 1;
+    }
     g_funcs = mock_nif_table(&g_nfuncs, &load);
     if (load(ENV, NULL, 0) != 0) {
         fprintf(stderr, "FAIL load\n");
         return 1;
     }
-    printf("{");
+    fprintf(g_out, "{");
     /* ---- C2 in small: HyParView overlay, then a Plumtree heartbeat -------- */
     {
         const uint32_t n = 2000;
@@ -108,7 +116,7 @@ int main(void) {
         uint64_t got = 0;
         for (size_t i = 0; i < dsz; i++) got += d[i];
         ERL_NIF_TERM th = mock_elem(want_ok_tuple("trace_hash", call("trace_hash", 1, A(sim))), 1);
-        printf("\"c2\": {\"n\": %u, \"edges\": %llu, \"mono\": %llu, \"rounds\": %llu, \"delivered\": %llu, "
+        fprintf(g_out, "\"c2\": {\"n\": %u, \"edges\": %llu, \"mono\": %llu, \"rounds\": %llu, \"delivered\": %llu, "
                "\"broadcasts\": %llu, \"trace\": [\"%llu\", \"%llu\", \"%llu\", \"%llu\"]}",
                n, (unsigned long long)e, (unsigned long long)mock_int(mock_elem(bc, 1)), (unsigned long long)rounds,
                (unsigned long long)got, (unsigned long long)bsum, (unsigned long long)mock_int(mock_elem(th, 0)),
@@ -125,7 +133,7 @@ int main(void) {
         d = mock_bin_data(mock_elem(dl7, 1), &dsz);
         uint64_t got7 = 0;
         for (size_t i = 0; i < dsz; i++) got7 += d[i];
-        printf(", \"shard_rccl_world1\": {\"rounds\": %llu, \"delivered\": %llu}",
+        fprintf(g_out, ", \"shard_rccl_world1\": {\"rounds\": %llu, \"delivered\": %llu}",
                (unsigned long long)mock_int(mock_elem(sr, 1)), (unsigned long long)got7);
         free(rp);
         free(col);
@@ -140,7 +148,7 @@ int main(void) {
         const uint64_t* seen = (const uint64_t*)mock_bin_data(mock_elem(r, 2), &sz);
         uint64_t full = 0;
         for (size_t i = 0; i < sz / 8; i++) full += seen[i] == ~0ull;
-        printf(", \"demers\": {\"n\": 20000, \"rounds\": %llu, \"complete\": %llu}",
+        fprintf(g_out, ", \"demers\": {\"n\": 20000, \"rounds\": %llu, \"complete\": %llu}",
                (unsigned long long)mock_int(mock_elem(r, 1)), (unsigned long long)full);
     }
     /* ---- SCAMP v2 join waves ---------------------------------------------- */
@@ -170,7 +178,7 @@ int main(void) {
         const uint32_t* npv = (const uint32_t*)mock_bin_data(mock_elem(vw, 2), &sz);
         uint64_t tot = 0;
         for (size_t i = 0; i < sz / 4; i++) tot += npv[i];
-        printf(", \"scamp\": {\"n\": %u, \"pv_sum\": %llu, \"view_entries\": %llu}", n, (unsigned long long)pv,
+        fprintf(g_out, ", \"scamp\": {\"n\": %u, \"pv_sum\": %llu, \"view_entries\": %llu}", n, (unsigned long long)pv,
                (unsigned long long)tot);
     }
     /* ---- full membership (C1 shape: 16 nodes join node 0) ------------------ */
@@ -195,7 +203,7 @@ int main(void) {
         const uint32_t* tn = (const uint32_t*)mock_bin_data(mock_elem(tk, 1), &tsz);
         uint64_t ident = 0;
         for (uint32_t i = 0; i < n; i++) ident += tn[i] == i;          /* token v = node v's init/1 add */
-        printf(", \"fullmem\": {\"n\": %u, \"knows_all\": %llu, \"tokens_used\": %llu, \"own_tokens\": %llu}", n,
+        fprintf(g_out, ", \"fullmem\": {\"n\": %u, \"knows_all\": %llu, \"tokens_used\": %llu, \"own_tokens\": %llu}", n,
                (unsigned long long)full, (unsigned long long)mock_int(mock_elem(tk, 2)), (unsigned long long)ident);
     }
     /* ---- C3: SCAMP v2 churn + Plumtree repair ------------------------------- */
@@ -227,7 +235,7 @@ int main(void) {
         for (int i = 0; i < 20; i++) crash[i] = 100 + 17 * i;
         want_ok("c3_crash", call("c3_crash", 2, A(sim, u32s(crash, 20))));
         want_ok_tuple("c3_step", call("c3_step", 2, A(sim, mock_uint(2))));
-        printf(", \"c3\": {\"n\": %u, \"delivered_live\": %llu, \"live\": %llu}", n, (unsigned long long)dl,
+        fprintf(g_out, ", \"c3\": {\"n\": %u, \"delivered_live\": %llu, \"live\": %llu}", n, (unsigned long long)dl,
                (unsigned long long)live);
     }
     /* ---- causal delivery ------------------------------------------------------ */
@@ -240,7 +248,7 @@ int main(void) {
         for (size_t i = 0; i < mock_list_len(st); i++)
             if (mock_map_get(mock_list_nth(st, i), "delivered", &x)) delivered += x;
         want_ok_tuple("causal_clocks", call("causal_clocks", 1, A(sim)));
-        printf(", \"causal\": {\"n\": 1000, \"delivered\": %llu}", (unsigned long long)delivered);
+        fprintf(g_out, ", \"causal\": {\"n\": 1000, \"delivered\": %llu}", (unsigned long long)delivered);
     }
     /* ---- vclock merge on dense lanes ------------------------------------------ */
     {
@@ -250,9 +258,10 @@ int main(void) {
         ERL_NIF_TERM m = want_ok_tuple("vclock", call("vclock", 4, A(sim, mock_atom("merge"), u32s(a, 64), u32s(b, 64))));
         size_t sz;
         const uint32_t* o = (const uint32_t*)mock_bin_data(mock_elem(m, 1), &sz);
-        printf(", \"vclock_merge\": [%u, %u, %u]", o[0], o[5], o[7]);
+        fprintf(g_out, ", \"vclock_merge\": [%u, %u, %u]", o[0], o[5], o[7]);
     }
-    printf("}\n");
+    fprintf(g_out, "}\n");
+    if (g_out != stdout) fclose(g_out);
     mock_drop_terms();      /* resource destructors: psim_destroy on every handle */
     return 0;
 }

@@ -46,11 +46,12 @@ def _lcg(s):
 
 
 @pytest.mark.gpu
-def test_nif_harness_on_gpu():
+def test_nif_harness_on_gpu(tmp_path):
     exe = build_harness()
-    out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    report = tmp_path / "report.json"
+    out = subprocess.run([exe, str(report)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
-    rep = json.loads(out.stdout)
+    rep = json.loads(report.read_text())
     n = rep["c2"]["n"]
     assert rep["c2"]["delivered"] == n                       # the reliable-broadcast postcondition
     assert rep["shard_rccl_world1"] == {"rounds": rep["c2"]["rounds"], "delivered": n}
