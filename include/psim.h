@@ -124,8 +124,13 @@ int  psim_plumtree_reset_trees(psim_handle* h);
  * (:341-368) -> partisan_plumtree_broadcast:broadcast/2 (:324-326) ->
  * handle_cast({broadcast, Id, Payload, Mod}) (:565-569).  Emits round-0
  * eager pushes delivered by the next step.  *mono_out = the Monotonic of
- * the id {Root, Epoch, Monotonic}.  PSIM_EBUSY if the previous broadcast is
- * not quiescent. */
+ * the id {Root, Epoch, Monotonic}.  A root may heartbeat again while its
+ * previous heartbeats are in flight (the backend's timer does not wait):
+ * on one GPU with the slot-scatter engine its lane then becomes a window
+ * lane (ptwin.hip) that keeps each heartbeat's messages, rows and the
+ * backend's timestamp interval set apart -- the same per-root eager / lazy
+ * sets, per-message ids -- from then until the lane is reused.  Sharded,
+ * binned and delay-fault handles keep one heartbeat per root: PSIM_EBUSY. */
 int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
 /* Several roots: on one GPU without PSIM_CFG_BINNED each
  * heartbeat root gets a lane of its own (per-root eager / lazy sets, rows,
@@ -156,6 +161,22 @@ int  psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n);
  * RECEIVER: bits 0..15 = FIFO of 4-bit PSIM_MSG_* kinds (first in the low
  * nibble), bits 16..31 = Round carried by broadcast / i_have.  words[E]. */
 int  psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words);
+/* Every message the next round delivers to this handle's vertices, in the
+ * order they are handled (receiver, then sender, then emission order): its
+ * sender, receiver (global ids), PSIM_MSG_* kind, Round and Monotonic (prune
+ * carries neither: 0).  Any array may be NULL; *count = total, entries past
+ * cap are not written.  Works for both lane kinds (psim_get_inflight is the
+ * static lanes' word view). */
+int  psim_get_messages(const psim_handle* h, uint32_t* src, uint32_t* dst, uint32_t* kind, uint32_t* round,
+                       uint32_t* mono, size_t cap, size_t* count);
+/* Vertex v's outstanding i_have rows in insertion order (the ETS bag
+ * {Peer, {Id, Mod, Round, Root}}, :1207-1219): peer, Round, Monotonic. */
+int  psim_get_rows(const psim_handle* h, uint32_t v, uint32_t* peer, uint32_t* round, uint32_t* mono, size_t cap,
+                   size_t* count);
+/* delivered[n]: Mod:is_stale({Root, Epoch, mono}) (backend :229-244) for the
+ * focused root, any Monotonic of a window lane; a static lane answers for
+ * its newest heartbeat only (PSIM_EINVAL otherwise). */
+int  psim_get_delivered_mono(const psim_handle* h, uint32_t mono, uint8_t* delivered, size_t n);
 /* Omission faults (test/prop_partisan_crash_fault_model.erl:117-196, send /
  * receive omission interposition funs): every Plumtree message over a
  * directed pair (src[i], dst[i]) is sent -- counted, the sender moves on --

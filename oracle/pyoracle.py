@@ -506,6 +506,13 @@ class Plumtree:
         lib().orc_pt_pending(self._h, arr, n)
         return [(m.src, m.dst, m.type, m.round) for m in arr[:n]]
 
+    def pending_full(self):
+        """(src, dst, kind, Round, Monotonic) of the messages the next round delivers, in handling order."""
+        n = lib().orc_pt_pending(self._h, None, 0)
+        arr = (Msg * max(1, n))()
+        lib().orc_pt_pending(self._h, arr, n)
+        return [(m.src, m.dst, m.type, m.round, m.id_mono) for m in arr[:n]]
+
     def peers(self, v, root, cap=4096):
         e = (C.c_uint32 * cap)()
         l_ = (C.c_uint32 * cap)()

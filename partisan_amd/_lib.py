@@ -174,6 +174,11 @@ SIGNATURES = {
     "psim_plumtree_focus": (C.c_int, [_H, C.c_uint32]),
     "psim_set_omissions": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_set_delays": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
+    "psim_get_messages": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),
+                                    _P(C.c_uint32), C.c_size_t, _P(C.c_size_t)]),
+    "psim_get_rows": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t,
+                                _P(C.c_size_t)]),
+    "psim_get_delivered_mono": (C.c_int, [_H, C.c_uint32, _P(C.c_uint8), C.c_size_t]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
     "psim_shard_init": (C.c_int, [_H, C.c_int, C.c_int]),
     "psim_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),

@@ -23,6 +23,21 @@ constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-
 constexpr size_t kStatsRow = size_t(kStatShards) * kNStat + kDelayHist;   // shards, then messages per delay
 }  // namespace
 
+// A window lane's device state (ptwin.hip; psim_internal.h WinArgs)
+struct Win {
+    uint4* iset = nullptr;
+    psim::PdRow* rows = nullptr;
+    uint2* head = nullptr;
+    psim::PdMsg* msg[2] = {nullptr, nullptr};   // records read / written by a round (lane parity)
+    uint32_t* nmsg = nullptr;                   // [2] record counts
+    uint32_t cap = 0;
+    ~Win() {
+        void* p[] = {iset, rows, head, msg[0], msg[1], nmsg};
+        for (void* x : p)
+            if (x) (void)hipFree(x);
+    }
+};
+
 struct psim_handle {
     psim_config cfg{};
     int device = 0;
@@ -53,6 +68,10 @@ struct psim_handle {
     uint32_t* ring = nullptr;
     uint8_t* pring = nullptr;
     uint64_t due[kRing] = {};       // messages pending per arrival round mod kRing (focused lane)
+    Win* win = nullptr;             // the focused lane's window state (null: a static lane)
+    // window lanes' bucketing scratch (shared: lanes run one after another)
+    uint32_t *w_cnt = nullptr, *w_cur = nullptr, *w_off = nullptr, *w_idx = nullptr, *w_bsum = nullptr;
+    size_t w_idx_cap = 0;
     // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
     struct Bin {
         uint2 *rec_c = nullptr, *rec_f = nullptr;
@@ -97,6 +116,7 @@ struct psim_handle {
         uint32_t* ring = nullptr;
         uint8_t* pring = nullptr;
         uint64_t due[kRing] = {};
+        Win* win = nullptr;
         uint32_t par = 0, serial = 0, root = 0;
         bool have_root = false;
         int64_t ost_cnt = 0, live_rows = 0;
@@ -245,6 +265,7 @@ void free_graph(psim_handle* h) {
             void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost, l.ring, l.pring};
             for (void* p : lp)
                 if (p) (void)hipFree(p);
+            delete l.win;
         }
         h->lanes.clear();
         h->cur_lane = 0;
@@ -259,6 +280,15 @@ void free_graph(psim_handle* h) {
     h->pend[0] = h->pend[1] = h->ost = nullptr;
     h->dly = h->pring = nullptr;
     h->ring = nullptr;
+    delete h->win;
+    h->win = nullptr;
+    {
+        void* wp[] = {h->w_cnt, h->w_cur, h->w_off, h->w_idx, h->w_bsum};
+        for (void* p : wp)
+            if (p) (void)hipFree(p);
+        h->w_cnt = h->w_cur = h->w_off = h->w_idx = h->w_bsum = nullptr;
+        h->w_idx_cap = 0;
+    }
     for (auto& x : h->due) x = 0;
     if (h->omit) (void)hipFree(h->omit);
     h->omit = nullptr;
@@ -356,6 +386,89 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     return a;
 }
 
+// ---- window lanes (ptwin.hip) ----------------------------------------------
+uint32_t cur_mono(const psim_handle* h) {
+    const auto it = h->mono_of.find(h->root);
+    return h->have_root && it != h->mono_of.end() ? it->second : 0u;
+}
+
+// Arguments of the focused window lane for the round reading records[par].
+WinArgs make_win_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
+    WinArgs a{};
+    a.n = h->n;
+    a.v_lo = h->sh.v_lo;
+    a.ell = h->ell;
+    a.mono = cur_mono(h);
+    a.mono8 = h->serial & 0xFFu;
+    a.epoch8 = h->epoch & 0xFFu;
+    a.tick = tick;
+    a.rowp = h->rowp;
+    a.col = h->col;
+    a.memb = h->memb;
+    a.alive = h->alive;
+    a.omit = h->omit;
+    a.vs = h->vs;
+    a.iset = h->win->iset;
+    a.rows = h->win->rows;
+    a.head = h->win->head;
+    a.ost = h->ost;
+    a.in = h->win->msg[par];
+    a.nin = h->win->nmsg + par;
+    a.off = h->w_off;
+    a.idx = h->w_idx;
+    a.out = h->win->msg[par ^ 1];
+    a.nout = h->win->nmsg + (par ^ 1);
+    a.cap = h->win->cap;
+    a.stats = stats;
+    return a;
+}
+
+// Window lanes need the per-message machinery of the single-GPU static
+// engine (not the binned one; delay faults keep their own ring).
+bool win_capable(const psim_handle* h) { return h->sh.world == 1 && !h->bin.rec_c && !h->dly; }
+
+// The focused static lane becomes a window lane (its root heartbeats again
+// while a heartbeat is in flight).  Nothing is lost: ptwin.hip
+// win_convert_kernel restates the lane's state and in-flight words.
+int to_window(psim_handle* h) {
+    const size_t n = h->n;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(4ull * h->Ed + 4096, 0xF0000000ull);
+    const size_t nb = (n + kBlock - 1) / kBlock;
+    if (!h->w_cnt) {
+        if (!alloc_zero((void**)&h->w_cnt, n * 4) || !alloc_zero((void**)&h->w_cur, n * 4) ||
+            !alloc_zero((void**)&h->w_off, (n + 1) * 4) || !alloc_zero((void**)&h->w_bsum, nb * 4))
+            return fail(h, PSIM_ENOMEM, "window lane scratch for n=%zu", n);
+    }
+    if (h->w_idx_cap < cap) {
+        if (h->w_idx) (void)hipFree(h->w_idx);
+        h->w_idx = nullptr;
+        h->w_idx_cap = 0;
+        if (!alloc_zero((void**)&h->w_idx, size_t(cap) * 4)) return fail(h, PSIM_ENOMEM, "window lane scratch");
+        h->w_idx_cap = cap;
+    }
+    Win* w = new Win();
+    w->cap = cap;
+    if (!alloc_zero((void**)&w->iset, n * 2 * sizeof(uint4)) || !alloc_zero((void**)&w->rows, n * kWinRows * sizeof(PdRow)) ||
+        !alloc_zero((void**)&w->head, n * sizeof(uint2)) || !alloc_zero((void**)&w->msg[0], size_t(cap) * sizeof(PdMsg)) ||
+        !alloc_zero((void**)&w->msg[1], size_t(cap) * sizeof(PdMsg)) || !alloc_zero((void**)&w->nmsg, 16)) {
+        delete w;
+        return fail(h, PSIM_ENOMEM, "window lane of root %u (n=%zu)", h->root, n);
+    }
+    h->win = w;
+    h->lanes[h->cur_lane].win = w;
+    WinArgs a = make_win_args(h, h->par, 0, h->stats);
+    a.out = w->msg[h->par];            // the words the next round reads become its records
+    a.nout = w->nmsg + h->par;
+    const PtArgs pa = make_args(h, h->par, 0, h->stats);
+    HIPCHK(h, launch_win_convert(a, pa, h->stream));
+    uint32_t cnt = 0;
+    HIPCHK(h, hipMemcpyAsync(&cnt, w->nmsg + h->par, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (cnt > cap) return fail(h, PSIM_EOVERFLOW, "window lane: %u in-flight messages > %u", cnt, cap);
+    h->inflight = cnt;
+    return PSIM_OK;
+}
+
 // Early exit of no-op rounds (psim_step / psim_run on one GPU with the
 // slot-scatter engine): round R reads the messages emitted by round R-1 (or
 // the origin) from msgs3[(R-1) mod 3], adds its own into msgs3[R mod 3] and
@@ -403,6 +516,7 @@ void save_lane(psim_handle* h) {
     l.scrub = h->scrub;
     l.ring = h->ring; l.pring = h->pring;
     memcpy(l.due, h->due, sizeof l.due);
+    l.win = h->win;
 }
 void load_lane(psim_handle* h, int j) {
     const auto& l = h->lanes[j];
@@ -412,6 +526,7 @@ void load_lane(psim_handle* h, int j) {
     h->scrub = l.scrub;
     h->ring = l.ring; h->pring = l.pring;
     memcpy(h->due, l.due, sizeof h->due);
+    h->win = l.win;
     h->cur_lane = j;
 }
 void swap_lane(psim_handle* h, int j) {
@@ -552,6 +667,8 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
             HIPCHK(h, hipMemsetAsync(l.pring, 0, kRing * ng, h->stream));
         }
         for (auto& x : l.due) x = 0;
+        delete l.win;                               // a reused window lane starts static again
+        l.win = nullptr;
         l.par = 0;
         l.serial = 0;
         l.have_root = false;
@@ -618,8 +735,19 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             return a;
         };
         HIPCHK(h, hipMemsetAsync(h->stats, 0, k * A * kStatsRow * sizeof(unsigned long long), h->stream));
+        bool any_win = false;
+        for (size_t q = 0; q < A; q++) any_win |= h->lanes[act[q]].win != nullptr;
+        // a window lane's round: bucket its records, handle them (ptwin.hip)
+        auto win_round = [&](size_t q, uint32_t i, uint32_t tick) -> hipError_t {
+            load_lane(h, act[q]);
+            const WinArgs a = make_win_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
+            par[q] ^= 1u;
+            const hipError_t e = hipMemsetAsync(a.nout, 0, 4, h->stream);
+            if (e != hipSuccess) return e;
+            return launch_win_round(a, h->w_cnt, h->w_cur, h->w_bsum, h->stream);
+        };
 #ifndef PT_LANE_LAUNCHES
-        if (A > 1) {
+        if (A > 1 && !any_win) {
             // several lanes: one launch per round over all of them (blockIdx.y = lane)
             for (uint32_t i = 0; i < k; i++) {
                 const uint32_t tick = ((h->round + i + 1) % L) == 0;
@@ -637,7 +765,10 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         for (uint32_t i = 0; i < k; i++) {
             const uint32_t tick = ((h->round + i + 1) % L) == 0;
             HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-            for (size_t q = 0; q < A; q++) HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
+            for (size_t q = 0; q < A; q++) {
+                if (h->lanes[act[q]].win) HIPCHK(h, win_round(q, i, tick));
+                else HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
+            }
             HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
         }
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
@@ -655,8 +786,10 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
                 if (r[S_OVERFLOW]) {
                     load_lane(h, focus);
                     return fail(h, PSIM_EOVERFLOW,
-                                "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 65535, "
-                                "4: outstanding rows of an older heartbeat, 8: a bin region overran)",
+                                "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 4095, "
+                                "4: outstanding rows of an older heartbeat, 8: a bin region overran; window lanes: "
+                                "16: message records full, 32: > 32 outstanding rows at a vertex, "
+                                "64: a timestamp set of > 4 intervals, 128: a message off the overlay)",
                                 (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
                 }
                 auto& l = h->lanes[act[q]];
@@ -1157,7 +1290,18 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         const int rc = focus_root(h, root, true);
         if (rc) return rc;
     }
-    if (!quiescent(h)) return fail(h, PSIM_EBUSY, "previous broadcast of this root still in flight");
+    if (!quiescent(h) || (h->ost_cnt > 0 && win_capable(h) && !h->win)) {
+        // the root heartbeats again while its last heartbeat is in flight
+        // (backend :341-368), or rows of it wait for a dead peer: its lane
+        // keeps every heartbeat apart from then on
+        if (!win_capable(h))
+            return fail(h, PSIM_EBUSY, "previous broadcast of this root still in flight (sharded, binned or "
+                                       "delay-fault handles keep one heartbeat per root)");
+        if (!h->win) {
+            const int rc = to_window(h);
+            if (rc) return rc;
+        }
+    }
     if (!lanes_enabled(h) && h->have_root && root != h->root) {
         // single-root engine: the previous root's per-root sets are dropped
         // (DESIGN.md "Limitations": multi-root trees are SURVEY 8(f) row 1)
@@ -1177,21 +1321,30 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
     const uint32_t lr = root - h->sh.v_lo;
     if (lr < h->n) {
         HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
-        // origin emits into the buffer the next round reads
-        PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
-        set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
-        a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
-        a.root = lr;
-        HIPCHK(h, launch_pt_origin(a, h->stream));
+        if (h->win) {                           // window lane: records for the next round
+            WinArgs a = make_win_args(h, h->par, 0, h->stats);
+            a.out = h->win->msg[h->par];
+            a.nout = h->win->nmsg + h->par;
+            HIPCHK(h, launch_win_origin(a, lr, h->stream));
+        } else {
+            // origin emits into the buffer the next round reads
+            PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+            set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
+            a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
+            a.root = lr;
+            HIPCHK(h, launch_pt_origin(a, h->stream));
+        }
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         reduce_row(h->h_stats, r);
-        if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "origin: outstanding rows of an older heartbeat");
+        if (r[S_OVERFLOW])
+            return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat; "
+                        "window lanes: 32: > 32 rows, 64: > 4 timestamp intervals)", r[S_OVERFLOW]);
     }
     h->ost_cnt += (int64_t)r[S_OST_DELTA];
     h->live_rows += (int64_t)r[S_LIVE_DELTA];
-    h->inflight = r[PSIM_MSG_BROADCAST];
+    h->inflight = (h->win ? h->inflight : 0) + r[PSIM_MSG_BROADCAST];
     if (h->dly) h->inflight = lr < h->n ? add_due(h->due, h->round, h->h_stats + size_t(kStatShards) * kNStat) : 0;
     return PSIM_OK;
 }
@@ -1617,6 +1770,113 @@ int psim_get_plumtree(const psim_handle* h, uint32_t* eager, uint32_t* lazy, uin
     return PSIM_OK;
 }
 
+int psim_get_messages(const psim_handle* h, uint32_t* src, uint32_t* dst, uint32_t* kind, uint32_t* round,
+                      uint32_t* mono, size_t cap, size_t* count) {
+    if (!h || !count || !h->n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    std::vector<PdMsg> m;
+    if (h->win) {
+        uint32_t k = 0;
+        HIPCHK(hh, hipMemcpy(&k, h->win->nmsg + h->par, 4, hipMemcpyDeviceToHost));
+        k = std::min(k, h->win->cap);
+        m.resize(k);
+        if (k) HIPCHK(hh, hipMemcpy(m.data(), h->win->msg[h->par], size_t(k) * sizeof(PdMsg), hipMemcpyDeviceToHost));
+        std::sort(m.begin(), m.end(), [](const PdMsg& x, const PdMsg& y) {
+            return x.dst != y.dst ? x.dst < y.dst : (x.src != y.src ? x.src < y.src : x.seq < y.seq);
+        });
+    } else {
+        // one heartbeat: the words' FIFOs; a graft / ignored_i_have answers
+        // the receiver's own i_have, whose Round is the receiver's pushed Round
+        std::vector<uint32_t> w(h->E);
+        std::vector<uint4> vs(h->n);
+        int rc = psim_get_inflight(h, w.data(), h->E);
+        if (rc) return rc;
+        HIPCHK(hh, hipMemcpy(vs.data(), h->vs, size_t(h->n) * 16, hipMemcpyDeviceToHost));
+        const uint32_t mo = cur_mono(h);
+        for (uint32_t v = 0; v < h->n; v++)
+            for (uint64_t e = h->h_rowp[v]; e < h->h_rowp[v + 1]; e++) {
+                uint32_t f = w[e] & 0xFFFFu, q = 0;
+                for (; f; f >>= 4) {
+                    PdMsg x;
+                    x.type = f & 0xFu;
+                    x.src = h->h_col[e];
+                    x.dst = h->sh.v_lo + v;
+                    x.seq = q++;
+                    x.mono = x.type == PSIM_MSG_PRUNE ? 0u : mo;
+                    x.round = (x.type == PSIM_MSG_BROADCAST || x.type == PSIM_MSG_IHAVE) ? (w[e] >> 16)
+                            : (x.type == PSIM_MSG_PRUNE ? 0u : (vs[v].w & 0xFFFFu));
+                    m.push_back(x);
+                }
+            }
+    }
+    *count = m.size();
+    for (size_t i = 0; i < m.size() && i < cap; i++) {
+        if (src) src[i] = m[i].src;
+        if (dst) dst[i] = m[i].dst;
+        if (kind) kind[i] = m[i].type;
+        if (round) round[i] = m[i].round;
+        if (mono) mono[i] = m[i].mono;
+    }
+    return PSIM_OK;
+}
+
+int psim_get_rows(const psim_handle* h, uint32_t v, uint32_t* peer, uint32_t* round, uint32_t* mono, size_t cap,
+                  size_t* count) {
+    if (!h || !count || !h->n || v >= h->n || h->bin.rec_c) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    std::vector<PdRow> r;
+    if (h->win) {
+        uint2 hd;
+        HIPCHK(hh, hipMemcpy(&hd, h->win->head + v, sizeof hd, hipMemcpyDeviceToHost));
+        r.resize(std::min<uint32_t>(hd.x, kWinRows));
+        if (!r.empty())
+            HIPCHK(hh, hipMemcpy(r.data(), h->win->rows + size_t(v) * kWinRows, r.size() * sizeof(PdRow),
+                                 hipMemcpyDeviceToHost));
+    } else {
+        uint4 st;
+        HIPCHK(hh, hipMemcpy(&st, h->vs + v, 16, hipMemcpyDeviceToHost));
+        for (uint32_t m = st.z; m; m &= m - 1) {
+            const uint32_t s = __builtin_ctz(m);
+            r.push_back(PdRow{h->h_col[h->h_rowp[v] + s], cur_mono(h), st.w & 0xFFFFu});
+        }
+    }
+    *count = r.size();
+    for (size_t i = 0; i < r.size() && i < cap; i++) {
+        if (peer) peer[i] = r[i].peer;
+        if (round) round[i] = r[i].round;
+        if (mono) mono[i] = r[i].mono;
+    }
+    return PSIM_OK;
+}
+
+int psim_get_delivered_mono(const psim_handle* h, uint32_t mono, uint8_t* delivered, size_t n) {
+    if (!h || !delivered || n != h->n || !h->n) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    if (!h->win) {
+        if (mono != cur_mono(h))
+            return fail(hh, PSIM_EINVAL, "a static lane keeps the newest heartbeat (%u) only", cur_mono(h));
+        return psim_get_delivered(h, delivered, n);
+    }
+    HIPCHK(hh, hipSetDevice(h->device));
+    const size_t need = n;
+    if (hh->scratch_cap < need) {
+        if (hh->scratch_buf) (void)hipFree(hh->scratch_buf);
+        hh->scratch_buf = nullptr;
+        hh->scratch_cap = 0;
+        if (hipMalloc(&hh->scratch_buf, need) != hipSuccess) return fail(hh, PSIM_ENOMEM, "delivered scratch");
+        hh->scratch_cap = need;
+    }
+    HIPCHK(hh, launch_win_delivered(make_win_args(h, h->par, 0, h->stats), mono, (uint8_t*)hh->scratch_buf,
+                                    h->stream));
+    HIPCHK(hh, hipMemcpyAsync(delivered, hh->scratch_buf, n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
 int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
     if (!h || !delivered || n != h->n || !h->n) return PSIM_EINVAL;
     psim_handle* hh = const_cast<psim_handle*>(h);
@@ -1632,6 +1892,7 @@ int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
 int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     if (!h || !words || n_words != h->E) return PSIM_EINVAL;
     psim_handle* hh = const_cast<psim_handle*>(h);
+    if (h->win) return fail(hh, PSIM_ESTATE, "window lane (several heartbeats in flight): use psim_get_messages");
     HIPCHK(hh, hipSetDevice(h->device));
     HIPCHK(hh, hipStreamSynchronize(h->stream));
     if (!h->bin.rec_c) {
@@ -1931,8 +2192,10 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
-    for (const auto& l : h->lanes)
+    for (const auto& l : h->lanes) {
         if (l.inflight) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
+        if (l.win) return fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
+    }
     std::vector<uint8_t> dl(h->Ed, 0);
     for (size_t i = 0; i < k; i++) {
         if (src[i] >= h->n || dst[i] >= h->n)
@@ -1971,8 +2234,9 @@ int psim_trace_hash(const psim_handle* h, uint64_t* out) {
     PtArgs a = make_args(h, h->par, 0, h->stats);
     const uint32_t rl = h->have_root ? h->root - h->sh.v_lo : 0xFFFFFFFFu;
     HIPCHK(hh, hipMemsetAsync(h->scratch, 0, 32, h->stream));
-    HIPCHK(hh, launch_pt_hash(a, h->serial != 0, rl < h->n ? rl : 0xFFFFFFFFu, h->bin.rec_c ? 0ull : h->Ed,
-                              h->scratch, h->stream));
+    HIPCHK(hh, launch_pt_hash(a, h->serial != 0, rl < h->n ? rl : 0xFFFFFFFFu,
+                              (h->bin.rec_c || h->win) ? 0ull : h->Ed, h->scratch, h->stream));
+    if (h->win) HIPCHK(hh, launch_win_hash(make_win_args(h, h->par, 0, h->stats), h->scratch, h->stream));
     unsigned long long r[4];
     HIPCHK(hh, hipMemcpyAsync(r, h->scratch, 32, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hh, hipStreamSynchronize(h->stream));

@@ -374,9 +374,56 @@ struct PdArgs {
     uint32_t *cnt, *cur, *off, *idx, *bsum;
     unsigned long long* __restrict__ stats;   // [kPdNStat]
 };
+// messages of a.in bucketed by destination: off[n+1], idx[] (order inside a bucket unspecified)
+hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s);
 hipError_t launch_pd_init(const PdArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s);
 hipError_t launch_pd_round(const PdArgs& a, hipStream_t s);
+
+// Window lanes (ptwin.hip): a heartbeat root whose previous
+// heartbeat is still in flight when it heartbeats again.  The lane keeps the
+// slot-mask eager / lazy sets of the static engine, and per vertex the
+// backend's timestamp interval set for the root (<= kWinIs disjoint
+// intervals of Monotonics), the outstanding rows {Peer, Monotonic, Round} in
+// insertion order and an emission counter; messages are PdMsg records
+// carrying their heartbeat's Monotonic and Round, bucketed by receiver and
+// handled in (src, emission seq) order, as in the C3 engine.
+constexpr uint32_t kWinIs = 4;        // intervals of a vertex's timestamp set
+constexpr uint32_t kWinRows = 32;     // outstanding rows per vertex
+struct WinArgs {
+    uint32_t n, v_lo, ell;            // as PtArgs
+    uint32_t mono;                    // Monotonic of the root's newest heartbeat
+    uint32_t mono8, epoch8, tick;
+    const uint32_t* __restrict__ rowp;
+    const uint32_t* __restrict__ col;
+    const uint32_t* __restrict__ memb;
+    const uint32_t* __restrict__ alive;   // bitmap over global ids
+    const uint32_t* __restrict__ omit;    // omission bitmap over sender slots, or null
+    uint4* __restrict__ vs;           // eager, lazy, OR of the rows' slots, myround | rseq | epoch (as PtArgs)
+    uint4* __restrict__ iset;         // [n][2]: lo[kWinIs], hi[kWinIs]; lo == 0: unused
+    PdRow* __restrict__ rows;         // [n][kWinRows]
+    uint2* __restrict__ head;         // [n]: rows, emission seq
+    uint8_t* __restrict__ ost;        // [n] 1 = rows exist (the static engine's flag: psim_set_alive counts from it)
+    const PdMsg* __restrict__ in;     // this round's messages, bucketed: off[n+1], idx
+    const uint32_t* nin;
+    const uint32_t* __restrict__ off;
+    uint32_t* __restrict__ idx;
+    PdMsg* __restrict__ out;          // messages for the next round
+    uint32_t* nout;
+    uint32_t cap;
+    unsigned long long* __restrict__ stats;   // [kStatShards][kNStat] (the static engine's row)
+};
+// bucket a.in by receiver (cnt, cur: [n], bsum: [ceil(n / kBlock)] scratch), then the round
+hipError_t launch_win_round(const WinArgs& a, uint32_t* cnt, uint32_t* cur, uint32_t* bsum, hipStream_t s);
+hipError_t launch_win_origin(const WinArgs& a, uint32_t root_local, hipStream_t s);
+// a static-engine lane becomes a window lane: rows from the outstanding
+// masks, the timestamp sets from the current delivery, the in-flight words
+// of `pa` (the words the next round reads) as records
+hipError_t launch_win_convert(const WinArgs& a, const PtArgs& pa, hipStream_t s);
+// psim_trace_hash out[1] over the in-flight records
+hipError_t launch_win_hash(const WinArgs& a, unsigned long long* out, hipStream_t s);
+// delivered[v] = Mod:is_stale({root, epoch, mono})
+hipError_t launch_win_delivered(const WinArgs& a, uint32_t mono, uint8_t* out, hipStream_t s);
 
 // Cross-shard exchange owned by a handle (transport.hip).  Calls return
 // PSIM_* codes and put a detail into *err.

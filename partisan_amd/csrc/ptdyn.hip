@@ -430,7 +430,7 @@ hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pd_round(const PdArgs& a, hipStream_t s) {
+hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
@@ -439,6 +439,12 @@ hipError_t launch_pd_round(const PdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(pd_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
     hipLaunchKernelGGL(pd_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(pd_scatter, dim3(kPdStrideBlocks), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pd_round(const PdArgs& a, hipStream_t s) {
+    const hipError_t e = launch_pd_bucket(a, s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(pd_process, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }

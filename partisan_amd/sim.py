@@ -121,6 +121,29 @@ class Simulator:
         self._c(lib().psim_get_delivered(self._h, _u8p(out), self.n))
         return out
 
+    def delivered_mono(self, mono):
+        """Mod:is_stale({root, epoch, mono}) per vertex (psim_get_delivered_mono)."""
+        out = np.zeros(self.n, np.uint8)
+        self._c(lib().psim_get_delivered_mono(self._h, mono, _u8p(out), self.n))
+        return out
+
+    def messages(self):
+        """Messages the next round delivers, in handling order: a list of
+        (src, dst, kind, Round, Monotonic) (psim_get_messages)."""
+        k = C.c_size_t(0)
+        self._c(lib().psim_get_messages(self._h, None, None, None, None, None, 0, C.byref(k)))
+        a = [np.zeros(max(1, k.value), np.uint32) for _ in range(5)]
+        self._c(lib().psim_get_messages(self._h, *[_u32p(x) for x in a], k.value, C.byref(k)))
+        return list(zip(*[x[:k.value].tolist() for x in a]))
+
+    def rows(self, v):
+        """Vertex v's outstanding i_have rows in insertion order: (peer, Round, Monotonic)."""
+        k = C.c_size_t(0)
+        self._c(lib().psim_get_rows(self._h, v, None, None, None, 0, C.byref(k)))
+        a = [np.zeros(max(1, k.value), np.uint32) for _ in range(3)]
+        self._c(lib().psim_get_rows(self._h, v, *[_u32p(x) for x in a], k.value, C.byref(k)))
+        return list(zip(*[x[:k.value].tolist() for x in a]))
+
     def inflight(self):
         w = np.zeros(max(1, self.num_slots), np.uint32)
         self._c(lib().psim_get_inflight(self._h, _u32p(w), self.num_slots))

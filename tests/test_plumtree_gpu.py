@@ -653,3 +653,114 @@ def test_delay_faults_across_tag_wrap(psim):
         sim.step(7)                                # part of the next gap with rows still acked late
         orc.step(7)
         compare(sim, orc, 9, m)
+
+
+def _win_compare(sim, orc, root, monos):
+    """Window lanes: every heartbeat in flight checked apart -- delivered
+    per Monotonic, rows {peer, Round, Monotonic} in insertion order, the
+    messages with their ids in handling order -- plus the shared eager /
+    lazy sets and the newest heartbeat's Rounds."""
+    for m in monos:
+        assert np.array_equal(sim.delivered_mono(m), orc.delivered(root, m)), m
+    eager, lazy, _, rr = sim.plumtree_state()
+    orr = orc.recv_round(root, monos[-1])
+    for v in range(sim.n):
+        oe, ol = orc.peers(v, root)
+        assert sim.mask_to_peers(v, eager[v]) == oe, f"eager set of {v}"
+        assert sim.mask_to_peers(v, lazy[v]) == ol, f"lazy set of {v}"
+        assert sim.rows(v) == orc.outstanding(v), f"rows of {v}"
+        want = 0xFFFF if orr[v] == 0xFFFFFFFF else (0xFFFE if orr[v] == 0xFFFFFFFE else orr[v])
+        assert rr[v] == want, v
+    assert sim.messages() == orc.pending_full(), "in-flight messages differ"
+
+
+def _win_step(sim, orc, root, monos):
+    gs, os_ = sim.step(1)[0], orc.step(1)[0]
+    for k in KINDS:
+        assert gs[k] == os_[k], (k, gs, os_)
+    assert gs["delivered_new"] == os_["delivered_new"]
+    _win_compare(sim, orc, root, monos)
+    return gs, os_
+
+
+@pytest.mark.parametrize("n,seed,L", [(400, 1, 1), (1200, 2, 2), (800, 3, 1)])
+def test_overlapping_heartbeats_lockstep(psim, n, seed, L):
+    """SURVEY 8(f) row 1 / backend :341-368: the root heartbeats every 3
+    rounds during its own flood.  Its lane turns into a window lane at the
+    second heartbeat; round by round against the oracle, every heartbeat's
+    deliveries, rows and messages are kept apart (the backend's interval set
+    answers is_stale per Monotonic), over the shared per-root eager / lazy
+    sets; the run ends quiescent with every heartbeat delivered everywhere."""
+    rp, col = psim.overlay.random_regular(n, 5, 300 + seed)
+    sim, orc = make(psim, rp, col, L)
+    root = 11 * seed % n
+    monos = []
+    if psim.engine == "binned":
+        sim.broadcast(root)
+        sim.step(2)
+        with pytest.raises(psim.PsimError):
+            sim.broadcast(root)              # one heartbeat per root on the binned engine
+        return
+    for rnd in range(60):
+        if rnd % 3 == 0 and rnd <= 12:
+            m = sim.broadcast(root)
+            assert m == orc.heartbeat(root)
+            monos.append(m)
+            _win_compare(sim, orc, root, monos)
+        gs, os_ = _win_step(sim, orc, root, monos)
+        if rnd > 12 and sum(gs[k] for k in KINDS) == 0 and os_["outstanding_live"] == 0:
+            break
+    for m in monos:
+        assert sim.delivered_mono(m).all(), m
+    stats, r = sim.run(100)
+    assert r == 0 or all(sum(s[k] for k in KINDS) == 0 for s in stats)
+
+
+def test_window_lane_with_faults_and_dead_peers(psim):
+    """A window lane under omission faults and dead vertices: vertices die
+    after the first flood, so the second leaves rows to dead lazy peers (a
+    static lane would then hold rows of an older heartbeat: the next
+    heartbeat switches the lane), omitted messages are counted and lost;
+    lockstep with the oracle throughout, then every vertex revives."""
+    if psim.engine == "binned":
+        return
+    n = 900
+    rp, col = psim.overlay.random_regular(n, 5, 331)
+    sim, orc = make(psim, rp, col, 1)
+    root = 4
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    lockstep(sim, orc, root, m)
+    rng = np.random.default_rng(3)
+    alive = np.ones(n, np.uint8)
+    alive[rng.choice(n, 60, replace=False)] = 0
+    alive[root] = 1
+    sim.set_alive(alive)
+    orc.set_alive(alive)
+    monos = [sim.broadcast(root)]
+    assert monos[0] == orc.heartbeat(root)
+    for _ in range(25):
+        _win_step(sim, orc, root, monos)
+    assert any(orc.outstanding(v) for v in range(n))          # rows to dead peers outlive the flood
+    src = np.repeat(np.arange(n), np.diff(sim.slot_row_ptr.astype(np.int64)))
+    pick = rng.random(len(src)) < 0.05
+    pairs = np.stack([src[pick], sim.slot_col[pick]], axis=1)
+    sim.set_omissions(pairs)
+    orc.set_omissions(pairs)
+    for rnd in range(40):
+        if rnd in (0, 2, 7):
+            m = sim.broadcast(root)
+            assert m == orc.heartbeat(root)
+            monos.append(m)
+        if rnd == 20:
+            sim.set_omissions([])
+            orc.set_omissions([])
+        _win_step(sim, orc, root, monos)
+    sim.set_alive(np.ones(n, np.uint8))
+    orc.set_alive(np.ones(n, np.uint8))
+    m = sim.broadcast(root)
+    assert m == orc.heartbeat(root)
+    monos.append(m)
+    for _ in range(30):
+        _win_step(sim, orc, root, monos)
+    assert sim.delivered_mono(m).all()
