@@ -292,13 +292,20 @@ int  psim_rccl_unique_id(uint8_t* id_out /* PSIM_RCCL_ID_BYTES */);
 int  psim_shard_init_rccl(psim_handle* h, int rank, int world, const uint8_t* id /* PSIM_RCCL_ID_BYTES */);
 int  psim_shard_set_transport(psim_handle* h, const psim_transport* t);
 /* heartbeat at `root` on every rank (collective): the origin's pushes are
- * exchanged before it returns */
+ * exchanged before it returns.  Through this in-library path a sharded
+ * handle has heartbeat lanes as on one GPU (one per root, window lanes for a
+ * root heartbeating while its last heartbeat is in flight); every rank
+ * decides busy / window / lane reuse on the same all-reduced counts.  The
+ * split-phase entry points above return PSIM_ESTATE once a handle has more
+ * than one lane or a window lane. */
 int  psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out);
 /* collective: rounds until global quiescence (or max_rounds); stats are the
  * GLOBAL per-round counters (summed over ranks; kernel_ms this rank's),
  * *xs this rank's exchange figures (may be NULL) */
 int  psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds_run,
                     psim_exchange_stats* xs);
+/* Exactly `rounds` rounds of psim_shard_run (collective; no quiescence stop). */
+int  psim_shard_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap, psim_exchange_stats* xs);
 
 /* --- partisan_vclock on dense lanes ----------------------------------- */
 /* A clock is PSIM_VC_LANES u32 lanes, lane i = actor i (actor ids are ranks

@@ -199,6 +199,7 @@ SIGNATURES = {
     "psim_shard_set_transport": (C.c_int, [_H, _P(Transport)]),
     "psim_shard_broadcast_x": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
     "psim_shard_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32), _P(ExchangeStats)]),
+    "psim_shard_step": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(ExchangeStats)]),
     "psim_demers_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_demers_broadcast_all": (C.c_int, [_H]),
     "psim_demers_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),

@@ -72,6 +72,10 @@ struct psim_handle {
     // window lanes' bucketing scratch (shared: lanes run one after another)
     uint32_t *w_cnt = nullptr, *w_cur = nullptr, *w_off = nullptr, *w_idx = nullptr, *w_bsum = nullptr;
     size_t w_idx_cap = 0;
+    // sharded window lanes: records split by receiver shard (ptwin.hip)
+    psim::PdMsg* w_send = nullptr;
+    uint32_t *w_counts = nullptr, *w_rcnt = nullptr, *w_base = nullptr, *w_cursor = nullptr;
+    uint32_t w_send_cap = 0;
     // binned engine (single GPU with PSIM_CFG_BINNED): DESIGN.md 5.1
     struct Bin {
         uint2 *rec_c = nullptr, *rec_f = nullptr;
@@ -117,6 +121,9 @@ struct psim_handle {
         uint8_t* pring = nullptr;
         uint64_t due[kRing] = {};
         Win* win = nullptr;
+        // sharded handles: the lane's GLOBAL state after the last collective
+        // (every rank decides busy / window / eviction on the same values)
+        int64_t g_inflight = 0, g_live = 0, g_ost = 0;
         uint32_t par = 0, serial = 0, root = 0;
         bool have_root = false;
         int64_t ost_cnt = 0, live_rows = 0;
@@ -283,11 +290,15 @@ void free_graph(psim_handle* h) {
     delete h->win;
     h->win = nullptr;
     {
-        void* wp[] = {h->w_cnt, h->w_cur, h->w_off, h->w_idx, h->w_bsum};
+        void* wp[] = {h->w_cnt, h->w_cur, h->w_off, h->w_idx, h->w_bsum, h->w_send, h->w_counts, h->w_rcnt,
+                      h->w_base, h->w_cursor};
         for (void* p : wp)
             if (p) (void)hipFree(p);
         h->w_cnt = h->w_cur = h->w_off = h->w_idx = h->w_bsum = nullptr;
+        h->w_counts = h->w_rcnt = h->w_base = h->w_cursor = nullptr;
+        h->w_send = nullptr;
         h->w_idx_cap = 0;
+        h->w_send_cap = 0;
     }
     for (auto& x : h->due) x = 0;
     if (h->omit) (void)hipFree(h->omit);
@@ -425,7 +436,8 @@ WinArgs make_win_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigne
 
 // Window lanes need the per-message machinery of the single-GPU static
 // engine (not the binned one; delay faults keep their own ring).
-bool win_capable(const psim_handle* h) { return h->sh.world == 1 && !h->bin.rec_c && !h->dly; }
+bool lanes_enabled(const psim_handle* h);
+bool win_capable(const psim_handle* h) { return lanes_enabled(h) && !h->dly; }
 
 // The focused static lane becomes a window lane (its root heartbeats again
 // while a heartbeat is in flight).  Nothing is lost: ptwin.hip
@@ -534,8 +546,15 @@ void swap_lane(psim_handle* h, int j) {
     save_lane(h);
     load_lane(h, j);
 }
-bool lanes_enabled(const psim_handle* h) { return h->sh.world == 1 && !h->bin.rec_c; }
-bool lane_quiescent(const psim_handle::Lane& l) { return l.inflight == 0 && l.live_rows == 0; }
+// Heartbeat lanes: one GPU with the slot-scatter engine, or a sharded
+// handle whose exchange is in the library (psim_shard_broadcast_x /
+// psim_shard_run / psim_shard_step); the split-phase sharded entry points
+// keep one lane.
+bool lanes_enabled(const psim_handle* h) { return !h->bin.rec_c && (h->sh.world == 1 || h->sh.xport); }
+bool lane_quiescent(const psim_handle* h, const psim_handle::Lane& l) {
+    if (h->sh.world > 1) return l.g_inflight == 0 && l.g_live == 0;
+    return l.inflight == 0 && l.live_rows == 0;
+}
 
 // Binned engine geometry: fine bins of 2^fv vertices whose slots fit the LDS
 // inbox, coarse bins of 2^cv vertices with about sqrt(#fine) fine bins each.
@@ -572,7 +591,15 @@ void reduce_row(const unsigned long long* row, unsigned long long* out) {
         }
 }
 
-bool quiescent(const psim_handle* h) { return h->inflight == 0 && h->live_rows == 0; }
+bool quiescent(const psim_handle* h) {
+    if (h->sh.world > 1 && !h->lanes.empty()) return lane_quiescent(h, h->lanes[h->cur_lane]);
+    return h->inflight == 0 && h->live_rows == 0;
+}
+// vertices holding rows (all shards)
+int64_t rows_held(const psim_handle* h) {
+    if (h->sh.world > 1 && !h->lanes.empty()) return h->lanes[h->cur_lane].g_ost;
+    return h->ost_cnt;
+}
 
 int renorm_if_needed(psim_handle* h) {
     const int focus = h->cur_lane;
@@ -648,7 +675,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
     }
     if (pick < 0) {                                 // evict the least recently used quiescent lane
         for (int j = 0; j < (int)L.size(); j++)
-            if (lane_quiescent(L[j]) && (pick < 0 || L[j].last_use < L[pick].last_use)) pick = j;
+            if (lane_quiescent(h, L[j]) && (pick < 0 || L[j].last_use < L[pick].last_use)) pick = j;
         if (pick < 0) return fail(h, PSIM_EBUSY, "all %d heartbeat lanes are in flight", kMaxLanes);
         fresh = true;
     }
@@ -669,6 +696,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         for (auto& x : l.due) x = 0;
         delete l.win;                               // a reused window lane starts static again
         l.win = nullptr;
+        l.g_inflight = l.g_live = l.g_ost = 0;
         l.par = 0;
         l.serial = 0;
         l.have_root = false;
@@ -704,7 +732,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     } refocus{h, focus};
     auto all_quiet = [&]() {
         for (const auto& l : h->lanes)
-            if (!lane_quiescent(l)) return false;
+            if (!lane_quiescent(h, l)) return false;
         return true;
     };
     bool done = stop_q && all_quiet();
@@ -714,7 +742,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         // focused lane always runs, so a plain psim_step still launches)
         std::vector<int> act;
         for (int j = 0; j < (int)h->lanes.size(); j++)
-            if (j == focus || !lane_quiescent(h->lanes[j])) act.push_back(j);
+            if (j == focus || !lane_quiescent(h, h->lanes[j])) act.push_back(j);
         const size_t A = act.size();
         // inbox parities advance on a copy, committed once every launch of the
         // chunk is enqueued (a failed launch leaves the lanes' parities alone)
@@ -1279,6 +1307,16 @@ int psim_plumtree_reset_trees(psim_handle* h) {
 
 namespace {
 
+int ingest_dense(psim_handle* h, const void* recv_dev);
+
+// The split-phase sharded entry points drive the focused lane's words only.
+int one_lane_only(psim_handle* h) {
+    if (h->lanes.size() > 1 || h->win)
+        return fail(h, PSIM_ESTATE, "several heartbeat lanes or a window lane: drive with psim_shard_broadcast_x / "
+                                    "psim_shard_run / psim_shard_step");
+    return PSIM_OK;
+}
+
 // Shared by psim_plumtree_broadcast and psim_shard_broadcast: every shard
 // advances the same serial / epoch / Monotonic; only the root's owner runs
 // the origin kernel.  Returns the origin's emitted-message stats row.
@@ -1290,7 +1328,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         const int rc = focus_root(h, root, true);
         if (rc) return rc;
     }
-    if (!quiescent(h) || (h->ost_cnt > 0 && win_capable(h) && !h->win)) {
+    if (!quiescent(h) || (rows_held(h) > 0 && win_capable(h) && !h->win)) {
         // the root heartbeats again while its last heartbeat is in flight
         // (backend :341-368), or rows of it wait for a dead peer: its lane
         // keeps every heartbeat apart from then on
@@ -1407,6 +1445,7 @@ int psim_shard_layout(const psim_handle* h, uint64_t* region_base, size_t world)
 int psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev, uint64_t send_cap,
                          uint64_t* counts, int64_t* local_live) {
     if (!h || !counts) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
     unsigned long long r[kNStat];
     int rc = broadcast_common(h, root, mono_out, r);
     if (rc) return rc;
@@ -1417,6 +1456,7 @@ int psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void
 int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts,
                      psim_round_stats* st, int64_t* local_live) {
     if (!h || !counts) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
     HIPCHK(h, hipSetDevice(h->device));
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
@@ -1477,6 +1517,7 @@ int psim_shard_recv_layout(const psim_handle* h, uint64_t* recv_base, size_t wor
 
 int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev) {
     if (!h) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
     if (h->sh.world > 1 && !send_dev) return PSIM_EINVAL;
     if (h->sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
     unsigned long long r[kNStat];
@@ -1490,6 +1531,7 @@ int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out
 
 int psim_shard_round_async(psim_handle* h, void* send_dev) {
     if (!h) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
     auto& sh = h->sh;
     if (sh.world > 1 && !send_dev) return PSIM_EINVAL;
@@ -1514,6 +1556,15 @@ int psim_shard_round_async(psim_handle* h, void* send_dev) {
 
 int psim_shard_ingest_dense(psim_handle* h, const void* recv_dev) {
     if (!h) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
+    return ingest_dense(h, recv_dev);
+}
+
+}  // extern "C"
+
+namespace {
+// the focused lane's received words -> the inbox the next round reads
+int ingest_dense(psim_handle* h, const void* recv_dev) {
     auto& sh = h->sh;
     const uint64_t nr = sh.recv_base.empty() ? 0 : sh.recv_base[sh.world];
     if (nr == 0) return PSIM_OK;
@@ -1523,6 +1574,9 @@ int psim_shard_ingest_dense(psim_handle* h, const void* recv_dev) {
     HIPCHK(h, launch_pt_ingest_dense(a, (const uint32_t*)recv_dev, sh.recv_map, (uint32_t)nr, sh.slot2v, h->stream));
     return PSIM_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32_t* n_out, int64_t* local_live) {
     if (!h) return PSIM_EINVAL;
@@ -1621,34 +1675,237 @@ int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs) {
     if (rc) return fail(h, rc, "exchange: %s", err.c_str());
     HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
     if (xs) xs->fabric_bytes += 4ull * (sh.send_base[sh.world] - (sh.send_base[sh.rank + 1] - sh.send_base[sh.rank]));
-    return psim_shard_ingest_dense(h, sh.xrecv);
+    return ingest_dense(h, sh.xrecv);
 }
 
-}  // namespace
-
-extern "C" {
-
-int psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out) {
-    if (!h) return PSIM_EINVAL;
-    int rc = x_buffers(h);
-    if (rc) return rc;
-    rc = psim_shard_broadcast_dense(h, root, mono_out, h->sh.xsend);
-    if (rc) return rc;
-    rc = x_exchange(h, 0, nullptr);
-    if (rc) return rc;
+// Sharded window lane: the records the last round (or origin) wrote into
+// msg[par] go to the shards owning their receivers -- counts all-to-all,
+// records all-to-all-v -- and msg[par] ends up holding exactly this shard's
+// records for the next round (own ones first, then by source rank).
+int win_exchange(psim_handle* h, psim_exchange_stats* xs) {
+    auto& sh = h->sh;
+    const uint32_t W = (uint32_t)sh.world, R = (uint32_t)sh.rank;
+    if (W == 1) return PSIM_OK;
+    if (W > kWinMaxWorld) return fail(h, PSIM_EINVAL, "window lanes support up to %u shards", kWinMaxWorld);
+    Win& w = *h->win;
+    const uint32_t par = h->par;
+    if (!h->w_counts) {
+        if (!alloc_zero((void**)&h->w_counts, kWinMaxWorld * 4) || !alloc_zero((void**)&h->w_rcnt, kWinMaxWorld * 4) ||
+            !alloc_zero((void**)&h->w_base, kWinMaxWorld * 4) || !alloc_zero((void**)&h->w_cursor, kWinMaxWorld * 4))
+            return fail(h, PSIM_ENOMEM, "window exchange counters");
+    }
+    if (h->w_send_cap < w.cap) {
+        if (h->w_send) (void)hipFree(h->w_send);
+        h->w_send = nullptr;
+        h->w_send_cap = 0;
+        if (!alloc_zero((void**)&h->w_send, size_t(w.cap) * sizeof(PdMsg))) return fail(h, PSIM_ENOMEM, "window send buffer");
+        h->w_send_cap = w.cap;
+    }
+    HIPCHK(h, hipMemsetAsync(h->w_counts, 0, W * 4, h->stream));
+    HIPCHK(h, launch_win_split(w.msg[par], w.nmsg + par, w.cap, sh.n_global, W, h->w_counts, h->stream));
+    std::vector<uint64_t> one(W + 1);
+    for (uint32_t i = 0; i <= W; i++) one[i] = i;
+    std::string err;
+    int rc = sh.xport->alltoallv(h->w_counts, one.data(), h->w_rcnt, one.data(), (int)R, (int)W, h->stream, &err);
+    if (rc) return fail(h, rc, "window counts exchange: %s", err.c_str());
+    std::vector<uint32_t> cnt(W), rcv(W);
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), h->w_counts, W * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(rcv.data(), h->w_rcnt, W * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    rcv[R] = cnt[R];
+    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+    std::vector<uint32_t> base(W);
+    for (uint32_t i = 0; i < W; i++) {
+        base[i] = (uint32_t)soff[i];
+        soff[i + 1] = soff[i] + cnt[i];
+        roff[i + 1] = roff[i] + rcv[i];
+    }
+    if (roff[W] > w.cap) return fail(h, PSIM_EOVERFLOW, "window lane: %llu records for one shard > %u",
+                                     (unsigned long long)roff[W], w.cap);
+    HIPCHK(h, hipMemcpyAsync(h->w_base, base.data(), W * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->w_cursor, 0, W * 4, h->stream));
+    HIPCHK(h, launch_win_scatter(w.msg[par], w.nmsg + par, w.cap, sh.n_global, W, h->w_base, h->w_cursor, h->w_send,
+                                 h->stream));
+    if (cnt[R])     // own records (an RCCL all-to-all-v skips the own rank)
+        HIPCHK(h, hipMemcpyAsync(w.msg[par] + roff[R], h->w_send + soff[R], size_t(cnt[R]) * sizeof(PdMsg),
+                                 hipMemcpyDeviceToDevice, h->stream));
+    constexpr uint64_t kW = sizeof(PdMsg) / 4;
+    for (auto& x : soff) x *= kW;
+    for (auto& x : roff) x *= kW;
+    rc = sh.xport->alltoallv(reinterpret_cast<const uint32_t*>(h->w_send), soff.data(),
+                             reinterpret_cast<uint32_t*>(w.msg[par]), roff.data(), (int)R, (int)W, h->stream, &err);
+    if (rc) return fail(h, rc, "window records exchange: %s", err.c_str());
+    const uint32_t total = uint32_t(roff[W] / kW);
+    HIPCHK(h, hipMemcpyAsync(w.nmsg + par, &total, 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (xs) xs->fabric_bytes += sizeof(PdMsg) * (soff[W] / kW - cnt[R]);
+    h->inflight = total;
     return PSIM_OK;
 }
 
-int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, uint32_t* rounds_run,
-                   psim_exchange_stats* xs) {
+// After a sharded broadcast: the focused lane's global in-flight / live-row
+// / row-holder counts (one all-reduce; every rank then decides alike).
+int lane_globals(psim_handle* h) {
+    save_lane(h);
+    auto& l = h->lanes[h->cur_lane];
+    int64_t v[3] = {(int64_t)h->inflight, h->live_rows, h->ost_cnt};
+    if (h->sh.world > 1) {
+        std::string err;
+        const int rc = h->sh.xport->allreduce(v, 3, h->stream, &err);
+        if (rc) return fail(h, rc, "lane all-reduce: %s", err.c_str());
+    }
+    l.g_inflight = v[0];
+    l.g_live = v[1];
+    l.g_ost = v[2];
+    return PSIM_OK;
+}
+
+// Rounds of a sharded handle with several lanes or a window lane: each round
+// runs every lane with a root (round kernel, then its exchange), one
+// all-reduce of every lane's counters per round.
+int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+                      uint32_t* ran_out, psim_exchange_stats* xs) {
+    const int focus = h->cur_lane;
+    save_lane(h);
+    struct Refocus {
+        psim_handle* h;
+        int f;
+        ~Refocus() { load_lane(h, f); }
+    } refocus{h, focus};
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    constexpr int NK = 10;    // 5 kinds, delivered_new, senders, degree sum, live rows, row holders
+    uint32_t ran = 0;
+    auto quiet = [&]() {
+        for (const auto& l : h->lanes)
+            if (l.have_root && !lane_quiescent(h, l)) return false;
+        return true;
+    };
+    bool done = stop_q && quiet();
+    while (!done && ran < max_rounds) {
+        std::vector<int> act;
+        for (int j = 0; j < (int)h->lanes.size(); j++)
+            if (h->lanes[j].have_root) act.push_back(j);
+        const size_t A = act.size();
+        if (A == 0) break;
+        const uint32_t tick = ((h->round + 1) % L) == 0;
+        HIPCHK(h, hipMemsetAsync(h->stats, 0, A * kStatsRow * sizeof(unsigned long long), h->stream));
+        HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
+        for (size_t q = 0; q < A; q++) {
+            load_lane(h, act[q]);
+            unsigned long long* row = h->stats + q * kStatsRow;
+            int rc;
+            if (h->win) {
+                const WinArgs a = make_win_args(h, h->par, tick, row);
+                HIPCHK(h, hipMemsetAsync(a.nout, 0, 4, h->stream));
+                HIPCHK(h, launch_win_round(a, h->w_cnt, h->w_cur, h->w_bsum, h->stream));
+                h->par ^= 1u;
+                rc = win_exchange(h, xs);
+            } else {
+                HIPCHK(h, scrub_if_needed(h, h->round + 1));
+                PtArgs a = make_args(h, h->par, tick, row);
+                HIPCHK(h, launch_pt_round(a, h->stream));
+                if (h->sh.world > 1)
+                    HIPCHK(h, launch_pt_pack_dense(a, h->sh.rem, (uint32_t)h->sh.send_base[h->sh.world], h->sh.xsend,
+                                                   h->stream));
+                h->par ^= 1u;
+                rc = x_exchange(h, 0, xs);
+            }
+            if (rc) return rc;
+            save_lane(h);
+        }
+        HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, A * kStatsRow * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        h->round++;
+        h->kernel_ms_total += ms;
+        h->rounds_total++;
+        std::vector<int64_t> flat(A * NK);
+        unsigned long long loc[kNStat] = {0};
+        for (size_t q = 0; q < A; q++) {
+            unsigned long long r[kNStat];
+            reduce_row(h->h_stats + q * kStatsRow, r);
+            if (r[S_OVERFLOW])
+                return fail(h, PSIM_EOVERFLOW, "round %llu: overflow flags 0x%llx", (unsigned long long)h->round,
+                            r[S_OVERFLOW]);
+            auto& l = h->lanes[act[q]];
+            uint64_t lm = 0;
+            for (int t = 1; t <= 5; t++) lm += r[t];
+            l.ost_cnt += (int64_t)r[S_OST_DELTA];
+            l.live_rows += (int64_t)r[S_LIVE_DELTA];
+            if (!l.win) l.inflight = lm;
+            int64_t* f = flat.data() + q * NK;
+            for (int t = 1; t <= 5; t++) f[t - 1] = (int64_t)r[t];
+            f[5] = (int64_t)r[S_DELIV];
+            f[6] = (int64_t)r[S_SENDERS];
+            f[7] = (int64_t)r[S_DEGSUM];
+            f[8] = l.live_rows;
+            f[9] = l.ost_cnt;
+            for (int t = 0; t < kNStat; t++) loc[t] += r[t];
+        }
+        if (h->sh.world > 1) {
+            std::string err;
+            const int rc = h->sh.xport->allreduce(flat.data(), flat.size(), h->stream, &err);
+            if (rc) return fail(h, rc, "counter all-reduce: %s", err.c_str());
+        }
+        int64_t tot[NK] = {0};
+        for (size_t q = 0; q < A; q++) {
+            auto& l = h->lanes[act[q]];
+            const int64_t* f = flat.data() + q * NK;
+            l.g_inflight = f[0] + f[1] + f[2] + f[3] + f[4];
+            l.g_live = f[8];
+            l.g_ost = f[9];
+            for (int t = 0; t < NK; t++) tot[t] += f[t];
+        }
+        if (out && ran < cap) {
+            psim_round_stats& o = out[ran];
+            memset(&o, 0, sizeof o);
+            for (int t = 1; t <= 5; t++) o.sent[t] = (uint64_t)tot[t - 1];
+            o.delivered_new = (uint64_t)tot[5];
+            o.senders = (uint64_t)tot[6];
+            o.sender_degree_sum = (uint64_t)tot[7];
+            o.active = loc[S_ACTIVE];
+            o.outstanding_vertices = (uint64_t)tot[9];
+            uint64_t lm = 0;
+            for (int t = 1; t <= 5; t++) lm += loc[t];
+            o.algo_bytes = 16ull * h->n * A + 8ull * loc[S_SENDERS] + 4ull * loc[S_DEGSUM] + 32ull * lm;
+            o.kernel_ms = ms;
+        }
+        if (xs) {
+            xs->rounds++;
+            xs->kernel_ms += ms;
+        }
+        ran++;
+        if (stop_q && quiet()) done = true;
+    }
+    if (ran_out) *ran_out = ran;
+    return PSIM_OK;
+}
+
+int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+                     uint32_t* rounds_run, psim_exchange_stats* xs);
+
+int shard_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+                uint32_t* rounds_run, psim_exchange_stats* xs) {
     if (!h) return PSIM_EINVAL;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    HIPCHK(h, hipSetDevice(h->device));
     int rc = x_buffers(h);
     if (rc) return rc;
     if (xs) memset(xs, 0, sizeof *xs);
+    if (h->lanes.size() > 1 || h->win) return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
+    return shard_drive_fast(h, max_rounds, out, cap, stop_q, rounds_run, xs);
+}
+
+// One lane of static words: rounds pipelined 4 at a time (kernel -> pack ->
+// all-to-all-v -> ingest, stream-ordered), one sync + one all-reduce per chunk.
+int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+                     uint32_t* rounds_run, psim_exchange_stats* xs) {
+    int rc;
     constexpr uint32_t K = 4;                  // rounds between counter collections
-    constexpr int NK = 9;                      // 5 kinds, delivered_new, senders, degree sum, live rows
+    constexpr int NK = 10;                     // 5 kinds, delivered_new, senders, degree sum, live rows, row holders
     uint32_t ran = 0;
     bool done = false;
     while (!done && ran < max_rounds) {
@@ -1681,6 +1938,7 @@ int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, s
             f[6] = (int64_t)st[j].senders;
             f[7] = (int64_t)st[j].sender_degree_sum;
             f[8] = live[j];
+            f[9] = (int64_t)st[j].outstanding_vertices;
         }
         if (h->sh.world > 1) {
             std::string err;
@@ -1691,6 +1949,12 @@ int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, s
             const int64_t* f = flat.data() + size_t(j) * NK;
             int64_t msgs = 0;
             for (int t = 0; t < 5; t++) msgs += f[t];
+            if (!h->lanes.empty()) {
+                auto& l = h->lanes[h->cur_lane];
+                l.g_inflight = msgs;
+                l.g_live = f[8];
+                l.g_ost = f[9];
+            }
             if (out && ran < cap) {
                 psim_round_stats& o = out[ran];
                 const double kms = st[j].kernel_ms;
@@ -1700,12 +1964,12 @@ int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, s
                 o.senders = (uint64_t)f[6];
                 o.sender_degree_sum = (uint64_t)f[7];
                 o.active = st[j].active;                        // this rank's
-                o.outstanding_vertices = st[j].outstanding_vertices;
+                o.outstanding_vertices = (uint64_t)f[9];
                 o.algo_bytes = st[j].algo_bytes;                // this rank's (its kernel's bytes)
                 o.kernel_ms = kms;
             }
             ran++;
-            if (msgs == 0 && f[8] == 0) {                       // globally quiescent after this round
+            if (stop_q && msgs == 0 && f[8] == 0) {             // globally quiescent after this round
                 done = true;
                 const uint32_t extra = got - (j + 1);
                 if (extra) {
@@ -1720,8 +1984,44 @@ int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, s
     return PSIM_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out) {
+    if (!h) return PSIM_EINVAL;
+    int rc = x_buffers(h);
+    if (rc) return rc;
+    if (h->sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
+    unsigned long long r[kNStat];
+    rc = broadcast_common(h, root, mono_out, r);
+    if (rc) return rc;
+    if (h->win) {
+        rc = win_exchange(h, nullptr);
+    } else {
+        PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+        if (h->sh.world > 1)
+            HIPCHK(h, launch_pt_pack_dense(a, h->sh.rem, (uint32_t)h->sh.send_base[h->sh.world], h->sh.xsend,
+                                           h->stream));
+        rc = x_exchange(h, 0, nullptr);
+    }
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return lane_globals(h);
+}
+
+int psim_shard_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, uint32_t* rounds_run,
+                   psim_exchange_stats* xs) {
+    return shard_drive(h, max_rounds, out, cap, true, rounds_run, xs);
+}
+
+int psim_shard_step(psim_handle* h, uint32_t rounds, psim_round_stats* out, size_t cap, psim_exchange_stats* xs) {
+    return shard_drive(h, rounds, out, cap, false, nullptr, xs);
+}
+
 int psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records) {
     if (!h || (!recv_dev && n_records)) return PSIM_EINVAL;
+    if (int rc = one_lane_only(h)) return rc;
     if (n_records == 0) return PSIM_OK;
     if (n_records > 0xFFFFFFFFull) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));

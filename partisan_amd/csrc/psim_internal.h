@@ -357,6 +357,7 @@ struct PdRow { uint32_t peer, mono, round; };                   // {Peer, {Id, M
 struct PdMsg { uint32_t type, src, dst, seq, round, mono; };   // 24 B
 struct PdArgs {
     uint32_t n, mono, tick;
+    uint32_t v_lo;                            // bucketing: receiver dst - v_lo (a shard's window lane; C3: 0)
     const uint8_t* __restrict__ alive;        // SCAMP's (a stopped manager takes its node down)
     const uint32_t* __restrict__ pv;          // SCAMP partial views: the connections
     const ScHead* __restrict__ sch;
@@ -416,6 +417,13 @@ struct WinArgs {
 // bucket a.in by receiver (cnt, cur: [n], bsum: [ceil(n / kBlock)] scratch), then the round
 hipError_t launch_win_round(const WinArgs& a, uint32_t* cnt, uint32_t* cur, uint32_t* bsum, hipStream_t s);
 hipError_t launch_win_origin(const WinArgs& a, uint32_t root_local, hipStream_t s);
+// sharded window lanes: counts[r] += records whose receiver shard r owns ...
+constexpr uint32_t kWinMaxWorld = 64;
+hipError_t launch_win_split(const PdMsg* m, const uint32_t* nm, uint32_t cap, uint32_t n_global, uint32_t world,
+                            uint32_t* counts, hipStream_t s);
+// ... and the records, grouped by shard at base[r] (cursor[r] zeroed)
+hipError_t launch_win_scatter(const PdMsg* m, const uint32_t* nm, uint32_t cap, uint32_t n_global, uint32_t world,
+                              const uint32_t* base, uint32_t* cursor, PdMsg* out, hipStream_t s);
 // a static-engine lane becomes a window lane: rows from the outstanding
 // masks, the timestamp sets from the current delivery, the in-flight words
 // of `pa` (the words the next round reads) as records

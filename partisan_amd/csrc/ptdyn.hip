@@ -240,7 +240,7 @@ __device__ __forceinline__ uint32_t n_in(const PdArgs& a) { return *a.nin < a.ou
 __global__ __launch_bounds__(kBlock) void pd_count(PdArgs a) {
     const uint32_t k = n_in(a);
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock)
-        atomicAdd(&a.cnt[a.in[i].dst], 1u);
+        atomicAdd(&a.cnt[a.in[i].dst - a.v_lo], 1u);
 }
 __global__ __launch_bounds__(kBlock) void pd_scan_blocks(PdArgs a) {
     __shared__ uint32_t ws[kBlock / 64];
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void pd_scan_add(PdArgs a) {
 __global__ __launch_bounds__(kBlock) void pd_scatter(PdArgs a) {
     const uint32_t k = n_in(a);
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock) {
-        const uint32_t d = a.in[i].dst;
+        const uint32_t d = a.in[i].dst - a.v_lo;
         a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
     }
 }

@@ -402,6 +402,42 @@ __global__ __launch_bounds__(kBlock) void win_delivered_kernel(WinArgs a, uint32
     if (v < a.n) out[v] = is_member(is_load(a, v), mono) ? 1 : 0;
 }
 
+// Sharded window lanes: the records a round emitted are split by the shard
+// owning their receiver (contiguous ranges lo(r) = n r / W, psim_load_csr).
+__device__ __forceinline__ uint32_t owner(uint32_t v, uint32_t n, uint32_t W) {
+    uint32_t r = uint32_t((uint64_t(v) * W) / n);
+    while (r + 1 < W && uint32_t((uint64_t(n) * (r + 1)) / W) <= v) r++;
+    while (r > 0 && uint32_t((uint64_t(n) * r) / W) > v) r--;
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void win_split_count_kernel(const PdMsg* __restrict__ m, const uint32_t* nm,
+                                                                 uint32_t cap, uint32_t n, uint32_t W,
+                                                                 uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[kWinMaxWorld];
+    for (uint32_t i = threadIdx.x; i < W; i += kBlock) hist[i] = 0;
+    __syncthreads();
+    const uint32_t k = min(*nm, cap);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += gridDim.x * kBlock)
+        atomicAdd(&hist[owner(m[i].dst, n, W)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < W; i += kBlock)
+        if (hist[i]) atomicAdd(&counts[i], hist[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void win_split_scatter_kernel(const PdMsg* __restrict__ m, const uint32_t* nm,
+                                                                   uint32_t cap, uint32_t n, uint32_t W,
+                                                                   const uint32_t* __restrict__ base,
+                                                                   uint32_t* __restrict__ cursor,
+                                                                   PdMsg* __restrict__ out) {
+    const uint32_t k = min(*nm, cap);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += gridDim.x * kBlock) {
+        const PdMsg x = m[i];
+        const uint32_t r = owner(x.dst, n, W);
+        out[base[r] + atomicAdd(&cursor[r], 1u)] = x;
+    }
+}
+
 inline uint32_t blocks(uint32_t n) { return n ? (n + kBlock - 1) / kBlock : 1u; }
 
 }  // namespace
@@ -409,6 +445,7 @@ inline uint32_t blocks(uint32_t n) { return n ? (n + kBlock - 1) / kBlock : 1u; 
 hipError_t launch_win_round(const WinArgs& a, uint32_t* cnt, uint32_t* cur, uint32_t* bsum, hipStream_t s) {
     PdArgs b{};
     b.n = a.n;
+    b.v_lo = a.v_lo;
     b.in = a.in;
     b.nin = a.nin;
     b.out_cap = a.cap;
@@ -420,6 +457,20 @@ hipError_t launch_win_round(const WinArgs& a, uint32_t* cnt, uint32_t* cur, uint
     hipError_t e = launch_pd_bucket(b, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(win_round_kernel, dim3(blocks(a.n)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_win_split(const PdMsg* m, const uint32_t* nm, uint32_t cap, uint32_t n_global, uint32_t world,
+                            uint32_t* counts, hipStream_t s) {
+    if (world > kWinMaxWorld) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(win_split_count_kernel, dim3(256), dim3(kBlock), 0, s, m, nm, cap, n_global, world, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_win_scatter(const PdMsg* m, const uint32_t* nm, uint32_t cap, uint32_t n_global, uint32_t world,
+                              const uint32_t* base, uint32_t* cursor, PdMsg* out, hipStream_t s) {
+    hipLaunchKernelGGL(win_split_scatter_kernel, dim3(256), dim3(kBlock), 0, s, m, nm, cap, n_global, world, base,
+                       cursor, out);
     return hipGetLastError();
 }
 

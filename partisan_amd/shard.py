@@ -229,6 +229,15 @@ class ShardedPlumtree:
                 break
         return out, rounds
 
+    def step(self, rounds=1):
+        """Exactly `rounds` rounds (psim_shard_step, collective): GLOBAL per-round stats."""
+        if self.transport == "torch":
+            raise ValueError("step() needs the in-library exchange (transport 'rccl' or 'callback')")
+        st = (RoundStats * max(1, rounds))()
+        xs = ExchangeStats()
+        check(lib().psim_shard_step(self._h, rounds, st, rounds, C.byref(xs)), self._h)
+        return [s_.as_dict() for s_ in st[:rounds]]
+
     def _run_in_library(self, max_rounds, cap=4096):
         st = (RoundStats * cap)()
         ran = C.c_uint32()

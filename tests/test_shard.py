@@ -118,6 +118,86 @@ def test_sharded_matches_oracle(world, n, seed, L, transport):
         assert res[r] == "ok", res[r]
 
 
+def _lanes_check(sim, orc, monos, exact):
+    """This rank's vertices against the oracle, per root lane: delivered per
+    Monotonic, eager / lazy sets; rows and in-flight messages over all lanes
+    (in order when one root is in play: window lanes keep the emission order)."""
+    lo, nl = sim.v_lo, sim.n
+    rows = [[] for _ in range(nl)]
+    msgs = []
+    for root, ms in monos.items():
+        if not ms:
+            continue
+        sim.focus(root)
+        for m in ms:
+            assert np.array_equal(sim.delivered_mono(m), orc.delivered(root, m)[lo:lo + nl]), (root, m)
+        eager, lazy, _, _ = sim.plumtree_state()
+        for lv in range(nl):
+            oe, ol = orc.peers(lo + lv, root)
+            assert sim.mask_to_peers(lv, eager[lv]) == oe, (root, lo + lv)
+            assert sim.mask_to_peers(lv, lazy[lv]) == ol, (root, lo + lv)
+            rows[lv] += sim.rows(lv)
+        msgs += sim.messages()
+    want = [m for m in orc.pending_full() if lo <= m[1] < lo + nl]
+    for lv in range(nl):
+        o = orc.outstanding(lo + lv)
+        assert (rows[lv] == o) if exact else (sorted(rows[lv]) == sorted(o)), lo + lv
+    assert (msgs == want) if exact else (sorted(msgs) == sorted(want))
+
+
+def _lanes_worker(rank, world, port, n, seed, schedule, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        dist = _init(rank, world, port)
+        import partisan_amd as pa
+        from partisan_amd.shard import ShardedPlumtree
+        import pyoracle as O
+        rp, col = pa.overlay.random_regular(n, 5, seed)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", transport="callback")
+        orc = O.Plumtree(rp, col, 1)
+        roots = sorted({r for rs in schedule.values() for r in rs})
+        monos = {r: [] for r in roots}
+        for rnd in range(45):
+            for root in schedule.get(rnd, []):
+                m = sp.broadcast(root)
+                assert m == orc.heartbeat(root), (rnd, root)
+                monos[root].append(m)
+            g, o = sp.step(1)[0], orc.step(1)[0]
+            for k in KINDS:
+                assert g[k] == o[k], (rnd, k, g, o)
+            assert g["delivered_new"] == o["delivered_new"], rnd
+            _lanes_check(sp.sim, orc, monos, exact=len(roots) == 1)
+        for root, ms in monos.items():
+            sp.sim.focus(root)
+            for m in ms:
+                assert sp.sim.delivered_mono(m).all(), (root, m)
+        st, r = sp.run(200)
+        assert r == 0 or all(sum(x[k] for k in KINDS) == 0 for x in st)
+        sp.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,seed,multi", [(2, 600, 41, False), (3, 900, 42, False), (2, 700, 43, True)])
+def test_sharded_overlapping_and_multi_root_lockstep(world, n, seed, multi):
+    """SURVEY 8(f) row 1 on the sharded engine (in-library exchange, gloo
+    callbacks): one root heartbeating every 3 rounds during its own flood
+    (a window lane on every shard, its records routed to the owning shard),
+    and -- multi -- two roots interleaved (two lanes).  Round by round the
+    global counters, and each shard's vertices, equal the oracle's."""
+    sched = {0: [7], 3: [7], 6: [7], 9: [7], 12: [7]}
+    if multi:
+        sched = {0: [7], 1: [n // 2], 3: [7], 4: [n // 2], 6: [7], 9: [7]}
+    res = run_world(_lanes_worker, world, n, seed, sched)
+    for r in range(world):
+        assert res[r] == "ok", res[r]
+
+
 # ------------------------------------------------------------------ CPU gloo
 def _cpu_worker(rank, world, port, q):
     try:
