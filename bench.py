@@ -247,11 +247,13 @@ def main():
     achieved_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
 
     if rank == 0:
+        # ELL rows (one GPU, every degree <= 8) run the sweep kernel
+        kernel = "pt_round_kernel" if (sharded or args.csr or sim.max_degree() > 8) else "pt_round_ell_kernel"
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("n") == args.n and tj.get("peers") == args.peers:
+            if tj.get("n") == args.n and tj.get("peers") == args.peers and tj.get("kernel") == kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -289,7 +291,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "pt_round_kernel",
+                "kernel": kernel,
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "algo_bytes_per_launch": algo_bytes / max(1, counted),
             },

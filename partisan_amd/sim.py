@@ -121,6 +121,11 @@ class Simulator:
         self._c(lib().psim_get_delivered(self._h, _u8p(out), self.n))
         return out
 
+    def max_degree(self):
+        """Widest peer row of this handle's vertices (rows of <= 8 slots load as ELL rows)."""
+        d = np.diff(np.asarray(self.slot_row_ptr, dtype=np.int64))
+        return int(d.max()) if len(d) else 0
+
     def delivered_mono(self, mono):
         """Mod:is_stale({root, epoch, mono}) per vertex (psim_get_delivered_mono)."""
         out = np.zeros(self.n, np.uint8)

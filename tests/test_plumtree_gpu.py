@@ -775,3 +775,32 @@ def test_window_lane_with_faults_and_dead_peers(psim):
     for _ in range(30):
         _win_step(sim, orc, root, monos)
     assert sim.delivered_mono(m).all()
+
+
+def _tree_csr(arity, n, cycles):
+    """partisan_plumtree_util:build_tree/3 (the KAT-pinned oracle
+    restatement) as a membership CSR: node k's members = its children
+    (self dropped); the loader symmetrises them into peer slots."""
+    t = dict((k, [c for c in ch if c != k]) for k, ch in O.build_tree(arity, list(range(n)), cycles))
+    rows = [sorted(set(t.get(v, []))) for v in range(n)]
+    rp = np.zeros(n + 1, np.uint64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    return rp, np.asarray([u for r in rows for u in r], np.uint32)
+
+
+@pytest.mark.parametrize("arity,n,cycles", [(1, 8, False), (2, 8, True), (3, 40, False), (2, 300, True),
+                                             (3, 2000, True), (1, 64, True)])
+def test_build_tree_overlays_lockstep(psim, arity, n, cycles):
+    """SURVEY 8(a) build_tree row: the trees partisan_plumtree_util builds
+    (arity 1-3, with and without cycles) as overlays -- paths, rings, k-ary
+    trees, their cyclic closures -- flooded and re-flooded in lockstep with
+    the oracle; a tree without cycles has no lazy link, so its second
+    heartbeat sends no i_have."""
+    rp, col = _tree_csr(arity, n, cycles)
+    sim, orc = make(psim, rp, col, 1)
+    for hb in range(3):
+        m = sim.broadcast(0)
+        assert m == orc.heartbeat(0)
+        compare(sim, orc, 0, m)
+        lockstep(sim, orc, 0, m)
+        assert sim.delivered().all()

@@ -1,4 +1,4 @@
-"""Per-launch HBM traffic of pt_round_kernel from rocprofv3 PMC passes.
+"""Per-launch HBM traffic of the Plumtree round kernel from rocprofv3 PMC passes.
 
 Collected as MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7 prescribe:
 two separate --pmc passes (FETCH_SIZE, WRITE_SIZE; they do not fit one
@@ -16,11 +16,11 @@ import json
 import os
 
 
-def load(d, counter):
+def load(d, counter, kernel):
     path = os.path.join(d, "run_counter_collection.csv")
-    rows = [r for r in csv.DictReader(open(path)) if "pt_round_kernel" in r["Kernel_Name"]
-            and r["Counter_Name"] == counter]
-    return [float(r["Counter_Value"]) * 1024.0 for r in rows]
+    rows = [r for r in csv.DictReader(open(path))
+            if ("::" + kernel + "<") in r["Kernel_Name"] or ("::" + kernel + "(") in r["Kernel_Name"]]
+    return [float(r["Counter_Value"]) * 1024.0 for r in rows if r["Counter_Name"] == counter]
 
 
 def main():
@@ -31,21 +31,23 @@ def main():
     p.add_argument("--peers", type=int, required=True)
     p.add_argument("--rounds-per-step", type=int, required=True)
     p.add_argument("--steps", type=int, required=True, help="steps incl. warmup in the profiled run")
+    p.add_argument("--kernel", default="pt_round_ell_kernel",
+                   help="the round kernel bench.py runs (ELL rows: pt_round_ell_kernel; CSR: pt_round_kernel)")
     p.add_argument("--out", default=None)
     a = p.parse_args()
-    f = load(a.fetch_dir, "FETCH_SIZE")
-    w = load(a.write_dir, "WRITE_SIZE")
+    f = load(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    w = load(a.write_dir, "WRITE_SIZE", a.kernel)
     counted = a.rounds_per_step * a.steps
     fetch = sum(f) / counted
     write = sum(w) / counted
     out = {
-        "n": a.n, "peers": a.peers, "kernel": "pt_round_kernel",
+        "n": a.n, "peers": a.peers, "kernel": a.kernel,
         "launches_profiled": len(f), "counted_launches": counted,
         "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
         "hbm_bytes_per_launch_read_doubled": 2 * fetch + write,
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB*1024, "
-                  "summed over all pt_round_kernel launches / counted rounds",
+                  "summed over all launches of the kernel / counted rounds",
     }
     print(json.dumps(out, indent=1))
     if a.out:
