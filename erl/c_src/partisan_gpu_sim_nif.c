@@ -1063,6 +1063,94 @@ static ERL_NIF_TERM nif_shard_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     return enif_make_tuple_from_array(env, out, 4);
 }
 
+/* delivered_mono(Sim, Mono) -> {ok, Bin}: Mod:is_stale({Root, Epoch, Mono}) per
+ * vertex of the focused root (psim_get_delivered_mono) */
+static ERL_NIF_TERM nif_delivered_mono(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned mono;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &mono)) return enif_make_badarg(env);
+    ERL_NIF_TERM t;
+    unsigned char* d = enif_make_new_binary(env, r->n, &t);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_delivered_mono(r->h, mono, d, r->n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), t);
+}
+
+/* rows(Sim, V) -> {ok, [{Peer, Round, Mono}]}: v's outstanding i_have rows in
+ * insertion order (psim_get_rows) */
+static ERL_NIF_TERM nif_rows(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned v;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &v) || v >= r->n) return enif_make_badarg(env);
+    enum { CAP = 64 };
+    uint32_t p[CAP], rd[CAP], m[CAP];
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_rows(r->h, v, p, rd, m, CAP, &k);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (size_t i = k < CAP ? k : CAP; i > 0; i--)
+        list = enif_make_list_cell(env, enif_make_tuple3(env, enif_make_uint(env, p[i - 1]), enif_make_uint(env, rd[i - 1]),
+                                                         enif_make_uint(env, m[i - 1])), list);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* messages(Sim) -> {ok, [{Src, Dst, Kind, Round, Mono}]}: the next round's
+ * messages in handling order (psim_get_messages) */
+static ERL_NIF_TERM nif_messages(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_messages(r->h, NULL, NULL, NULL, NULL, NULL, 0, &k);
+    uint32_t* a = NULL;
+    if (rc == PSIM_OK && k) {
+        a = (uint32_t*)enif_alloc(k * 5 * sizeof(uint32_t));
+        if (!a) rc = PSIM_ENOMEM;
+        else rc = psim_get_messages(r->h, a, a + k, a + 2 * k, a + 3 * k, a + 4 * k, k, &k);
+    }
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { if (a) enif_free(a); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (size_t i = k; i > 0; i--) {
+        ERL_NIF_TERM e[5];
+        for (int j = 0; j < 5; j++) e[j] = enif_make_uint(env, a[j * k + i - 1]);
+        list = enif_make_list_cell(env, enif_make_tuple_from_array(env, e, 5), list);
+    }
+    if (a) enif_free(a);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* shard_step(Sim, Rounds) -> {ok, [Stats], {FabricBytes, ExchangeUs, KernelUs}}:
+ * exactly Rounds collective rounds (psim_shard_step) */
+static ERL_NIF_TERM nif_shard_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned rounds;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &rounds) || rounds > 4096)
+        return enif_make_badarg(env);
+    psim_round_stats* st = (psim_round_stats*)enif_alloc((rounds ? rounds : 1) * sizeof(psim_round_stats));
+    if (!st) return err(env, PSIM_ENOMEM);
+    psim_exchange_stats xs;
+    enif_mutex_lock(r->mu);
+    int rc = psim_shard_step(r->h, rounds, st, rounds, &xs);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (unsigned i = rounds; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    ERL_NIF_TERM x = enif_make_tuple3(env, enif_make_uint64(env, xs.fabric_bytes),
+                                      enif_make_uint64(env, (uint64_t)(xs.exchange_ms * 1000.0)),
+                                      enif_make_uint64(env, (uint64_t)(xs.kernel_ms * 1000.0)));
+    return enif_make_tuple3(env, mk_atom(env, "ok"), list, x);
+}
+
 static ErlNifFunc funcs[] = {
     {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -1078,6 +1166,10 @@ static ErlNifFunc funcs[] = {
     {"focus", 2, nif_focus, 0},
     {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_delays", 4, nif_set_delays, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"delivered_mono", 2, nif_delivered_mono, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"rows", 2, nif_rows, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"messages", 1, nif_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"shard_step", 2, nif_shard_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"relay_run", 10, nif_relay_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_setup", 3, nif_hv_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"hv_join", 3, nif_hv_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},

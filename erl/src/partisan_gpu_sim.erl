@@ -7,7 +7,8 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
-         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, relay_run/10,
+         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, rows/2, messages/1, shard_step/2,
+         relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
          vclock/4,
@@ -74,6 +75,23 @@ set_omissions(_Sim, _Src, _Dst) -> erlang:nif_error(nif_not_loaded).
 %% u32 binaries, Rounds one byte per pair; refused while messages are in flight.
 -spec set_delays(sim(), binary(), binary(), binary()) -> ok | error().
 set_delays(_Sim, _Src, _Dst, _Rounds) -> erlang:nif_error(nif_not_loaded).
+
+%% Mod:is_stale({Root, Epoch, Mono}) per vertex of the focused root, any
+%% heartbeat of a window lane (psim_get_delivered_mono).
+-spec delivered_mono(sim(), non_neg_integer()) -> {ok, binary()} | error().
+delivered_mono(_Sim, _Mono) -> erlang:nif_error(nif_not_loaded).
+
+%% Vertex V's outstanding i_have rows {Peer, Round, Mono} in insertion order.
+-spec rows(sim(), non_neg_integer()) -> {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer()}]} | error().
+rows(_Sim, _V) -> erlang:nif_error(nif_not_loaded).
+
+%% The next round's messages {Src, Dst, Kind, Round, Mono} in handling order.
+-spec messages(sim()) -> {ok, [tuple()]} | error().
+messages(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% Exactly Rounds collective rounds of a sharded handle (psim_shard_step).
+-spec shard_step(sim(), non_neg_integer()) -> {ok, [map()], tuple()} | error().
+shard_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 
 %% Transitive relay (psim_relay_run): forward_message(Node, Message,
 %% #{transitive => true}) for a batch of sends over active views (ActPtr u64 /

@@ -122,6 +122,17 @@ int main(int argc, char** argv) {
                (unsigned long long)got, (unsigned long long)bsum, (unsigned long long)mock_int(mock_elem(th, 0)),
                (unsigned long long)mock_int(mock_elem(th, 1)), (unsigned long long)mock_int(mock_elem(th, 2)),
                (unsigned long long)mock_int(mock_elem(th, 3)));
+        {   /* window-lane-era getters on the static lane: every vertex delivered this Monotonic, nothing in flight */
+            ERL_NIF_TERM dm = want_ok_tuple("delivered_mono", call("delivered_mono", 2, A(sim, mock_elem(bc, 1))));
+            size_t dmz;
+            const unsigned char* dmb = mock_bin_data(mock_elem(dm, 1), &dmz);
+            uint64_t dmsum = 0;
+            for (size_t i = 0; i < dmz; i++) dmsum += dmb[i];
+            ERL_NIF_TERM ms = want_ok_tuple("messages", call("messages", 1, A(sim)));
+            ERL_NIF_TERM rw = want_ok_tuple("rows", call("rows", 2, A(sim, mock_uint(0))));
+            fprintf(g_out, ", \"c2_getters\": {\"delivered_mono\": %llu, \"messages\": %zu, \"rows0\": %zu}",
+                    (unsigned long long)dmsum, mock_list_len(mock_elem(ms, 1)), mock_list_len(mock_elem(rw, 1)));
+        }
         /* the same overlay, vertex-sharded at world 1 with the library's own RCCL communicator */
         ERL_NIF_TERM sim7 = new_sim(0x5EED0002ull);
         ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);
@@ -133,8 +144,9 @@ int main(int argc, char** argv) {
         d = mock_bin_data(mock_elem(dl7, 1), &dsz);
         uint64_t got7 = 0;
         for (size_t i = 0; i < dsz; i++) got7 += d[i];
-        fprintf(g_out, ", \"shard_rccl_world1\": {\"rounds\": %llu, \"delivered\": %llu}",
-               (unsigned long long)mock_int(mock_elem(sr, 1)), (unsigned long long)got7);
+        ERL_NIF_TERM ss = want_ok_tuple("shard_step", call("shard_step", 2, A(sim7, mock_uint(2))));
+        fprintf(g_out, ", \"shard_rccl_world1\": {\"rounds\": %llu, \"delivered\": %llu, \"step2\": %zu}",
+               (unsigned long long)mock_int(mock_elem(sr, 1)), (unsigned long long)got7, mock_list_len(mock_elem(ss, 1)));
         free(rp);
         free(col);
     }
