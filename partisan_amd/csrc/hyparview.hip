@@ -25,54 +25,86 @@ enum { HV_JOIN = 1, HV_NEIGHBOR, HV_FORWARD_JOIN, HV_DISCONNECT, HV_NEIGHBOR_REQ
 
 __device__ __forceinline__ bool alive_of(const HvArgs& a, uint32_t v) { return (a.alive[v >> 5] >> (v & 31)) & 1u; }
 
-// ---------------------------------------------------------------- context
-struct Ctx {
+// ---------------------------------------------------------------- one wave per vertex
+// A vertex is handled by a whole wavefront.  Every control decision is
+// wave-uniform (the same on all 64 lanes: message fields, view sizes, draws),
+// so the clauses run without divergence; the lanes hold the views -- lane i
+// the i-th active (i < 8) and passive (i < 32) id, in `sets` order -- and the
+// set operations of the reference (ordsets add / del / member, pick_random's
+// filter, the exchange list's usort) are ballots, popcounts and shuffles.
+// Nothing is indexed at run time from a private array, so nothing spills.
+struct W {
     const HvArgs* a;
     uint32_t v;
-    uint32_t act[8], na;
-    uint32_t pas[32], np;
-    uint32_t nsent, nrecv;
-    uint32_t seq;
+    uint32_t A, P;                 // this lane's active / passive view element
+    uint32_t na, np;
+    uint32_t nsent, nrecv, seq;
     uint64_t draws;
-    uint32_t sent_cnt[10];
+    uint64_t k0, k1, k2;           // messages sent by kind: 16-bit fields, kinds 1-3 / 4-7 / 8-9 (no indexed array)
     uint32_t ndraw, err;
 };
+__device__ __forceinline__ void count_kind(W& c, uint32_t t) {
+    const uint64_t inc = 1ull << (16 * (t & 3));
+    if (t < 4) c.k0 += inc; else if (t < 8) c.k1 += inc; else c.k2 += inc;
+}
+__device__ __forceinline__ uint32_t kind_count(uint64_t k0, uint64_t k1, uint64_t k2, uint32_t t) {
+    const uint64_t w = t < 4 ? k0 : (t < 8 ? k1 : k2);
+    return (uint32_t)((w >> (16 * (t & 3))) & 0xFFFFull);
+}
 
-__device__ uint64_t draw64(Ctx& c) {
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// index of the k-th (0-based) set bit of m (m has > k set bits)
+__device__ __forceinline__ uint32_t kth_bit(uint64_t m, uint32_t k) {
+    uint32_t lo = 0, hi = 64;                         // smallest i with popc(m & ((2 << i) - 1)) > k
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint32_t)__popcll(m & ((1ull << mid) - 1ull)) > k) hi = mid; else lo = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t draw64(W& c) {
     const uint4 r = philox4x32_10(make_uint4(c.v, (uint32_t)c.draws, KIND_HV, (uint32_t)(c.draws >> 32)), c.a->key);
     c.draws++;
     c.ndraw++;
     return (uint64_t)r.x | ((uint64_t)r.y << 32);
 }
-__device__ __forceinline__ uint32_t uniform(Ctx& c, uint32_t n) {   // rand:uniform(N), N >= 1
+__device__ __forceinline__ uint32_t uniform(W& c, uint32_t n) {   // rand:uniform(N), N >= 1
     return 1u + (uint32_t)__umul64hi(draw64(c), (uint64_t)n);
 }
 
-__device__ __forceinline__ bool has(const uint32_t* s, uint32_t n, uint32_t x) {
-    for (uint32_t i = 0; i < n; i++)
-        if (s[i] == x) return true;
-    return false;
-}
-__device__ __forceinline__ void sadd(uint32_t* s, uint32_t& n, uint32_t x) {
-    if (has(s, n, x)) return;
-    uint32_t i = n;
-    while (i > 0 && s[i - 1] > x) { s[i] = s[i - 1]; i--; }
-    s[i] = x;
+// ordsets over a lane-distributed sorted list (x = this lane's element, n valid)
+__device__ __forceinline__ bool l_has(uint32_t x, uint32_t n, uint32_t q) { return ballot(lane_id() < n && x == q) != 0; }
+__device__ __forceinline__ void l_add(uint32_t& x, uint32_t& n, uint32_t q) {
+    if (l_has(x, n, q)) return;
+    const uint32_t l = lane_id();
+    const uint32_t pos = (uint32_t)__popcll(ballot(l < n && x < q));
+    const uint32_t prev = __shfl(x, l ? l - 1 : 0, 64);
+    if (l > pos && l <= n) x = prev;
+    else if (l == pos) x = q;
     n++;
 }
-__device__ __forceinline__ void sdel(uint32_t* s, uint32_t& n, uint32_t x) {
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < n; i++)
-        if (s[i] != x) s[k++] = s[i];
+__device__ __forceinline__ void l_del(uint32_t& x, uint32_t& n, uint32_t q) {
+    const uint32_t l = lane_id();
+    const uint64_t keep = ballot(l < n && x != q);
+    const uint32_t k = (uint32_t)__popcll(keep);
+    const uint32_t src = l < k ? kth_bit(keep, l) : l;
+    const uint32_t y = __shfl(x, src, 64);
+    x = l < k ? y : 0xFFFFFFFFu;
     n = k;
 }
+// the element at position i (uniform i < n)
+__device__ __forceinline__ uint32_t l_at(uint32_t x, uint32_t i) { return uni(__shfl(x, i, 64)); }
 
 // id maps (sent_message_map / recv_message_map, unbounded maps in the
 // reference): one global open-addressing table per map, key (v << 32 | peer),
 // value {epoch, cnt}.  Only vertex v inserts or reads keys of v, so a key is
 // never raced; distinct vertices share probe chains through atomicCAS on the
 // empty key.  Nothing is ever deleted, so a find that meets an empty slot is
-// a definite miss.
+// a definite miss.  The wave probes 64 consecutive slots per load.
 constexpr unsigned long long kEmpty = ~0ull;
 constexpr uint32_t kProbeMax = 256;
 struct IdMap { unsigned long long* key; uint2* val; uint32_t mask; };
@@ -80,108 +112,197 @@ __device__ __forceinline__ uint32_t hslot(unsigned long long k, uint32_t mask) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
     return (uint32_t)k & mask;
 }
-__device__ bool mget(const IdMap& m, uint32_t v, uint32_t p, uint2& out) {
+// Map words are read at device scope (past this CU's L1): a key or value may
+// have been written by another lane of this wave (its lane 0) or claimed by
+// another wave since this CU last cached the line.
+__device__ __forceinline__ unsigned long long key_at(const IdMap& m, uint32_t i) {
+    return __hip_atomic_load(&m.key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint2 val_at(const IdMap& m, uint32_t i) {
+    const unsigned long long x =
+        __hip_atomic_load(reinterpret_cast<unsigned long long*>(&m.val[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2((uint32_t)x, (uint32_t)(x >> 32));
+}
+__device__ __forceinline__ bool mget(const IdMap& m, uint32_t v, uint32_t p, uint2& out) {
     const unsigned long long k = ((unsigned long long)v << 32) | p;
-    uint32_t i = hslot(k, m.mask);
-    for (uint32_t t = 0; t < kProbeMax; t++, i = (i + 1) & m.mask) {
-        const unsigned long long x = m.key[i];
-        if (x == k) { out = m.val[i]; return true; }
-        if (x == kEmpty) return false;
+    const uint32_t h = hslot(k, m.mask);
+    for (uint32_t t = 0; t < kProbeMax; t += 64) {
+        const uint32_t i = (h + t + lane_id()) & m.mask;
+        const unsigned long long x = key_at(m, i);
+        const uint64_t hit = ballot(x == k), emp = ballot(x == kEmpty);
+        const uint64_t any = hit | emp;
+        if (any) {
+            const uint32_t f = (uint32_t)__ffsll((long long)any) - 1;
+            if (!((hit >> f) & 1ull)) return false;
+            const uint2 val = val_at(m, (h + t + f) & m.mask);
+            out = make_uint2(uni(val.x), uni(val.y));
+            return true;
+        }
     }
     return false;
 }
-__device__ void mput(Ctx& c, const IdMap& m, uint32_t& n, uint32_t p, uint32_t e, uint32_t cnt) {
+__device__ __forceinline__ void mput(W& c, const IdMap& m, uint32_t& n, uint32_t p, uint32_t e, uint32_t cnt) {
     const unsigned long long k = ((unsigned long long)c.v << 32) | p;
-    uint32_t i = hslot(k, m.mask);
-    for (uint32_t t = 0; t < kProbeMax; t++, i = (i + 1) & m.mask) {
-        unsigned long long x = m.key[i];
-        if (x == kEmpty) {
-            x = atomicCAS(&m.key[i], kEmpty, k);
-            if (x == kEmpty) { n++; x = k; }
+    const uint32_t h = hslot(k, m.mask);
+    uint32_t t = 0;
+    while (t < kProbeMax) {
+        const uint32_t i = (h + t + lane_id()) & m.mask;
+        const unsigned long long x = (t + lane_id() < kProbeMax) ? key_at(m, i) : 0ull;
+        const uint64_t cand = ballot(t + lane_id() < kProbeMax && (x == k || x == kEmpty));
+        if (!cand) { t += 64; continue; }
+        const uint32_t f = (uint32_t)__ffsll((long long)cand) - 1;
+        const uint32_t slot = (h + t + f) & m.mask;
+        bool mine = true;
+        if (uni((uint32_t)(__shfl((uint32_t)(x == kEmpty), f, 64)))) {   // empty: claim it
+            unsigned long long old = 0;
+            if (lane_id() == 0) old = atomicCAS(&m.key[slot], kEmpty, k);
+            const uint32_t lo = uni((uint32_t)old), hi = uni((uint32_t)(old >> 32));
+            old = ((unsigned long long)hi << 32) | lo;
+            if (old == kEmpty) n++;
+            else mine = old == k;                       // another vertex took it: probe on
         }
-        if (x == k) { m.val[i] = make_uint2(e, cnt); return; }
+        if (mine) {
+            if (lane_id() == 0)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(&m.val[slot]),
+                                   (unsigned long long)e | ((unsigned long long)cnt << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        t += f + 1;
     }
     c.err |= 2u;
 }
-__device__ __forceinline__ IdMap sent_map(const Ctx& c) { return IdMap{c.a->skey, c.a->sval, c.a->map_mask}; }
-__device__ __forceinline__ IdMap recv_map(const Ctx& c) { return IdMap{c.a->rkey, c.a->rval, c.a->map_mask}; }
+__device__ __forceinline__ IdMap sent_map(const W& c) { return IdMap{c.a->skey, c.a->sval, c.a->map_mask}; }
+__device__ __forceinline__ IdMap recv_map(const W& c) { return IdMap{c.a->rkey, c.a->rval, c.a->map_mask}; }
 
-__device__ HvMsg* emit(Ctx& c, uint32_t dst, uint32_t type) {
-    const uint32_t pos = atomicAdd(c.a->nout, 1u);
-    c.sent_cnt[type]++;
-    if (pos >= c.a->out_cap) { c.err |= 1u; return nullptr; }
-    HvMsg* m = &c.a->out[pos];
-    m->type = type;
-    m->src = c.v;
-    m->dst = dst;
-    m->seq = c.seq++;
-    m->peer = 0; m->epoch = 0; m->ttl = 0; m->prio = 0; m->did_e = 0; m->did_c = 0; m->nx = 0;
-    return m;
+// A message under construction: uniform header fields plus the exchange list
+// held one element per lane (x, nx).
+struct Out {
+    uint32_t type, ttl, prio, nx, peer, epoch, did_e, did_c;
+    uint32_t x;
+};
+__device__ __forceinline__ Out out_msg(uint32_t type) {
+    Out o;
+    o.type = type; o.ttl = 0; o.prio = 0; o.nx = 0; o.peer = 0; o.epoch = 0; o.did_e = 0; o.did_c = 0; o.x = 0;
+    return o;
+}
+// emission: one reservation per message (lane 0), the 64-byte record written
+// by lanes 0..15 (one dword each, one transaction)
+__device__ __forceinline__ void emit(W& c, uint32_t dst, const Out& o) {
+    if (dst >= c.a->n) { c.err |= 16u; return; }
+    count_kind(c, o.type);
+    const uint32_t seq = c.seq++;
+    uint32_t pos = 0;
+    if (lane_id() == 0) pos = atomicAdd(c.a->nout, 1u);
+    pos = uni(pos);
+    if (pos >= c.a->out_cap) { c.err |= 1u; return; }
+    const uint32_t l = lane_id();
+    uint32_t w = 0;
+    switch (l) {
+    case 0: w = o.type | (o.ttl << 8) | (o.prio << 16) | (o.nx << 24); break;
+    case 1: w = c.v; break;
+    case 2: w = dst; break;
+    case 3: w = seq; break;
+    case 4: w = o.peer; break;
+    case 5: w = o.epoch; break;
+    case 6: w = o.did_e; break;
+    case 7: w = o.did_c; break;
+    default: break;
+    }
+    const uint32_t xv = __shfl(o.x, (l - 8) & 63, 64);
+    if (l >= 8 && l < 16) w = (l - 8 < o.nx) ? xv : 0u;
+    if (l < 16) reinterpret_cast<uint32_t*>(c.a->out + pos)[l] = w;
 }
 
-// pick_random(View, Omit) (:2291-2301); returns false = undefined (no draw, Q13)
-__device__ bool pick_random(Ctx& c, const uint32_t* view, uint32_t nv, const uint32_t* om, uint32_t no, uint32_t& out) {
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < nv; i++)
-        if (!has(om, no, view[i])) k++;
+__device__ __forceinline__ bool alive_w(W& c, uint32_t p) {
+    if (p >= c.a->n) { c.err |= 16u; return false; }      // not a vertex id: reported, never dereferenced
+    return alive_of(*c.a, p);
+}
+
+// pick_random(View, Omit) (:2291-2301) over a lane-distributed view; false =
+// undefined (no draw, Q13)
+__device__ __forceinline__ bool pick_random(W& c, uint32_t view, uint32_t nv, uint32_t o0, uint32_t o1, uint32_t o2,
+                                            uint32_t& out) {
+    const uint64_t ok = ballot(lane_id() < nv && view != o0 && view != o1 && view != o2);
+    const uint32_t k = (uint32_t)__popcll(ok);
     if (k == 0) return false;
-    uint32_t idx = uniform(c, k) - 1;
-    for (uint32_t i = 0; i < nv; i++)
-        if (!has(om, no, view[i])) {
-            if (idx == 0) { out = view[i]; return true; }
-            idx--;
-        }
-    return false;
+    const uint32_t idx = uniform(c, k) - 1;
+    out = l_at(view, kth_bit(ok, idx));
+    return true;
 }
 
-// select_peers_for_exchange/1 (:2324-2333); shuffle/2 draws one float per element (Q8)
-__device__ uint32_t select_exchange(Ctx& c, uint32_t* out) {
+// select_peers_for_exchange/1 (:2324-2333): shuffle/2 draws one float per
+// element (Q8); the list is usort([Myself | k_active of Active ++ k_passive of
+// Passive]), returned lane-distributed
+__device__ __forceinline__ uint32_t select_exchange(W& c, uint32_t& ex) {
     for (uint32_t i = 0; i < c.na + c.np; i++) (void)draw64(c);
-    uint32_t n = 0;
-    sadd(out, n, c.v);
-    for (uint32_t i = 0; i < c.na && i < c.a->cfg.shuffle_k_active; i++) sadd(out, n, c.act[i]);
-    for (uint32_t i = 0; i < c.np && i < c.a->cfg.shuffle_k_passive; i++) sadd(out, n, c.pas[i]);
+    const uint32_t l = lane_id();
+    const uint32_t ka = min(c.na, c.a->cfg.shuffle_k_active), kp = min(c.np, c.a->cfg.shuffle_k_passive);
+    const uint32_t av = __shfl(c.A, (l - 1) & 63, 64), pv = __shfl(c.P, (l - 1 - ka) & 63, 64);
+    const uint32_t cand = l == 0 ? c.v : (l <= ka ? av : pv);
+    const uint32_t nc = 1 + ka + kp;
+    const bool valid = l < nc;
+    // keep the first occurrence of each id; rank = number of kept ids below it
+    // (every shuffle runs with all lanes active: a lane that is switched off
+    // in a branch cannot be read)
+    bool keep = valid;
+    for (uint32_t j = 0; j < nc; j++) {
+        const uint32_t y = __shfl(cand, j, 64);
+        if (j < l && y == cand) keep = false;
+    }
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < nc; j++) {
+        const uint32_t y = __shfl(cand, j, 64), kj = __shfl((uint32_t)keep, j, 64);
+        rank += (kj && y < cand) ? 1u : 0u;
+    }
+    const uint64_t km = ballot(keep && valid);
+    const uint32_t n = (uint32_t)__popcll(km);
+    // lane t takes the kept candidate of rank t
+    uint32_t got = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < nc; j++) {
+        const uint32_t rj = __shfl(rank, j, 64), cj = __shfl(cand, j, 64);
+        if (((km >> j) & 1ull) && rj == l) got = cj;
+    }
+    ex = got;
     return n;
 }
 
-__device__ void get_current_id(Ctx& c, uint32_t p, uint32_t& e, uint32_t& cnt) {   // :2618-2627
+__device__ __forceinline__ void get_current_id(W& c, uint32_t p, uint32_t& e, uint32_t& cnt) {   // :2618-2627
     uint2 r;
     if (mget(recv_map(c), c.v, p, r)) { e = r.x; cnt = r.y; }
     else { e = 1; cnt = 0; }
 }
-__device__ bool is_addable_did(Ctx& c, uint32_t ie, uint32_t ic, uint32_t p) {       // :2652-2665
+__device__ __forceinline__ bool is_addable_did(W& c, uint32_t ie, uint32_t ic, uint32_t p) {       // :2652-2665
     uint2 r;
     if (!mget(sent_map(c), c.v, p, r)) return true;
     if (ie > r.x) return true;
     if (ie == r.x) return ic >= r.y;
     return false;
 }
-__device__ bool is_addable_epoch(Ctx& c, uint32_t pe, uint32_t p) {                  // :2667-2674
+__device__ __forceinline__ bool is_addable_epoch(W& c, uint32_t pe, uint32_t p) {                  // :2667-2674
     uint2 r;
     return !mget(sent_map(c), c.v, p, r) || pe >= r.x;
 }
-__device__ bool is_valid_disconnect(Ctx& c, uint32_t ie, uint32_t ic, uint32_t p) {  // :2639-2650
+__device__ __forceinline__ bool is_valid_disconnect(W& c, uint32_t ie, uint32_t ic, uint32_t p) {  // :2639-2650
     uint2 r;
     if (!mget(recv_map(c), c.v, p, r)) return true;
     if (ie > r.x) return true;
     return ic > r.y;
 }
 
-__device__ void add_to_passive(Ctx& c, uint32_t p) {                                 // :2418-2449
-    if (p == c.v || has(c.act, c.na, p) || has(c.pas, c.np, p)) return;
+__device__ __forceinline__ void add_to_passive(W& c, uint32_t p) {                                 // :2418-2449
+    if (p == c.v || l_has(c.A, c.na, p) || l_has(c.P, c.np, p)) return;
     if (c.np >= c.a->cfg.passive_max_size) {
         uint32_t r;
-        const uint32_t om[1] = {c.v};
-        if (pick_random(c, c.pas, c.np, om, 1, r)) sdel(c.pas, c.np, r);
+        if (pick_random(c, c.P, c.np, c.v, c.v, c.v, r)) l_del(c.P, c.np, r);
     }
-    sadd(c.pas, c.np, p);
+    l_add(c.P, c.np, p);
 }
 
-__device__ void drop_random_active(Ctx& c) {                                         // :2476-2525
+__device__ __forceinline__ void drop_random_active(W& c) {                                         // :2476-2525
     uint32_t r;
-    const uint32_t om[1] = {c.v};
-    if (!pick_random(c, c.act, c.na, om, 1, r)) return;
-    sdel(c.act, c.na, r);
+    if (!pick_random(c, c.A, c.na, c.v, c.v, c.v, r)) return;
+    l_del(c.A, c.na, r);
     add_to_passive(c, r);
     const IdMap m = sent_map(c);
     uint2 prev;
@@ -191,130 +312,136 @@ __device__ void drop_random_active(Ctx& c) {                                    
         nc = prev.y + 1;
     }
     mput(c, m, c.nsent, r, ne, nc);
-    if (alive_of(*c.a, r)) {
-        HvMsg* x = emit(c, r, HV_DISCONNECT);
-        if (x) { x->peer = c.v; x->did_e = ne; x->did_c = nc; }
+    if (alive_w(c, r)) {
+        Out o = out_msg(HV_DISCONNECT);
+        o.peer = c.v; o.did_e = ne; o.did_c = nc;
+        emit(c, r, o);
     }
 }
 
-__device__ void add_to_active(Ctx& c, uint32_t p) {                                  // :2344-2410
-    if (p == c.v || has(c.act, c.na, p)) return;
-    sdel(c.pas, c.np, p);
+__device__ __forceinline__ void add_to_active(W& c, uint32_t p) {                                  // :2344-2410
+    if (p == c.v || l_has(c.A, c.na, p)) return;
+    l_del(c.P, c.np, p);
     if (c.na >= c.a->cfg.active_max_size) drop_random_active(c);
-    sadd(c.act, c.na, p);
+    l_add(c.A, c.na, p);
 }
 
-__device__ void merge_exchange(Ctx& c, const uint32_t* ex, uint32_t nx) {            // :2569-2576
-    uint32_t to[kHvX + 1], k = 0;
-    for (uint32_t i = 0; i < nx; i++)
-        if (ex[i] != c.v && !has(c.act, c.na, ex[i])) sadd(to, k, ex[i]);
-    for (uint32_t i = 0; i < k; i++) add_to_passive(c, to[i]);
+// merge_exchange/2 (:2569-2576): usort(Exchange) minus self and active, each
+// added to the passive view in order
+__device__ __forceinline__ void merge_exchange(W& c, uint32_t ex, uint32_t nx) {
+    const uint32_t l = lane_id();
+    uint32_t to = 0xFFFFFFFFu, k = 0;
+    for (uint32_t i = 0; i < nx; i++) {
+        const uint32_t y = l_at(ex, i);
+        if (y != c.v && !l_has(c.A, c.na, y)) l_add(to, k, y);
+    }
+    (void)l;
+    for (uint32_t i = 0; i < k; i++) add_to_passive(c, l_at(to, i));
 }
 
-__device__ void promote_peer(Ctx& c, uint32_t p) {                                   // :2675-2697
-    uint32_t ex[kHvX];
+__device__ __forceinline__ void promote_peer(W& c, uint32_t p) {                                   // :2675-2697
+    uint32_t ex;
     const uint32_t nx = select_exchange(c, ex);
     uint32_t e, cnt;
     get_current_id(c, p, e, cnt);
-    if (!alive_of(*c.a, p)) return;
-    HvMsg* x = emit(c, p, HV_NEIGHBOR_REQUEST);
-    if (!x) return;
-    x->peer = c.v; x->prio = 1; x->did_e = e; x->did_c = cnt; x->nx = nx;
-    for (uint32_t i = 0; i < nx; i++) x->x[i] = ex[i];
+    if (!alive_w(c, p)) return;
+    Out o = out_msg(HV_NEIGHBOR_REQUEST);
+    o.peer = c.v; o.prio = 1; o.did_e = e; o.did_c = cnt; o.nx = nx; o.x = ex;
+    emit(c, p, o);
 }
 
-__device__ void send_neighbor(Ctx& c, uint32_t p) {
+__device__ __forceinline__ void send_neighbor(W& c, uint32_t p) {
     uint32_t e, cnt;
     get_current_id(c, p, e, cnt);
-    HvMsg* x = emit(c, p, HV_NEIGHBOR);
-    if (x) { x->peer = c.v; x->did_e = e; x->did_c = cnt; }
+    Out o = out_msg(HV_NEIGHBOR);
+    o.peer = c.v; o.did_e = e; o.did_c = cnt;
+    emit(c, p, o);
 }
 
-__device__ void handle(Ctx& c, const HvMsg& m) {
+// one received message (uniform header m*, exchange list mx one per lane)
+struct In {
+    uint32_t type, ttl, prio, nx, src, peer, epoch, did_e, did_c;
+    uint32_t x;
+};
+
+__device__ __forceinline__ void handle(W& c, const In& m) {
     const uint32_t P = m.peer;
     switch (m.type) {
     case HV_JOIN:                                                                   // :1234-1338
-        if (is_addable_epoch(c, m.epoch, P) && !has(c.act, c.na, P) && alive_of(*c.a, P)) {
+        if (is_addable_epoch(c, m.epoch, P) && !l_has(c.A, c.na, P) && alive_w(c, P)) {
             add_to_active(c, P);
             send_neighbor(c, P);
             for (uint32_t i = 0; i < c.na; i++) {
-                const uint32_t q = c.act[i];
-                if (q == c.v || q == P || !alive_of(*c.a, q)) continue;
-                HvMsg* f = emit(c, q, HV_FORWARD_JOIN);
-                if (f) { f->peer = P; f->epoch = m.epoch; f->ttl = c.a->cfg.active_rwl; }
+                const uint32_t q = l_at(c.A, i);
+                if (q == c.v || q == P || !alive_w(c, q)) continue;
+                Out o = out_msg(HV_FORWARD_JOIN);
+                o.peer = P; o.epoch = m.epoch; o.ttl = c.a->cfg.active_rwl;
+                emit(c, q, o);
             }
         }
         break;
     case HV_NEIGHBOR:                                                               // :1340-1379
-        if (is_addable_did(c, m.did_e, m.did_c, P) && alive_of(*c.a, P)) add_to_active(c, P);
+        if (is_addable_did(c, m.did_e, m.did_c, P) && alive_w(c, P)) add_to_active(c, P);
         break;
     case HV_FORWARD_JOIN: {                                                         // :1381-1563
         const uint32_t S = m.src;
         if (m.ttl == 0 || c.na == 1) {
-            if (is_addable_epoch(c, m.epoch, P) && !has(c.act, c.na, P) && alive_of(*c.a, P)) {
+            if (is_addable_epoch(c, m.epoch, P) && !l_has(c.A, c.na, P) && alive_w(c, P)) {
                 add_to_active(c, P);
                 send_neighbor(c, P);
             }
         } else {
-            uint32_t act0[8], na0 = c.na, pas0[32], np0 = c.np;
-            for (uint32_t i = 0; i < 8; i++) act0[i] = c.act[i];
-            for (uint32_t i = 0; i < np0; i++) pas0[i] = c.pas[i];
+            const uint32_t A0 = c.A, na0 = c.na, P0 = c.P, np0 = c.np;
             if (m.ttl == c.a->cfg.passive_rwl) add_to_passive(c, P);
-            const uint32_t om[3] = {S, c.v, P};
             uint32_t r;
-            if (!pick_random(c, act0, na0, om, 3, r)) {
-                if (is_addable_epoch(c, m.epoch, P) && !has(act0, na0, P)) {
-                    if (alive_of(*c.a, P)) {
+            if (!pick_random(c, A0, na0, S, c.v, P, r)) {
+                if (is_addable_epoch(c, m.epoch, P) && !l_has(A0, na0, P)) {
+                    if (alive_w(c, P)) {
                         add_to_active(c, P);
                         send_neighbor(c, P);
                     } else {                                   // `false -> State0`
                         c.np = np0;
-                        for (uint32_t i = 0; i < np0; i++) c.pas[i] = pas0[i];
+                        c.P = P0;
                     }
                 }
-            } else if (alive_of(*c.a, r)) {
-                HvMsg* f = emit(c, r, HV_FORWARD_JOIN);
-                if (f) { f->peer = P; f->epoch = m.epoch; f->ttl = m.ttl - 1; }
+            } else if (alive_w(c, r)) {
+                Out o = out_msg(HV_FORWARD_JOIN);
+                o.peer = P; o.epoch = m.epoch; o.ttl = m.ttl - 1;
+                emit(c, r, o);
             }
         }
         break;
     }
     case HV_DISCONNECT: {                                                           // :1565-1617
         if (!is_valid_disconnect(c, m.did_e, m.did_c, P)) break;
-        uint32_t pas0[32], np0 = c.np;
-        for (uint32_t i = 0; i < np0; i++) pas0[i] = c.pas[i];
-        sdel(c.act, c.na, P);
+        const uint32_t P0 = c.P, np0 = c.np;
+        l_del(c.A, c.na, P);
         add_to_passive(c, P);
         mput(c, recv_map(c), c.nrecv, P, m.did_e, m.did_c);
         if (c.na == 1) {
-            const uint32_t om[2] = {c.v, P};
             uint32_t r;
-            if (pick_random(c, pas0, np0, om, 2, r)) promote_peer(c, r);
+            if (pick_random(c, P0, np0, c.v, P, P, r)) promote_peer(c, r);
         }
         break;
     }
     case HV_NEIGHBOR_REQUEST: {                                                     // :1619-1711
-        uint32_t ack[kHvX];
+        uint32_t ack;
         const uint32_t nack = select_exchange(c, ack);
         if (!m.prio && c.na >= c.a->cfg.active_max_size) {
             c.err |= 8u;                                       // 2-tuple neighbor_rejected: no clause
         } else if (is_addable_did(c, m.did_e, m.did_c, P)) {
-            if (alive_of(*c.a, P)) {
+            if (alive_w(c, P)) {
                 uint32_t e, cnt;
                 get_current_id(c, P, e, cnt);
-                HvMsg* x = emit(c, P, HV_NEIGHBOR_ACCEPTED);
-                if (x) {
-                    x->peer = c.v; x->did_e = e; x->did_c = cnt; x->nx = nack;
-                    for (uint32_t i = 0; i < nack; i++) x->x[i] = ack[i];
-                }
+                Out o = out_msg(HV_NEIGHBOR_ACCEPTED);
+                o.peer = c.v; o.did_e = e; o.did_c = cnt; o.nx = nack; o.x = ack;
+                emit(c, P, o);
                 add_to_active(c, P);
             }
-        } else if (alive_of(*c.a, P)) {
-            HvMsg* x = emit(c, P, HV_NEIGHBOR_REJECTED);
-            if (x) {
-                x->peer = c.v; x->nx = nack;
-                for (uint32_t i = 0; i < nack; i++) x->x[i] = ack[i];
-            }
+        } else if (alive_w(c, P)) {
+            Out o = out_msg(HV_NEIGHBOR_REJECTED);
+            o.peer = c.v; o.nx = nack; o.x = ack;
+            emit(c, P, o);
         }
         merge_exchange(c, m.x, m.nx);
         break;
@@ -332,24 +459,19 @@ __device__ void handle(Ctx& c, const HvMsg& m) {
     case HV_SHUFFLE: {                                                              // :1754-1798
         const uint32_t S = P;
         if (m.ttl > 0 && c.na > 1) {
-            const uint32_t om[2] = {S, c.v};
             uint32_t r;
-            if (pick_random(c, c.act, c.na, om, 2, r) && alive_of(*c.a, r)) {
-                HvMsg* f = emit(c, r, HV_SHUFFLE);
-                if (f) {
-                    f->peer = c.v; f->ttl = m.ttl - 1; f->nx = m.nx;
-                    for (uint32_t i = 0; i < m.nx; i++) f->x[i] = m.x[i];
-                }
+            if (pick_random(c, c.A, c.na, S, c.v, c.v, r) && alive_w(c, r)) {
+                Out o = out_msg(HV_SHUFFLE);
+                o.peer = c.v; o.ttl = m.ttl - 1; o.nx = m.nx; o.x = m.x;
+                emit(c, r, o);
             }
         } else {
             for (uint32_t i = 0; i < c.np; i++) (void)draw64(c);     // shuffle(Passive, |Exchange|)
             const uint32_t k = c.np < m.nx ? c.np : m.nx;
-            if (alive_of(*c.a, S)) {
-                HvMsg* f = emit(c, S, HV_SHUFFLE_REPLY);
-                if (f) {
-                    f->peer = c.v; f->nx = k;
-                    for (uint32_t i = 0; i < k; i++) f->x[i] = c.pas[i];
-                }
+            if (alive_w(c, S)) {
+                Out o = out_msg(HV_SHUFFLE_REPLY);
+                o.peer = c.v; o.nx = k; o.x = c.P;
+                emit(c, S, o);
             }
             merge_exchange(c, m.x, m.nx);
         }
@@ -360,9 +482,6 @@ __device__ void handle(Ctx& c, const HvMsg& m) {
     }
 }
 
-__device__ __forceinline__ bool msg_less(const HvMsg& x, const HvMsg& y) {
-    return x.src < y.src || (x.src == y.src && x.seq < y.seq);
-}
 
 __device__ __forceinline__ uint32_t n_in(const HvArgs& a) { const uint32_t k = *a.nin; return k < a.out_cap ? k : a.out_cap; }
 
@@ -424,83 +543,132 @@ __global__ __launch_bounds__(kBlock) void hv_scatter(HvArgs a) {
     }
 }
 
+constexpr uint32_t kHvWaves = kBlock / 64;
+
+// the message with index i, fields made wave-uniform, x[] one per lane
+__device__ __forceinline__ In load_msg(const HvArgs& a, uint32_t i) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a.in + i);
+    const uint32_t l = lane_id();
+    const uint32_t mine = l < 16 ? w[l] : 0u;
+    In m;
+    const uint32_t h = uni(__shfl(mine, 0, 64));
+    m.type = h & 0xFFu; m.ttl = (h >> 8) & 0xFFu; m.prio = (h >> 16) & 0xFFu; m.nx = h >> 24;
+    m.src = uni(__shfl(mine, 1, 64));
+    m.peer = uni(__shfl(mine, 4, 64));
+    m.epoch = uni(__shfl(mine, 5, 64));
+    m.did_e = uni(__shfl(mine, 6, 64));
+    m.did_c = uni(__shfl(mine, 7, 64));
+    const uint32_t xv = __shfl(mine, (8 + l) & 63, 64);
+    m.x = l < m.nx ? xv : 0xFFFFFFFFu;
+    return m;
+}
+
+// One wave per vertex: a wave takes 64 consecutive vertices at a time, keeps
+// those with messages (or every live one on a timer round), and runs each of
+// them with all its lanes.
 __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
-    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
-    uint32_t ndraw = 0, err = 0, nproc = 0, act1 = 0;
-    uint32_t sent[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (v < a.n) {
-        const uint32_t lo = a.off[v], hi = a.off[v + 1];
-        const bool up = alive_of(a, v);
-        if (up && (hi > lo || a.timers)) {
-            Ctx c;
+    const uint32_t l = lane_id();
+    const uint32_t gw = blockIdx.x * kHvWaves + (threadIdx.x >> 6), nw = gridDim.x * kHvWaves;
+    uint32_t err = 0;
+    for (uint32_t base = gw * 64; base < a.n; base += nw * 64) {
+        uint64_t k0 = 0, k1 = 0, k2 = 0;     // this group's counters (flushed per group: no field overflows)
+        uint32_t ndraw = 0, nproc = 0, act1 = 0;
+        const uint32_t u = base + l;
+        bool want = false;
+        if (u < a.n && alive_of(a, u)) want = a.timers || a.off[u + 1] > a.off[u];
+        uint64_t todo = ballot(want);
+        while (todo) {
+            const uint32_t j = (uint32_t)__ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            W c;
             c.a = &a;
-            c.v = v;
+            c.v = base + j;
+            const uint32_t v = c.v;
             const HvHead h = a.head[v];
-            c.na = h.na; c.np = h.np; c.nsent = h.nsent; c.nrecv = h.nrecv; c.seq = h.seq; c.draws = h.draws;
-            for (uint32_t i = 0; i < 8; i++) c.act[i] = a.act[(size_t)v * 8 + i];
-            for (uint32_t i = 0; i < 32; i++) c.pas[i] = a.pas[(size_t)v * 32 + i];
-            for (int i = 0; i < 10; i++) c.sent_cnt[i] = 0;
+            c.na = uni(h.na); c.np = uni(h.np); c.nsent = uni(h.nsent); c.nrecv = uni(h.nrecv); c.seq = uni(h.seq);
+            c.draws = ((uint64_t)uni((uint32_t)(h.draws >> 32)) << 32) | uni((uint32_t)h.draws);
+            c.A = l < 8 ? a.act[(size_t)v * 8 + l] : 0xFFFFFFFFu;
+            c.P = l < 32 ? a.pas[(size_t)v * 32 + l] : 0xFFFFFFFFu;
+            if (l >= c.na) c.A = 0xFFFFFFFFu;
+            if (l >= c.np) c.P = 0xFFFFFFFFu;
+            c.k0 = c.k1 = c.k2 = 0;
             c.ndraw = 0;
             c.err = 0;
-            // sort the bucket by (src, seq): insertion sort of indices
-            for (uint32_t i = lo + 1; i < hi; i++) {
-                const uint32_t x = a.idx[i];
-                const HvMsg& mx = a.in[x];
-                uint32_t j = i;
-                while (j > lo && msg_less(mx, a.in[a.idx[j - 1]])) { a.idx[j] = a.idx[j - 1]; j--; }
-                a.idx[j] = x;
+            const uint32_t lo = uni(a.off[v]), hi = uni(a.off[v + 1]), nb = hi - lo;
+            // the bucket in (src, seq) order
+            if (nb <= 64) {
+                const uint32_t mi = l < nb ? a.idx[lo + l] : 0u;
+                uint32_t src = 0xFFFFFFFFu, sq = 0xFFFFFFFFu;
+                if (l < nb) { src = a.in[mi].src; sq = a.in[mi].seq; }
+                uint32_t rank = 0;
+                for (uint32_t q = 0; q < nb; q++) {
+                    const uint32_t s2 = __shfl(src, q, 64), q2 = __shfl(sq, q, 64);
+                    rank += (s2 < src || (s2 == src && q2 < sq)) ? 1u : 0u;
+                }
+                // lane r holds the index of the message of rank r
+                const uint32_t sorted = __builtin_amdgcn_ds_permute((l < nb ? rank : l) * 4, (int)mi);
+                for (uint32_t q = 0; q < nb; q++) handle(c, load_msg(a, uni(__shfl(sorted, q, 64))));
+            } else {
+                if (l == 0)   // a crowded bucket: insertion sort of its indices by one lane
+                    for (uint32_t i = lo + 1; i < hi; i++) {
+                        const uint32_t x = a.idx[i];
+                        const HvMsg& mx = a.in[x];
+                        uint32_t jj = i;
+                        while (jj > lo && (mx.src < a.in[a.idx[jj - 1]].src ||
+                                           (mx.src == a.in[a.idx[jj - 1]].src && mx.seq < a.in[a.idx[jj - 1]].seq))) {
+                            a.idx[jj] = a.idx[jj - 1];
+                            jj--;
+                        }
+                        a.idx[jj] = x;
+                    }
+                __threadfence_block();
+                for (uint32_t q = lo; q < hi; q++) handle(c, load_msg(a, uni(a.idx[q])));
             }
-            for (uint32_t i = lo; i < hi; i++) handle(c, a.in[a.idx[i]]);
-            nproc = hi - lo;
-            act1 = 1;
+            nproc += nb;
+            act1++;
             if (a.timers & 1u) {                                   // random_promotion (:1046-1067)
                 if (c.na < a.cfg.active_min_size) {
-                    const uint32_t om[1] = {v};
                     uint32_t r;
-                    if (pick_random(c, c.pas, c.np, om, 1, r)) promote_peer(c, r);
+                    if (pick_random(c, c.P, c.np, v, v, v, r)) promote_peer(c, r);
                 }
             }
             if (a.timers & 2u) {                                   // passive_view_maintenance (:1078-1111)
-                uint32_t ex[kHvX];
+                uint32_t ex;
                 const uint32_t nx = select_exchange(c, ex);
-                const uint32_t om[1] = {v};
                 uint32_t r;
-                if (pick_random(c, c.act, c.na, om, 1, r) && alive_of(a, r)) {
-                    HvMsg* f = emit(c, r, HV_SHUFFLE);
-                    if (f) {
-                        f->peer = v; f->ttl = a.cfg.active_rwl; f->nx = nx;
-                        for (uint32_t i = 0; i < nx; i++) f->x[i] = ex[i];
-                    }
+                if (pick_random(c, c.A, c.na, v, v, v, r) && alive_w(c, r)) {
+                    Out o = out_msg(HV_SHUFFLE);
+                    o.peer = v; o.ttl = a.cfg.active_rwl; o.nx = nx; o.x = ex;
+                    emit(c, r, o);
                 }
             }
-            for (uint32_t i = 0; i < 8; i++) a.act[(size_t)v * 8 + i] = i < c.na ? c.act[i] : 0xFFFFFFFFu;
-            for (uint32_t i = 0; i < 32; i++) a.pas[(size_t)v * 32 + i] = i < c.np ? c.pas[i] : 0xFFFFFFFFu;
-            HvHead nh;
-            nh.na = c.na; nh.np = c.np; nh.nsent = c.nsent; nh.nrecv = c.nrecv; nh.seq = c.seq; nh.draws = c.draws;
-            a.head[v] = nh;
-            ndraw = c.ndraw;
-            err = c.err;
-            for (int i = 0; i < 10; i++) sent[i] = c.sent_cnt[i];
+            if (l < 8) a.act[(size_t)v * 8 + l] = l < c.na ? c.A : 0xFFFFFFFFu;
+            if (l < 32) a.pas[(size_t)v * 32 + l] = l < c.np ? c.P : 0xFFFFFFFFu;
+            if (l == 0) {
+                HvHead nh;
+                nh.na = (uint8_t)c.na; nh.np = (uint8_t)c.np; nh.nsent = (uint16_t)c.nsent; nh.nrecv = (uint16_t)c.nrecv;
+                nh.seq = c.seq; nh.draws = c.draws;
+                a.head[v] = nh;
+            }
+            ndraw += c.ndraw;
+            err |= c.err;
+            k0 += c.k0;
+            k1 += c.k1;
+            k2 += c.k2;
+        }
+        // counters: wave-uniform, one atomic per group and counter
+        if (l == 0 && act1) {
+#pragma unroll
+            for (uint32_t t = 1; t < 10; t++) {
+                const uint32_t x = kind_count(k0, k1, k2, t);
+                if (x) atomicAdd(&a.stats[t], (unsigned long long)x);
+            }
+            if (ndraw) atomicAdd(&a.stats[10], (unsigned long long)ndraw);
+            if (nproc) atomicAdd(&a.stats[12], (unsigned long long)nproc);
+            atomicAdd(&a.stats[13], (unsigned long long)act1);
         }
     }
-    // counters: one atomic per wave per counter
-    unsigned long long vals[14];
-    for (int i = 1; i < 10; i++) vals[i] = sent[i];
-    vals[10] = ndraw;
-    vals[11] = 0;
-    vals[12] = nproc;
-    vals[13] = act1;
-    for (int i = 1; i <= 13; i++) {
-        if (i == 11) continue;
-        unsigned long long x = vals[i];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[i], x);
-    }
-    unsigned long long e = err;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) e |= __shfl_xor(e, o, 64);
-    if ((threadIdx.x & 63) == 0 && e) atomicOr(&a.stats[11], e);
+    if (l == 0 && err) atomicOr(&a.stats[11], (unsigned long long)err);
 }
 
 // handle_cast({join, Peer}) (:999-1016) at v[i]: connect + {join, Myself, Tag, Epoch};
@@ -532,6 +700,13 @@ __global__ __launch_bounds__(kBlock) void hv_init_kernel(HvArgs a) {
 }
 
 inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+// hv_process: one 64-vertex group per wave (the waves are latency-bound:
+// as many as the chip holds), grid-striding beyond 64K workgroups
+inline uint32_t hv_blocks(uint32_t n) {
+    const uint32_t groups = (n + 63) / 64;
+    const uint32_t b = (groups + kHvWaves - 1) / kHvWaves;
+    return b < 1 ? 1 : (b > 65535 ? 65535 : b);
+}
 
 }  // namespace
 
@@ -555,7 +730,7 @@ hipError_t launch_hv_round(const HvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(hv_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
     hipLaunchKernelGGL(hv_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(hv_scatter, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(hv_process, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(hv_process, dim3(hv_blocks(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -2593,6 +2593,8 @@ int hv_check_err(psim_handle* h, unsigned long long e, uint64_t round) {
                               (unsigned long long)round, h->hv.cap);
     if (e & 2ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: id-map table (%u slots) too full",
                               (unsigned long long)round, h->hv.map_cap);
+    if (e & 16ull) return fail(h, PSIM_ESTATE, "hyparview round %llu: a view held a non-vertex id (engine bug)",
+                               (unsigned long long)round);
     return PSIM_OK;
 }
 

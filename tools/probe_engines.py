@@ -92,6 +92,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "c3":
         print(json.dumps(c3(int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000, 30)), flush=True)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "hv":
+        print(json.dumps(hv(int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000, 5000)), flush=True)
+        sys.exit(0)
     res = [hv(int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000, 5000), causal(1_000_000, 64, 12)]
     for r in res:
         print(json.dumps(r), flush=True)
