@@ -33,8 +33,11 @@ __device__ __forceinline__ bool alive_of(const HvArgs& a, uint32_t v) { return (
 // set operations of the reference (ordsets add / del / member, pick_random's
 // filter, the exchange list's usort) are ballots, popcounts and shuffles.
 // Nothing is indexed at run time from a private array, so nothing spills.
+constexpr uint32_t kHvStage = 32;    // records a wave stages in LDS before one reservation
 struct W {
     const HvArgs* a;
+    uint32_t* stage;               // this wave's LDS staging: kHvStage records of 16 dwords
+    uint32_t* nstage;              // records staged (wave-uniform, in registers of the caller)
     uint32_t v;
     uint32_t A, P;                 // this lane's active / passive view element
     uint32_t na, np;
@@ -71,6 +74,12 @@ __device__ __forceinline__ uint64_t draw64(W& c) {
     c.draws++;
     c.ndraw++;
     return (uint64_t)r.x | ((uint64_t)r.y << 32);
+}
+// draws whose values nothing uses (shuffle/2's sort keys of a list that is
+// only truncated): the counter-based stream just moves on
+__device__ __forceinline__ void skip_draws(W& c, uint32_t k) {
+    c.draws += k;
+    c.ndraw += k;
 }
 __device__ __forceinline__ uint32_t uniform(W& c, uint32_t n) {   // rand:uniform(N), N >= 1
     return 1u + (uint32_t)__umul64hi(draw64(c), (uint64_t)n);
@@ -186,16 +195,37 @@ __device__ __forceinline__ Out out_msg(uint32_t type) {
     o.type = type; o.ttl = 0; o.prio = 0; o.nx = 0; o.peer = 0; o.epoch = 0; o.did_e = 0; o.did_c = 0; o.x = 0;
     return o;
 }
-// emission: one reservation per message (lane 0), the 64-byte record written
-// by lanes 0..15 (one dword each, one transaction)
+// The wave's staged records go to the queue with ONE reservation (lane 0's
+// atomicAdd) and a coalesced copy: where a record lands never matters, the
+// next round re-sorts each bucket by (src, seq).  One atomic per message on
+// the queue counter was the round's bound (~0.8M serialised atomics).
+__device__ __forceinline__ uint32_t flush_stage(const HvArgs& a, uint32_t* stage, uint32_t ns) {
+    if (ns == 0) return 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(a.nout, ns);
+    base = uni(base);
+    uint32_t err = 0;
+    uint32_t fit = ns;
+    if (base >= a.out_cap) { fit = 0; err = 1u; }
+    else if (base + ns > a.out_cap) { fit = a.out_cap - base; err = 1u; }
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out + base);
+    for (uint32_t k = lane_id(); k < fit * 16; k += 64) out[k] = stage[k];
+    __builtin_amdgcn_wave_barrier();
+    return err;
+}
+
+// emission: the 64-byte record written into the wave's LDS stage by lanes
+// 0..15 (one dword each)
 __device__ __forceinline__ void emit(W& c, uint32_t dst, const Out& o) {
     if (dst >= c.a->n) { c.err |= 16u; return; }
     count_kind(c, o.type);
     const uint32_t seq = c.seq++;
-    uint32_t pos = 0;
-    if (lane_id() == 0) pos = atomicAdd(c.a->nout, 1u);
-    pos = uni(pos);
-    if (pos >= c.a->out_cap) { c.err |= 1u; return; }
+    if (*c.nstage == kHvStage) {
+        c.err |= flush_stage(*c.a, c.stage, *c.nstage);
+        *c.nstage = 0;
+    }
+    const uint32_t pos = (*c.nstage)++;
     const uint32_t l = lane_id();
     uint32_t w = 0;
     switch (l) {
@@ -211,7 +241,8 @@ __device__ __forceinline__ void emit(W& c, uint32_t dst, const Out& o) {
     }
     const uint32_t xv = __shfl(o.x, (l - 8) & 63, 64);
     if (l >= 8 && l < 16) w = (l - 8 < o.nx) ? xv : 0u;
-    if (l < 16) reinterpret_cast<uint32_t*>(c.a->out + pos)[l] = w;
+    if (l < 16) c.stage[pos * 16 + l] = w;
+    __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ bool alive_w(W& c, uint32_t p) {
@@ -235,7 +266,7 @@ __device__ __forceinline__ bool pick_random(W& c, uint32_t view, uint32_t nv, ui
 // element (Q8); the list is usort([Myself | k_active of Active ++ k_passive of
 // Passive]), returned lane-distributed
 __device__ __forceinline__ uint32_t select_exchange(W& c, uint32_t& ex) {
-    for (uint32_t i = 0; i < c.na + c.np; i++) (void)draw64(c);
+    skip_draws(c, c.na + c.np);
     const uint32_t l = lane_id();
     const uint32_t ka = min(c.na, c.a->cfg.shuffle_k_active), kp = min(c.np, c.a->cfg.shuffle_k_passive);
     const uint32_t av = __shfl(c.A, (l - 1) & 63, 64), pv = __shfl(c.P, (l - 1 - ka) & 63, 64);
@@ -466,7 +497,7 @@ __device__ __forceinline__ void handle(W& c, const In& m) {
                 emit(c, r, o);
             }
         } else {
-            for (uint32_t i = 0; i < c.np; i++) (void)draw64(c);     // shuffle(Passive, |Exchange|)
+            skip_draws(c, c.np);                                      // shuffle(Passive, |Exchange|)
             const uint32_t k = c.np < m.nx ? c.np : m.nx;
             if (alive_w(c, S)) {
                 Out o = out_msg(HV_SHUFFLE_REPLY);
@@ -567,8 +598,11 @@ __device__ __forceinline__ In load_msg(const HvArgs& a, uint32_t i) {
 // those with messages (or every live one on a timer round), and runs each of
 // them with all its lanes.
 __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
+    __shared__ uint32_t stage_all[kHvWaves][kHvStage * 16];
     const uint32_t l = lane_id();
     const uint32_t gw = blockIdx.x * kHvWaves + (threadIdx.x >> 6), nw = gridDim.x * kHvWaves;
+    uint32_t* stage = stage_all[threadIdx.x >> 6];
+    uint32_t nstage = 0;
     uint32_t err = 0;
     for (uint32_t base = gw * 64; base < a.n; base += nw * 64) {
         uint64_t k0 = 0, k1 = 0, k2 = 0;     // this group's counters (flushed per group: no field overflows)
@@ -582,6 +616,8 @@ __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
             todo &= todo - 1;
             W c;
             c.a = &a;
+            c.stage = stage;
+            c.nstage = &nstage;
             c.v = base + j;
             const uint32_t v = c.v;
             const HvHead h = a.head[v];
@@ -668,6 +704,7 @@ __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
             atomicAdd(&a.stats[13], (unsigned long long)act1);
         }
     }
+    err |= flush_stage(a, stage, nstage);
     if (l == 0 && err) atomicOr(&a.stats[11], (unsigned long long)err);
 }
 

@@ -23,6 +23,22 @@ inline bool alloc_zero(void** p, size_t bytes) {
 }
 
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+
+// One slot of a shared record queue for each calling lane: the lanes of a
+// wave that reach the call together share ONE atomicAdd on the counter (the
+// lowest active lane's), each taking base + its rank among them.  Record
+// order in the queues never matters (every consumer re-sorts by (src, seq)),
+// and one atomic per message on a single counter serialises at L2.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)act) - 1;
+    const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(act));
+    base = __shfl(base, (int)leader, 64);
+    return base + rank;
+}
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard

@@ -58,7 +58,7 @@ __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
 __device__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     if (!connected(c, t)) { c.dropped++; return; }
     const PdArgs& a = *c.a;
-    const uint32_t pos = atomicAdd(a.nout, 1u);
+    const uint32_t pos = wave_reserve(a.nout);
     c.sent[type]++;
     if (pos >= a.out_cap) { c.err |= 1u; return; }
     PdMsg m;

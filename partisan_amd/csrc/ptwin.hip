@@ -105,7 +105,7 @@ __device__ void emit(const WinArgs& a, V& x, Ctr& c, uint32_t s, uint32_t type, 
     x.sent = true;
     const uint32_t e = x.rs + s;
     if (a.omit && ((a.omit[e >> 5] >> (e & 31)) & 1u)) return;
-    const uint32_t pos = atomicAdd(a.nout, 1u);
+    const uint32_t pos = wave_reserve(a.nout);
     if (pos >= a.cap) { c.overflow |= 16u; return; }
     PdMsg m;
     m.type = type; m.src = a.v_lo + x.v; m.dst = a.col[e]; m.seq = seq; m.round = round; m.mono = mono;
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void win_convert_kernel(WinArgs a, PtArgs p
             r.mono = t == PSIM_MSG_PRUNE ? 0u : a.mono;              // a prune carries no id
             r.round = (t == PSIM_MSG_BROADCAST || t == PSIM_MSG_IHAVE) ? (w >> kRoundShift)
                     : (t == PSIM_MSG_PRUNE ? 0u : myround);
-            const uint32_t pos = atomicAdd(a.nout, 1u);
+            const uint32_t pos = wave_reserve(a.nout);
             if (pos < a.cap) a.out[pos] = r;
         }
     }

@@ -94,7 +94,7 @@ __device__ void emit(Ctx& c, uint32_t t, uint32_t type, uint32_t x, uint32_t y, 
     const ScArgs& a = *c.a;
     const bool conn = t != c.v && a.alive0[t] && (t == extra || in_pv(c, t));
     if (!conn) { c.dropped++; return; }
-    const uint32_t pos = atomicAdd(a.nout, 1u);
+    const uint32_t pos = wave_reserve(a.nout);
     c.sent[type]++;
     if (pos >= a.out_cap) { c.err |= 1u; return; }
     ScMsg m;
