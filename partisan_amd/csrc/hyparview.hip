@@ -33,7 +33,10 @@ __device__ __forceinline__ bool alive_of(const HvArgs& a, uint32_t v) { return (
 // set operations of the reference (ordsets add / del / member, pick_random's
 // filter, the exchange list's usort) are ballots, popcounts and shuffles.
 // Nothing is indexed at run time from a private array, so nothing spills.
-constexpr uint32_t kHvStage = 32;    // records a wave stages in LDS before one reservation
+#ifndef HV_STAGE
+#define HV_STAGE 32
+#endif
+constexpr uint32_t kHvStage = HV_STAGE;   // records a wave stages in LDS before one reservation
 struct W {
     const HvArgs* a;
     uint32_t* stage;               // this wave's LDS staging: kHvStage records of 16 dwords
@@ -597,7 +600,10 @@ __device__ __forceinline__ In load_msg(const HvArgs& a, uint32_t i) {
 // One wave per vertex: a wave takes 64 consecutive vertices at a time, keeps
 // those with messages (or every live one on a timer round), and runs each of
 // them with all its lanes.
-__global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
+#ifndef HV_WAVES_PER_EU
+#define HV_WAVES_PER_EU 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HV_WAVES_PER_EU))) void hv_process(HvArgs a) {
     __shared__ uint32_t stage_all[kHvWaves][kHvStage * 16];
     const uint32_t l = lane_id();
     const uint32_t gw = blockIdx.x * kHvWaves + (threadIdx.x >> 6), nw = gridDim.x * kHvWaves;
@@ -609,7 +615,12 @@ __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
         uint32_t ndraw = 0, nproc = 0, act1 = 0;
         const uint32_t u = base + l;
         bool want = false;
-        if (u < a.n && alive_of(a, u)) want = a.timers || a.off[u + 1] > a.off[u];
+        if (u < a.n && alive_of(a, u)) {
+            // a random_promotion-only round leaves a vertex with >= active_min_size
+            // active peers and an empty inbox untouched (no draw, no send)
+            want = (a.timers & 2u) || a.off[u + 1] > a.off[u] ||
+                   ((a.timers & 1u) && a.head[u].na < a.cfg.active_min_size);
+        }
         uint64_t todo = ballot(want);
         while (todo) {
             const uint32_t j = (uint32_t)__ffsll((long long)todo) - 1;
@@ -627,6 +638,9 @@ __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
             c.P = l < 32 ? a.pas[(size_t)v * 32 + l] : 0xFFFFFFFFu;
             if (l >= c.na) c.A = 0xFFFFFFFFu;
             if (l >= c.np) c.P = 0xFFFFFFFFu;
+            const uint32_t A_in = c.A, P_in = c.P, na_in = c.na, np_in = c.np, ns_in = c.nsent, nr_in = c.nrecv,
+                           seq_in = c.seq;
+            const uint64_t dr_in = c.draws;
             c.k0 = c.k1 = c.k2 = 0;
             c.ndraw = 0;
             c.err = 0;
@@ -678,9 +692,15 @@ __global__ __launch_bounds__(kBlock) void hv_process(HvArgs a) {
                     emit(c, r, o);
                 }
             }
-            if (l < 8) a.act[(size_t)v * 8 + l] = l < c.na ? c.A : 0xFFFFFFFFu;
-            if (l < 32) a.pas[(size_t)v * 32 + l] = l < c.np ? c.P : 0xFFFFFFFFu;
-            if (l == 0) {
+            // write back only what changed
+            if (ballot(l < 8 && c.A != A_in)) {
+                if (l < 8) a.act[(size_t)v * 8 + l] = l < c.na ? c.A : 0xFFFFFFFFu;
+            }
+            if (ballot(l < 32 && c.P != P_in)) {
+                if (l < 32) a.pas[(size_t)v * 32 + l] = l < c.np ? c.P : 0xFFFFFFFFu;
+            }
+            if (l == 0 && (c.na != na_in || c.np != np_in || c.nsent != ns_in || c.nrecv != nr_in || c.seq != seq_in ||
+                           c.draws != dr_in)) {
                 HvHead nh;
                 nh.na = (uint8_t)c.na; nh.np = (uint8_t)c.np; nh.nsent = (uint16_t)c.nsent; nh.nrecv = (uint16_t)c.nrecv;
                 nh.seq = c.seq; nh.draws = c.draws;
