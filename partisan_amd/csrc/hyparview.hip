@@ -645,7 +645,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HV_WAVES
             c.ndraw = 0;
             c.err = 0;
             const uint32_t lo = uni(a.off[v]), hi = uni(a.off[v + 1]), nb = hi - lo;
-            // the bucket in (src, seq) order
+            // the bucket in (src, seq) order: a rank sort over the wave --
+            // in registers for <= 64 messages, 64 keys at a time for more --
+            // then the messages handled in order, the next one's record loaded
+            // while the current one is handled
+            uint32_t sorted = 0;
+            const uint32_t* order = nullptr;
             if (nb <= 64) {
                 const uint32_t mi = l < nb ? a.idx[lo + l] : 0u;
                 uint32_t src = 0xFFFFFFFFu, sq = 0xFFFFFFFFu;
@@ -656,23 +661,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HV_WAVES
                     rank += (s2 < src || (s2 == src && q2 < sq)) ? 1u : 0u;
                 }
                 // lane r holds the index of the message of rank r
-                const uint32_t sorted = __builtin_amdgcn_ds_permute((l < nb ? rank : l) * 4, (int)mi);
-                for (uint32_t q = 0; q < nb; q++) handle(c, load_msg(a, uni(__shfl(sorted, q, 64))));
+                sorted = __builtin_amdgcn_ds_permute((l < nb ? rank : l) * 4, (int)mi);
             } else {
-                if (l == 0)   // a crowded bucket: insertion sort of its indices by one lane
-                    for (uint32_t i = lo + 1; i < hi; i++) {
-                        const uint32_t x = a.idx[i];
-                        const HvMsg& mx = a.in[x];
-                        uint32_t jj = i;
-                        while (jj > lo && (mx.src < a.in[a.idx[jj - 1]].src ||
-                                           (mx.src == a.in[a.idx[jj - 1]].src && mx.seq < a.in[a.idx[jj - 1]].seq))) {
-                            a.idx[jj] = a.idx[jj - 1];
-                            jj--;
+                for (uint32_t oc = 0; oc < nb; oc += 64) {
+                    const uint32_t me = oc + l < nb ? a.idx[lo + oc + l] : 0u;
+                    uint64_t mk = ~0ull;
+                    if (oc + l < nb) mk = ((uint64_t)a.in[me].src << 32) | a.in[me].seq;
+                    uint32_t rank = 0;
+                    for (uint32_t kc = 0; kc < nb; kc += 64) {
+                        const uint32_t oi = kc + l < nb ? a.idx[lo + kc + l] : 0u;
+                        uint64_t ok = ~0ull;
+                        if (kc + l < nb) ok = ((uint64_t)a.in[oi].src << 32) | a.in[oi].seq;
+                        const uint32_t klo = (uint32_t)ok, khi = (uint32_t)(ok >> 32);
+                        const uint32_t lim = min(64u, nb - kc);
+                        for (uint32_t q = 0; q < lim; q++) {
+                            const uint64_t y = ((uint64_t)__shfl(khi, q, 64) << 32) | __shfl(klo, q, 64);
+                            rank += y < mk ? 1u : 0u;
                         }
-                        a.idx[jj] = x;
                     }
+                    if (oc + l < nb) a.idx2[lo + rank] = me;
+                }
                 __threadfence_block();
-                for (uint32_t q = lo; q < hi; q++) handle(c, load_msg(a, uni(a.idx[q])));
+                order = a.idx2 + lo;
+            }
+            if (nb) {
+                In cur = load_msg(a, order ? uni(order[0]) : uni(__shfl(sorted, 0, 64)));
+                for (uint32_t q = 0; q < nb; q++) {
+                    In nxt = cur;
+                    if (q + 1 < nb) nxt = load_msg(a, order ? uni(order[q + 1]) : uni(__shfl(sorted, q + 1, 64)));
+                    handle(c, cur);
+                    cur = nxt;
+                }
             }
             nproc += nb;
             act1++;

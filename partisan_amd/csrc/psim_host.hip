@@ -187,6 +187,7 @@ struct psim_handle {
         HvMsg* msg[2] = {nullptr, nullptr};
         uint32_t* nmsg = nullptr;                 // [2] device queue counts
         uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
+        uint32_t* idx2 = nullptr;                 // [cap] crowded buckets, sorted
         uint32_t* joinbuf = nullptr;              // [2][n] staged join pairs
         unsigned long long* stats = nullptr;      // [kHvChunk][kHvNStat]
         unsigned long long* h_stats = nullptr;    // pinned mirror
@@ -244,7 +245,7 @@ constexpr uint32_t kHvChunk = 16;   // HyParView rounds between host synchronisa
 void free_hv(psim_handle* h) {
     auto& v = h->hv;
     void* ptrs[] = {v.head, v.act, v.pas, v.skey, v.sval, v.rkey, v.rval, v.alive, v.msg[0], v.msg[1], v.nmsg,
-                    v.cnt, v.cur, v.off, v.idx, v.bsum, v.joinbuf, v.stats};
+                    v.cnt, v.cur, v.off, v.idx, v.bsum, v.joinbuf, v.stats, v.idx2};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v.h_stats) (void)hipHostFree(v.h_stats);
@@ -2583,6 +2584,7 @@ HvArgs make_hv_args(const psim_handle* h, uint32_t par, unsigned long long* stat
     a.cur = v.cur;
     a.off = v.off;
     a.idx = v.idx;
+    a.idx2 = v.idx2;
     a.bsum = v.bsum;
     a.stats = stats;
     return a;
@@ -2624,7 +2626,8 @@ int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
               A((void**)&v.alive, ((N + 31) / 32) * 4) && A((void**)&v.msg[0], size_t(cap) * sizeof(HvMsg)) &&
               A((void**)&v.msg[1], size_t(cap) * sizeof(HvMsg)) && A((void**)&v.nmsg, 16) &&
               A((void**)&v.cnt, N * 4) && A((void**)&v.cur, N * 4) && A((void**)&v.off, (N + 1) * 4) &&
-              A((void**)&v.idx, size_t(cap) * 4) && A((void**)&v.bsum, size_t(nb) * 4) &&
+              A((void**)&v.idx, size_t(cap) * 4) && A((void**)&v.idx2, size_t(cap) * 4) &&
+              A((void**)&v.bsum, size_t(nb) * 4) &&
               A((void**)&v.joinbuf, 2 * N * 4) && A((void**)&v.stats, kHvChunk * kHvNStat * 8) &&
               hipHostMalloc((void**)&v.h_stats, kHvChunk * kHvNStat * 8, 0) == hipSuccess;
     for (auto& e : v.ev) ok = ok && hipEventCreate(&e) == hipSuccess;

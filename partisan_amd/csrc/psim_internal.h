@@ -227,6 +227,7 @@ struct HvArgs {
     uint32_t* __restrict__ cur;           // [n] bucket cursors
     uint32_t* __restrict__ off;           // [n+1] bucket starts
     uint32_t* __restrict__ idx;           // [cap] message indices bucketed by destination
+    uint32_t* __restrict__ idx2;          // [cap] a crowded bucket's indices in (src, seq) order
     uint32_t* __restrict__ bsum;          // [ceil(n/256)] scan partials
     unsigned long long* __restrict__ stats;  // [kHvNStat] for this round
 };
