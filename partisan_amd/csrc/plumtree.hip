@@ -67,7 +67,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 
 // Reduce the per-thread counters of a workgroup and add them to a shard.
 __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long* __restrict__ stats,
-                                               int* ost_total, int* msgs = nullptr) {
+                                               int* ost_total, uint32_t* msgs = nullptr) {
     __shared__ unsigned long long red[kBlock / 64][kNStat];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -97,11 +97,11 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
             if (s && i == S_OST_DELTA && ost_total) atomicAdd(ost_total, (int)(long long)s);
         }
     }
-    if (msgs && threadIdx.x == 0) {          // "this round sent something" for the next round's early exit:
-        unsigned long long m = 0;            // a plain store of 1 (an atomic per workgroup on one
-        for (int k = 1; k <= 5; k++)         // address serialises at ~12 ns each)
+    if (msgs && threadIdx.x == 0) {          // this round's messages into its count shard (PtArgs::mcnt)
+        unsigned long long m = 0;
+        for (int k = 1; k <= 5; k++)
             for (int w = 0; w < kBlock / 64; w++) m += red[w][k];
-        if (m) *msgs = 1;
+        if (m) atomicAdd(msgs, (uint32_t)m);
     }
 }
 
@@ -159,7 +159,7 @@ __device__ __forceinline__ unsigned long long* delay_hist() {
 
 template <bool kFault = true>
 __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w,
-                                             unsigned long long* hist = nullptr) {
+                                             unsigned long long* hist = nullptr, bool flag = true) {
     if (kFault && omitted(a, e)) return;
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
@@ -172,7 +172,7 @@ __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32
 #else
         a.in_nxt[a.rev[e] - a.slot_base] = w;
 #endif
-        a.pend_nxt[u >> kGroupShift] = 1;
+        if (flag) a.pend_nxt[u >> kGroupShift] = 1;
     } else {
         a.stage[e] = w;
     }
@@ -347,7 +347,7 @@ constexpr uint32_t kFastDeg = 8;
 // into LDS (pt_round_ell_body) and `lw` points at them.
 template <bool kFault, bool kLdsWords = false>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
-                                               bool due, Ctr& c, const uint32_t* lw = nullptr) {
+                                               bool due, Ctr& c, const uint32_t* lw = nullptr, bool flag = true) {
     uint32_t w[kFastDeg];
     uint32_t any = 0;
 #pragma unroll
@@ -400,7 +400,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 #else
             a.in_nxt[rv[s] - a.slot_base] = wo;
 #endif
-            a.pend_nxt[u >> kGroupShift] = 1;
+            if (flag) a.pend_nxt[u >> kGroupShift] = 1;
         } else {
             a.stage[rs + s] = wo;
         }
@@ -430,16 +430,16 @@ __device__ __forceinline__ void flush_delays(const PtArgs& a) {
 
 template <bool kFault>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
-                                          Ctr& c) {
+                                          Ctr& c, bool flag) {
     if (a.ell) {
-        pt_vertex_fast<kFault>(a, v, v * a.ell, a.ell, pend, due, c);
+        pt_vertex_fast<kFault>(a, v, v * a.ell, a.ell, pend, due, c, nullptr, flag);
         return;
     }
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
 #ifndef PT_NO_FAST
     if (deg <= kFastDeg) {
-        pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c);
+        pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c, nullptr, flag);
         return;
     }
 #endif
@@ -467,7 +467,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
-        deliver_word<kFault>(a, rs + s, w);
+        deliver_word<kFault>(a, rs + s, w, nullptr, flag);
         sent = true;
     }
     if (sent) {
@@ -481,6 +481,35 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 // them: their group flag (set by any sender to the group) and, on a tick
 // round while some vertex holds outstanding rows, their outstanding byte.
 // Candidates are compacted into an LDS list and spread over the threads.
+// The counts of the last two rounds (PtArgs::mcnt): wave 0 sums the 64
+// shards; block 0 zeroes the slot of the round after next.  Returns false
+// when the round is a no-op (nothing was sent, no row is due).
+__device__ __forceinline__ bool round_counts(const PtArgs& a, bool& flag_out, bool& all_in) {
+    __shared__ uint32_t cnt2[2];
+    flag_out = true;
+    all_in = false;
+    if (!a.mcnt) return true;
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {
+        uint32_t c1 = a.mcnt[a.m_s * 64 + t], c2 = a.mcnt[a.m_r * 64 + t];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            c1 += __shfl_xor(c1, off, 64);
+            c2 += __shfl_xor(c2, off, 64);
+        }
+        if (t == 0) { cnt2[0] = c1; cnt2[1] = c2; }
+        if (blockIdx.x == 0) a.mcnt[a.m_z * 64 + t] = 0;   // the round after next starts empty
+    }
+    __syncthreads();
+    const uint32_t prev = cnt2[0], prev2 = cnt2[1];
+    // nothing was sent last round and no row is due: every vertex is idle
+    // (no inbox flag can be set), so the whole round is a no-op
+    if (prev == 0 && !(a.tick && *a.ost_total > 0)) return false;
+    flag_out = prev < a.dense;       // many senders expected: no group flags this round
+    all_in = prev2 >= a.dense;       // the last round wrote none: every group is read
+    return true;
+}
+
 // kFault: omission faults installed (psim_set_omissions); the common case
 // compiles without the per-word bitmap test.
 template <bool kFault>
@@ -490,12 +519,8 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     static_assert(kChunkV == 4 * kBlock && (kChunkV << 2) <= 65536, "candidate encoding");
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
-    if (a.msgs3) {
-        if (blockIdx.x == 0 && t == 0) a.msgs3[a.mnext] = 0;   // the next round's counter starts empty
-        // nothing was sent last round and no row is due: every vertex is idle
-        // (no inbox flag can be set), so the whole round is a no-op
-        if (a.msgs3[a.mprev] == 0 && !(a.tick && *a.ost_total > 0)) return;
-    }
+    bool flag, all_in;
+    if (!round_counts(a, flag, all_in)) return;
     const uint32_t base = blockIdx.x * kChunkV;
     if (t == 0) ncand = 0;
     if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
@@ -504,7 +529,9 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     uint32_t pmask = 0, dmask = 0;
     if (v0 < a.n) {
         const uint32_t g = v0 >> kGroupShift;
-        if (a.pend_cur[g]) {
+        if (all_in) {
+            pmask = 0xFu;
+        } else if (a.pend_cur[g]) {
             pmask = 0xFu;
             if ((t & ((1u << (kGroupShift - 2)) - 1)) == 0) a.pend_cur[g] = 0;   // threads of a group share the byte
         }
@@ -534,9 +561,9 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c);
+        pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c, flag);
     }
-    flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
     flush_delays<kFault>(a);
 }
 
@@ -563,10 +590,8 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     __shared__ uint32_t ncand, ngrp;
     constexpr uint32_t kGroups = kChunkV >> kGroupShift, kGV = 1u << kGroupShift;
     const uint32_t t = threadIdx.x;
-    if (a.msgs3) {
-        if (blockIdx.x == 0 && t == 0) a.msgs3[a.mnext] = 0;
-        if (a.msgs3[a.mprev] == 0 && !(a.tick && *a.ost_total > 0)) return;
-    }
+    bool flag, all_in;
+    if (!round_counts(a, flag, all_in)) return;
     const uint32_t W = a.ell, base = blockIdx.x * kChunkV;
     const uint32_t nv = min(kChunkV, a.n - base);
     if (t < kChunkV / 32) {
@@ -578,7 +603,9 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     __syncthreads();
     if (t < kGroups && t * kGV < nv) {
         const uint32_t g = (base >> kGroupShift) + t;
-        if (a.pend_cur[g]) {
+        if (all_in) {
+            glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
+        } else if (a.pend_cur[g]) {
             a.pend_cur[g] = 0;
             glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
         }
@@ -624,9 +651,10 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i], lv = x >> 2;
-        pt_vertex_fast<kFault, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W]);
+        pt_vertex_fast<kFault, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W],
+                                     flag);
     }
-    flush_counters(c, a.stats, a.ost_total, a.msgs3 ? a.msgs3 + a.mcur : nullptr);
+    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
     flush_delays<kFault>(a);
 }
 
@@ -908,7 +936,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
     }
     if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
     if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);
-    if (nmsg && a.msgs3) a.msgs3[a.mprev] = 1;   // read by the next round
+    if (nmsg && a.mcnt) atomicAdd(&a.mcnt[a.m_s * 64], nmsg);   // read by the next round
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
 }
 

@@ -90,6 +90,7 @@ struct psim_handle {
     unsigned long long* scratch = nullptr;   // 1 counter
     int* ost_total = nullptr;                // device mirror of ost_cnt (the focused lane's)
     int* ost_total_base = nullptr;           // [kMaxLanes] allocation
+    uint32_t* mcnt_base = nullptr;           // [kMaxLanes][4][64] per-round message counts (PtArgs::mcnt)
     hipEvent_t ev[2 * kChunk] = {};
 
     uint32_t par = 0;          // inbox buffer the next round reads
@@ -482,17 +483,24 @@ int to_window(psim_handle* h) {
     return PSIM_OK;
 }
 
-// Early exit of no-op rounds (psim_step / psim_run on one GPU with the
-// slot-scatter engine): round R reads the messages emitted by round R-1 (or
-// the origin) from msgs3[(R-1) mod 3], adds its own into msgs3[R mod 3] and
-// clears msgs3[(R+1) mod 3]; lane-local, next to the lane's ost_total.
+// Per-round message counts (psim_step / psim_run on one GPU with the
+// slot-scatter engine; lane-local): round R adds its messages into slot R mod
+// 4 (64 shards), reads the counts of rounds R-1 and R-2 -- none sent -> the
+// round is a no-op; many sent -> the flag-free mode below -- and zeroes slot
+// R+1 mod 4.  A broadcast zeroes all four (psim_handle_broadcast), so the
+// rounds that read them were run back to back.
+// Flag-free rounds: a round that follows >= n/4 messages expects most
+// 16-vertex groups to receive words, so its senders write no group flags and
+// the next round reads every group's words with its coalesced sweep (the
+// same decision, taken from the same count, on both sides).
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     if (h->sh.world != 1 || h->bin.rec_c || h->dly) return;   // delays: a silent round may precede arrivals
-    a.msgs3 = h->ost_total + 1;
-    const uint32_t r = uint32_t(R % 3);
-    a.mprev = (r + 2) % 3;
-    a.mcur = r;
-    a.mnext = (r + 1) % 3;
+    a.mcnt = h->mcnt_base + 256 * size_t(h->cur_lane);
+    a.m_w = uint32_t(R % 4);
+    a.m_s = uint32_t((R + 3) % 4);
+    a.m_r = uint32_t((R + 2) % 4);
+    a.m_z = uint32_t((R + 1) % 4);
+    a.dense = std::max<uint32_t>(1u, h->n / 4);
 }
 
 // Round tags (psim_internal.h): a slot-scatter inbox word carries the round
@@ -669,7 +677,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
                 if (p) (void)hipFree(p);
             return fail(h, PSIM_ENOMEM, "delay ring of heartbeat lane %zu", L.size());
         }
-        l.ost_total = h->ost_total_base + 4 * L.size();     // {ost_total, msgs3[3]} per lane
+        l.ost_total = h->ost_total_base + 4 * L.size();     // the lane's ost_total (stride 4 ints)
         L.push_back(l);
         pick = (int)L.size() - 1;
         fresh = true;
@@ -946,6 +954,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             hipHostMalloc(&h->h_lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->ost_total_base, kMaxLanes * 4 * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->mcnt_base, kMaxLanes * 256 * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(h->mcnt_base, 0, kMaxLanes * 256 * sizeof(uint32_t)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) { rc = PSIM_EHIP; break; }
         h->ost_total = h->ost_total_base;
@@ -976,6 +986,7 @@ int psim_destroy(psim_handle* h) {
     if (h->h_lane_args) (void)hipHostFree(h->h_lane_args);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->ost_total_base) (void)hipFree(h->ost_total_base);
+    if (h->mcnt_base) (void)hipFree(h->mcnt_base);
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1221,6 +1232,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
     HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)));
+    HIPCHK(h, hipMemset(h->mcnt_base, 0, kMaxLanes * 256 * sizeof(uint32_t)));
     h->ost_total = h->ost_total_base;
     h->lanes.assign(1, psim_handle::Lane());
     h->cur_lane = 0;
@@ -1369,6 +1381,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
             // origin emits into the buffer the next round reads
             PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
             set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
+            if (a.mcnt) HIPCHK(h, hipMemsetAsync(a.mcnt, 0, 256 * sizeof(uint32_t), h->stream));
             a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
             a.root = lr;
             HIPCHK(h, launch_pt_origin(a, h->stream));

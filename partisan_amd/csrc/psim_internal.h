@@ -117,8 +117,13 @@ struct PtArgs {
     uint8_t* __restrict__ pend_nxt;
     uint8_t* __restrict__ ost;             // [n+3] 1 = outstanding rows exist
     int* ost_total;                        // device count of vertices with outstanding rows
-    int* msgs3;                            // [3] "round r mod 3 sent messages" flags (null: no early exit)
-    uint32_t mprev, mcur, mnext;           // this round r: (r-1) mod 3, r mod 3, (r+1) mod 3
+    // messages sent per round, [4 rounds][64 shards] (null: no early exit, group flags always written):
+    // round R adds its count into slot m_w = R mod 4, reads R-1 (m_s: no message -> no-op round; many ->
+    // this round's senders write no group flags) and R-2 (m_r: the last round wrote none -> every group
+    // is read), and zeroes m_z = (R+1) mod 4
+    uint32_t* mcnt;
+    uint32_t m_w, m_s, m_r, m_z;
+    uint32_t dense;                        // a round following >= dense messages runs flag-free
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
