@@ -345,47 +345,66 @@ constexpr uint32_t kFastDeg = 8;
 // kNoPeer) never carry a word, a mask bit or an outgoing message.
 // kLdsWords: the round kernel already gathered the vertex's live inbox words
 // into LDS (pt_round_ell_body) and `lw` points at them.
-template <bool kFault, bool kLdsWords = false>
-__device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
-                                               bool due, Ctr& c, const uint32_t* lw = nullptr, bool flag = true) {
-    uint32_t w[kFastDeg];
-    uint32_t any = 0;
+// kCap (>= deg): the register arrays' size.  The ELL kernel is instantiated
+// per row-width class (4 / 6 / 8) so a 5-wide HyParView row holds 6 slots in
+// registers, not 8: fewer VGPRs, more waves per SIMD to hide the chain.
+template <uint32_t kCap>
+struct VLoad {
+    uint4 st;
+    uint32_t aw;
+    uint32_t cl[kCap], rv[kCap];
+    bool rows;   // cl / rv were loaded
+};
+
+// `rows` false: the vertex's words hold only prunes and no row is due, so it
+// sends nothing and never tests a peer's liveness -- its peer ids and
+// reverse slots (2 x 4 B per slot, most of a sparse round's row bytes) are
+// not loaded.
+template <uint32_t kCap>
+__device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, VLoad<kCap>& L,
+                                      bool rows = true) {
+    L.aw = a.alive[(a.v_lo + v) >> 5];
+    L.st = a.vs[v];
+    L.rows = rows;
 #pragma unroll
-    for (uint32_t s = 0; s < kFastDeg; s++) {
-        if (kLdsWords) {
-            w[s] = (pend && s < deg) ? lw[s] : 0u;
-        } else {
-            w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
-            if (!live_word(w[s], a.ctag)) w[s] = 0u;   // stale: consumed in an earlier round
-        }
-        any |= w[s];
+    for (uint32_t s = 0; s < kCap; s++) {
+        L.cl[s] = (rows && s < deg) ? a.col[rs + s] : 0u;
+        L.rv[s] = (rows && s < deg) ? a.rev[rs + s] : 0u;
     }
-    pend = any != 0;
-    if (!pend && !due) return;
-    const uint32_t aw = a.alive[(a.v_lo + v) >> 5];
-    const uint4 st = a.vs[v];
-    uint32_t cl[kFastDeg], rv[kFastDeg];
-#pragma unroll
-    for (uint32_t s = 0; s < kFastDeg; s++) {
-        cl[s] = s < deg ? a.col[rs + s] : 0u;
-        rv[s] = s < deg ? a.rev[rs + s] : 0u;
-    }
+}
+
+// Does the FIFO of w hold a kind other than PSIM_MSG_PRUNE?  (3-bit fields:
+// non-zero and != 2.)
+__device__ __forceinline__ bool word_non_prune(uint32_t w) {
+    const uint32_t f = w & kFifoMask, g = f ^ 0x492u;   // 0x492: PRUNE in every field
+    return ((f | (f >> 1) | (f >> 2)) & (g | (g >> 1) | (g >> 2)) & 0x249u) != 0;
+}
+
+template <bool kFault, uint32_t kCap>
+__device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
+                                               const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, bool flag) {
+    const uint32_t aw = L.aw;
+    const uint4 st = L.st;
+    const uint32_t(&cl)[kCap] = L.cl;
+    const uint32_t(&rv)[kCap] = L.rv;
     if (!((aw >> ((a.v_lo + v) & 31)) & 1u)) return;   // a dead vertex receives nothing
     c.active++;
     VSt x;
     vst_load(a, v, st, x);
-    uint32_t r[kFastDeg];
+    uint32_t r[kCap];
 #pragma unroll
-    for (uint32_t s = 0; s < kFastDeg; s++) r[s] = w[s] ? pt_word(a, rs, s, w[s], x, c) : 0u;
+    for (uint32_t s = 0; s < kCap; s++) r[s] = w[s] ? pt_word(a, rs, s, w[s], x, c) : 0u;
     uint32_t ihave = 0;                                  // pt_ihave over the registers
     if (a.tick && x.outst) {
+        // rows held but not due cannot happen (ost mirrors them); still, never test id 0's liveness
 #pragma unroll
-        for (uint32_t s = 0; s < kFastDeg; s++)
-            if ((x.outst >> s) & 1u) ihave |= (bit_alive(a.alive, cl[s]) ? 1u : 0u) << s;
+        for (uint32_t s = 0; s < kCap; s++)
+            if ((x.outst >> s) & 1u)
+                ihave |= (bit_alive(a.alive, L.rows ? cl[s] : a.col[rs + s]) ? 1u : 0u) << s;
     }
     bool sent = false;
 #pragma unroll
-    for (uint32_t s = 0; s < kFastDeg; s++) {
+    for (uint32_t s = 0; s < kCap; s++) {
         if (s >= deg) break;
         const uint32_t wo = pt_out<true>(s, r[s], x, ihave, a.wtag, c);
         if (!wo) continue;
@@ -411,11 +430,38 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
         if (a.ell) {                                     // true degree: the non-padding slots
             d = 0;
 #pragma unroll
-            for (uint32_t s = 0; s < kFastDeg; s++) d += (s < deg && cl[s] != kNoPeer) ? 1u : 0u;
+            for (uint32_t s = 0; s < kCap; s++) d += (s < deg && cl[s] != kNoPeer) ? 1u : 0u;
         }
         c.degsum += d;
     }
     vst_store(a, v, st, x, c);
+}
+
+template <bool kFault, bool kLdsWords = false, uint32_t kCap = kFastDeg>
+__device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
+                                               bool due, Ctr& c, const uint32_t* lw = nullptr, bool flag = true) {
+    uint32_t w[kCap];
+    uint32_t any = 0;
+    bool rows = due;
+#pragma unroll
+    for (uint32_t s = 0; s < kCap; s++) {
+        if (kLdsWords) {
+            w[s] = (pend && s < deg) ? lw[s] : 0u;
+        } else {
+            w[s] = (pend && s < deg) ? a.in_cur[rs + s] : 0u;
+            if (!live_word(w[s], a.ctag)) w[s] = 0u;   // stale: consumed in an earlier round
+        }
+        any |= w[s];
+        rows |= word_non_prune(w[s]);
+    }
+    pend = any != 0;
+    if (!pend && !due) return;
+    VLoad<kCap> L;
+#ifdef PT_ROWS_ALWAYS
+    rows = true;
+#endif
+    vload(a, v, rs, deg, L, rows);
+    pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, flag);
 }
 
 template <bool kFault>
@@ -580,21 +626,31 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
 // threads, which then need one round trip (state, peer ids, reverse slots)
 // instead of a per-vertex dependent load of words that are mostly stale
 // (a flagged group typically has one or two receivers in the sparse rounds).
-template <bool kFault>
+// kEllChunk vertices per workgroup (kVpt per thread): the words buffer is
+// kEllChunk * W * 4 bytes of LDS, which is what bounds workgroups per CU.
+#ifndef PT_ELL_CHUNK
+#define PT_ELL_CHUNK 1024
+#endif
+constexpr uint32_t kEllChunk = PT_ELL_CHUNK;
+constexpr uint32_t kVpt = kEllChunk / kBlock;
+static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) <= 65536,
+              "ELL chunk: 1-8 vertices per thread, candidates fit 16 bits");
+
+template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
-    extern __shared__ uint32_t wbuf[];                 // [kChunkV * W] the chunk's live words (flagged groups)
-    __shared__ uint32_t actm[kChunkV / 32];            // vertices with live words
-    __shared__ uint32_t duem[kChunkV / 32];            // vertices holding outstanding rows on a tick round
-    __shared__ uint16_t cand[kChunkV];
-    __shared__ uint8_t glist[kChunkV >> kGroupShift];
+    extern __shared__ uint32_t wbuf[];                 // [kEllChunk * W] the chunk's live words (flagged groups)
+    __shared__ uint32_t actm[kEllChunk / 32];          // vertices with live words
+    __shared__ uint32_t duem[kEllChunk / 32];          // vertices holding outstanding rows on a tick round
+    __shared__ uint16_t cand[kEllChunk];
+    __shared__ uint8_t glist[kEllChunk >> kGroupShift];
     __shared__ uint32_t ncand, ngrp;
-    constexpr uint32_t kGroups = kChunkV >> kGroupShift, kGV = 1u << kGroupShift;
+    constexpr uint32_t kGroups = kEllChunk >> kGroupShift, kGV = 1u << kGroupShift;
     const uint32_t t = threadIdx.x;
     bool flag, all_in;
     if (!round_counts(a, flag, all_in)) return;
-    const uint32_t W = a.ell, base = blockIdx.x * kChunkV;
-    const uint32_t nv = min(kChunkV, a.n - base);
-    if (t < kChunkV / 32) {
+    const uint32_t W = a.ell, base = blockIdx.x * kEllChunk;
+    const uint32_t nv = min(kEllChunk, a.n - base);
+    if (t < kEllChunk / 32) {
         actm[t] = 0;
         duem[t] = 0;
     }
@@ -610,37 +666,71 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
         }
     }
-    if (a.tick && *a.ost_total > 0 && 4 * t < nv) {
-        uint32_t w;
-        const uint32_t v0 = base + 4 * t;
-        if (v0 + 4 <= a.n) w = *reinterpret_cast<const uint32_t*>(a.ost + v0);
-        else { w = 0; for (uint32_t i = 0; v0 + i < a.n; i++) w |= uint32_t(a.ost[v0 + i]) << (8 * i); }
+    if (a.tick && *a.ost_total > 0 && kVpt * t < nv) {
+        const uint32_t v0 = base + kVpt * t;
         uint32_t d = 0;
-        for (int i = 0; i < 4; i++) d |= ((w >> (8 * i)) & 0xFFu) ? (1u << i) : 0u;
-        if (d) atomicOr(&duem[(4 * t) >> 5], d << ((4 * t) & 31));
+        for (uint32_t i = 0; i < kVpt; i++)
+            if (v0 + i < a.n && a.ost[v0 + i]) d |= 1u << i;
+        if (d) atomicOr(&duem[(kVpt * t) >> 5], d << ((kVpt * t) & 31));
     }
     __syncthreads();
     const uint32_t ng = ngrp, gw = kGV * W;
     const uint32_t lim = nv * W;                        // chunk-local words that exist
-    for (uint32_t i = t; i < ng * gw; i += kBlock) {
-        const uint32_t lwi = glist[i / gw] * gw + i % gw;   // chunk-local word = local vertex * W + slot
-        if (lwi >= lim) continue;
-        uint32_t w = a.in_cur[base * W + lwi];
+    const uint32_t* src = a.in_cur + size_t(base) * W;
+    auto keep = [&](uint32_t lwi, uint32_t w) {          // chunk-local word = local vertex * W + slot
         if (!live_word(w, a.ctag)) w = 0u;
         wbuf[lwi] = w;
         if (w) {
             const uint32_t lv = lwi / W;
             atomicOr(&actm[lv >> 5], 1u << (lv & 31));
         }
+    };
+#ifndef PT_SCALAR_SWEEP
+    if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+        // A group's 16 W words start on a 16-byte boundary: read them as
+        // quads, kSweepU quads per thread in flight before any is used (the
+        // word-at-a-time loop waited out one load latency per word).
+        constexpr uint32_t kSweepU = 4;
+        const uint32_t gq = gw >> 2, nq = ng * gq;
+        for (uint32_t q0 = 0; q0 < nq; q0 += kBlock * kSweepU) {
+            uint4 wv[kSweepU];
+            uint32_t li[kSweepU];
+#pragma unroll
+            for (uint32_t k = 0; k < kSweepU; k++) {
+                const uint32_t q = q0 + k * kBlock + t;
+                li[k] = q < nq ? (uint32_t(glist[q / gq]) * gq + q % gq) * 4u : lim;
+                wv[k] = li[k] + 4 <= lim ? *reinterpret_cast<const uint4*>(src + li[k]) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kSweepU; k++) {
+                if (li[k] >= lim) continue;
+                if (li[k] + 4 <= lim) {
+                    keep(li[k], wv[k].x);
+                    keep(li[k] + 1, wv[k].y);
+                    keep(li[k] + 2, wv[k].z);
+                    keep(li[k] + 3, wv[k].w);
+                } else {
+                    for (uint32_t j = li[k]; j < lim; j++) keep(j, src[j]);   // the last chunk's tail
+                }
+            }
+        }
+    } else
+#endif
+    {
+        for (uint32_t i = t; i < ng * gw; i += kBlock) {
+            const uint32_t lwi = glist[i / gw] * gw + i % gw;
+            if (lwi < lim) keep(lwi, src[lwi]);
+        }
     }
     __syncthreads();
     {
-        const uint32_t v4 = 4 * t;
-        const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & 0xFu, dm = (duem[v4 >> 5] >> (v4 & 31)) & 0xFu;
+        constexpr uint32_t kMask = (1u << kVpt) - 1u;
+        const uint32_t v4 = kVpt * t;
+        const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & kMask, dm = (duem[v4 >> 5] >> (v4 & 31)) & kMask;
         const uint32_t m = am | dm;
         if (m) {
             uint32_t k = atomicAdd(&ncand, (uint32_t)__popc(m));
-            for (uint32_t i = 0; i < 4; i++)
+            for (uint32_t i = 0; i < kVpt; i++)
                 if (m & (1u << i)) cand[k++] = (uint16_t)(((v4 + i) << 2) | (((am >> i) & 1u) << 1) | ((dm >> i) & 1u));
         }
     }
@@ -649,18 +739,18 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     if (nc == 0) return;                                // uniform: idle chunk
     Ctr c;
     c.zero();
-    for (uint32_t i = t; i < nc; i += kBlock) {
+for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i], lv = x >> 2;
-        pt_vertex_fast<kFault, true>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W],
-                                     flag);
+        pt_vertex_fast<kFault, true, kCap>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c,
+                                           &wbuf[lv * W], flag);
     }
     flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
     flush_delays<kFault>(a);
 }
 
-template <bool kFault>
+template <bool kFault, uint32_t kCap>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_kernel(PtArgs a) {
-    pt_round_ell_body<kFault>(a);
+    pt_round_ell_body<kFault, kCap>(a);
 }
 
 // Multi-root rounds: one launch runs the round of every
@@ -672,9 +762,9 @@ __global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __
     pt_round_body<kFault>(args[blockIdx.y]);
 }
 
-template <bool kFault>
+template <bool kFault, uint32_t kCap>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs* __restrict__ args) {
-    pt_round_ell_body<kFault>(args[blockIdx.y]);
+    pt_round_ell_body<kFault, kCap>(args[blockIdx.y]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1145,6 +1235,7 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const
 }
 
 uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }
+uint32_t grid_ell(uint32_t n) { return (n + kEllChunk - 1) / kEllChunk; }
 
 uint32_t grid_for(uint32_t n) {
     uint32_t g = (n + kBlock - 1) / kBlock;
@@ -1162,11 +1253,12 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.ell) {
-        const size_t lds = size_t(kChunkV) * a.ell * 4;
-        if (a.omit || a.dly)
-            hipLaunchKernelGGL(pt_round_ell_kernel<true>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
-        else
-            hipLaunchKernelGGL(pt_round_ell_kernel<false>, dim3(grid_chunks(a.n)), dim3(kBlock), lds, s, a);
+        const size_t lds = size_t(kEllChunk) * a.ell * 4;
+        const bool f = a.omit || a.dly;
+        const auto k = a.ell <= 4 ? (f ? pt_round_ell_kernel<true, 4> : pt_round_ell_kernel<false, 4>)
+                     : a.ell <= 6 ? (f ? pt_round_ell_kernel<true, 6> : pt_round_ell_kernel<false, 6>)
+                                  : (f ? pt_round_ell_kernel<true, 8> : pt_round_ell_kernel<false, 8>);
+        hipLaunchKernelGGL(k, dim3(grid_ell(a.n)), dim3(kBlock), lds, s, a);
         return hipGetLastError();
     }
     if (a.omit || a.dly)
@@ -1179,11 +1271,13 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s) {
     const dim3 grid(grid_chunks(a0.n), nlanes);
     if (a0.ell) {
-        const size_t lds = size_t(kChunkV) * a0.ell * 4;
-        if (a0.omit || a0.dly)
-            hipLaunchKernelGGL(pt_round_ell_lanes_kernel<true>, grid, dim3(kBlock), lds, s, d_args);
-        else
-            hipLaunchKernelGGL(pt_round_ell_lanes_kernel<false>, grid, dim3(kBlock), lds, s, d_args);
+        const dim3 grid(grid_ell(a0.n), nlanes);
+        const size_t lds = size_t(kEllChunk) * a0.ell * 4;
+        const bool f = a0.omit || a0.dly;
+        const auto k = a0.ell <= 4 ? (f ? pt_round_ell_lanes_kernel<true, 4> : pt_round_ell_lanes_kernel<false, 4>)
+                     : a0.ell <= 6 ? (f ? pt_round_ell_lanes_kernel<true, 6> : pt_round_ell_lanes_kernel<false, 6>)
+                                   : (f ? pt_round_ell_lanes_kernel<true, 8> : pt_round_ell_lanes_kernel<false, 8>);
+        hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, d_args);
         return hipGetLastError();
     }
     if (a0.omit || a0.dly)

@@ -43,6 +43,26 @@ __global__ void scan128(const uint4* __restrict__ in, uint32_t n16, uint32_t* cn
     if (c) atomicAdd(cnt, c);
 }
 __global__ void empty_kernel() {}
+// a round kernel's idle workgroup: read the chunk's 64 group flags (1 load), barrier, exit
+__global__ __launch_bounds__(256) void idle_chunks(const uint8_t* __restrict__ pend, uint32_t* cnt) {
+    extern __shared__ uint32_t lds[];
+    __shared__ uint32_t any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    if (threadIdx.x < 64 && pend[blockIdx.x * 64 + threadIdx.x]) atomicOr(&any, 1u);
+    __syncthreads();
+    if (any) { lds[threadIdx.x] = any; __syncthreads(); if (threadIdx.x == 0) atomicAdd(cnt, lds[1]); }
+}
+// the same with a chain of three dependent loads before the flags (counts, scalar, flags)
+__global__ __launch_bounds__(256) void idle_chain(const uint8_t* __restrict__ pend, const uint32_t* c3, uint32_t* cnt) {
+    __shared__ uint32_t any, k;
+    if (threadIdx.x == 0) { any = 0; k = c3[blockIdx.x & 63]; }
+    __syncthreads();
+    const uint32_t kk = c3[64 + (k & 63)];
+    if (threadIdx.x < 64 && pend[blockIdx.x * 64 + threadIdx.x + (kk & 1)]) atomicOr(&any, 1u);
+    __syncthreads();
+    if (any && threadIdx.x == 0) atomicAdd(cnt, 1u);
+}
 
 int main() {
     const uint32_t E = 50'000'000, M = 26'000'000, N = 10'000'000;
@@ -66,6 +86,11 @@ int main() {
     };
     dim3 g(8192), blk(256);
     T("empty kernel", 0, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0); });
+    T("empty kernel 9766 x 256", 0, [&] { hipLaunchKernelGGL(empty_kernel, dim3(9766), dim3(256), 0, 0); });
+    T("empty kernel 9766 x 256, 20 KB LDS", 0, [&] { hipLaunchKernelGGL(empty_kernel, dim3(9766), dim3(256), 20480, 0); });
+    T("idle chunks 9766 (flags load, 20 KB LDS)", 0, [&] { hipLaunchKernelGGL(idle_chunks, dim3(9766), dim3(256), 20480, 0, flags, cnt); });
+    T("idle chunks 9766, 3-load chain", 0, [&] { hipLaunchKernelGGL(idle_chain, dim3(9766), dim3(256), 20480, 0, flags, buf, cnt); });
+    T("idle chunks 2442 x 4096 vertices", 0, [&] { hipLaunchKernelGGL(idle_chunks, dim3(2442), dim3(256), 20480, 0, flags, cnt); });
     T("copy 128-bit 200MB->200MB", 2.0 * E * 4, [&] { hipLaunchKernelGGL(copy128, g, blk, 0, 0, (uint4*)out, (const uint4*)buf, E / 4); });
     T("scatter 4B into 200MB (26M)", 4.0 * M, [&] { hipLaunchKernelGGL(scatter32, g, blk, 0, 0, buf, idx, M); });
     T("gather 4B from 200MB (26M)", 4.0 * M, [&] { hipLaunchKernelGGL(gather32, g, blk, 0, 0, out, buf, idx, M); });
