@@ -206,7 +206,10 @@ __device__ __forceinline__ void vst_load(const PtArgs& a, uint32_t v, const uint
 
 // handle_cast of the messages of one inbox word (slot s of the vertex whose
 // row starts at rs); returns the FIFO of replies sent back over s.
-__device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32_t s, uint32_t w, VSt& x, Ctr& c) {
+// `peer(q)`: the peer id of slot q (global col by default; the ELL kernel
+// passes the ids it already holds in registers).
+template <class Peer>
+__device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t s, uint32_t w, VSt& x, Ctr& c, Peer peer) {
     const uint32_t b = 1u << s;
     uint32_t f = w & kFifoMask;
     const uint32_t rnd = w >> kRoundShift;
@@ -234,7 +237,7 @@ __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32
                     while (add) {
                         const uint32_t q = __ffs(add) - 1;
                         add &= add - 1;
-                        x.live_delta += bit_alive(a.alive, a.col[rs + q]);
+                        x.live_delta += bit_alive(a.alive, peer(q));
                     }
                 }
             } else {                       // handle_broadcast(false) :843-850
@@ -259,7 +262,7 @@ __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32
         case PSIM_MSG_IGNORED:             // :592-598 ack_outstanding/5
             if (x.outst & b) {
                 x.outst &= ~b;
-                x.live_delta -= bit_alive(a.alive, a.col[rs + s]);
+                x.live_delta -= bit_alive(a.alive, peer(s));
             }
             break;
         case PSIM_MSG_GRAFT:               // :600-605 -> handle_graft/7 :880-906
@@ -279,6 +282,10 @@ __device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32
         }
     }
     return r;
+}
+
+__device__ __forceinline__ uint32_t pt_word(const PtArgs& a, uint32_t rs, uint32_t s, uint32_t w, VSt& x, Ctr& c) {
+    return pt_word(a, s, w, x, c, [&](uint32_t q) { return a.col[rs + q]; });
 }
 
 // lazy tick: send_lazy/0 (:992-1019), connected peers only, rows persist
@@ -366,6 +373,16 @@ __device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, 
     L.aw = a.alive[(a.v_lo + v) >> 5];
     L.st = a.vs[v];
     L.rows = rows;
+    if (a.ecol) {                // ELL packed rows: half the row bytes
+        const uint32_t W = a.ell;
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) {
+            const uint32_t p = (rows && s < deg) ? a.ecol[rs + s] : 0u;
+            L.cl[s] = p == kNoPeer ? kNoPeer : p >> 3;
+            L.rv[s] = p == kNoPeer ? 0u : (p >> 3) * W + (p & 7u);
+        }
+        return;
+    }
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         L.cl[s] = (rows && s < deg) ? a.col[rs + s] : 0u;
@@ -393,7 +410,13 @@ __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint
     vst_load(a, v, st, x);
     uint32_t r[kCap];
 #pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) r[s] = w[s] ? pt_word(a, rs, s, w[s], x, c) : 0u;
+    for (uint32_t s = 0; s < kCap; s++)
+        r[s] = w[s] ? pt_word(a, s, w[s], x, c, [&](uint32_t q) {   // ids from the registers (select chain)
+                   uint32_t id = 0;
+#pragma unroll
+                   for (uint32_t k = 0; k < kCap; k++) id = k == q ? cl[k] : id;
+                   return L.rows ? id : a.col[rs + q];
+               }) : 0u;
     uint32_t ihave = 0;                                  // pt_ihave over the registers
     if (a.tick && x.outst) {
         // rows held but not due cannot happen (ost mirrors them); still, never test id 0's liveness

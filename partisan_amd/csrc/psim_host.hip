@@ -55,6 +55,7 @@ struct psim_handle {
     uint32_t* rowp = nullptr;
     uint32_t* col = nullptr;
     uint32_t* rev = nullptr;
+    uint32_t* ecol = nullptr;       // ELL rows, n < 2^29: col << 3 | reverse slot (PtArgs::ecol)
     uint32_t* memb = nullptr;
     uint32_t* alive = nullptr;
     uint4* vs = nullptr;
@@ -279,11 +280,11 @@ void free_graph(psim_handle* h) {
         h->lanes.clear();
         h->cur_lane = 0;
     }
-    void* ptrs[] = {h->rowp, h->col, h->rev, h->memb, h->alive, h->vs, h->in[0], h->in[1],
+    void* ptrs[] = {h->rowp, h->col, h->rev, h->ecol, h->memb, h->alive, h->vs, h->in[0], h->in[1],
                     h->pend[0], h->pend[1], h->ost, h->dly, h->ring, h->pring};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    h->rowp = h->col = h->rev = h->memb = h->alive = nullptr;
+    h->rowp = h->col = h->rev = h->ecol = h->memb = h->alive = nullptr;
     h->vs = nullptr;
     h->in[0] = h->in[1] = nullptr;
     h->pend[0] = h->pend[1] = h->ost = nullptr;
@@ -356,6 +357,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.rowp = h->rowp;
     a.col = h->col;
     a.rev = h->rev;
+    a.ecol = h->ecol;
     a.memb = h->memb;
     a.alive = h->alive;
     a.vs = h->vs;
@@ -1133,6 +1135,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     // degree <= kEllMax, slot s of v is v*W + s (W = the maximum degree), so
     // the round kernel finds a vertex's inbox words without reading rowp
     uint32_t ell = 0;
+    std::vector<uint32_t> ep;
     if (W == 1 && !(h->cfg.flags & (PSIM_CFG_BINNED | PSIM_CFG_CSR))) {
         uint32_t mx = 0;
         for (uint32_t v = 0; v < nl; v++) mx = std::max(mx, rpl[v + 1] - rpl[v]);
@@ -1148,6 +1151,11 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
                 ce[uint64_t(v) * ell + (e - rpl[v])] = cl[e];
                 re[uint64_t(v) * ell + (e - rpl[v])] = u * ell + (rvl[e] - rpl[u]);
             }
+        if (nl < (1u << 29) - 1) {                         // packed rows for the ELL round kernel
+            ep.resize(Ed);
+            for (uint64_t e = 0; e < Ed; e++)
+                ep[e] = ce[e] == kNoPeer ? kNoPeer : (ce[e] << 3) | (re[e] - ce[e] * ell);
+        }
         cl_dev.swap(ce);
         rv_dev.swap(re);
     }
@@ -1182,6 +1190,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, Ed * 4) != hipSuccess ||
         alloc((void**)&h->rev, Ed * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl) * 4) != hipSuccess ||
+        (!ep.empty() && alloc((void**)&h->ecol, Ed * 4) != hipSuccess) ||
         alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
         (!binned && (alloc((void**)&h->in[0], Ed * 4) != hipSuccess || alloc((void**)&h->in[1], Ed * 4) != hipSuccess ||
                      alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess)) ||
@@ -1213,6 +1222,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     HIPCHK(h, hipMemcpy(h->rowp, rpl.data(), (size_t(nl) + 1) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->col, cl_up.data(), Ed * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->rev, rv_up.data(), Ed * 4, hipMemcpyHostToDevice));
+    if (!ep.empty()) HIPCHK(h, hipMemcpy(h->ecol, ep.data(), Ed * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->memb, mbl.data(), size_t(nl) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
     // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..

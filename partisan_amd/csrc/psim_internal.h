@@ -108,6 +108,8 @@ struct PtArgs {
     const uint32_t* __restrict__ rowp;     // [n+1] local slot row pointers
     const uint32_t* __restrict__ col;      // [E]   neighbour (global) id per slot (sorted in a row)
     const uint32_t* __restrict__ rev;      // [E]   global slot id of the reverse slot
+    const uint32_t* __restrict__ ecol;     // [n*W] ELL only: col << 3 | reverse slot s' (rev = col*W + s'),
+                                           //       kNoPeer for padding; null = read col / rev
     const uint32_t* __restrict__ memb;     // [n]   member mask = common_eagers
     const uint32_t* __restrict__ alive;    // [ceil(N/32)] bitmap over GLOBAL ids
     uint4* __restrict__ vs;                // [n]   state records
