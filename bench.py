@@ -17,9 +17,10 @@ scalar port of the reference modules) on a bounded sample of the same
 workload, rank 0 only.
 
 Multi-GPU (N > 1): the SAME 10M-peer overlay is vertex-sharded over the N
-GPUs (strong scaling); cross-shard records move every round
-with RCCL all-to-all over xGMI (torch.distributed backend "nccl");
---mode replicas runs N independent copies instead.
+GPUs (strong scaling; N = 1 is its one-shard case); cross-shard
+words move every round through libpsim's own RCCL communicator (grouped
+ncclSend / ncclRecv over xGMI); --mode replicas runs N independent copies
+instead (weak scaling).
 """
 import argparse
 import json
@@ -185,7 +186,7 @@ def main():
     if sharded:
         from partisan_amd.shard import ShardedPlumtree
         sp = ShardedPlumtree(rp, col, rank, world, device=local, backend=args.transport,
-                             lazy_tick_rounds=args.lazy_tick_rounds)
+                             lazy_tick_rounds=args.lazy_tick_rounds, csr=args.csr)
         sim = sp.sim
     else:
         sp = None
@@ -246,9 +247,10 @@ def main():
     avg_launch_ms = round_ms / max(1, counted)
     achieved_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
 
+    # ELL rows (every degree of the whole overlay <= 8) run the sweep kernel
+    max_deg = int(max_over_ranks(pg, float(sim.max_degree())))
+    kernel = "pt_round_kernel" if (args.csr or max_deg > 8) else "pt_round_ell_kernel"
     if rank == 0:
-        # ELL rows (one GPU, every degree <= 8) run the sweep kernel
-        kernel = "pt_round_kernel" if (sharded or args.csr or sim.max_degree() > 8) else "pt_round_ell_kernel"
         traffic = None
         try:
             with open(args.traffic_json) as f:
@@ -266,7 +268,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": step_s * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
+            "scaling": "weak" if args.mode == "replicas" else "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",

@@ -61,11 +61,14 @@ def gloo_transport():
 
 
 class ShardedPlumtree:
-    def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None):
+    def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None,
+                 csr=False):
+        """csr: keep CSR slot rows (PSIM_CFG_CSR) instead of the ELL rows every
+        shard uses when the overlay's widest row has <= 8 slots."""
         self.rank, self.world, self.backend = rank, world, backend
         self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
-        self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world)
+        self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world, csr=csr)
         self._h = self.sim._h
         self.last_exchange = {}
         self.exchange_total = {}      # psim_exchange_stats summed over runs (this rank)

@@ -39,7 +39,7 @@ def _init(rank, world, port):
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-def _gpu_worker(rank, world, port, n, seed, L, transport, q):
+def _gpu_worker(rank, world, port, n, seed, L, transport, csr, q):
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -48,7 +48,8 @@ def _gpu_worker(rank, world, port, n, seed, L, transport, q):
         from partisan_amd.shard import ShardedPlumtree
         import pyoracle as O
         rp, col = pa.overlay.random_regular(n, 5, seed)
-        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L, transport=transport)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L, transport=transport,
+                             csr=csr)
         orc = O.Plumtree(rp, col, L)
         sim = sp.sim
         root = 7
@@ -108,12 +109,13 @@ def run_world(target, world, *args, timeout=600):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["callback", "torch"])
+@pytest.mark.parametrize("transport,csr", [("callback", False), ("torch", False), ("callback", True)])
 @pytest.mark.parametrize("world,n,seed,L", [(2, 3000, 1, 1), (4, 5000, 2, 2)])
-def test_sharded_matches_oracle(world, n, seed, L, transport):
+def test_sharded_matches_oracle(world, n, seed, L, transport, csr):
     """callback: psim_shard_run's in-library loop (exchange through the
-    psim_transport hook, gloo); torch: the split-phase ABI driven from Python."""
-    res = run_world(_gpu_worker, world, n, seed, L, transport)
+    psim_transport hook, gloo); torch: the split-phase ABI driven from Python.
+    Shards hold ELL rows (global slot ids v * W + s) unless csr."""
+    res = run_world(_gpu_worker, world, n, seed, L, transport, csr)
     for r in range(world):
         assert res[r] == "ok", res[r]
 

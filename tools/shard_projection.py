@@ -35,13 +35,14 @@ def main():
     p.add_argument("--seed", type=int, default=0x5EED0001)
     p.add_argument("--xgmi-gbps", type=float, default=7 * 153.0)
     p.add_argument("--floods", type=int, default=3)
+    p.add_argument("--csr", action="store_true", help="CSR slot rows instead of the ELL rows shards load by default")
     a = p.parse_args()
     W, n = a.world, a.n
     dev = torch.device("cuda", 0)
     rp, col = pa.overlay.random_regular(n, a.peers, a.seed)
     sims, base, rbase, send, recv = [], [], [], [], []
     for r in range(W):
-        s = pa.Simulator(lazy_tick_rounds=1, device=0, rank=r, world=W, csr=True)
+        s = pa.Simulator(lazy_tick_rounds=1, device=0, rank=r, world=W, csr=a.csr)
         s.load_overlay(rp, col)
         b = (C.c_uint64 * (W + 1))()
         check(lib().psim_shard_layout(s._h, b, W), s._h)
@@ -103,7 +104,7 @@ def main():
     ksum = [sum(r["kernel_ms"][i] for r in last) for i in range(W)]
     xms = len(last) * max(fabric) / (a.xgmi_gbps * 1e6)
     out = {
-        "n": n, "world": W, "rounds": len(last), "rows": "csr",
+        "n": n, "world": W, "rounds": len(last), "rows": "csr" if a.csr else "ell",
         "per_shard_vertices": [s.n for s in sims],
         "kernel_ms_per_flood_max_over_shards": round(kmax, 4),
         "kernel_ms_per_flood_each_shard": [round(x, 4) for x in ksum],
