@@ -157,9 +157,52 @@ __device__ __forceinline__ unsigned long long* delay_hist() {
     return dh;
 }
 
+// Group flag of receiver group g (mark: 0 = none, the next round reads every
+// group; 1 = flag; 2 = flag + worklist).  Mode 2 claims the flag with an
+// atomicOr on its 4-byte word; the sender that set it appends g to this
+// workgroup's LDS list (`wl`, flushed by wl_flush) or, past its capacity or
+// without one, straight to the round's worklist shard.  The flags stay
+// authoritative: a reader takes the list only when it is complete.
+constexpr uint32_t kWlLds = 256;
+struct WlLds {
+    uint32_t n;
+    uint32_t g[kWlLds];
+};
+
+__device__ __forceinline__ void wl_push_global(const PtArgs& a, uint32_t g) {
+    const uint32_t sh = blockIdx.x & 63u;
+    const uint32_t pos = atomicAdd(&a.wlcnt[a.m_w * 64 + sh], 1u);
+    if (pos < a.wl_cap) a.wl_nxt[size_t(sh) * a.wl_cap + pos] = g;
+}
+
+__device__ __forceinline__ void mark_group(const PtArgs& a, uint32_t g, uint32_t mark, WlLds* wl) {
+    if (mark == 1) {
+        a.pend_nxt[g] = 1;
+    } else if (mark == 2) {
+        const uint32_t bit = 1u << (8 * (g & 3u));
+        if (atomicOr(reinterpret_cast<uint32_t*>(a.pend_nxt) + (g >> 2), bit) & bit) return;   // already listed
+        const uint32_t k = wl ? atomicAdd(&wl->n, 1u) : kWlLds;
+        if (k < kWlLds) wl->g[k] = g;
+        else wl_push_global(a, g);
+    }
+}
+
+// End of a mark-2 round in a workgroup: its LDS list into the worklist shard
+// (one atomicAdd per workgroup).  Uniform call; contains barriers.
+__device__ __forceinline__ void wl_flush(const PtArgs& a, WlLds* wl) {
+    __shared__ uint32_t wbase;
+    __syncthreads();
+    const uint32_t k = min(wl->n, kWlLds), sh = blockIdx.x & 63u;
+    if (threadIdx.x == 0) wbase = k ? atomicAdd(&a.wlcnt[a.m_w * 64 + sh], k) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < k; i += kBlock)
+        if (wbase + i < a.wl_cap) a.wl_nxt[size_t(sh) * a.wl_cap + wbase + i] = wl->g[i];
+}
+
 template <bool kFault = true>
 __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32_t w,
-                                             unsigned long long* hist = nullptr, bool flag = true) {
+                                             unsigned long long* hist = nullptr, uint32_t mark = 1,
+                                             WlLds* wl = nullptr) {
     if (kFault && omitted(a, e)) return;
     const uint32_t u = a.col[e] - a.v_lo;
     if (u < a.n) {
@@ -172,7 +215,7 @@ __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32
 #else
         a.in_nxt[a.rev[e] - a.slot_base] = w;
 #endif
-        if (flag) a.pend_nxt[u >> kGroupShift] = 1;
+        mark_group(a, u >> kGroupShift, mark, wl);
     } else {
         a.stage[e] = w;
     }
@@ -399,7 +442,8 @@ __device__ __forceinline__ bool word_non_prune(uint32_t w) {
 
 template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
-                                               const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, bool flag) {
+                                               const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, uint32_t mark,
+                                               WlLds* wl) {
     const uint32_t aw = L.aw;
     const uint4 st = L.st;
     const uint32_t(&cl)[kCap] = L.cl;
@@ -442,7 +486,7 @@ __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint
 #else
             a.in_nxt[rv[s] - a.slot_base] = wo;
 #endif
-            if (flag) a.pend_nxt[u >> kGroupShift] = 1;
+            mark_group(a, u >> kGroupShift, mark, wl);
         } else {
             a.stage[rs + s] = wo;
         }
@@ -462,7 +506,8 @@ __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint
 
 template <bool kFault, bool kLdsWords = false, uint32_t kCap = kFastDeg>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
-                                               bool due, Ctr& c, const uint32_t* lw = nullptr, bool flag = true) {
+                                               bool due, Ctr& c, const uint32_t* lw = nullptr, uint32_t mark = 1,
+                                               WlLds* wl = nullptr) {
     uint32_t w[kCap];
     uint32_t any = 0;
     bool rows = due;
@@ -484,7 +529,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
     rows = true;
 #endif
     vload(a, v, rs, deg, L, rows);
-    pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, flag);
+    pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, mark, wl);
 }
 
 template <bool kFault>
@@ -499,16 +544,16 @@ __device__ __forceinline__ void flush_delays(const PtArgs& a) {
 
 template <bool kFault>
 __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend, bool due, uint16_t* rep,
-                                          Ctr& c, bool flag) {
+                                          Ctr& c, uint32_t mark) {
     if (a.ell) {
-        pt_vertex_fast<kFault>(a, v, v * a.ell, a.ell, pend, due, c, nullptr, flag);
+        pt_vertex_fast<kFault>(a, v, v * a.ell, a.ell, pend, due, c, nullptr, mark);
         return;
     }
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
 #ifndef PT_NO_FAST
     if (deg <= kFastDeg) {
-        pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c, nullptr, flag);
+        pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c, nullptr, mark);
         return;
     }
 #endif
@@ -536,7 +581,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
-        deliver_word<kFault>(a, rs + s, w, nullptr, flag);
+        deliver_word<kFault>(a, rs + s, w, nullptr, mark);
         sent = true;
     }
     if (sent) {
@@ -553,29 +598,56 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
 // The counts of the last two rounds (PtArgs::mcnt): wave 0 sums the 64
 // shards; block 0 zeroes the slot of the round after next.  Returns false
 // when the round is a no-op (nothing was sent, no row is due).
-__device__ __forceinline__ bool round_counts(const PtArgs& a, bool& flag_out, bool& all_in) {
-    __shared__ uint32_t cnt2[2];
-    flag_out = true;
-    all_in = false;
+struct RoundMode {
+    uint32_t mark;   // this round's senders: 0 = no group flags, 1 = flags, 2 = flags + worklist
+    bool all_in;     // the last round wrote no flags: every group is read
+    bool list_in;    // the last round's worklist is complete: read its groups, not the flags
+};
+
+// wl_off (ELL kernel): [65] prefix of the worklist shards this round reads.
+__device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint32_t* wl_off = nullptr) {
+    __shared__ uint32_t cnt2[3];
+    m.mark = 1;
+    m.all_in = m.list_in = false;
     if (!a.mcnt) return true;
     const uint32_t t = threadIdx.x;
     if (t < 64) {
         uint32_t c1 = a.mcnt[a.m_s * 64 + t], c2 = a.mcnt[a.m_r * 64 + t];
+        uint32_t l = a.wl_cur ? a.wlcnt[a.m_s * 64 + t] : 0u;
+        const bool ovf = __ballot(l > a.wl_cap) != 0ull;   // a shard overflowed: the flags are read
+        l = min(l, a.wl_cap);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(l, off, 64);
+            if (t >= (uint32_t)off) l += y;
+        }
+        if (wl_off) {
+            wl_off[t + 1] = l;
+            if (t == 0) wl_off[0] = 0;
+        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             c1 += __shfl_xor(c1, off, 64);
             c2 += __shfl_xor(c2, off, 64);
         }
-        if (t == 0) { cnt2[0] = c1; cnt2[1] = c2; }
-        if (blockIdx.x == 0) a.mcnt[a.m_z * 64 + t] = 0;   // the round after next starts empty
+        if (t == 0) { cnt2[0] = c1; cnt2[1] = c2; cnt2[2] = ovf; }
+        if (blockIdx.x == 0) {                            // the round after next starts empty
+            a.mcnt[a.m_z * 64 + t] = 0;
+            if (a.wl_cur) a.wlcnt[a.m_z * 64 + t] = 0;
+        }
     }
     __syncthreads();
     const uint32_t prev = cnt2[0], prev2 = cnt2[1];
+    const bool rows_due = a.tick && *a.ost_total > 0;
     // nothing was sent last round and no row is due: every vertex is idle
     // (no inbox flag can be set), so the whole round is a no-op
-    if (prev == 0 && !(a.tick && *a.ost_total > 0)) return false;
-    flag_out = prev < a.dense;       // many senders expected: no group flags this round
-    all_in = prev2 >= a.dense;       // the last round wrote none: every group is read
+    if (prev == 0 && !rows_due) return false;
+    // many senders expected: no group flags this round; few: flags + worklist
+    m.mark = prev >= a.dense ? 0u : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
+    m.all_in = prev2 >= a.dense;                       // the last round wrote none: every group is read
+    // the last round's senders listed every group they flagged (the same
+    // test on the same count) and no row is due: only the listed groups
+    m.list_in = wl_off && a.wl_cur && prev2 < a.wl_thr && !cnt2[2] && !rows_due;
     return true;
 }
 
@@ -588,8 +660,9 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     static_assert(kChunkV == 4 * kBlock && (kChunkV << 2) <= 65536, "candidate encoding");
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
-    bool flag, all_in;
-    if (!round_counts(a, flag, all_in)) return;
+    RoundMode md;
+    if (!round_counts(a, md)) return;
+    const bool all_in = md.all_in;
     const uint32_t base = blockIdx.x * kChunkV;
     if (t == 0) ncand = 0;
     if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
@@ -630,7 +703,7 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     c.zero();
     for (uint32_t i = t; i < nc; i += kBlock) {
         const uint32_t x = cand[i];
-        pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c, flag);
+        pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c, md.mark);
     }
     flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
     flush_delays<kFault>(a);
@@ -661,112 +734,153 @@ static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) 
 
 template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
-    extern __shared__ uint32_t wbuf[];                 // [kEllChunk * W] the chunk's live words (flagged groups)
+    extern __shared__ uint32_t wbuf[];                 // [kEllChunk * W] the live words of the groups read
     __shared__ uint32_t actm[kEllChunk / 32];          // vertices with live words
     __shared__ uint32_t duem[kEllChunk / 32];          // vertices holding outstanding rows on a tick round
     __shared__ uint16_t cand[kEllChunk];
-    __shared__ uint8_t glist[kEllChunk >> kGroupShift];
+    __shared__ uint8_t glist[kEllChunk >> kGroupShift];   // flag mode: chunk-local groups to read
+    __shared__ uint32_t gl[kEllChunk >> kGroupShift];     // list mode: global groups to read
+    __shared__ uint32_t wl_off[65];
+    __shared__ WlLds wl;
     __shared__ uint32_t ncand, ngrp;
     constexpr uint32_t kGroups = kEllChunk >> kGroupShift, kGV = 1u << kGroupShift;
     const uint32_t t = threadIdx.x;
-    bool flag, all_in;
-    if (!round_counts(a, flag, all_in)) return;
-    const uint32_t W = a.ell, base = blockIdx.x * kEllChunk;
-    const uint32_t nv = min(kEllChunk, a.n - base);
-    if (t < kEllChunk / 32) {
-        actm[t] = 0;
-        duem[t] = 0;
-    }
-    if (t == 0) ncand = ngrp = 0;
+    RoundMode md;
+    if (!round_counts(a, md, wl_off)) return;
+    const uint32_t W = a.ell;
+    const bool list = md.list_in;
+    // The grid is the chip's resident workgroups (PtArgs::ell_grid), each
+    // looping over chunks c = blockIdx.x, + gridDim.x, ...: a chunk is 1024
+    // consecutive vertices, or in list mode (sparse rounds) entries [64 c,
+    // 64 c + 64) of the groups the last round listed -- so a sparse round
+    // costs one dispatch of the resident grid, not of n / 1024 workgroups
+    // whose LDS must be allocated before each can find it has nothing to do.
+    const uint32_t nchunks = list ? (wl_off[64] + kGroups - 1) / kGroups : (a.n + kEllChunk - 1) / kEllChunk;
+    if (blockIdx.x >= nchunks) return;                 // uniform
+    if (t == 0) wl.n = 0;
     if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
-    __syncthreads();
-    if (t < kGroups && t * kGV < nv) {
-        const uint32_t g = (base >> kGroupShift) + t;
-        if (all_in) {
-            glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
-        } else if (a.pend_cur[g]) {
-            a.pend_cur[g] = 0;
-            glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
-        }
-    }
-    if (a.tick && *a.ost_total > 0 && kVpt * t < nv) {
-        const uint32_t v0 = base + kVpt * t;
-        uint32_t d = 0;
-        for (uint32_t i = 0; i < kVpt; i++)
-            if (v0 + i < a.n && a.ost[v0 + i]) d |= 1u << i;
-        if (d) atomicOr(&duem[(kVpt * t) >> 5], d << ((kVpt * t) & 31));
-    }
-    __syncthreads();
-    const uint32_t ng = ngrp, gw = kGV * W;
-    const uint32_t lim = nv * W;                        // chunk-local words that exist
-    const uint32_t* src = a.in_cur + size_t(base) * W;
-    auto keep = [&](uint32_t lwi, uint32_t w) {          // chunk-local word = local vertex * W + slot
-        if (!live_word(w, a.ctag)) w = 0u;
-        wbuf[lwi] = w;
-        if (w) {
-            const uint32_t lv = lwi / W;
-            atomicOr(&actm[lv >> 5], 1u << (lv & 31));
-        }
-    };
-#ifndef PT_SCALAR_SWEEP
-    if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
-        // A group's 16 W words start on a 16-byte boundary: read them as
-        // quads, kSweepU quads per thread in flight before any is used (the
-        // word-at-a-time loop waited out one load latency per word).
-        constexpr uint32_t kSweepU = 4;
-        const uint32_t gq = gw >> 2, nq = ng * gq;
-        for (uint32_t q0 = 0; q0 < nq; q0 += kBlock * kSweepU) {
-            uint4 wv[kSweepU];
-            uint32_t li[kSweepU];
-#pragma unroll
-            for (uint32_t k = 0; k < kSweepU; k++) {
-                const uint32_t q = q0 + k * kBlock + t;
-                li[k] = q < nq ? (uint32_t(glist[q / gq]) * gq + q % gq) * 4u : lim;
-                wv[k] = li[k] + 4 <= lim ? *reinterpret_cast<const uint4*>(src + li[k]) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kSweepU; k++) {
-                if (li[k] >= lim) continue;
-                if (li[k] + 4 <= lim) {
-                    keep(li[k], wv[k].x);
-                    keep(li[k] + 1, wv[k].y);
-                    keep(li[k] + 2, wv[k].z);
-                    keep(li[k] + 3, wv[k].w);
-                } else {
-                    for (uint32_t j = li[k]; j < lim; j++) keep(j, src[j]);   // the last chunk's tail
-                }
-            }
-        }
-    } else
-#endif
-    {
-        for (uint32_t i = t; i < ng * gw; i += kBlock) {
-            const uint32_t lwi = glist[i / gw] * gw + i % gw;
-            if (lwi < lim) keep(lwi, src[lwi]);
-        }
-    }
-    __syncthreads();
-    {
-        constexpr uint32_t kMask = (1u << kVpt) - 1u;
-        const uint32_t v4 = kVpt * t;
-        const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & kMask, dm = (duem[v4 >> 5] >> (v4 & 31)) & kMask;
-        const uint32_t m = am | dm;
-        if (m) {
-            uint32_t k = atomicAdd(&ncand, (uint32_t)__popc(m));
-            for (uint32_t i = 0; i < kVpt; i++)
-                if (m & (1u << i)) cand[k++] = (uint16_t)(((v4 + i) << 2) | (((am >> i) & 1u) << 1) | ((dm >> i) & 1u));
-        }
-    }
-    __syncthreads();
-    const uint32_t nc = ncand;
-    if (nc == 0) return;                                // uniform: idle chunk
     Ctr c;
     c.zero();
-for (uint32_t i = t; i < nc; i += kBlock) {
-        const uint32_t x = cand[i], lv = x >> 2;
-        pt_vertex_fast<kFault, true, kCap>(a, base + lv, (base + lv) * W, W, (x >> 1) & 1u, x & 1u, c,
-                                           &wbuf[lv * W], flag);
+    const uint32_t nW = a.n * W;                       // words that exist
+    const uint32_t gw = kGV * W;
+    for (uint32_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const uint32_t base = ch * kEllChunk;
+        const uint32_t nv = list ? 0u : min(kEllChunk, a.n - base);
+        if (t < kEllChunk / 32) {
+            actm[t] = 0;
+            duem[t] = 0;
+        }
+        if (t == 0) ncand = ngrp = 0;
+        __syncthreads();
+        if (list) {
+            const uint32_t idx = ch * kGroups + t;
+            if (t < kGroups && idx < wl_off[64]) {
+                uint32_t lo = 0, hi = 64;              // shard: wl_off[lo] <= idx < wl_off[lo + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (wl_off[mid] <= idx) lo = mid; else hi = mid;
+                }
+                const uint32_t g = a.wl_cur[size_t(lo) * a.wl_cap + (idx - wl_off[lo])];
+                gl[t] = g;
+                a.pend_cur[g] = 0;
+            }
+            if (t == 0) ngrp = min(kGroups, wl_off[64] - ch * kGroups);
+        } else {
+            if (t < kGroups && t * kGV < nv) {
+                const uint32_t g = (base >> kGroupShift) + t;
+                if (md.all_in) {
+                    glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
+                } else if (a.pend_cur[g]) {
+                    a.pend_cur[g] = 0;
+                    glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
+                }
+            }
+            if (a.tick && *a.ost_total > 0 && kVpt * t < nv) {
+                const uint32_t v0 = base + kVpt * t;
+                uint32_t d = 0;
+                for (uint32_t i = 0; i < kVpt; i++)
+                    if (v0 + i < a.n && a.ost[v0 + i]) d |= 1u << i;
+                if (d) atomicOr(&duem[(kVpt * t) >> 5], d << ((kVpt * t) & 31));
+            }
+        }
+        __syncthreads();
+        const uint32_t ng = ngrp;
+        // group slot i of this chunk: LDS words at pos(i) * gw, first vertex gv(i)
+        auto pos = [&](uint32_t i) -> uint32_t { return list ? i : uint32_t(glist[i]); };
+        auto gv = [&](uint32_t i) -> uint32_t {
+            return list ? gl[i] << kGroupShift : base + (uint32_t(glist[i]) << kGroupShift);
+        };
+        auto keep = [&](uint32_t lwi, uint32_t w) {      // LDS word = group slot vertex * W + slot
+            if (!live_word(w, a.ctag)) w = 0u;
+            wbuf[lwi] = w;
+            if (w) {
+                const uint32_t lv = lwi / W;
+                atomicOr(&actm[lv >> 5], 1u << (lv & 31));
+            }
+        };
+#ifndef PT_SCALAR_SWEEP
+        if ((reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0) {   // group g's words start at 64 W g bytes
+            // A group's 16 W words start on a 16-byte boundary: read them as
+            // quads, kSweepU quads per thread in flight before any is used (the
+            // word-at-a-time loop waited out one load latency per word).
+            constexpr uint32_t kSweepU = 4;
+            const uint32_t gq = gw >> 2, nq = ng * gq;
+            for (uint32_t q0 = 0; q0 < nq; q0 += kBlock * kSweepU) {
+                uint4 wv[kSweepU];
+                uint32_t li[kSweepU], gi[kSweepU];
+#pragma unroll
+                for (uint32_t k = 0; k < kSweepU; k++) {
+                    const uint32_t q = q0 + k * kBlock + t;
+                    const uint32_t i = q / gq, r = (q % gq) * 4u;
+                    li[k] = q < nq ? pos(i) * gw + r : 0xFFFFFFFFu;
+                    gi[k] = q < nq ? gv(i) * W + r : nW;
+                    wv[k] = gi[k] + 4 <= nW ? *reinterpret_cast<const uint4*>(a.in_cur + gi[k])
+                                            : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kSweepU; k++) {
+                    if (gi[k] >= nW) continue;
+                    if (gi[k] + 4 <= nW) {
+                        keep(li[k], wv[k].x);
+                        keep(li[k] + 1, wv[k].y);
+                        keep(li[k] + 2, wv[k].z);
+                        keep(li[k] + 3, wv[k].w);
+                    } else {
+                        for (uint32_t j = 0; gi[k] + j < nW; j++) keep(li[k] + j, a.in_cur[gi[k] + j]);   // the tail
+                    }
+                }
+            }
+        } else
+#endif
+        {
+            for (uint32_t q = t; q < ng * gw; q += kBlock) {
+                const uint32_t i = q / gw, r = q % gw;
+                if (gv(i) * W + r < nW) keep(pos(i) * gw + r, a.in_cur[gv(i) * W + r]);
+            }
+        }
+        __syncthreads();
+        {
+            constexpr uint32_t kMask = (1u << kVpt) - 1u;
+            const uint32_t v4 = kVpt * t;
+            const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & kMask, dm = (duem[v4 >> 5] >> (v4 & 31)) & kMask;
+            const uint32_t m = am | dm;
+            if (m) {
+                uint32_t k = atomicAdd(&ncand, (uint32_t)__popc(m));
+                for (uint32_t i = 0; i < kVpt; i++)
+                    if (m & (1u << i))
+                        cand[k++] = (uint16_t)(((v4 + i) << 2) | (((am >> i) & 1u) << 1) | ((dm >> i) & 1u));
+            }
+        }
+        __syncthreads();
+        const uint32_t nc = ncand;
+        for (uint32_t i = t; i < nc; i += kBlock) {
+            const uint32_t x = cand[i], lv = x >> 2;
+            const uint32_t v = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
+            pt_vertex_fast<kFault, true, kCap>(a, v, v * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W], md.mark, &wl);
+        }
+        __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
     }
+    if (md.mark == 2) wl_flush(a, &wl);
     flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
     flush_delays<kFault>(a);
 }
@@ -1010,6 +1124,8 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
 __global__ void pt_origin_kernel(PtArgs a) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint32_t v = a.root;   // local index of the origin (only its owner launches this)
+    PtArgs ao = a;               // listed groups count as the round the next round reads as previous
+    ao.m_w = a.m_s;
     const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
     const uint32_t deg = a.ell ? a.ell : a.rowp[v + 1] - rs;   // ELL padding: no mask bits
     const uint4 st = a.vs[v];
@@ -1031,7 +1147,8 @@ __global__ void pt_origin_kernel(PtArgs a) {
                 a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] =
                     make_uint2(a.rev[e], PSIM_MSG_BROADCAST | (a.wtag << kTagShift));
             } else {
-                deliver_word(a, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift), a.dhist);  // Round 0
+                deliver_word(ao, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift), a.dhist,  // Round 0
+                             a.wl_nxt ? 2u : 1u);
             }
             nmsg++;
         }
@@ -1112,7 +1229,7 @@ __global__ __launch_bounds__(kBlock) void pt_hash_words_kernel(PtArgs a, unsigne
         const uint32_t w = a.in_cur[i];
         if (!live_word(w, a.ctag)) continue;
         const unsigned long long e = a.ell ? a.rowp[i / a.ell] + i % a.ell : i;   // ELL -> CSR slot id
-        sum += mix64(((a.slot_base + e) << 32) | abi_word(w));
+        sum += mix64(((a.abi_slot_base + e) << 32) | abi_word(w));
     }
     sum = wave_sum(sum);
     if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&out[1], sum);
@@ -1175,10 +1292,15 @@ __global__ void pt_scrub_tail_kernel(uint32_t* __restrict__ w, unsigned long lon
 // entries of ONE destination's remote-slot list (blk = {rank, start, len}),
 // so it reserves its run with a single atomicAdd.  Record order inside a
 // region is irrelevant: every receiver slot has one writer per round.
+// send_base null (the in-library record exchange of sparse rounds): region d
+// starts at record (d - [d > self]) * cap and holds at most cap records; a
+// region that would overflow is reported (S_OVERFLOW bit 0x200), never
+// written past.
 __global__ __launch_bounds__(kBlock) void pt_compact_kernel(PtArgs a, const uint32_t* __restrict__ rem,
                                                             const uint4* __restrict__ blk,
                                                             const uint32_t* __restrict__ send_base,
-                                                            uint32_t* __restrict__ cursor, uint2* __restrict__ out) {
+                                                            uint32_t* __restrict__ cursor, uint2* __restrict__ out,
+                                                            uint32_t cap, uint32_t self) {
     __shared__ uint32_t wsum_[kBlock / 64];
     __shared__ uint32_t base;
     const uint4 b = blk[blockIdx.x];
@@ -1210,12 +1332,19 @@ __global__ __launch_bounds__(kBlock) void pt_compact_kernel(PtArgs a, const uint
         if (i < (int)wv) pre += wsum_[i];
         tot += wsum_[i];
     }
-    if (t == 0) base = tot ? atomicAdd(&cursor[b.x], tot) : 0u;
+    if (t == 0) {
+        base = tot ? atomicAdd(&cursor[b.x], tot) : 0u;
+        if (tot && base + tot > cap) atomicOr(&a.stats[S_OVERFLOW], 0x200ull);
+    }
     __syncthreads();
-    uint32_t pos = send_base[b.x] + base + pre + x - cnt;
+    const uint32_t rbase = send_base ? send_base[b.x] : (b.x - (b.x > self ? 1u : 0u)) * cap;
+    uint32_t pos = base + pre + x - cnt;                // within the region
 #pragma unroll
     for (int i = 0; i < 4; i++)
-        if (w[i]) out[pos++] = make_uint2(a.rev[e[i]], w[i]);
+        if (w[i]) {
+            if (pos < cap) out[rbase + pos] = make_uint2(a.rev[e[i]], w[i]);
+            pos++;
+        }
 }
 
 // Scatter records received from other shards into the local receiver slots.
@@ -1224,6 +1353,7 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= nrec) return;
     const uint2 r = rec[i];
+    if (!r.y) return;                                   // padding of a fixed-size record region
     const uint32_t ls = r.x - a.slot_base;
     a.in_nxt[ls] = r.y;
     a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
@@ -1260,6 +1390,7 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const
 uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }
 uint32_t grid_ell(uint32_t n) { return (n + kEllChunk - 1) / kEllChunk; }
 
+
 uint32_t grid_for(uint32_t n) {
     uint32_t g = (n + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;     // grid-stride beyond 32 blocks per CU
@@ -1267,6 +1398,21 @@ uint32_t grid_for(uint32_t n) {
 }
 
 }  // namespace
+
+// Workgroups of the ELL round kernel for W-slot rows the chip holds at once
+// (LDS-bound: the words buffer is kEllChunk W 4 bytes): the kernel's grid.
+uint32_t ell_round_grid(uint32_t W, int device) {
+    int cus = 0, o0 = 0, o1 = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
+    const size_t lds = size_t(kEllChunk) * W * 4;
+    const auto k0 = W <= 4 ? pt_round_ell_kernel<false, 4> : W <= 6 ? pt_round_ell_kernel<false, 6> : pt_round_ell_kernel<false, 8>;
+    const auto k1 = W <= 4 ? pt_round_ell_kernel<true, 4> : W <= 6 ? pt_round_ell_kernel<true, 6> : pt_round_ell_kernel<true, 8>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, k0, kBlock, lds) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k1, kBlock, lds) != hipSuccess)
+        return 0;
+    const int o = std::min(o0, o1);
+    return o > 0 ? uint32_t(cus) * uint32_t(o) : 0u;
+}
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
     if (a.rec_c) {
@@ -1281,7 +1427,8 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         const auto k = a.ell <= 4 ? (f ? pt_round_ell_kernel<true, 4> : pt_round_ell_kernel<false, 4>)
                      : a.ell <= 6 ? (f ? pt_round_ell_kernel<true, 6> : pt_round_ell_kernel<false, 6>)
                                   : (f ? pt_round_ell_kernel<true, 8> : pt_round_ell_kernel<false, 8>);
-        hipLaunchKernelGGL(k, dim3(grid_ell(a.n)), dim3(kBlock), lds, s, a);
+        hipLaunchKernelGGL(k, dim3(a.ell_grid ? min(a.ell_grid, grid_ell(a.n)) : grid_ell(a.n)), dim3(kBlock), lds, s,
+                           a);
         return hipGetLastError();
     }
     if (a.omit || a.dly)
@@ -1294,7 +1441,8 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s) {
     const dim3 grid(grid_chunks(a0.n), nlanes);
     if (a0.ell) {
-        const dim3 grid(grid_ell(a0.n), nlanes);
+        const uint32_t gx = a0.ell_grid ? std::max<uint32_t>(1u, a0.ell_grid / nlanes) : grid_ell(a0.n);
+        const dim3 grid(std::min(gx, grid_ell(a0.n)), nlanes);
         const size_t lds = size_t(kEllChunk) * a0.ell * 4;
         const bool f = a0.omit || a0.dly;
         const auto k = a0.ell <= 4 ? (f ? pt_round_ell_lanes_kernel<true, 4> : pt_round_ell_lanes_kernel<false, 4>)
@@ -1321,9 +1469,11 @@ hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStr
 }
 
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
-                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s) {
+                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s, uint32_t cap,
+                             uint32_t self) {
     if (nblk == 0) return hipSuccess;
-    hipLaunchKernelGGL(pt_compact_kernel, dim3(nblk), dim3(kBlock), 0, s, a, rem, blk, send_base, cursor, out);
+    hipLaunchKernelGGL(pt_compact_kernel, dim3(nblk), dim3(kBlock), 0, s, a, rem, blk, send_base, cursor, out, cap,
+                       self);
     return hipGetLastError();
 }
 

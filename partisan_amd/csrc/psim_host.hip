@@ -20,6 +20,7 @@ using namespace psim;
 namespace {
 constexpr int kChunk = 16;  // rounds launched between host synchronisations (no-op rounds exit early)
 constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-scatter engine)
+constexpr size_t kMcntLane = 512;   // u32 per lane in mcnt_base: message counts, worklist counts
 constexpr size_t kStatsRow = size_t(kStatShards) * kNStat + kDelayHist;   // shards, then messages per delay
 }  // namespace
 
@@ -91,7 +92,13 @@ struct psim_handle {
     unsigned long long* scratch = nullptr;   // 1 counter
     int* ost_total = nullptr;                // device mirror of ost_cnt (the focused lane's)
     int* ost_total_base = nullptr;           // [kMaxLanes] allocation
-    uint32_t* mcnt_base = nullptr;           // [kMaxLanes][4][64] per-round message counts (PtArgs::mcnt)
+    uint32_t* mcnt_base = nullptr;           // [kMaxLanes][kMcntLane]: [4][64] per-round message counts
+                                             // (PtArgs::mcnt), then [4][64] worklist counts (PtArgs::wlcnt)
+    // group flags + worklist (ELL, one GPU): a pend buffer is the ng flag bytes, then at wl_off the
+    // [64][wl_cap] worklist shards of the same round (PtArgs::wl_cur / wl_nxt)
+    size_t pend_bytes = 0, wl_off = 0;
+    uint32_t wl_cap = 0;
+    uint32_t ell_grid = 0;                   // grid of the ELL round kernel (resident workgroups)
     hipEvent_t ev[2 * kChunk] = {};
 
     uint32_t par = 0;          // inbox buffer the next round reads
@@ -141,7 +148,8 @@ struct psim_handle {
     struct Sh {
         int rank = 0, world = 1;
         uint32_t n_global = 0, v_lo = 0;
-        uint64_t slot_base = 0;
+        uint64_t slot_base = 0;         // ABI (CSR) global slot id of local slot 0
+        uint64_t dev_slot_base = 0;     // the same in device slot ids (ELL: v_lo * W)
         uint32_t* stage = nullptr;       // [E_local] staged cross-shard words
         uint32_t* rem = nullptr;         // local slots whose receiver is remote, grouped by shard
         uint4* blk = nullptr;            // compaction blocks {shard, start, len, 0}
@@ -161,6 +169,14 @@ struct psim_handle {
         // the exchange inside the library (psim_shard_init_rccl / _set_transport, transport.hip)
         psim::Transport* xport = nullptr;
         uint32_t *xsend = nullptr, *xrecv = nullptr;   // dense word regions (psim_shard_layout / _recv_layout)
+        // sparse rounds of the in-library exchange: fixed-size record regions
+        // ({receiver slot, word}, rec_k per peer, rec_k <= rec_thr) sized from a bound
+        // on the words the round can send (shard_drive_fast); plan_ok: the lane's
+        // global counts g_inflight / g_ost are current, so the bound holds
+        uint2 *xrs = nullptr, *xrr = nullptr;
+        uint64_t rec_thr = 0;
+        uint32_t max_deg_g = 0;
+        bool plan_ok = false;
         hipEvent_t xev[2 * 16] = {};                   // exchange start / end per pending round
     } sh;
     hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
@@ -314,10 +330,13 @@ void free_graph(psim_handle* h) {
         b = psim_handle::Bin();
     }
     auto& sh = h->sh;
-    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map, sh.xsend, sh.xrecv};
+    void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map, sh.xsend, sh.xrecv,
+                  sh.xrs, sh.xrr};
     for (void* p : sp)
         if (p) (void)hipFree(p);
     sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = sh.xsend = sh.xrecv = nullptr;
+    sh.xrs = sh.xrr = nullptr;
+    sh.plan_ok = false;
     sh.recv_base.clear();
     sh.pending = 0;
     sh.blk = nullptr;
@@ -352,7 +371,8 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     PtArgs a{};
     a.n = h->n;
     a.v_lo = h->sh.v_lo;
-    a.slot_base = (uint32_t)h->sh.slot_base;
+    a.slot_base = (uint32_t)h->sh.dev_slot_base;
+    a.abi_slot_base = (uint32_t)h->sh.slot_base;
     a.stage = h->sh.stage;
     a.rowp = h->rowp;
     a.col = h->col;
@@ -376,6 +396,7 @@ PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned lon
     a.root = h->root;
     a.omit = h->omit;
     a.ell = h->ell;
+    a.ell_grid = h->ell_grid;
     if (h->dly) {
         // delay ring: `par` names the round as in[] does -- h->par reads the
         // next round's words, h->par ^ 1 writes them (the origin)
@@ -497,12 +518,20 @@ int to_window(psim_handle* h) {
 // same decision, taken from the same count, on both sides).
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     if (h->sh.world != 1 || h->bin.rec_c || h->dly) return;   // delays: a silent round may precede arrivals
-    a.mcnt = h->mcnt_base + 256 * size_t(h->cur_lane);
+    a.mcnt = h->mcnt_base + kMcntLane * size_t(h->cur_lane);
     a.m_w = uint32_t(R % 4);
     a.m_s = uint32_t((R + 3) % 4);
     a.m_r = uint32_t((R + 2) % 4);
     a.m_z = uint32_t((R + 1) % 4);
     a.dense = std::max<uint32_t>(1u, h->n / 4);
+    if (h->wl_cap) {          // sparse rounds: the groups written are listed
+        const uint32_t ng = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
+        a.wlcnt = a.mcnt + 256;
+        a.wl_cur = reinterpret_cast<uint32_t*>(a.pend_cur + h->wl_off);
+        a.wl_nxt = reinterpret_cast<uint32_t*>(a.pend_nxt + h->wl_off);
+        a.wl_cap = h->wl_cap;
+        a.wl_thr = std::max<uint32_t>(1u, ng / 8);
+    }
 }
 
 // Round tags (psim_internal.h): a slot-scatter inbox word carries the round
@@ -663,10 +692,10 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
     bool fresh = false;
     if (pick < 0 && (int)L.size() < kMaxLanes) {
         psim_handle::Lane l;
-        const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
         if (hipMalloc((void**)&l.vs, size_t(h->n) * 16) != hipSuccess ||
             hipMalloc((void**)&l.in[0], h->Ed * 4) != hipSuccess || hipMalloc((void**)&l.in[1], h->Ed * 4) != hipSuccess ||
-            hipMalloc((void**)&l.pend[0], ng) != hipSuccess || hipMalloc((void**)&l.pend[1], ng) != hipSuccess ||
+            hipMalloc((void**)&l.pend[0], h->pend_bytes) != hipSuccess ||
+            hipMalloc((void**)&l.pend[1], h->pend_bytes) != hipSuccess ||
             hipMalloc((void**)&l.ost, size_t(h->n) + 4) != hipSuccess) {
             void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
             for (void* p : lp)
@@ -956,8 +985,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             hipHostMalloc(&h->h_lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->ost_total_base, kMaxLanes * 4 * sizeof(int)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipMalloc(&h->mcnt_base, kMaxLanes * 256 * sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(h->mcnt_base, 0, kMaxLanes * 256 * sizeof(uint32_t)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->mcnt_base, kMaxLanes * kMcntLane * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(h->mcnt_base, 0, kMaxLanes * kMcntLane * sizeof(uint32_t)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) { rc = PSIM_EHIP; break; }
         h->ost_total = h->ost_total_base;
@@ -1100,12 +1129,28 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         mbl[v] = memb[lo + v];
         for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) s2v[e] = v;
     }
+    // ELL rows: with the slot-scatter engine and every degree
+    // <= kEllMax, slot s of v is v*Wd + s (Wd = the maximum degree over the
+    // WHOLE overlay, so every shard derives the same global slot ids), and the
+    // round kernel finds a vertex's inbox words without reading rowp.  Device
+    // slot ids are then ELL ids; the ABI keeps CSR slot ids (getters convert).
+    uint32_t ell = 0;
+    if (!(h->cfg.flags & (PSIM_CFG_BINNED | PSIM_CFG_CSR))) {
+        uint64_t mx = 0;
+        for (uint32_t v = 0; v < n; v++) mx = std::max<uint64_t>(mx, rp[v + 1] - rp[v]);
+        if (mx >= 1 && mx <= kEllMax) ell = uint32_t(mx);
+    }
+    const uint64_t Ed = ell ? uint64_t(nl) * ell : El;
+    if (ell && uint64_t(n) * ell >= 0xFFFFFFFFull)
+        return fail(h, PSIM_EINVAL, "too many ELL slots (%llu)", (unsigned long long)(uint64_t(n) * ell));
+    // local CSR slot e of local vertex v -> device slot (identity for CSR rows)
+    auto dslot = [&](uint32_t v, uint64_t e) -> uint32_t { return ell ? v * ell + uint32_t(e - rpl[v]) : uint32_t(e); };
     // remote slots grouped by destination shard, and the compaction blocks
     std::vector<std::vector<uint32_t>> remd(W);
     if (W > 1)
         for (uint64_t e = 0; e < El; e++) {
             const uint32_t d = owner(cl[e]);
-            if (d != (uint32_t)sh.rank) remd[d].push_back(uint32_t(e));
+            if (d != (uint32_t)sh.rank) remd[d].push_back(dslot(s2v[e], e));
         }
     std::vector<uint32_t> remflat;
     std::vector<uint4> blks;
@@ -1128,36 +1173,31 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
             if (src == (uint32_t)sh.rank) continue;
             const uint32_t slo = uint32_t((uint64_t(n) * src) / W), shi = uint32_t((uint64_t(n) * (src + 1)) / W);
             for (uint64_t e = rp[slo]; e < rp[shi]; e++)
-                if (cc[e] >= lo && cc[e] < hi) recvflat.push_back(uint32_t(rev[e] - sbase));
+                if (cc[e] >= lo && cc[e] < hi) recvflat.push_back(dslot(cc[e] - lo, rev[e] - sbase));
         }
     rbases[W] = recvflat.size();
-    // ELL rows: on one GPU with the slot-scatter engine and every
-    // degree <= kEllMax, slot s of v is v*W + s (W = the maximum degree), so
-    // the round kernel finds a vertex's inbox words without reading rowp
-    uint32_t ell = 0;
     std::vector<uint32_t> ep;
-    if (W == 1 && !(h->cfg.flags & (PSIM_CFG_BINNED | PSIM_CFG_CSR))) {
-        uint32_t mx = 0;
-        for (uint32_t v = 0; v < nl; v++) mx = std::max(mx, rpl[v + 1] - rpl[v]);
-        if (mx >= 1 && mx <= kEllMax) ell = mx;
-    }
-    const uint64_t Ed = ell ? uint64_t(nl) * ell : El;
     if (ell) {
-        if (Ed >= 0xFFFFFFFFull) return fail(h, PSIM_EINVAL, "too many ELL slots (%llu)", (unsigned long long)Ed);
+        // reverse slot of local slot e: global ELL id of (receiver cl[e], its
+        // CSR position rev - rp[receiver]); packed rows hold col << 3 | position
         std::vector<uint32_t> ce(Ed, kNoPeer), re(Ed, 0u);
         for (uint32_t v = 0; v < nl; v++)
             for (uint32_t e = rpl[v]; e < rpl[v + 1]; e++) {
-                const uint32_t u = s2v[rvl[e]];                  // owner of the reverse slot
-                ce[uint64_t(v) * ell + (e - rpl[v])] = cl[e];
-                re[uint64_t(v) * ell + (e - rpl[v])] = u * ell + (rvl[e] - rpl[u]);
+                const uint32_t u = cl[e];
+                ce[dslot(v, e)] = u;
+                re[dslot(v, e)] = u * ell + uint32_t(rvl[e] - rp[u]);
             }
-        if (nl < (1u << 29) - 1) {                         // packed rows for the ELL round kernel
+        if (n < (1u << 29) - 1) {                          // packed rows for the ELL round kernel
             ep.resize(Ed);
             for (uint64_t e = 0; e < Ed; e++)
                 ep[e] = ce[e] == kNoPeer ? kNoPeer : (ce[e] << 3) | (re[e] - ce[e] * ell);
         }
         cl_dev.swap(ce);
         rv_dev.swap(re);
+        if (W > 1) {                                       // receiver vertex of a device slot
+            s2v.resize(Ed);
+            for (uint64_t e = 0; e < Ed; e++) s2v[e] = uint32_t(e / ell);
+        }
     }
     const std::vector<uint32_t>& cl_up = ell ? cl_dev : cl;
     const std::vector<uint32_t>& rv_up = ell ? rv_dev : rvl;
@@ -1166,6 +1206,13 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     const size_t nw = (size_t(n) + 31) / 32;
     const size_t ng = (size_t(nl) + (1u << kGroupShift) - 1) >> kGroupShift;
     const bool binned = W == 1 && (h->cfg.flags & PSIM_CFG_BINNED);
+    // worklist of the sparse rounds (ELL rows on one GPU): 64 shards of
+    // ng / 16 groups each after the flag bytes; an overflowing shard only
+    // sends the next round back to the flags
+    const size_t wl_off = (ng + 15) & ~size_t(15);
+    const bool wl_on = ell && W == 1 && !getenv("PSIM_NO_WORKLIST");   // A/B switch
+    const uint32_t wl_cap = wl_on ? std::max<uint32_t>(64u, uint32_t((ng + 15) / 16)) : 0u;
+    const size_t pend_bytes = wl_off + size_t(64) * wl_cap * 4;
     auto& bn = h->bin;
     if (binned) {
         if (!bin_geometry(rpl, nl, bn.fv_shift, bn.cv_shift, bn.nf, bn.nc))
@@ -1193,7 +1240,8 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         (!ep.empty() && alloc((void**)&h->ecol, Ed * 4) != hipSuccess) ||
         alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
         (!binned && (alloc((void**)&h->in[0], Ed * 4) != hipSuccess || alloc((void**)&h->in[1], Ed * 4) != hipSuccess ||
-                     alloc((void**)&h->pend[0], ng) != hipSuccess || alloc((void**)&h->pend[1], ng) != hipSuccess)) ||
+                     alloc((void**)&h->pend[0], pend_bytes) != hipSuccess ||
+                     alloc((void**)&h->pend[1], pend_bytes) != hipSuccess)) ||
         (binned && (alloc((void**)&bn.rec_c, El * 8) != hipSuccess || alloc((void**)&bn.rec_f, El * 8) != hipSuccess ||
                     alloc((void**)&bn.cnt_c[0], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
                     alloc((void**)&bn.cnt_c[1], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
@@ -1202,12 +1250,12 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
                     alloc((void**)&bn.fslot, (size_t(bn.nf) + 1) * 4) != hipSuccess ||
                     alloc((void**)&bn.obin, size_t(bn.nf) * 4) != hipSuccess)) ||
         alloc((void**)&h->ost, size_t(nl) + 4) != hipSuccess ||
-        (W > 1 && (alloc((void**)&sh.stage, El * 4) != hipSuccess ||
+        (W > 1 && (alloc((void**)&sh.stage, Ed * 4) != hipSuccess ||
                    alloc((void**)&sh.rem, remflat.size() * 4) != hipSuccess ||
                    alloc((void**)&sh.blk, blks.size() * 16) != hipSuccess ||
                    alloc((void**)&sh.send_base_d, W * 4) != hipSuccess ||
                    alloc((void**)&sh.cursor, W * 4) != hipSuccess ||
-                   alloc((void**)&sh.slot2v, El * 4) != hipSuccess ||
+                   alloc((void**)&sh.slot2v, Ed * 4) != hipSuccess ||
                    alloc((void**)&sh.recv_map, recvflat.size() * 4) != hipSuccess))) {
         free_graph(h);
         return fail(h, PSIM_ENOMEM, "device allocation failed for n=%u E=%llu", nl, (unsigned long long)El);
@@ -1216,9 +1264,22 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->E = El;
     h->Ed = Ed;
     h->ell = ell;
+    h->ell_grid = ell ? ell_round_grid(ell, h->device) : 0u;
+    {
+        uint64_t mx = 0;                               // the same on every shard: the whole overlay
+        for (uint32_t v = 0; v < n; v++) mx = std::max<uint64_t>(mx, rp[v + 1] - rp[v]);
+        sh.max_deg_g = uint32_t(mx);
+        // a sparse round sends records while the bound stays under a quarter of
+        // a peer pair's dense region (~ n deg / W^2 words): 8-byte records
+        sh.rec_thr = W > 1 ? std::max<uint64_t>(64, uint64_t(n) * std::max<uint64_t>(1, mx) / (8ull * W * W)) : 0;
+    }
+    h->pend_bytes = pend_bytes;
+    h->wl_off = wl_off;
+    h->wl_cap = wl_cap;
     sh.n_global = n;
     sh.v_lo = lo;
     sh.slot_base = sbase;
+    sh.dev_slot_base = ell ? uint64_t(lo) * ell : sbase;
     HIPCHK(h, hipMemcpy(h->rowp, rpl.data(), (size_t(nl) + 1) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->col, cl_up.data(), Ed * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->rev, rv_up.data(), Ed * 4, hipMemcpyHostToDevice));
@@ -1242,18 +1303,18 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
     HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)));
-    HIPCHK(h, hipMemset(h->mcnt_base, 0, kMaxLanes * 256 * sizeof(uint32_t)));
+    HIPCHK(h, hipMemset(h->mcnt_base, 0, kMaxLanes * kMcntLane * sizeof(uint32_t)));
     h->ost_total = h->ost_total_base;
     h->lanes.assign(1, psim_handle::Lane());
     h->cur_lane = 0;
     if (W > 1) {
         std::vector<uint32_t> sb32(W);
         for (uint32_t d = 0; d < W; d++) sb32[d] = uint32_t(sbases[d]);
-        HIPCHK(h, hipMemset(sh.stage, 0, El * 4));
+        HIPCHK(h, hipMemset(sh.stage, 0, Ed * 4));
         HIPCHK(h, hipMemcpy(sh.rem, remflat.data(), remflat.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(sh.blk, blks.data(), blks.size() * 16, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(sh.send_base_d, sb32.data(), W * 4, hipMemcpyHostToDevice));
-        HIPCHK(h, hipMemcpy(sh.slot2v, s2v.data(), El * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(sh.slot2v, s2v.data(), Ed * 4, hipMemcpyHostToDevice));
         if (!recvflat.empty())
             HIPCHK(h, hipMemcpy(sh.recv_map, recvflat.data(), recvflat.size() * 4, hipMemcpyHostToDevice));
         sh.nblk = uint32_t(blks.size());
@@ -1391,7 +1452,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
             // origin emits into the buffer the next round reads
             PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
             set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
-            if (a.mcnt) HIPCHK(h, hipMemsetAsync(a.mcnt, 0, 256 * sizeof(uint32_t), h->stream));
+            if (a.mcnt) HIPCHK(h, hipMemsetAsync(a.mcnt, 0, kMcntLane * sizeof(uint32_t), h->stream));
             a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
             a.root = lr;
             HIPCHK(h, launch_pt_origin(a, h->stream));
@@ -1468,6 +1529,7 @@ int psim_shard_layout(const psim_handle* h, uint64_t* region_base, size_t world)
 
 int psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev, uint64_t send_cap,
                          uint64_t* counts, int64_t* local_live) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     if (!h || !counts) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     unsigned long long r[kNStat];
@@ -1479,6 +1541,7 @@ int psim_shard_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out, void
 
 int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* counts,
                      psim_round_stats* st, int64_t* local_live) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     if (!h || !counts) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
@@ -1540,6 +1603,7 @@ int psim_shard_recv_layout(const psim_handle* h, uint64_t* recv_base, size_t wor
 }
 
 int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out, void* send_dev) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     if (!h) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     if (h->sh.world > 1 && !send_dev) return PSIM_EINVAL;
@@ -1553,7 +1617,10 @@ int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out
     return PSIM_OK;
 }
 
-int psim_shard_round_async(psim_handle* h, void* send_dev) {
+// rec_k > 0 (in-library exchange only): this round's cross-shard words go out
+// as {receiver slot, word} records, rec_k per peer (sh.xrs), instead of the
+// dense regions.
+static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k) {
     if (!h) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
@@ -1570,15 +1637,27 @@ int psim_shard_round_async(psim_handle* h, void* send_dev) {
     HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
     HIPCHK(h, launch_pt_round(a, h->stream));
     HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending + 1], h->stream));
-    if (sh.world > 1)
+    if (sh.world > 1 && rec_k) {
+        HIPCHK(h, hipMemsetAsync(sh.cursor, 0, sh.world * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(sh.xrs, 0, size_t(sh.world - 1) * rec_k * 8, h->stream));
+        HIPCHK(h, launch_pt_compact(a, sh.rem, sh.blk, sh.nblk, nullptr, sh.cursor, sh.xrs, h->stream, rec_k,
+                                    (uint32_t)sh.rank));
+    } else if (sh.world > 1) {
         HIPCHK(h, launch_pt_pack_dense(a, sh.rem, (uint32_t)sh.send_base[sh.world], (uint32_t*)send_dev, h->stream));
+    }
     h->par ^= 1u;
     h->round++;
     sh.pending++;
     return PSIM_OK;
 }
 
+int psim_shard_round_async(psim_handle* h, void* send_dev) {
+    if (h) h->sh.plan_ok = false;       // split-phase rounds: the record-bound bookkeeping is off
+    return shard_round_async_k(h, send_dev, 0);
+}
+
 int psim_shard_ingest_dense(psim_handle* h, const void* recv_dev) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     if (!h) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     return ingest_dense(h, recv_dev);
@@ -1681,7 +1760,9 @@ int x_buffers(psim_handle* h) {
     if (sh.world > 1 && !sh.xport) return fail(h, PSIM_ESTATE, "sharded handle without a transport (psim_shard_init_rccl)");
     if (sh.xsend || sh.world == 1) return PSIM_OK;
     const size_t ns = std::max<uint64_t>(1, sh.send_base[sh.world]), nr = std::max<uint64_t>(1, sh.recv_base[sh.world]);
-    if (hipMalloc((void**)&sh.xsend, ns * 4) != hipSuccess || hipMalloc((void**)&sh.xrecv, nr * 4) != hipSuccess)
+    const size_t nrec = std::max<uint64_t>(1, (sh.world - 1) * sh.rec_thr);
+    if (hipMalloc((void**)&sh.xsend, ns * 4) != hipSuccess || hipMalloc((void**)&sh.xrecv, nr * 4) != hipSuccess ||
+        hipMalloc((void**)&sh.xrs, nrec * 8) != hipSuccess || hipMalloc((void**)&sh.xrr, nrec * 8) != hipSuccess)
         return fail(h, PSIM_ENOMEM, "exchange buffers");
     HIPCHK(h, hipMemsetAsync(sh.xsend, 0, ns * 4, h->stream));
     HIPCHK(h, hipMemsetAsync(sh.xrecv, 0, nr * 4, h->stream));
@@ -1689,11 +1770,24 @@ int x_buffers(psim_handle* h) {
 }
 
 // exchange the dense regions just packed into xsend, then ingest them
-int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs) {
+int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k = 0) {
     auto& sh = h->sh;
     if (sh.world == 1) return PSIM_OK;
     std::string err;
     HIPCHK(h, hipEventRecord(sh.xev[2 * slot], h->stream));
+    if (rec_k) {        // fixed-size record regions: 2 rec_k words per peer, none to self
+        const int W = sh.world;
+        std::vector<uint64_t> off(size_t(W) + 1, 0);
+        for (int d = 0; d < W; d++) off[d + 1] = off[d] + (d == sh.rank ? 0 : 2ull * rec_k);
+        int rc = sh.xport->alltoallv(reinterpret_cast<const uint32_t*>(sh.xrs), off.data(),
+                                     reinterpret_cast<uint32_t*>(sh.xrr), off.data(), sh.rank, W, h->stream, &err);
+        if (rc) return fail(h, rc, "exchange: %s", err.c_str());
+        HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
+        if (xs) xs->fabric_bytes += 8ull * rec_k * uint64_t(W - 1);
+        PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
+        HIPCHK(h, launch_pt_ingest(a, sh.xrr, uint32_t(uint64_t(W - 1) * rec_k), sh.slot2v, h->stream));
+        return PSIM_OK;
+    }
     int rc = sh.xport->alltoallv(sh.xsend, sh.send_base.data(), sh.xrecv, sh.recv_base.data(), sh.rank, sh.world,
                                  h->stream, &err);
     if (rc) return fail(h, rc, "exchange: %s", err.c_str());
@@ -1781,6 +1875,7 @@ int lane_globals(psim_handle* h) {
     l.g_inflight = v[0];
     l.g_live = v[1];
     l.g_ost = v[2];
+    h->sh.plan_ok = true;      // shard_drive_fast may bound the next rounds' words from these
     return PSIM_OK;
 }
 
@@ -1789,6 +1884,7 @@ int lane_globals(psim_handle* h) {
 // all-reduce of every lane's counters per round.
 int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
                       uint32_t* ran_out, psim_exchange_stats* xs) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     const int focus = h->cur_lane;
     save_lane(h);
     struct Refocus {
@@ -1932,12 +2028,31 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
     constexpr int NK = 10;                     // 5 kinds, delivered_new, senders, degree sum, live rows, row holders
     uint32_t ran = 0;
     bool done = false;
+    auto& sh = h->sh;
+    // Record bound of the sparse rounds: a vertex sends at most
+    // one word per slot and only when it received words or holds rows due, so
+    // a round after M words in flight with H row holders sends <= D (M + H)
+    // words (D = the overlay's widest row) and the next round starts with
+    // <= H + M holders.  Every rank derives the same bound from the global
+    // counts of the last collective, so every rank picks the same format.
+    double bM = 0, bH = 0;
+    if (sh.plan_ok && !h->lanes.empty()) {
+        bM = double(h->lanes[h->cur_lane].g_inflight);
+        bH = double(h->lanes[h->cur_lane].g_ost);
+    }
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(K, max_rounds - ran);
         for (uint32_t j = 0; j < k; j++) {
-            rc = psim_shard_round_async(h, h->sh.xsend);
+            uint32_t rec_k = 0;
+            if (sh.plan_ok && sh.world > 1) {
+                const double S = double(std::max<uint32_t>(1u, sh.max_deg_g)) * (bM + bH);
+                bH += bM;
+                bM = S;
+                if (S <= double(sh.rec_thr)) rec_k = std::max<uint32_t>(1u, uint32_t(S));
+            }
+            rc = shard_round_async_k(h, sh.xsend, rec_k);
             if (rc) return rc;
-            rc = x_exchange(h, (int)j, xs);
+            rc = x_exchange(h, (int)j, xs, rec_k);
             if (rc) return rc;
         }
         psim_round_stats st[K];
@@ -1978,6 +2093,10 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
                 l.g_inflight = msgs;
                 l.g_live = f[8];
                 l.g_ost = f[9];
+            }
+            if (j + 1 == got) {                                 // the next chunk's bound starts here
+                bM = double(msgs);
+                bH = double(f[9]);
             }
             if (out && ran < cap) {
                 psim_round_stats& o = out[ran];
@@ -2023,11 +2142,19 @@ int psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     if (h->win) {
         rc = win_exchange(h, nullptr);
     } else {
+        // the origin sends at most one word per slot: records unless its row is wide
+        auto& sh = h->sh;
         PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
-        if (h->sh.world > 1)
-            HIPCHK(h, launch_pt_pack_dense(a, h->sh.rem, (uint32_t)h->sh.send_base[h->sh.world], h->sh.xsend,
-                                           h->stream));
-        rc = x_exchange(h, 0, nullptr);
+        const uint32_t rec_k = std::max<uint32_t>(1u, sh.max_deg_g) <= sh.rec_thr ? std::max<uint32_t>(1u, sh.max_deg_g) : 0u;
+        if (sh.world > 1 && rec_k) {
+            HIPCHK(h, hipMemsetAsync(sh.cursor, 0, sh.world * 4, h->stream));
+            HIPCHK(h, hipMemsetAsync(sh.xrs, 0, size_t(sh.world - 1) * rec_k * 8, h->stream));
+            HIPCHK(h, launch_pt_compact(a, sh.rem, sh.blk, sh.nblk, nullptr, sh.cursor, sh.xrs, h->stream, rec_k,
+                                        (uint32_t)sh.rank));
+        } else if (sh.world > 1) {
+            HIPCHK(h, launch_pt_pack_dense(a, sh.rem, (uint32_t)sh.send_base[sh.world], sh.xsend, h->stream));
+        }
+        rc = x_exchange(h, 0, nullptr, rec_k);
     }
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2044,6 +2171,7 @@ int psim_shard_step(psim_handle* h, uint32_t rounds, psim_round_stats* out, size
 }
 
 int psim_shard_ingest(psim_handle* h, const void* recv_dev, uint64_t n_records) {
+    if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
     if (!h || (!recv_dev && n_records)) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     if (n_records == 0) return PSIM_OK;

@@ -103,7 +103,8 @@ __host__ __device__ inline uint32_t abi_word(uint32_t w) {   // inbox word -> ps
 struct PtArgs {
     uint32_t n;                            // vertices of this shard (all of them on one GPU)
     uint32_t v_lo;                         // global id of local vertex 0
-    uint32_t slot_base;                    // global slot id of local slot 0
+    uint32_t slot_base;                    // global device slot id of local slot 0 (ELL: v_lo * W)
+    uint32_t abi_slot_base;                // the same as an ABI (CSR) slot id
     uint32_t* __restrict__ stage;          // [E_local] words for receivers on other shards (sharded only)
     const uint32_t* __restrict__ rowp;     // [n+1] local slot row pointers
     const uint32_t* __restrict__ col;      // [E]   neighbour (global) id per slot (sorted in a row)
@@ -126,6 +127,14 @@ struct PtArgs {
     uint32_t* mcnt;
     uint32_t m_w, m_s, m_r, m_z;
     uint32_t dense;                        // a round following >= dense messages runs flag-free
+    // sparse rounds (ELL, one GPU; null wl_cur: off): a round following < wl_thr messages lists the
+    // groups it flags -- 64 shards of wl_cap entries, counts in wlcnt [4 rounds][64] like mcnt -- and
+    // the next round reads only those groups (plumtree.hip round_counts)
+    uint32_t* wlcnt;
+    uint32_t* wl_cur;
+    uint32_t* wl_nxt;
+    uint32_t wl_cap, wl_thr;
+    uint32_t ell_grid;                     // ELL kernel grid = resident workgroups (0: one per chunk)
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
@@ -489,6 +498,7 @@ void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing to
 hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);   // binned when a.rec_c is set
+uint32_t ell_round_grid(uint32_t W, int device);              // resident workgroups of the ELL kernel
 // one slot-scatter round for nlanes heartbeat lanes (d_args[0..nlanes) on device; a0 = d_args[0] on host)
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s);
 // op: 0 descends, 1 dominates, 2 merge, 3 increment
@@ -502,7 +512,8 @@ hipError_t launch_pt_scrub(uint32_t* words, uint64_t n, uint32_t keep, uint32_t 
 hipError_t launch_pt_hash(const PtArgs& a, uint32_t has_serial, uint32_t root_local, unsigned long long E,
                           unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_compact(const PtArgs& a, const uint32_t* rem, const uint4* blk, uint32_t nblk,
-                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s);
+                             const uint32_t* send_base, uint32_t* cursor, uint2* out, hipStream_t s,
+                             uint32_t cap = 0xFFFFFFFFu, uint32_t self = 0);
 hipError_t launch_pt_ingest(const PtArgs& a, const uint2* rec, uint32_t nrec, const uint32_t* slot2v, hipStream_t s);
 hipError_t launch_pt_pack_dense(const PtArgs& a, const uint32_t* rem, uint32_t nrem, uint32_t* send, hipStream_t s);
 hipError_t launch_pt_ingest_dense(const PtArgs& a, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,

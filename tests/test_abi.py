@@ -33,6 +33,15 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_library_has_no_undefined_internal_symbols():
+    """Every psim:: function the library calls is defined in it (a declaration
+    matching a definition hidden in an anonymous namespace links as a shared
+    object and only fails at load or first call)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", LIB], capture_output=True, text=True, check=True).stdout
+    assert not [l for l in out.splitlines() if "psim" in l.lower()], out
+
+
 def test_python_binding_covers_header():
     from partisan_amd._lib import SIGNATURES
     assert sorted(SIGNATURES) == declared_symbols()

@@ -84,6 +84,7 @@ def main():
             ks = []
             tot = 0
             live = 0
+            hold = 0
             for r, s in enumerate(sims):
                 check(lib().psim_shard_round_async(s._h, C.c_void_p(send[r].data_ptr())), s._h)
                 st = (RoundStats * 1)()
@@ -94,8 +95,9 @@ def main():
                 ks.append(d["kernel_ms"])
                 tot += sum(d[k] for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft"))
                 live += int(lv[0])
+                hold += d["outstanding_vertices"]
             exchange()
-            per_round.append({"kernel_ms": ks, "msgs": tot})
+            per_round.append({"kernel_ms": ks, "msgs": tot, "holders": hold})
             if tot == 0 and live == 0:
                 break
         floods.append(per_round)
@@ -103,6 +105,20 @@ def main():
     kmax = sum(max(r["kernel_ms"]) for r in last)
     ksum = [sum(r["kernel_ms"][i] for r in last) for i in range(W)]
     xms = len(last) * max(fabric) / (a.xgmi_gbps * 1e6)
+    # the in-library driver's format per round (psim_host.hip shard_drive_fast):
+    # records of K = D (M + H) per peer while K <= n D / (8 W^2), M / H chained
+    # from the last 4-round collective (the origin's D words after a broadcast)
+    D = max(s.max_degree() for s in sims)
+    thr = max(64, n * D // (8 * W * W))
+    rec_fabric, bM, bH = [], float(D), 0.0
+    for i, r in enumerate(last):
+        S = D * (bM + bH)
+        bH += bM
+        bM = S
+        rec_fabric.append((W - 1) * max(1, int(S)) * 8 if S <= thr else max(fabric))
+        if i % 4 == 3:                               # collective: actual counts
+            bM, bH = float(r["msgs"]), float(r["holders"])
+    xms_rec = sum(rec_fabric) / (a.xgmi_gbps * 1e6)
     out = {
         "n": n, "world": W, "rounds": len(last), "rows": "csr" if a.csr else "ell",
         "per_shard_vertices": [s.n for s in sims],
@@ -112,6 +128,9 @@ def main():
         "fabric_bytes_per_round_per_shard": fabric,
         "exchange_ms_per_flood_at_xgmi": round(xms, 4),
         "xgmi_GBps_assumed": a.xgmi_gbps,
+        "fabric_bytes_per_round_with_records": rec_fabric,
+        "exchange_ms_per_flood_with_records": round(xms_rec, 4),
+        "projected_step_ms_with_records": round(kmax + xms_rec, 4),
         "projected_step_ms": round(kmax + xms, 4),
         "projected_peer_rounds_per_s": n * len(last) / ((kmax + xms) / 1e3),
         "method": "8 shard handles in one process on one GPU, each round's kernels run alone (sync per shard), "
