@@ -10,9 +10,10 @@ value = n_peers * rounds / step time, summed over ranks.  The overlay is
 resident in HBM before the timed region; nothing crosses PCIe inside it
 except the per-chunk 8 KB counter read-back the round driver needs.
 
-Roofline: dominant kernel pt_round_kernel, HBM-bound; achieved = SURVEY 8(d)
-algorithmic bytes of the timed rounds / their summed hipEvent durations
-(events on the library's own stream).  cpu_baseline: the C oracle (a
+Roofline: dominant kernel pt_round_ell_kernel, HBM-bound; achieved = SURVEY
+8(d) algorithmic bytes of the timed rounds / their summed hipEvent durations
+(events on the library's own stream: one pair per 16-round chunk, so the
+average launch includes the dispatch gaps between round kernels).  cpu_baseline: the C oracle (a
 scalar port of the reference modules) on a bounded sample of the same
 workload, rank 0 only.
 
@@ -51,6 +52,9 @@ def parse():
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
     p.add_argument("--csr", action="store_true", help="A/B: CSR slot rows instead of ELL rows (DESIGN.md 4)")
+    p.add_argument("--round-events", action="store_true",
+                   help="a hipEvent pair around every round kernel (the markers cost ~10 us between rounds); "
+                        "default: one pair per 16-round chunk (PSIM_CFG_CHUNK_TIMING)")
     p.add_argument("--transport", choices=["nccl", "gloo"], default="nccl",
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
     p.add_argument("--all-on-device0", action="store_true",
@@ -104,7 +108,7 @@ def sum_over_ranks(pg, x):
 def one_step(sim, root):
     sim.reset_trees()
     sim.broadcast(root)
-    return sim.run()
+    return sim.run(as_dicts=False)     # a numpy record array: no per-round Python dicts in the timed loop
 
 
 def verify(sim, pg, n, rounds_per_step):
@@ -190,7 +194,8 @@ def main():
         sim = sp.sim
     else:
         sp = None
-        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local, csr=args.csr)
+        sim = pa.Simulator(lazy_tick_rounds=args.lazy_tick_rounds, device=local, csr=args.csr,
+                           chunk_timing=not args.round_events)
         sim.load_overlay(rp, col)
     del rp, col
     root = 0
@@ -217,8 +222,8 @@ def main():
         stats, rounds = step()
         rounds_per_step.append(rounds)
         if sp is None:
-            algo_bytes += sum(s["algo_bytes"] for s in stats)
-            round_ms += sum(s["kernel_ms"] for s in stats)
+            algo_bytes += int(stats["algo_bytes"].sum())
+            round_ms += float(stats["kernel_ms"].sum())
     # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
     barrier(pg)
     t1 = time.perf_counter()

@@ -73,6 +73,12 @@ typedef struct psim_config {
  * vertex's inbox words are found without reading row pointers;
  * PSIM_CFG_CSR keeps the CSR layout instead (same results; A/B and tests). */
 #define PSIM_CFG_CSR 2u
+/* psim_step / psim_run time each round with its own pair of hipEvents
+ * (psim_round_stats.kernel_ms).  PSIM_CFG_CHUNK_TIMING records one pair per
+ * chunk of up to 16 rounds instead -- each round's kernel_ms is then the
+ * chunk's device time / its rounds -- so no event marker sits between two
+ * round kernels (same results). */
+#define PSIM_CFG_CHUNK_TIMING 4u
 
 /* Per-round counters, reduced on device (psim_step / psim_run). */
 typedef struct psim_round_stats {

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("PSIM_LIB_PATH") or os.path.join(HERE, "libpsim.so")  
 PSIM_ABI_VERSION = 2
 PSIM_CFG_BINNED = 1   # psim_config.flags: binned Plumtree engine on one GPU
 PSIM_CFG_CSR = 2      # slot-scatter engine keeps CSR rows instead of ELL rows
+PSIM_CFG_CHUNK_TIMING = 4   # one hipEvent pair per chunk of rounds instead of per round
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EHIP", -4: "PSIM_ERCCL",
     -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV",

@@ -647,7 +647,7 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
     m.all_in = prev2 >= a.dense;                       // the last round wrote none: every group is read
     // the last round's senders listed every group they flagged (the same
     // test on the same count) and no row is due: only the listed groups
-    m.list_in = wl_off && a.wl_cur && prev2 < a.wl_thr && !cnt2[2] && !rows_due;
+    m.list_in = wl_off && a.wl_cur && prev2 < a.dense && prev2 < a.wl_thr && !cnt2[2] && !rows_due;
     return true;
 }
 

@@ -98,6 +98,7 @@ struct psim_handle {
     // [64][wl_cap] worklist shards of the same round (PtArgs::wl_cur / wl_nxt)
     size_t pend_bytes = 0, wl_off = 0;
     uint32_t wl_cap = 0;
+    uint32_t wl_thr = 0;                     // 0: ng / 8 (PSIM_WL_THR test knob: list mode up to that count)
     uint32_t ell_grid = 0;                   // grid of the ELL round kernel (resident workgroups)
     hipEvent_t ev[2 * kChunk] = {};
 
@@ -530,7 +531,7 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
         a.wl_cur = reinterpret_cast<uint32_t*>(a.pend_cur + h->wl_off);
         a.wl_nxt = reinterpret_cast<uint32_t*>(a.pend_nxt + h->wl_off);
         a.wl_cap = h->wl_cap;
-        a.wl_thr = std::max<uint32_t>(1u, ng / 8);
+        a.wl_thr = h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
     }
 }
 
@@ -778,6 +779,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     bool done = stop_q && all_quiet();
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
+        const bool per_round = !(h->cfg.flags & PSIM_CFG_CHUNK_TIMING);   // events between round kernels
         // a quiescent lane's round changes nothing: only the others run (the
         // focused lane always runs, so a plain psim_step still launches)
         std::vector<int> act;
@@ -824,28 +826,30 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             HIPCHK(h, hipMemcpyAsync(h->lane_args, h->h_lane_args, k * A * sizeof(PtArgs), hipMemcpyHostToDevice,
                                      h->stream));
             for (uint32_t i = 0; i < k; i++) {
-                HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+                if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
                 HIPCHK(h, launch_pt_round_lanes(h->lane_args + i * A, h->h_lane_args[i * A], (uint32_t)A, h->stream));
-                HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
+                if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
             }
         } else
 #endif
         for (uint32_t i = 0; i < k; i++) {
             const uint32_t tick = ((h->round + i + 1) % L) == 0;
-            HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+            if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
             for (size_t q = 0; q < A; q++) {
                 if (h->lanes[act[q]].win) HIPCHK(h, win_round(q, i, tick));
                 else HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
             }
-            HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
+            if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
         }
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        float chunk_ms = 0.f;
+        if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
         for (uint32_t i = 0; i < k; i++) {
-            float ms = 0.f;
-            HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
+            float ms = chunk_ms / float(k);
+            if (per_round) HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
             unsigned long long tot[kNStat] = {0};
             uint64_t msgs = 0;
             for (size_t q = 0; q < A; q++) {
@@ -1211,7 +1215,9 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     // sends the next round back to the flags
     const size_t wl_off = (ng + 15) & ~size_t(15);
     const bool wl_on = ell && W == 1 && !getenv("PSIM_NO_WORKLIST");   // A/B switch
-    const uint32_t wl_cap = wl_on ? std::max<uint32_t>(64u, uint32_t((ng + 15) / 16)) : 0u;
+    uint32_t wl_cap = wl_on ? std::max<uint32_t>(64u, uint32_t((ng + 15) / 16)) : 0u;
+    if (wl_on && getenv("PSIM_WL_CAP"))          // test knob: tiny shards exercise the overflow fallback
+        wl_cap = std::max<uint32_t>(1u, uint32_t(strtoul(getenv("PSIM_WL_CAP"), nullptr, 10)));
     const size_t pend_bytes = wl_off + size_t(64) * wl_cap * 4;
     auto& bn = h->bin;
     if (binned) {
@@ -1274,6 +1280,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         sh.rec_thr = W > 1 ? std::max<uint64_t>(64, uint64_t(n) * std::max<uint64_t>(1, mx) / (8ull * W * W)) : 0;
     }
     h->pend_bytes = pend_bytes;
+    h->wl_thr = getenv("PSIM_WL_THR") ? uint32_t(strtoul(getenv("PSIM_WL_THR"), nullptr, 10)) : 0u;
     h->wl_off = wl_off;
     h->wl_cap = wl_cap;
     sh.n_global = n;

@@ -7,7 +7,8 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import PSIM_ABI_VERSION, PSIM_CFG_BINNED, PSIM_CFG_CSR, Config, RoundStats, check, lib
+from ._lib import (PSIM_ABI_VERSION, PSIM_CFG_BINNED, PSIM_CFG_CHUNK_TIMING, PSIM_CFG_CSR, Config, RoundStats, check,
+                   lib)
 
 _u8p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))    # noqa: E731
 _u16p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint16))  # noqa: E731
@@ -15,16 +16,25 @@ _u32p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
 _u64p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
 
 
+_ROUND_DTYPE = np.dtype([("sent", np.uint64, 6), ("delivered_new", np.uint64), ("active", np.uint64),
+                         ("senders", np.uint64), ("sender_degree_sum", np.uint64),
+                         ("outstanding_vertices", np.uint64), ("algo_bytes", np.uint64), ("kernel_ms", np.float64)])
+assert _ROUND_DTYPE.itemsize == C.sizeof(RoundStats)
+
+
 class Simulator:
     """Round-synchronous simulator of Partisan's gossip hot path."""
 
     def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0, rank=0, world=1,
-                 binned=False, csr=False):
+                 binned=False, csr=False, chunk_timing=False):
         """binned: route Plumtree messages through receiver bins on a single
         GPU instead of scattering receiver-slot words (PSIM_CFG_BINNED; same
         results).  csr: keep CSR slot rows in the slot-scatter
-        engine instead of fixed-width ELL rows (PSIM_CFG_CSR; same results)."""
-        flags = (PSIM_CFG_BINNED if binned else 0) | (PSIM_CFG_CSR if csr else 0)
+        engine instead of fixed-width ELL rows (PSIM_CFG_CSR; same results).
+        chunk_timing: one hipEvent pair per chunk of rounds (PSIM_CFG_CHUNK_TIMING;
+        kernel_ms of a round = the chunk's device time / its rounds)."""
+        flags = ((PSIM_CFG_BINNED if binned else 0) | (PSIM_CFG_CSR if csr else 0)
+                 | (PSIM_CFG_CHUNK_TIMING if chunk_timing else 0))
         cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
                      exchange_tick_rounds=exchange_tick_rounds, flags=flags, _reserved=0, seed=seed)
         h = C.c_void_p()
@@ -101,11 +111,19 @@ class Simulator:
         self._c(lib().psim_step(self._h, rounds, st, rounds))
         return [s.as_dict() for s in st[:rounds]]
 
-    def run(self, max_rounds=100000, cap=4096):
-        st = (RoundStats * cap)()
+    def run(self, max_rounds=100000, cap=4096, as_dicts=True):
+        """Rounds to quiescence (psim_run): (per-round stats, rounds).  as_dicts=False
+        returns the stats as a numpy structured array (fields of psim_round_stats)
+        instead of one dict per round -- no per-round Python objects."""
+        st = getattr(self, "_run_buf", None)          # reused: a 4096-row ctypes array costs ~0.1 ms to zero
+        if st is None or len(st) < cap:
+            st = self._run_buf = (RoundStats * cap)()
         ran = C.c_uint32()
         self._c(lib().psim_run(self._h, max_rounds, st, cap, C.byref(ran)))
-        return [s.as_dict() for s in st[: min(ran.value, cap)]], ran.value
+        k = min(ran.value, cap)
+        if not as_dicts:
+            return np.frombuffer(st, dtype=_ROUND_DTYPE, count=k).copy(), ran.value
+        return [s.as_dict() for s in st[:k]], ran.value
 
     def plumtree_state(self):
         n = self.n

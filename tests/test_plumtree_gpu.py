@@ -804,3 +804,36 @@ def test_build_tree_overlays_lockstep(psim, arity, n, cycles):
         compare(sim, orc, 0, m)
         lockstep(sim, orc, 0, m)
         assert sim.delivered().all()
+
+
+@pytest.mark.parametrize("cap,thr", [("1", None), ("2", "100000000"), (None, "100000000"), ("3", None)])
+def test_worklist_overflow_and_forced_list_mode(psim, monkeypatch, cap, thr):
+    """The sparse-round worklist is an optimisation over the
+    group flags: with list shards of 1-3 entries every sparse round overflows
+    and must fall back to the flags, and with the list threshold above any
+    round's count every round lists its groups (dense ones too, overflowing
+    or not).  Either way the rounds equal the oracle's, over a flood, tree
+    heartbeats with i_have / graft (L = 2: tick rounds with rows read the
+    flags) and dead vertices."""
+    if psim.engine != "slot_scatter":
+        pytest.skip("worklist: ELL rows on the slot-scatter engine")
+    if cap:
+        monkeypatch.setenv("PSIM_WL_CAP", cap)
+    if thr:
+        monkeypatch.setenv("PSIM_WL_THR", thr)
+    n = 2500
+    rp, col = psim.overlay.random_regular(n, 5, 91)
+    for L in (1, 2):
+        sim, orc = make(psim, rp, col, L)
+        root = 17
+        for hb in range(3):
+            if hb == 2:
+                alive = np.ones(n, np.uint8)
+                alive[np.random.default_rng(3).choice(n, n // 15, replace=False)] = 0
+                alive[root] = 1
+                sim.set_alive(alive)
+                orc.set_alive(alive)
+            m = sim.broadcast(root)
+            assert m == orc.heartbeat(root)
+            lockstep(sim, orc, root, m)
+        sim.close()
