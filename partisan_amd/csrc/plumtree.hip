@@ -29,6 +29,8 @@ namespace psim {
 
 namespace {
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));   // 16-byte vector for non-temporal access
+
 __device__ __forceinline__ bool bit_alive(const uint32_t* __restrict__ alive, uint32_t v) {
     return (alive[v >> 5] >> (v & 31)) & 1u;
 }
@@ -366,8 +368,14 @@ __device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x,
 // in "holds outstanding rows" (-1, 0, +1).
 __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint4& st, const VSt& x, Ctr& c) {
     const uint32_t nw = x.myround | (x.rseq << 16) | (x.ep << 24);
-    if (x.eager != st.x || x.lazy != st.y || x.outst != st.z || nw != st.w)
+    if (x.eager != st.x || x.lazy != st.y || x.outst != st.z || nw != st.w) {
+#ifndef PT_TEMPORAL_STATE_STORE     // the record is not read again this round: 2.34 -> 2.27 ms per 10M flood
+        u32x4_t q = {x.eager, x.lazy, x.outst, nw};
+        __builtin_nontemporal_store(q, reinterpret_cast<u32x4_t*>(a.vs) + v);
+#else
         a.vs[v] = make_uint4(x.eager, x.lazy, x.outst, nw);
+#endif
+    }
     c.live_delta += (uint32_t)x.live_delta;
     if ((x.outst0 != 0) != (x.outst != 0)) {
         a.ost[v] = x.outst != 0;
@@ -398,6 +406,33 @@ constexpr uint32_t kFastDeg = 8;
 // kCap (>= deg): the register arrays' size.  The ELL kernel is instantiated
 // per row-width class (4 / 6 / 8) so a 5-wide HyParView row holds 6 slots in
 // registers, not 8: fewer VGPRs, more waves per SIMD to hide the chain.
+// Streaming loads: the inbox words a round sweeps are read once and are stale
+// after it, so the sweep loads them non-temporally and they do not displace
+// the lines the round scatters its own words into (2.43 -> 2.33 ms per 10M
+// flood, profiles/r02/experiments/ab_nt_loads.txt).  Rows and state records
+// are re-read every round: non-temporal loads of those were slower (A/B
+// macros PT_NT_ROWS, PT_NT_STATE).
+template <bool kNt, class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+    if constexpr (kNt) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+#ifdef PT_NT_ROWS
+constexpr bool kNtRows = true;
+#else
+constexpr bool kNtRows = false;
+#endif
+#ifndef PT_TEMPORAL_SWEEP      // A/B: 2.43 -> 2.33 ms per 10M flood with the sweep non-temporal
+constexpr bool kNtSweep = true;
+#else
+constexpr bool kNtSweep = false;
+#endif
+#ifdef PT_NT_STATE
+constexpr bool kNtState = true;
+#else
+constexpr bool kNtState = false;
+#endif
+
 template <uint32_t kCap>
 struct VLoad {
     uint4 st;
@@ -414,13 +449,18 @@ template <uint32_t kCap>
 __device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, VLoad<kCap>& L,
                                       bool rows = true) {
     L.aw = a.alive[(a.v_lo + v) >> 5];
-    L.st = a.vs[v];
+    if constexpr (kNtState) {
+        const u32x4_t q = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.vs) + v);
+        L.st = make_uint4(q.x, q.y, q.z, q.w);
+    } else {
+        L.st = a.vs[v];
+    }
     L.rows = rows;
     if (a.ecol) {                // ELL packed rows: half the row bytes
         const uint32_t W = a.ell;
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) {
-            const uint32_t p = (rows && s < deg) ? a.ecol[rs + s] : 0u;
+            const uint32_t p = (rows && s < deg) ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
             L.cl[s] = p == kNoPeer ? kNoPeer : p >> 3;
             L.rv[s] = p == kNoPeer ? 0u : (p >> 3) * W + (p & 7u);
         }
@@ -834,8 +874,12 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
                     const uint32_t i = q / gq, r = (q % gq) * 4u;
                     li[k] = q < nq ? pos(i) * gw + r : 0xFFFFFFFFu;
                     gi[k] = q < nq ? gv(i) * W + r : nW;
-                    wv[k] = gi[k] + 4 <= nW ? *reinterpret_cast<const uint4*>(a.in_cur + gi[k])
-                                            : make_uint4(0, 0, 0, 0);
+                    if (gi[k] + 4 <= nW) {
+                        const u32x4_t q = ld_stream<kNtSweep>(reinterpret_cast<const u32x4_t*>(a.in_cur + gi[k]));
+                        wv[k] = make_uint4(q.x, q.y, q.z, q.w);
+                    } else {
+                        wv[k] = make_uint4(0, 0, 0, 0);
+                    }
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < kSweepU; k++) {
