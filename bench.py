@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
+    p.add_argument("--force-sharded", action="store_true",
+                   help="measurement aid: drive one GPU through the sharded engine (psim_shard_run, world 1)")
     p.add_argument("--csr", action="store_true", help="A/B: CSR slot rows instead of ELL rows (DESIGN.md 4)")
     p.add_argument("--round-events", action="store_true",
                    help="a hipEvent pair around every round kernel (the markers cost ~10 us between rounds); "
@@ -183,14 +185,22 @@ def main():
     rank, local, world, pg = dist_setup(args)
     import numpy as np  # noqa: F401
 
+    sharded = (world > 1 or args.force_sharded) and args.mode == "sharded"
+    if sharded:
+        # the sharded engine allocates its exchange buffers with torch: bring
+        # torch's HIP runtime up before libpsim is loaded (as the multi-GPU
+        # launch does in dist_setup), so both share it
+        import torch
+        torch.cuda.set_device(local)
+        torch.empty(1, device=torch.device("cuda", local))
     import partisan_amd as pa
 
-    sharded = world > 1 and args.mode == "sharded"
     rp, col = pa.overlay.random_regular(args.n, args.peers, args.seed)
     if sharded:
         from partisan_amd.shard import ShardedPlumtree
         sp = ShardedPlumtree(rp, col, rank, world, device=local, backend=args.transport,
-                             lazy_tick_rounds=args.lazy_tick_rounds, csr=args.csr)
+                             lazy_tick_rounds=args.lazy_tick_rounds, csr=args.csr,
+                             chunk_timing=not args.round_events)
         sim = sp.sim
     else:
         sp = None

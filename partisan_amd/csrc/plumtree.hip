@@ -1392,15 +1392,25 @@ __global__ __launch_bounds__(kBlock) void pt_compact_kernel(PtArgs a, const uint
 }
 
 // Scatter records received from other shards into the local receiver slots.
+// Sharded rounds with per-round counts (psim_shard_run): the words received
+// count as messages of the round that sent them (PtArgs::mcnt slot m_w), so
+// the next round's no-op test and flag-free decision see remote senders too.
+__device__ __forceinline__ void ingest_count(const PtArgs& a, uint32_t c) {
+    if (!a.mcnt) return;
+    const unsigned long long s = wave_sum((unsigned long long)c);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(&a.mcnt[a.m_w * 64 + (blockIdx.x & 63)], (uint32_t)s);
+}
+
 __global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2* __restrict__ rec, uint32_t nrec,
                                                            const uint32_t* __restrict__ slot2v) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nrec) return;
-    const uint2 r = rec[i];
-    if (!r.y) return;                                   // padding of a fixed-size record region
-    const uint32_t ls = r.x - a.slot_base;
-    a.in_nxt[ls] = r.y;
-    a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+    const uint2 r = i < nrec ? rec[i] : make_uint2(0u, 0u);
+    if (r.y) {                                          // else padding of a fixed-size record region
+        const uint32_t ls = r.x - a.slot_base;
+        a.in_nxt[ls] = r.y;
+        a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+    }
+    ingest_count(a, r.y ? 1u : 0u);
 }
 
 // Dense exchange (no counts, no host sync): word i of the send buffer is the
@@ -1422,13 +1432,16 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const
                                                                  const uint32_t* __restrict__ recv_map, uint32_t nrecv,
                                                                  const uint32_t* __restrict__ slot2v) {
     const uint32_t stride = gridDim.x * kBlock;
+    uint32_t c = 0;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrecv; i += stride) {
         const uint32_t w = recv[i];
         if (!w) continue;
         const uint32_t ls = recv_map[i];
         a.in_nxt[ls] = w;
         a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+        c++;
     }
+    ingest_count(a, c);
 }
 
 uint32_t grid_chunks(uint32_t n) { return (n + kChunkV - 1) / kChunkV; }

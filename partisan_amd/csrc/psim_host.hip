@@ -175,7 +175,16 @@ struct psim_handle {
         // on the words the round can send (shard_drive_fast); plan_ok: the lane's
         // global counts g_inflight / g_ost are current, so the bound holds
         uint2 *xrs = nullptr, *xrr = nullptr;
+        uint8_t* xrs_raw = nullptr;            // [256 B: per-peer cursors][records]: one memset clears both
+        uint32_t* xcur = nullptr;
         uint64_t rec_thr = 0;
+        // shard_drive_fast under PSIM_CFG_CHUNK_TIMING: no event markers and no stats
+        // memset between a chunk's kernels; one event pair per chunk (rev_[0], rev_[1])
+        bool chunk_mode = false;
+        // shard_drive_fast: per-round message counts on (PtArgs::mcnt) -- the
+        // round kernels' no-op exit and flag-free dense rounds, fed by the
+        // ingests with the words received
+        bool mcnt_on = false;
         uint32_t max_deg_g = 0;
         bool plan_ok = false;
         hipEvent_t xev[2 * 16] = {};                   // exchange start / end per pending round
@@ -332,11 +341,13 @@ void free_graph(psim_handle* h) {
     }
     auto& sh = h->sh;
     void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map, sh.xsend, sh.xrecv,
-                  sh.xrs, sh.xrr};
+                  sh.xrs_raw, sh.xrr};
     for (void* p : sp)
         if (p) (void)hipFree(p);
     sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = sh.xsend = sh.xrecv = nullptr;
     sh.xrs = sh.xrr = nullptr;
+    sh.xrs_raw = nullptr;
+    sh.xcur = nullptr;
     sh.plan_ok = false;
     sh.recv_base.clear();
     sh.pending = 0;
@@ -518,7 +529,10 @@ int to_window(psim_handle* h) {
 // the next round reads every group's words with its coalesced sweep (the
 // same decision, taken from the same count, on both sides).
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
-    if (h->sh.world != 1 || h->bin.rec_c || h->dly) return;   // delays: a silent round may precede arrivals
+    // delays: a silent round may precede arrivals; sharded handles: only
+    // psim_shard_run's rounds keep the counts (sh.mcnt_on: ingests add the
+    // words received to them)
+    if ((h->sh.world != 1 && !h->sh.mcnt_on) || h->bin.rec_c || h->dly) return;
     a.mcnt = h->mcnt_base + kMcntLane * size_t(h->cur_lane);
     a.m_w = uint32_t(R % 4);
     a.m_s = uint32_t((R + 3) % 4);
@@ -1558,6 +1572,7 @@ int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t
     HIPCHK(h, scrub_if_needed(h, h->round + 1));
     HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, h->stats);
+    set_round_slots(h, a, h->round + 1);         // one shard: the counts every path keeps
     HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
     HIPCHK(h, launch_pt_round(a, h->stream));
     HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
@@ -1639,15 +1654,16 @@ static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k) {
     const uint32_t tick = ((h->round + 1) % L) == 0;
     unsigned long long* row = sh.ring + size_t(sh.pending) * kStatsRow;
     HIPCHK(h, scrub_if_needed(h, h->round + 1));
-    HIPCHK(h, hipMemsetAsync(row, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+    const bool marks = !sh.chunk_mode;           // chunk mode: rows zeroed and timed per chunk by the driver
+    if (marks) HIPCHK(h, hipMemsetAsync(row, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, row);
-    HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
+    set_round_slots(h, a, h->round + 1);         // off unless shard_drive_fast turned the counts on
+    if (marks) HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
     HIPCHK(h, launch_pt_round(a, h->stream));
-    HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending + 1], h->stream));
+    if (marks) HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending + 1], h->stream));
     if (sh.world > 1 && rec_k) {
-        HIPCHK(h, hipMemsetAsync(sh.cursor, 0, sh.world * 4, h->stream));
-        HIPCHK(h, hipMemsetAsync(sh.xrs, 0, size_t(sh.world - 1) * rec_k * 8, h->stream));
-        HIPCHK(h, launch_pt_compact(a, sh.rem, sh.blk, sh.nblk, nullptr, sh.cursor, sh.xrs, h->stream, rec_k,
+        HIPCHK(h, hipMemsetAsync(sh.xrs_raw, 0, 256 + size_t(sh.world - 1) * rec_k * 8, h->stream));
+        HIPCHK(h, launch_pt_compact(a, sh.rem, sh.blk, sh.nblk, nullptr, sh.xcur, sh.xrs, h->stream, rec_k,
                                     (uint32_t)sh.rank));
     } else if (sh.world > 1) {
         HIPCHK(h, launch_pt_pack_dense(a, sh.rem, (uint32_t)sh.send_base[sh.world], (uint32_t*)send_dev, h->stream));
@@ -1681,6 +1697,7 @@ int ingest_dense(psim_handle* h, const void* recv_dev) {
     if (!recv_dev) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
+    set_round_slots(h, a, h->round);                      // counts: the round that sent them (m_w)
     HIPCHK(h, launch_pt_ingest_dense(a, (const uint32_t*)recv_dev, sh.recv_map, (uint32_t)nr, sh.slot2v, h->stream));
     return PSIM_OK;
 }
@@ -1701,7 +1718,12 @@ int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32
         unsigned long long r[kNStat];
         reduce_row(hs.data() + size_t(i) * kStatsRow, r);
         float ms = 0.f;
-        HIPCHK(h, hipEventElapsedTime(&ms, sh.rev_[2 * i], sh.rev_[2 * i + 1]));
+        if (sh.chunk_mode) {                      // the chunk's device time (kernels + exchange) / its rounds
+            HIPCHK(h, hipEventElapsedTime(&ms, sh.rev_[0], sh.rev_[1]));
+            ms /= float(k);
+        } else {
+            HIPCHK(h, hipEventElapsedTime(&ms, sh.rev_[2 * i], sh.rev_[2 * i + 1]));
+        }
         if (r[S_OVERFLOW]) return fail(h, PSIM_EOVERFLOW, "async round: overflow flags 0x%llx", r[S_OVERFLOW]);
         uint64_t msgs = 0;
         for (int t = 1; t <= 5; t++) msgs += r[t];
@@ -1769,8 +1791,10 @@ int x_buffers(psim_handle* h) {
     const size_t ns = std::max<uint64_t>(1, sh.send_base[sh.world]), nr = std::max<uint64_t>(1, sh.recv_base[sh.world]);
     const size_t nrec = std::max<uint64_t>(1, (sh.world - 1) * sh.rec_thr);
     if (hipMalloc((void**)&sh.xsend, ns * 4) != hipSuccess || hipMalloc((void**)&sh.xrecv, nr * 4) != hipSuccess ||
-        hipMalloc((void**)&sh.xrs, nrec * 8) != hipSuccess || hipMalloc((void**)&sh.xrr, nrec * 8) != hipSuccess)
+        hipMalloc((void**)&sh.xrs_raw, 256 + nrec * 8) != hipSuccess || hipMalloc((void**)&sh.xrr, nrec * 8) != hipSuccess)
         return fail(h, PSIM_ENOMEM, "exchange buffers");
+    sh.xcur = reinterpret_cast<uint32_t*>(sh.xrs_raw);           // <= 64 shards
+    sh.xrs = reinterpret_cast<uint2*>(sh.xrs_raw + 256);
     HIPCHK(h, hipMemsetAsync(sh.xsend, 0, ns * 4, h->stream));
     HIPCHK(h, hipMemsetAsync(sh.xrecv, 0, nr * 4, h->stream));
     return PSIM_OK;
@@ -1781,7 +1805,8 @@ int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k
     auto& sh = h->sh;
     if (sh.world == 1) return PSIM_OK;
     std::string err;
-    HIPCHK(h, hipEventRecord(sh.xev[2 * slot], h->stream));
+    const bool marks = !sh.chunk_mode;
+    if (marks) HIPCHK(h, hipEventRecord(sh.xev[2 * slot], h->stream));
     if (rec_k) {        // fixed-size record regions: 2 rec_k words per peer, none to self
         const int W = sh.world;
         std::vector<uint64_t> off(size_t(W) + 1, 0);
@@ -1789,16 +1814,17 @@ int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k
         int rc = sh.xport->alltoallv(reinterpret_cast<const uint32_t*>(sh.xrs), off.data(),
                                      reinterpret_cast<uint32_t*>(sh.xrr), off.data(), sh.rank, W, h->stream, &err);
         if (rc) return fail(h, rc, "exchange: %s", err.c_str());
-        HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
+        if (marks) HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
         if (xs) xs->fabric_bytes += 8ull * rec_k * uint64_t(W - 1);
         PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
+        set_round_slots(h, a, h->round);                      // counts: the round that sent them (m_w)
         HIPCHK(h, launch_pt_ingest(a, sh.xrr, uint32_t(uint64_t(W - 1) * rec_k), sh.slot2v, h->stream));
         return PSIM_OK;
     }
     int rc = sh.xport->alltoallv(sh.xsend, sh.send_base.data(), sh.xrecv, sh.recv_base.data(), sh.rank, sh.world,
                                  h->stream, &err);
     if (rc) return fail(h, rc, "exchange: %s", err.c_str());
-    HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
+    if (marks) HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
     if (xs) xs->fabric_bytes += 4ull * (sh.send_base[sh.world] - (sh.send_base[sh.rank + 1] - sh.send_base[sh.rank]));
     return ingest_dense(h, sh.xrecv);
 }
@@ -2047,8 +2073,32 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
         bM = double(h->lanes[h->cur_lane].g_inflight);
         bH = double(h->lanes[h->cur_lane].g_ost);
     }
+    // PSIM_CFG_CHUNK_TIMING: no event marker or stats memset between a chunk's
+    // launches (each cost ~10 us of idle GPU between dependent kernels); the
+    // chunk's rows are zeroed at once and it is timed by one event pair
+    struct ChunkMode {
+        psim_handle* h;
+        ~ChunkMode() { h->sh.chunk_mode = h->sh.mcnt_on = false; }
+    } chunk_guard{h};
+    sh.chunk_mode = (h->cfg.flags & PSIM_CFG_CHUNK_TIMING) != 0;
+    // per-round counts from here on (several shards): the ring starts empty except the count the
+    // first round reads as its previous round's, which is seeded 1 (words may
+    // wait from a broadcast or from rounds run without counts: no no-op exit,
+    // group flags written and read -- what every other path does)
+    // (one shard: the counts are kept by every path, as on a plain handle)
+    if (sh.world > 1 && h->bin.rec_c == nullptr && !h->dly && !h->lanes.empty()) {
+        uint32_t* mc = h->mcnt_base + kMcntLane * size_t(h->cur_lane);
+        HIPCHK(h, hipMemsetAsync(mc, 0, kMcntLane * sizeof(uint32_t), h->stream));
+        HIPCHK(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mc + (h->round % 4) * 64), 1, 1, h->stream));
+        sh.mcnt_on = true;
+    }
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(K, max_rounds - ran);
+        if (sh.chunk_mode) {
+            if (sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
+            HIPCHK(h, hipMemsetAsync(sh.ring, 0, size_t(k) * kStatsRow * sizeof(unsigned long long), h->stream));
+            HIPCHK(h, hipEventRecord(sh.rev_[0], h->stream));
+        }
         for (uint32_t j = 0; j < k; j++) {
             uint32_t rec_k = 0;
             if (sh.plan_ok && sh.world > 1) {
@@ -2062,6 +2112,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
             rc = x_exchange(h, (int)j, xs, rec_k);
             if (rc) return rc;
         }
+        if (sh.chunk_mode) HIPCHK(h, hipEventRecord(sh.rev_[1], h->stream));
         psim_round_stats st[K];
         int64_t live[K];
         uint32_t got = 0;
@@ -2071,8 +2122,9 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
             xs->rounds += got;
             for (uint32_t j = 0; j < got; j++) {
                 xs->kernel_ms += st[j].kernel_ms;
-                float ms = 0.f;
-                if (h->sh.world > 1) HIPCHK(h, hipEventElapsedTime(&ms, h->sh.xev[2 * j], h->sh.xev[2 * j + 1]));
+                float ms = 0.f;      // chunk mode: the exchange is inside kernel_ms (one event pair per chunk)
+                if (h->sh.world > 1 && !sh.chunk_mode)
+                    HIPCHK(h, hipEventElapsedTime(&ms, h->sh.xev[2 * j], h->sh.xev[2 * j + 1]));
                 xs->exchange_ms += ms;
             }
         }

@@ -62,13 +62,20 @@ def gloo_transport():
 
 class ShardedPlumtree:
     def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None,
-                 csr=False):
+                 csr=False, chunk_timing=False):
         """csr: keep CSR slot rows (PSIM_CFG_CSR) instead of the ELL rows every
-        shard uses when the overlay's widest row has <= 8 slots."""
+        shard uses when the overlay's widest row has <= 8 slots.  chunk_timing:
+        psim_shard_run times each 4-round chunk with one event pair and puts no
+        marker between its kernels (PSIM_CFG_CHUNK_TIMING; kernel_ms then
+        includes the exchange)."""
         self.rank, self.world, self.backend = rank, world, backend
         self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
-        self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world, csr=csr)
+        # torch's HIP runtime first: brought up after libpsim's RCCL communicator
+        # it finds no device (torch ships its own libamdhip64)
+        torch.cuda.set_device(self.dev)
+        self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world, csr=csr,
+                             chunk_timing=chunk_timing)
         self._h = self.sim._h
         self.last_exchange = {}
         self.exchange_total = {}      # psim_exchange_stats summed over runs (this rank)

@@ -49,7 +49,7 @@ def _gpu_worker(rank, world, port, n, seed, L, transport, csr, q):
         import pyoracle as O
         rp, col = pa.overlay.random_regular(n, 5, seed)
         sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L, transport=transport,
-                             csr=csr)
+                             csr=csr, chunk_timing=(seed % 2 == 0))   # world 4: chunk events, no markers
         orc = O.Plumtree(rp, col, L)
         sim = sp.sim
         root = 7
