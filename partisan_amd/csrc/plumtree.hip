@@ -863,7 +863,11 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             // A group's 16 W words start on a 16-byte boundary: read them as
             // quads, kSweepU quads per thread in flight before any is used (the
             // word-at-a-time loop waited out one load latency per word).
-            constexpr uint32_t kSweepU = 4;
+#ifndef PT_SWEEP_U
+            constexpr uint32_t kSweepU = 8;   // a dense round's 5 quads per thread all in flight at once
+#else
+            constexpr uint32_t kSweepU = PT_SWEEP_U;
+#endif
             const uint32_t gq = gw >> 2, nq = ng * gq;
             for (uint32_t q0 = 0; q0 < nq; q0 += kBlock * kSweepU) {
                 uint4 wv[kSweepU];
