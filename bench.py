@@ -242,14 +242,38 @@ def main():
 
     verified = verify(sim, pg, args.n, rounds_per_step)
     exchange = None
+    counted = sum(rounds_per_step)
     if sp is not None:   # the in-library exchange (psim_shard_run): fabric bytes and device time per step
         xt = sp.exchange_total
+        chunk_ms = float(xt.get("kernel_ms", 0.0)) / args.steps
+        timed_rounds = float(xt.get("rounds", 0)) / args.steps
+        fabric = float(xt.get("fabric_bytes", 0))
+        if not args.round_events:
+            # the timed chunks carry one event pair each, so their time holds the
+            # exchanges too: one more step (outside the timed region) with an event
+            # pair around every round kernel and every exchange gives the kernel's
+            # own launch time for the roofline and the exchange time
+            sp.sim.set_chunk_timing(False)
+            sp.local_algo_bytes, sp.local_kernel_ms, sp.exchange_total = 0, 0.0, {}
+            _, r_inst = step()
+            algo_bytes, round_ms, counted = sp.local_algo_bytes, sp.local_kernel_ms, r_inst
+            xi = sp.exchange_total
+            kernel_ms_step, exchange_ms_step = float(xi.get("kernel_ms", 0.0)), float(xi.get("exchange_ms", 0.0))
+            sp.sim.set_chunk_timing(True)
+        else:
+            kernel_ms_step = chunk_ms
+            exchange_ms_step = float(xt.get("exchange_ms", 0.0)) / args.steps
         exchange = {
             "transport": sp.transport,
-            "fabric_bytes_per_step": sum_over_ranks(pg, float(xt.get("fabric_bytes", 0))) / args.steps,
-            "exchange_ms_per_step_max_rank": max_over_ranks(pg, float(xt.get("exchange_ms", 0.0))) / args.steps,
-            "kernel_ms_per_step_max_rank": max_over_ranks(pg, float(xt.get("kernel_ms", 0.0))) / args.steps,
-            "rounds_enqueued_per_step": float(xt.get("rounds", 0)) / args.steps,
+            "fabric_bytes_per_step": sum_over_ranks(pg, fabric) / args.steps,
+            "exchange_ms_per_step_max_rank": max_over_ranks(pg, exchange_ms_step),
+            "kernel_ms_per_step_max_rank": max_over_ranks(pg, kernel_ms_step),
+            "device_ms_per_step_max_rank": max_over_ranks(pg, chunk_ms if not args.round_events
+                                                         else kernel_ms_step + exchange_ms_step),
+            "rounds_enqueued_per_step": timed_rounds,
+            "timing": ("kernel / exchange split from one extra step with an event pair per round kernel and "
+                       "exchange; device time per step from the timed steps' chunk events"
+                       if not args.round_events else "event pairs per round kernel and exchange"),
         }
 
     step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
@@ -258,7 +282,6 @@ def main():
     value = peer_rounds / step_s
     # per-launch figures over the rounds up to quiescence (the no-op tail of a
     # step's last chunk is not counted): hipEvent durations of each launch
-    counted = sum(rounds_per_step)
     avg_launch_ms = round_ms / max(1, counted)
     achieved_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
 

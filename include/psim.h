@@ -611,6 +611,11 @@ int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, cons
 
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
+/* Switch PSIM_CFG_CHUNK_TIMING on (chunk != 0) or off after creation: one event
+ * pair per chunk (round kernels back to back; on a sharded handle the chunk's
+ * time includes its exchanges) or a pair per round kernel (kernel-only times,
+ * at ~10 us of idle GPU per marker).  Not while async rounds are pending. */
+int  psim_set_chunk_timing(psim_handle* h, int chunk);
 
 #ifdef __cplusplus
 }

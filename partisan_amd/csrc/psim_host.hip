@@ -2758,6 +2758,14 @@ int psim_trace_hash(const psim_handle* h, uint64_t* out) {
     return PSIM_OK;
 }
 
+int psim_set_chunk_timing(psim_handle* h, int chunk) {
+    if (!h) return PSIM_EINVAL;
+    if (h->sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
+    if (chunk) h->cfg.flags |= PSIM_CFG_CHUNK_TIMING;
+    else h->cfg.flags &= ~PSIM_CFG_CHUNK_TIMING;
+    return PSIM_OK;
+}
+
 int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds) {
     if (!h) return PSIM_EINVAL;
     if (round_kernel_ms) *round_kernel_ms = h->kernel_ms_total;

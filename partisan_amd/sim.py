@@ -225,6 +225,10 @@ class Simulator:
         self._c(lib().psim_trace_hash(self._h, out))
         return tuple(int(x) for x in out)
 
+    def set_chunk_timing(self, chunk):
+        """psim_set_chunk_timing: one event pair per chunk (True) or per round kernel."""
+        self._c(lib().psim_set_chunk_timing(self._h, 1 if chunk else 0))
+
     def timing(self):
         ms = C.c_double()
         r = C.c_uint64()
