@@ -256,3 +256,109 @@ def test_c3_1m_invariants():
     assert checked > 19000
     print(f"C3 1M: heartbeat reached {reach:.3f} of live vertices 39 rounds after it")
     sim.close()
+
+
+def _sharded_world1_worker(rank, world, port, n, q):
+    """psim_shard_run (world 1, RCCL, chunk events) on the bench overlay: the
+    same per-round global counts and final trace hash as a plain handle, two
+    heartbeats (a flood from a fresh tree, then one over the tree)."""
+    try:
+        sys.path.insert(0, ROOT)
+        import torch
+        torch.cuda.set_device(0)
+        torch.empty(1, device="cuda:0")              # torch's HIP runtime before libpsim's
+        import partisan_amd as pa
+        from partisan_amd.shard import ShardedPlumtree
+        rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
+        plain = pa.Simulator(device=0, chunk_timing=True)
+        plain.load_overlay(rp, col)
+        sp = ShardedPlumtree(rp, col, 0, 1, device=0, backend="nccl", chunk_timing=True)
+        for hb in range(2):
+            if hb == 0:
+                plain.reset_trees()
+                sp.reset_trees()
+            assert plain.broadcast(0) == sp.broadcast(0)
+            a, ra = plain.run()
+            b, rb = sp.run()
+            assert ra == rb, (ra, rb)
+            for x, y in zip(a, b):
+                for k in KINDS + ("delivered_new", "senders", "sender_degree_sum"):
+                    assert x[k] == y[k], (hb, k, x, y)
+            assert plain.trace_hash()[:3] == sp.sim.trace_hash()[:3]
+        sp.close()
+        plain.close()
+        q.put((0, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((0, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_bench_config_10m_sharded_engine_matches_plain_handle():
+    """The sharded engine's own machinery (per-round counts fed by nothing at
+    one shard, the worklist, chunk events, the record bound) at the bench
+    size, against the plain handle round by round."""
+    res = run_world(_sharded_world1_worker, 1, 10_000_000, timeout=600)
+    assert res[0] == "ok", res[0]
+
+
+def _sharded_world2_worker(rank, world, port, n, q):
+    """Two shards on one GPU (gloo transport, the in-library loop: seeded
+    per-round counts fed by the ingests, record regions for the sparse rounds,
+    chunk events) against a plain handle at 1M: per-round global counts and
+    the summed trace hashes."""
+    try:
+        sys.path.insert(0, ROOT)
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.cuda.set_device(0)
+        torch.empty(1, device="cuda:0")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import partisan_amd as pa
+        from partisan_amd.shard import ShardedPlumtree
+        rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", transport="callback", chunk_timing=True)
+        plain = None
+        if rank == 0:
+            plain = pa.Simulator(device=0)
+            plain.load_overlay(rp, col)
+        M = 0xFFFFFFFFFFFFFFFF
+        for hb in range(2):
+            if hb == 0:
+                sp.reset_trees()
+                if plain:
+                    plain.reset_trees()
+            m = sp.broadcast(0)
+            b, rb = sp.run()
+            th = sp.sim.trace_hash()
+            t = torch.tensor([th[0] & 0x7FFFFFFF, th[1] & 0x7FFFFFFF, th[2], (th[0] >> 31), (th[1] >> 31)],
+                             dtype=torch.int64)
+            dist.all_reduce(t)
+            if plain:
+                assert plain.broadcast(0) == m
+                a, ra = plain.run()
+                assert ra == rb, (hb, ra, rb)
+                for x, y in zip(a, b):
+                    for k in KINDS + ("delivered_new", "senders", "sender_degree_sum"):
+                        assert x[k] == y[k], (hb, k, x, y)
+                ph = plain.trace_hash()
+                got = [(int(t[0]) + (int(t[3]) << 31)) & M, (int(t[1]) + (int(t[4]) << 31)) & M, int(t[2])]
+                assert got == [ph[0], ph[1], ph[2]], (got, ph)
+            assert sp.last_exchange["fabric_bytes"] > 0
+        sp.close()
+        if plain:
+            plain.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_sharded_world2_1m_matches_plain_handle():
+    res = run_world(_sharded_world2_worker, 2, 1_000_000, timeout=600)
+    for r in range(2):
+        assert res[r] == "ok", res[r]
