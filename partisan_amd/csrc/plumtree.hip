@@ -934,7 +934,12 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
 }
 
 template <bool kFault, uint32_t kCap>
-__global__ __launch_bounds__(kBlock) void pt_round_ell_kernel(PtArgs a) {
+#ifdef PT_WAVES_PER_EU
+#define PT_ELL_ATTR __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU, PT_WAVES_PER_EU)))
+#else
+#define PT_ELL_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) PT_ELL_ATTR void pt_round_ell_kernel(PtArgs a) {
     pt_round_ell_body<kFault, kCap>(a);
 }
 
