@@ -683,7 +683,7 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
     // (no inbox flag can be set), so the whole round is a no-op
     if (prev == 0 && !rows_due) return false;
     // many senders expected: no group flags this round; few: flags + worklist
-    m.mark = prev >= a.dense ? 0u : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
+    m.mark = prev >= a.dense ? (a.force_flags ? 1u : 0u) : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
     m.all_in = prev2 >= a.dense;                       // the last round wrote none: every group is read
     // the last round's senders listed every group they flagged (the same
     // test on the same count) and no row is due: only the listed groups
@@ -1410,14 +1410,33 @@ __device__ __forceinline__ void ingest_count(const PtArgs& a, uint32_t c) {
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(&a.mcnt[a.m_w * 64 + (blockIdx.x & 63)], (uint32_t)s);
 }
 
+// The group-flag mode of the round whose words an ingest delivers: the same
+// decision its local senders took (round_counts), from the same count, so a
+// flag-free round's remote words set no flag either and a listed round's are
+// listed.  Without counts: flags.  Uniform call (barrier).
+__device__ __forceinline__ uint32_t ingest_mark(const PtArgs& a) {
+    if (!a.mcnt) return 1u;
+    __shared__ uint32_t pm;
+    if (threadIdx.x < 64) {
+        uint32_t c = a.mcnt[a.m_s * 64 + threadIdx.x];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+        if (threadIdx.x == 0) pm = c;
+    }
+    __syncthreads();
+    const uint32_t prev = pm;
+    return prev >= a.dense ? (a.force_flags ? 1u : 0u) : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
+}
+
 __global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2* __restrict__ rec, uint32_t nrec,
                                                            const uint32_t* __restrict__ slot2v) {
+    const uint32_t mark = ingest_mark(a);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint2 r = i < nrec ? rec[i] : make_uint2(0u, 0u);
     if (r.y) {                                          // else padding of a fixed-size record region
         const uint32_t ls = r.x - a.slot_base;
         a.in_nxt[ls] = r.y;
-        a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+        mark_group(a, slot2v[ls] >> kGroupShift, mark, nullptr);
     }
     ingest_count(a, r.y ? 1u : 0u);
 }
@@ -1440,6 +1459,7 @@ __global__ __launch_bounds__(kBlock) void pt_pack_dense_kernel(PtArgs a, const u
 __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const uint32_t* __restrict__ recv,
                                                                  const uint32_t* __restrict__ recv_map, uint32_t nrecv,
                                                                  const uint32_t* __restrict__ slot2v) {
+    const uint32_t mark = ingest_mark(a);
     const uint32_t stride = gridDim.x * kBlock;
     uint32_t c = 0;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrecv; i += stride) {
@@ -1447,7 +1467,7 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const
         if (!w) continue;
         const uint32_t ls = recv_map[i];
         a.in_nxt[ls] = w;
-        a.pend_nxt[slot2v[ls] >> kGroupShift] = 1;
+        mark_group(a, slot2v[ls] >> kGroupShift, mark, nullptr);
         c++;
     }
     ingest_count(a, c);

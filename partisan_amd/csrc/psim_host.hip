@@ -528,6 +528,17 @@ int to_window(psim_handle* h) {
 // 16-vertex groups to receive words, so its senders write no group flags and
 // the next round reads every group's words with its coalesced sweep (the
 // same decision, taken from the same count, on both sides).
+// Message count under which a round lists the groups it flags (0: no list).
+// Several shards need it below the flag-free count (n / 4): psim_shard_run
+// seeds its first round's predecessor-but-one with it (flag mode, no list).
+uint32_t list_threshold(const psim_handle* h) {
+    if (!h->wl_cap) return 0;
+    const uint32_t ng = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
+    const uint32_t thr = h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
+    const uint32_t dense = std::max<uint32_t>(1u, h->n / 4);
+    return (h->sh.world > 1 && thr >= dense) ? 0u : thr;
+}
+
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     // delays: a silent round may precede arrivals; sharded handles: only
     // psim_shard_run's rounds keep the counts (sh.mcnt_on: ingests add the
@@ -539,13 +550,13 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     a.m_r = uint32_t((R + 2) % 4);
     a.m_z = uint32_t((R + 1) % 4);
     a.dense = std::max<uint32_t>(1u, h->n / 4);
-    if (h->wl_cap) {          // sparse rounds: the groups written are listed
-        const uint32_t ng = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
+    const uint32_t thr = list_threshold(h);
+    if (thr) {                // sparse rounds: the groups written are listed
         a.wlcnt = a.mcnt + 256;
         a.wl_cur = reinterpret_cast<uint32_t*>(a.pend_cur + h->wl_off);
         a.wl_nxt = reinterpret_cast<uint32_t*>(a.pend_nxt + h->wl_off);
         a.wl_cap = h->wl_cap;
-        a.wl_thr = h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
+        a.wl_thr = thr;
     }
 }
 
@@ -1228,7 +1239,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     // ng / 16 groups each after the flag bytes; an overflowing shard only
     // sends the next round back to the flags
     const size_t wl_off = (ng + 15) & ~size_t(15);
-    const bool wl_on = ell && W == 1 && !getenv("PSIM_NO_WORKLIST");   // A/B switch
+    const bool wl_on = ell && !getenv("PSIM_NO_WORKLIST");   // A/B switch
     uint32_t wl_cap = wl_on ? std::max<uint32_t>(64u, uint32_t((ng + 15) / 16)) : 0u;
     if (wl_on && getenv("PSIM_WL_CAP"))          // test knob: tiny shards exercise the overflow fallback
         wl_cap = std::max<uint32_t>(1u, uint32_t(strtoul(getenv("PSIM_WL_CAP"), nullptr, 10)));
@@ -1412,7 +1423,7 @@ int psim_plumtree_reset_trees(psim_handle* h) {
 
 namespace {
 
-int ingest_dense(psim_handle* h, const void* recv_dev);
+int ingest_dense(psim_handle* h, const void* recv_dev, bool force_flags = false);
 
 // The split-phase sharded entry points drive the focused lane's words only.
 int one_lane_only(psim_handle* h) {
@@ -1642,7 +1653,7 @@ int psim_shard_broadcast_dense(psim_handle* h, uint32_t root, uint32_t* mono_out
 // rec_k > 0 (in-library exchange only): this round's cross-shard words go out
 // as {receiver slot, word} records, rec_k per peer (sh.xrs), instead of the
 // dense regions.
-static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k) {
+static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k, bool force_flags = false) {
     if (!h) return PSIM_EINVAL;
     if (int rc = one_lane_only(h)) return rc;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
@@ -1658,6 +1669,7 @@ static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k) {
     if (marks) HIPCHK(h, hipMemsetAsync(row, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, row);
     set_round_slots(h, a, h->round + 1);         // off unless shard_drive_fast turned the counts on
+    a.force_flags = force_flags ? 1u : 0u;
     if (marks) HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending], h->stream));
     HIPCHK(h, launch_pt_round(a, h->stream));
     if (marks) HIPCHK(h, hipEventRecord(sh.rev_[2 * sh.pending + 1], h->stream));
@@ -1690,7 +1702,7 @@ int psim_shard_ingest_dense(psim_handle* h, const void* recv_dev) {
 
 namespace {
 // the focused lane's received words -> the inbox the next round reads
-int ingest_dense(psim_handle* h, const void* recv_dev) {
+int ingest_dense(psim_handle* h, const void* recv_dev, bool force_flags) {
     auto& sh = h->sh;
     const uint64_t nr = sh.recv_base.empty() ? 0 : sh.recv_base[sh.world];
     if (nr == 0) return PSIM_OK;
@@ -1698,6 +1710,7 @@ int ingest_dense(psim_handle* h, const void* recv_dev) {
     HIPCHK(h, hipSetDevice(h->device));
     PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
     set_round_slots(h, a, h->round);                      // counts: the round that sent them (m_w)
+    a.force_flags = force_flags ? 1u : 0u;
     HIPCHK(h, launch_pt_ingest_dense(a, (const uint32_t*)recv_dev, sh.recv_map, (uint32_t)nr, sh.slot2v, h->stream));
     return PSIM_OK;
 }
@@ -1801,7 +1814,7 @@ int x_buffers(psim_handle* h) {
 }
 
 // exchange the dense regions just packed into xsend, then ingest them
-int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k = 0) {
+int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k = 0, bool force_flags = false) {
     auto& sh = h->sh;
     if (sh.world == 1) return PSIM_OK;
     std::string err;
@@ -1818,6 +1831,7 @@ int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k
         if (xs) xs->fabric_bytes += 8ull * rec_k * uint64_t(W - 1);
         PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);   // in_nxt / pend_nxt = what the next round reads
         set_round_slots(h, a, h->round);                      // counts: the round that sent them (m_w)
+        a.force_flags = force_flags ? 1u : 0u;
         HIPCHK(h, launch_pt_ingest(a, sh.xrr, uint32_t(uint64_t(W - 1) * rec_k), sh.slot2v, h->stream));
         return PSIM_OK;
     }
@@ -1826,7 +1840,7 @@ int x_exchange(psim_handle* h, int slot, psim_exchange_stats* xs, uint32_t rec_k
     if (rc) return fail(h, rc, "exchange: %s", err.c_str());
     if (marks) HIPCHK(h, hipEventRecord(sh.xev[2 * slot + 1], h->stream));
     if (xs) xs->fabric_bytes += 4ull * (sh.send_base[sh.world] - (sh.send_base[sh.rank + 1] - sh.send_base[sh.rank]));
-    return ingest_dense(h, sh.xrecv);
+    return ingest_dense(h, sh.xrecv, force_flags);
 }
 
 // Sharded window lane: the records the last round (or origin) wrote into
@@ -2090,6 +2104,12 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
         uint32_t* mc = h->mcnt_base + kMcntLane * size_t(h->cur_lane);
         HIPCHK(h, hipMemsetAsync(mc, 0, kMcntLane * sizeof(uint32_t), h->stream));
         HIPCHK(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mc + (h->round % 4) * 64), 1, 1, h->stream));
+        // the first round's predecessor-but-one: the list threshold, so it reads
+        // the flags (its words were not listed) and clears them, and the rounds
+        // after it list and read lists as their counts say
+        if (const uint32_t thr = list_threshold(h))
+            HIPCHK(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mc + ((h->round + 3) % 4) * 64), thr, 1,
+                                        h->stream));
         sh.mcnt_on = true;
     }
     while (!done && ran < max_rounds) {
@@ -2107,9 +2127,13 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
                 bM = S;
                 if (S <= double(sh.rec_thr)) rec_k = std::max<uint32_t>(1u, uint32_t(S));
             }
-            rc = shard_round_async_k(h, sh.xsend, rec_k);
+            // the last round this call may run writes group flags whatever its
+            // count: whoever reads next (another call, a path without counts)
+            // finds its words by the flags
+            const bool last = ran + j + 1 == max_rounds;
+            rc = shard_round_async_k(h, sh.xsend, rec_k, last);
             if (rc) return rc;
-            rc = x_exchange(h, (int)j, xs, rec_k);
+            rc = x_exchange(h, (int)j, xs, rec_k, last);
             if (rc) return rc;
         }
         if (sh.chunk_mode) HIPCHK(h, hipEventRecord(sh.rev_[1], h->stream));

@@ -135,6 +135,8 @@ struct PtArgs {
     uint32_t* wl_nxt;
     uint32_t wl_cap, wl_thr;
     uint32_t ell_grid;                     // ELL kernel grid = resident workgroups (0: one per chunk)
+    uint32_t force_flags;                  // this round writes group flags whatever its count (the last round
+                                           // of a sharded psim_shard_step: readers without counts come next)
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
