@@ -331,6 +331,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
+                # the same launch time against the PMC-measured bytes (tools/pmc_traffic.py): what
+                # actually crossed the memory side, vs the algorithmic model's credited bytes
+                "frac_traffic": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "kernel": kernel,
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "algo_bytes_per_launch": algo_bytes / max(1, counted),
