@@ -153,6 +153,21 @@ size_t orc_pt_get_outstanding(const orc_plumtree* s, uint32_t v, uint32_t* peers
 void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint8_t* out);
 /* Round field of the broadcast each vertex accepted for (origin, mono); 0xFFFFFFFF if none */
 void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint32_t* out);
+/* Bulk views for whole-overlay lockstep checks (test digests, not reference
+ * behaviour).  Vertices [lo, hi) in psim_get_plumtree's form: eager / lazy /
+ * outstanding peers as bit masks over v's slot row (row_ptr/col: the CSR the
+ * handle holds; bit s = col[row_ptr[v] + s]), recv Round as u16 (0xFFFF not
+ * delivered, 0xFFFE the origin).  ORC_NOSPACE: a peer not in v's row. */
+int orc_pt_dump_state(const orc_plumtree* s, uint32_t root, uint32_t mono, const uint64_t* row_ptr,
+                      const uint32_t* col, uint32_t lo, uint32_t hi, uint32_t* eager, uint32_t* lazy,
+                      uint32_t* outst, uint16_t* rr);
+/* The messages the next round delivers to receivers in [lo, hi) as
+ * psim_get_inflight words: words[e - row_ptr[lo]] for receiver slot e (the
+ * slot of dst's row holding src), 4-bit kinds in FIFO order in [15:0], the
+ * carried Round in [31:16] when the word holds a broadcast or an i_have.
+ * ORC_NOSPACE: > 4 messages over one slot, or a sender not in the row. */
+int orc_pt_inflight_words(const orc_plumtree* s, const uint64_t* row_ptr, const uint32_t* col, uint32_t lo,
+                          uint32_t hi, uint32_t* words);
 
 /* ------------------------------------------------------------------ */
 /* Philox4x32-10 (Random123) -- the simulation's counter-based RNG      */

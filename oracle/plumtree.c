@@ -651,6 +651,68 @@ void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono,
     }
 }
 
+/* slot of peer p in v's row of the given slot layout, or -1 */
+static int64_t row_slot(const uint64_t* row_ptr, const uint32_t* col, uint32_t v, uint32_t p) {
+    for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++)
+        if (col[e] == p) return (int64_t)(e - row_ptr[v]);
+    return -1;
+}
+
+static int set_mask(const oset* x, const uint64_t* row_ptr, const uint32_t* col, uint32_t v, uint32_t* m) {
+    *m = 0;
+    for (uint32_t i = 0; i < x->n; i++) {
+        const int64_t q = row_slot(row_ptr, col, v, x->a[i]);
+        if (q < 0 || q >= 32) return ORC_NOSPACE;
+        *m |= 1u << q;
+    }
+    return ORC_OK;
+}
+
+int orc_pt_dump_state(const orc_plumtree* s, uint32_t root, uint32_t mono, const uint64_t* row_ptr,
+                      const uint32_t* col, uint32_t lo, uint32_t hi, uint32_t* eager, uint32_t* lazy,
+                      uint32_t* outst, uint16_t* rr) {
+    for (uint32_t v = lo; v < hi && v < s->n; v++) {
+        node_t* nd = &s->nodes[v];
+        const uint32_t i = v - lo;
+        if (set_mask(all_peers(nd, root, 0), row_ptr, col, v, &eager[i]) ||
+            set_mask(all_peers(nd, root, 1), row_ptr, col, v, &lazy[i]))
+            return ORC_NOSPACE;
+        outst[i] = 0;
+        for (size_t k = 0; k < nd->nout; k++) {
+            const int64_t q = row_slot(row_ptr, col, v, nd->out[k].peer);
+            if (q < 0 || q >= 32) return ORC_NOSPACE;
+            outst[i] |= 1u << q;
+        }
+        rr[i] = 0xFFFFu;
+        for (size_t k = 0; k < nd->nrr; k++)
+            if (nd->rr[k].node == root && nd->rr[k].mono == mono) { rr[i] = (uint16_t)nd->rr[k].round; break; }
+    }
+    return ORC_OK;
+}
+
+int orc_pt_inflight_words(const orc_plumtree* s, const uint64_t* row_ptr, const uint32_t* col, uint32_t lo,
+                          uint32_t hi, uint32_t* words) {
+    const uint64_t base = row_ptr[lo];
+    memset(words, 0, (size_t)(row_ptr[hi] - base) * sizeof(uint32_t));
+    const size_t k = s->nnxt + s->ndq;              /* FIFO order per pair = emission (seq) order */
+    orc_msg* m = (orc_msg*)malloc((k ? k : 1) * sizeof(orc_msg));
+    size_t got = orc_pt_pending(s, m, k);
+    int rc = ORC_OK;
+    for (size_t i = 0; i < got && i < k && rc == ORC_OK; i++) {
+        if (m[i].dst < lo || m[i].dst >= hi) continue;
+        const int64_t q = row_slot(row_ptr, col, m[i].dst, m[i].src);
+        if (q < 0) { rc = ORC_NOSPACE; break; }
+        uint32_t* w = &words[row_ptr[m[i].dst] + (uint64_t)q - base];
+        uint32_t nk = 0;
+        while (nk < 4 && ((*w >> (4 * nk)) & 0xFu)) nk++;
+        if (nk == 4) { rc = ORC_NOSPACE; break; }
+        *w |= m[i].type << (4 * nk);
+        if (m[i].type == ORC_MSG_BROADCAST || m[i].type == ORC_MSG_IHAVE) *w = (*w & 0xFFFFu) | (m[i].round << 16);
+    }
+    free(m);
+    return rc;
+}
+
 void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint32_t* out) {
     for (uint32_t v = 0; v < s->n; v++) {
         node_t* nd = &s->nodes[v];

@@ -154,6 +154,11 @@ def lib():
         L.orc_pt_get_outstanding.restype = sz
         L.orc_pt_get_delivered.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint8)]
         L.orc_pt_get_recv_round.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.orc_pt_dump_state.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(C.c_uint64), P(C.c_uint32),
+                                        C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), P(C.c_uint32),
+                                        P(C.c_uint16)]
+        L.orc_pt_inflight_words.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_uint32, C.c_uint32,
+                                            P(C.c_uint32)]
         L.orc_pt_set_omissions.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), sz]
         L.orc_pt_omitted.argtypes = [C.c_void_p]
         L.orc_pt_omitted.restype = C.c_uint64
@@ -536,6 +541,50 @@ class Plumtree:
         out = np.zeros(self.n, dtype=np.uint32)
         lib().orc_pt_get_recv_round(self._h, origin, mono, _u32p(out))
         return out
+
+    def dump_state(self, root, mono, slot_row_ptr, slot_col, lo=0, hi=None):
+        """Vertices [lo, hi) as psim_get_plumtree returns them: (eager, lazy,
+        outstanding) masks over the slot layout (slot_row_ptr, slot_col) --
+        the handle's global layout, rows sorted by id -- and the accepted
+        Round as u16 (0xFFFF none, 0xFFFE the origin)."""
+        hi = self.n if hi is None else hi
+        k = hi - lo
+        rp = np.ascontiguousarray(slot_row_ptr, dtype=np.uint64)
+        cl = np.ascontiguousarray(slot_col, dtype=np.uint32)
+        e, l_, o = (np.zeros(max(1, k), np.uint32) for _ in range(3))
+        rr = np.zeros(max(1, k), np.uint16)
+        rc = lib().orc_pt_dump_state(self._h, root, mono, _u64p(rp), _u32p(cl), lo, hi, _u32p(e),
+                                     _u32p(l_), _u32p(o), rr.ctypes.data_as(C.POINTER(C.c_uint16)))
+        if rc:
+            raise RuntimeError("orc_pt_dump_state: a peer outside its slot row")
+        return e[:k], l_[:k], o[:k], rr[:k]
+
+    def inflight_words(self, slot_row_ptr, slot_col, lo=0, hi=None):
+        """The next round's messages to receivers [lo, hi) as psim_get_inflight
+        words over slots slot_row_ptr[lo] .. slot_row_ptr[hi] (Round kept for
+        broadcast / i_have only)."""
+        hi = self.n if hi is None else hi
+        rp = np.ascontiguousarray(slot_row_ptr, dtype=np.uint64)
+        cl = np.ascontiguousarray(slot_col, dtype=np.uint32)
+        k = int(rp[hi] - rp[lo])
+        w = np.zeros(max(1, k), np.uint32)
+        rc = lib().orc_pt_inflight_words(self._h, _u64p(rp), _u32p(cl), lo, hi, _u32p(w))
+        if rc:
+            raise RuntimeError("orc_pt_inflight_words: > 4 messages on a slot or a sender off the row")
+        return w[:k]
+
+
+def inflight_protocol_words(words):
+    """psim_get_inflight words with the Round kept only where the word holds a
+    broadcast or an i_have (the others carry the sender's pushed Round as an
+    echo the protocol never reads) -- comparable with Plumtree.inflight_words."""
+    w = np.asarray(words, dtype=np.uint32)
+    f = w & np.uint32(0xFFFF)
+    nib = [(f >> np.uint32(4 * i)) & np.uint32(0xF) for i in range(4)]
+    keep = np.zeros(w.shape, bool)
+    for x in nib:
+        keep |= (x == 1) | (x == 3)
+    return np.where(keep, w, f).astype(np.uint32)
 
 
 def stats_dict(s):

@@ -69,7 +69,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 
 // Reduce the per-thread counters of a workgroup and add them to a shard.
 __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long* __restrict__ stats,
-                                               int* ost_total, uint32_t* msgs = nullptr) {
+                                               int* ost_total, uint32_t* msgs = nullptr, int* hold_d = nullptr) {
     __shared__ unsigned long long red[kBlock / 64][kNStat];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -97,6 +97,7 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
             for (int w = 0; w < kBlock / 64; w++) s += red[w][i];
             if (s) atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kNStat + i], s);
             if (s && i == S_OST_DELTA && ost_total) atomicAdd(ost_total, (int)(long long)s);
+            if (s && i == S_OST_DELTA && hold_d) atomicAdd(hold_d, (int)(long long)s);   // kMcntHoldD ring
         }
     }
     if (msgs && threadIdx.x == 0) {          // this round's messages into its count shard (PtArgs::mcnt)
@@ -642,15 +643,40 @@ struct RoundMode {
     uint32_t mark;   // this round's senders: 0 = no group flags, 1 = flags, 2 = flags + worklist
     bool all_in;     // the last round wrote no flags: every group is read
     bool list_in;    // the last round's worklist is complete: read its groups, not the flags
+    bool rows_due;   // the lazy tick fires and some vertex held rows when the round started
 };
 
+// This round's change in row holders (kMcntHoldD ring slot m_w), or null without counts.
+__device__ __forceinline__ int* hold_delta(const PtArgs& a) {
+    return a.mcnt ? reinterpret_cast<int*>(a.mcnt + kMcntHoldD + a.m_w) : nullptr;
+}
+
 // wl_off (ELL kernel): [65] prefix of the worklist shards this round reads.
+// Every decision below is taken from values written by EARLIER launches, so
+// all workgroups of this launch agree: the running holder count
+// (*ost_total) moves while the launch runs, and a workgroup that read it
+// after another had flushed used to pick the flags while the others read the
+// list -- a listed vertex that gained rows this round was then visited again
+// as "due" and sent a second i_have (the 1M world-2 mismatch of round 2).
 __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint32_t* wl_off = nullptr) {
-    __shared__ uint32_t cnt2[3];
+    __shared__ uint32_t cnt2[4];
     m.mark = 1;
     m.all_in = m.list_in = false;
-    if (!a.mcnt) return true;
+    if (!a.mcnt) {
+        // no counts: flag mode only, every workgroup reads its own chunks'
+        // row bytes, which no other workgroup writes -- a stale total is harmless
+        m.rows_due = a.tick && *a.ost_total > 0;
+        return true;
+    }
     const uint32_t t = threadIdx.x;
+    if (t == 0) {                                         // holders at the start of this round
+        const int hold = int(a.mcnt[kMcntHold + a.m_r]) + int(a.mcnt[kMcntHoldD + a.m_s]);
+        cnt2[3] = uint32_t(hold);
+        if (blockIdx.x == 0) {
+            a.mcnt[kMcntHold + a.m_s] = uint32_t(hold);  // = holders at the end of round R-1
+            a.mcnt[kMcntHoldD + a.m_z] = 0u;             // the round after next adds into it
+        }
+    }
     if (t < 64) {
         uint32_t c1 = a.mcnt[a.m_s * 64 + t], c2 = a.mcnt[a.m_r * 64 + t];
         uint32_t l = a.wl_cur ? a.wlcnt[a.m_s * 64 + t] : 0u;
@@ -678,7 +704,8 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
     }
     __syncthreads();
     const uint32_t prev = cnt2[0], prev2 = cnt2[1];
-    const bool rows_due = a.tick && *a.ost_total > 0;
+    const bool rows_due = a.tick && int(cnt2[3]) > 0;
+    m.rows_due = rows_due;
     // nothing was sent last round and no row is due: every vertex is idle
     // (no inbox flag can be set), so the whole round is a no-op
     if (prev == 0 && !rows_due) return false;
@@ -711,13 +738,17 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     uint32_t pmask = 0, dmask = 0;
     if (v0 < a.n) {
         const uint32_t g = v0 >> kGroupShift;
+        const bool lead = (t & ((1u << (kGroupShift - 2)) - 1)) == 0;   // threads of a group share the byte
         if (all_in) {
+            // flags a forced-flag round left (PtArgs::force_flags) are cleared too, or a
+            // later worklist round would find the claim bit set and not list the group
             pmask = 0xFu;
+            if (lead) a.pend_cur[g] = 0;
         } else if (a.pend_cur[g]) {
             pmask = 0xFu;
-            if ((t & ((1u << (kGroupShift - 2)) - 1)) == 0) a.pend_cur[g] = 0;   // threads of a group share the byte
+            if (lead) a.pend_cur[g] = 0;
         }
-        if (a.tick && *a.ost_total > 0) {
+        if (md.rows_due) {
             uint32_t w;
             if (v0 + 4 <= a.n) w = *reinterpret_cast<const uint32_t*>(a.ost + v0);
             else { w = 0; for (uint32_t i = 0; v0 + i < a.n; i++) w |= uint32_t(a.ost[v0 + i]) << (8 * i); }
@@ -745,7 +776,8 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
         const uint32_t x = cand[i];
         pt_vertex<kFault>(a, base + (x >> 2), (x >> 1) & 1u, x & 1u, &rep[t], c, md.mark);
     }
-    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
+    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr,
+                   hold_delta(a));
     flush_delays<kFault>(a);
 }
 
@@ -829,13 +861,14 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             if (t < kGroups && t * kGV < nv) {
                 const uint32_t g = (base >> kGroupShift) + t;
                 if (md.all_in) {
+                    a.pend_cur[g] = 0;                 // a forced-flag round's flags (see pt_round_body)
                     glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
                 } else if (a.pend_cur[g]) {
                     a.pend_cur[g] = 0;
                     glist[atomicAdd(&ngrp, 1u)] = (uint8_t)t;
                 }
             }
-            if (a.tick && *a.ost_total > 0 && kVpt * t < nv) {
+            if (md.rows_due && kVpt * t < nv) {
                 const uint32_t v0 = base + kVpt * t;
                 uint32_t d = 0;
                 for (uint32_t i = 0; i < kVpt; i++)
@@ -929,7 +962,8 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
     }
     if (md.mark == 2) wl_flush(a, &wl);
-    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr);
+    flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr,
+                   hold_delta(a));
     flush_delays<kFault>(a);
 }
 
@@ -1216,6 +1250,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
         if (a.obin) a.obin[v >> a.fv_shift] += 1u;
         atomicAdd(&a.stats[S_OST_DELTA], 1ull);
         atomicAdd(a.ost_total, 1);
+        if (int* d = hold_delta(ao)) atomicAdd(d, 1);   // a change of the round before the next one
     }
     if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
     if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);

@@ -20,7 +20,6 @@ using namespace psim;
 namespace {
 constexpr int kChunk = 16;  // rounds launched between host synchronisations (no-op rounds exit early)
 constexpr int kMaxLanes = 16;   // concurrent heartbeat roots (single GPU, slot-scatter engine)
-constexpr size_t kMcntLane = 512;   // u32 per lane in mcnt_base: message counts, worklist counts
 constexpr size_t kStatsRow = size_t(kStatShards) * kNStat + kDelayHist;   // shards, then messages per delay
 }  // namespace
 
@@ -292,6 +291,8 @@ void free_cs(psim_handle* h) {
 }
 
 void swap_lane(psim_handle* h, int j);
+void save_lane(psim_handle* h);
+void load_lane(psim_handle* h, int j);
 
 void free_graph(psim_handle* h) {
     if (!h->lanes.empty()) {
@@ -534,13 +535,7 @@ int to_window(psim_handle* h) {
 uint32_t list_threshold(const psim_handle* h) {
     if (!h->wl_cap) return 0;
     const uint32_t ng = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
-    const uint32_t thr = h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
-    const uint32_t dense = std::max<uint32_t>(1u, h->n / 4);
-    // several shards: no list for now -- one 1M world-2 parity run disagreed
-    // with the plain handle by one i_have after a heartbeat over the tree
-    // (not reproduced, cause not found); the flags serve every sharded round
-    (void)dense;
-    return h->sh.world > 1 ? 0u : thr;
+    return h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
 }
 
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
@@ -562,6 +557,35 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
         a.wl_cap = h->wl_cap;
         a.wl_thr = thr;
     }
+}
+
+// The row-holder ring of the focused lane (psim_internal.h kMcntHold): before
+// round R runs with counts, holders(R-2) := the host's count and
+// delta(R-1) := 0, so R's "row due" test starts from the exact count whatever
+// ran before (rounds without counts, rewound rounds, a broadcast's memset).
+// Host-side ost_cnt is exact whenever no round is pending.
+hipError_t seed_hold_ring(psim_handle* h, uint64_t R) {
+    PtArgs a = make_args(h, h->par, 0, h->stats);
+    set_round_slots(h, a, R);
+    if (!a.mcnt) return hipSuccess;
+    const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.mcnt + kMcntHold + a.m_r),
+                                           int(uint32_t(h->ost_cnt)), 1, h->stream);
+    if (e != hipSuccess) return e;
+    return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.mcnt + kMcntHoldD + a.m_s), 0, 1, h->stream);
+}
+
+// ... for every lane (a driver call that may run any of them)
+hipError_t seed_hold_rings(psim_handle* h, uint64_t R) {
+    if (h->lanes.empty()) return seed_hold_ring(h, R);
+    const int focus = h->cur_lane;
+    save_lane(h);
+    hipError_t e = hipSuccess;
+    for (int j = 0; j < (int)h->lanes.size() && e == hipSuccess; j++) {
+        load_lane(h, j);
+        e = seed_hold_ring(h, R);
+    }
+    load_lane(h, focus);
+    return e;
 }
 
 // Round tags (psim_internal.h): a slot-scatter inbox word carries the round
@@ -806,6 +830,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         return true;
     };
     bool done = stop_q && all_quiet();
+    HIPCHK(h, seed_hold_rings(h, h->round + 1));
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
         const bool per_round = !(h->cfg.flags & PSIM_CFG_CHUNK_TIMING);   // events between round kernels
@@ -1488,7 +1513,10 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
             // origin emits into the buffer the next round reads
             PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
             set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
-            if (a.mcnt) HIPCHK(h, hipMemsetAsync(a.mcnt, 0, kMcntLane * sizeof(uint32_t), h->stream));
+            if (a.mcnt) {
+                HIPCHK(h, hipMemsetAsync(a.mcnt, 0, kMcntLane * sizeof(uint32_t), h->stream));
+                HIPCHK(h, seed_hold_ring(h, h->round + 1));   // holders before the origin's own change
+            }
             a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
             a.root = lr;
             HIPCHK(h, launch_pt_origin(a, h->stream));
@@ -1588,6 +1616,7 @@ int psim_shard_round(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t
     HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
     PtArgs a = make_args(h, h->par, tick, h->stats);
     set_round_slots(h, a, h->round + 1);         // one shard: the counts every path keeps
+    if (!h->sh.pending) HIPCHK(h, seed_hold_ring(h, h->round + 1));
     HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
     HIPCHK(h, launch_pt_round(a, h->stream));
     HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
@@ -1692,6 +1721,8 @@ static int shard_round_async_k(psim_handle* h, void* send_dev, uint32_t rec_k, b
 
 int psim_shard_round_async(psim_handle* h, void* send_dev) {
     if (h) h->sh.plan_ok = false;       // split-phase rounds: the record-bound bookkeeping is off
+    if (h && h->n && !h->sh.pending && h->lanes.size() <= 1 && !h->win)
+        HIPCHK(h, seed_hold_ring(h, h->round + 1));
     return shard_round_async_k(h, send_dev, 0);
 }
 
@@ -2066,7 +2097,10 @@ int shard_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size
     int rc = x_buffers(h);
     if (rc) return rc;
     if (xs) memset(xs, 0, sizeof *xs);
-    if (h->lanes.size() > 1 || h->win) return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
+    if (h->lanes.size() > 1 || h->win) {
+        if (!h->sh.pending) HIPCHK(h, seed_hold_rings(h, h->round + 1));
+        return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
+    }
     return shard_drive_fast(h, max_rounds, out, cap, stop_q, rounds_run, xs);
 }
 
@@ -2116,6 +2150,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
                                         h->stream));
         sh.mcnt_on = true;
     }
+    if (!sh.pending) HIPCHK(h, seed_hold_ring(h, h->round + 1));   // the local holder count is exact
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(K, max_rounds - ran);
         if (sh.chunk_mode) {

@@ -39,6 +39,18 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter) {
     base = __shfl(base, (int)leader, 64);
     return base + rank;
 }
+// Per-lane round-count area (PtArgs::mcnt), u32 words:
+//   [0, 256)    messages sent per round, [4 rounds][64 shards]
+//   [256, 512)  worklist entries per round, [4][64] (PtArgs::wlcnt)
+//   [512, 516)  row holders at the END of round k (k mod 4): round R writes
+//               slot R-1 once (block 0) -- a value no workgroup of R reads
+//   [516, 520)  change in row holders during round k (two's complement)
+// Round R's "any row due" test reads holders(R-2) + delta(R-1): both written
+// by earlier launches, so every workgroup of a launch takes the same decision
+// (the running count PtArgs::ost_total moves while the launch runs).
+constexpr size_t kMcntHold = 512;
+constexpr size_t kMcntHoldD = 516;
+constexpr size_t kMcntLane = 520;
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard

@@ -106,3 +106,49 @@ def test_update_resets_per_root_sets():
     orc.update(v, members)
     e2, _ = orc.peers(v, 0)
     assert e2 == [u for u in members if u != v]
+
+
+def test_bulk_views_match_per_vertex_getters():
+    """orc_pt_dump_state / orc_pt_inflight_words (the whole-overlay lockstep
+    views of tests/test_worklist_parity.py) agree with the per-vertex getters
+    and the pending list, round by round, over a flood and a tree heartbeat
+    with dead vertices (L = 2: outstanding rows over several rounds)."""
+    n = 1200
+    rp, col = overlay.random_regular(n, 5, 77)
+    rp = np.asarray(rp, np.int64)
+    row = np.repeat(np.arange(n), np.diff(rp))
+    scol = np.asarray(col, np.uint32)[np.lexsort((col, row))]
+    orc = O.Plumtree(rp, col, 2)
+    for hb in range(2):
+        if hb == 1:
+            alive = np.ones(n, np.uint8)
+            alive[np.random.default_rng(1).choice(n, 60, replace=False)] = 0
+            alive[5] = 1
+            orc.set_alive(alive)
+        mono = orc.heartbeat(5)
+        for _ in range(40):
+            e, l_, o, rr = orc.dump_state(5, mono, rp, scol)
+            orr = orc.recv_round(5, mono)
+            assert np.array_equal(rr, np.where(orr == 0xFFFFFFFF, 0xFFFF, orr & 0xFFFF).astype(np.uint16))
+            for v in range(0, n, 13):
+                row_v = scol[rp[v]:rp[v + 1]].tolist()
+                dec = lambda m: sorted(row_v[s] for s in range(len(row_v)) if (int(m) >> s) & 1)
+                pe, pl = orc.peers(v, 5)
+                assert dec(e[v]) == pe and dec(l_[v]) == pl
+                assert dec(o[v]) == sorted({p for p, _, _ in orc.outstanding(v)})
+            w = orc.inflight_words(rp, scol)
+            msgs = []
+            for s in np.nonzero(w)[0].tolist():
+                dst = int(np.searchsorted(rp, s, side="right") - 1)
+                f = int(w[s]) & 0xFFFF
+                while f:
+                    t = f & 0xF
+                    f >>= 4
+                    msgs.append((int(scol[s]), dst, t, int(w[s]) >> 16 if t in (1, 3) else 0))
+            want = sorted((s_, d, t, r if t in (1, 3) else 0) for (s_, d, t, r) in orc.pending())
+            assert sorted(msgs) == want
+            st = orc.step(1)[0]
+            if sum(st[k] for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft")) == 0 \
+                    and st["outstanding_live"] == 0:
+                break
+    orc.close()
