@@ -598,8 +598,17 @@ void set_round_tags(PtArgs& a, uint64_t R) {
     a.wtag = uint32_t(R + 1) & 0xFFu;
 }
 
+// A scrub at round S keeps the words tagged for the `span` rounds in flight
+// (S+1 .. S+span; span 1 for the double buffer, kRing - 1 for the delay ring)
+// and zeroes the rest.  A stale word written for round R' aliases round
+// R' + 256, so the scrub must run while no stale word can carry a kept tag:
+// before round S_prev + 256 - span + 1, i.e. when last + span reaches
+// S_prev + 255.  (Until round 3 the test was last > S + 256: a one-round
+// psim_step at exactly S + 256 kept the stale words of round S + 1 as live --
+// found when the word format was shortened to a 64-round tag)
 hipError_t scrub_if_needed(psim_handle* h, uint64_t last) {
-    if (h->bin.rec_c || last <= h->scrub + kTagSpan) return hipSuccess;
+    const uint64_t span = h->dly ? kRing - 1 : 1;
+    if (h->bin.rec_c || last + span < h->scrub + kTagSpan) return hipSuccess;
     const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
     if (h->dly) {       // the ring: words for the next kRing - 1 rounds are in flight
         const hipError_t e = launch_pt_scrub(h->ring, kRing * h->Ed, keep, kRing - 1, h->stream);

@@ -524,6 +524,30 @@ def test_round_tags_across_wrap(psim):
         lockstep(sim, orc, 5, m)
 
 
+def test_round_tags_one_round_steps_at_wrap(psim):
+    """Single-round steps across the tag period, then two heartbeats in
+    lockstep.  A scrub run at exactly round S + 256 keeps the words tagged for
+    round S + 257 -- and any stale word written for round S + 1 carries the
+    same tag; round 3 moved the scrub one round earlier (psim_host.hip
+    scrub_if_needed).  That case needs a stale round-(S+1) word nobody
+    overwrote, which this overlay does not produce (every origin word is
+    overwritten by a prune); it did occur with a 64-round tag on a ring lattice
+    (profiles/r03/experiments/ab_word16_round_profile.txt)."""
+    rp, col = psim.overlay.random_regular(300, 5, 153)
+    sim, orc = make(psim, rp, col, 1)
+    m = sim.broadcast(3)
+    assert m == orc.heartbeat(3)
+    for r in range(256):
+        gs, os_ = sim.step(1)[0], orc.step(1)[0]
+        for k in KINDS:
+            assert gs[k] == os_[k], (r, k)
+    for _ in range(2):
+        m = sim.broadcast(3)
+        assert m == orc.heartbeat(3)
+        compare(sim, orc, 3, m)
+        lockstep(sim, orc, 3, m)
+
+
 def _delay_pairs(sim, frac, dmax, seed):
     rng = np.random.default_rng(seed)
     src = np.repeat(np.arange(sim.n), np.diff(sim.slot_row_ptr.astype(np.int64)))
