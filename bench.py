@@ -13,9 +13,12 @@ except the per-chunk 8 KB counter read-back the round driver needs.
 Roofline: dominant kernel pt_round_ell_kernel, HBM-bound; achieved = SURVEY
 8(d) algorithmic bytes of the timed rounds / their summed hipEvent durations
 (events on the library's own stream: one pair per 16-round chunk, so the
-average launch includes the dispatch gaps between round kernels).  cpu_baseline: the C oracle (a
-scalar port of the reference modules) on a bounded sample of the same
-workload, rank 0 only.
+average launch includes the dispatch gaps between round kernels); traffic =
+rocprofv3 PMC bytes per launch from profiles/pmc_traffic.json, reported only
+when that profile was taken on the very libpsim.so this run loaded (sha256).
+cpu_baseline: the C oracle (a scalar port of the reference modules) running
+one flood of the benchmark's own configuration single-threaded, rank 0 only
+(plus the 1M-peer sample and the 16-process all-core figure beside it).
 
 Multi-GPU (N > 1): the SAME 10M-peer overlay is vertex-sharded over the N
 GPUs (strong scaling; N = 1 is its one-shard case); cross-shard
@@ -46,6 +49,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0x5EED0001)
     p.add_argument("--lazy-tick-rounds", type=int, default=1)
     p.add_argument("--cpu-sample-n", type=int, default=1_000_000)
+    p.add_argument("--no-cpu-full", action="store_true",
+                   help="skip the single-thread C-oracle flood of the full --num-peers config (~25 s at 10M)")
     p.add_argument("--cpu-sample-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=16,
@@ -130,6 +135,41 @@ def verify(sim, pg, n, rounds_per_step):
         raise SystemExit(f"bench: the timed steps did not converge: {ok} (delivered {tot[0]} of {n}, "
                          f"outstanding vertices {tot[1]}, eager entries {tot[2]}, rounds {rounds_per_step})")
     return ok
+
+
+def cpu_baseline_full(args):
+    """One single-thread C-oracle flood of the benchmark's own configuration
+    (the same --num-peers overlay, seed and root), timed from heartbeat to
+    quiescence (the 10M config itself, beside the 1M sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from partisan_amd import overlay
+    rp, col = overlay.random_regular(args.n, args.peers, args.seed)
+    orc = O.Plumtree(rp, col, args.lazy_tick_rounds)
+    del rp, col
+    t0 = time.perf_counter()
+    orc.heartbeat(0)
+    _, rounds = orc.run()
+    dt = time.perf_counter() - t0
+    orc.close()
+    return {
+        "value": args.n * rounds / dt, "unit": "peer-rounds/s", "cores": 1, "kind": "port",
+        "sample": (f"C oracle (oracle/plumtree.c), one flood of the benchmark's own {args.n}-peer random "
+                   f"{args.peers}-peer overlay from root 0 to quiescence ({rounds} rounds), single thread, "
+                   f"{dt:.1f} s"),
+    }
+
+
+def lib_fingerprint():
+    """sha256 of the libpsim.so this process loaded: profiles/pmc_traffic.json
+    is keyed to it, so a kernel change cannot leave a stale traffic figure."""
+    import hashlib
+    from partisan_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
 
 
 def cpu_baseline(args):
@@ -221,6 +261,7 @@ def main():
         step()
 
     algo_bytes = 0
+    active_bytes = 0
     round_ms = 0.0
     rounds_per_step = []
     if sp is not None:
@@ -234,6 +275,8 @@ def main():
         if sp is None:
             algo_bytes += int(stats["algo_bytes"].sum())
             round_ms += float(stats["kernel_ms"].sum())
+            # the same model crediting the state bytes of the vertices a round touched, not of all N
+            active_bytes += int((stats["algo_bytes"] - np.uint64(16 * args.n) + np.uint64(16) * stats["active"]).sum())
     # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
     barrier(pg)
     t1 = time.perf_counter()
@@ -289,14 +332,26 @@ def main():
     max_deg = int(max_over_ranks(pg, float(sim.max_degree())))
     kernel = "pt_round_kernel" if (args.csr or max_deg > 8) else "pt_round_ell_kernel"
     if rank == 0:
-        traffic = None
+        traffic = traffic_fetch = traffic_write = None
+        traffic_note = "no PMC profile for this workload"
+        fp = lib_fingerprint()
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("n") == args.n and tj.get("peers") == args.peers and tj.get("kernel") == kernel:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+            if not (tj.get("n") == args.n and tj.get("peers") == args.peers and tj.get("kernel") == kernel):
+                traffic_note = "PMC profile is for another workload"
+            elif tj.get("lib_sha256") != fp:
+                traffic_note = (f"PMC profile taken on another libpsim build ({str(tj.get('lib_sha256'))[:12]} "
+                                f"vs loaded {fp[:12]}): not reported")
+            else:
+                traffic_fetch = tj["fetch_bytes_per_launch"]
+                traffic_write = tj["write_bytes_per_launch"]
+                traffic = traffic_fetch + traffic_write
+                traffic_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this libpsim build "
+                                f"({tj.get('source', args.traffic_json)}), per launch")
+        except (OSError, ValueError, KeyError):
             pass
+        launch_s = avg_launch_ms * 1e-3
         out = {
             "metric": METRIC,
             "value": value,
@@ -331,18 +386,35 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_note": traffic_note,
                 # the same launch time against the PMC-measured bytes (tools/pmc_traffic.py): what
-                # actually crossed the memory side, vs the algorithmic model's credited bytes
-                "frac_traffic": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                # actually crossed the memory side.  MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts
+                # half the bytes of wide coalesced reads (the sweep's 16-B loads), so the read side is
+                # doubled for frac_traffic (an upper bound: the scattered 4-B reads need no doubling);
+                # frac_traffic_raw is the uncorrected figure
+                "frac_traffic": ((2 * traffic_fetch + traffic_write) / launch_s / 1e9 / HBM_PEAK_GBS)
+                                if traffic else None,
+                "frac_traffic_raw": (traffic / launch_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "kernel": kernel,
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "algo_bytes_per_launch": algo_bytes / max(1, counted),
+                # SURVEY 8(d)'s model credits 16 B of state for all N vertices every round; this
+                # variant credits only the vertices the round touched (sparse rounds get no credit
+                # for the vertices they skip)
+                "achieved_active_state": ((active_bytes / max(1, counted)) / launch_s / 1e9) if sp is None else None,
+                "frac_active_state": ((active_bytes / max(1, counted)) / launch_s / 1e9 / HBM_PEAK_GBS)
+                                     if sp is None else None,
+                "lib_sha256": fp,
             },
         }
         if exchange is not None:
             out["exchange"] = exchange
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args)
+            if args.no_cpu_full:
+                out["cpu_baseline"] = cpu_baseline(args)
+            else:
+                out["cpu_baseline"] = cpu_baseline_full(args)
+                out["cpu_baseline_sample_1m"] = cpu_baseline(args)
             if args.cpu_workers > 1:
                 out["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
         print(json.dumps(out), flush=True)

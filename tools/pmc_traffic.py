@@ -34,7 +34,14 @@ def main():
     p.add_argument("--kernel", default="pt_round_ell_kernel",
                    help="the round kernel bench.py runs (ELL rows: pt_round_ell_kernel; CSR: pt_round_kernel)")
     p.add_argument("--out", default=None)
+    p.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "partisan_amd", "libpsim.so"),
+                   help="the libpsim.so the profiled run loaded: bench.py reports the traffic only for this build")
+    p.add_argument("--source", default=None, help="where the raw rocprofv3 outputs are kept (profiles/...)")
     a = p.parse_args()
+    import hashlib
+    with open(a.lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
     f = load(a.fetch_dir, "FETCH_SIZE", a.kernel)
     w = load(a.write_dir, "WRITE_SIZE", a.kernel)
     counted = a.rounds_per_step * a.steps
@@ -48,6 +55,8 @@ def main():
         "hbm_bytes_per_launch_read_doubled": 2 * fetch + write,
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB*1024, "
                   "summed over all launches of the kernel / counted rounds",
+        "lib_sha256": lib_sha,
+        "source": a.source,
     }
     print(json.dumps(out, indent=1))
     if a.out:
