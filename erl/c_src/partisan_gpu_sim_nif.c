@@ -322,9 +322,21 @@ static ERL_NIF_TERM nif_set_delays(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
         !enif_inspect_binary(env, argv[2], &d) || !enif_inspect_binary(env, argv[3], &k) || s.size != d.size ||
         s.size % 4 || k.size != s.size / 4)
         return enif_make_badarg(env);
+    /* binary data carries no alignment guarantee: copy the ids (as pair_call does) */
+    uint32_t* src = (uint32_t*)enif_alloc(s.size + 4);
+    uint32_t* dst = (uint32_t*)enif_alloc(d.size + 4);
+    if (src) memcpy(src, s.data, s.size);
+    if (dst) memcpy(dst, d.data, d.size);
+    if (!src || !dst) {
+        enif_free(src);
+        enif_free(dst);
+        return err(env, PSIM_ENOMEM);
+    }
     enif_mutex_lock(r->mu);
-    int rc = psim_set_delays(r->h, (const uint32_t*)s.data, (const uint32_t*)d.data, (const uint8_t*)k.data, k.size);
+    int rc = psim_set_delays(r->h, src, dst, (const uint8_t*)k.data, k.size);
     enif_mutex_unlock(r->mu);
+    enif_free(src);
+    enif_free(dst);
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
 }
 
@@ -1079,6 +1091,25 @@ static ERL_NIF_TERM nif_delivered_mono(ErlNifEnv* env, int argc, const ERL_NIF_T
     return enif_make_tuple2(env, mk_atom(env, "ok"), t);
 }
 
+/* is_delivered(Sim, V, Mono) -> {ok, boolean()}: Mod:is_stale({Root, Epoch,
+ * Mono}) at one vertex of the focused root (Mono 0: the newest heartbeat),
+ * psim_get_delivered_range over one vertex -- O(1) per call, where
+ * delivered/1 copies the whole overlay's set */
+static ERL_NIF_TERM nif_is_delivered(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned v, mono;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &v) || !enif_get_uint(env, argv[2], &mono) ||
+        v >= r->n)
+        return enif_make_badarg(env);
+    uint8_t d = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_delivered_range(r->h, mono, v, 1, &d);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), mk_atom(env, d ? "true" : "false"));
+}
+
 /* rows(Sim, V) -> {ok, [{Peer, Round, Mono}]}: v's outstanding i_have rows in
  * insertion order (psim_get_rows) */
 static ERL_NIF_TERM nif_rows(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -1167,6 +1198,7 @@ static ErlNifFunc funcs[] = {
     {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_delays", 4, nif_set_delays, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered_mono", 2, nif_delivered_mono, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"is_delivered", 3, nif_is_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"rows", 2, nif_rows, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"messages", 1, nif_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"shard_step", 2, nif_shard_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
-         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, rows/2, messages/1, shard_step/2,
+         peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, is_delivered/3, rows/2, messages/1, shard_step/2,
          relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
          demers_setup/5, demers_run/2,
@@ -80,6 +80,11 @@ set_delays(_Sim, _Src, _Dst, _Rounds) -> erlang:nif_error(nif_not_loaded).
 %% heartbeat of a window lane (psim_get_delivered_mono).
 -spec delivered_mono(sim(), non_neg_integer()) -> {ok, binary()} | error().
 delivered_mono(_Sim, _Mono) -> erlang:nif_error(nif_not_loaded).
+
+%% Mod:is_stale/1 at ONE vertex of the focused root (Mono 0: the newest
+%% heartbeat): psim_get_delivered_range over one vertex, no whole-set copy.
+-spec is_delivered(sim(), non_neg_integer(), non_neg_integer()) -> {ok, boolean()} | error().
+is_delivered(_Sim, _V, _Mono) -> erlang:nif_error(nif_not_loaded).
 
 %% Vertex V's outstanding i_have rows {Peer, Round, Mono} in insertion order.
 -spec rows(sim(), non_neg_integer()) -> {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer()}]} | error().

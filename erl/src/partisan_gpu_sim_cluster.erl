@@ -201,10 +201,12 @@ delivered(V, Origin, Mono) ->
         [{_, Latest}] when Mono > Latest ->
             false;
         [{_, Mono}] ->
+            %% one vertex of the newest heartbeat: psim_get_delivered_range,
+            %% O(1) -- not a copy of the whole overlay's delivered set
             Sim = sim(),
             ok = partisan_gpu_sim:focus(Sim, Origin),
-            {ok, D} = partisan_gpu_sim:delivered(Sim),
-            binary:at(D, V) =:= 1;
+            {ok, D} = partisan_gpu_sim:is_delivered(Sim, V, 0),
+            D;
         [_] ->
             case ets:lookup(?HIST, {Origin, Mono}) of
                 [{_, D}] -> binary:at(D, V) =:= 1;

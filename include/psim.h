@@ -183,6 +183,10 @@ int  psim_get_rows(const psim_handle* h, uint32_t v, uint32_t* peer, uint32_t* r
  * focused root, any Monotonic of a window lane; a static lane answers for
  * its newest heartbeat only (PSIM_EINVAL otherwise). */
 int  psim_get_delivered_mono(const psim_handle* h, uint32_t mono, uint8_t* delivered, size_t n);
+/* The same for local vertices [v0, v0 + count) only -- one vertex's
+ * Mod:is_stale/1 without copying the whole delivered set (the NIF adapter's
+ * is_stale/graft).  mono 0 = the focused root's newest heartbeat. */
+int  psim_get_delivered_range(const psim_handle* h, uint32_t mono, uint32_t v0, size_t count, uint8_t* delivered);
 /* Omission faults (test/prop_partisan_crash_fault_model.erl:117-196, send /
  * receive omission interposition funs): every Plumtree message over a
  * directed pair (src[i], dst[i]) is sent -- counted, the sender moves on --

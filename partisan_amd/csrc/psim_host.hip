@@ -2460,6 +2460,35 @@ int psim_get_delivered_mono(const psim_handle* h, uint32_t mono, uint8_t* delive
     return PSIM_OK;
 }
 
+int psim_get_delivered_range(const psim_handle* h, uint32_t mono, uint32_t v0, size_t count, uint8_t* delivered) {
+    if (!h || !h->n || (count && !delivered) || v0 > h->n || count > h->n - v0) return PSIM_EINVAL;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    if (!count) return PSIM_OK;
+    const uint32_t cm = cur_mono(h);
+    if (mono == 0) mono = cm;
+    HIPCHK(hh, hipSetDevice(h->device));
+    HIPCHK(hh, hipStreamSynchronize(h->stream));
+    if (mono == cm) {                          // the newest heartbeat: the records' Monotonic tags
+        std::vector<uint4> vs(count);
+        HIPCHK(hh, hipMemcpy(vs.data(), h->vs + v0, count * 16, hipMemcpyDeviceToHost));
+        const uint32_t s8 = h->serial & 0xFFu;
+        for (size_t i = 0; i < count; i++) delivered[i] = h->serial && ((vs[i].w >> 16) & 0xFFu) == s8;
+        return PSIM_OK;
+    }
+    if (!h->win)
+        return fail(hh, PSIM_EINVAL, "a static lane keeps the newest heartbeat (%u) only", cm);
+    std::vector<uint4> is(2 * count);          // window lane: each vertex's timestamp interval set
+    HIPCHK(hh, hipMemcpy(is.data(), h->win->iset + 2 * size_t(v0), count * 32, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < count; i++) {
+        const uint32_t lo[4] = {is[2 * i].x, is[2 * i].y, is[2 * i].z, is[2 * i].w};
+        const uint32_t hi[4] = {is[2 * i + 1].x, is[2 * i + 1].y, is[2 * i + 1].z, is[2 * i + 1].w};
+        bool d = false;
+        for (int k = 0; k < 4; k++) d |= lo[k] && lo[k] <= mono && mono <= hi[k];
+        delivered[i] = d;
+    }
+    return PSIM_OK;
+}
+
 int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
     if (!h || !delivered || n != h->n || !h->n) return PSIM_EINVAL;
     psim_handle* hh = const_cast<psim_handle*>(h);

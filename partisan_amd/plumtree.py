@@ -79,7 +79,10 @@ class PlumtreeBackend(PlumtreeBroadcastHandler):
         if cur is None or mono > cur[2]:
             return False
         if mono == cur[2]:
-            return bool(c._delivered(origin)[self.node])
+            if origin in c._state:                # this round's state is cached: no device call
+                return bool(c._delivered(origin)[self.node])
+            c.sim.focus(origin)                   # one vertex: psim_get_delivered_range, O(1)
+            return c.sim.delivered_at(self.node)
         past = c._hist.get(origin, {}).get(mono)   # recorded when the origin heartbeated again
         return bool(past is not None and past[self.node])
 

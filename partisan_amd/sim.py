@@ -144,6 +144,13 @@ class Simulator:
         d = np.diff(np.asarray(self.slot_row_ptr, dtype=np.int64))
         return int(d.max()) if len(d) else 0
 
+    def delivered_at(self, v, mono=0):
+        """Mod:is_stale at ONE local vertex (psim_get_delivered_range): mono 0 =
+        the focused root's newest heartbeat.  No copy of the whole set."""
+        out = np.zeros(1, np.uint8)
+        self._c(lib().psim_get_delivered_range(self._h, mono, v, 1, _u8p(out)))
+        return bool(out[0])
+
     def delivered_mono(self, mono):
         """Mod:is_stale({root, epoch, mono}) per vertex (psim_get_delivered_mono)."""
         out = np.zeros(self.n, np.uint8)

@@ -130,8 +130,16 @@ int main(int argc, char** argv) {
             for (size_t i = 0; i < dmz; i++) dmsum += dmb[i];
             ERL_NIF_TERM ms = want_ok_tuple("messages", call("messages", 1, A(sim)));
             ERL_NIF_TERM rw = want_ok_tuple("rows", call("rows", 2, A(sim, mock_uint(0))));
-            fprintf(g_out, ", \"c2_getters\": {\"delivered_mono\": %llu, \"messages\": %zu, \"rows0\": %zu}",
-                    (unsigned long long)dmsum, mock_list_len(mock_elem(ms, 1)), mock_list_len(mock_elem(rw, 1)));
+            uint64_t one = 0;                    /* is_delivered/3: Mod:is_stale at one vertex, O(1) */
+            for (uint32_t v = 0; v < n; v++) {
+                ERL_NIF_TERM iv = want_ok_tuple("is_delivered",
+                                                call("is_delivered", 3, A(sim, mock_uint(v), mock_uint(0))));
+                one += mock_is_atom(mock_elem(iv, 1), "true");
+            }
+            fprintf(g_out, ", \"c2_getters\": {\"delivered_mono\": %llu, \"messages\": %zu, \"rows0\": %zu, "
+                    "\"is_delivered\": %llu}",
+                    (unsigned long long)dmsum, mock_list_len(mock_elem(ms, 1)), mock_list_len(mock_elem(rw, 1)),
+                    (unsigned long long)one);
         }
         /* the same overlay, vertex-sharded at world 1 with the library's own RCCL communicator */
         ERL_NIF_TERM sim7 = new_sim(0x5EED0002ull);

@@ -55,7 +55,7 @@ def test_nif_harness_on_gpu(tmp_path):
     n = rep["c2"]["n"]
     assert rep["c2"]["delivered"] == n                       # the reliable-broadcast postcondition
     assert rep["shard_rccl_world1"] == {"rounds": rep["c2"]["rounds"], "delivered": n, "step2": 2}
-    assert rep["c2_getters"] == {"delivered_mono": n, "messages": 0, "rows0": 0}
+    assert rep["c2_getters"] == {"delivered_mono": n, "messages": 0, "rows0": 0, "is_delivered": n}
     assert rep["demers"]["complete"] == rep["demers"]["n"]
     assert rep["fullmem"]["knows_all"] == rep["fullmem"]["n"]
     assert rep["fullmem"]["tokens_used"] == rep["fullmem"]["own_tokens"] == rep["fullmem"]["n"]
