@@ -716,6 +716,120 @@ static ERL_NIF_TERM nif_scamp_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
     return out;
 }
 
+/* ---- membership messages on the wire ------------------
+ * A SCAMP message as the pluggable manager carries it
+ * (partisan_pluggable_peer_service_manager.erl:1396-1407):
+ *   {Src, Dst, Seq, {membership_strategy, Msg}}
+ * Msg in the strategy's own shape (partisan_scamp_v2_membership_strategy.erl
+ * :101-347): {forward_subscription, A} | {keep_subscription, A} | {ping, A} |
+ * {remove_subscription, A} | {replace_subscription, A, B} |
+ * {bootstrap_remove_subscription, A}; A, B, Src, Dst are vertex ids (the
+ * Erlang cluster maps them to node specs), Seq the sender's emission index. */
+static const char* const kScTag[] = {"", "forward_subscription", "keep_subscription", "ping",
+                                     "remove_subscription", "replace_subscription", "bootstrap_remove_subscription"};
+
+static ERL_NIF_TERM sc_msg_term(ErlNifEnv* env, const psim_scamp_msg* m) {
+    ERL_NIF_TERM body = m->type == PSIM_SC_REPLACE
+                            ? enif_make_tuple3(env, mk_atom(env, kScTag[m->type]), enif_make_uint(env, m->a),
+                                               enif_make_uint(env, m->b))
+                            : enif_make_tuple2(env, mk_atom(env, kScTag[m->type]), enif_make_uint(env, m->a));
+    return enif_make_tuple4(env, enif_make_uint(env, m->src), enif_make_uint(env, m->dst), enif_make_uint(env, m->seq),
+                            enif_make_tuple2(env, mk_atom(env, "membership_strategy"), body));
+}
+
+static ERL_NIF_TERM sc_msg_list(ErlNifEnv* env, const psim_scamp_msg* m, size_t k) {
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (size_t i = k; i-- > 0;) list = enif_make_list_cell(env, sc_msg_term(env, &m[i]), list);
+    return list;
+}
+
+/* the inverse of sc_msg_term; 0 on a malformed term */
+static int sc_msg_parse(ErlNifEnv* env, ERL_NIF_TERM t, psim_scamp_msg* m) {
+    int n, nb, nm;
+    const ERL_NIF_TERM *f, *b, *w;
+    unsigned src, dst, seq, x, y = 0;
+    if (!enif_get_tuple(env, t, &n, &f) || n != 4 || !enif_get_uint(env, f[0], &src) ||
+        !enif_get_uint(env, f[1], &dst) || !enif_get_uint(env, f[2], &seq) || !enif_get_tuple(env, f[3], &nm, &w) ||
+        nm != 2 || !enif_is_identical(w[0], mk_atom(env, "membership_strategy")) || !enif_get_tuple(env, w[1], &nb, &b) ||
+        nb < 2 || !enif_get_uint(env, b[1], &x))
+        return 0;
+    for (uint32_t k = PSIM_SC_FORWARD; k <= PSIM_SC_BOOTSTRAP_REMOVE; k++) {
+        if (!enif_is_identical(b[0], mk_atom(env, kScTag[k]))) continue;
+        if (nb != (k == PSIM_SC_REPLACE ? 3 : 2)) return 0;
+        if (k == PSIM_SC_REPLACE && !enif_get_uint(env, b[2], &y)) return 0;
+        m->type = k; m->src = src; m->dst = dst; m->seq = seq; m->a = x; m->b = y;
+        return 1;
+    }
+    return 0;
+}
+
+/* scamp_messages(Sim) -> {ok, [{Src, Dst, Seq, {membership_strategy, Msg}}]}:
+ * the messages the next round delivers, in handling order (psim_scamp_messages) */
+static ERL_NIF_TERM nif_scamp_messages(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_messages(r->h, NULL, 0, &k);
+    psim_scamp_msg* m = rc == PSIM_OK ? (psim_scamp_msg*)enif_alloc((k ? k : 1) * sizeof(psim_scamp_msg)) : NULL;
+    if (rc == PSIM_OK) rc = m ? psim_scamp_messages(r->h, m, k, &k) : PSIM_ENOMEM;
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(m); return err(env, rc); }
+    ERL_NIF_TERM list = sc_msg_list(env, m, k);
+    enif_free(m);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* scamp_take(Sim, Dst) -> {ok, [Message]}: takes Dst's messages off the wire
+ * (psim_scamp_take) -- what a manager hands to the node they are for */
+static ERL_NIF_TERM nif_scamp_take(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned dst;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &dst)) return enif_make_badarg(env);
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_messages(r->h, NULL, 0, &k);          /* an upper bound for Dst's share */
+    psim_scamp_msg* m = rc == PSIM_OK ? (psim_scamp_msg*)enif_alloc((k ? k : 1) * sizeof(psim_scamp_msg)) : NULL;
+    if (rc == PSIM_OK) rc = m ? psim_scamp_take(r->h, dst, m, k, &k) : PSIM_ENOMEM;
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(m); return err(env, rc); }
+    ERL_NIF_TERM list = sc_msg_list(env, m, k);
+    enif_free(m);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* scamp_put(Sim, [Message]) -> ok: messages onto the wire for the next round
+ * (psim_scamp_put) -- what handle_message/2 of a simulated node received */
+static ERL_NIF_TERM nif_scamp_put(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+    size_t k = 0, cap = 16;
+    psim_scamp_msg* m = (psim_scamp_msg*)enif_alloc(cap * sizeof(psim_scamp_msg));
+    ERL_NIF_TERM list = argv[1], head, tail;
+    while (m && enif_get_list_cell(env, list, &head, &tail)) {
+        if (k == cap) {
+            psim_scamp_msg* g = (psim_scamp_msg*)enif_alloc(2 * cap * sizeof(psim_scamp_msg));
+            if (g) memcpy(g, m, cap * sizeof(psim_scamp_msg));
+            enif_free(m);
+            m = g;
+            cap *= 2;
+            if (!m) break;
+        }
+        if (!sc_msg_parse(env, head, &m[k])) { enif_free(m); return enif_make_badarg(env); }
+        k++;
+        list = tail;
+    }
+    if (!m) return err(env, PSIM_ENOMEM);
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_put(r->h, m, k);
+    enif_mutex_unlock(r->mu);
+    enif_free(m);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
 /* scamp_views(Sim) -> {ok, PartialViews, PvLens, InViews, IvLens}: u32 rows of
  * PSIM_SCAMP_PV_CAP / PSIM_SCAMP_IV_CAP ids in the reference's list order */
 static ERL_NIF_TERM nif_scamp_views(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -1216,6 +1330,9 @@ static ErlNifFunc funcs[] = {
     {"scamp_crash", 2, nif_scamp_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_step", 2, nif_scamp_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_views", 1, nif_scamp_views, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_messages", 1, nif_scamp_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_take", 2, nif_scamp_take, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_put", 2, nif_scamp_put, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_setup", 4, nif_fm_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_join", 3, nif_fm_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_leave", 3, nif_fm_leave, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -13,6 +13,7 @@
          demers_setup/5, demers_run/2,
          vclock/4,
          scamp_setup/5, scamp_join/3, scamp_leave/3, scamp_crash/2, scamp_step/2, scamp_views/1,
+         scamp_messages/1, scamp_take/2, scamp_put/2,
          fm_setup/4, fm_join/3, fm_leave/3, fm_step/2, fm_state/1, fm_tokens/1,
          c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
          causal_setup/6, causal_step/2, causal_clocks/1,
@@ -149,6 +150,20 @@ scamp_crash(_Sim, _Vs) -> erlang:nif_error(nif_not_loaded).
 scamp_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 -spec scamp_views(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
 scamp_views(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% The membership messages on the wire: {Src, Dst, Seq, {membership_strategy,
+%% Msg}} with Msg in partisan_scamp_v2_membership_strategy's own shapes
+%% ({forward_subscription, A}, {replace_subscription, A, B}, ...; vertex ids).
+-type wire_msg() :: {non_neg_integer(), non_neg_integer(), non_neg_integer(), {membership_strategy, tuple()}}.
+%% the next round's messages in handling order (dst, src, seq)
+-spec scamp_messages(sim()) -> {ok, [wire_msg()]} | error().
+scamp_messages(_Sim) -> erlang:nif_error(nif_not_loaded).
+%% takes Dst's messages off the wire (the next round does not deliver them)
+-spec scamp_take(sim(), non_neg_integer()) -> {ok, [wire_msg()]} | error().
+scamp_take(_Sim, _Dst) -> erlang:nif_error(nif_not_loaded).
+%% puts messages on the wire for the next round (a node's handle_message/2)
+-spec scamp_put(sim(), [wire_msg()]) -> ok | error().
+scamp_put(_Sim, _Msgs) -> erlang:nif_error(nif_not_loaded).
 
 %% ---- full membership (psim_fm_*): state_orset token bitmaps per node ----------
 -spec fm_setup(sim(), pos_integer(), pos_integer(), pos_integer()) -> ok | error().

@@ -8,7 +8,9 @@
 %% device rounds -- one periodic interval (`periodic_rounds' rounds, the
 %% strategy's periodic/1 inside them, src/partisan_pluggable_peer_service_manager.erl
 %% :1386-1419) once every live simulated node's periodic/1 has been called
-%% for the interval.  Membership messages never leave the device.
+%% for the interval.  Membership messages travel on the device; outgoing/1,
+%% incoming/1 and deliver/2 render, take and put them in the wire form
+%% {membership_strategy, Msg} the pluggable manager carries.
 %%
 %% Simulated node v is named 'nXXXXXXXX' (zero-padded v) with listen port
 %% 10000 + v, so every Erlang term order of node specs equals vertex order
@@ -18,7 +20,8 @@
 -export([start/1, stop/0, sim/0, n/0,
          node_spec/1, vertex/1, self_vertex/0, set_self/1,
          join/2, leave/2, periodic/1, members/1, run_interval/0,
-         load_overlay/2, heartbeat/1, delivered/3]).
+         load_overlay/2, heartbeat/1, delivered/3,
+         outgoing/1, incoming/1, deliver/2]).
 
 -define(KEY, ?MODULE).
 -define(HIST, partisan_gpu_sim_heartbeats).
@@ -39,7 +42,7 @@ start(#{n := N, strategy := Strategy} = Opts) ->
                     end,
             case Setup of
                 ok ->
-                    Calls = atomics:new(1, []),
+                    Calls = atomics:new(2, []),     %% 1: periodic calls this interval; 2: wire seq
                     catch ets:delete(?HIST),
                     ?HIST = ets:new(?HIST, [named_table, public, set]),
                     persistent_term:put(?KEY, #{sim => Sim, n => N, strategy => Strategy,
@@ -190,6 +193,44 @@ heartbeat(Root) ->
         Err ->
             Err
     end.
+
+%% ---- membership messages on the wire (SURVEY 8(f) row 3) ------------------
+%% What the pluggable manager of simulated node V would put on
+%% ?MEMBERSHIP_CHANNEL for its strategy's Outgoing messages
+%% (src/partisan_pluggable_peer_service_manager.erl:1396-1407, 1764-1776):
+%% [{DstSpec, {membership_strategy, Msg}}] with Msg in the strategy's own
+%% shape and node specs for node ids.  The simulated nodes' messages travel
+%% on the device; this renders the ones V sent that the next round delivers.
+-spec outgoing(non_neg_integer()) -> [{map(), {membership_strategy, tuple()}}].
+outgoing(V) ->
+    {ok, Msgs} = partisan_gpu_sim:scamp_messages(sim()),
+    [{node_spec(Dst), {membership_strategy, spec_msg(M)}}
+     || {Src, Dst, _Seq, {membership_strategy, M}} <- Msgs, Src =:= V].
+
+%% The messages for V the next round would deliver, taken off the device:
+%% what V's manager receives as {membership_strategy, Msg} and hands to
+%% handle_message/2 (:1739-1808) -- e.g. for a node that is run outside the
+%% simulation.  [{SrcSpec, Msg}] in handling order.
+-spec incoming(non_neg_integer()) -> [{map(), tuple()}].
+incoming(V) ->
+    {ok, Msgs} = partisan_gpu_sim:scamp_take(sim(), V),
+    [{node_spec(Src), spec_msg(M)} || {Src, _Dst, _Seq, {membership_strategy, M}} <- Msgs].
+
+%% handle_message(Msg, State) at simulated node V: Msg, as a manager received
+%% it, goes onto the device for V's next round.  The sender is not part of
+%% the message (the manager does not pass it), so it is ordered after the
+%% simulated senders (source id N, by arrival).
+-spec deliver(non_neg_integer(), tuple()) -> ok | {error, term()}.
+deliver(V, Msg) ->
+    #{sim := Sim, n := N, calls := Calls} = persistent_term:get(?KEY),
+    Seq = atomics:add_get(Calls, 2, 1),
+    partisan_gpu_sim:scamp_put(Sim, [{N, V, Seq, {membership_strategy, id_msg(Msg)}}]).
+
+spec_msg({replace_subscription, A, B}) -> {replace_subscription, node_spec(A), node_spec(B)};
+spec_msg({Tag, A}) -> {Tag, node_spec(A)}.
+
+id_msg({replace_subscription, A, B}) -> {replace_subscription, vertex(A), vertex(B)};
+id_msg({Tag, A}) -> {Tag, vertex(A)}.
 
 %% Mod:is_stale/1 at vertex V for heartbeat Mono of Origin (the backend's
 %% interval set, src/partisan_plumtree_backend.erl:229-244).

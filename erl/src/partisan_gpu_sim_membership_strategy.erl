@@ -8,9 +8,14 @@
 %% (psim_scamp_* / psim_fm_*, the same restatement the oracle checks).
 %%
 %% The simulated nodes' membership messages travel on the device, so every
-%% callback returns no outgoing messages; members are read back from the
-%% device after the interval runs.  A membership message from a node outside
-%% the simulation is not part of it and leaves the state unchanged.
+%% callback returns no outgoing messages (the manager would send them twice);
+%% partisan_gpu_sim_cluster:outgoing/1 renders them as the manager puts them
+%% on the wire, [{DstSpec, {membership_strategy, Msg}}], and incoming/1 takes
+%% a node's messages off the device.  A {membership_strategy, Msg} the node's
+%% manager receives (SCAMP: forward_subscription, keep_subscription, ping,
+%% remove_subscription, replace_subscription, bootstrap_remove_subscription)
+%% goes onto the device for the node's next round (handle_message/2).
+%% Members are read back from the device after the interval runs.
 -module(partisan_gpu_sim_membership_strategy).
 
 -behaviour(partisan_membership_strategy).
@@ -43,7 +48,11 @@ periodic(#gpu_state{vertex = V} = State) ->
     ok = partisan_gpu_sim_cluster:periodic(V),
     {ok, partisan_gpu_sim_cluster:members(V), [], State}.
 
-%% {membership_strategy, Msg} (pluggable :1739-1808)
+%% {membership_strategy, Msg} (pluggable :1739-1808): onto the device for V
+%% (SCAMP strategies; a full-membership state is merged by join/3's path)
+handle_message(Msg, #gpu_state{vertex = V} = State) when is_tuple(Msg), is_atom(element(1, Msg)) ->
+    ok = partisan_gpu_sim_cluster:deliver(V, Msg),
+    {ok, partisan_gpu_sim_cluster:members(V), [], State};
 handle_message(_Msg, #gpu_state{vertex = V} = State) ->
     {ok, partisan_gpu_sim_cluster:members(V), [], State}.
 

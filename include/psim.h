@@ -549,6 +549,30 @@ int  psim_scamp_get_views(const psim_handle* h, uint32_t* pv, uint32_t* npv, uin
 /* draws of the current incarnation, round of the last ping handled (-1 none), alive */
 int  psim_scamp_get_nodes(const psim_handle* h, uint64_t* draws, int32_t* last_ping, uint8_t* alive, size_t n);
 int  psim_scamp_inflight(const psim_handle* h, uint64_t* messages);
+/* The membership messages on the wire: what the pluggable
+ * manager sends as {membership_strategy, Msg} on ?MEMBERSHIP_CHANNEL
+ * (partisan_pluggable_peer_service_manager.erl:1396-1407, 1764-1776), one
+ * record per message the next round delivers.  type (PSIM_SC_*) and a / b
+ * give the reference term (partisan_scamp_v{1,2}_membership_strategy.erl):
+ *   FORWARD {forward_subscription, A}  KEEP {keep_subscription, A}
+ *   PING {ping, A}  REMOVE {remove_subscription, A}
+ *   REPLACE {replace_subscription, A, B}  BOOTSTRAP_REMOVE {bootstrap_remove_subscription, A}
+ * with A, B vertex ids (node specs in the Erlang adapter); seq = the sender's
+ * emission index (the schedule handles a vertex's inbox in (src, seq) order). */
+enum { PSIM_SC_FORWARD = 1, PSIM_SC_KEEP = 2, PSIM_SC_PING = 3, PSIM_SC_REMOVE = 4, PSIM_SC_REPLACE = 5,
+       PSIM_SC_BOOTSTRAP_REMOVE = 6 };
+typedef struct psim_scamp_msg { uint32_t type, src, dst, seq, a, b; } psim_scamp_msg;
+/* the messages in handling order (dst, src, seq); *count = total, entries past cap not written */
+int  psim_scamp_messages(const psim_handle* h, psim_scamp_msg* out, size_t cap, size_t* count);
+/* takes the messages for vertex dst off the wire (the next round will not
+ * deliver them), in (src, seq) order; PSIM_EINVAL when cap is too small
+ * (nothing taken; *count = what it needs) */
+int  psim_scamp_take(psim_handle* h, uint32_t dst, psim_scamp_msg* out, size_t cap, size_t* count);
+/* puts messages on the wire for the next round -- e.g. the ones a node's
+ * manager received (handle_message/2 of the Erlang adapter); src may be any
+ * id, a sender outside the simulated cluster included: the schedule orders
+ * by (src, seq) */
+int  psim_scamp_put(psim_handle* h, const psim_scamp_msg* msgs, size_t k);
 
 /* --- C3: Plumtree repair over churning SCAMP v2 ------------------------
  * The pluggable manager runs SCAMP v2 (the psim_scamp_* state of this

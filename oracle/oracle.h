@@ -312,6 +312,8 @@ void orc_scamp_leave(orc_scamp* s, uint32_t v, uint32_t node);
 void orc_scamp_crash(orc_scamp* s, uint32_t v);
 uint32_t orc_scamp_step(orc_scamp* s, uint32_t rounds, orc_scamp_stats* st);
 size_t orc_scamp_inflight(const orc_scamp* s);
+/* next round's messages as {type, src, dst, seq, a, b} records (out6[6 * cap]), handling order */
+size_t orc_scamp_pending(const orc_scamp* s, uint32_t* out6, size_t cap);
 size_t orc_scamp_view(const orc_scamp* s, uint32_t v, int which, uint32_t* out, size_t cap);
 uint64_t orc_scamp_draws(const orc_scamp* s, uint32_t v);
 int orc_scamp_alive(const orc_scamp* s, uint32_t v);

@@ -255,6 +255,8 @@ def lib():
         L.orc_scamp_step.argtypes = [C.c_void_p, C.c_uint32, P(ScampStats)]
         L.orc_scamp_inflight.argtypes = [C.c_void_p]
         L.orc_scamp_inflight.restype = sz
+        L.orc_scamp_pending.argtypes = [C.c_void_p, P(C.c_uint32), sz]
+        L.orc_scamp_pending.restype = sz
         L.orc_scamp_view.argtypes = [C.c_void_p, C.c_uint32, C.c_int, P(C.c_uint32), sz]
         L.orc_scamp_view.restype = sz
         L.orc_scamp_draws.argtypes = [C.c_void_p, C.c_uint32]
@@ -892,6 +894,13 @@ class Scamp:
 
     def inflight(self):
         return lib().orc_scamp_inflight(self._h)
+
+    def pending(self):
+        """Next round's messages as (type, src, dst, seq, a, b) tuples in handling order."""
+        n = lib().orc_scamp_pending(self._h, None, 0)
+        buf = np.zeros(max(1, 6 * n), np.uint32)
+        lib().orc_scamp_pending(self._h, _u32p(buf), n)
+        return [tuple(int(x) for x in buf[6 * i:6 * i + 6]) for i in range(n)]
 
     def view(self, v, which=0, cap=4096):
         out = (C.c_uint32 * cap)()

@@ -396,6 +396,27 @@ uint32_t orc_scamp_step(orc_scamp* s, uint32_t rounds, orc_scamp_stats* st) {
 
 size_t orc_scamp_inflight(const orc_scamp* s) { return s->nnxt; }
 
+static int scmsg_cmp(const void* x, const void* y) {
+    const scmsg* p = (const scmsg*)x; const scmsg* q = (const scmsg*)y;
+    if (p->dst != q->dst) return p->dst < q->dst ? -1 : 1;
+    if (p->src != q->src) return p->src < q->src ? -1 : 1;
+    return p->seq < q->seq ? -1 : p->seq > q->seq;
+}
+/* the messages the next round delivers, in handling order (dst, src, seq):
+ * the wire the pluggable manager carries ({membership_strategy, Msg},
+ * partisan_pluggable_peer_service_manager.erl:1396-1407) -- test view */
+size_t orc_scamp_pending(const orc_scamp* s, uint32_t* out6, size_t cap) {
+    scmsg* m = (scmsg*)malloc((s->nnxt ? s->nnxt : 1) * sizeof(scmsg));
+    memcpy(m, s->nxt, s->nnxt * sizeof(scmsg));
+    qsort(m, s->nnxt, sizeof(scmsg), scmsg_cmp);
+    for (size_t i = 0; i < s->nnxt && i < cap; i++) {
+        uint32_t* o = out6 + 6 * i;
+        o[0] = m[i].type; o[1] = m[i].src; o[2] = m[i].dst; o[3] = (uint32_t)m[i].seq; o[4] = m[i].a; o[5] = m[i].b;
+    }
+    free(m);
+    return s->nnxt;
+}
+
 size_t orc_scamp_view(const orc_scamp* s, uint32_t v, int which, uint32_t* out, size_t cap) {
     const ulist* l = which ? &s->nd[v].iv : &s->nd[v].pv;
     for (uint32_t i = 0; i < l->n && i < cap; i++) out[i] = l->a[i];

@@ -98,6 +98,11 @@ SCAMP_MSG_KINDS = {1: "forward_subscription", 2: "keep_subscription", 3: "ping",
                    5: "replace_subscription", 6: "bootstrap_remove_subscription"}
 
 
+class ScampMsg(C.Structure):
+    """psim_scamp_msg: one membership message on the wire (PSIM_SC_* type, a / b node ids)."""
+    _fields_ = [(k, C.c_uint32) for k in ("type", "src", "dst", "seq", "a", "b")]
+
+
 class ScampStats(C.Structure):
     _fields_ = [("sent", C.c_uint64 * 7)] + [(k, C.c_uint64) for k in (
         "dropped", "processed", "draws", "stopped", "error", "pv_sum", "inview_sum", "resub", "algo_bytes")] + \
@@ -254,6 +259,9 @@ SIGNATURES = {
                                        C.c_size_t]),
     "psim_scamp_get_nodes": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_int32), _P(C.c_uint8), C.c_size_t]),
     "psim_scamp_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_scamp_messages": (C.c_int, [_H, _P(ScampMsg), C.c_size_t, _P(C.c_size_t)]),
+    "psim_scamp_take": (C.c_int, [_H, C.c_uint32, _P(ScampMsg), C.c_size_t, _P(C.c_size_t)]),
+    "psim_scamp_put": (C.c_int, [_H, _P(ScampMsg), C.c_size_t]),
     "psim_c3_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_c3_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_c3_crash": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),

@@ -750,3 +750,88 @@ int psim_scamp_inflight(const psim_handle* h, uint64_t* messages) {
 }
 
 }  // extern "C"
+
+namespace {
+// The queue the next round reads, copied down (record order is the
+// atomics' order: meaningless; callers sort).
+int sc_queue(psim_handle* h, const ScState& s, std::vector<ScMsg>& q) {
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    SCCHK(h, hipStreamSynchronize(handle_stream(h)));
+    uint32_t c = 0;
+    SCCHK(h, hipMemcpy(&c, s.nmsg + s.par, 4, hipMemcpyDeviceToHost));
+    q.resize(std::min(c, s.cap));
+    if (!q.empty()) SCCHK(h, hipMemcpy(q.data(), s.msg[s.par], q.size() * sizeof(ScMsg), hipMemcpyDeviceToHost));
+    return PSIM_OK;
+}
+bool handling_less(const ScMsg& x, const ScMsg& y) {
+    return x.dst != y.dst ? x.dst < y.dst : (x.src != y.src ? x.src < y.src : x.seq < y.seq);
+}
+psim_scamp_msg to_abi(const ScMsg& m) { return psim_scamp_msg{m.type, m.src, m.dst, m.seq, m.a, m.b}; }
+}  // namespace
+
+extern "C" {
+
+int psim_scamp_messages(const psim_handle* h, psim_scamp_msg* out, size_t cap, size_t* count) {
+    if (!h || !count || (cap && !out)) return PSIM_EINVAL;
+    const ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    std::vector<ScMsg> q;
+    if (int rc = sc_queue(hh, *s, q)) return rc;
+    std::sort(q.begin(), q.end(), handling_less);
+    *count = q.size();
+    for (size_t i = 0; i < q.size() && i < cap; i++) out[i] = to_abi(q[i]);
+    return PSIM_OK;
+}
+
+int psim_scamp_take(psim_handle* h, uint32_t dst, psim_scamp_msg* out, size_t cap, size_t* count) {
+    if (!h || !count || (cap && !out)) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    if (dst >= s->n) return handle_fail(h, PSIM_EINVAL, "scamp_take: vertex %u of %u", dst, s->n);
+    std::vector<ScMsg> q, keep, took;
+    if (int rc = sc_queue(h, *s, q)) return rc;
+    for (const ScMsg& m : q) (m.dst == dst ? took : keep).push_back(m);
+    *count = took.size();
+    if (took.size() > cap) return handle_fail(h, PSIM_EINVAL, "scamp_take: %zu messages for %u, room for %zu",
+                                              took.size(), dst, cap);
+    std::sort(took.begin(), took.end(), handling_less);
+    for (size_t i = 0; i < took.size(); i++) out[i] = to_abi(took[i]);
+    if (took.empty()) return PSIM_OK;
+    const hipStream_t st = handle_stream(h);
+    const uint32_t k = uint32_t(keep.size());
+    if (k) SCCHK(h, hipMemcpyAsync(s->msg[s->par], keep.data(), keep.size() * sizeof(ScMsg), hipMemcpyHostToDevice, st));
+    SCCHK(h, hipMemcpyAsync(s->nmsg + s->par, &k, 4, hipMemcpyHostToDevice, st));
+    SCCHK(h, hipStreamSynchronize(st));
+    return PSIM_OK;
+}
+
+int psim_scamp_put(psim_handle* h, const psim_scamp_msg* msgs, size_t k) {
+    if (!h || (k && !msgs)) return PSIM_EINVAL;
+    ScState* s = sc_of(h);
+    if (!s) return PSIM_ESTATE;
+    std::vector<ScMsg> add(k);
+    for (size_t i = 0; i < k; i++) {
+        const psim_scamp_msg& m = msgs[i];
+        if (m.type < PSIM_SC_FORWARD || m.type > PSIM_SC_BOOTSTRAP_REMOVE || m.dst >= s->n || m.a >= s->n ||
+            (m.type == PSIM_SC_REPLACE && m.b >= s->n))
+            return handle_fail(h, PSIM_EINVAL, "scamp_put: message %zu (type %u, dst %u, a %u, b %u)", i, m.type, m.dst,
+                               m.a, m.b);
+        add[i] = ScMsg{m.type, m.src, m.dst, m.seq, m.a, m.b};
+    }
+    if (!k) return PSIM_OK;
+    SCCHK(h, hipSetDevice(handle_device(h)));
+    const hipStream_t st = handle_stream(h);
+    SCCHK(h, hipStreamSynchronize(st));
+    uint32_t c = 0;
+    SCCHK(h, hipMemcpy(&c, s->nmsg + s->par, 4, hipMemcpyDeviceToHost));
+    if (uint64_t(c) + k > s->cap)
+        return handle_fail(h, PSIM_EOVERFLOW, "scamp_put: %u + %zu messages > queue of %u", c, k, s->cap);
+    SCCHK(h, hipMemcpyAsync(s->msg[s->par] + c, add.data(), k * sizeof(ScMsg), hipMemcpyHostToDevice, st));
+    const uint32_t nc = c + uint32_t(k);
+    SCCHK(h, hipMemcpyAsync(s->nmsg + s->par, &nc, 4, hipMemcpyHostToDevice, st));
+    SCCHK(h, hipStreamSynchronize(st));
+    return PSIM_OK;
+}
+
+}  // extern "C"

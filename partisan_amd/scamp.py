@@ -12,12 +12,15 @@ Host mirror of the pluggable peer service manager driving the
   * ``step(rounds)``      -- handle_message/2 deliveries (:1739-1808) and the
                              periodic/1 timer (:1386-1419)
   * ``views()``           -- each node's partial view (its `members`) and in-view
+  * ``messages()`` / ``take(v)`` / ``put(msgs)`` -- the membership messages on
+                             the wire, {membership_strategy, Msg} in the
+                             strategy's term shapes (pluggable :1396-1407, :1739-1808)
 """
 import ctypes as C
 
 import numpy as np
 
-from ._lib import ScampStats, check, lib
+from ._lib import ScampMsg, ScampStats, check, lib
 
 _P = C.POINTER
 PV_CAP = 128
@@ -89,6 +92,47 @@ class ScampCluster:
         x = C.c_uint64()
         self._c(lib().psim_scamp_inflight(self.sim._h, C.byref(x)))
         return x.value
+
+    # ---- the wire -------------------------------------
+    KINDS = {1: "forward_subscription", 2: "keep_subscription", 3: "ping", 4: "remove_subscription",
+             5: "replace_subscription", 6: "bootstrap_remove_subscription"}
+
+    @staticmethod
+    def term(m):
+        """(src, dst, seq, ('membership_strategy', Msg)) with Msg the reference's
+        tuple, e.g. ('forward_subscription', A) or ('replace_subscription', A, B)."""
+        t, src, dst, seq, a, b = m
+        body = (ScampCluster.KINDS[t], a, b) if t == 5 else (ScampCluster.KINDS[t], a)
+        return (src, dst, seq, ("membership_strategy", body))
+
+    @staticmethod
+    def parse(term):
+        src, dst, seq, (tag, body) = term
+        if tag != "membership_strategy":
+            raise ValueError(term)
+        kind = {v: k for k, v in ScampCluster.KINDS.items()}[body[0]]
+        return (kind, src, dst, seq, body[1], body[2] if kind == 5 else 0)
+
+    def messages(self):
+        """The messages the next round delivers as (type, src, dst, seq, a, b), handling order."""
+        k = C.c_size_t()
+        self._c(lib().psim_scamp_messages(self.sim._h, None, 0, C.byref(k)))
+        buf = (ScampMsg * max(1, k.value))()
+        self._c(lib().psim_scamp_messages(self.sim._h, buf, k.value, C.byref(k)))
+        return [(m.type, m.src, m.dst, m.seq, m.a, m.b) for m in buf[:k.value]]
+
+    def take(self, v):
+        """Takes vertex v's messages off the wire (the next round will not deliver them)."""
+        cap = max(1, len(self.messages()))
+        buf = (ScampMsg * cap)()
+        k = C.c_size_t()
+        self._c(lib().psim_scamp_take(self.sim._h, v, buf, cap, C.byref(k)))
+        return [(m.type, m.src, m.dst, m.seq, m.a, m.b) for m in buf[:k.value]]
+
+    def put(self, msgs):
+        """Puts (type, src, dst, seq, a, b) messages on the wire for the next round."""
+        buf = (ScampMsg * max(1, len(msgs)))(*[ScampMsg(*m) for m in msgs])
+        self._c(lib().psim_scamp_put(self.sim._h, buf, len(msgs)))
 
 
 def join_waves(n, seed):

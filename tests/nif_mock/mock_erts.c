@@ -235,6 +235,24 @@ int enif_get_uint(ErlNifEnv* env, ERL_NIF_TERM t, unsigned* out) {
     return 1;
 }
 
+int enif_get_list_cell(ErlNifEnv* env, ERL_NIF_TERM list, ERL_NIF_TERM* head, ERL_NIF_TERM* tail) {
+    (void)env;
+    term_t* x = T(list);
+    if (x->tag != T_CONS) return 0;
+    *head = x->a[0];
+    *tail = x->a[1];
+    return 1;
+}
+
+int enif_get_tuple(ErlNifEnv* env, ERL_NIF_TERM t, int* arity, const ERL_NIF_TERM** items) {
+    (void)env;
+    term_t* x = T(t);
+    if (x->tag != T_TUPLE) return 0;
+    *arity = (int)x->n;
+    *items = x->a;
+    return 1;
+}
+
 int enif_inspect_binary(ErlNifEnv* env, ERL_NIF_TERM t, ErlNifBinary* bin) {
     (void)env;
     term_t* x = T(t);

@@ -201,6 +201,64 @@ int main(int argc, char** argv) {
         fprintf(g_out, ", \"scamp\": {\"n\": %u, \"pv_sum\": %llu, \"view_entries\": %llu}", n, (unsigned long long)pv,
                (unsigned long long)tot);
     }
+    /* ---- SCAMP v2 on the wire: {membership_strategy, Msg} terms each round,
+     *      and one node's messages taken off and put back */
+    {
+        const uint32_t n = 400;
+        ERL_NIF_TERM sim = new_sim(0x5EED0004ull);
+        want_ok("scamp_setup", call("scamp_setup", 5, A(sim, mock_uint(n), mock_uint(2), mock_uint(5), mock_uint(10))));
+        uint64_t s = 11;
+        for (uint32_t k = 1; k < n; k *= 2) {
+            const uint32_t hi = 2 * k < n ? 2 * k : n;
+            uint32_t v[512], c[512];
+            for (uint32_t i = k; i < hi; i++) {
+                v[i - k] = i;
+                c[i - k] = lcg(&s) % k;
+            }
+            want_ok("scamp_join", call("scamp_join", 3, A(sim, u32s(v, hi - k), u32s(c, hi - k))));
+            want_ok_tuple("scamp_step", call("scamp_step", 2, A(sim, mock_uint(3))));
+        }
+        static const char* const tags[] = {"", "forward_subscription", "keep_subscription", "ping",
+                                           "remove_subscription", "replace_subscription",
+                                           "bootstrap_remove_subscription"};
+        fprintf(g_out, ", \"scamp_wire\": {\"n\": %u, \"rounds\": [", n);
+        uint64_t taken = 0;
+        for (int r = 0; r < 12; r++) {
+            ERL_NIF_TERM ms = mock_elem(want_ok_tuple("scamp_messages", call("scamp_messages", 1, A(sim))), 1);
+            fprintf(g_out, "%s[", r ? ", " : "");
+            for (size_t i = 0; i < mock_list_len(ms); i++) {
+                ERL_NIF_TERM m = mock_list_nth(ms, i);             /* {Src, Dst, Seq, {membership_strategy, Msg}} */
+                ERL_NIF_TERM w = mock_elem(m, 3), body = mock_elem(w, 1);
+                if (!mock_is_atom(mock_elem(w, 0), "membership_strategy")) { fprintf(stderr, "bad wire term\n"); return 1; }
+                int t = 0;
+                for (int k = 1; k <= 6; k++) if (mock_is_atom(mock_elem(body, 0), tags[k])) t = k;
+                const uint64_t b = mock_tuple_arity(body) == 3 ? mock_int(mock_elem(body, 2)) : 0;
+                fprintf(g_out, "%s[%d, %llu, %llu, %llu, %llu, %llu]", i ? ", " : "", t,
+                        (unsigned long long)mock_int(mock_elem(m, 0)), (unsigned long long)mock_int(mock_elem(m, 1)),
+                        (unsigned long long)mock_int(mock_elem(m, 2)), (unsigned long long)mock_int(mock_elem(body, 1)),
+                        (unsigned long long)b);
+            }
+            fprintf(g_out, "]");
+            if (r == 5 && mock_list_len(ms) > 0) {   /* a manager's round trip: take one node's messages, put them back */
+                const uint64_t d = mock_int(mock_elem(mock_list_nth(ms, 0), 1));
+                ERL_NIF_TERM got = mock_elem(want_ok_tuple("scamp_take", call("scamp_take", 2, A(sim, mock_uint(d)))), 1);
+                taken = mock_list_len(got);
+                want_ok("scamp_put", call("scamp_put", 2, A(sim, got)));
+            }
+            want_ok_tuple("scamp_step", call("scamp_step", 2, A(sim, mock_uint(1))));
+        }
+        ERL_NIF_TERM vw = want_ok_tuple("scamp_views", call("scamp_views", 1, A(sim)));
+        size_t sz, szl;
+        const uint32_t* pv = (const uint32_t*)mock_bin_data(mock_elem(vw, 1), &sz);
+        const uint32_t* npv = (const uint32_t*)mock_bin_data(mock_elem(vw, 2), &szl);
+        fprintf(g_out, "], \"taken\": %llu, \"views\": [", (unsigned long long)taken);
+        for (uint32_t v = 0; v < n; v++) {
+            fprintf(g_out, "%s[", v ? ", " : "");
+            for (uint32_t j = 0; j < npv[v]; j++) fprintf(g_out, "%s%u", j ? ", " : "", pv[v * 128 + j]);
+            fprintf(g_out, "]");
+        }
+        fprintf(g_out, "]}");
+    }
     /* ---- full membership (C1 shape: 16 nodes join node 0) ------------------ */
     {
         const uint32_t n = 16;

@@ -45,6 +45,34 @@ def _lcg(s):
     return s, s >> 33
 
 
+def _check_scamp_wire(w):
+    """the {membership_strategy, Msg} terms the shim renders
+    for a SCAMP v2 run, round by round, equal the oracle's messages in
+    flight (type, src, dst, emission seq, node ids) in handling order; one
+    node's messages taken off the wire (scamp_take) and put back
+    (scamp_put, as its manager's handle_message/2 would) change nothing: the
+    views after 12 more rounds equal the oracle's, which never took them."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    n = w["n"]
+    orc = O.Scamp(n, version=2, c=5, periodic_rounds=10, seed=0x5EED0004)
+    s, k = 11, 1
+    while k < n:
+        hi = min(2 * k, n)
+        for i in range(k, hi):
+            s, r = _lcg(s)
+            orc.join(i, r % k)
+        orc.step(3)
+        k *= 2
+    assert w["taken"] > 0
+    for r, got in enumerate(w["rounds"]):
+        assert [tuple(m) for m in got] == orc.pending(), r
+        orc.step(1)
+    for v in range(n):
+        assert w["views"][v] == orc.view(v), v
+
+
 @pytest.mark.gpu
 def test_nif_harness_on_gpu(tmp_path):
     exe = build_harness()
@@ -60,6 +88,7 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rep["fullmem"]["knows_all"] == rep["fullmem"]["n"]
     assert rep["fullmem"]["tokens_used"] == rep["fullmem"]["own_tokens"] == rep["fullmem"]["n"]
     assert rep["scamp"]["view_entries"] > rep["scamp"]["n"]
+    _check_scamp_wire(rep["scamp_wire"])
     assert 0 < rep["c3"]["delivered_live"] <= rep["c3"]["live"]
     assert rep["causal"]["delivered"] > 0
     assert rep["vclock_merge"] == [3, 1, 4]

@@ -212,3 +212,50 @@ def test_gpu_scamp_c3_scale():
     # every live manager's members contain itself
     assert all(v in pv[v, :npv[v]] for v in idx[:: max(1, len(idx) // 5000)])
     assert all(x["error"] == 0 for x in st)
+
+
+@pytest.mark.gpu
+def test_gpu_scamp_wire_messages():
+    """SURVEY 8(f) row 3 through the Python binding: the messages on the wire
+    (psim_scamp_messages, rendered as the reference terms) equal the oracle's
+    in handling order every round, through churn; taking a node's messages
+    off the wire and putting them back as terms (ScampCluster.term / parse,
+    what a manager's handle_message/2 would hand back) changes nothing."""
+    import partisan_amd as pa
+    n = 600
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.scamp.ScampCluster(sim, n, version=2, c=5, periodic_rounds=5)
+    orc = O.Scamp(n, 2, 5, 5, SEED)
+    for v, c in waves(n):
+        g.join(v, c)
+        for a, b in zip(v, c):
+            orc.join(int(a), int(b))
+        g.step(3)
+        orc.step(3)
+    took = 0
+    for r in range(15):
+        if r in (4, 9):
+            v, c = churn(n, r)
+            g.crash(v)
+            g.join(v, c)
+            for a, b in zip(v, c):
+                orc.crash(int(a))
+                orc.join(int(a), int(b))
+        msgs = g.messages()
+        assert [(t, s, d, q, a, b) for (t, s, d, q, a, b) in msgs] == orc.pending(), r
+        if msgs:
+            d = msgs[len(msgs) // 2][2]
+            terms = [g.term(m) for m in g.take(d)]
+            assert all(t[1] == d and t[3][0] == "membership_strategy" for t in terms)
+            took += len(terms)
+            assert all(m[2] != d for m in g.messages())
+            g.put([g.parse(t) for t in terms])
+            assert sorted(g.messages()) == sorted(msgs)
+        g.step(1)
+        orc.step(1)
+    assert took > 0
+    pv, npv, iv, niv = g.views()
+    for v in range(n):
+        assert list(pv[v, :npv[v]]) == orc.view(v, 0), v
+        assert list(iv[v, :niv[v]]) == orc.view(v, 1), v
+    sim.close()
