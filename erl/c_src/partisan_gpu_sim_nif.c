@@ -154,7 +154,21 @@ static ERL_NIF_TERM nif_reset_trees(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
 }
 
-/* broadcast(Sim, Root) -> {ok, Monotonic} */
+/* restart_backend(Sim, Vertex) -> ok   (the vertex's heartbeat backend
+ * restarts: newer epoch, Monotonic 0, empty timestamp table; heartbeat ids
+ * from then on are Epoch bsl 24 bor Monotonic) */
+static ERL_NIF_TERM nif_restart_backend(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned v;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &v)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_restart_backend(r->h, v);
+    enif_mutex_unlock(r->mu);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
+/* broadcast(Sim, Root) -> {ok, Id}   (Id = Epoch bsl 24 bor Monotonic) */
 static ERL_NIF_TERM nif_broadcast(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
     sim_res* r;
@@ -1301,6 +1315,7 @@ static ErlNifFunc funcs[] = {
     {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_alive", 2, nif_set_alive, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"reset_trees", 1, nif_reset_trees, 0},
+    {"restart_backend", 2, nif_restart_backend, 0},
     {"broadcast", 2, nif_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -6,7 +6,7 @@
 %% pointers u64, byte maps one byte per vertex (see include/psim.h).
 -module(partisan_gpu_sim).
 
--export([new/1, load_csr/3, set_alive/2, reset_trees/1, broadcast/2, step/2, run/2,
+-export([new/1, load_csr/3, set_alive/2, reset_trees/1, restart_backend/2, broadcast/2, step/2, run/2,
          peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, is_delivered/3, rows/2, messages/1, shard_step/2,
          relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
@@ -46,6 +46,12 @@ set_alive(_Sim, _Alive) -> erlang:nif_error(nif_not_loaded).
 -spec reset_trees(sim()) -> ok | error().
 reset_trees(_Sim) -> erlang:nif_error(nif_not_loaded).
 
+%% Vertex's heartbeat backend restarts (backend init/1): newer epoch,
+%% Monotonic 0, empty timestamp table.  Ids are Epoch bsl 24 bor Monotonic.
+-spec restart_backend(sim(), non_neg_integer()) -> ok | error().
+restart_backend(_Sim, _V) -> erlang:nif_error(nif_not_loaded).
+
+%% {ok, Id}: Id = Epoch bsl 24 bor Monotonic (Epoch 0 until a restart)
 -spec broadcast(sim(), non_neg_integer()) -> {ok, non_neg_integer()} | error().
 broadcast(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
 

@@ -20,7 +20,7 @@
 -export([start/1, stop/0, sim/0, n/0,
          node_spec/1, vertex/1, self_vertex/0, set_self/1,
          join/2, leave/2, periodic/1, members/1, run_interval/0,
-         load_overlay/2, heartbeat/1, delivered/3,
+         load_overlay/2, heartbeat/1, restart_backend/1, delivered/3, is_stale/4, graft/4,
          outgoing/1, incoming/1, deliver/2]).
 
 -define(KEY, ?MODULE).
@@ -42,7 +42,8 @@ start(#{n := N, strategy := Strategy} = Opts) ->
                     end,
             case Setup of
                 ok ->
-                    Calls = atomics:new(2, []),     %% 1: periodic calls this interval; 2: wire seq
+                    %% 1: periodic calls this interval; 2: wire seq; 3: heartbeats started
+                    Calls = atomics:new(3, []),
                     catch ets:delete(?HIST),
                     ?HIST = ets:new(?HIST, [named_table, public, set]),
                     persistent_term:put(?KEY, #{sim => Sim, n => N, strategy => Strategy,
@@ -172,26 +173,55 @@ token_node(TokNodes, T) ->
 load_overlay(RowPtr, Col) -> partisan_gpu_sim:load_csr(sim(), RowPtr, Col).
 
 %% backend heartbeat at Root (src/partisan_plumtree_backend.erl:341-368), run to
-%% quiescence; the delivered set of the previous heartbeat of Root is kept for
-%% is_stale/1 of older ids.
--spec heartbeat(non_neg_integer()) -> {ok, {node(), 0, non_neg_integer()}, non_neg_integer()} | {error, term()}.
+%% quiescence.  Returns the broadcast id {Node, Epoch, Monotonic}: Epoch counts
+%% Root's backend restarts (restart_backend/1; erlang:system_time() at init/1
+%% in the reference -- only its order matters, :229-244).  The delivered set
+%% of Root's previous heartbeat is kept for is_stale/1 of older ids.
+-spec heartbeat(non_neg_integer()) ->
+          {ok, {node(), non_neg_integer(), pos_integer()}, non_neg_integer()} | {error, term()}.
 heartbeat(Root) ->
     Sim = sim(),
-    case ets:lookup(?HIST, {latest, Root}) of
-        [{_, Prev}] ->
-            ok = partisan_gpu_sim:focus(Sim, Root),
-            {ok, D} = partisan_gpu_sim:delivered(Sim),
-            ets:insert(?HIST, {{Root, Prev}, D});
-        [] ->
-            ok
-    end,
+    ok = snapshot_latest(Sim, Root),
     case partisan_gpu_sim:broadcast(Sim, Root) of
-        {ok, Mono} ->
-            ets:insert(?HIST, {{latest, Root}, Mono}),
+        {ok, Id} ->
+            S = atomics:add_get(calls(), 3, 1),
+            ets:insert(?HIST, {{latest, Root}, Id, S}),
             {ok, Rounds, _Stats} = partisan_gpu_sim:run(Sim, 100000),
-            {ok, {maps:get(name, node_spec(Root)), 0, Mono}, Rounds};
+            {ok, {maps:get(name, node_spec(Root)), Id bsr 24, Id band 16#FFFFFF}, Rounds};
         Err ->
             Err
+    end.
+
+%% V's heartbeat backend crashes and its supervisor starts it again (backend
+%% init/1 :316-329): newer epoch, Monotonic 0, an empty timestamp table -- V
+%% forgets every origin's heartbeats.  Heartbeats started before this are
+%% not in V's table any more.
+-spec restart_backend(non_neg_integer()) -> ok | {error, term()}.
+restart_backend(V) ->
+    Sim = sim(),
+    %% the newest heartbeat of each origin as delivered so far, before V's
+    %% record of it goes
+    [ok = snapshot_latest(Sim, O) || {{latest, O}, _, _} <- ets:match_object(?HIST, {{latest, '_'}, '_', '_'})],
+    case partisan_gpu_sim:restart_backend(Sim, V) of
+        ok ->
+            ets:insert(?HIST, {{restart, V}, atomics:get(calls(), 3)}),
+            ok;
+        Err ->
+            Err
+    end.
+
+calls() -> maps:get(calls, persistent_term:get(?KEY)).
+
+%% the delivered set of Origin's newest heartbeat, kept as {{hb, Origin, S}, Id, D}
+snapshot_latest(Sim, Origin) ->
+    case ets:lookup(?HIST, {latest, Origin}) of
+        [{_, Id, S}] ->
+            ok = partisan_gpu_sim:focus(Sim, Origin),
+            {ok, D} = partisan_gpu_sim:delivered(Sim),
+            ets:insert(?HIST, {{hb, Origin, S}, Id, D}),
+            ok;
+        [] ->
+            ok
     end.
 
 %% ---- membership messages on the wire (SURVEY 8(f) row 3) ------------------
@@ -232,25 +262,62 @@ spec_msg({Tag, A}) -> {Tag, node_spec(A)}.
 id_msg({replace_subscription, A, B}) -> {replace_subscription, vertex(A), vertex(B)};
 id_msg({Tag, A}) -> {Tag, vertex(A)}.
 
-%% Mod:is_stale/1 at vertex V for heartbeat Mono of Origin (the backend's
-%% interval set, src/partisan_plumtree_backend.erl:229-244).
--spec delivered(non_neg_integer(), non_neg_integer(), non_neg_integer()) -> boolean().
-delivered(V, Origin, Mono) ->
-    case ets:lookup(?HIST, {latest, Origin}) of
+%% V's timestamp-table row for Origin: the ids of Origin's heartbeats V
+%% delivered since its backend last restarted, of the newest epoch among them
+%% (add_timestamp/1 :400-417: a newer epoch replaces the set).  {Epoch, Ids}
+%% or none.
+ts_row(V, Origin) ->
+    Since = case ets:lookup(?HIST, {restart, V}) of [{_, R}] -> R; [] -> 0 end,
+    Latest = ets:lookup(?HIST, {latest, Origin}),
+    LS = case Latest of [{_, _, S0}] -> S0; [] -> 0 end,
+    Old = [{S, Id} || {{hb, _, S}, Id, D} <- ets:match_object(?HIST, {{hb, Origin, '_'}, '_', '_'}),
+                      S > Since, S =/= LS, binary:at(D, V) =:= 1],
+    New = case Latest of
+              [{_, Id, S}] when S > Since ->
+                  %% the newest heartbeat: one vertex, psim_get_delivered_range, O(1)
+                  Sim = sim(),
+                  ok = partisan_gpu_sim:focus(Sim, Origin),
+                  case partisan_gpu_sim:is_delivered(Sim, V, 0) of
+                      {ok, true} -> [{S, Id}];
+                      _ -> []
+                  end;
+              _ ->
+                  []
+          end,
+    case lists:sort(Old ++ New) of
         [] ->
-            false;
-        [{_, Latest}] when Mono > Latest ->
-            false;
-        [{_, Mono}] ->
-            %% one vertex of the newest heartbeat: psim_get_delivered_range,
-            %% O(1) -- not a copy of the whole overlay's delivered set
-            Sim = sim(),
-            ok = partisan_gpu_sim:focus(Sim, Origin),
-            {ok, D} = partisan_gpu_sim:is_delivered(Sim, V, 0),
-            D;
-        [_] ->
-            case ets:lookup(?HIST, {Origin, Mono}) of
-                [{_, D}] -> binary:at(D, V) =:= 1;
-                [] -> false
-            end
+            none;
+        Got ->
+            {_, Last} = lists:last(Got),
+            E = Last bsr 24,
+            {E, [Id || {_, Id} <- Got, Id bsr 24 =:= E]}
     end.
+
+%% Mod:is_stale({Origin, Epoch, Monotonic}) at vertex V (backend :229-244)
+-spec is_stale(non_neg_integer(), non_neg_integer(), non_neg_integer(), non_neg_integer()) -> boolean().
+is_stale(V, Origin, Epoch, Mono) ->
+    case ts_row(V, Origin) of
+        none -> false;
+        {Epoch, Ids} -> lists:member(Epoch bsl 24 bor Mono, Ids);
+        {Epoch0, _} -> Epoch0 > Epoch
+    end.
+
+%% Mod:graft({Origin, Epoch, Monotonic}) at vertex V (backend :254-280):
+%% ok (the payload is the id itself) | stale | not_found
+-spec graft(non_neg_integer(), non_neg_integer(), non_neg_integer(), non_neg_integer()) -> ok | stale | not_found.
+graft(V, Origin, Epoch, Mono) ->
+    case ts_row(V, Origin) of
+        none -> not_found;
+        {Epoch, Ids} ->
+            case lists:member(Epoch bsl 24 bor Mono, Ids) of
+                true -> ok;
+                false -> not_found
+            end;
+        {Epoch0, _} when Epoch0 > Epoch -> stale;
+        _ -> not_found
+    end.
+
+%% is_stale/4 for an id in psim's packed form, Epoch bsl 24 bor Monotonic
+-spec delivered(non_neg_integer(), non_neg_integer(), non_neg_integer()) -> boolean().
+delivered(V, Origin, Id) ->
+    is_stale(V, Origin, Id bsr 24, Id band 16#FFFFFF).

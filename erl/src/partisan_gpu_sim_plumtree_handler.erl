@@ -33,16 +33,18 @@ merge(Timestamp, Timestamp) ->
 merge(_Id, _Payload) ->
     false.
 
-%% backend :229-244: {Node, Epoch, Monotonic} in the origin's interval set
-is_stale({Node, _Epoch, Monotonic}) ->
-    partisan_gpu_sim_cluster:delivered(partisan_gpu_sim_cluster:self_vertex(),
-                                       partisan_gpu_sim_cluster:vertex(Node), Monotonic).
+%% backend :229-244: the origin's row {Node, Epoch0, ISet} of the node's table
+is_stale({Node, Epoch, Monotonic}) ->
+    partisan_gpu_sim_cluster:is_stale(partisan_gpu_sim_cluster:self_vertex(),
+                                      partisan_gpu_sim_cluster:vertex(Node), Epoch, Monotonic).
 
 %% backend :254-280
-graft({_Node, _Epoch, _Monotonic} = Timestamp) ->
-    case is_stale(Timestamp) of
-        true -> {ok, Timestamp};
-        false -> {error, {not_found, Timestamp}}
+graft({Node, Epoch, Monotonic} = Timestamp) ->
+    case partisan_gpu_sim_cluster:graft(partisan_gpu_sim_cluster:self_vertex(),
+                                        partisan_gpu_sim_cluster:vertex(Node), Epoch, Monotonic) of
+        ok -> {ok, Timestamp};
+        stale -> stale;
+        not_found -> {error, {not_found, Timestamp}}
     end.
 
 %% backend :292-293

@@ -126,6 +126,20 @@ int  psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
  * drops all per-root eager/lazy sets (partisan_plumtree_broadcast.erl:607-639,
  * :1320-1328).  O(1): sets are tagged with a tree epoch. */
 int  psim_plumtree_reset_trees(psim_handle* h);
+/* Vertex v's heartbeat backend restarts (its gen_server crashes and is
+ * started again: partisan_plumtree_backend init/1 :316-329): a newer epoch
+ * (erlang:system_time() there; here the restart count, 1..255), Monotonic
+ * 0, and a new timestamp table -- v forgets every origin's heartbeats (each
+ * lane's delivered tag / timestamp set at v).  v's next heartbeat is
+ * {v, Epoch + 1, 1}; a heartbeat of an older epoch is then stale wherever
+ * the newer one was recorded (is_stale :229-244) and the newer one replaces
+ * the origin's set (add_timestamp :400-417).  Heartbeat ids are reported as
+ * Epoch << 24 | Monotonic by every call that returns or takes one (epoch 0
+ * until a restart: the plain Monotonic).  Sharded handles: every shard
+ * calls it.  A static lane keeps one Round per vertex: a vertex that
+ * re-delivers a heartbeat it forgot while still holding its rows reports
+ * PSIM_EOVERFLOW (bit 4); window lanes keep every id. */
+int  psim_plumtree_restart_backend(psim_handle* h, uint32_t v);
 /* Heartbeat at `root`: partisan_plumtree_backend handle_info(heartbeat)
  * (:341-368) -> partisan_plumtree_broadcast:broadcast/2 (:324-326) ->
  * handle_cast({broadcast, Id, Payload, Mod}) (:565-569).  Emits round-0

@@ -149,7 +149,9 @@ int orc_pt_get_peers(const orc_plumtree* s, uint32_t v, uint32_t root,
 /* outstanding rows of v: (peer, round) pairs for message (root, mono) */
 size_t orc_pt_get_outstanding(const orc_plumtree* s, uint32_t v, uint32_t* peers,
                               uint32_t* rounds, uint32_t* monos, size_t cap);
-/* delivered bitmap for heartbeat (origin, mono): 1 byte per vertex */
+/* Heartbeat ids below are psim's form, epoch << 24 | Monotonic (epoch 0
+ * until the origin's backend restarts).  delivered: is_stale(id) at each
+ * vertex (same epoch -> member; else the vertex's set is newer), 1 byte each */
 void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint8_t* out);
 /* Round field of the broadcast each vertex accepted for (origin, mono); 0xFFFFFFFF if none */
 void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint32_t* out);
@@ -333,6 +335,9 @@ void orc_scamp_set_update_hook(orc_scamp* s, orc_scamp_update_fn fn, void* ctx);
 typedef int (*orc_pt_conn_fn)(void* ctx, uint32_t u, uint32_t t);
 void orc_pt_set_conn(orc_plumtree* s, orc_pt_conn_fn fn, void* ctx);
 void orc_pt_restart(orc_plumtree* s, uint32_t v);
+/* v's heartbeat backend restarts: newer epoch, Monotonic 0, empty timestamp table */
+void orc_pt_restart_backend(orc_plumtree* s, uint32_t v);
+uint32_t orc_pt_epoch(const orc_plumtree* s, uint32_t v);
 void orc_pt_queue_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n);
 uint64_t orc_pt_dropped(const orc_plumtree* s);
 /* omission faults: the directed pairs (src[i], dst[i]) lose every message

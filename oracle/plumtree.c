@@ -94,7 +94,7 @@ typedef struct { uint32_t peer, id_node, id_epoch, id_mono, round, root; } outro
 
 /* ---------------- backend ETS {Node, Epoch, ISet} ------------------------ */
 typedef struct { uint32_t node, epoch; orc_iel* is; size_t n, cap; } tsrow;
-typedef struct { uint32_t node, mono, round; } recvrec;   /* instrumentation only */
+typedef struct { uint32_t node, epoch, mono, round; } recvrec;   /* instrumentation only */
 
 typedef struct {
     oset all_members, common_eagers, common_lazys;
@@ -354,7 +354,8 @@ static void handle(orc_plumtree* s, uint32_t v, const orc_msg* m) {
         } else {
             if (s->st) s->st->delivered_new++;
             if (nd->nrr == nd->caprr) { nd->caprr = nd->caprr ? nd->caprr * 2 : 2; nd->rr = (recvrec*)realloc(nd->rr, nd->caprr * sizeof(recvrec)); }
-            nd->rr[nd->nrr].node = m->id_node; nd->rr[nd->nrr].mono = m->id_mono; nd->rr[nd->nrr].round = m->round; nd->nrr++;
+            nd->rr[nd->nrr].node = m->id_node; nd->rr[nd->nrr].epoch = m->id_epoch; nd->rr[nd->nrr].mono = m->id_mono;
+            nd->rr[nd->nrr].round = m->round; nd->nrr++;
             update_peers(nd, m->src, m->root, 0);    /* add_eager(From, Root) */
             eager_push(s, v, m->id_node, m->id_epoch, m->id_mono, m->round + 1, m->root, m->src);
             schedule_lazy_push(s, v, m->id_node, m->id_epoch, m->id_mono, m->round + 1, m->root, m->src);
@@ -448,7 +449,8 @@ uint32_t orc_pt_heartbeat(orc_plumtree* s, uint32_t root) {
     uint32_t mono = ++nd->hb_monotonic;
     add_timestamp(nd, root, nd->hb_epoch, mono);
     if (nd->nrr == nd->caprr) { nd->caprr = nd->caprr ? nd->caprr * 2 : 2; nd->rr = (recvrec*)realloc(nd->rr, nd->caprr * sizeof(recvrec)); }
-    nd->rr[nd->nrr].node = root; nd->rr[nd->nrr].mono = mono; nd->rr[nd->nrr].round = 0xFFFFFFFEu; nd->nrr++;
+    nd->rr[nd->nrr].node = root; nd->rr[nd->nrr].epoch = nd->hb_epoch; nd->rr[nd->nrr].mono = mono;
+    nd->rr[nd->nrr].round = 0xFFFFFFFEu; nd->nrr++;
     orc_round_stats* saved = s->st; s->st = NULL;
     eager_push(s, root, root, nd->hb_epoch, mono, 0, root, root);
     schedule_lazy_push(s, root, root, nd->hb_epoch, mono, 0, root, root);
@@ -498,6 +500,22 @@ void orc_pt_restart(orc_plumtree* s, uint32_t v) {
     nd->nupd = 0;
     nd->fresh = 1;
 }
+
+/* The heartbeat backend of v restarts (its gen_server crashes and the
+ * supervisor starts it again, backend init/1 :316-329): a newer epoch
+ * (erlang:system_time() at init: later than every earlier one), Monotonic 0,
+ * and a new ETS table -- v forgets every origin's timestamps.  The
+ * plumtree server keeps its state.  recv records are instrumentation of the
+ * table, so they go with it. */
+void orc_pt_restart_backend(orc_plumtree* s, uint32_t v) {
+    node_t* nd = &s->nodes[v];
+    nd->hb_epoch++;
+    nd->hb_monotonic = 0;
+    for (size_t i = 0; i < nd->nts; i++) free(nd->ts[i].is);
+    nd->nts = 0;
+    nd->nrr = 0;
+}
+uint32_t orc_pt_epoch(const orc_plumtree* s, uint32_t v) { return s->nodes[v].hb_epoch; }
 
 void orc_pt_queue_update(orc_plumtree* s, uint32_t v, const uint32_t* members, size_t n) {
     node_t* nd = &s->nodes[v];
@@ -637,18 +655,17 @@ size_t orc_pt_get_outstanding(const orc_plumtree* s, uint32_t v, uint32_t* peers
                               uint32_t* rounds, uint32_t* monos, size_t cap) {
     node_t* nd = &s->nodes[v];
     for (size_t i = 0; i < nd->nout && i < cap; i++) {
-        peers[i] = nd->out[i].peer; rounds[i] = nd->out[i].round; monos[i] = nd->out[i].id_mono;
+        /* the id as psim reports it: epoch << 24 | Monotonic (epoch 0 until a backend restart) */
+        peers[i] = nd->out[i].peer; rounds[i] = nd->out[i].round;
+        monos[i] = (nd->out[i].id_epoch << 24) | nd->out[i].id_mono;
     }
     return nd->nout;
 }
 
-void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t mono, uint8_t* out) {
-    for (uint32_t v = 0; v < s->n; v++) {
-        node_t* nd = &s->nodes[v];
-        tsrow* r = ts_lookup(nd, origin);
-        orc_iel e = {mono, mono, 0, 0};
-        out[v] = (r && r->epoch == s->nodes[origin].hb_epoch && orc_iset_is_element(&e, r->is, r->n) == 1) ? 1 : 0;
-    }
+/* id = epoch << 24 | Monotonic (psim's form): out[v] = is_stale(id) at v */
+void orc_pt_get_delivered(const orc_plumtree* s, uint32_t origin, uint32_t id, uint8_t* out) {
+    for (uint32_t v = 0; v < s->n; v++)
+        out[v] = (uint8_t)is_stale((node_t*)&s->nodes[v], origin, id >> 24, id & 0xFFFFFFu);
 }
 
 /* slot of peer p in v's row of the given slot layout, or -1 */
@@ -685,7 +702,10 @@ int orc_pt_dump_state(const orc_plumtree* s, uint32_t root, uint32_t mono, const
         }
         rr[i] = 0xFFFFu;
         for (size_t k = 0; k < nd->nrr; k++)
-            if (nd->rr[k].node == root && nd->rr[k].mono == mono) { rr[i] = (uint16_t)nd->rr[k].round; break; }
+            if (nd->rr[k].node == root && nd->rr[k].epoch == mono >> 24 && nd->rr[k].mono == (mono & 0xFFFFFFu)) {
+                rr[i] = (uint16_t)nd->rr[k].round;
+                break;
+            }
     }
     return ORC_OK;
 }
@@ -718,6 +738,9 @@ void orc_pt_get_recv_round(const orc_plumtree* s, uint32_t origin, uint32_t mono
         node_t* nd = &s->nodes[v];
         out[v] = 0xFFFFFFFFu;
         for (size_t i = 0; i < nd->nrr; i++)
-            if (nd->rr[i].node == origin && nd->rr[i].mono == mono) { out[v] = nd->rr[i].round; break; }
+            if (nd->rr[i].node == origin && nd->rr[i].epoch == mono >> 24 && nd->rr[i].mono == (mono & 0xFFFFFFu)) {
+                out[v] = nd->rr[i].round;
+                break;
+            }
     }
 }

@@ -159,6 +159,9 @@ def lib():
                                         P(C.c_uint16)]
         L.orc_pt_inflight_words.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint32), C.c_uint32, C.c_uint32,
                                             P(C.c_uint32)]
+        L.orc_pt_restart_backend.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_pt_epoch.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_pt_epoch.restype = C.c_uint32
         L.orc_pt_set_omissions.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), sz]
         L.orc_pt_omitted.argtypes = [C.c_void_p]
         L.orc_pt_omitted.restype = C.c_uint64
@@ -465,7 +468,9 @@ class Plumtree:
         lib().orc_pt_set_alive(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)))
 
     def heartbeat(self, root):
-        return lib().orc_pt_heartbeat(self._h, root)
+        """The Monotonic; after a backend restart, epoch << 24 | Monotonic (psim's id form)."""
+        m = lib().orc_pt_heartbeat(self._h, root)
+        return (self.epoch(root) << 24) | m
 
     def update(self, v, members):
         m = np.ascontiguousarray(members, dtype=np.uint32)
@@ -473,6 +478,13 @@ class Plumtree:
 
     def reset_peers_all(self):
         lib().orc_pt_reset_peers_all(self._h)
+
+    def restart_backend(self, v):
+        """v's heartbeat backend restarts: newer epoch, Monotonic 0, empty table."""
+        lib().orc_pt_restart_backend(self._h, v)
+
+    def epoch(self, v):
+        return int(lib().orc_pt_epoch(self._h, v))
 
     def set_omissions(self, pairs):
         """Omission faults on directed (src, dst) pairs; [] heals."""
@@ -513,11 +525,16 @@ class Plumtree:
         lib().orc_pt_pending(self._h, arr, n)
         return [(m.src, m.dst, m.type, m.round) for m in arr[:n]]
 
-    def pending_full(self):
-        """(src, dst, kind, Round, Monotonic) of the messages the next round delivers, in handling order."""
+    def pending_full(self, packed=False):
+        """(src, dst, kind, Round, Monotonic) of the messages the next round
+        delivers, in handling order; packed: the id as psim reports it,
+        epoch << 24 | Monotonic (a prune carries no id: 0)."""
         n = lib().orc_pt_pending(self._h, None, 0)
         arr = (Msg * max(1, n))()
         lib().orc_pt_pending(self._h, arr, n)
+        if packed:
+            return [(m.src, m.dst, m.type, m.round, (m.id_epoch << 24 | m.id_mono) if m.type != 2 else 0)
+                    for m in arr[:n]]
         return [(m.src, m.dst, m.type, m.round, m.id_mono) for m in arr[:n]]
 
     def peers(self, v, root, cap=4096):
@@ -535,6 +552,8 @@ class Plumtree:
         return [(p[i], r[i], m[i]) for i in range(min(n, cap))]
 
     def delivered(self, origin, mono):
+        """is_stale({origin, epoch, mono}) at every vertex; mono is psim's id
+        form, epoch << 24 | Monotonic (epoch 0 until a backend restart)."""
         out = np.zeros(self.n, dtype=np.uint8)
         lib().orc_pt_get_delivered(self._h, origin, mono, out.ctypes.data_as(C.POINTER(C.c_uint8)))
         return out

@@ -169,6 +169,7 @@ SIGNATURES = {
     "psim_get_slots": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint32)]),
     "psim_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_plumtree_reset_trees": (C.c_int, [_H]),
+    "psim_plumtree_restart_backend": (C.c_int, [_H, C.c_uint32]),
     "psim_plumtree_broadcast": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
     "psim_step": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t]),
     "psim_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32)]),

@@ -108,7 +108,8 @@ struct psim_handle {
     uint32_t epoch = 1;        // tree epoch (device tag, low 8 bits)
     uint32_t root = 0;
     bool have_root = false;
-    std::unordered_map<uint32_t, uint32_t> mono_of;  // backend #state.monotonic per origin
+    std::unordered_map<uint32_t, uint32_t> mono_of;  // backend #state per origin: epoch << 24 | monotonic
+    std::unordered_map<uint32_t, uint32_t> next_epoch;  // origins whose backend restarted: the new epoch
     int64_t ost_cnt = 0;       // vertices with outstanding rows
     int64_t live_rows = 0;     // outstanding rows to live peers
     uint64_t inflight = 0;     // messages emitted by the last round / origin
@@ -1446,6 +1447,40 @@ int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
     return PSIM_OK;
 }
 
+int psim_plumtree_restart_backend(psim_handle* h, uint32_t v) {
+    if (!h || !h->n) return PSIM_ESTATE;
+    if (v >= h->sh.n_global) return PSIM_EINVAL;
+    if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "binned handles keep one epoch per root");
+    HIPCHK(h, hipSetDevice(h->device));
+    const auto it = h->mono_of.find(v);
+    const uint32_t cur = it == h->mono_of.end() ? 0u : it->second >> 24;
+    const auto ne = h->next_epoch.find(v);
+    const uint32_t e = (ne == h->next_epoch.end() ? cur : ne->second) + 1u;
+    if (e > 0xFFu) return fail(h, PSIM_EOVERFLOW, "vertex %u: 255 backend restarts", v);
+    h->next_epoch[v] = e;
+    const uint32_t lv = v - h->sh.v_lo;
+    const int focus = h->cur_lane;
+    if (!h->lanes.empty()) save_lane(h);
+    const int nl = h->lanes.empty() ? 1 : (int)h->lanes.size();
+    for (int j = 0; j < nl; j++) {            // v forgets every origin: each lane's root
+        if (!h->lanes.empty()) load_lane(h, j);
+        if (!h->have_root) continue;
+        if (!quiescent(h) && win_capable(h) && !h->win) {
+            // v may deliver the heartbeat in flight again and hold a second
+            // row per peer for it: the lane keeps every row from then on
+            // (every shard decides alike: quiescent() is the global count)
+            const int rc = to_window(h);
+            if (rc) { save_lane(h); load_lane(h, focus); return rc; }
+            save_lane(h);
+        }
+        if (lv < h->n)
+            HIPCHK(h, launch_pt_forget(h->vs, h->win ? h->win->iset : nullptr, lv, (h->serial - 1u) & 0xFFu, h->stream));
+    }
+    if (!h->lanes.empty()) load_lane(h, focus);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PSIM_OK;
+}
+
 int psim_plumtree_reset_trees(psim_handle* h) {
     if (!h || !h->n) return PSIM_ESTATE;
     HIPCHK(h, hipSetDevice(h->device));
@@ -1507,7 +1542,15 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         if (rc) return rc;
     }
     uint32_t& mono = h->mono_of[root];
-    mono++;
+    const auto ne = h->next_epoch.find(root);
+    if (ne != h->next_epoch.end()) {          // the first heartbeat of a restarted backend (init/1: monotonic 0)
+        mono = (ne->second << 24) | 1u;
+        h->next_epoch.erase(ne);
+    } else {
+        // Monotonic 2^24-1 is never an id (a probe for "the row's epoch is newer")
+        if ((mono & 0xFFFFFFu) >= 0xFFFFFEu) return fail(h, PSIM_EOVERFLOW, "root %u: 2^24-2 heartbeats in one epoch", root);
+        mono++;
+    }
     if (mono_out) *mono_out = mono;
     for (int i = 0; i < kNStat; i++) r[i] = 0;
     const uint32_t lr = root - h->sh.v_lo;
@@ -2482,8 +2525,10 @@ int psim_get_delivered_range(const psim_handle* h, uint32_t mono, uint32_t v0, s
     for (size_t i = 0; i < count; i++) {
         const uint32_t lo[4] = {is[2 * i].x, is[2 * i].y, is[2 * i].z, is[2 * i].w};
         const uint32_t hi[4] = {is[2 * i + 1].x, is[2 * i + 1].y, is[2 * i + 1].z, is[2 * i + 1].w};
-        bool d = false;
-        for (int k = 0; k < 4; k++) d |= lo[k] && lo[k] <= mono && mono <= hi[k];
+        bool d = false;                        // is_stale (backend :229-244): same epoch -> member; else newer set
+        if (lo[0] && (lo[0] >> 24) != (mono >> 24)) d = (lo[0] >> 24) > (mono >> 24);
+        else
+            for (int k = 0; k < 4; k++) d |= lo[k] && lo[k] <= mono && mono <= hi[k];
         delivered[i] = d;
     }
     return PSIM_OK;

@@ -479,6 +479,8 @@ hipError_t launch_win_convert(const WinArgs& a, const PtArgs& pa, hipStream_t s)
 hipError_t launch_win_hash(const WinArgs& a, unsigned long long* out, hipStream_t s);
 // delivered[v] = Mod:is_stale({root, epoch, mono})
 hipError_t launch_win_delivered(const WinArgs& a, uint32_t mono, uint8_t* out, hipStream_t s);
+// a backend restart at local vertex v of one lane (iset: the window lane's sets, or null)
+hipError_t launch_pt_forget(uint4* vs, uint4* iset, uint32_t v, uint32_t bad, hipStream_t s);
 
 // Cross-shard exchange owned by a handle (transport.hip).  Calls return
 // PSIM_* codes and put a detail into *err.

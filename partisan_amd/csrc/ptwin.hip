@@ -72,6 +72,35 @@ __device__ bool is_add(ISet& s, uint32_t x) {
     return true;
 }
 
+// ---- the backend's table row for the root: {Root, Epoch, ISet} ----------
+// A heartbeat id is epoch << 24 | Monotonic (psim_plumtree_restart_backend:
+// the root's backend restarted that many times); every interval of a set
+// holds ids of one epoch, so the set's epoch is that of its first interval.
+__device__ __forceinline__ uint32_t id_epoch(uint32_t id) { return id >> 24; }
+__device__ __forceinline__ bool is_empty(const ISet& s) { return s.lo[0] == 0u; }
+// is_stale/1 (backend :229-244): same epoch -> is_element; else Epoch0 > Epoch
+__device__ __forceinline__ bool ts_stale(const ISet& s, uint32_t id) {
+    if (is_empty(s)) return false;
+    const uint32_t e = id_epoch(s.lo[0]);
+    return e == id_epoch(id) ? is_member(s, id) : e > id_epoch(id);
+}
+// add_timestamp/1 (:400-417): a newer epoch replaces the set, an older one is ignored
+__device__ bool ts_add(ISet& s, uint32_t id) {
+    if (!is_empty(s)) {
+        const uint32_t e = id_epoch(s.lo[0]);
+        if (e > id_epoch(id)) return true;
+        if (e < id_epoch(id)) s = ISet{};
+    }
+    return is_add(s, id);
+}
+// graft/1 (:254-280): 0 {ok, M}, 1 stale, 2 {error, not_found}
+__device__ __forceinline__ int ts_graft(const ISet& s, uint32_t id) {
+    if (is_empty(s)) return 2;
+    const uint32_t e = id_epoch(s.lo[0]);
+    if (e == id_epoch(id)) return is_member(s, id) ? 0 : 2;
+    return e > id_epoch(id) ? 1 : 2;
+}
+
 // ---- one vertex of a window lane for one round ----
 struct Ctr {
     uint32_t sent[6], deliv, active, senders, degsum, overflow;
@@ -160,8 +189,8 @@ __device__ __forceinline__ void to_lazy(V& x, uint32_t s) { x.lazy |= 1u << s; x
 __device__ void handle(const WinArgs& a, V& x, Ctr& c, uint32_t s, const PdMsg& m) {
     switch (m.type) {
     case PSIM_MSG_BROADCAST:                          // handle_broadcast/8 :843-857
-        if (!is_member(x.is, m.mono)) {               // merge/2: not stale -> add_timestamp, true
-            if (!is_add(x.is, m.mono)) c.overflow |= 64u;
+        if (!ts_stale(x.is, m.mono)) {                // merge/2: not stale -> add_timestamp, true
+            if (!ts_add(x.is, m.mono)) c.overflow |= 64u;
             c.deliv++;
             if (m.mono == a.mono) {                   // the newest heartbeat's Round / serial tag
                 x.myround = m.round + 1;
@@ -179,7 +208,7 @@ __device__ void handle(const WinArgs& a, V& x, Ctr& c, uint32_t s, const PdMsg& 
         to_lazy(x, s);
         break;
     case PSIM_MSG_IHAVE:                              // handle_ihave/7 :861-876
-        if (is_member(x.is, m.mono)) {
+        if (ts_stale(x.is, m.mono)) {
             emit(a, x, c, s, PSIM_MSG_IGNORED, m.mono, m.round);
         } else {
             emit(a, x, c, s, PSIM_MSG_GRAFT, m.mono, m.round);
@@ -189,12 +218,16 @@ __device__ void handle(const WinArgs& a, V& x, Ctr& c, uint32_t s, const PdMsg& 
     case PSIM_MSG_IGNORED:                            // ack_outstanding/5
         ack_rows(a, x, s, m.mono, m.round);
         break;
-    case PSIM_MSG_GRAFT:                              // handle_graft/7 :880-906: Mod:graft -> {ok, M}
-        if (is_member(x.is, m.mono)) {
+    case PSIM_MSG_GRAFT: {                            // handle_graft/7 :880-906
+        const int g = ts_graft(x.is, m.mono);
+        if (g == 0) {                                 // {ok, M}
             to_eager(x, s);
             emit(a, x, c, s, PSIM_MSG_BROADCAST, m.mono, m.round);
+        } else if (g == 1) {                          // stale: ack_outstanding
+            ack_rows(a, x, s, m.mono, m.round);
         }                                             // {error, not_found}: logged only
         break;
+    }
     default:
         break;
     }
@@ -319,7 +352,7 @@ __global__ void win_origin_kernel(WinArgs a, uint32_t root) {
     v_load(a, root, x);
     const uint32_t live0 = live_slots(a, x);
     const bool rows0 = x.nrow != 0;
-    if (!is_add(x.is, a.mono)) c.overflow |= 64u;
+    if (!ts_add(x.is, a.mono)) c.overflow |= 64u;
     x.myround = 0;
     x.rseq = a.mono8;
     push(a, x, c, kNoPeer, a.mono, 0);
@@ -399,7 +432,7 @@ __global__ __launch_bounds__(kBlock) void win_hash_kernel(WinArgs a, unsigned lo
 
 __global__ __launch_bounds__(kBlock) void win_delivered_kernel(WinArgs a, uint32_t mono, uint8_t* out) {
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
-    if (v < a.n) out[v] = is_member(is_load(a, v), mono) ? 1 : 0;
+    if (v < a.n) out[v] = ts_stale(is_load(a, v), mono) ? 1 : 0;
 }
 
 // Sharded window lanes: the records a round emitted are split by the shard
@@ -486,6 +519,26 @@ hipError_t launch_win_convert(const WinArgs& a, const PtArgs& pa, hipStream_t s)
 
 hipError_t launch_win_hash(const WinArgs& a, unsigned long long* out, hipStream_t s) {
     hipLaunchKernelGGL(win_hash_kernel, dim3(1024), dim3(kBlock), 0, s, a, out);
+    return hipGetLastError();
+}
+
+// psim_plumtree_restart_backend at local vertex v of one lane: the backend's
+// new ETS table has no row for the lane's root -- the static record's
+// delivered tag stops matching (bad = a tag no heartbeat of the lane uses)
+// and a window lane's timestamp set empties
+__global__ void pt_forget_kernel(uint4* vs, uint4* iset, uint32_t v, uint32_t bad) {
+    if (threadIdx.x != 0) return;
+    uint4 st = vs[v];
+    st.w = (st.w & 0xFF00FFFFu) | ((bad & 0xFFu) << 16);
+    vs[v] = st;
+    if (iset) {
+        iset[2 * size_t(v)] = make_uint4(0u, 0u, 0u, 0u);
+        iset[2 * size_t(v) + 1] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+hipError_t launch_pt_forget(uint4* vs, uint4* iset, uint32_t v, uint32_t bad, hipStream_t s) {
+    hipLaunchKernelGGL(pt_forget_kernel, dim3(1), dim3(64), 0, s, vs, iset, v, bad);
     return hipGetLastError();
 }
 

@@ -22,6 +22,7 @@ path; registering any other module raises (no silent CPU fallback).
 import numpy as np
 
 from .sim import Simulator
+from ._lib import PsimError
 
 MEMBERSHIP_CHANNEL = "partisan_membership"   # include/partisan.hrl:120
 
@@ -69,30 +70,49 @@ class PlumtreeBackend(PlumtreeBroadcastHandler):
         return ts, ts
 
     def is_stale(self, message_id):                       # backend :229-244
-        """Monotonic in this node's interval set for the origin: the latest
-        heartbeat's delivery is read from the device, an earlier one's from the
-        delivered set recorded when the origin heartbeated again (a heartbeat
-        runs to quiescence before its origin's next one: PSIM_EBUSY)."""
-        origin, _epoch, mono = message_id
-        c = self.cluster
-        cur = c.ids.get(origin)
-        if cur is None or mono > cur[2]:
-            return False
-        if mono == cur[2]:
-            if origin in c._state:                # this round's state is cached: no device call
-                return bool(c._delivered(origin)[self.node])
-            c.sim.focus(origin)                   # one vertex: psim_get_delivered_range, O(1)
-            return c.sim.delivered_at(self.node)
-        past = c._hist.get(origin, {}).get(mono)   # recorded when the origin heartbeated again
-        return bool(past is not None and past[self.node])
+        """{Origin, Epoch, Monotonic} against this node's table row for the
+        origin: same epoch -> Monotonic in the row's interval set; otherwise
+        stale iff the row holds a newer epoch.  A heartbeat lane that keeps
+        every id (window lane) answers for any id on device; a static lane
+        holds the newest id only, and earlier ones are read from the delivered
+        set recorded when the origin heartbeated again (the lane was static,
+        so that heartbeat had finished)."""
+        return self._row_has(message_id)[0]
 
     def merge(self, message_id, payload):                 # backend :205-215 (read-only view)
         return not self.is_stale(message_id)
 
     def graft(self, message_id):                          # backend :254-280
-        if self.is_stale(message_id):
-            return ("ok", message_id)
-        return ("error", ("not_found", message_id))
+        stale, newer = self._row_has(message_id, want_epoch=True)
+        if not stale:
+            return ("error", ("not_found", message_id))
+        return "stale" if newer else ("ok", message_id)
+
+    def _row_has(self, message_id, want_epoch=False):
+        """(is_stale(id), the row holds a newer epoch than id's)."""
+        origin, epoch, mono = message_id
+        c = self.cluster
+        cur = c.ids.get(origin)
+        if cur is None:
+            return False, False
+        pid = (epoch << 24) | mono
+        cid = (cur[1] << 24) | cur[2]
+        if pid > cid:                                     # not started yet: no row holds it
+            return False, False
+        if pid == cid:                            # the newest id: no row holds a newer epoch
+            if origin in c._state:                # this round's state is cached: no device call
+                return bool(c._delivered(origin)[self.node]), False
+            c.sim.focus(origin)                   # one vertex: psim_get_delivered_range, O(1)
+            return c.sim.delivered_at(self.node), False
+        c.sim.focus(origin)
+        try:                                      # a window lane's table rows answer any id
+            st = c.sim.delivered_at(self.node, pid)
+            # Monotonic 2^24-1 is never an id: stale for it <=> the row's epoch is newer
+            newer = want_epoch and st and c.sim.delivered_at(self.node, (epoch << 24) | 0xFFFFFF)
+            return st, bool(newer)
+        except PsimError:                         # a static lane: the newest id only
+            pass
+        return c._row_from_history(self.node, origin, pid)
 
     def exchange(self, peer):                             # backend :292-293
         return "ignore"
@@ -116,7 +136,10 @@ class PlumtreeBroadcast:
         self.mods = mods
         self.current_id = None            # {Node, Epoch, Monotonic} of the latest heartbeat
         self.ids = {}                     # origin -> its latest heartbeat id
-        self._hist = {}                   # origin -> {Monotonic: delivered set} of its earlier heartbeats
+        self._hist = {}                   # origin -> [(seq, id, delivered set)] of its earlier heartbeats
+        self._seq = 0                     # heartbeats started
+        self._restart = {}                # node -> heartbeats started before its backend last restarted
+        self._latest_seq = {}             # origin -> seq of its newest heartbeat
         self._state = {}                  # root -> device state of its lane (cached until the next round)
         # roots whose per-root sets the device keeps: every root on one GPU
         # (heartbeat lanes); only the latest on a binned / sharded handle
@@ -126,16 +149,58 @@ class PlumtreeBroadcast:
     def broadcast(self, node, mod=PlumtreeBackend):
         """Heartbeat at `node` (backend handle_info(heartbeat) :341-368 ->
         broadcast/2 :324-326).  Returns the message id."""
-        prev = self.ids.get(node)
-        if prev is not None:
-            self._hist.setdefault(node, {})[prev[2]] = self._delivered(node).astype(bool)
-        mono = self.sim.broadcast(node)
+        self._snapshot(node)
+        pid = self.sim.broadcast(node)
         if self._one_lane:
             self.ids = {r: i for r, i in self.ids.items() if r == node}
-        self.current_id = (node, 0, mono)
+        self._seq += 1
+        self.current_id = (node, pid >> 24, pid & 0xFFFFFF)
         self.ids[node] = self.current_id
+        self._latest_seq[node] = self._seq
         self._state = {}
         return self.current_id
+
+    def restart_backend(self, node):
+        """`node`'s heartbeat backend crashes and its supervisor starts it again
+        (backend init/1 :316-329): a newer epoch, Monotonic 0 and an empty
+        timestamp table (psim_plumtree_restart_backend).  The broadcast
+        server's state (trees, outstanding i_haves) is kept."""
+        for origin in list(self.ids):
+            self._snapshot(origin, keep_latest=True)
+        self.sim.restart_backend(node)
+        self._restart[node] = self._seq
+        self._state = {}
+
+    def _snapshot(self, origin, keep_latest=False):
+        """Record the delivered set of origin's newest heartbeat (its lane may
+        be static, keeping the newest id only)."""
+        prev = self.ids.get(origin)
+        if prev is None:
+            return
+        d = self._delivered(origin).astype(bool)
+        h = self._hist.setdefault(origin, [])
+        s = self._latest_seq[origin]
+        h[:] = [x for x in h if x[0] != s]
+        h.append((s, (prev[1] << 24) | prev[2], d))
+
+    def _row_from_history(self, node, origin, pid):
+        """is_stale / newer-epoch from the recorded sets: node's row holds the
+        ids it delivered since its backend last restarted, of the newest
+        epoch among them (add_timestamp/1 :400-417)."""
+        since = self._restart.get(node, 0)
+        got = [(s, i) for s, i, d in self._hist.get(origin, []) if s > since and d[node]]
+        ls = self._latest_seq.get(origin)
+        if ls is not None and ls > since and not any(s == ls for s, _ in got):
+            self.sim.focus(origin)
+            if self.sim.delivered_at(node):
+                cur = self.ids[origin]
+                got.append((ls, (cur[1] << 24) | cur[2]))
+        if not got:
+            return False, False
+        e = max(got)[1] >> 24
+        if e == pid >> 24:
+            return any(i == pid for _, i in got), False
+        return e > pid >> 24, e > pid >> 24
 
     def run(self, max_rounds=100000):
         stats, rounds = self.sim.run(max_rounds)

@@ -144,6 +144,12 @@ class Simulator:
         d = np.diff(np.asarray(self.slot_row_ptr, dtype=np.int64))
         return int(d.max()) if len(d) else 0
 
+    def restart_backend(self, v):
+        """v's heartbeat backend restarts (psim_plumtree_restart_backend): newer
+        epoch, Monotonic 0, v forgets every origin's heartbeats.  Ids are then
+        reported as epoch << 24 | Monotonic."""
+        self._c(lib().psim_plumtree_restart_backend(self._h, v))
+
     def delivered_at(self, v, mono=0):
         """Mod:is_stale at ONE local vertex (psim_get_delivered_range): mono 0 =
         the focused root's newest heartbeat.  No copy of the whole set."""

@@ -861,3 +861,173 @@ def test_worklist_overflow_and_forced_list_mode(psim, monkeypatch, cap, thr):
             assert m == orc.heartbeat(root)
             lockstep(sim, orc, root, m)
         sim.close()
+
+
+def _win_compare_ids(sim, orc, root, ids):
+    """_win_compare with heartbeat ids in psim's packed form (epoch << 24 |
+    Monotonic): a restarted origin's heartbeats of two epochs in flight."""
+    for m in ids:
+        assert np.array_equal(sim.delivered_mono(m), orc.delivered(root, m)), hex(m)
+    eager, lazy, _, rr = sim.plumtree_state()
+    orr = orc.recv_round(root, ids[-1])
+    for v in range(sim.n):
+        oe, ol = orc.peers(v, root)
+        assert sim.mask_to_peers(v, eager[v]) == oe, f"eager set of {v}"
+        assert sim.mask_to_peers(v, lazy[v]) == ol, f"lazy set of {v}"
+        assert sim.rows(v) == orc.outstanding(v), f"rows of {v}"
+        want = 0xFFFF if orr[v] == 0xFFFFFFFF else (0xFFFE if orr[v] == 0xFFFFFFFE else orr[v])
+        assert rr[v] == want, v
+    assert sim.messages() == orc.pending_full(packed=True), "in-flight messages differ"
+
+
+def test_backend_restart_quiescent_lockstep(psim):
+    """backend init/1 (:316-329) after a crash: a vertex's table forgets every
+    origin, so the heartbeat it had delivered is no longer stale there (a
+    later copy would be delivered again); the root's next heartbeat carries
+    the newer epoch, {Root, 1, 1} = 1 << 24 | 1, and floods the pruned tree
+    like any other -- lockstep with the oracle."""
+    n = 400
+    rp, col = psim.overlay.random_regular(n, 5, 77)
+    sim, orc = make(psim, rp, col, 1)
+    root, u = 7, 123
+    m0 = sim.broadcast(root)
+    assert m0 == orc.heartbeat(root) == 1
+    lockstep(sim, orc, root, m0)
+    if psim.engine == "binned":
+        with pytest.raises(psim.PsimError):
+            sim.restart_backend(u)          # the binned engine keeps one epoch per root
+        return
+    for v in (u, root):
+        sim.restart_backend(v)
+        orc.restart_backend(v)
+    d = sim.delivered_mono(m0)
+    assert np.array_equal(d, orc.delivered(root, m0))
+    assert not d[u] and not d[root] and d.sum() == n - 2
+    m1 = sim.broadcast(root)
+    assert m1 == orc.heartbeat(root) == (1 << 24) | 1
+    compare(sim, orc, root, m1)
+    lockstep(sim, orc, root, m1)
+    assert sim.delivered().all()
+    m2 = sim.broadcast(root)                # the epoch's Monotonic counts on
+    assert m2 == orc.heartbeat(root) == (1 << 24) | 2
+    lockstep(sim, orc, root, m2)
+
+
+def test_backend_restart_in_flight_lockstep(psim):
+    """Restarts while a heartbeat floods: three vertices that delivered it
+    forget it (each delivers the next copy again and holds a second row set
+    for it -- the lane keeps every row: a window lane), then the root itself
+    restarts and heartbeats at once, so heartbeats of two epochs are in
+    flight together; a vertex holding the newer epoch treats the older one
+    as stale (is_stale :237-238: Epoch0 > Epoch) and prunes its sender.
+    Round by round against the oracle: deliveries per id, rows, messages."""
+    if psim.engine == "binned":
+        return                              # covered by the quiescent test's EBUSY/ESTATE check
+    n = 600
+    rp, col = psim.overlay.random_regular(n, 5, 78)
+    sim, orc = make(psim, rp, col, 1)
+    root = 31
+    m0 = sim.broadcast(root)
+    assert m0 == orc.heartbeat(root)
+    ids = [m0]
+    for _ in range(3):
+        lockstep_one(sim, orc, root, m0)
+    got = np.flatnonzero(sim.delivered())
+    forget = [int(v) for v in got if v != root][:3]
+    assert len(forget) == 3
+    for v in forget:
+        sim.restart_backend(v)
+        orc.restart_backend(v)
+    _win_compare_ids(sim, orc, root, ids)
+    for _ in range(2):
+        _win_step_ids(sim, orc, root, ids)
+    sim.restart_backend(root)
+    orc.restart_backend(root)
+    m1 = sim.broadcast(root)
+    assert m1 == orc.heartbeat(root) == (1 << 24) | 1
+    ids.append(m1)
+    _win_compare_ids(sim, orc, root, ids)
+    for _ in range(200):
+        gs, os_ = _win_step_ids(sim, orc, root, ids)
+        if sum(gs[k] for k in KINDS) == 0 and os_["outstanding_live"] == 0:
+            break
+    else:
+        raise AssertionError("no quiescence")
+    assert sim.delivered_mono(m1).all()
+    assert sim.delivered_mono(m0).all()     # stale everywhere: delivered, or the newer epoch is held
+
+
+def lockstep_one(sim, orc, root, mono):
+    gs, os_ = sim.step(1)[0], orc.step(1)[0]
+    for k in KINDS:
+        assert gs[k] == os_[k], (k, gs, os_)
+    compare(sim, orc, root, mono)
+
+
+def _win_step_ids(sim, orc, root, ids):
+    gs, os_ = sim.step(1)[0], orc.step(1)[0]
+    for k in KINDS:
+        assert gs[k] == os_[k], (k, gs, os_)
+    assert gs["delivered_new"] == os_["delivered_new"]
+    _win_compare_ids(sim, orc, root, ids)
+    return gs, os_
+
+
+def _expect_graft(orc, root, v, mid):
+    """backend graft/1 (:254-280) from the oracle's is_stale views: the id
+    itself in v's row -> ok; a newer epoch in v's row -> stale."""
+    pid = (mid[1] << 24) | mid[2]
+    if not orc.delivered(root, pid)[v]:
+        return ("error", ("not_found", mid))
+    if orc.delivered(root, (mid[1] << 24) | 0xFFFFFF)[v]:
+        return "stale"
+    return ("ok", mid)
+
+
+@pytest.mark.parametrize("in_flight", [False, True])
+def test_facade_backend_restart_epochs(in_flight):
+    """PlumtreeBackend.is_stale/graft with {Node, Epoch, Monotonic} ids across
+    backend restarts, for every vertex and every id, against the oracle's
+    table rows: quiescent heartbeats (static lanes: earlier ids from the
+    recorded sets) and, with in_flight, a restart and a new-epoch heartbeat
+    while the old one floods (a window lane answers on device)."""
+    import partisan_amd as P
+    n = 300
+    rp, col = P.overlay.random_regular(n, 5, 91)
+    pb = P.PlumtreeBroadcast(rp, col)
+    orc = O.Plumtree(rp, col)
+    root, u = 5, 77
+
+    def advance():
+        if in_flight:
+            pb.step(2)
+            orc.step(2)
+        else:
+            pb.run()
+            orc.run(100000)
+
+    id0 = pb.broadcast(root)
+    assert id0 == (root, 0, 1) and orc.heartbeat(root) == 1
+    advance()
+    id0b = pb.broadcast(root)
+    assert id0b == (root, 0, 2) and orc.heartbeat(root) == 2
+    advance()
+    for v in (u, root):
+        pb.restart_backend(v)
+        orc.restart_backend(v)
+    advance()
+    id1 = pb.broadcast(root)
+    assert id1 == (root, 1, 1) and orc.heartbeat(root) == (1 << 24) | 1
+    advance()
+    pb.run()
+    orc.run(100000)
+    for mid in (id0, id0b, id1):
+        want = orc.delivered(root, (mid[1] << 24) | mid[2])
+        for v in range(n):
+            h = pb.handler(v)
+            assert h.is_stale(mid) == bool(want[v]), (mid, v)
+            assert h.merge(mid, mid) == (not want[v])
+        for v in (u, root, 0, 1, n - 1):
+            assert pb.handler(v).graft(mid) == _expect_graft(orc, root, v, mid), (mid, v)
+    assert pb.handler(3).graft(id0) == "stale"          # the row holds epoch 1 now
+    assert pb.handler(3).graft(id1) == ("ok", id1)
