@@ -653,6 +653,10 @@ int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, cons
 
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
+/* Totals since creation of the frontier kernel: rounds it ran
+ * (one workgroup running a chunk's leading sparse rounds back to back) and the
+ * chunks it was launched for.  Diagnostic; no reference counterpart. */
+int  psim_get_frontier(const psim_handle* h, uint64_t* rounds, uint64_t* launches);
 /* Switch PSIM_CFG_CHUNK_TIMING on (chunk != 0) or off after creation: one event
  * pair per chunk (round kernels back to back; on a sharded handle the chunk's
  * time includes its exchanges) or a pair per round kernel (kernel-only times,

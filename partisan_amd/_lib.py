@@ -188,6 +188,7 @@ SIGNATURES = {
     "psim_get_delivered_mono": (C.c_int, [_H, C.c_uint32, _P(C.c_uint8), C.c_size_t]),
     "psim_get_delivered_range": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_size_t, _P(C.c_uint8)]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
+    "psim_get_frontier": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint64)]),
     "psim_set_chunk_timing": (C.c_int, [_H, C.c_int]),
     "psim_shard_init": (C.c_int, [_H, C.c_int, C.c_int]),
     "psim_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),

@@ -248,6 +248,13 @@ class Simulator:
         self._c(lib().psim_get_timing(self._h, C.byref(ms), C.byref(r)))
         return ms.value, r.value
 
+    def frontier_stats(self):
+        """psim_get_frontier: (rounds run by the frontier kernel, chunks it was launched for)."""
+        r = C.c_uint64()
+        k = C.c_uint64()
+        self._c(lib().psim_get_frontier(self._h, C.byref(r), C.byref(k)))
+        return r.value, k.value
+
     # ---------------------------------------------------------------- helpers
     def mask_to_peers(self, v, mask):
         """Decode a per-vertex slot mask into the sorted list of peer ids."""

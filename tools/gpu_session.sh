@@ -28,6 +28,9 @@ for s in $STEPS; do
         t:*)   f=${s#t:}; run "pytest_${f}" 900 python -m pytest "tests/test_${f}.py" -m gpu -x -q ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        benchq) run benchq 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+        rprof) run round_profile 300 python tools/round_profile.py --steps 3 ;;
+        frprof) PSIM_FRONTIER=1 PSIM_FR_PROFILE=1 run fr_profile 300 python tools/round_profile.py --steps 2 ;;
         prof)
             export TMPDIR=/tmp
             run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
