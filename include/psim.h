@@ -384,21 +384,27 @@ int  psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m);
  * Shard `rank` owns global ids [rank C, min((rank+1) C, n)), C = ceil(n/world)
  * (*chunk_out).  Rounds are split-phase; the transport is the caller's
  * (RCCL via torch.distributed "nccl" on a node, gloo in tests).  Caller-owned
- * device buffers, u64 words:  rm_shadow [3][world C] and pull_shadow
- * [world C][2] (zeroed by the caller before each round), snap_all [world C],
- * rm_recv [3][world C] (plane k = the world slices of plane k sent to this
- * shard, slice g from shard g), pull_recv [C][2].  After psim_demers_shard_round
- * the caller does, per plane, all_to_all(rm_shadow -> rm_recv) in slices of C,
- * reduce_scatter(sum, pull_shadow -> pull_recv) (one writer per slot), and
- * when *tick: all_gather(snap_all) in slices of C; then psim_demers_shard_ingest.
- * Same workload, draws and results as psim_demers_* on one GPU. */
+ * device buffers:  rm_shadow [3][world C] u64 and pull_shadow [world C][2]
+ * u64 (zeroed by the caller before each round), snap_all [world C] u64,
+ * rmx_all = [world C] u64 then [world C] u32 (each RM process's calls of the
+ * round and its calls before it: a receiver checks whether its own targets
+ * sent it a rumor from them), rm_recv [3][world C] u64 (plane k = the world
+ * slices of plane k sent to this shard, slice g from shard g), pull_recv
+ * [C][2] u64.  After psim_demers_shard_broadcast_all and after each
+ * psim_demers_shard_round the caller does, per plane, all_to_all(rm_shadow ->
+ * rm_recv) in slices of C, reduce_scatter(sum, pull_shadow -> pull_recv) (one
+ * writer per slot), all_gather of both rmx_all planes in slices of C, and
+ * when *tick: all_gather(snap_all) in slices of C; then
+ * psim_demers_shard_ingest.  Same workload, draws and results as
+ * psim_demers_* on one GPU. */
 int  psim_demers_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on, int rank,
                              int world, uint64_t* chunk_out);
 int  psim_demers_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local, uint64_t* chunk);
-int  psim_demers_shard_broadcast_all(psim_handle* h, void* rm_shadow);
-int  psim_demers_shard_round(psim_handle* h, void* rm_shadow, void* pull_shadow, void* snap_all,
+int  psim_demers_shard_broadcast_all(psim_handle* h, void* rm_shadow, void* rmx_all);
+int  psim_demers_shard_round(psim_handle* h, void* rm_shadow, void* pull_shadow, void* snap_all, void* rmx_all,
                              psim_demers_stats* stats, uint32_t* tick);
-int  psim_demers_shard_ingest(psim_handle* h, const void* rm_recv, const void* pull_recv, uint32_t tick);
+int  psim_demers_shard_ingest(psim_handle* h, const void* rm_recv, const void* pull_recv, const void* rmx_all,
+                              uint32_t tick);
 int  psim_demers_shard_get_seen(const psim_handle* h, uint64_t* seen, size_t n_local);
 
 /* --- HyParView view maintenance (partisan_hyparview_peer_service_manager.erl) */

@@ -10,9 +10,19 @@
  * Simulation contract (DESIGN.md "Demers"):
  *  - full membership: members = all vertices incl. self (membership/1 =
  *    lists:usort(Members), :177-178) -- implicit ids 0..N-1;
- *  - select_random_sublist(Members, 2) = the first two of shuffle/1, i.e. a
- *    uniformly random ordered pair of distinct members; drawn from Philox
- *    stream (seed, vertex, event, kind): RM event = rumor id, AE event = tick;
+ *  - each process has its own sequential draw stream, as Erlang's per-process
+ *    `rand` state (partisan_config.erl:701-716 seeds each process): Philox
+ *    stream (seed, vertex, kind) -- kind RM for demers_rumor_mongering, AE for
+ *    demers_anti_entropy -- whose j-th draw is the u64 {x, y} of Philox
+ *    counter {vertex, j_lo, kind, j_hi}; the process's counter advances by the
+ *    draws each call consumes, in the order the process makes its calls;
+ *  - select_random_sublist(usort(Members), 2) (:179-186, :222-227) =
+ *    lists:sublist(shuffle(L), 2), shuffle/1 = sort of {rand:uniform(), N}:
+ *    FAITHFUL mode (n <= DM_FAITHFUL_MAX): one draw per member in list order,
+ *    the two smallest (draw >> 11, member) -- rand:uniform()'s 53-bit float and
+ *    the tuple order; n draws per call.  SCALED mode (larger n): the same
+ *    distribution -- a uniform ordered pair of distinct members -- from 2
+ *    draws, i1 = floor(d0 n / 2^64), i2 = floor(d1 (n-1) / 2^64) (+1 if >= i1);
  *  - rumor m originates at origin(m) = uniform draw of the workload stream;
  *  - the two processes share one message store (Demers et al.'s rumor
  *    mongering backed by anti-entropy; run alone, each is the reference
@@ -45,23 +55,43 @@ void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint3
 
 static uint64_t mulhi64(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
 
-/* select_random_sublist(usort(Members), 2) over members 0..n-1 */
-static int sample2(uint64_t seed, uint32_t v, uint32_t event, uint32_t kind, uint32_t n, uint32_t out[2]) {
-    uint32_t ctr[4] = {v, event, kind, 0}, key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, r[4];
+/* draw j of process (v, kind)'s stream */
+static uint64_t draw64(uint64_t seed, uint32_t v, uint32_t kind, uint64_t j) {
+    uint32_t ctr[4] = {v, (uint32_t)j, kind, (uint32_t)(j >> 32)}, key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, r[4];
     orc_philox4x32_10(ctr, key, r);
-    uint64_t r0 = (uint64_t)r[0] | ((uint64_t)r[1] << 32), r1 = (uint64_t)r[2] | ((uint64_t)r[3] << 32);
-    if (n == 0) return 0;
-    out[0] = (uint32_t)mulhi64(r0, n);
-    if (n == 1) return 1;
-    uint32_t i2 = (uint32_t)mulhi64(r1, n - 1);
+    return (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+}
+
+/* draws one select_random_sublist(usort(Members), 2) call consumes over n members */
+static uint64_t dm_draws_per_call(uint32_t n) { return n <= DM_FAITHFUL_MAX ? n : 2; }
+
+/* select_random_sublist(usort(Members), 2) over members 0..n-1 (n >= 2), the
+ * call whose first draw is draw j of process (v, kind) */
+static void select2(uint64_t seed, uint32_t v, uint32_t kind, uint32_t n, uint64_t j, uint32_t out[2]) {
+    if (n <= DM_FAITHFUL_MAX) {                      /* lists:sort([{rand:uniform(), N} || N <- L]) */
+        uint64_t k0 = ~0ull, k1 = ~0ull;
+        uint32_t i0 = 0, i1 = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t k = draw64(seed, v, kind, j + i) >> 11;
+            if (k < k0) { k1 = k0; i1 = i0; k0 = k; i0 = i; }
+            else if (k < k1) { k1 = k; i1 = i; }
+        }
+        out[0] = i0; out[1] = i1;
+        return;
+    }
+    out[0] = (uint32_t)mulhi64(draw64(seed, v, kind, j), n);
+    uint32_t i2 = (uint32_t)mulhi64(draw64(seed, v, kind, j + 1), n - 1);
     if (i2 >= out[0]) i2++;
     out[1] = i2;
+}
+
+int orc_dm_select2(uint64_t seed, uint32_t v, uint32_t kind, uint32_t n, uint64_t j, uint32_t* out) {
+    if (n < 2) return 0;
+    select2(seed, v, kind, n, j, out);
     return 2;
 }
 
-int orc_dm_sample2(uint64_t seed, uint32_t v, uint32_t event, uint32_t kind, uint32_t n, uint32_t* out) {
-    return sample2(seed, v, event, kind, n, out);
-}
+uint64_t orc_dm_draws_per_call(uint32_t n) { return dm_draws_per_call(n); }
 
 enum { DM_RM = 1, DM_PUSH = 2, DM_PULL = 3 };
 enum { KIND_WORKLOAD = 1, KIND_RM = 2, KIND_AE = 3 };
@@ -73,6 +103,10 @@ struct orc_demers {
     uint64_t seed, round;
     uint64_t* seen;              /* ETS ?MODULE of each process (shared store) */
     uint64_t* emitted;           /* per-vertex emission counter (FIFO seq)     */
+    uint64_t* rmdraw;            /* draws taken by each vertex's RM process     */
+    uint64_t* aedraw;            /* draws taken by each vertex's AE process     */
+    uint64_t* newrm;             /* scratch: rumors new at v among this round's RM messages */
+    uint64_t dpc;                /* draws per select_random_sublist call        */
     uint32_t* origin;            /* origin of rumor m                           */
     uint32_t* idbit;             /* store bit of rumor m (Q20 in ae-only mode)  */
     uint64_t full;
@@ -99,6 +133,10 @@ orc_demers* orc_dm_create(uint32_t n, uint32_t m, uint64_t seed, uint32_t ae_per
     s->n = n; s->m = m; s->seed = seed; s->ae_period = ae_period; s->rm_on = rm_on;
     s->seen = (uint64_t*)calloc(n, 8);
     s->emitted = (uint64_t*)calloc(n, 8);
+    s->rmdraw = (uint64_t*)calloc(n, 8);
+    s->aedraw = (uint64_t*)calloc(n, 8);
+    s->newrm = (uint64_t*)calloc(n, 8);
+    s->dpc = dm_draws_per_call(n);
     s->origin = (uint32_t*)calloc(m, 4);
     s->idbit = (uint32_t*)calloc(m, 4);
     for (uint32_t i = 0; i < m; i++) {
@@ -115,7 +153,7 @@ orc_demers* orc_dm_create(uint32_t n, uint32_t m, uint64_t seed, uint32_t ae_per
 
 void orc_dm_destroy(orc_demers* s) {
     if (!s) return;
-    free(s->seen); free(s->emitted); free(s->origin); free(s->idbit); free(s->cur); free(s->nxt);
+    free(s->seen); free(s->emitted); free(s->rmdraw); free(s->aedraw); free(s->newrm); free(s->origin); free(s->idbit); free(s->cur); free(s->nxt);
     free(s);
 }
 
@@ -137,8 +175,9 @@ void orc_dm_broadcast_all(orc_demers* s) {
             continue;
         }
         uint32_t t[2];
-        int k = sample2(s->seed, o, i, KIND_RM, s->n, t);
-        for (int j = 0; j < k; j++) if (t[j] != o) emit(s, DM_RM, o, t[j], i, 0);
+        select2(s->seed, o, KIND_RM, s->n, s->rmdraw[o], t);   /* the origin's RM process calls once per rumor */
+        s->rmdraw[o] += s->dpc;
+        for (int j = 0; j < 2; j++) if (t[j] != o) emit(s, DM_RM, o, t[j], i, 0);
     }
 }
 
@@ -161,15 +200,24 @@ static void one_round(orc_demers* s, orc_dm_stats* st) {
     dmsg* t = s->cur; size_t tc = s->capcur;
     s->cur = s->nxt; s->ncur = s->nnxt; s->capcur = s->capnxt;
     s->nxt = t; s->nnxt = 0; s->capnxt = tc;
-    /* class of an RM message: is the sender one of the receiver's own targets */
+    /* class of an RM message: is the sender one of the receiver's own targets
+     * for the rumor, i.e. of the call the receiver's RM process makes when it
+     * accepts it -- its (rank + 1)-th call this round, rank = the new rumors
+     * with smaller ids (RM messages are handled by rumor first) */
+    for (size_t i = 0; i < s->ncur; i++) {
+        const dmsg* x = &s->cur[i];
+        if (x->type == DM_RM && !(s->seen[x->dst] & (1ull << s->idbit[x->m]))) s->newrm[x->dst] |= 1ull << x->m;
+    }
     for (size_t i = 0; i < s->ncur; i++) {
         dmsg* x = &s->cur[i];
-        if (x->type != DM_RM || s->rm_on == 2) continue;
-        uint32_t tg[2];
-        int k = sample2(s->seed, x->dst, x->m, KIND_RM, s->n, tg);
         x->cls = 0;
-        for (int j = 0; j < k; j++) if (tg[j] == x->src) x->cls = 1;
+        if (x->type != DM_RM || s->rm_on == 2 || !((s->newrm[x->dst] >> x->m) & 1ull)) continue;
+        const uint64_t below = s->newrm[x->dst] & ((1ull << x->m) - 1ull);
+        uint32_t tg[2];
+        select2(s->seed, x->dst, KIND_RM, s->n, s->rmdraw[x->dst] + s->dpc * (uint64_t)__builtin_popcountll(below), tg);
+        for (int j = 0; j < 2; j++) if (tg[j] == x->src) x->cls = 1;
     }
+    for (size_t i = 0; i < s->ncur; i++) s->newrm[s->cur[i].dst] = 0;
     qsort(s->cur, s->ncur, sizeof(dmsg), cmp_msg);
     for (size_t i = 0; i < s->ncur; i++) {
         const dmsg* x = &s->cur[i];
@@ -181,8 +229,9 @@ static void one_round(orc_demers* s, orc_dm_stats* st) {
             st->delivered_new++;
             if (s->rm_on == 2) continue;             /* direct mail :127-143: store only */
             uint32_t tg[2];
-            int k = sample2(s->seed, v, x->m, KIND_RM, s->n, tg);
-            for (int j = 0; j < k; j++)              /* AntiEntropyMembers -- [MyNode, FromNode] */
+            select2(s->seed, v, KIND_RM, s->n, s->rmdraw[v], tg);
+            s->rmdraw[v] += s->dpc;
+            for (int j = 0; j < 2; j++)              /* AntiEntropyMembers -- [MyNode, FromNode] */
                 if (tg[j] != v && tg[j] != x->src) emit(s, DM_RM, v, tg[j], x->m, 0);
         } else if (x->type == DM_PUSH) {             /* handle_info({push, FromNode, TheirMessages}) :143-176 */
             uint64_t nw = x->payload & ~s->seen[v];
@@ -197,11 +246,11 @@ static void one_round(orc_demers* s, orc_dm_stats* st) {
     }
     s->round++;
     if (s->ae_period && s->round % s->ae_period == 0) {   /* handle_info(antientropy) :118-141 */
-        uint32_t tick = (uint32_t)(s->round / s->ae_period);
         for (uint32_t v = 0; v < s->n; v++) {
             uint32_t tg[2];
-            int k = sample2(s->seed, v, tick, KIND_AE, s->n, tg);
-            for (int j = 0; j < k; j++) if (tg[j] != v) emit(s, DM_PUSH, v, tg[j], 0, s->seen[v]);
+            select2(s->seed, v, KIND_AE, s->n, s->aedraw[v], tg);   /* one call per tick: (tick - 1) dpc draws before */
+            s->aedraw[v] += s->dpc;
+            for (int j = 0; j < 2; j++) if (tg[j] != v) emit(s, DM_PUSH, v, tg[j], 0, s->seen[v]);
         }
     }
     uint64_t done = 0;

@@ -177,7 +177,12 @@ int orc_pt_inflight_words(const orc_plumtree* s, const uint64_t* row_ptr, const 
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* select_random_sublist(usort(Members), 2) over members 0..n-1 for the
  * Philox stream (seed, v, event, kind); returns the number of draws (<= 2) */
-int orc_dm_sample2(uint64_t seed, uint32_t v, uint32_t event, uint32_t kind, uint32_t n, uint32_t* out);
+/* Demers select_random_sublist(usort(Members), 2): faithful (one draw per
+ * member) up to DM_FAITHFUL_MAX members, scaled (2 draws) above; `j` = the
+ * process's draw index at the call (demers.c) */
+#define DM_FAITHFUL_MAX 1024
+int orc_dm_select2(uint64_t seed, uint32_t v, uint32_t kind, uint32_t n, uint64_t j, uint32_t* out);
+uint64_t orc_dm_draws_per_call(uint32_t n);
 
 /* ------------------------------------------------------------------ */
 /* Demers rumor mongering + anti-entropy (protocols/demers_*.erl)       */

@@ -173,7 +173,9 @@ def lib():
                                     P(C.c_uint64), P(C.c_uint32), P(RelayRound), sz, sz]
         L.orc_relay_run.restype = C.c_int64
         L.orc_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
-        L.orc_dm_sample2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.orc_dm_select2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, P(C.c_uint32)]
+        L.orc_dm_draws_per_call.argtypes = [C.c_uint32]
+        L.orc_dm_draws_per_call.restype = C.c_uint64
         L.orc_dm_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
         L.orc_dm_create.restype = C.c_void_p
         L.orc_dm_destroy.argtypes = [C.c_void_p]
@@ -625,10 +627,17 @@ def philox(ctr, key):
     return list(o)
 
 
-def sample2(seed, v, event, kind, n):
+def select2(seed, v, kind, n, j):
+    """Demers select_random_sublist(usort(Members), 2) over 0..n-1 for the call
+    whose first draw is draw j of process (v, kind) (oracle/demers.c)."""
     o = (C.c_uint32 * 2)()
-    k = lib().orc_dm_sample2(seed, v, event, kind, n, o)
+    k = lib().orc_dm_select2(seed, v, kind, n, j, o)
     return list(o[:k])
+
+
+def draws_per_call(n):
+    """Draws one select_random_sublist call consumes: n (faithful) or 2 (scaled)."""
+    return int(lib().orc_dm_draws_per_call(n))
 
 
 class Demers:

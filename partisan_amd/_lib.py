@@ -219,9 +219,10 @@ SIGNATURES = {
     "psim_demers_shard_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
                                           _P(C.c_uint64)]),
     "psim_demers_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint64)]),
-    "psim_demers_shard_broadcast_all": (C.c_int, [_H, C.c_void_p]),
-    "psim_demers_shard_round": (C.c_int, [_H, C.c_void_p, C.c_void_p, C.c_void_p, _P(DemersStats), _P(C.c_uint32)]),
-    "psim_demers_shard_ingest": (C.c_int, [_H, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "psim_demers_shard_broadcast_all": (C.c_int, [_H, C.c_void_p, C.c_void_p]),
+    "psim_demers_shard_round": (C.c_int, [_H, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, _P(DemersStats),
+                                          _P(C.c_uint32)]),
+    "psim_demers_shard_ingest": (C.c_int, [_H, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "psim_demers_shard_get_seen": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_hv_setup": (C.c_int, [_H, C.c_uint32, _P(HvConfig)]),
     "psim_hv_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),

@@ -1,23 +1,28 @@
 // demers.hip -- Demers rumor mongering + anti-entropy
 // (protocols/demers_rumor_mongering.erl :92-186, protocols/demers_anti_entropy.erl
 // :95-227) as one gfx950 kernel per round; the store of each vertex is a
-// 64-bit seen-set (one bit per rumor id).
+// 64-bit seen-set (one bit per rumor id).  Host side: demers_host.hip.
 //
-// Round formulation (DESIGN.md "Demers"), one thread per vertex:
-//  * RM inbox = three 64-bit sets per vertex, written by senders with atomicOr:
-//    `reg` (sender is not one of the receiver's own forward targets for the
-//    rumor), `t0`/`t1` (sender is the receiver's first/second target).  The
-//    schedule processes RM messages by (rumor, class, sender), so for a new
-//    rumor the FromNode excluded by `-- [MyNode, FromNode]` is a regular
-//    sender (never a target: no effect) unless only targets sent it, in
-//    which case it is the smaller of them -- computable from the three sets
-//    alone.  Forward draws are the Philox stream (v, rumor, RM), so every
-//    vertex can recompute any other vertex's targets: no sorting needed.
+// Round formulation, one thread per vertex:
+//  * every process draws from its own sequential Philox stream (philox.h
+//    draw64 / select2): a vertex's RM process calls select_random_sublist once
+//    per rumor it accepts (and once per rumor it originates), in the order it
+//    handles them; its AE process once per tick;
+//  * RM inbox = three 64-bit planes per vertex -- rumors received this round
+//    from >= 1, >= 2, >= 3 senders -- raised by the senders with atomicOr
+//    cascades.  The schedule handles RM messages by (rumor, class, sender),
+//    class 0 = senders that are not among the receiver's own two targets for
+//    the rumor, so the FromNode that `-- [MyNode, FromNode]` drops is a
+//    non-target (no effect) whenever the senders outnumber the targets that
+//    sent it, else the smallest target that sent it.  Whether target T sent it:
+//    T called select for the rumor last round (rmnew_prev) and drew the
+//    receiver -- recomputed from T's call count (ncall_prev) and T's stream;
 //  * AE pushes: the sender appends its id to the receiver's list (atomicAdd
 //    slot); the receiver sorts its list (schedule: by sender), merges each
 //    pusher's snapshot and answers with its prefix union into the pusher's
-//    pull slot k (k = the receiver's index in the pusher's target pair).
-//  * AE tick (end of the round): snapshot + push to sample2(v, tick, AE) -- [v].
+//    pull slot k (k = the receiver's index in the pusher's target pair: the
+//    pusher's tick-th AE call, a pure function of (pusher, tick));
+//  * AE tick (end of the round): snapshot + push to the tick's select -- [v].
 #include "psim_internal.h"
 #include "philox.h"
 #include "../../include/psim.h"
@@ -62,13 +67,25 @@ __device__ __forceinline__ void dm_flush(const DmCtr& c, unsigned long long* __r
     }
 }
 
-// send RM(m) from v to t: the class is decided by t's own targets for m
-__device__ __forceinline__ void rm_send(const DmArgs& a, uint32_t v, uint32_t t, uint32_t m, DmCtr& c) {
-    const uint2 tp = sample2(a.key, t, m, KIND_RM, a.n_global);
+// send RM(m) to t: raise the first count plane of t's rumor-m bit that was clear
+// (>= 1, >= 2, >= 3 senders); the planes saturate at 3
+__device__ __forceinline__ void rm_send(const DmArgs& a, uint32_t t, uint32_t m, DmCtr& c) {
     const unsigned long long b = 1ull << m;
-    unsigned long long* dst = v == tp.x ? a.rm_nxt_t0 : (v == tp.y ? a.rm_nxt_t1 : a.rm_nxt_reg);
-    atomicOr(&dst[t], b);
+    if (atomicOr(&a.rm_nxt_any[t], b) & b)
+        if (atomicOr(&a.rm_nxt_multi[t], b) & b) atomicOr(&a.rm_nxt_tri[t], b);
     c.rm++;
+}
+
+// Did target T send rumor m to v last round?  T called select_random_sublist
+// for m last round (its call index: the calls before that round plus its
+// earlier rumors of that round, handled in rumor order) and drew v.  The
+// FromNode T excluded cannot be v: v did not hold m.
+__device__ __forceinline__ bool rm_sent_by(const DmArgs& a, uint32_t T, uint32_t v, uint32_t m) {
+    const unsigned long long rn = a.rmnew_prev[T];
+    if (T == v || !((rn >> m) & 1ull)) return false;
+    const uint64_t calls = a.ncall_prev[T] + (uint32_t)__popcll(rn & ((1ull << m) - 1ull));
+    const uint2 u = select2(a.key, T, KIND_RM, a.n_global, a.dpc * calls);
+    return u.x == v || u.y == v;
 }
 
 __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
@@ -84,33 +101,42 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
 
         // ---- rumor mongering: handle_info({broadcast, Id, ..., FromNode}) :127-158
         if (a.rm_on) {
-#ifndef DM_TEMPORAL_INBOX   // the inbox sets are read once (then cleared): non-temporal, ~1-3 % per C4 round
-            const unsigned long long reg = __builtin_nontemporal_load(a.rm_cur_reg + i),
-                                     t0 = __builtin_nontemporal_load(a.rm_cur_t0 + i),
-                                     t1 = __builtin_nontemporal_load(a.rm_cur_t1 + i);
+            const unsigned long long rn_prev = a.rmnew_prev[v];
+            const uint32_t calls0 = a.ncall_prev[v] + (uint32_t)__popcll(rn_prev);   // calls before this round
+            unsigned long long rn = 0;
+#ifndef DM_TEMPORAL_INBOX   // the inbox planes are read once (then cleared): non-temporal, ~1-3 % per C4 round
+            const unsigned long long any = __builtin_nontemporal_load(a.rm_cur_any + i);
 #else
-            const unsigned long long reg = a.rm_cur_reg[i], t0 = a.rm_cur_t0[i], t1 = a.rm_cur_t1[i];
+            const unsigned long long any = a.rm_cur_any[i];
 #endif
-            if (reg | t0 | t1) {
-                if (reg) a.rm_cur_reg[i] = 0;
-                if (t0) a.rm_cur_t0[i] = 0;
-                if (t1) a.rm_cur_t1[i] = 0;
-                unsigned long long nw = (reg | t0 | t1) & ~s;
+            if (any) {
+                const unsigned long long multi = a.rm_cur_multi[i], tri = a.rm_cur_tri[i];
+                a.rm_cur_any[i] = 0;
+                if (multi) a.rm_cur_multi[i] = 0;
+                if (tri) a.rm_cur_tri[i] = 0;
+                unsigned long long nw = any & ~s;
                 while (nw) {
                     const uint32_t m = __ffsll(nw) - 1;
                     nw &= nw - 1;
                     s |= 1ull << m;                                  // deliver + ets:insert
-                    const uint2 tp = sample2(a.key, v, m, KIND_RM, a.n_global);
-                    uint32_t from = 0xFFFFFFFFu;                     // a regular sender: not a target
-                    if (!((reg >> m) & 1ull)) {
-                        const bool f0 = (t0 >> m) & 1ull, f1 = (t1 >> m) & 1ull;
-                        if (f0 && f1) from = tp.x < tp.y ? tp.x : tp.y;
-                        else from = f0 ? tp.x : tp.y;
+                    const uint2 tp = select2(a.key, v, KIND_RM, a.n_global,
+                                             a.dpc * (calls0 + (uint32_t)__popcll(rn)));
+                    rn |= 1ull << m;
+                    // FromNode: a non-target sender comes first in the schedule; only when every
+                    // sender is one of the two targets is it the smaller target that sent
+                    uint32_t from = 0xFFFFFFFFu;
+                    const uint32_t senders = 1u + (uint32_t)((multi >> m) & 1ull) + (uint32_t)((tri >> m) & 1ull);
+                    if (senders <= 2) {
+                        const bool s0 = rm_sent_by(a, tp.x, v, m), s1 = rm_sent_by(a, tp.y, v, m);
+                        if (senders == (s0 ? 1u : 0u) + (s1 ? 1u : 0u))
+                            from = s0 && s1 ? min(tp.x, tp.y) : (s0 ? tp.x : tp.y);
                     }
-                    if (tp.x != v && tp.x != from) rm_send(a, v, tp.x, m, c);
-                    if (a.n_global > 1 && tp.y != v && tp.y != from) rm_send(a, v, tp.y, m, c);
+                    if (tp.x != v && tp.x != from) rm_send(a, tp.x, m, c);
+                    if (tp.y != v && tp.y != from) rm_send(a, tp.y, m, c);
                 }
             }
+            a.rmnew_cur[v] = rn;            // every vertex, every round: the next round's rmnew_prev
+            a.ncall_cur[v] = calls0;
         }
 
         // ---- anti-entropy push: handle_info({push, FromNode, TheirMessages}) :143-176
@@ -144,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
                 for (uint32_t j = 0; j < kDmFastPush; j++) {
                     if (j >= cnt) break;
                     s |= P[j];
-                    const uint2 sp = sample2(a.key, x[j], a.prev_tick, KIND_AE, a.n_global);
+                    const uint2 sp = select2(a.key, x[j], KIND_AE, a.n_global, a.dpc * (a.prev_tick - 1u));
                     a.pull_nxt[2 * (size_t)x[j] + (sp.x == v ? 0u : 1u)] = s;   // {pull, MyNode, OurMessages}
                     c.pull++;
                 }
@@ -163,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
                 last = best;
                 const unsigned long long P = a.snap[best];
                 s |= P;
-                const uint2 sp = sample2(a.key, best, a.prev_tick, KIND_AE, a.n_global);
+                const uint2 sp = select2(a.key, best, KIND_AE, a.n_global, a.dpc * (a.prev_tick - 1u));
                 const uint32_t slot = sp.x == v ? 0u : 1u;
                 a.pull_nxt[2 * (size_t)best + slot] = s;             // {pull, MyNode, OurMessages}
                 c.pull++;
@@ -192,12 +218,12 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
         // ---- anti-entropy tick: handle_info(antientropy) :118-141
         if (a.tick) {
             a.snap[v] = s;
-            const uint2 tp = sample2(a.key, v, a.tick_idx, KIND_AE, a.n_global);
+            const uint2 tp = select2(a.key, v, KIND_AE, a.n_global, a.dpc * (a.tick_idx - 1u));   // the tick-th call
             const uint32_t tg[2] = {tp.x, tp.y};
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const uint32_t t = tg[j];
-                if (t == v || (j == 1 && a.n_global < 2)) continue;
+                if (t == v) continue;
                 c.push++;
                 if (a.sharded) continue;                            // listed by dm_pushscan_kernel
                 const uint32_t pos = atomicAdd(&a.pushcnt_nxt[t], 1u);
@@ -211,6 +237,9 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
 
 // handle_cast({broadcast, ServerRef, Message}) at every origin (RM :92-115,
 // AE :95-106), one thread per rumor; the origins come from the workload stream.
+// An origin's RM process makes one select call per rumor it originates, in
+// rumor order; the calls are "round 0" for the next round's sender checks
+// (rmnew_cur: the buffer round 1 reads as rmnew_prev, zeroed with ncall_cur).
 __global__ void dm_broadcast_kernel(DmArgs a, const uint32_t* __restrict__ origin, const uint32_t* __restrict__ idbit) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     DmCtr c = {0, 0, 0, 0, 0, 0};
@@ -218,9 +247,12 @@ __global__ void dm_broadcast_kernel(DmArgs a, const uint32_t* __restrict__ origi
         const uint32_t o = origin[i];
         atomicOr(&a.seen[o - a.v_lo], 1ull << idbit[i]);
         if (a.rm_on) {
-            const uint2 tp = sample2(a.key, o, i, KIND_RM, a.n_global);
-            if (tp.x != o) rm_send(a, o, tp.x, i, c);
-            if (a.n_global > 1 && tp.y != o) rm_send(a, o, tp.y, i, c);
+            uint32_t rank = 0;                       // the origin's earlier rumors
+            for (uint32_t j = 0; j < i; j++) rank += origin[j] == o ? 1u : 0u;
+            atomicOr(&a.rmnew_cur[o], 1ull << i);
+            const uint2 tp = select2(a.key, o, KIND_RM, a.n_global, a.dpc * rank);
+            if (tp.x != o) rm_send(a, tp.x, i, c);
+            if (tp.y != o) rm_send(a, tp.y, i, c);
         }
     }
     if (c.rm) atomicAdd(&a.stats[1], (unsigned long long)c.rm);
@@ -234,12 +266,12 @@ __global__ __launch_bounds__(kBlock) void dm_pushscan_kernel(DmArgs a, uint32_t 
     const uint32_t stride = gridDim.x * kBlock;
     unsigned long long ov = 0;
     for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < a.n_global; u += stride) {
-        const uint2 tp = sample2(a.key, u, tick_idx, KIND_AE, a.n_global);
+        const uint2 tp = select2(a.key, u, KIND_AE, a.n_global, a.dpc * (tick_idx - 1u));
         const uint32_t tg[2] = {tp.x, tp.y};
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const uint32_t t = tg[j];
-            if (t == u || (j == 1 && a.n_global < 2)) continue;
+            if (t == u) continue;
             const uint32_t lt = t - a.v_lo;
             if (lt >= a.n) continue;
             const uint32_t pos = atomicAdd(&a.pushcnt_nxt[lt], 1u);
@@ -249,25 +281,26 @@ __global__ __launch_bounds__(kBlock) void dm_pushscan_kernel(DmArgs a, uint32_t 
     (void)ov;
 }
 
-// Sharded ingest: this shard's RM inboxes = OR of the slices every shard
-// wrote for its range (world slices of `chunk`); its pull slots = the
-// reduce-scattered slice (one writer per slot).
+// Sharded ingest: this shard's RM count planes = the saturating sum of the
+// slices every shard wrote for its range (world slices of `chunk`); its pull
+// slots = the reduce-scattered slice (one writer per slot).
 __global__ __launch_bounds__(kBlock) void dm_ingest_kernel(DmArgs a, const unsigned long long* __restrict__ rm_recv,
                                                            const unsigned long long* __restrict__ pull_recv,
                                                            uint32_t world, uint32_t chunk) {
     const uint32_t stride = gridDim.x * kBlock;
     const size_t plane = (size_t)world * chunk;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += stride) {
-        unsigned long long r0 = 0, r1 = 0, r2 = 0;
+        unsigned long long A = 0, M = 0, T = 0;      // >= 1, >= 2, >= 3 senders so far
         for (uint32_t g = 0; g < world; g++) {
             const size_t o = (size_t)g * chunk + i;
-            r0 |= rm_recv[o];
-            r1 |= rm_recv[plane + o];
-            r2 |= rm_recv[2 * plane + o];
+            const unsigned long long x1 = rm_recv[o], x2 = rm_recv[plane + o], x3 = rm_recv[2 * plane + o];
+            T |= x3 | (M & x1) | (A & x2);
+            M |= x2 | (A & x1);
+            A |= x1;
         }
-        a.rm_nxt_reg[i] = r0;
-        a.rm_nxt_t0[i] = r1;
-        a.rm_nxt_t1[i] = r2;
+        a.rm_nxt_any[i] = A;
+        a.rm_nxt_multi[i] = M;
+        a.rm_nxt_tri[i] = T;
         a.pull_nxt[2 * (size_t)i] = pull_recv[2 * (size_t)i];
         a.pull_nxt[2 * (size_t)i + 1] = pull_recv[2 * (size_t)i + 1];
     }
@@ -299,8 +332,8 @@ hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_dm_ingest(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
-                            uint32_t world, uint32_t chunk, hipStream_t s) {
+hipError_t launch_dm_ingest_rm(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
+                               uint32_t world, uint32_t chunk, hipStream_t s) {
     uint32_t g = (a.n + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;
     if (g == 0) return hipSuccess;
@@ -316,237 +349,3 @@ hipError_t launch_dm_round(const DmArgs& a, hipStream_t s) {
 }
 
 }  // namespace psim
-
-// ---------------------------------------------------------------------------
-// host side of the vertex-sharded Demers epidemic (psim_demers_shard_*):
-// shard r owns global ids [r C, min((r+1) C, n)), C = ceil(n / world).  A
-// round is split-phase so that the transport stays the caller's:
-//   psim_demers_shard_round  -- the local round; RM messages to any vertex
-//       land in the caller's rm_shadow [3][world C] (OR), pull replies in
-//       pull_shadow [world C][2] (one writer per slot), the tick's snapshot
-//       in snap_all[v];
-//   caller: all_to_all of rm_shadow (slice d -> shard d), reduce_scatter(sum)
-//       of pull_shadow, all_gather of snap_all after a tick (RCCL on a node);
-//   psim_demers_shard_ingest -- OR the received RM slices into the inboxes,
-//       take the pull slice, list the tick's pushers per local receiver.
-// ---------------------------------------------------------------------------
-#include <algorithm>
-#include <cstring>
-#include <vector>
-
-using namespace psim;
-
-namespace {
-
-struct DmShard : ModuleState {
-    uint32_t n_global = 0, m = 0, ae_period = 0, rm_on = 0, world = 1, rank = 0, chunk = 0, v_lo = 0, n = 0;
-    unsigned long long full = 0;
-    unsigned long long *seen = nullptr, *rm[3] = {}, *pull = nullptr, *stats = nullptr;
-    uint32_t *pushcnt[2] = {}, *pushlist[2] = {}, *origin = nullptr, *idbit = nullptr;
-    std::vector<uint32_t> h_origin;
-    uint32_t par = 0;
-    uint64_t round = 0;
-    ~DmShard() override {
-        void* p[] = {seen, rm[0], rm[1], rm[2], pull, stats, pushcnt[0], pushcnt[1], pushlist[0], pushlist[1], origin,
-                     idbit};
-        for (void* x : p)
-            if (x) (void)hipFree(x);
-    }
-};
-
-DmShard* dms_of(psim_handle* h) { return static_cast<DmShard*>(handle_module(h, MOD_DMSHARD)); }
-const DmShard* dms_of(const psim_handle* h) { return static_cast<const DmShard*>(handle_module(h, MOD_DMSHARD)); }
-
-#define DMCHK(h, x)                                                                         \
-    do {                                                                                    \
-        hipError_t e_ = (x);                                                                \
-        if (e_ != hipSuccess)                                                               \
-            return handle_fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_)); \
-    } while (0)
-
-DmArgs dms_args(const psim_handle* h, const DmShard& d, void* rm_shadow, void* pull_shadow, void* snap_all) {
-    DmArgs a{};
-    a.n = d.n;
-    a.m = d.m;
-    a.v_lo = d.v_lo;
-    a.n_global = d.n_global;
-    a.sharded = 1;
-    const uint64_t seed = handle_seed(h);
-    a.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-    a.rm_on = d.rm_on;
-    a.full = d.full;
-    a.seen = d.seen;
-    a.snap = (unsigned long long*)snap_all;
-    a.rm_cur_reg = d.rm[0];
-    a.rm_cur_t0 = d.rm[1];
-    a.rm_cur_t1 = d.rm[2];
-    const size_t plane = (size_t)d.world * d.chunk;
-    unsigned long long* rs = (unsigned long long*)rm_shadow;
-    a.rm_nxt_reg = rs;
-    a.rm_nxt_t0 = rs ? rs + plane : nullptr;
-    a.rm_nxt_t1 = rs ? rs + 2 * plane : nullptr;
-    a.pushcnt_cur = d.pushcnt[d.par];
-    a.pushcnt_nxt = d.pushcnt[d.par ^ 1];
-    a.pushlist_cur = d.pushlist[d.par];
-    a.pushlist_nxt = d.pushlist[d.par ^ 1];
-    a.pull_cur = d.pull;
-    a.pull_nxt = (unsigned long long*)pull_shadow;
-    a.stats = d.stats;
-    return a;
-}
-
-}  // namespace
-
-extern "C" {
-
-int psim_demers_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on, int rank,
-                            int world, uint64_t* chunk_out) {
-    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1 || rm_on > 1 || world < 1 || rank < 0 || rank >= world)
-        return PSIM_EINVAL;
-    DMCHK(h, hipSetDevice(handle_device(h)));
-    DMCHK(h, hipStreamSynchronize(handle_stream(h)));
-    ModuleState*& slot = handle_module(h, MOD_DMSHARD);
-    delete slot;
-    slot = nullptr;
-    DmShard* d = new DmShard();
-    d->n_global = n;
-    d->m = m;
-    d->ae_period = ae_period;
-    d->rm_on = rm_on ? 1u : 0u;
-    d->world = (uint32_t)world;
-    d->rank = (uint32_t)rank;
-    d->chunk = (uint32_t)((uint64_t(n) + world - 1) / world);
-    d->v_lo = std::min<uint32_t>(n, d->chunk * (uint32_t)rank);
-    d->n = std::min<uint32_t>(n, d->v_lo + d->chunk) - d->v_lo;
-    const size_t N = std::max<uint32_t>(d->n, 1);
-    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
-    bool ok = A((void**)&d->seen, N * 8) && A((void**)&d->pull, N * 16) && A((void**)&d->stats, kStatShards * kNStat * 8) &&
-              A((void**)&d->origin, 64 * 4) && A((void**)&d->idbit, 64 * 4);
-    for (int k = 0; k < 3 && ok; k++) ok = A((void**)&d->rm[k], N * 8);
-    for (int p = 0; p < 2 && ok; p++)
-        ok = A((void**)&d->pushcnt[p], N * 4) && A((void**)&d->pushlist[p], N * kDmPushCap * 4);
-    if (!ok) {
-        const uint32_t nl = d->n;
-        delete d;
-        return handle_fail(h, PSIM_ENOMEM, "demers shard state for %u vertices", nl);
-    }
-    slot = d;
-    const uint64_t seed = handle_seed(h);
-    const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-    DMCHK(h, launch_dm_origins(key, n, m, d->origin, handle_stream(h)));
-    d->h_origin.assign(m, 0);
-    DMCHK(h, hipMemcpyAsync(d->h_origin.data(), d->origin, m * 4, hipMemcpyDeviceToHost, handle_stream(h)));
-    DMCHK(h, hipStreamSynchronize(handle_stream(h)));
-    std::vector<uint32_t> idbit(m);
-    for (uint32_t i = 0; i < m; i++) {
-        idbit[i] = i;
-        if (!d->rm_on)   // anti-entropy alone: ids {Node, 0} (Q20)
-            for (uint32_t j = 0; j < i; j++)
-                if (d->h_origin[j] == d->h_origin[i]) { idbit[i] = idbit[j]; break; }
-        d->full |= 1ull << idbit[i];
-    }
-    DMCHK(h, hipMemcpy(d->idbit, idbit.data(), m * 4, hipMemcpyHostToDevice));
-    if (chunk_out) *chunk_out = d->chunk;
-    return PSIM_OK;
-}
-
-int psim_demers_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local, uint64_t* chunk) {
-    if (!h) return PSIM_EINVAL;
-    const DmShard* d = dms_of(h);
-    if (!d) return PSIM_ESTATE;
-    if (v_lo) *v_lo = d->v_lo;
-    if (n_local) *n_local = d->n;
-    if (chunk) *chunk = d->chunk;
-    return PSIM_OK;
-}
-
-int psim_demers_shard_broadcast_all(psim_handle* h, void* rm_shadow) {
-    if (!h || !rm_shadow) return PSIM_EINVAL;
-    DmShard* d = dms_of(h);
-    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
-    DMCHK(h, hipSetDevice(handle_device(h)));
-    DMCHK(h, hipMemsetAsync(d->stats, 0, kStatShards * kNStat * 8, handle_stream(h)));
-    DmArgs a = dms_args(h, *d, rm_shadow, nullptr, nullptr);
-    DMCHK(h, launch_dm_broadcast(a, d->origin, d->idbit, handle_stream(h)));
-    DMCHK(h, hipStreamSynchronize(handle_stream(h)));
-    return PSIM_OK;
-}
-
-int psim_demers_shard_round(psim_handle* h, void* rm_shadow, void* pull_shadow, void* snap_all,
-                            psim_demers_stats* st, uint32_t* tick) {
-    if (!h || !rm_shadow || !pull_shadow || !snap_all) return PSIM_EINVAL;
-    DmShard* d = dms_of(h);
-    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
-    const hipStream_t s = handle_stream(h);
-    DMCHK(h, hipSetDevice(handle_device(h)));
-    DMCHK(h, hipMemsetAsync(d->stats, 0, kStatShards * kNStat * 8, s));
-    DmArgs a = dms_args(h, *d, rm_shadow, pull_shadow, snap_all);
-    const uint64_t t = d->round + 1;
-    a.tick = d->ae_period && (t % d->ae_period) == 0;
-    a.tick_idx = d->ae_period ? (uint32_t)(t / d->ae_period) : 0;
-    a.prev_tick = d->ae_period ? (uint32_t)(d->round / d->ae_period) : 0;
-    DMCHK(h, hipEventRecord(handle_event(h, 0), s));
-    DMCHK(h, launch_dm_round(a, s));
-    DMCHK(h, hipEventRecord(handle_event(h, 1), s));
-    std::vector<unsigned long long> hs(size_t(kStatShards) * kNStat);
-    DMCHK(h, hipMemcpyAsync(hs.data(), d->stats, hs.size() * 8, hipMemcpyDeviceToHost, s));
-    DMCHK(h, hipStreamSynchronize(s));
-    unsigned long long r[kNStat] = {0};
-    for (int sh = 0; sh < kStatShards; sh++)
-        for (int i = 0; i < kNStat; i++) {
-            if (i == 6) r[i] |= hs[sh * kNStat + i];
-            else r[i] += hs[sh * kNStat + i];
-        }
-    float ms = 0.f;
-    DMCHK(h, hipEventElapsedTime(&ms, handle_event(h, 0), handle_event(h, 1)));
-    handle_add_round(h, ms);
-    d->round = t;
-    if (tick) *tick = a.tick;
-    if (r[6]) return handle_fail(h, PSIM_EOVERFLOW, "demers shard round %llu: > %u anti-entropy pushes to one vertex",
-                                 (unsigned long long)t, kDmPushCap);
-    if (st) {
-        memset(st, 0, sizeof *st);
-        st->rm_sent = r[1];
-        st->push_sent = r[2];
-        st->pull_sent = r[3];
-        st->delivered_new = r[4];
-        st->complete = r[5];
-        const uint64_t msgs = r[1] + r[2] + r[3];
-        st->algo_bytes = 2ull * d->n * d->m / 8 + r[2] * 6ull * d->m / 8 + 32ull * msgs;
-        st->kernel_ms = ms;
-    }
-    return PSIM_OK;
-}
-
-int psim_demers_shard_ingest(psim_handle* h, const void* rm_recv, const void* pull_recv, uint32_t tick) {
-    if (!h || !rm_recv || !pull_recv) return PSIM_EINVAL;
-    DmShard* d = dms_of(h);
-    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
-    const hipStream_t s = handle_stream(h);
-    DMCHK(h, hipSetDevice(handle_device(h)));
-    DmArgs a = dms_args(h, *d, nullptr, nullptr, nullptr);
-    a.rm_nxt_reg = d->rm[0];          // the inboxes the next round reads
-    a.rm_nxt_t0 = d->rm[1];
-    a.rm_nxt_t1 = d->rm[2];
-    a.pull_nxt = d->pull;
-    DMCHK(h, launch_dm_ingest(a, (const unsigned long long*)rm_recv, (const unsigned long long*)pull_recv, d->world,
-                              d->chunk, s));
-    if (tick) DMCHK(h, launch_dm_pushscan(a, (uint32_t)(d->round / d->ae_period), s));
-    DMCHK(h, hipStreamSynchronize(s));
-    d->par ^= 1u;
-    return PSIM_OK;
-}
-
-int psim_demers_shard_get_seen(const psim_handle* h, uint64_t* seen, size_t n) {
-    if (!h || !seen) return PSIM_EINVAL;
-    const DmShard* d = dms_of(h);
-    if (!d) return PSIM_ESTATE;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    if (n != d->n) return handle_fail(hh, PSIM_EINVAL, "shard holds %u vertices", d->n);
-    DMCHK(hh, hipSetDevice(handle_device(h)));
-    DMCHK(hh, hipStreamSynchronize(handle_stream(h)));
-    if (n) DMCHK(hh, hipMemcpy(seen, d->seen, n * 8, hipMemcpyDeviceToHost));
-    return PSIM_OK;
-}
-
-}  // extern "C"

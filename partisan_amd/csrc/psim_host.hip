@@ -209,17 +209,6 @@ struct psim_handle {
     } sh;
     hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
 
-    // Demers epidemic state (demers.hip)
-    struct Dm {
-        uint32_t n = 0, m = 0, ae_period = 0, rm_on = 0;   // rm_on: 0 off, 1 rumor mongering, 2 direct mail
-        unsigned long long full = 0;
-        unsigned long long dm_pending = 0;                 // direct-mail ids the next round delivers
-        unsigned long long *seen = nullptr, *snap = nullptr, *rm[2][3] = {}, *pull[2] = {};
-        uint32_t *pushcnt[2] = {}, *pushlist[2] = {}, *origin = nullptr, *idbit = nullptr;
-        std::vector<uint32_t> h_origin;
-        uint32_t par = 0;
-        uint64_t round = 0, complete = 0;
-    } dm;
 
     // HyParView state (hyparview.hip)
     struct Hv {
@@ -276,15 +265,6 @@ int fail(psim_handle* h, int code, const char* fmt, ...) {
         if (e_ != hipSuccess)                                                            \
             return fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));     \
     } while (0)
-
-void free_demers(psim_handle* h) {
-    auto& d = h->dm;
-    void* ptrs[] = {d.seen, d.snap, d.rm[0][0], d.rm[0][1], d.rm[0][2], d.rm[1][0], d.rm[1][1], d.rm[1][2],
-                    d.pull[0], d.pull[1], d.pushcnt[0], d.pushcnt[1], d.pushlist[0], d.pushlist[1], d.origin, d.idbit};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-    h->dm = psim_handle::Dm();
-}
 
 constexpr uint32_t kHvChunk = 16;   // HyParView rounds between host synchronisations
 
@@ -1239,7 +1219,6 @@ int psim_destroy(psim_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
     free_graph(h);
-    free_demers(h);
     free_hv(h);
     free_cs(h);
     for (auto& m : h->mods) {
@@ -2824,170 +2803,6 @@ int psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uint
 }
 int psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n) {
     return vc_op(h, 3, a, nullptr, actor, out, nullptr, n);
-}
-
-}  // extern "C"
-
-namespace {
-
-DmArgs make_dm_args(const psim_handle* h, uint32_t par, unsigned long long* stats) {
-    const auto& d = h->dm;
-    DmArgs a{};
-    a.n = d.n;
-    a.m = d.m;
-    a.v_lo = 0;
-    a.n_global = d.n;
-    a.sharded = 0;
-    a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
-    a.rm_on = d.rm_on == 1u;
-    a.full = d.full;
-    a.seen = d.seen;
-    a.snap = d.snap;
-    a.rm_cur_reg = d.rm[par][0];
-    a.rm_cur_t0 = d.rm[par][1];
-    a.rm_cur_t1 = d.rm[par][2];
-    a.rm_nxt_reg = d.rm[par ^ 1][0];
-    a.rm_nxt_t0 = d.rm[par ^ 1][1];
-    a.rm_nxt_t1 = d.rm[par ^ 1][2];
-    a.pushcnt_cur = d.pushcnt[par];
-    a.pushcnt_nxt = d.pushcnt[par ^ 1];
-    a.pushlist_cur = d.pushlist[par];
-    a.pushlist_nxt = d.pushlist[par ^ 1];
-    a.pull_cur = d.pull[par];
-    a.pull_nxt = d.pull[par ^ 1];
-    a.stats = stats;
-    return a;
-}
-
-int dm_drive(psim_handle* h, uint32_t max_rounds, psim_demers_stats* out, size_t cap, bool stop, uint32_t* ran_out) {
-    auto& d = h->dm;
-    if (!d.n) return fail(h, PSIM_ESTATE, "psim_demers_setup not called");
-    uint32_t ran = 0;
-    while (ran < max_rounds && !(stop && d.complete == d.n)) {
-        HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
-        DmArgs a = make_dm_args(h, d.par, h->stats);
-        const uint64_t t = d.round + 1;   // 1-based round being run
-        a.tick = d.ae_period && (t % d.ae_period) == 0;
-        a.tick_idx = d.ae_period ? (uint32_t)(t / d.ae_period) : 0;
-        a.prev_tick = d.ae_period ? (uint32_t)(d.round / d.ae_period) : 0;
-        a.dm_mail = d.dm_pending;
-        d.dm_pending = 0;
-        HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
-        HIPCHK(h, launch_dm_round(a, h->stream));
-        HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        d.par ^= 1u;
-        d.round = t;
-        unsigned long long r[kNStat];
-        reduce_row(h->h_stats, r);
-        float ms = 0.f;
-        HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-        if (r[6]) return fail(h, PSIM_EOVERFLOW, "demers round %llu: > %u anti-entropy pushes to one vertex",
-                              (unsigned long long)t, kDmPushCap);
-        d.complete = r[5];
-        h->kernel_ms_total += ms;
-        h->rounds_total++;
-        if (out && ran < cap) {
-            psim_demers_stats& o = out[ran];
-            o.rm_sent = r[1];
-            o.push_sent = r[2];
-            o.pull_sent = r[3];
-            o.delivered_new = r[4];
-            o.complete = r[5];
-            const uint64_t msgs = r[1] + r[2] + r[3];
-            o.algo_bytes = 2ull * d.n * d.m / 8 + r[2] * 6ull * d.m / 8 + 32ull * msgs;
-            o.kernel_ms = ms;
-        }
-        ran++;
-    }
-    if (ran_out) *ran_out = ran;
-    return PSIM_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int psim_demers_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t ae_period, uint32_t rm_on) {
-    if (!h || n < 2 || m == 0 || m > 64 || ae_period == 1 || rm_on > 2) return PSIM_EINVAL;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    free_demers(h);
-    auto& d = h->dm;
-    const size_t N = n;
-    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
-    bool ok = A((void**)&d.seen, N * 8) && A((void**)&d.snap, N * 8) && A((void**)&d.origin, 64 * 4) &&
-              A((void**)&d.idbit, 64 * 4);
-    for (int p = 0; p < 2 && ok; p++) {
-        for (int k = 0; k < 3 && ok; k++) ok = A((void**)&d.rm[p][k], N * 8);
-        ok = ok && A((void**)&d.pull[p], N * 16) && A((void**)&d.pushcnt[p], N * 4) &&
-             A((void**)&d.pushlist[p], N * kDmPushCap * 4);
-    }
-    if (!ok) {
-        free_demers(h);
-        return fail(h, PSIM_ENOMEM, "demers state for n=%u", n);
-    }
-    d.n = n;
-    d.m = m;
-    d.ae_period = ae_period;
-    d.rm_on = rm_on;
-    d.dm_pending = 0;
-    const uint2 key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
-    HIPCHK(h, launch_dm_origins(key, n, m, d.origin, h->stream));
-    d.h_origin.assign(m, 0);
-    HIPCHK(h, hipMemcpyAsync(d.h_origin.data(), d.origin, m * 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    std::vector<uint32_t> idbit(m);
-    d.full = 0;
-    for (uint32_t i = 0; i < m; i++) {
-        idbit[i] = i;
-        if (!d.rm_on)   // anti-entropy alone: ids {Node, 0} (next_id never increments, Q20)
-            for (uint32_t j = 0; j < i; j++)
-                if (d.h_origin[j] == d.h_origin[i]) { idbit[i] = idbit[j]; break; }
-        d.full |= 1ull << idbit[i];
-    }
-    HIPCHK(h, hipMemcpy(d.idbit, idbit.data(), m * 4, hipMemcpyHostToDevice));
-    return PSIM_OK;
-}
-
-int psim_demers_broadcast_all(psim_handle* h) {
-    if (!h || !h->dm.n) return PSIM_ESTATE;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
-    DmArgs a = make_dm_args(h, h->dm.par ^ 1u, h->stats);   // writes the inbox the next round reads
-    HIPCHK(h, launch_dm_broadcast(a, h->dm.origin, h->dm.idbit, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (h->dm.rm_on == 2u) h->dm.dm_pending |= h->dm.full;   // every other member receives every rumor
-    return PSIM_OK;
-}
-
-int psim_demers_step(psim_handle* h, uint32_t rounds, psim_demers_stats* stats, size_t cap) {
-    if (!h) return PSIM_EINVAL;
-    HIPCHK(h, hipSetDevice(h->device));
-    return dm_drive(h, rounds, stats, cap, false, nullptr);
-}
-
-int psim_demers_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* stats, size_t cap, uint32_t* rounds_run) {
-    if (!h) return PSIM_EINVAL;
-    HIPCHK(h, hipSetDevice(h->device));
-    return dm_drive(h, max_rounds, stats, cap, true, rounds_run);
-}
-
-int psim_demers_get_seen(const psim_handle* h, uint64_t* seen, size_t n) {
-    if (!h || !seen || n != h->dm.n || !n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    HIPCHK(hh, hipMemcpy(seen, h->dm.seen, n * 8, hipMemcpyDeviceToHost));
-    return PSIM_OK;
-}
-
-int psim_demers_origins(const psim_handle* h, uint32_t* origins, size_t m) {
-    if (!h || !origins || m != h->dm.m || !m) return PSIM_EINVAL;
-    memcpy(origins, h->dm.h_origin.data(), m * 4);
-    return PSIM_OK;
 }
 
 int psim_plumtree_focus(psim_handle* h, uint32_t root) {

@@ -218,16 +218,27 @@ struct DmArgs {
     uint2 key;                            // Philox key {seed_lo, seed_hi}
     uint32_t rm_on;
     uint32_t tick, tick_idx, prev_tick;   // AE tick at the end of this round; tick indices
+    uint64_t dpc;                         // draws per select_random_sublist call (philox.h dm_draws_per_call)
     unsigned long long dm_mail;           // direct mail: rumor ids every vertex receives this round
     unsigned long long full;              // every rumor id's bit
     unsigned long long* __restrict__ seen;       // [n] the message store
     unsigned long long* __restrict__ snap;       // [n_global] AE payload taken at the tick (global ids)
-    unsigned long long* __restrict__ rm_cur_reg; // [n] RM inbox read this round
-    unsigned long long* __restrict__ rm_cur_t0;
-    unsigned long long* __restrict__ rm_cur_t1;
-    unsigned long long* __restrict__ rm_nxt_reg; // [n_global] RM inbox written this round (global ids)
-    unsigned long long* __restrict__ rm_nxt_t0;
-    unsigned long long* __restrict__ rm_nxt_t1;
+    // RM inbox: rumors received this round from >= 1 / >= 2 / >= 3 senders (bit planes of a
+    // saturating count; senders raise them with atomicOr cascades) -- cur [n], nxt [n_global]
+    unsigned long long* __restrict__ rm_cur_any;
+    unsigned long long* __restrict__ rm_cur_multi;
+    unsigned long long* __restrict__ rm_cur_tri;
+    unsigned long long* __restrict__ rm_nxt_any;
+    unsigned long long* __restrict__ rm_nxt_multi;
+    unsigned long long* __restrict__ rm_nxt_tri;
+    // each vertex's RM process (its sequential draw stream): the rumors it called
+    // select_random_sublist for in the last round and the calls it made before that
+    // round (global ids, all vertices), and the same for this round (every vertex
+    // writes its own every round)
+    const unsigned long long* __restrict__ rmnew_prev;
+    const uint32_t* __restrict__ ncall_prev;
+    unsigned long long* __restrict__ rmnew_cur;
+    uint32_t* __restrict__ ncall_cur;
     uint32_t* __restrict__ pushcnt_cur;   // [n]
     uint32_t* __restrict__ pushcnt_nxt;
     uint32_t* __restrict__ pushlist_cur;  // [n][kDmPushCap]
@@ -238,10 +249,11 @@ struct DmArgs {
 };
 hipError_t launch_dm_origins(uint2 key, uint32_t n, uint32_t m, uint32_t* origin, hipStream_t s);
 hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const uint32_t* idbit, hipStream_t s);
+// sharded ingest: the RM planes of every shard's slice (saturating sum), the pull slice
+hipError_t launch_dm_ingest_rm(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
+                               uint32_t world, uint32_t chunk, hipStream_t s);
 hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
 hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s);
-hipError_t launch_dm_ingest(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
-                            uint32_t world, uint32_t chunk, hipStream_t s);
 
 // HyParView (hyparview.hip)
 constexpr uint32_t kHvX = 8;          // exchange list capacity (1 + k_active + k_passive)
@@ -532,7 +544,9 @@ int rccl_unique_id(void* out);
 struct ModuleState {
     virtual ~ModuleState() {}
 };
-enum ModuleSlot : int { MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_RELAY = 4, MOD_COUNT = 5 };
+enum ModuleSlot : int {
+    MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_RELAY = 4, MOD_DEMERS = 5, MOD_COUNT = 6
+};
 ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);
 hipStream_t handle_stream(const psim_handle* h);

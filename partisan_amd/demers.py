@@ -51,9 +51,11 @@ class DemersEpidemic:
 class ShardedDemers:
     """Demers epidemic vertex-sharded over `world` processes, one GPU each
     (SURVEY 8(e)); include/psim.h "vertex-sharded Demers".  The exchange per
-    round: all-to-all of the RM inbox slices (OR-merged by the receiver),
-    reduce-scatter of the pull slots, all-gather of the AE snapshots after a
-    tick -- RCCL over xGMI with backend "nccl", host-staged with "gloo"."""
+    round: all-to-all of the RM count-plane slices (summed, saturating, by the
+    receiver), reduce-scatter of the pull slots, all-gather of every RM
+    process's call records (rumors called, calls before the round), all-gather
+    of the AE snapshots after a tick -- RCCL over xGMI with backend "nccl",
+    host-staged with "gloo"."""
 
     def __init__(self, n, m, rank, world, device=0, backend="nccl", ae_period=2, rumor_mongering=True, seed=0):
         import torch
@@ -76,6 +78,8 @@ class ShardedDemers:
         self.rm_shadow, self.rm_recv = z(3, G * Cn), z(3, G * Cn)
         self.pull_shadow, self.pull_recv = z(2 * G * Cn), z(2 * Cn)
         self.snap_all = z(G * Cn)
+        # RM call records: [G C] u64 rumors called, then [G C] u32 calls before the round
+        self.rmx_all = torch.zeros(3 * G * Cn, dtype=torch.int32, device=self.dev)
         self.local_kernel_ms = 0.0
         self.local_algo_bytes = 0
 
@@ -91,6 +95,9 @@ class ShardedDemers:
             for k in range(3):
                 dist.all_to_all_single(self.rm_recv[k], self.rm_shadow[k])
             dist.reduce_scatter_tensor(self.pull_recv, self.pull_shadow, op=dist.ReduceOp.SUM)
+            for plane in self._rmx_planes():
+                mine = plane[r * plane.numel() // G:(r + 1) * plane.numel() // G].clone()
+                dist.all_gather_into_tensor(plane, mine)
             if tick:
                 mine = self.snap_all[r * Cn:(r + 1) * Cn].clone()
                 dist.all_gather_into_tensor(self.snap_all, mine)
@@ -108,6 +115,12 @@ class ShardedDemers:
             for x in pull_all:
                 ps += x[2 * r * Cn:2 * (r + 1) * Cn]
             self.pull_recv.copy_(ps.to(self.dev))
+            for plane in self._rmx_planes():
+                k = plane.numel() // G
+                host = plane.cpu()
+                parts = [torch.zeros_like(host) for _ in range(G)]
+                dist.all_gather(parts, host)
+                plane.copy_(torch.cat([parts[g][g * k:(g + 1) * k] for g in range(G)]).to(self.dev))
             if tick:
                 snap = self.snap_all.cpu()
                 snap_all = [torch.zeros_like(snap) for _ in range(G)]
@@ -118,7 +131,12 @@ class ShardedDemers:
         self.rm_shadow.zero_()
         self.pull_shadow.zero_()
         check(lib().psim_demers_shard_ingest(self._h, self._p(self.rm_recv), self._p(self.pull_recv),
-                                             1 if tick else 0), self._h)
+                                             self._p(self.rmx_all), 1 if tick else 0), self._h)
+
+    def _rmx_planes(self):
+        """The two rmx_all planes as separate views: [G C] int64, [G C] int32."""
+        n = self.world * self.chunk
+        return [self.rmx_all[:2 * n].view(self.torch.int64), self.rmx_all[2 * n:3 * n]]
 
     @staticmethod
     def _dist():
@@ -132,7 +150,7 @@ class ShardedDemers:
 
     # -------------------------------------------------------------- protocol
     def broadcast(self):
-        check(lib().psim_demers_shard_broadcast_all(self._h, self._p(self.rm_shadow)), self._h)
+        check(lib().psim_demers_shard_broadcast_all(self._h, self._p(self.rm_shadow), self._p(self.rmx_all)), self._h)
         self._exchange(False)
 
     def step(self, rounds=1):
@@ -142,7 +160,8 @@ class ShardedDemers:
             st = DemersStats()
             tick = C.c_uint32()
             check(lib().psim_demers_shard_round(self._h, self._p(self.rm_shadow), self._p(self.pull_shadow),
-                                                self._p(self.snap_all), C.byref(st), C.byref(tick)), self._h)
+                                                self._p(self.snap_all), self._p(self.rmx_all), C.byref(st),
+                                                C.byref(tick)), self._h)
             d = st.as_dict()
             self.local_kernel_ms += d["kernel_ms"]
             self.local_algo_bytes += d["algo_bytes"]

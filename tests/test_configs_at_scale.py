@@ -136,7 +136,8 @@ def test_c4_10m_single_gpu():
     """C4: 10M peers, 64 rumors from Philox origins, rumor
     mongering fanout 2 + anti-entropy every 2 rounds: every vertex ends with
     every rumor, each (vertex, rumor) pair is stored exactly once (the origins
-    start with theirs), in the 21 rounds profiles/r01/configs.jsonl records."""
+    start with theirs), in 20 rounds (21 until round 3 keyed the draws by event;
+    each process now draws from its own sequential stream)."""
     import partisan_amd as pa
     n, m = 10_000_000, 64
     sim = pa.Simulator(seed=0x5EED0004, device=0)
@@ -145,7 +146,7 @@ def test_c4_10m_single_gpu():
     st, rounds = dm.run(200)
     assert st[-1]["complete"] == n
     assert sum(s["delivered_new"] for s in st) == n * m - m
-    assert rounds == 21, rounds
+    assert rounds == 20, rounds
     assert (dm.seen() == M64).all()
     sim.close()
 

@@ -21,15 +21,34 @@ def test_philox_known_answers():
         [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
 
 
-def test_sample2_is_uniform_pair():
-    n = 7
-    counts = np.zeros((n, n))
-    for e in range(20000):
-        a, b = O.sample2(123, 5, e, 2, n)
+@pytest.mark.parametrize("n", [7, 5000])
+def test_select2_is_uniform_pair(n):
+    """Faithful (n <= 1024: the two smallest of n sort keys) and scaled (2 draws)
+    select_random_sublist(.., 2): a uniform ordered pair of distinct members,
+    each call at its own draw index of the process's stream."""
+    dpc = O.draws_per_call(n)
+    assert dpc == (n if n <= 1024 else 2)
+    bins = n if n == 7 else 10
+    ha, hb = np.zeros(bins), np.zeros(bins)
+    for call in range(20000):
+        a, b = O.select2(123, 5, 2, n, call * dpc)
         assert a != b and 0 <= a < n and 0 <= b < n
-        counts[a, b] += 1
-    off = counts[~np.eye(n, dtype=bool)]
-    assert off.min() > 0.7 * off.mean() and off.max() < 1.3 * off.mean()
+        ha[a * bins // n] += 1
+        hb[b * bins // n] += 1
+    for h in (ha, hb):
+        assert h.min() > 0.8 * h.mean() and h.max() < 1.2 * h.mean()
+
+
+def test_select2_faithful_is_the_sorted_shuffle():
+    """shuffle/1 (demers_rumor_mongering.erl:185-186): sort {uniform(), N};
+    the first two = the members with the two smallest 53-bit keys."""
+    n, j = 300, 1234
+    keys = []
+    for i in range(n):
+        r = O.philox([5, (j + i) & 0xFFFFFFFF, 2, (j + i) >> 32], [123 & 0xFFFFFFFF, 0])
+        keys.append(((r[0] | (r[1] << 32)) >> 11, i))
+    keys.sort()
+    assert O.select2(123, 5, 2, n, j) == [keys[0][1], keys[1][1]]
 
 
 @pytest.mark.parametrize("rm,ae", [(True, 2), (True, 0), (False, 2), (True, 3), ("direct_mail", 0)])

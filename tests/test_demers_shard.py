@@ -88,7 +88,7 @@ def _cpu_worker(rank, world, port, q):
         seen = {}
 
         class FakeLib:
-            def psim_demers_shard_ingest(self, h, rm_ptr, pull_ptr, tick):
+            def psim_demers_shard_ingest(self, h, rm_ptr, pull_ptr, rmx_ptr, tick):
                 seen["tick"] = tick
                 return 0
 
@@ -99,6 +99,10 @@ def _cpu_worker(rank, world, port, q):
         z = lambda *s: torch.zeros(*s, dtype=torch.int64)  # noqa: E731
         sd.rm_shadow, sd.rm_recv = z(3, G * Cn), z(3, G * Cn)
         sd.pull_shadow, sd.pull_recv, sd.snap_all = z(2 * G * Cn), z(2 * Cn), z(G * Cn)
+        sd.rmx_all = torch.zeros(3 * G * Cn, dtype=torch.int32)
+        rmx64, rmx32 = sd._rmx_planes()
+        rmx64[rank * Cn:(rank + 1) * Cn] = (1 << 40) + rank      # this shard's call records, both planes
+        rmx32[rank * Cn:(rank + 1) * Cn] = 50 + rank
         # rank r sets bit r of every RM entry and writes pull slot values r+1
         # into the slots of vertex 2*rank+1 of every shard; snapshot of its own slice
         for k in range(3):
@@ -127,6 +131,8 @@ def _cpu_worker(rank, world, port, q):
             assert int(sd.pull_recv[2 * s]) == 100 * (s + 1) + rank
         for g in range(G):
             assert (sd.snap_all[g * Cn:(g + 1) * Cn] == 7 + g).all()
+            assert (rmx64[g * Cn:(g + 1) * Cn] == (1 << 40) + g).all()     # all-gathered in slices of C
+            assert (rmx32[g * Cn:(g + 1) * Cn] == 50 + g).all()
         assert int(sd.rm_shadow.abs().sum()) == 0 and int(sd.pull_shadow.abs().sum()) == 0
         assert seen["tick"] == 1
         dist.destroy_process_group()

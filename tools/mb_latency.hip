@@ -54,6 +54,30 @@ __global__ void chase_with_load(const uint32_t* __restrict__ nxt, uint32_t hops,
     if (acc.x == 0xFFFFFFFFu) sink[0] = acc;
 }
 
+// one lane: `k` operations to random addresses (all issued, then waited for), repeated `reps` times
+// op 0: store, 1: non-returning device atomicOr, 2: returning atomicOr, 3: load
+__global__ void ops_latency(uint32_t* __restrict__ buf, size_t n, uint32_t k, uint32_t reps, int op,
+                            unsigned long long* ticks, uint32_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t x = 88172645463325252ull;
+    uint32_t acc = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t r = 0; r < reps; r++) {
+        for (uint32_t i = 0; i < k; i++) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            const size_t a = (size_t)(x % n);
+            if (op == 0) buf[a] = (uint32_t)x;
+            else if (op == 1) atomicOr(buf + a, 1u);
+            else if (op == 2) acc += atomicOr(buf + a, 1u);
+            else acc += __builtin_nontemporal_load(buf + a);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    ticks[0] = t1 - t0;
+    out[0] = acc;
+}
+
 int main() {
     const size_t n = size_t(1) << 28;   // 1 GiB of u32: every hop misses every cache
     std::vector<uint32_t> h(n);
@@ -70,8 +94,18 @@ int main() {
     CHK(hipMalloc(&big, nbig * 16));
     CHK(hipMemset(big, 1, nbig * 16));
     CHK(hipMalloc(&sink, 64));
-    const uint32_t hops = 2000;
     unsigned long long t;
+    for (int op = 0; op < 4; op++)
+        for (uint32_t k : {1u, 8u}) {
+            const uint32_t reps = 200;
+            hipLaunchKernelGGL(ops_latency, dim3(1), dim3(64), 0, 0, d, n, k, reps, op, ticks, out);
+            CHK(hipDeviceSynchronize());
+            CHK(hipMemcpy(&t, ticks, 8, hipMemcpyDeviceToHost));
+            static const char* nm[] = {"store", "atomicOr (no return)", "atomicOr (returned)", "nt load"};
+            printf("%-22s x%u to random words of 1 GiB, then vmcnt(0): %.3f us per batch\n", nm[op], k,
+                   t * 0.01 / reps);
+        }
+    const uint32_t hops = 2000;
     for (int rep = 0; rep < 3; rep++) {
         for (uint32_t grid : {1u, 8u, 256u, 1024u}) {
             hipLaunchKernelGGL(chase, dim3(grid), dim3(64), 0, 0, d, hops, out, ticks);
