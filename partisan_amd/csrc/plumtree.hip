@@ -498,12 +498,44 @@ __device__ __forceinline__ bool word_non_prune(uint32_t w) {
 // What happens to a local receiver u after its word over slot s was stored:
 // the round kernels flag its group (and list it in a sparse round); the
 // frontier kernel claims it for its own next round (pt_frontier_kernel).
+// Mark 2 (flag + worklist) claims a flag with a RETURNING atomicOr: the
+// claims of a vertex's words are all issued before any result is used, so the
+// vertex waits for one atomic round trip instead of one per word (a wave's
+// dependent random memory operations are what a sparse round costs).
+template <uint32_t kCap>
 struct GroupSink {
     const PtArgs& a;
     uint32_t mark;
     WlLds* wl;
-    __device__ __forceinline__ void word(uint32_t, uint32_t u) { mark_group(a, u >> kGroupShift, mark, wl); }
-    __device__ __forceinline__ void done() {}
+    uint32_t m = 0;
+    uint32_t g[kCap];
+    __device__ __forceinline__ void word(uint32_t s, uint32_t u) {
+#ifndef PT_SERIAL_CLAIMS                // A/B: each claim's result used before the next word is sent
+        if (mark != 2)
+#endif
+        {
+            mark_group(a, u >> kGroupShift, mark, wl);
+            return;
+        }
+        g[s] = u >> kGroupShift;
+        m |= 1u << s;
+    }
+    __device__ __forceinline__ void done() {
+        if (!m) return;
+        uint32_t old[kCap];
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++)
+            old[s] = ((m >> s) & 1u)
+                         ? atomicOr(reinterpret_cast<uint32_t*>(a.pend_nxt) + (g[s] >> 2), 1u << (8 * (g[s] & 3u)))
+                         : 0u;
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) {
+            if (!((m >> s) & 1u) || (old[s] & (1u << (8 * (g[s] & 3u))))) continue;   // not sent / already listed
+            const uint32_t k = wl ? atomicAdd(&wl->n, 1u) : kWlLds;
+            if (k < kWlLds) wl->g[k] = g[s];
+            else wl_push_global(a, g[s]);
+        }
+    }
 };
 
 // Returns the change in "holds outstanding rows" (vst_store).
@@ -575,7 +607,7 @@ template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
                                                const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, uint32_t mark,
                                                WlLds* wl) {
-    GroupSink sink{a, mark, wl};
+    GroupSink<kCap> sink{a, mark, wl};
     (void)pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, sink);
 }
 

@@ -78,6 +78,68 @@ __global__ void ops_latency(uint32_t* __restrict__ buf, size_t n, uint32_t k, ui
     out[0] = acc;
 }
 
+// batches of `k` random loads, varying how they are spread: mode 0: one lane, k
+// instructions; 1: k lanes of one wave, one instruction; 2: k waves of one
+// workgroup, one lane each; 3: one lane, k loads inside one 64 KB window
+// (random window per batch); 4: one lane, k loads inside one 2 MB window
+__global__ __launch_bounds__(1024) void spread_latency(const uint32_t* __restrict__ buf, size_t n, uint32_t k,
+                                                       uint32_t reps, int mode, unsigned long long* ticks, uint32_t* out) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const bool active = mode == 1 ? (wv == 0 && lane < k) : mode == 2 ? (lane == 0 && wv < k) : threadIdx.x == 0;
+    uint64_t x = 88172645463325252ull + threadIdx.x * 7919ull;
+    uint32_t acc = 0;
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t r = 0; r < reps; r++) {
+        if (active) {
+            if (mode == 0 || mode >= 3) {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                const size_t win = (mode == 3 || mode == 6) ? 16384 : mode == 4 ? 524288 : n;
+                const size_t base = (mode == 3 || mode == 4 || mode == 6) ? (size_t)(x % (n / win)) * win : 0;
+                for (uint32_t i = 0; i < k; i++) {
+                    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                    if (mode >= 5) acc += buf[base + (size_t)(x % win)];            // plain (cached) loads
+                    else acc += __builtin_nontemporal_load(buf + base + (size_t)(x % win));
+                }
+            } else {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                acc += __builtin_nontemporal_load(buf + (size_t)(x % n));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) ticks[0] = t1 - t0;
+    out[threadIdx.x] = acc;
+}
+
+// one lane, 8 independent loads issued back to back (unrolled, addresses first), then one wait
+template <bool kNt>
+__global__ void unrolled8(const uint32_t* __restrict__ buf, size_t n, uint32_t reps, unsigned long long* ticks, uint32_t* out) {
+    if (threadIdx.x != 0) return;
+    uint64_t x = 88172645463325252ull;
+    uint32_t acc = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t r = 0; r < reps; r++) {
+        size_t ad[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            ad[i] = (size_t)(x % n);
+        }
+        uint32_t v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = kNt ? __builtin_nontemporal_load(buf + ad[i]) : buf[ad[i]];
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc += v[i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    ticks[0] = t1 - t0;
+    out[0] = acc;
+}
+
 int main() {
     const size_t n = size_t(1) << 28;   // 1 GiB of u32: every hop misses every cache
     std::vector<uint32_t> h(n);
@@ -105,6 +167,24 @@ int main() {
             printf("%-22s x%u to random words of 1 GiB, then vmcnt(0): %.3f us per batch\n", nm[op], k,
                    t * 0.01 / reps);
         }
+    for (int mode = 0; mode < 7; mode++) {
+        const uint32_t reps = 200, k = 8;
+        hipLaunchKernelGGL(spread_latency, dim3(1), dim3(1024), 0, 0, d, n, k, reps, mode, ticks, out);
+        CHK(hipDeviceSynchronize());
+        CHK(hipMemcpy(&t, ticks, 8, hipMemcpyDeviceToHost));
+        static const char* nm[] = {"1 lane, 8 instructions", "8 lanes, 1 instruction", "8 waves x 1 lane",
+                                   "1 lane, 8 in a 64 KB window", "1 lane, 8 in a 2 MB window",
+                                   "1 lane, 8 plain loads", "1 lane, 8 plain in 64 KB"};
+        printf("8 random loads, %-28s: %.3f us per batch\n", nm[mode], t * 0.01 / reps);
+    }
+    for (int nt = 0; nt < 2; nt++) {
+        if (nt) hipLaunchKernelGGL(unrolled8<true>, dim3(1), dim3(64), 0, 0, d, n, 200u, ticks, out);
+        else hipLaunchKernelGGL(unrolled8<false>, dim3(1), dim3(64), 0, 0, d, n, 200u, ticks, out);
+        CHK(hipDeviceSynchronize());
+        CHK(hipMemcpy(&t, ticks, 8, hipMemcpyDeviceToHost));
+        printf("8 random loads, 1 lane, unrolled, all issued then one wait (%s): %.3f us per batch\n", nt ? "nt" : "plain",
+               t * 0.01 / 200);
+    }
     const uint32_t hops = 2000;
     for (int rep = 0; rep < 3; rep++) {
         for (uint32_t grid : {1u, 8u, 256u, 1024u}) {
