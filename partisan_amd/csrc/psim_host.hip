@@ -210,37 +210,9 @@ struct psim_handle {
     hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
 
 
-    // HyParView state (hyparview.hip)
-    struct Hv {
-        uint32_t n = 0, cap = 0;
-        psim_hv_config cfg{};
-        HvHead* head = nullptr;
-        uint32_t *act = nullptr, *pas = nullptr, *alive = nullptr;
-        unsigned long long *skey = nullptr, *rkey = nullptr;   // id-map hash tables
-        uint2 *sval = nullptr, *rval = nullptr;
-        uint32_t map_cap = 0;
-        HvMsg* msg[2] = {nullptr, nullptr};
-        uint32_t* nmsg = nullptr;                 // [2] device queue counts
-        uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
-        uint32_t* idx2 = nullptr;                 // [cap] crowded buckets, sorted
-        uint32_t* joinbuf = nullptr;              // [2][n] staged join pairs
-        unsigned long long* stats = nullptr;      // [kHvChunk][kHvNStat]
-        unsigned long long* h_stats = nullptr;    // pinned mirror
-        hipEvent_t ev[2 * 16] = {};
-        uint32_t par = 0;                         // queue the next round reads
-        uint64_t round = 0;
-    } hv;
 
     psim::ModuleState* mods[psim::MOD_COUNT] = {};   // fullmem / scamp host state
 
-    // causal delivery state (causal.hip)
-    struct Cs {
-        uint32_t n = 0, m = 0, period = 1, dmax = 1, redeliver = 1;
-        uint32_t n_global = 0, v_lo = 0, rank = 0, world = 1;   // vertex shard [v_lo, v_lo + n) of n_global
-        uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr;
-        unsigned long long *delivered = nullptr, *stats = nullptr, *h_stats = nullptr;
-        uint64_t round = 0;
-    } cs;
 };
 
 namespace {
@@ -265,29 +237,6 @@ int fail(psim_handle* h, int code, const char* fmt, ...) {
         if (e_ != hipSuccess)                                                            \
             return fail((h), PSIM_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));     \
     } while (0)
-
-constexpr uint32_t kHvChunk = 16;   // HyParView rounds between host synchronisations
-
-void free_hv(psim_handle* h) {
-    auto& v = h->hv;
-    void* ptrs[] = {v.head, v.act, v.pas, v.skey, v.sval, v.rkey, v.rval, v.alive, v.msg[0], v.msg[1], v.nmsg,
-                    v.cnt, v.cur, v.off, v.idx, v.bsum, v.joinbuf, v.stats, v.idx2};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-    if (v.h_stats) (void)hipHostFree(v.h_stats);
-    for (auto& e : v.ev)
-        if (e) (void)hipEventDestroy(e);
-    h->hv = psim_handle::Hv();
-}
-
-void free_cs(psim_handle* h) {
-    auto& c = h->cs;
-    void* ptrs[] = {c.clk, c.self, c.buf, c.nbuf, c.base, c.delivered, c.stats};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-    if (c.h_stats) (void)hipHostFree(c.h_stats);
-    h->cs = psim_handle::Cs();
-}
 
 void swap_lane(psim_handle* h, int j);
 void save_lane(psim_handle* h);
@@ -1219,8 +1168,6 @@ int psim_destroy(psim_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
     free_graph(h);
-    free_hv(h);
-    free_cs(h);
     for (auto& m : h->mods) {
         delete m;
         m = nullptr;
@@ -2924,485 +2871,4 @@ int psim_get_frontier(const psim_handle* h, uint64_t* rounds, uint64_t* launches
 
 }  // extern "C"
 
-namespace {
 
-HvArgs make_hv_args(const psim_handle* h, uint32_t par, unsigned long long* stats) {
-    const auto& v = h->hv;
-    HvArgs a{};
-    a.n = v.n;
-    a.cfg = HvCfg{v.cfg.active_max_size, v.cfg.active_min_size, v.cfg.active_rwl, v.cfg.passive_max_size,
-                  v.cfg.passive_rwl, v.cfg.shuffle_k_active, v.cfg.shuffle_k_passive};
-    a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
-    a.alive = v.alive;
-    a.head = v.head;
-    a.act = v.act;
-    a.pas = v.pas;
-    a.skey = v.skey;
-    a.sval = v.sval;
-    a.rkey = v.rkey;
-    a.rval = v.rval;
-    a.map_mask = v.map_cap - 1;
-    a.in = v.msg[par];
-    a.nin = v.nmsg + par;
-    a.out = v.msg[par ^ 1];
-    a.nout = v.nmsg + (par ^ 1);
-    a.out_cap = v.cap;
-    a.cnt = v.cnt;
-    a.cur = v.cur;
-    a.off = v.off;
-    a.idx = v.idx;
-    a.idx2 = v.idx2;
-    a.bsum = v.bsum;
-    a.stats = stats;
-    return a;
-}
-
-int hv_check_err(psim_handle* h, unsigned long long e, uint64_t round) {
-    if (e & 1ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: message queue over %u records",
-                              (unsigned long long)round, h->hv.cap);
-    if (e & 2ull) return fail(h, PSIM_EOVERFLOW, "hyparview round %llu: id-map table (%u slots) too full",
-                              (unsigned long long)round, h->hv.map_cap);
-    if (e & 16ull) return fail(h, PSIM_ESTATE, "hyparview round %llu: a view held a non-vertex id (engine bug)",
-                               (unsigned long long)round);
-    return PSIM_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int psim_hv_setup(psim_handle* h, uint32_t n, const psim_hv_config* cfg) {
-    if (!h || !cfg || n < 1) return PSIM_EINVAL;
-    if (cfg->active_max_size < 2 || cfg->active_max_size > 8 || cfg->passive_max_size < 1 ||
-        cfg->passive_max_size > 32 || cfg->active_rwl > 255 || cfg->passive_rwl > 255 ||
-        cfg->shuffle_k_active + cfg->shuffle_k_passive > kHvX - 1)
-        return fail(h, PSIM_EINVAL, "hyparview config out of range (active <= 8, passive <= 32, k_a + k_p <= 7)");
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    free_hv(h);
-    auto& v = h->hv;
-    const size_t N = n;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(8ull * n + 4096, 0xFFFFFFF0ull);
-    const uint32_t nb = (n + kBlock - 1) / kBlock;
-    uint32_t mcap = 1u << 16;                  // id-map tables: >= 16 rows per vertex, power of two
-    while (mcap < 16ull * n && mcap < (1u << 31)) mcap <<= 1;
-    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
-    bool ok = A((void**)&v.head, N * sizeof(HvHead)) && A((void**)&v.act, N * 32) && A((void**)&v.pas, N * 128) &&
-              A((void**)&v.skey, size_t(mcap) * 8) && A((void**)&v.sval, size_t(mcap) * 8) &&
-              A((void**)&v.rkey, size_t(mcap) * 8) && A((void**)&v.rval, size_t(mcap) * 8) &&
-              A((void**)&v.alive, ((N + 31) / 32) * 4) && A((void**)&v.msg[0], size_t(cap) * sizeof(HvMsg)) &&
-              A((void**)&v.msg[1], size_t(cap) * sizeof(HvMsg)) && A((void**)&v.nmsg, 16) &&
-              A((void**)&v.cnt, N * 4) && A((void**)&v.cur, N * 4) && A((void**)&v.off, (N + 1) * 4) &&
-              A((void**)&v.idx, size_t(cap) * 4) && A((void**)&v.idx2, size_t(cap) * 4) &&
-              A((void**)&v.bsum, size_t(nb) * 4) &&
-              A((void**)&v.joinbuf, 2 * N * 4) && A((void**)&v.stats, kHvChunk * kHvNStat * 8) &&
-              hipHostMalloc((void**)&v.h_stats, kHvChunk * kHvNStat * 8, 0) == hipSuccess;
-    for (auto& e : v.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-    if (!ok) {
-        free_hv(h);
-        return fail(h, PSIM_ENOMEM, "hyparview state for n=%u", n);
-    }
-    v.n = n;
-    v.cap = cap;
-    v.map_cap = mcap;
-    v.cfg = *cfg;
-    HIPCHK(h, hipMemsetAsync(v.skey, 0xFF, size_t(mcap) * 8, h->stream));
-    HIPCHK(h, hipMemsetAsync(v.rkey, 0xFF, size_t(mcap) * 8, h->stream));
-    HIPCHK(h, hipMemsetAsync(v.alive, 0xFF, ((N + 31) / 32) * 4, h->stream));
-    HIPCHK(h, launch_hv_init(make_hv_args(h, 0, v.stats), h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return PSIM_OK;
-}
-
-int psim_hv_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
-    if (!h || !alive) return PSIM_EINVAL;
-    if (!h->hv.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
-    if (n != h->hv.n) return fail(h, PSIM_EINVAL, "alive has %zu entries, cluster has %u", n, h->hv.n);
-    std::vector<uint32_t> bm((n + 31) / 32, 0);
-    for (size_t i = 0; i < n; i++)
-        if (alive[i]) bm[i >> 5] |= 1u << (i & 31);
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMemcpyAsync(h->hv.alive, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return PSIM_OK;
-}
-
-int psim_hv_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k) {
-    if (!h || (k && (!v || !contact))) return PSIM_EINVAL;
-    auto& hv = h->hv;
-    if (!hv.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
-    if (k > hv.n) return fail(h, PSIM_EINVAL, "%zu joins for %u vertices", k, hv.n);
-    std::vector<uint8_t> seen(hv.n, 0);
-    for (size_t i = 0; i < k; i++) {
-        if (v[i] >= hv.n || contact[i] >= hv.n) return fail(h, PSIM_EINVAL, "join %zu: vertex out of range", i);
-        if (seen[v[i]]) return fail(h, PSIM_EINVAL, "join %zu: vertex %u joins twice in one batch", i, v[i]);
-        seen[v[i]] = 1;
-    }
-    if (!k) return PSIM_OK;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMemcpyAsync(hv.joinbuf, v, k * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(hv.joinbuf + hv.n, contact, k * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemsetAsync(hv.stats, 0, kHvNStat * 8, h->stream));
-    // the join messages go to the queue the next round reads
-    HvArgs a = make_hv_args(h, hv.par ^ 1u, hv.stats);
-    HIPCHK(h, launch_hv_join(a, hv.joinbuf, hv.joinbuf + hv.n, (uint32_t)k, h->stream));
-    HIPCHK(h, hipMemcpyAsync(hv.h_stats, hv.stats, kHvNStat * 8, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return hv_check_err(h, hv.h_stats[11], hv.round);
-}
-
-int psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* out, size_t cap) {
-    if (!h) return PSIM_EINVAL;
-    auto& v = h->hv;
-    if (!v.n) return fail(h, PSIM_ESTATE, "psim_hv_setup not called");
-    HIPCHK(h, hipSetDevice(h->device));
-    uint32_t done = 0;
-    while (done < rounds) {
-        const uint32_t k = std::min(kHvChunk, rounds - done);
-        HIPCHK(h, hipMemsetAsync(v.stats, 0, size_t(k) * kHvNStat * 8, h->stream));
-        for (uint32_t i = 0; i < k; i++) {
-            HvArgs a = make_hv_args(h, v.par, v.stats + size_t(i) * kHvNStat);
-            const uint64_t t = v.round + i + 1;   // 1-based round; timers fire at its end
-            a.timers = (v.cfg.promotion_rounds && t % v.cfg.promotion_rounds == 0 ? 1u : 0u) |
-                       (v.cfg.shuffle_rounds && t % v.cfg.shuffle_rounds == 0 ? 2u : 0u);
-            HIPCHK(h, hipMemsetAsync(v.nmsg + (v.par ^ 1u), 0, 4, h->stream));
-            HIPCHK(h, hipEventRecord(v.ev[2 * i], h->stream));
-            HIPCHK(h, launch_hv_round(a, h->stream));
-            HIPCHK(h, hipEventRecord(v.ev[2 * i + 1], h->stream));
-            v.par ^= 1u;
-        }
-        HIPCHK(h, hipMemcpyAsync(v.h_stats, v.stats, size_t(k) * kHvNStat * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        for (uint32_t i = 0; i < k; i++) {
-            const unsigned long long* r = v.h_stats + size_t(i) * kHvNStat;
-            const uint64_t t = v.round + i + 1;
-            int rc = hv_check_err(h, r[11], t);
-            if (rc != PSIM_OK) { v.round += k; return rc; }
-            float ms = 0.f;
-            HIPCHK(h, hipEventElapsedTime(&ms, v.ev[2 * i], v.ev[2 * i + 1]));
-            h->kernel_ms_total += ms;
-            h->rounds_total++;
-            const size_t j = done + i;
-            if (out && j < cap) {
-                psim_hv_stats& o = out[j];
-                memset(&o, 0, sizeof o);
-                uint64_t emitted = 0;
-                for (int q = 1; q < 10; q++) { o.sent[q] = r[q]; emitted += r[q]; }
-                o.draws = r[10];
-                o.error = r[11];
-                o.processed = r[12];
-                o.active = r[13];
-                o.algo_bytes = 64ull * (r[12] + emitted) + 2ull * 176ull * r[13] + 12ull * v.n;
-                o.kernel_ms = ms;
-            }
-        }
-        v.round += k;
-        done += k;
-    }
-    return PSIM_OK;
-}
-
-int psim_hv_get_views(const psim_handle* h, uint32_t* act, uint8_t* na, uint32_t* pas, uint8_t* np, size_t n) {
-    if (!h || n != h->hv.n || !n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    const auto& v = h->hv;
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    if (act) HIPCHK(hh, hipMemcpy(act, v.act, n * 32, hipMemcpyDeviceToHost));
-    if (pas) HIPCHK(hh, hipMemcpy(pas, v.pas, n * 128, hipMemcpyDeviceToHost));
-    if (na || np) {
-        std::vector<HvHead> hd(n);
-        HIPCHK(hh, hipMemcpy(hd.data(), v.head, n * sizeof(HvHead), hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < n; i++) {
-            if (na) na[i] = hd[i].na;
-            if (np) np[i] = hd[i].np;
-        }
-    }
-    return PSIM_OK;
-}
-
-int psim_hv_get_draws(const psim_handle* h, uint64_t* draws, size_t n) {
-    if (!h || !draws || n != h->hv.n || !n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    std::vector<HvHead> hd(n);
-    HIPCHK(hh, hipMemcpy(hd.data(), h->hv.head, n * sizeof(HvHead), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < n; i++) draws[i] = hd[i].draws;
-    return PSIM_OK;
-}
-
-int psim_hv_get_idmap(const psim_handle* h, uint32_t v, int which, uint32_t* peer, uint32_t* epoch, uint32_t* cnt,
-                      size_t cap, size_t* len) {
-    if (!h || !len || v >= h->hv.n || (which != 0 && which != 1)) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    HvHead hd;
-    HIPCHK(hh, hipMemcpy(&hd, h->hv.head + v, sizeof hd, hipMemcpyDeviceToHost));
-    const uint32_t m = which ? hd.nrecv : hd.nsent;
-    const size_t M = h->hv.map_cap;
-    std::vector<unsigned long long> keys(M);
-    std::vector<uint2> vals(M);
-    HIPCHK(hh, hipMemcpy(keys.data(), which ? h->hv.rkey : h->hv.skey, M * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hh, hipMemcpy(vals.data(), which ? h->hv.rval : h->hv.sval, M * 8, hipMemcpyDeviceToHost));
-    size_t k = 0;
-    for (size_t i = 0; i < M; i++) {
-        if (keys[i] == ~0ull || (uint32_t)(keys[i] >> 32) != v) continue;
-        if (k < cap) {
-            if (peer) peer[k] = (uint32_t)keys[i];
-            if (epoch) epoch[k] = vals[i].x;
-            if (cnt) cnt[k] = vals[i].y;
-        }
-        k++;
-    }
-    if (k != m) return fail(hh, PSIM_ESTATE, "id map of %u: %zu rows in the table, head says %u", v, k, m);
-    *len = m;
-    return PSIM_OK;
-}
-
-int psim_hv_inflight(const psim_handle* h, uint64_t* messages) {
-    if (!h || !messages || !h->hv.n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    uint32_t c = 0;
-    HIPCHK(hh, hipMemcpy(&c, h->hv.nmsg + h->hv.par, 4, hipMemcpyDeviceToHost));
-    *messages = c;
-    return PSIM_OK;
-}
-
-}  // extern "C"
-
-namespace {
-
-CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
-    const auto& c = h->cs;
-    CsArgs a{};
-    a.n = c.n;
-    a.m = c.m;
-    a.period = c.period;
-    a.dmax = c.dmax;
-    a.redeliver = c.redeliver;
-    a.v_lo = c.v_lo;
-    a.n_global = c.n_global;
-    a.key = make_uint2((uint32_t)h->cfg.seed, (uint32_t)(h->cfg.seed >> 32));
-    a.t = t;
-    a.clk = c.clk;
-    a.self = c.self;
-    a.buf = c.buf;
-    a.nbuf = c.nbuf;
-    a.delivered = c.delivered;
-    a.base = c.base;
-    a.stats = c.stats;
-    return a;
-}
-
-}  // namespace
-
-extern "C" {
-
-int psim_causal_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax, uint32_t redeliver) {
-    return psim_causal_shard_setup(h, n, m, period, dmax, redeliver, 0, 1);
-}
-
-int psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t period, uint32_t dmax,
-                            uint32_t redeliver, int rank, int world) {
-    if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
-    if (n < 2 || m < 1 || m > kCsLanes || m > n || period < 1 || dmax < 1 || dmax > 30 ||
-        dmax + 2 * redeliver + period + 2 >= kCsWindow)
-        return fail(h, PSIM_EINVAL, "causal: need 2 <= n, 1 <= m <= min(64, n), period >= 1, 1 <= dmax <= 30, "
-                                    "dmax + 2 redeliver + period + 2 < %u", kCsWindow);
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    free_cs(h);
-    auto& c = h->cs;
-    const uint32_t lo = uint32_t((uint64_t(n) * rank) / world), hi = uint32_t((uint64_t(n) * (rank + 1)) / world);
-    const size_t N = std::max<uint32_t>(hi - lo, 1);
-    auto A = [&](void** p, size_t bytes) { return alloc_zero(p, bytes); };
-    const bool ok = A((void**)&c.clk, N * kCsLanes * 4) && A((void**)&c.self, N * 4) &&
-                    A((void**)&c.buf, N * kCsBufCap * 4) && A((void**)&c.nbuf, N * 4) &&
-                    A((void**)&c.base, size_t(kCsWindow) * kCsLanes * kCsLanes * 4) &&
-                    A((void**)&c.delivered, N * 8) && A((void**)&c.stats, kStatShards * kCsNStat * 8) &&
-                    hipHostMalloc((void**)&c.h_stats, kStatShards * kCsNStat * 8, 0) == hipSuccess;
-    if (!ok) {
-        free_cs(h);
-        return fail(h, PSIM_ENOMEM, "causal state for n=%u", n);
-    }
-    c.n = hi - lo;
-    c.n_global = n;
-    c.v_lo = lo;
-    c.rank = (uint32_t)rank;
-    c.world = (uint32_t)world;
-    c.m = m;
-    c.period = period;
-    c.dmax = dmax;
-    c.redeliver = redeliver;
-    return PSIM_OK;
-}
-
-int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, size_t cap) {
-    if (!h) return PSIM_EINVAL;
-    auto& c = h->cs;
-    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_setup not called");
-    if (c.world > 1) return fail(h, PSIM_ESTATE, "sharded causal handle: use psim_causal_shard_round");
-    HIPCHK(h, hipSetDevice(h->device));
-    for (uint32_t i = 0; i < rounds; i++) {
-        const uint64_t t = c.round + 1;
-        if (t >= (1u << 24)) return fail(h, PSIM_EOVERFLOW, "causal: round %llu exceeds 2^24", (unsigned long long)t);
-        CsArgs a = make_cs_args(h, (uint32_t)t);
-        HIPCHK(h, hipMemsetAsync(c.stats, 0, kStatShards * kCsNStat * 8, h->stream));
-        HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
-        HIPCHK(h, launch_cs_round(a, h->stream));
-        HIPCHK(h, launch_cs_broadcast(a, h->stream));
-        HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
-        HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        c.round = t;
-        unsigned long long r[kCsNStat] = {0};
-        unsigned long long err = 0;
-        for (int sh = 0; sh < kStatShards; sh++)
-            for (int q = 0; q < kCsNStat; q++) {
-                if (q == 5) err |= c.h_stats[sh * kCsNStat + q];
-                else r[q] += c.h_stats[sh * kCsNStat + q];
-            }
-        if (err & 1ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
-                                    (unsigned long long)t, kCsBufCap);
-        if (err & 2ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
-                                    "clock window", (unsigned long long)t, kCsWindow);
-        if (err & 4ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a u32 clock entry overflowed",
-                                    (unsigned long long)t);
-        float ms = 0.f;
-        HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-        h->kernel_ms_total += ms;
-        h->rounds_total++;
-        if (out && i < cap) {
-            psim_causal_stats& o = out[i];
-            memset(&o, 0, sizeof o);
-            o.emitted = r[6];
-            o.received = r[1];
-            o.delivered = r[2];
-            o.checks = r[3];
-            o.buffered = r[4];
-            o.algo_bytes = 1024ull * r[2] + 256ull * r[3] + 32ull * r[1];
-            o.kernel_ms = ms;
-        }
-    }
-    return PSIM_OK;
-}
-
-// Split-phase sharded round: the local round and the broadcasts of this
-// shard's emitters; their base-clock rows go to the caller's `slab`
-// (64 x 64 u32, zero elsewhere) to be sum-all-reduced, then
-// psim_causal_shard_ingest installs the reduced slab for every receiver.
-int psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* out) {
-    if (!h || !slab) return PSIM_EINVAL;
-    auto& c = h->cs;
-    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_shard_setup not called");
-    HIPCHK(h, hipSetDevice(h->device));
-    const uint64_t t = c.round + 1;
-    if (t >= (1u << 24)) return fail(h, PSIM_EOVERFLOW, "causal: round %llu exceeds 2^24", (unsigned long long)t);
-    CsArgs a = make_cs_args(h, (uint32_t)t);
-    uint32_t* sl = c.base + size_t(t % kCsWindow) * kCsLanes * kCsLanes;
-    HIPCHK(h, hipMemsetAsync(c.stats, 0, kStatShards * kCsNStat * 8, h->stream));
-    HIPCHK(h, hipEventRecord(h->ev[0], h->stream));
-    if (c.n) HIPCHK(h, launch_cs_round(a, h->stream));
-    HIPCHK(h, hipMemsetAsync(sl, 0, kCsLanes * kCsLanes * 4, h->stream));
-    HIPCHK(h, launch_cs_broadcast(a, h->stream));
-    HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
-    HIPCHK(h, hipMemcpyAsync(slab, sl, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    c.round = t;
-    unsigned long long r[kCsNStat] = {0};
-    unsigned long long err = 0;
-    for (int sh = 0; sh < kStatShards; sh++)
-        for (int q = 0; q < kCsNStat; q++) {
-            if (q == 5) err |= c.h_stats[sh * kCsNStat + q];
-            else r[q] += c.h_stats[sh * kCsNStat + q];
-        }
-    if (err & 1ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
-                                (unsigned long long)t, kCsBufCap);
-    if (err & 2ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
-                                "clock window", (unsigned long long)t, kCsWindow);
-    if (err & 4ull) return fail(h, PSIM_EOVERFLOW, "causal round %llu: a u32 clock entry overflowed",
-                                (unsigned long long)t);
-    float ms = 0.f;
-    HIPCHK(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-    h->kernel_ms_total += ms;
-    h->rounds_total++;
-    if (out) {
-        memset(out, 0, sizeof *out);
-        out->emitted = r[6];
-        out->received = r[1];
-        out->delivered = r[2];
-        out->checks = r[3];
-        out->buffered = r[4];
-        out->algo_bytes = 1024ull * r[2] + 256ull * r[3] + 32ull * r[1];
-        out->kernel_ms = ms;
-    }
-    return PSIM_OK;
-}
-
-int psim_causal_shard_ingest(psim_handle* h, const void* slab) {
-    if (!h || !slab) return PSIM_EINVAL;
-    auto& c = h->cs;
-    if (!c.n_global) return fail(h, PSIM_ESTATE, "psim_causal_shard_setup not called");
-    HIPCHK(h, hipSetDevice(h->device));
-    uint32_t* sl = c.base + size_t(c.round % kCsWindow) * kCsLanes * kCsLanes;
-    HIPCHK(h, hipMemcpyAsync(sl, slab, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return PSIM_OK;
-}
-
-int psim_causal_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local) {
-    if (!h) return PSIM_EINVAL;
-    if (v_lo) *v_lo = h->cs.v_lo;
-    if (n_local) *n_local = h->cs.n;
-    return PSIM_OK;
-}
-
-int psim_causal_get_clocks(const psim_handle* h, uint32_t* lanes, uint32_t* self, size_t n) {
-    if (!h || n != h->cs.n || !n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    if (lanes) HIPCHK(hh, hipMemcpy(lanes, h->cs.clk, n * kCsLanes * 4, hipMemcpyDeviceToHost));
-    if (self) HIPCHK(hh, hipMemcpy(self, h->cs.self, n * 4, hipMemcpyDeviceToHost));
-    return PSIM_OK;
-}
-
-int psim_causal_get_buffered(const psim_handle* h, uint32_t v, uint32_t* k, uint32_t* round, size_t cap,
-                             size_t* len) {
-    if (!h || !len || v >= h->cs.n) return PSIM_EINVAL;   // v: index in this shard's range
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    uint32_t nb = 0;
-    HIPCHK(hh, hipMemcpy(&nb, h->cs.nbuf + v, 4, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> e(nb);
-    if (nb) HIPCHK(hh, hipMemcpy(e.data(), h->cs.buf + size_t(v) * kCsBufCap, nb * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < nb && i < cap; i++) {
-        if (k) k[i] = e[i] >> 24;
-        if (round) round[i] = e[i] & 0xFFFFFFu;
-    }
-    *len = nb;
-    return PSIM_OK;
-}
-
-int psim_causal_get_delivered(const psim_handle* h, uint64_t* delivered, size_t n) {
-    if (!h || !delivered || n != h->cs.n || !n) return PSIM_EINVAL;
-    psim_handle* hh = const_cast<psim_handle*>(h);
-    HIPCHK(hh, hipSetDevice(h->device));
-    HIPCHK(hh, hipStreamSynchronize(h->stream));
-    HIPCHK(hh, hipMemcpy(delivered, h->cs.delivered, n * 8, hipMemcpyDeviceToHost));
-    return PSIM_OK;
-}
-
-int psim_causal_emitters(const psim_handle* h, uint32_t* emitters, size_t m) {
-    if (!h || !emitters || m != h->cs.m || !m) return PSIM_EINVAL;
-    for (size_t k = 0; k < m; k++) emitters[k] = (uint32_t)((uint64_t(k) * h->cs.n_global) / h->cs.m);
-    return PSIM_OK;
-}
-
-}  // extern "C"

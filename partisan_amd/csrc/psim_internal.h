@@ -545,7 +545,8 @@ struct ModuleState {
     virtual ~ModuleState() {}
 };
 enum ModuleSlot : int {
-    MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_RELAY = 4, MOD_DEMERS = 5, MOD_COUNT = 6
+    MOD_FULLMEM = 0, MOD_SCAMP = 1, MOD_DMSHARD = 2, MOD_PTDYN = 3, MOD_RELAY = 4, MOD_DEMERS = 5, MOD_HV = 6,
+    MOD_CAUSAL = 7, MOD_COUNT = 8
 };
 ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);

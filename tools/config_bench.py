@@ -81,6 +81,7 @@ def c5(n=1_000_000, m=64, rounds=16):
     gbs = b / 1e6 / ms
     line("C5", n=n, emitters=m, rounds=rounds, ms_per_round=round(ms / len(last), 4),
          deliveries_per_round=sum(s["delivered"] for s in last) / len(last),
+         checks_per_round=sum(s["checks"] for s in last) / len(last), buffered_end=int(last[-1]["buffered"]),
          deliveries_per_s=sum(s["delivered"] for s in last) / (ms / 1e3),
          algo_GBps=round(gbs, 1), hbm_frac=round(gbs / HBM, 4))
     sim.close()
