@@ -35,50 +35,122 @@ __device__ __forceinline__ uint32_t delay_of(uint2 key, uint32_t v, uint32_t r, 
     return 1u + (uint32_t)__umul64hi((unsigned long long)x.x | ((unsigned long long)x.y << 32), dmax);
 }
 
+// Watch of a buffered entry: the cheapest condition that must change before
+// its dependency check can pass again.  A failed `dominates` leaves either a
+// lane j with Local[j] < Dep[j] (recheck once Local[j] >= Dep[j]: the clock
+// only grows) or Local == Dep (recheck after the next delivery, the only thing
+// that changes the clock).  Entries loaded at the start of a round are
+// unchecked.  A fold visits every entry in list order exactly as
+// lists:foldl does; an entry whose watch still holds is not deliverable, so
+// skipping its full check changes nothing but the work (it still counts as
+// one dependency check).
+constexpr uint32_t kWatchAny = 64;      // Local == Dep: recheck after a delivery
+constexpr uint32_t kWatchNone = 65;     // not checked this round
+
 struct Wave {
     const CsArgs* a;
     uint32_t v, lane, c, self, nb;
+    uint32_t eid;                       // lane k: emitter_id(k)
     int ke;
-    uint32_t* sbuf;
+    uint32_t* sbuf;                     // entries (k << 24 | round), list order
+    uint32_t* wj;                       // watch lane / kWatchAny / kWatchNone
+    uint32_t* wx;                       // watch value (clock entry or delivery count)
     uint32_t received, delivered, checks, err;
 };
 
-// internal_receive_message/2 (:309-344) + deliver/5 (:265-300) for (k, r)
-__device__ bool try_deliver(Wave& w, uint32_t k, uint32_t r) {
+// the clocks entry (k, r) is checked against, at this lane: the message's
+// (ml) and its order-buffer dependency's (dl, only used when r > period)
+struct Clocks { uint32_t ml, dl; };
+__device__ __forceinline__ Clocks load_clocks(const Wave& w, uint32_t k, uint32_t r) {
     const CsArgs& a = *w.a;
-    if (a.t - r >= kCsWindow - 1 || (r > a.period && a.t - (r - a.period) >= kCsWindow - 1)) w.err |= 2u;
-    const uint32_t e = emitter_id(k, a.n_global, a.m);
-    const uint32_t rank = w.v - (w.v > e ? 1u : 0u);
-    if (r > a.period) {                                   // orddict:find(MyNode, IncomingOrderBuffer) -> {ok, Dep}
-        uint32_t dl = a.base[((r - a.period) % kCsWindow) * kCsLanes * kCsLanes + k * kCsLanes + w.lane];
-        if (w.lane == k) dl += rank + 1u;
-        w.checks++;
-        // dominates(Local, Dep) = descends(Local, Dep) andalso not descends(Dep, Local)
-        const bool d1 = __ballot(!(dl == 0u || w.c >= dl)) == 0ull;
-        const bool d2 = __ballot(!(w.c == 0u || dl >= w.c)) == 0ull && w.self == 0u;
-        if (!(d1 && !d2)) return false;
-    }
-    uint32_t ml = a.base[(r % kCsWindow) * kCsLanes * kCsLanes + k * kCsLanes + w.lane];
-    if (w.lane == k) ml += rank + 1u;
-    w.c = max(w.c, ml);                                   // merge([LocalClock, MessageClock])
-    if (w.ke >= 0) { if (w.lane == (uint32_t)w.ke) w.c += 1u; }   // increment(MyNode, ...)
-    else w.self += 1u;
-    w.delivered++;
-    return true;
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)w.eid, (int)k);
+    const uint32_t raise = w.lane == k ? w.v - (w.v > e ? 1u : 0u) + 1u : 0u;
+    const uint32_t* row = a.base + k * kCsLanes + w.lane;
+    Clocks q;
+    q.ml = row[(r % kCsWindow) * kCsLanes * kCsLanes] + raise;
+    q.dl = r > a.period ? row[((r - a.period) % kCsWindow) * kCsLanes * kCsLanes] + raise : 0u;
+    return q;
 }
 
-// one lists:foldl over the buffer snapshot; delivered entries leave the
-// buffer, the others keep their order
-__device__ void fold(Wave& w) {
-    const uint32_t n0 = w.nb;
-    uint32_t keep = 0;
-    for (uint32_t i = 0; i < n0; i++) {
-        const uint32_t e = w.sbuf[i];
-        __builtin_amdgcn_wave_barrier();
-        if (!try_deliver(w, e >> 24, e & 0xFFFFFFu)) {
-            if (w.lane == 0) w.sbuf[keep] = e;
-            keep++;
+// a wave-uniform value, moved to a scalar register (the compiler cannot
+// always prove uniformity through the fold's loops)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// internal_receive_message/2 (:309-344) + deliver/5 (:265-300) for (k, r);
+// on failure (jw, xw) is the entry's new watch
+__device__ bool try_deliver(Wave& w, uint32_t r, const Clocks& q, uint32_t& jw, uint32_t& xw) {
+    const CsArgs& a = *w.a;
+    bool ok = true;
+    if (r > a.period) {                                   // orddict:find(MyNode, IncomingOrderBuffer) -> {ok, Dep}
+        const uint32_t dl = q.dl;
+        w.checks = uni(w.checks + 1u);
+        // dominates(Local, Dep) = descends(Local, Dep) andalso not descends(Dep, Local)
+        const unsigned long long f1 = __ballot(!(dl == 0u || w.c >= dl));
+        const unsigned long long f2 = __ballot(!(w.c == 0u || dl >= w.c));
+        if (f1) {
+            jw = uni((uint32_t)__ffsll((long long)f1) - 1u);
+            xw = uni((uint32_t)__builtin_amdgcn_readlane((int)dl, (int)jw));
+            ok = false;
+        } else if (f2 == 0ull && w.self == 0u) {
+            jw = kWatchAny;
+            xw = w.delivered;
+            ok = false;
         }
+    }
+    if (ok) {
+        w.c = max(w.c, q.ml);                             // merge([LocalClock, MessageClock])
+        if (w.ke >= 0) w.c += w.lane == (uint32_t)w.ke ? 1u : 0u;   // increment(MyNode, ...)
+        else w.self = uni(w.self + 1u);
+        w.delivered = uni(w.delivered + 1u);
+    }
+    return ok;
+}
+
+// one lists:foldl over the buffer snapshot, 64 entries per pass of the
+// wave (lane l holds entry 64 s + l); delivered entries leave the buffer,
+// the others keep their order
+__device__ void fold(Wave& w) {
+    const CsArgs& a = *w.a;
+    const uint32_t n0 = uni(w.nb);
+    uint32_t keep = 0;
+    for (uint32_t s0 = 0; s0 < n0; s0 = uni(s0 + 64u)) {
+        const uint32_t i = s0 + w.lane;
+        const bool valid = i < n0;
+        uint32_t ent = 0, jw = kWatchNone, xw = 0;
+        if (valid) { ent = w.sbuf[i]; jw = w.wj[i]; xw = w.wx[i]; }
+        const uint32_t r0 = ent & 0xFFFFFFu;
+        const bool old = (a.t - r0 >= kCsWindow - 1) | ((r0 > a.period) & (a.t - (r0 - a.period) >= kCsWindow - 1));
+        if (__ballot(valid & old)) w.err = uni(w.err | 2u);
+        const unsigned long long vmask = __ballot(valid);
+        unsigned long long gone = 0, seen = 0;
+        uint32_t from = 0;                                // first lane not yet visited
+        for (;;) {
+            const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(jw & 63u), 64);
+            const bool cand = (jw == kWatchNone) | ((jw == kWatchAny) & (w.delivered > xw)) | ((jw < 64u) & (cj >= xw));
+            const unsigned long long m = __ballot(valid & cand) & (~0ull << from);
+            if (!m) break;
+            const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
+            const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)ent, (int)l));
+            uint32_t nj = 0, nx = 0;
+            seen |= 1ull << l;
+            const Clocks q = load_clocks(w, e >> 24, e & 0xFFFFFFu);
+            if (try_deliver(w, e & 0xFFFFFFu, q, nj, nx)) gone |= 1ull << l;
+            else {
+                jw = w.lane == l ? nj : jw;
+                xw = w.lane == l ? nx : xw;
+            }
+            if (l == 63u) break;
+            from = l + 1u;
+        }
+        w.checks = uni(w.checks + (uint32_t)__popcll(vmask & ~seen));   // watched entries: checks that cannot pass
+        const unsigned long long kept = vmask & ~gone;
+        if ((kept >> w.lane) & 1ull) {
+            const uint32_t o = keep + (uint32_t)__popcll(kept & ((1ull << w.lane) - 1ull));
+            w.sbuf[o] = ent;
+            w.wj[o] = jw;
+            w.wx[o] = xw;
+        }
+        keep = uni(keep + (uint32_t)__popcll(kept));
         __builtin_amdgcn_wave_barrier();
     }
     w.nb = keep;
@@ -86,8 +158,12 @@ __device__ void fold(Wave& w) {
 
 __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
     __shared__ uint32_t sbuf[kWavesPerBlock][kCsBufCap];
+    __shared__ uint32_t wj[kWavesPerBlock][kCsBufCap];
+    __shared__ uint32_t wx[kWavesPerBlock][kCsBufCap];
     __shared__ unsigned long long red[kWavesPerBlock][4];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave-uniform values are read into scalar registers explicitly, so the
+    // fold's control flow stays scalar (no exec-mask bookkeeping)
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const uint32_t lv = blockIdx.x * kWavesPerBlock + wv;
     Wave w;
     w.received = w.delivered = w.checks = w.err = 0;
@@ -97,31 +173,41 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         w.v = a.v_lo + lv;
         w.lane = lane;
         w.sbuf = sbuf[wv];
+        w.wj = wj[wv];
+        w.wx = wx[wv];
         w.c = a.clk[(size_t)lv * kCsLanes + lane];
-        w.self = a.self[lv];
+        w.self = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.self[lv]);
+        w.eid = lane < a.m ? emitter_id(lane, a.n_global, a.m) : 0xFFFFFFFFu;
         w.ke = emitter_index(w.v, a.n_global, a.m);
-        w.nb = a.nbuf[lv];
-        for (uint32_t i = lane; i < w.nb; i += 64) w.sbuf[i] = a.buf[(size_t)lv * kCsBufCap + i];
+        w.nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.nbuf[lv]);
+        for (uint32_t i = lane; i < w.nb; i += 64) {
+            w.sbuf[i] = a.buf[(size_t)lv * kCsBufCap + i];
+            w.wj[i] = kWatchNone;
+        }
         __builtin_amdgcn_wave_barrier();
         // arrivals of round t: lane k marks bit d if k's round-(t-d) message lands now
         uint32_t am = 0;
-        if (lane < a.m && emitter_id(lane, a.n_global, a.m) != w.v)
+        if (lane < a.m && w.eid != w.v) {
+            const uint32_t ph = lane % a.period;
             for (uint32_t d = 1; d <= a.dmax && d < a.t; d++) {
                 const uint32_t r = a.t - d;
-                if (r % a.period == lane % a.period && delay_of(a.key, w.v, r, lane, a.dmax) == d) am |= 1u << d;
+                if (r % a.period == ph && delay_of(a.key, w.v, r, lane, a.dmax) == d) am |= 1u << d;
             }
+        }
         // receive_message (:205-220) in (src, seq) order: emitter id, then oldest round first
         for (;;) {
             const unsigned long long any = __ballot(am != 0u);
             if (!any) break;
-            const uint32_t k = (uint32_t)__ffsll((long long)any) - 1u;
-            const uint32_t mk = __shfl(am, (int)k, 64);
-            const uint32_t d = 31u - __clz(mk);
+            const uint32_t k = uni((uint32_t)__ffsll((long long)any) - 1u);
+            const uint32_t d = uni(31u - __clz(__shfl(am, (int)k, 64)));
             if (lane == k) am &= ~(1u << d);
-            w.received++;
-            if (w.nb >= kCsBufCap) { w.err |= 1u; continue; }
-            if (lane == 0) w.sbuf[w.nb] = (k << 24) | (a.t - d);
-            w.nb++;
+            w.received = uni(w.received + 1u);
+            if (w.nb >= kCsBufCap) { w.err = uni(w.err | 1u); continue; }
+            if (lane == 0) {
+                w.sbuf[w.nb] = (k << 24) | (a.t - d);
+                w.wj[w.nb] = kWatchNone;
+            }
+            w.nb = uni(w.nb + 1u);
             __builtin_amdgcn_wave_barrier();
             fold(w);
         }

@@ -9,6 +9,9 @@ import partisan_amd as pa  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 sim = pa.Simulator(seed=0x5EED0005)
 g = pa.causal.CausalCluster(sim, n, m=64, period=1, dmax=4, redeliver=1)
-st = g.step(8)
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+st = g.step(rounds)
 print({k: st[-1][k] for k in ("received", "delivered", "checks", "buffered", "kernel_ms")})
+ms = [s["kernel_ms"] for s in st[4:]]
+print("kernel ms per round, rounds 5..%d: mean %.3f min %.3f max %.3f" % (rounds, sum(ms) / len(ms), min(ms), max(ms)))
 sim.close()
