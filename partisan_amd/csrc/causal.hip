@@ -55,6 +55,11 @@ struct Wave {
     uint32_t* sbuf;                     // entries (k << 24 | round), list order
     uint32_t* wj;                       // watch lane / kWatchAny / kWatchNone
     uint32_t* wx;                       // watch value (clock entry or delivery count)
+    // while nb <= 64 the buffer lives in registers, entry l at lane l
+    uint32_t rent, rjw, rxw;
+    unsigned long long pend;            // register entries whose watch no longer holds
+    uint32_t inreg;                     // 1 while the buffer is in registers
+    bool old_any;                       // a loaded entry is older than the clock window
     uint32_t received, delivered, checks, err;
 };
 
@@ -106,44 +111,110 @@ __device__ bool try_deliver(Wave& w, uint32_t r, const Clocks& q, uint32_t& jw, 
     return ok;
 }
 
-// one lists:foldl over the buffer snapshot, 64 entries per pass of the
-// wave (lane l holds entry 64 s + l); delivered entries leave the buffer,
-// the others keep their order
+// the fold over one 64-entry slice (lane l holds the slice's entry l; lanes
+// outside `vmask` hold none): every entry in list order, full dependency
+// checks only where the watch no longer holds; returns the delivered lanes
+__device__ unsigned long long fold_slice(Wave& w, uint32_t ent, uint32_t& jw, uint32_t& xw,
+                                         unsigned long long vmask) {
+    const bool valid = (vmask >> w.lane) & 1ull;
+    unsigned long long gone = 0, seen = 0;
+    uint32_t from = 0;                                    // first lane not yet visited
+    for (;;) {
+        const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(jw & 63u), 64);
+        const bool cand = (jw == kWatchNone) | ((jw == kWatchAny) & (w.delivered > xw)) | ((jw < 64u) & (cj >= xw));
+        const unsigned long long m = __ballot(valid & cand) & (~0ull << from);
+        if (!m) break;
+        const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
+        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)ent, (int)l));
+        uint32_t nj = 0, nx = 0;
+        seen |= 1ull << l;
+        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) gone |= 1ull << l;
+        else {
+            jw = w.lane == l ? nj : jw;
+            xw = w.lane == l ? nx : xw;
+        }
+        if (l == 63u) break;
+        from = l + 1u;
+    }
+    w.checks = uni(w.checks + (uint32_t)__popcll(vmask & ~seen));   // watched entries: checks that cannot pass
+    return gone;
+}
+
+__device__ __forceinline__ unsigned long long first_n(uint32_t n) { return n >= 64u ? ~0ull : (1ull << n) - 1ull; }
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+    return ((unsigned long long)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
+// the register entries whose watch no longer holds (clock or delivery count moved)
+__device__ __forceinline__ unsigned long long pending(const Wave& w) {
+    const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(w.rjw & 63u), 64);
+    const bool cand = (w.rjw == kWatchNone) | ((w.rjw == kWatchAny) & (w.delivered > w.rxw)) |
+                      ((w.rjw < 64u) & (cj >= w.rxw));
+    return uni64(__ballot(cand) & first_n(w.nb));
+}
+
+// the fold over the register entries: only pending entries are checked;
+// the pending set is recomputed after each delivery (the only event that
+// moves the clock), so a fold in which nothing is delivered costs one check
+// per pending entry
+__device__ void fold_reg(Wave& w) {
+    const uint32_t n0 = uni(w.nb);
+    unsigned long long gone = 0;
+    uint32_t tried = 0;
+    unsigned long long m = uni64(w.pend);
+    while (m) {
+        const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
+        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)l));
+        uint32_t nj = 0, nx = 0;
+        tried++;
+        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) {
+            gone |= 1ull << l;
+            w.pend = uni64(pending(w) & ~gone);
+        } else {
+            w.rjw = w.lane == l ? nj : w.rjw;
+            w.rxw = w.lane == l ? nx : w.rxw;
+            w.pend = uni64(w.pend & ~(1ull << l));
+        }
+        if (l == 63u) break;
+        m = uni64(w.pend & (~0ull << (l + 1u)));
+    }
+    w.checks = uni(w.checks + n0 - tried);                // watched entries: checks that cannot pass
+    if (!gone) return;
+    const uint32_t nk = uni(n0 - (uint32_t)__popcll(gone));
+    if (gone != 1ull << (n0 - 1u)) {
+        // compact: kept entries to the front in order, the rest behind them
+        // (a permutation of the 64 lanes, so ds_permute moves every value)
+        const unsigned long long kept = first_n(n0) & ~gone, lt = (1ull << w.lane) - 1ull;
+        const uint32_t o = 4u * ((kept >> w.lane) & 1ull ? (uint32_t)__popcll(kept & lt)
+                                                          : nk + (uint32_t)__popcll(~kept & lt));
+        w.rent = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rent);
+        w.rjw = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rjw);
+        w.rxw = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rxw);
+        const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)((w.pend >> w.lane) & 1ull));
+        w.nb = nk;
+        w.pend = uni64(__ballot(pb != 0u) & first_n(nk));
+    } else {
+        w.nb = nk;                                        // the last entry left: nothing moves
+    }
+}
+
+// one lists:foldl over the buffer snapshot; delivered entries leave the
+// buffer, the others keep their order.  An old entry is visited by every
+// fold, so the window error is raised by the first fold of the round.
 __device__ void fold(Wave& w) {
-    const CsArgs& a = *w.a;
+    if (w.old_any) w.err = uni(w.err | 2u);
+    if (uni(w.inreg)) {
+        fold_reg(w);
+        return;
+    }
     const uint32_t n0 = uni(w.nb);
     uint32_t keep = 0;
     for (uint32_t s0 = 0; s0 < n0; s0 = uni(s0 + 64u)) {
         const uint32_t i = s0 + w.lane;
-        const bool valid = i < n0;
         uint32_t ent = 0, jw = kWatchNone, xw = 0;
-        if (valid) { ent = w.sbuf[i]; jw = w.wj[i]; xw = w.wx[i]; }
-        const uint32_t r0 = ent & 0xFFFFFFu;
-        const bool old = (a.t - r0 >= kCsWindow - 1) | ((r0 > a.period) & (a.t - (r0 - a.period) >= kCsWindow - 1));
-        if (__ballot(valid & old)) w.err = uni(w.err | 2u);
-        const unsigned long long vmask = __ballot(valid);
-        unsigned long long gone = 0, seen = 0;
-        uint32_t from = 0;                                // first lane not yet visited
-        for (;;) {
-            const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(jw & 63u), 64);
-            const bool cand = (jw == kWatchNone) | ((jw == kWatchAny) & (w.delivered > xw)) | ((jw < 64u) & (cj >= xw));
-            const unsigned long long m = __ballot(valid & cand) & (~0ull << from);
-            if (!m) break;
-            const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
-            const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)ent, (int)l));
-            uint32_t nj = 0, nx = 0;
-            seen |= 1ull << l;
-            const Clocks q = load_clocks(w, e >> 24, e & 0xFFFFFFu);
-            if (try_deliver(w, e & 0xFFFFFFu, q, nj, nx)) gone |= 1ull << l;
-            else {
-                jw = w.lane == l ? nj : jw;
-                xw = w.lane == l ? nx : xw;
-            }
-            if (l == 63u) break;
-            from = l + 1u;
-        }
-        w.checks = uni(w.checks + (uint32_t)__popcll(vmask & ~seen));   // watched entries: checks that cannot pass
-        const unsigned long long kept = vmask & ~gone;
+        if (i < n0) { ent = w.sbuf[i]; jw = w.wj[i]; xw = w.wx[i]; }
+        const unsigned long long vmask = __ballot(i < n0);
+        const unsigned long long kept = vmask & ~fold_slice(w, ent, jw, xw, vmask);
         if ((kept >> w.lane) & 1ull) {
             const uint32_t o = keep + (uint32_t)__popcll(kept & ((1ull << w.lane) - 1ull));
             w.sbuf[o] = ent;
@@ -154,6 +225,35 @@ __device__ void fold(Wave& w) {
         __builtin_amdgcn_wave_barrier();
     }
     w.nb = keep;
+    if (keep <= 64u) {                                    // back to registers
+        w.inreg = 1u;
+        w.rent = w.lane < keep ? w.sbuf[w.lane] : 0u;
+        w.rjw = w.lane < keep ? w.wj[w.lane] : kWatchNone;
+        w.rxw = w.lane < keep ? w.wx[w.lane] : 0u;
+        w.pend = pending(w);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// append a received entry at the end of the buffer
+__device__ void append(Wave& w, uint32_t e) {
+    w.nb = uni(w.nb);
+    w.inreg = uni(w.inreg);
+    if (w.inreg && w.nb == 64u) {                         // spill the registers
+        w.sbuf[w.lane] = w.rent;
+        w.wj[w.lane] = w.rjw;
+        w.wx[w.lane] = w.rxw;
+        w.inreg = 0u;
+    }
+    if (w.inreg) {
+        if (w.lane == w.nb) { w.rent = e; w.rjw = kWatchNone; }
+        w.pend = uni64(w.pend | (1ull << w.nb));
+    } else if (w.lane == 0) {
+        w.sbuf[w.nb] = e;
+        w.wj[w.nb] = kWatchNone;
+    }
+    w.nb = uni(w.nb + 1u);
+    __builtin_amdgcn_wave_barrier();
 }
 
 __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
@@ -178,12 +278,24 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         w.c = a.clk[(size_t)lv * kCsLanes + lane];
         w.self = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.self[lv]);
         w.eid = lane < a.m ? emitter_id(lane, a.n_global, a.m) : 0xFFFFFFFFu;
-        w.ke = emitter_index(w.v, a.n_global, a.m);
-        w.nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.nbuf[lv]);
+        w.ke = (int)uni((uint32_t)emitter_index(w.v, a.n_global, a.m));
+        w.nb = uni(a.nbuf[lv]);
+        w.inreg = w.nb <= 64u ? 1u : 0u;
+        w.rent = 0;
+        w.rjw = kWatchNone;
+        w.rxw = 0;
+        w.pend = w.inreg ? first_n(w.nb) : 0ull;
+        bool old = false;
         for (uint32_t i = lane; i < w.nb; i += 64) {
-            w.sbuf[i] = a.buf[(size_t)lv * kCsBufCap + i];
-            w.wj[i] = kWatchNone;
+            const uint32_t e = a.buf[(size_t)lv * kCsBufCap + i], r0 = e & 0xFFFFFFu;
+            old |= (a.t - r0 >= kCsWindow - 1) | ((r0 > a.period) & (a.t - (r0 - a.period) >= kCsWindow - 1));
+            if (w.inreg) w.rent = e;
+            else {
+                w.sbuf[i] = e;
+                w.wj[i] = kWatchNone;
+            }
         }
+        w.old_any = __ballot(old) != 0ull;
         __builtin_amdgcn_wave_barrier();
         // arrivals of round t: lane k marks bit d if k's round-(t-d) message lands now
         uint32_t am = 0;
@@ -199,16 +311,11 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
             const unsigned long long any = __ballot(am != 0u);
             if (!any) break;
             const uint32_t k = uni((uint32_t)__ffsll((long long)any) - 1u);
-            const uint32_t d = uni(31u - __clz(__shfl(am, (int)k, 64)));
+            const uint32_t d = uni(31u - __clz((uint32_t)__builtin_amdgcn_readlane((int)am, (int)k)));
             if (lane == k) am &= ~(1u << d);
             w.received = uni(w.received + 1u);
             if (w.nb >= kCsBufCap) { w.err = uni(w.err | 1u); continue; }
-            if (lane == 0) {
-                w.sbuf[w.nb] = (k << 24) | (a.t - d);
-                w.wj[w.nb] = kWatchNone;
-            }
-            w.nb = uni(w.nb + 1u);
-            __builtin_amdgcn_wave_barrier();
+            append(w, (k << 24) | (a.t - d));
             fold(w);
         }
         if (a.redeliver && a.t % a.redeliver == 0) fold(w);   // handle_info(deliver) (:233-248)
@@ -218,7 +325,11 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
             a.nbuf[lv] = w.nb;
             a.delivered[lv] += w.delivered;
         }
-        for (uint32_t i = lane; i < w.nb; i += 64) a.buf[(size_t)lv * kCsBufCap + i] = w.sbuf[i];
+        if (w.inreg) {
+            if (lane < w.nb) a.buf[(size_t)lv * kCsBufCap + lane] = w.rent;
+        } else {
+            for (uint32_t i = lane; i < w.nb; i += 64) a.buf[(size_t)lv * kCsBufCap + i] = w.sbuf[i];
+        }
     }
     if (lane == 0) {
         red[wv][0] = w.received;
