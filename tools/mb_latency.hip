@@ -66,7 +66,7 @@ __global__ void ops_latency(uint32_t* __restrict__ buf, size_t n, uint32_t k, ui
         for (uint32_t i = 0; i < k; i++) {
             x ^= x << 13; x ^= x >> 7; x ^= x << 17;
             const size_t a = (size_t)(x % n);
-            if (op == 0) buf[a] = (uint32_t)x;
+            if (op == 0) buf[a] = (uint32_t)(x % n);   // the buffer is also the chase table: keep every entry < n
             else if (op == 1) atomicOr(buf + a, 1u);
             else if (op == 2) acc += atomicOr(buf + a, 1u);
             else acc += __builtin_nontemporal_load(buf + a);
