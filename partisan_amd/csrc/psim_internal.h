@@ -428,12 +428,13 @@ struct PdHead {
 struct PdBits {
     unsigned long long w[2];
     __host__ __device__ static PdBits none() { return PdBits{{0ull, 0ull}}; }
+    // selects, not w[i >> 6]: a variable index into a private array sends
+    // the kernel's whole context to scratch memory
     __host__ __device__ static PdBits one(int i) {
-        PdBits b = none();
-        if (i >= 0) b.w[i >> 6] = 1ull << (i & 63);
-        return b;
+        const unsigned long long x = i >= 0 ? 1ull << (i & 63) : 0ull;
+        return PdBits{{i < 64 ? x : 0ull, i >= 64 ? x : 0ull}};
     }
-    __host__ __device__ bool test(uint32_t i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
+    __host__ __device__ bool test(uint32_t i) const { return ((i < 64u ? w[0] : w[1]) >> (i & 63)) & 1ull; }
     __host__ __device__ bool any() const { return (w[0] | w[1]) != 0ull; }
     __host__ __device__ PdBits operator|(const PdBits& o) const { return PdBits{{w[0] | o.w[0], w[1] | o.w[1]}}; }
     __host__ __device__ PdBits operator&(const PdBits& o) const { return PdBits{{w[0] & o.w[0], w[1] & o.w[1]}}; }

@@ -45,7 +45,8 @@ struct Ctx {
     PdRow* rows;                   // outstanding rows in HBM
     const uint32_t* pv;            // SCAMP partial view row
     uint32_t npv;
-    uint32_t sent[6], dropped, deliv, err;
+    unsigned long long sent;       // 12 bits per message kind 1..5 (kind k at bit 12 k)
+    uint32_t dropped, deliv, err;
 };
 
 __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
@@ -55,42 +56,46 @@ __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
     return false;
 }
 
-__device__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
+__device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     if (!connected(c, t)) { c.dropped++; return; }
     const PdArgs& a = *c.a;
     const uint32_t pos = wave_reserve(a.nout);
-    c.sent[type]++;
+    c.sent += 1ull << (12u * type);
     if (pos >= a.out_cap) { c.err |= 1u; return; }
     PdMsg m;
     m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.mono = mono;
     a.out[pos] = m;
 }
 
-__device__ int tab_find(const Ctx& c, uint32_t x) {
+__device__ __forceinline__ int tab_find(const Ctx& c, uint32_t x) {
     for (uint32_t i = 0; i < c.h.ntab; i++)
         if (c.tab[i] == x) return (int)i;
     return -1;
 }
 
 // drop ids no set refers to (keeps the masks aligned with the row)
-__device__ void tab_compact(Ctx& c) {
+__device__ __forceinline__ void tab_compact(Ctx& c) {
     PdBits any = PdBits::none();
+    #pragma unroll
     for (int k = 0; k < S_NSET; k++) any |= c.m[k];
     uint32_t w = 0;
     PdBits nm[S_NSET];
+    #pragma unroll
     for (int k = 0; k < S_NSET; k++) nm[k] = PdBits::none();
     for (uint32_t i = 0; i < c.h.ntab; i++) {
         if (!any.test(i)) continue;
         c.tab[w] = c.tab[i];
+        #pragma unroll
         for (int k = 0; k < S_NSET; k++)
             if (c.m[k].test(i)) nm[k] |= PdBits::one((int)w);
         w++;
     }
     c.h.ntab = w;
+    #pragma unroll
     for (int k = 0; k < S_NSET; k++) c.m[k] = nm[k];
 }
 
-__device__ int tab_insert(Ctx& c, uint32_t x) {
+__device__ __forceinline__ int tab_insert(Ctx& c, uint32_t x) {
     const int f = tab_find(c, x);
     if (f >= 0) return f;
     if (c.h.ntab >= kPdTab) tab_compact(c);
@@ -113,18 +118,24 @@ __device__ __forceinline__ void ensure_root_sets(Ctx& c) {
     c.m[S_LAZ] = c.m[S_CL];
     c.h.flags |= 1u;
 }
-__device__ void add_eager(Ctx& c, const PdBits& b) {
+__device__ __forceinline__ void add_eager(Ctx& c, const PdBits& b) {
     ensure_root_sets(c);
     c.m[S_EAG] |= b;
     c.m[S_LAZ] &= ~b;
 }
-__device__ void add_lazy(Ctx& c, const PdBits& b) {
+__device__ __forceinline__ void add_lazy(Ctx& c, const PdBits& b) {
     ensure_root_sets(c);
     c.m[S_EAG] &= ~b;
     c.m[S_LAZ] |= b;
 }
-__device__ __forceinline__ PdBits eager_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_EAG] : c.m[S_CE]; }
-__device__ __forceinline__ PdBits lazy_now(const Ctx& c) { return (c.h.flags & 1u) ? c.m[S_LAZ] : c.m[S_CL]; }
+// x if f else y, blended by value: a select between two members' addresses
+// would keep the whole context in scratch memory
+__device__ __forceinline__ PdBits blend(bool f, const PdBits& x, const PdBits& y) {
+    const unsigned long long k = f ? ~0ull : 0ull;
+    return PdBits{{(x.w[0] & k) | (y.w[0] & ~k), (x.w[1] & k) | (y.w[1] & ~k)}};
+}
+__device__ __forceinline__ PdBits eager_now(const Ctx& c) { return blend(c.h.flags & 1u, c.m[S_EAG], c.m[S_CE]); }
+__device__ __forceinline__ PdBits lazy_now(const Ctx& c) { return blend(c.h.flags & 1u, c.m[S_LAZ], c.m[S_CL]); }
 
 // the backend's timestamp ISet for the root (partisan_plumtree_backend.erl
 // is_stale/1 :229-244, add_timestamp): heartbeat serials dbase-63..dbase
@@ -141,12 +152,12 @@ __device__ __forceinline__ void mark_delivered(Ctx& c, uint32_t mono) {
 }
 
 // add_all_outstanding/5 (:1215-1219)
-__device__ void add_row(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
+__device__ __forceinline__ void add_row(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
     if (c.h.nrow >= kPdRows) { c.err |= 4u; return; }
     c.rows[c.h.nrow++] = PdRow{peer, mono, round};
 }
 // ack_outstanding/5 (:1207-1211): ets:delete_object removes every identical row
-__device__ void ack_rows(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
+__device__ __forceinline__ void ack_rows(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
     uint32_t w = 0;
     for (uint32_t i = 0; i < c.h.nrow; i++) {
         const PdRow r = c.rows[i];
@@ -158,14 +169,14 @@ __device__ void ack_rows(Ctx& c, uint32_t peer, uint32_t mono, uint32_t round) {
 }
 
 // eager_push/7 (:962-970) to eager peers -- From, schedule_lazy_push/6 (:974-988)
-__device__ void push(Ctx& c, const PdBits& from_bit, uint32_t mono, uint32_t round) {
+__device__ __forceinline__ void push(Ctx& c, const PdBits& from_bit, uint32_t mono, uint32_t round) {
     PdBits e = eager_now(c) & ~from_bit;
     while (e.any()) send(c, c.tab[pop_low(e)], PD_BROADCAST, mono, round);
     PdBits l = lazy_now(c) & ~from_bit;
     while (l.any()) add_row(c, c.tab[pop_low(l)], mono, round);
 }
 
-__device__ void handle(Ctx& c, const PdMsg& m) {
+__device__ __forceinline__ void handle(Ctx& c, const PdMsg& m) {
     const PdArgs& a = *c.a;
     switch (m.type) {
     case PD_BROADCAST: {                           // :571-578 -> handle_broadcast/8 :843-857
@@ -208,7 +219,7 @@ __device__ void handle(Ctx& c, const PdMsg& m) {
 }
 
 // {update, Members} as a set delta (:607-639)
-__device__ void apply_update(Ctx& c, uint32_t added, uint32_t removed) {
+__device__ __forceinline__ void apply_update(Ctx& c, uint32_t added, uint32_t removed) {
     if (added != kNone) {
         const PdBits b = bit(tab_insert(c, added));
         c.m[S_MEM] |= b;
@@ -220,6 +231,7 @@ __device__ void apply_update(Ctx& c, uint32_t added, uint32_t removed) {
     if (removed != kNone) {                        // neighbors_down/2
         const int i = tab_find(c, removed);
         if (i >= 0)
+            #pragma unroll
             for (int k = 0; k < S_NSET; k++) c.m[k] &= ~bit(i);
         uint32_t w = 0;                            // ... and deletes the outstanding rows to it
         for (uint32_t j = 0; j < c.h.nrow; j++) {
@@ -289,11 +301,12 @@ __global__ __launch_bounds__(kBlock) void pd_scatter(PdArgs a) {
     }
 }
 
-__device__ void load(Ctx& c, const PdArgs& a, uint32_t v) {
+__device__ __forceinline__ void load(Ctx& c, const PdArgs& a, uint32_t v) {
     c.a = &a;
     c.v = v;
     c.h = a.head[v];
     c.tab = a.tab + (size_t)v * kPdTab;
+    #pragma unroll
     for (int k = 0; k < S_NSET; k++) c.m[k] = a.mask[(size_t)v * S_NSET + k];
     c.rows = a.rows + (size_t)v * kPdRows;
     if (a.mono > c.h.dbase) {                      // slide the delivered window to the newest serial
@@ -303,16 +316,18 @@ __device__ void load(Ctx& c, const PdArgs& a, uint32_t v) {
     }
     c.pv = a.pv + (size_t)v * kScPv;
     c.npv = a.sch[v].npv;
-    for (int i = 0; i < 6; i++) c.sent[i] = 0;
+    c.sent = 0;
     c.dropped = c.deliv = c.err = 0;
 }
-__device__ void store(const Ctx& c) {
+__device__ __forceinline__ void store(const Ctx& c) {
     const PdArgs& a = *c.a;
     a.head[c.v] = c.h;
+    #pragma unroll
     for (int k = 0; k < S_NSET; k++) a.mask[(size_t)c.v * S_NSET + k] = c.m[k];
 }
 
-__device__ void reduce_stats(const PdArgs& a, const unsigned long long* vals) {
+__device__ __forceinline__ void reduce_stats(const PdArgs& a, const unsigned long long* vals) {
+#pragma unroll
     for (int i = 1; i < kPdNStat; i++) {
         unsigned long long x = vals[i];
         if (i == 9) {
@@ -332,6 +347,7 @@ __device__ void reduce_stats(const PdArgs& a, const unsigned long long* vals) {
 __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
     unsigned long long vals[kPdNStat];
+#pragma unroll
     for (int i = 0; i < kPdNStat; i++) vals[i] = 0;
     if (v < a.n && a.alive[v]) {
         Ctx c;
@@ -369,7 +385,8 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
         }
         if (c.h.ntab > kPdTab - 8) tab_compact(c);
         store(c);
-        for (int i = 1; i <= 5; i++) vals[i] = c.sent[i];
+#pragma unroll
+        for (int i = 1; i <= 5; i++) vals[i] = (c.sent >> (12 * i)) & 0xFFFull;
         vals[6] = c.dropped;
         vals[7] = c.deliv;
         vals[9] = c.err;
