@@ -154,6 +154,17 @@ __device__ __forceinline__ void put_delayed(const PtArgs& a, uint32_t e, uint32_
     atomicAdd(&hist[d], (unsigned long long)word_msgs(w));
 }
 
+// ... and, receiver on another shard, to the staging ring slot of the round
+// whose exchange carries it (the round before its arrival), tagged with the
+// arrival round; the receiving shard's ingest puts it in its inbox ring.
+__device__ __forceinline__ void put_delayed_remote(const PtArgs& a, uint32_t e, uint32_t w, unsigned long long* hist) {
+    const uint32_t d = a.dly[e];
+    const uint32_t k = (a.rpos + kRing - 1u + d) & (kRing - 1);
+    w = (w & ~(0xFFu << kTagShift)) | (((a.wtag + d) & 0xFFu) << kTagShift);
+    a.srg[size_t(k) * a.ed + e] = w;
+    atomicAdd(&hist[d], (unsigned long long)word_msgs(w));
+}
+
 // The round kernels' per-delay message counts (LDS, flushed once per workgroup).
 __device__ __forceinline__ unsigned long long* delay_hist() {
     __shared__ unsigned long long dh[kRing];
@@ -219,6 +230,8 @@ __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32
         a.in_nxt[a.rev[e] - a.slot_base] = w;
 #endif
         mark_group(a, u >> kGroupShift, mark, wl);
+    } else if (kFault && a.srg) {
+        put_delayed_remote(a, e, w, hist ? hist : delay_hist());
     } else {
         a.stage[e] = w;
     }
@@ -585,6 +598,8 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
             a.in_nxt[rv[s] - a.slot_base] = wo;
 #endif
             sink.word(s, u);
+        } else if (kFault && a.srg) {
+            put_delayed_remote(a, rs + s, wo, delay_hist());
         } else {
             a.stage[rs + s] = wo;
         }

@@ -170,6 +170,8 @@ struct psim_handle {
         uint64_t slot_base = 0;         // ABI (CSR) global slot id of local slot 0
         uint64_t dev_slot_base = 0;     // the same in device slot ids (ELL: v_lo * W)
         uint32_t* stage = nullptr;       // [E_local] staged cross-shard words
+        uint32_t* srg = nullptr;         // [kRing][E_local] staging ring once delay faults are installed
+        std::vector<int64_t> pend_rows;  // delays: this shard's pending messages after each collected round
         uint32_t* rem = nullptr;         // local slots whose receiver is remote, grouped by shard
         uint4* blk = nullptr;            // compaction blocks {shard, start, len, 0}
         uint32_t nblk = 0;
@@ -293,10 +295,10 @@ void free_graph(psim_handle* h) {
     }
     auto& sh = h->sh;
     void* sp[] = {sh.stage, sh.rem, sh.blk, sh.send_base_d, sh.cursor, sh.slot2v, sh.recv_map, sh.xsend, sh.xrecv,
-                  sh.xrs_raw, sh.xrr};
+                  sh.xrs_raw, sh.xrr, sh.srg};
     for (void* p : sp)
         if (p) (void)hipFree(p);
-    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = sh.xsend = sh.xrecv = nullptr;
+    sh.stage = sh.rem = sh.send_base_d = sh.cursor = sh.slot2v = sh.recv_map = sh.xsend = sh.xrecv = sh.srg = nullptr;
     sh.xrs = sh.xrr = nullptr;
     sh.xrs_raw = nullptr;
     sh.xcur = nullptr;
@@ -329,6 +331,10 @@ void set_round_ring(const psim_handle* h, PtArgs& a, uint64_t R) {
     a.pend_nxt = h->pring + size_t(a.rpos) * ng;
     a.ctag = uint32_t(R) & 0xFFu;
     a.wtag = uint32_t(R + 1) & 0xFFu;
+    if (h->sh.srg) {            // sharded: the words the exchange after round R carries
+        a.srg = h->sh.srg;
+        a.stage = h->sh.srg + size_t(R & (kRing - 1)) * h->Ed;
+    }
 }
 
 PtArgs make_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats) {
@@ -1921,6 +1927,7 @@ int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32
     std::vector<unsigned long long> hs(size_t(k) * kStatsRow);
     if (k) HIPCHK(h, hipMemcpy(hs.data(), sh.ring, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     sh.pending = 0;
+    sh.pend_rows.assign(k, 0);
     for (uint32_t i = 0; i < k; i++) {
         unsigned long long r[kNStat];
         reduce_row(hs.data() + size_t(i) * kStatsRow, r);
@@ -1937,6 +1944,12 @@ int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32
         h->ost_cnt += (int64_t)r[S_OST_DELTA];
         h->live_rows += (int64_t)r[S_LIVE_DELTA];
         h->inflight = msgs;
+        if (h->dly) {          // round R consumed its arrivals; its sends are pending until R + 1 + d
+            const uint64_t R = h->round - k + 1 + i;
+            h->due[R & (kRing - 1)] = 0;
+            h->inflight = add_due(h->due, R, hs.data() + size_t(i) * kStatsRow + size_t(kStatShards) * kNStat);
+            sh.pend_rows[i] = (int64_t)h->inflight;
+        }
         h->kernel_ms_total += ms;
         h->rounds_total++;
         if (out && i < cap) {
@@ -2257,6 +2270,8 @@ int shard_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size
     if (rc) return rc;
     if (xs) memset(xs, 0, sizeof *xs);
     if (h->lanes.size() > 1 || h->win) {
+        if (h->dly && h->sh.world > 1)
+            return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: one heartbeat root at a time");
         if (!h->sh.pending) HIPCHK(h, seed_hold_rings(h, h->round + 1));
         return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
     }
@@ -2269,7 +2284,8 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
                      uint32_t* rounds_run, psim_exchange_stats* xs) {
     int rc;
     constexpr uint32_t K = 4;                  // rounds between counter collections
-    constexpr int NK = 10;                     // 5 kinds, delivered_new, senders, degree sum, live rows, row holders
+    constexpr int NK = 11;                     // 5 kinds, delivered_new, senders, degree sum, live rows, row holders,
+                                               // messages still pending (delay faults)
     uint32_t ran = 0;
     bool done = false;
     auto& sh = h->sh;
@@ -2319,7 +2335,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
         }
         for (uint32_t j = 0; j < k; j++) {
             uint32_t rec_k = 0;
-            if (sh.plan_ok && sh.world > 1) {
+            if (sh.plan_ok && sh.world > 1 && !h->dly) {   // delays: a round's words are not bounded by the last
                 const double S = double(std::max<uint32_t>(1u, sh.max_deg_g)) * (bM + bH);
                 bH += bM;
                 bM = S;
@@ -2359,6 +2375,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
             f[7] = (int64_t)st[j].sender_degree_sum;
             f[8] = live[j];
             f[9] = (int64_t)st[j].outstanding_vertices;
+            f[10] = h->dly && j < sh.pend_rows.size() ? sh.pend_rows[j] : 0;
         }
         if (h->sh.world > 1) {
             std::string err;
@@ -2369,6 +2386,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
             const int64_t* f = flat.data() + size_t(j) * NK;
             int64_t msgs = 0;
             for (int t = 0; t < 5; t++) msgs += f[t];
+            if (h->dly) msgs = f[10];                          // what is still on the wire, delayed included
             if (!h->lanes.empty()) {
                 auto& l = h->lanes[h->cur_lane];
                 l.g_inflight = msgs;
@@ -2787,8 +2805,9 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
 
 int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
     if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
-    if (h->sh.world != 1 || h->bin.rec_c)
-        return fail(h, PSIM_ESTATE, "delay faults need the single-GPU slot-scatter engine");
+    if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "delay faults need the slot-scatter engine (not the binned one)");
+    if (h->sh.world > 1 && (h->lanes.size() > 1 || h->win || h->sh.pending))
+        return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: one heartbeat lane, no async rounds pending");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
@@ -2796,12 +2815,15 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
         if (l.inflight) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
         if (l.win) return fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
     }
+    // every shard installs the table (its own senders' pairs) and the ring,
+    // so a delayed word from any shard finds its receiver's inbox ring
     std::vector<uint8_t> dl(h->Ed, 0);
     for (size_t i = 0; i < k; i++) {
-        if (src[i] >= h->n || dst[i] >= h->n)
+        if (src[i] >= h->sh.n_global || dst[i] >= h->sh.n_global)
             return fail(h, PSIM_EINVAL, "delay pair (%u, %u) out of range", src[i], dst[i]);
         if (rounds[i] > kMaxDelay) return fail(h, PSIM_EINVAL, "delay %u > %u rounds", rounds[i], kMaxDelay);
-        const uint32_t u = src[i];
+        const uint32_t u = src[i] - h->sh.v_lo;
+        if (u >= h->n) continue;                       // another shard's sender
         const auto b = h->h_col.begin() + h->h_rowp[u], e = h->h_col.begin() + h->h_rowp[u + 1];
         const auto it = std::lower_bound(b, e, dst[i]);
         if (it == e || *it != dst[i]) continue;        // not an overlay edge: nothing ever flows
@@ -2812,6 +2834,11 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     if (!h->dly) {
         // switch every lane to the ring; nothing is in flight, so no word moves
         if (hipMalloc((void**)&h->dly, h->Ed) != hipSuccess) return fail(h, PSIM_ENOMEM, "delay table");
+        if (h->sh.world > 1) {
+            if (!alloc_zero((void**)&h->sh.srg, size_t(kRing) * h->Ed * 4))
+                return fail(h, PSIM_ENOMEM, "staging ring of the delay faults");
+            h->sh.plan_ok = false;
+        }
         const int focus = h->cur_lane;
         for (int j = 0; j < (int)h->lanes.size(); j++) {
             auto& l = h->lanes[j];

@@ -170,6 +170,10 @@ struct PtArgs {
     uint8_t* __restrict__ pring;           // [kRing][ngrp] group flags
     unsigned long long* __restrict__ dhist;  // [kRing] messages written this round per delay
     uint32_t rpos;                         // ring slot read by the round after this one
+    // sharded handles: the staging words of remote receivers as a ring too --
+    // slot k holds the words the exchange after round k (mod kRing) carries,
+    // i.e. those arriving in round k + 1; `stage` points at this round's slot
+    uint32_t* __restrict__ srg;            // [kRing][ed] (null: not sharded or no delays)
     uint32_t ed, ngrp;                     // words per ring slot, flags per ring slot
     // binned engine (null for the slot-scatter engine)
     uint2* __restrict__ rec_c;             // [E] coarse-bin regions: {receiver slot, word}

@@ -180,6 +180,17 @@ class ShardedPlumtree:
     def set_alive(self, alive):
         self.sim.set_alive(alive)
 
+    def set_delays(self, pairs, rounds):
+        """Delay faults (psim_set_delays, collective: every rank passes the same
+        global pairs; each installs its own senders').  Needs the in-library
+        exchange: its stop rule waits for the delayed messages."""
+        if self.transport == "torch":
+            raise ValueError("delay faults need the in-library exchange (transport 'rccl' or 'callback')")
+        self.sim.set_delays(pairs, rounds)
+
+    def set_omissions(self, pairs):
+        self.sim.set_omissions(pairs)
+
     def broadcast(self, root):
         mono = C.c_uint32()
         if self.transport != "torch":

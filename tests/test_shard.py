@@ -125,6 +125,76 @@ def test_sharded_matches_oracle(world, n, seed, L, transport, csr):
         assert res[r] == "ok", res[r]
 
 
+def _delay_worker(rank, world, port, n, seed, L, dmax, csr, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        dist = _init(rank, world, port)
+        import partisan_amd as pa
+        from partisan_amd.shard import ShardedPlumtree
+        import pyoracle as O
+        rp, col = pa.overlay.random_regular(n, 5, seed)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L, transport="callback",
+                             csr=csr)
+        orc = O.Plumtree(rp, col, L)
+        sim = sp.sim
+        # 30 % of the directed edges of the whole overlay, 1..dmax rounds late
+        # (every rank passes the same pairs; each installs its own senders')
+        rng = np.random.default_rng(seed)
+        rp64 = np.asarray(rp, dtype=np.int64)
+        src = np.repeat(np.arange(n), np.diff(rp64))
+        pick = rng.random(len(src)) < 0.3
+        pairs = np.stack([src[pick], np.asarray(col)[pick]], axis=1).astype(np.uint32)
+        d = rng.integers(1, dmax + 1, len(pairs)).astype(np.uint8)
+        sp.set_delays(pairs, d)
+        orc.set_delays(pairs, d)
+        root = 11
+        for hb in range(3):
+            mono = sp.broadcast(root)
+            assert mono == orc.heartbeat(root)
+            if hb == 1:            # the first 12 rounds one at a time (psim_shard_step), then the rest
+                for r in range(12):
+                    g, o = sp.step(1)[0], orc.step(1)[0]
+                    for k in KINDS:
+                        assert g[k] == o[k], (hb, r, k, g, o)
+                    assert g["delivered_new"] == o["delivered_new"], (hb, r)
+            gst, gr = sp.run()
+            ost, orr = orc.run()
+            assert gr == orr, (hb, gr, orr)
+            for g, o in zip(gst, ost):
+                for k in KINDS:
+                    assert g[k] == o[k], (hb, k, g, o)
+            eager, lazy, outst, rr = sim.plumtree_state()
+            assert np.array_equal(sim.delivered(), orc.delivered(root, mono)[sim.v_lo:sim.v_lo + sim.n])
+            for lv in range(sim.n):
+                v = sim.v_lo + lv
+                oe, ol = orc.peers(v, root)
+                assert sim.mask_to_peers(lv, eager[lv]) == oe, (hb, v)
+                assert sim.mask_to_peers(lv, lazy[lv]) == ol, (hb, v)
+        assert sim.delivered().all()
+        sp.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,seed,L,dmax,csr", [(2, 3000, 31, 1, 4, False), (3, 2000, 32, 2, 9, False),
+                                                     (2, 1500, 33, 1, 14, True)])
+def test_sharded_delay_faults_match_oracle(world, n, seed, L, dmax, csr):
+    """SURVEY 8(f) row 4 on the sharded engine: delay faults on 30 % of the
+    directed edges, delayed words to other shards held in the sender's
+    staging ring until the exchange before their arrival round.  Per-round
+    global counters, round count to quiescence (psim_shard_run waits for the
+    delayed messages), and each shard's delivered / eager / lazy sets equal
+    the oracle's over three heartbeats (the second one stepped round by round)."""
+    res = run_world(_delay_worker, world, n, seed, L, dmax, csr)
+    for r in range(world):
+        assert res[r] == "ok", res[r]
+
+
 def _lanes_check(sim, orc, monos, exact):
     """This rank's vertices against the oracle, per root lane: delivered per
     Monotonic, eager / lazy sets; rows and in-flight messages over all lanes
