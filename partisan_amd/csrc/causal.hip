@@ -159,6 +159,24 @@ __device__ __forceinline__ unsigned long long pending(const Wave& w) {
 // per pending entry
 __device__ void fold_reg(Wave& w) {
     const uint32_t n0 = uni(w.nb);
+    if (n0 == 0u) return;
+    if (uni64(w.pend) == 1ull << (n0 - 1u)) {
+        // the common fold: only the entry just appended can pass (the others'
+        // watches hold); it leaves from the end, so nothing moves
+        const uint32_t l = n0 - 1u;
+        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)l));
+        uint32_t nj = 0, nx = 0;
+        w.checks = uni(w.checks + l);
+        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) {
+            w.nb = l;
+            w.pend = pending(w);
+        } else {
+            w.rjw = w.lane == l ? nj : w.rjw;
+            w.rxw = w.lane == l ? nx : w.rxw;
+            w.pend = 0ull;
+        }
+        return;
+    }
     unsigned long long gone = 0;
     uint32_t tried = 0;
     unsigned long long m = uni64(w.pend);
