@@ -127,3 +127,38 @@ def test_1m_properties():
     nonem[g.emitters] = False
     assert (slf[nonem].astype(np.uint64) == dl[nonem]).all()   # one increment per delivery
     sim.close()
+
+
+@pytest.mark.gpu
+def test_deep_buffers_at_scale_properties():
+    """200k vertices, 64 emitters, delays up to 12 rounds: buffers of ~100-200
+    messages, so folds run from LDS and move back into registers as buffers
+    drain.  Conservation (delivered + buffered = received), one own-counter
+    increment per delivery at non-emitters, per-emitter FIFO (no two buffered
+    entries of one emitter share a round) -- and 12 rounds equal the oracle's
+    at a size it finishes in seconds (2k vertices, buffers up to ~160)."""
+    import partisan_amd as pa
+    n, m = 200_000, 64
+    sim = pa.Simulator(seed=0x5EED0005)
+    g = pa.causal.CausalCluster(sim, n, m=m, period=1, dmax=12, redeliver=1)
+    st = g.step(16)
+    rec = sum(s["received"] for s in st)
+    dl = g.delivered()
+    assert int(dl.sum()) == sum(s["delivered"] for s in st)
+    assert int(dl.sum()) + st[-1]["buffered"] == rec
+    assert st[-1]["buffered"] > 64 * 1000          # deep buffers somewhere
+    lanes, slf = g.clocks()
+    nonem = np.ones(n, bool)
+    nonem[g.emitters] = False
+    assert (slf[nonem].astype(np.uint64) == dl[nonem]).all()
+    rng = np.random.default_rng(3)
+    for v in rng.choice(n, 64, replace=False):
+        b = g.buffered(int(v))
+        assert len({(k, r) for k, r in b}) == len(b)
+    sim.close()
+    sim, g, o = _pair(2000, 64, 1, 12, 1, 0x5EED0005)
+    gs, os_ = g.step(12), o.step(12)
+    assert [[a[k] for k in KEYS] for a in gs] == [[b[k] for k in KEYS] for b in os_]
+    assert max(len(o.buffered(v)) for v in range(2000)) > 64
+    _compare(g, o, 2000)
+    sim.close()
