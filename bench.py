@@ -41,7 +41,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (= ranks, one process each).  Without a launcher (WORLD_SIZE unset) N > 1 spawns the N "
+                        "rank processes itself; under torchrun it must equal WORLD_SIZE")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--num-peers", dest="n", type=int, default=10_000_000)
@@ -69,6 +71,59 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by tools/pmc_traffic.py for this workload")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` with no launcher around it: start the N rank
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1) as children of this process, which never imports torch or
+    touches a GPU, and exit with the first failing rank's status (rank 0
+    prints the JSON line).  A failing rank takes the others down."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:          # the collective peers of a dead rank would wait forever
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def check_world(args):
+    """The rank layout this process runs in; refuses --gpus != WORLD_SIZE."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        return 1 if args.gpus is None else args.gpus, False
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                         f"{world}-rank run as {args.gpus} GPUs")
+    return world, True
 
 
 def dist_setup(args):
@@ -137,10 +192,54 @@ def verify(sim, pg, n, rounds_per_step):
     return ok
 
 
-def cpu_baseline_full(args):
+KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
+
+
+def oracle_parity(sim, orc, root, gpu_stats, gpu_rounds, ost, orr, omono):
+    """The GPU's last heartbeat against the C oracle's heartbeat of the same
+    overlay (outside any timed region): round count, per-round message counts
+    by kind and new deliveries, and at the end every vertex's delivered bit,
+    eager / lazy / outstanding sets and accepted Round (orc_pt_dump_state over
+    the handle's slot layout).  gpu_stats: psim_run's rows (numpy records).
+    Returns {"ok": bool, ...} with the first mismatch named."""
+    import numpy as np
+    res = {"n_peers": int(sim.n), "rounds_gpu": int(gpu_rounds), "rounds_oracle": int(orr), "ok": False}
+    if gpu_rounds != orr:
+        res["mismatch"] = "round count"
+        return res
+    for r in range(orr):
+        g, o = gpu_stats[r], ost[r]
+        for i, k in enumerate(KINDS):
+            if int(g["sent"][i + 1]) != o[k]:
+                res["mismatch"] = f"round {r + 1} {k}: gpu {int(g['sent'][i + 1])} oracle {o[k]}"
+                return res
+        if int(g["delivered_new"]) != o["delivered_new"]:
+            res["mismatch"] = f"round {r + 1} delivered_new"
+            return res
+    if not np.array_equal(sim.delivered(), orc.delivered(root, omono)):
+        res["mismatch"] = "delivered set"
+        return res
+    ge, gl, go, grr = sim.plumtree_state()
+    oe, ol, oo, orrs = orc.dump_state(root, omono, sim.slot_row_ptr, sim.slot_col)
+    for name, g, o in (("eager", ge, oe), ("lazy", gl, ol), ("outstanding", go, oo), ("Round", grr, orrs)):
+        bad = np.flatnonzero(g != o)
+        if len(bad):
+            res["mismatch"] = f"{name} sets differ at {len(bad)} vertices (first {int(bad[0])})"
+            return res
+    res.update(ok=True, messages=int(sum(sum(o[k] for k in KINDS) for o in ost)),
+               compared=("round count; per-round broadcast / prune / i_have / ignored_i_have / graft and new "
+                         "deliveries; final delivered set, eager / lazy / outstanding masks and accepted Round "
+                         "of every vertex"))
+    return res
+
+
+def cpu_baseline_full(args, sim=None, gpu_stats=None, gpu_rounds=None):
     """One single-thread C-oracle flood of the benchmark's own configuration
     (the same --num-peers overlay, seed and root), timed from heartbeat to
-    quiescence (the 10M config itself, beside the 1M sample)."""
+    quiescence (the 10M config itself, beside the 1M sample).
+    With the GPU's last step (sim, its psim_run rows and round count) the
+    same flood is then the oracle parity check of the metric config
+    (VERDICT r3): returned as the second value."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     from partisan_amd import overlay
@@ -148,16 +247,21 @@ def cpu_baseline_full(args):
     orc = O.Plumtree(rp, col, args.lazy_tick_rounds)
     del rp, col
     t0 = time.perf_counter()
-    orc.heartbeat(0)
-    _, rounds = orc.run()
+    omono = orc.heartbeat(0)
+    ost, rounds = orc.run()
     dt = time.perf_counter() - t0
+    parity = None
+    if sim is not None:
+        t1 = time.perf_counter()
+        parity = oracle_parity(sim, orc, 0, gpu_stats, gpu_rounds, ost, rounds, omono)
+        parity["check_s"] = round(time.perf_counter() - t1, 1)
     orc.close()
     return {
         "value": args.n * rounds / dt, "unit": "peer-rounds/s", "cores": 1, "kind": "port",
         "sample": (f"C oracle (oracle/plumtree.c), one flood of the benchmark's own {args.n}-peer random "
                    f"{args.peers}-peer overlay from root 0 to quiescence ({rounds} rounds), single thread, "
                    f"{dt:.1f} s"),
-    }
+    }, parity
 
 
 def lib_fingerprint():
@@ -222,6 +326,9 @@ def cpu_baseline_allcores(args):
 
 def main():
     args = parse()
+    world, launched = check_world(args)
+    if world > 1 and not launched:
+        sys.exit(launch_ranks(world))
     rank, local, world, pg = dist_setup(args)
     import numpy as np  # noqa: F401
 
@@ -269,9 +376,11 @@ def main():
         sp.exchange_total = {}
     barrier(pg)
     t0 = time.perf_counter()
+    last_stats = None
     for _ in range(args.steps):
         stats, rounds = step()
         rounds_per_step.append(rounds)
+        last_stats = stats
         if sp is None:
             algo_bytes += int(stats["algo_bytes"].sum())
             round_ms += float(stats["kernel_ms"].sum())
@@ -308,6 +417,9 @@ def main():
             exchange_ms_step = float(xt.get("exchange_ms", 0.0)) / args.steps
         exchange = {
             "transport": sp.transport,
+            # the library's own view of the job (RCCL: ncclCommCount / ncclCommUserRank of its communicator)
+            "world": sp.transport_info()["world"],
+            "transport_info": sp.transport_info(),
             "fabric_bytes_per_step": sum_over_ranks(pg, fabric) / args.steps,
             "exchange_ms_per_step_max_rank": max_over_ranks(pg, exchange_ms_step),
             "kernel_ms_per_step_max_rank": max_over_ranks(pg, kernel_ms_step),
@@ -413,7 +525,8 @@ def main():
             if args.no_cpu_full:
                 out["cpu_baseline"] = cpu_baseline(args)
             else:
-                out["cpu_baseline"] = cpu_baseline_full(args)
+                out["cpu_baseline"], out["parity_10m"] = cpu_baseline_full(
+                    args, sim if sp is None else None, last_stats, rounds_per_step[-1])
                 out["cpu_baseline_sample_1m"] = cpu_baseline(args)
             if args.cpu_workers > 1:
                 out["cpu_baseline_allcores"] = cpu_baseline_allcores(args)

@@ -987,6 +987,107 @@ static ERL_NIF_TERM nif_fm_tokens(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     return enif_make_tuple3(env, mk_atom(env, "ok"), tt, enif_make_uint(env, used));
 }
 
+/* ---- full membership on the wire ---------------------------- */
+
+/* [{Src, Dst, Seq, Known, Removed}]: Known / Removed the message's state_orset
+ * as token bitmaps (u64 words, little endian; the cluster module renders the
+ * #full_v1{} term) */
+static ERL_NIF_TERM fm_msg_list(ErlNifEnv* env, const psim_fm_msg* m, const uint64_t* k, const uint64_t* rm, size_t c,
+                                size_t w) {
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (size_t i = c; i > 0; i--) {
+        ERL_NIF_TERM tk, tr;
+        unsigned char* kb = enif_make_new_binary(env, w * 8, &tk);
+        unsigned char* rb = enif_make_new_binary(env, w * 8, &tr);
+        if (kb) memcpy(kb, k + (i - 1) * w, w * 8);
+        if (rb) memcpy(rb, rm + (i - 1) * w, w * 8);
+        const psim_fm_msg* x = &m[i - 1];
+        ERL_NIF_TERM t[5] = {enif_make_uint(env, x->src), enif_make_uint(env, x->dst), enif_make_uint(env, x->seq), tk, tr};
+        list = enif_make_list_cell(env, enif_make_tuple_from_array(env, t, 5), list);
+    }
+    return list;
+}
+
+/* fm_messages(Sim) / fm_take(Sim, Dst) -> {ok, [{Src, Dst, Seq, Known, Removed}]}
+ * in handling order (psim_fm_messages / psim_fm_take) */
+static ERL_NIF_TERM fm_wire(ErlNifEnv* env, const ERL_NIF_TERM argv[], int take) {
+    sim_res* r;
+    unsigned dst = 0;
+    if (!get_res(env, argv[0], &r) || !r->fm_n || (take && !enif_get_uint(env, argv[1], &dst)))
+        return enif_make_badarg(env);
+    const size_t w = r->fm_words;
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_messages(r->h, NULL, NULL, NULL, 0, w, &k);     /* an upper bound for Dst's share */
+    const size_t cap = k ? k : 1;
+    psim_fm_msg* m = rc == PSIM_OK ? (psim_fm_msg*)enif_alloc(cap * sizeof(psim_fm_msg)) : NULL;
+    uint64_t* kw = rc == PSIM_OK ? (uint64_t*)enif_alloc(2 * cap * w * 8) : NULL;
+    if (rc == PSIM_OK && (!m || !kw)) rc = PSIM_ENOMEM;
+    if (rc == PSIM_OK)
+        rc = take ? psim_fm_take(r->h, dst, m, kw, kw + cap * w, cap, w, &k)
+                  : psim_fm_messages(r->h, m, kw, kw + cap * w, cap, w, &k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"),
+                                                        fm_msg_list(env, m, kw, kw + cap * w, k < cap ? k : cap, w))
+                                     : err(env, rc);
+    if (m) enif_free(m);
+    if (kw) enif_free(kw);
+    return out;
+}
+static ERL_NIF_TERM nif_fm_messages(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return fm_wire(env, argv, 0);
+}
+static ERL_NIF_TERM nif_fm_take(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return fm_wire(env, argv, 1);
+}
+
+/* fm_put(Sim, [{Src, Dst, Seq, Known, Removed}]) -> ok: what a simulated node's
+ * manager received (handle_message/2) onto the wire for the next round */
+static ERL_NIF_TERM nif_fm_put(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned len;
+    if (!get_res(env, argv[0], &r) || !r->fm_n || !enif_get_list_length(env, argv[1], &len))
+        return enif_make_badarg(env);
+    const size_t w = r->fm_words, cap = len ? len : 1;
+    psim_fm_msg* m = (psim_fm_msg*)enif_alloc(cap * sizeof(psim_fm_msg));
+    uint64_t* kw = (uint64_t*)enif_alloc(2 * cap * w * 8);
+    if (!m || !kw) {
+        if (m) enif_free(m);
+        if (kw) enif_free(kw);
+        return err(env, PSIM_ENOMEM);
+    }
+    ERL_NIF_TERM list = argv[1], head, tail;
+    size_t i = 0;
+    while (enif_get_list_cell(env, list, &head, &tail)) {
+        const ERL_NIF_TERM* t;
+        int ar;
+        ErlNifBinary kb, rb;
+        unsigned src, dst, seq;
+        if (!enif_get_tuple(env, head, &ar, &t) || ar != 5 || !enif_get_uint(env, t[0], &src) ||
+            !enif_get_uint(env, t[1], &dst) || !enif_get_uint(env, t[2], &seq) ||
+            !enif_inspect_binary(env, t[3], &kb) || !enif_inspect_binary(env, t[4], &rb) || kb.size != w * 8 ||
+            rb.size != w * 8) {
+            enif_free(m);
+            enif_free(kw);
+            return enif_make_badarg(env);
+        }
+        m[i].src = src; m[i].dst = dst; m[i].seq = seq; m[i].reserved = 0;
+        memcpy(kw + i * w, kb.data, w * 8);
+        memcpy(kw + cap * w + i * w, rb.data, w * 8);
+        i++;
+        list = tail;
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_fm_put(r->h, m, kw, kw + cap * w, i, w);
+    enif_mutex_unlock(r->mu);
+    enif_free(m);
+    enif_free(kw);
+    return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
+}
+
 /* ---- C3: Plumtree repair over churning SCAMP v2 ------------------------------- */
 
 /* c3_setup(Sim, N, C, PeriodicRounds) -> ok */
@@ -1314,8 +1415,8 @@ static ErlNifFunc funcs[] = {
     {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_csr", 3, nif_load_csr, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_alive", 2, nif_set_alive, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"reset_trees", 1, nif_reset_trees, 0},
-    {"restart_backend", 2, nif_restart_backend, 0},
+    {"reset_trees", 1, nif_reset_trees, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"restart_backend", 2, nif_restart_backend, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"broadcast", 2, nif_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -1323,7 +1424,7 @@ static ErlNifFunc funcs[] = {
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"trace_hash", 1, nif_trace_hash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"focus", 2, nif_focus, 0},
+    {"focus", 2, nif_focus, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_omissions", 3, nif_set_omissions, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_delays", 4, nif_set_delays, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered_mono", 2, nif_delivered_mono, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -1354,6 +1455,9 @@ static ErlNifFunc funcs[] = {
     {"fm_step", 2, nif_fm_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_state", 1, nif_fm_state, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_tokens", 1, nif_fm_tokens, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_messages", 1, nif_fm_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_take", 2, nif_fm_take, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_put", 2, nif_fm_put, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_setup", 4, nif_c3_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_join", 3, nif_c3_join, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_crash", 2, nif_c3_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -15,6 +15,7 @@
          scamp_setup/5, scamp_join/3, scamp_leave/3, scamp_crash/2, scamp_step/2, scamp_views/1,
          scamp_messages/1, scamp_take/2, scamp_put/2,
          fm_setup/4, fm_join/3, fm_leave/3, fm_step/2, fm_state/1, fm_tokens/1,
+         fm_messages/1, fm_take/2, fm_put/2,
          c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
          causal_setup/6, causal_step/2, causal_clocks/1,
          rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2]).
@@ -184,6 +185,17 @@ fm_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 fm_state(_Sim) -> erlang:nif_error(nif_not_loaded).
 -spec fm_tokens(sim()) -> {ok, binary(), non_neg_integer()} | error().
 fm_tokens(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% The full-membership gossip on the wire (psim_fm_messages / _take / _put):
+%% [{Src, Dst, Seq, Known, Removed}] in handling order, Known / Removed the
+%% message's state_orset as little-endian u64 token bitmaps.
+-spec fm_messages(sim()) -> {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]} | error().
+fm_messages(_Sim) -> erlang:nif_error(nif_not_loaded).
+-spec fm_take(sim(), non_neg_integer()) ->
+          {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]} | error().
+fm_take(_Sim, _Dst) -> erlang:nif_error(nif_not_loaded).
+-spec fm_put(sim(), [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]) -> ok | error().
+fm_put(_Sim, _Msgs) -> erlang:nif_error(nif_not_loaded).
 
 %% ---- C3: Plumtree over churning SCAMP v2 (psim_c3_*) -------------------------
 -spec c3_setup(sim(), pos_integer(), pos_integer(), pos_integer()) -> ok | error().

@@ -12,9 +12,10 @@
 %% partisan_gpu_sim_cluster:outgoing/1 renders them as the manager puts them
 %% on the wire, [{DstSpec, {membership_strategy, Msg}}], and incoming/1 takes
 %% a node's messages off the device.  A {membership_strategy, Msg} the node's
-%% manager receives (SCAMP: forward_subscription, keep_subscription, ping,
-%% remove_subscription, replace_subscription, bootstrap_remove_subscription)
-%% goes onto the device for the node's next round (handle_message/2).
+%% manager receives (full membership: {SenderSpec, #full_v1{}}; SCAMP:
+%% forward_subscription, keep_subscription, ping, remove_subscription,
+%% replace_subscription, bootstrap_remove_subscription) goes onto the device
+%% for the node's next round (handle_message/2).
 %% Members are read back from the device after the interval runs.
 -module(partisan_gpu_sim_membership_strategy).
 
@@ -48,8 +49,12 @@ periodic(#gpu_state{vertex = V} = State) ->
     ok = partisan_gpu_sim_cluster:periodic(V),
     {ok, partisan_gpu_sim_cluster:members(V), [], State}.
 
-%% {membership_strategy, Msg} (pluggable :1739-1808): onto the device for V
-%% (SCAMP strategies; a full-membership state is merged by join/3's path)
+%% {membership_strategy, Msg} (pluggable :1739-1808): onto the device for V --
+%% full membership's {SenderSpec, #full_v1{}} (:135-166) and the SCAMP
+%% strategies' atom-tagged messages
+handle_message({#{name := _}, {full_v1, _, _}} = Msg, #gpu_state{vertex = V} = State) ->
+    ok = partisan_gpu_sim_cluster:deliver(V, Msg),
+    {ok, partisan_gpu_sim_cluster:members(V), [], State};
 handle_message(Msg, #gpu_state{vertex = V} = State) when is_tuple(Msg), is_atom(element(1, Msg)) ->
     ok = partisan_gpu_sim_cluster:deliver(V, Msg),
     {ok, partisan_gpu_sim_cluster:members(V), [], State};

@@ -318,6 +318,10 @@ int  psim_rccl_unique_id(uint8_t* id_out /* PSIM_RCCL_ID_BYTES */);
 /* psim_shard_init + an RCCL communicator of `world` ranks; before psim_load_csr */
 int  psim_shard_init_rccl(psim_handle* h, int rank, int world, const uint8_t* id /* PSIM_RCCL_ID_BYTES */);
 int  psim_shard_set_transport(psim_handle* h, const psim_transport* t);
+/* The handle's exchange: kind 0 none, 1 the library's RCCL communicator,
+ * 2 a caller transport; comm_world / comm_rank as the communicator itself
+ * reports them (ncclCommCount / ncclCommUserRank; -1 for a caller transport). */
+int  psim_shard_transport_info(const psim_handle* h, int* kind, int* comm_world, int* comm_rank);
 /* heartbeat at `root` on every rank (collective): the origin's pushes are
  * exchanged before it returns.  Through this in-library path a sharded
  * handle has heartbeat lanes as on one GPU (one per root, window lanes for a
@@ -529,6 +533,31 @@ int  psim_fm_get_state(const psim_handle* h, uint64_t* known, uint64_t* removed,
 /* token_node[t] = the node token t adds; *used = tokens allocated so far */
 int  psim_fm_tokens(const psim_handle* h, uint32_t* token_node, size_t ntok, uint32_t* used);
 int  psim_fm_inflight(const psim_handle* h, uint64_t* messages);
+/* Full-membership messages on the wire: a node's
+ * gossip leaves its manager as {membership_strategy, {NodeSpec, #full_v1{}}}
+ * to every peer of its state (gossip_messages/2,
+ * partisan_full_membership_strategy.erl:247-267; the manager's sends
+ * partisan_pluggable_peer_service_manager.erl:1396-1407, 1764-1776) and is
+ * handled by handle_message/2 (:135-166).  One record per message the next
+ * round delivers, in handling order (dst, src, seq): seq = the sender's
+ * emission index in its round (a put keeps its own); the #full_v1{}
+ * membership of record i is known[i*words ...] / removed[i*words ...], token
+ * bitmaps as psim_fm_get_state (words = ceil(max_tokens / 64)).
+ * messages: *count = total, records past cap not written (cap 0: count only).
+ * take: the messages for node dst, off the wire (the next round will not
+ * deliver them); PSIM_EINVAL when cap is too small (nothing taken, *count =
+ * what it needs).  put: onto the wire for the next round (what a node's
+ * manager received); src may be any id, one outside the cluster included --
+ * the schedule handles an inbox in (src, seq) order, a put after an
+ * in-flight message of the same (src, seq); a state must hold only tokens
+ * already allocated (psim_fm_tokens), removed ones among the known. */
+typedef struct psim_fm_msg { uint32_t src, dst, seq, reserved; } psim_fm_msg;
+int  psim_fm_messages(const psim_handle* h, psim_fm_msg* out, uint64_t* known, uint64_t* removed, size_t cap,
+                      size_t words, size_t* count);
+int  psim_fm_take(psim_handle* h, uint32_t dst, psim_fm_msg* out, uint64_t* known, uint64_t* removed, size_t cap,
+                  size_t words, size_t* count);
+int  psim_fm_put(psim_handle* h, const psim_fm_msg* msgs, const uint64_t* known, const uint64_t* removed, size_t k,
+                 size_t words);
 
 /* --- SCAMP membership (partisan_scamp_v{1,2}_membership_strategy.erl) ----
  * Nodes 0..n-1 run the strategy inside the pluggable peer service manager.

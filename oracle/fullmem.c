@@ -104,6 +104,12 @@ static void put_tok(oel* e, uint64_t tok, uint8_t act) {
     e->nt++;
 }
 
+/* one (Elem, Token, Active) entry of a payload, as a received state carries it */
+int orc_orset_put(orc_orset* s, uint32_t elem, uint64_t token, uint8_t active) {
+    put_tok(insert_el(s, elem), token, active ? 1 : 0);
+    return ORC_OK;
+}
+
 /* state_orset:mutate({add, Elem}, Actor, S) via partisan_membership_set:add/3 (:125-127) */
 int orc_orset_add(orc_orset* s, uint32_t elem, uint64_t token) {
     put_tok(insert_el(s, elem), token, 1);
@@ -178,7 +184,7 @@ static int is_member(const orc_orset* s, uint32_t v) {
 /* ------------------------------------------------------------------------ */
 /* the round-synchronous full-membership simulation                          */
 /* ------------------------------------------------------------------------ */
-typedef struct { uint32_t src, dst; uint64_t seq; orc_orset* st; } fmmsg;
+typedef struct { uint32_t src, dst; uint64_t seq, ord; orc_orset* st; } fmmsg;   /* ord: arrival, breaks (src, seq) ties */
 typedef struct { uint32_t v, peer; uint64_t tok; } fmpair;
 
 struct orc_fullmem {
@@ -190,6 +196,7 @@ struct orc_fullmem {
     uint64_t* seq;
     fmmsg* cur; size_t ncur, capcur;
     fmmsg* nxt; size_t nnxt, capnxt;
+    uint64_t nord;
     fmpair* jq; size_t njq, capjq;
     fmpair* lq; size_t nlq, caplq;
     orc_fm_stats* stt;
@@ -247,7 +254,7 @@ static void gossip(orc_fullmem* s, uint32_t v, const orc_orset* peers_of, const 
         if (!s->alive0[p]) continue;                 /* lost (never connected) */
         if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? 2 * s->capnxt : 256; s->nxt = (fmmsg*)realloc(s->nxt, s->capnxt * sizeof(fmmsg)); }
         fmmsg* m = &s->nxt[s->nnxt++];
-        m->src = v; m->dst = p; m->seq = q; m->st = orc_orset_clone(st);
+        m->src = v; m->dst = p; m->seq = q; m->ord = s->nord++; m->st = orc_orset_clone(st);
     }
 }
 
@@ -269,7 +276,8 @@ static int cmp_msg(const void* a, const void* b) {
     const fmmsg *x = (const fmmsg*)a, *y = (const fmmsg*)b;
     if (x->dst != y->dst) return x->dst < y->dst ? -1 : 1;
     if (x->src != y->src) return x->src < y->src ? -1 : 1;
-    return x->seq < y->seq ? -1 : x->seq > y->seq;
+    if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+    return x->ord < y->ord ? -1 : x->ord > y->ord;
 }
 
 static void one_round(orc_fullmem* s) {
@@ -350,6 +358,48 @@ uint32_t orc_fm_step(orc_fullmem* s, uint32_t rounds, orc_fm_stats* st) {
 }
 
 size_t orc_fm_inflight(const orc_fullmem* s) { return s->nnxt; }
+
+/* The messages on the wire (the pluggable manager's {membership_strategy,
+ * {NodeSpec, #full_v1{}}} sends, partisan_full_membership_strategy.erl:247-267)
+ * in handling order (dst, src, seq); their states via orc_fm_message_state. */
+size_t orc_fm_messages(orc_fullmem* s, uint32_t* src, uint32_t* dst, uint64_t* seq, size_t cap) {
+    qsort(s->nxt, s->nnxt, sizeof(fmmsg), cmp_msg);
+    for (size_t i = 0; i < s->nnxt && i < cap; i++) {
+        if (src) src[i] = s->nxt[i].src;
+        if (dst) dst[i] = s->nxt[i].dst;
+        if (seq) seq[i] = s->nxt[i].seq;
+    }
+    return s->nnxt;
+}
+
+const orc_orset* orc_fm_message_state(const orc_fullmem* s, size_t i) { return i < s->nnxt ? s->nxt[i].st : NULL; }
+
+/* dst's messages off the wire, in handling order; the caller owns st[i].
+ * More than cap: nothing is taken. */
+size_t orc_fm_take(orc_fullmem* s, uint32_t dst, uint32_t* src, uint64_t* seq, orc_orset** st, size_t cap) {
+    qsort(s->nxt, s->nnxt, sizeof(fmmsg), cmp_msg);
+    size_t c = 0;
+    for (size_t i = 0; i < s->nnxt; i++) c += s->nxt[i].dst == dst;
+    if (c > cap) return c;
+    size_t k = 0, o = 0;
+    for (size_t i = 0; i < s->nnxt; i++) {
+        if (s->nxt[i].dst == dst) {
+            src[k] = s->nxt[i].src; seq[k] = s->nxt[i].seq; st[k] = s->nxt[i].st;
+            k++;
+        } else {
+            s->nxt[o++] = s->nxt[i];
+        }
+    }
+    s->nnxt = o;
+    return c;
+}
+
+/* a message a manager received, onto the wire for the next round (the state is copied) */
+void orc_fm_put(orc_fullmem* s, uint32_t src, uint32_t dst, uint64_t seq, const orc_orset* st) {
+    if (s->nnxt == s->capnxt) { s->capnxt = s->capnxt ? 2 * s->capnxt : 256; s->nxt = (fmmsg*)realloc(s->nxt, s->capnxt * sizeof(fmmsg)); }
+    fmmsg* m = &s->nxt[s->nnxt++];
+    m->src = src; m->dst = dst; m->seq = seq; m->ord = s->nord++; m->st = orc_orset_clone(st);
+}
 
 size_t orc_fm_members(const orc_fullmem* s, uint32_t v, uint32_t* out, size_t cap) {
     return orc_orset_to_list(s->st[v], out, cap);

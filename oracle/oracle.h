@@ -269,6 +269,7 @@ orc_orset* orc_orset_clone(const orc_orset* s);
 void orc_orset_free(orc_orset* s);
 int orc_orset_add(orc_orset* s, uint32_t elem, uint64_t token);
 int orc_orset_remove(orc_orset* s, uint32_t elem);          /* ORC_BADARG if absent */
+int orc_orset_put(orc_orset* s, uint32_t elem, uint64_t token, uint8_t active);
 orc_orset* orc_orset_merge(const orc_orset* a, const orc_orset* b);
 int orc_orset_equal(const orc_orset* a, const orc_orset* b);
 size_t orc_orset_to_list(const orc_orset* s, uint32_t* out, size_t cap);
@@ -293,6 +294,11 @@ size_t orc_fm_inflight(const orc_fullmem* s);
 size_t orc_fm_members(const orc_fullmem* s, uint32_t v, uint32_t* out, size_t cap);
 const orc_orset* orc_fm_state(const orc_fullmem* s, uint32_t v);
 int orc_fm_alive(const orc_fullmem* s, uint32_t v);
+/* the wire: in handling order (dst, src, seq); take hands the states to the caller */
+size_t orc_fm_messages(orc_fullmem* s, uint32_t* src, uint32_t* dst, uint64_t* seq, size_t cap);
+const orc_orset* orc_fm_message_state(const orc_fullmem* s, size_t i);
+size_t orc_fm_take(orc_fullmem* s, uint32_t dst, uint32_t* src, uint64_t* seq, orc_orset** st, size_t cap);
+void orc_fm_put(orc_fullmem* s, uint32_t src, uint32_t dst, uint64_t seq, const orc_orset* st);
 
 /* ------------------------------------------------------------------ */
 /* SCAMP v1 / v2 membership strategies (partisan_scamp_v{1,2}_membership_strategy.erl) */

@@ -250,6 +250,14 @@ def lib():
         L.orc_fm_state.argtypes = [C.c_void_p, C.c_uint32]
         L.orc_fm_state.restype = C.c_void_p
         L.orc_fm_alive.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_orset_put.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint8]
+        L.orc_fm_messages.argtypes = [C.c_void_p, P(C.c_uint32), P(C.c_uint32), P(C.c_uint64), sz]
+        L.orc_fm_messages.restype = sz
+        L.orc_fm_message_state.argtypes = [C.c_void_p, sz]
+        L.orc_fm_message_state.restype = C.c_void_p
+        L.orc_fm_take.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint64), P(C.c_void_p), sz]
+        L.orc_fm_take.restype = sz
+        L.orc_fm_put.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p]
         L.orc_scamp_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]
         L.orc_scamp_create.restype = C.c_void_p
         L.orc_scamp_destroy.argtypes = [C.c_void_p]
@@ -877,11 +885,41 @@ class FullMembership:
 
     def payload(self, v):
         """(elem, token, active) rows of node v's state_orset."""
-        h = lib().orc_fm_state(self._h, v)
-        cap = 65536
-        e, t, a = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_uint8 * cap)()
-        k = lib().orc_orset_dump(h, e, t, a, cap)
-        return [(e[i], t[i], bool(a[i])) for i in range(min(k, cap))]
+        return _dump_orset(lib().orc_fm_state(self._h, v))
+
+    def messages(self):
+        """The wire: [(src, dst, seq, payload rows)] in handling order (dst, src, seq)."""
+        k = lib().orc_fm_messages(self._h, None, None, None, 0)
+        src, dst, seq = (C.c_uint32 * max(1, k))(), (C.c_uint32 * max(1, k))(), (C.c_uint64 * max(1, k))()
+        lib().orc_fm_messages(self._h, src, dst, seq, k)
+        return [(src[i], dst[i], seq[i], _dump_orset(lib().orc_fm_message_state(self._h, i))) for i in range(k)]
+
+    def take(self, dst, cap=1 << 16):
+        """dst's messages off the wire: [(src, dst, seq, payload rows)] in handling order."""
+        src, seq, st = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_void_p * cap)()
+        k = lib().orc_fm_take(self._h, dst, src, seq, st, cap)
+        assert k <= cap
+        out = []
+        for i in range(k):
+            out.append((src[i], dst, seq[i], _dump_orset(st[i])))
+            lib().orc_orset_free(st[i])
+        return out
+
+    def put(self, msgs):
+        """[(src, dst, seq, payload rows)] onto the wire for the next round."""
+        for src, dst, seq, rows in msgs:
+            h = lib().orc_orset_new()
+            for e, t, a in rows:
+                lib().orc_orset_put(h, e, t, 1 if a else 0)
+            lib().orc_fm_put(self._h, src, dst, seq, h)
+            lib().orc_orset_free(h)
+
+
+def _dump_orset(h, cap=65536):
+    """(elem, token, active) rows of a state_orset handle."""
+    e, t, a = (C.c_uint32 * cap)(), (C.c_uint64 * cap)(), (C.c_uint8 * cap)()
+    k = lib().orc_orset_dump(h, e, t, a, cap)
+    return [(e[i], t[i], bool(a[i])) for i in range(min(k, cap))]
 
 
 # ---------------------------------------------------------------- SCAMP

@@ -28,6 +28,10 @@ class PsimError(RuntimeError):
         super().__init__(f"{self.name}: {detail}" if detail else self.name)
 
 
+class FmMsg(C.Structure):
+    _fields_ = [("src", C.c_uint32), ("dst", C.c_uint32), ("seq", C.c_uint32), ("reserved", C.c_uint32)]
+
+
 class Config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("lazy_tick_rounds", C.c_uint32),
                 ("exchange_tick_rounds", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32),
@@ -207,6 +211,7 @@ SIGNATURES = {
     "psim_rccl_unique_id": (C.c_int, [_P(C.c_uint8)]),
     "psim_shard_init_rccl": (C.c_int, [_H, C.c_int, C.c_int, _P(C.c_uint8)]),
     "psim_shard_set_transport": (C.c_int, [_H, _P(Transport)]),
+    "psim_shard_transport_info": (C.c_int, [_H, _P(C.c_int), _P(C.c_int), _P(C.c_int)]),
     "psim_shard_broadcast_x": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
     "psim_shard_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32), _P(ExchangeStats)]),
     "psim_shard_step": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(ExchangeStats)]),
@@ -252,6 +257,11 @@ SIGNATURES = {
     "psim_fm_get_state": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint64), _P(C.c_uint8), C.c_size_t, C.c_size_t]),
     "psim_fm_tokens": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t, _P(C.c_uint32)]),
     "psim_fm_inflight": (C.c_int, [_H, _P(C.c_uint64)]),
+    "psim_fm_messages": (C.c_int, [_H, _P(FmMsg), _P(C.c_uint64), _P(C.c_uint64), C.c_size_t, C.c_size_t,
+                              _P(C.c_size_t)]),
+    "psim_fm_take": (C.c_int, [_H, C.c_uint32, _P(FmMsg), _P(C.c_uint64), _P(C.c_uint64), C.c_size_t, C.c_size_t,
+                          _P(C.c_size_t)]),
+    "psim_fm_put": (C.c_int, [_H, _P(FmMsg), _P(C.c_uint64), _P(C.c_uint64), C.c_size_t, C.c_size_t]),
     "psim_scamp_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_scamp_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_scamp_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

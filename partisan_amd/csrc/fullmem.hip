@@ -251,6 +251,9 @@ struct FmState : ModuleState {
     size_t snap_cap[2] = {0, 0}, list_cap = 0;
     uint32_t S = 0, par = 0;
     uint64_t round = 0;
+    // seq of each in-flight snapshot when psim_fm_put placed some (empty: the
+    // sender's emission index, i.e. the position inside its run of snapshots)
+    std::vector<uint32_t> hseq;
     std::vector<uint32_t> jv, jpeer, lv, lwho, ltok;   // calls made since the last round
     ~FmState() override {
         void* p[] = {st[0], st[1], snap_st[0], snap_st[1], snap_p[0], snap_p[1], alive_bm, stats, alive[0], alive[1],
@@ -371,7 +374,57 @@ int fm_round(psim_handle* h, FmState& f, psim_fm_stats* out) {
     f.S = total;
     f.par ^= 1u;
     f.round = t;
+    f.hseq.clear();
     return PSIM_OK;
+}
+
+// The in-flight snapshots on the host: states [S][2W], recipients [S][NW], src, seq.
+struct FmWire {
+    std::vector<unsigned long long> st, p;
+    std::vector<uint32_t> src, seq;
+};
+
+int fm_download(psim_handle* h, const FmState& f, FmWire& w) {
+    const size_t S = f.S, L = 2 * f.W;
+    w.st.resize(S * L);
+    w.p.resize(S * f.NW);
+    w.src.resize(S);
+    if (S) {
+        FMCHK(h, hipMemcpy(w.st.data(), f.snap_st[f.par], w.st.size() * 8, hipMemcpyDeviceToHost));
+        FMCHK(h, hipMemcpy(w.p.data(), f.snap_p[f.par], w.p.size() * 8, hipMemcpyDeviceToHost));
+        FMCHK(h, hipMemcpy(w.src.data(), f.snap_src[f.par], S * 4, hipMemcpyDeviceToHost));
+    }
+    if (f.hseq.size() == S) {
+        w.seq = f.hseq;
+    } else {                      // emission index: position inside the sender's run (storage is (src, seq) order)
+        w.seq.resize(S);
+        for (size_t k = 0; k < S; k++) w.seq[k] = (k && w.src[k - 1] == w.src[k]) ? w.seq[k - 1] + 1 : 0;
+    }
+    return PSIM_OK;
+}
+
+// the messages of the snapshots to `dst` (or every recipient: dst = ~0u) in
+// handling order (dst, src, seq); take: clear the recipients' bits
+size_t fm_collect(const FmState& f, FmWire& w, uint32_t dst, bool take, psim_fm_msg* out, uint64_t* known,
+                  uint64_t* removed, size_t cap) {
+    const size_t L = 2 * f.W;
+    size_t c = 0;
+    const uint32_t lo = dst == ~0u ? 0 : dst, hi = dst == ~0u ? f.n : dst + 1;
+    for (uint32_t d = lo; d < hi; d++)
+        for (size_t k = 0; k < f.S; k++) {
+            unsigned long long& b = w.p[k * f.NW + (d >> 6)];
+            if (!((b >> (d & 63)) & 1ull)) continue;
+            if (c < cap) {
+                if (out) out[c] = psim_fm_msg{w.src[k], d, w.seq[k], 0u};
+                for (uint32_t j = 0; j < f.W; j++) {
+                    if (known) known[c * f.W + j] = w.st[k * L + j];
+                    if (removed) removed[c * f.W + j] = w.st[k * L + f.W + j];
+                }
+            }
+            if (take) b &= ~(1ull << (d & 63));
+            c++;
+        }
+    return c;
 }
 
 }  // namespace
@@ -505,6 +558,110 @@ int psim_fm_tokens(const psim_handle* h, uint32_t* token_node, size_t ntok, uint
     if (token_node)
         for (size_t t = 0; t < ntok && t < f->T; t++) token_node[t] = f->h_elem[t];
     if (used) *used = f->next_tok;
+    return PSIM_OK;
+}
+
+int psim_fm_messages(const psim_handle* h, psim_fm_msg* out, uint64_t* known, uint64_t* removed, size_t cap,
+                     size_t words, size_t* count) {
+    if (!h || !count || (cap && (!out || !known || !removed))) return PSIM_EINVAL;
+    const FmState* f = fm_of(h);
+    if (!f) return PSIM_ESTATE;
+    psim_handle* hh = const_cast<psim_handle*>(h);
+    if (cap && words != f->W) return handle_fail(hh, PSIM_EINVAL, "want words=%u", f->W);
+    FMCHK(hh, hipSetDevice(handle_device(h)));
+    FMCHK(hh, hipStreamSynchronize(handle_stream(h)));
+    FmWire w;
+    const int rc = fm_download(hh, *f, w);
+    if (rc) return rc;
+    *count = fm_collect(*f, w, ~0u, false, out, known, removed, cap);
+    return PSIM_OK;
+}
+
+int psim_fm_take(psim_handle* h, uint32_t dst, psim_fm_msg* out, uint64_t* known, uint64_t* removed, size_t cap,
+                 size_t words, size_t* count) {
+    if (!h || !count || (cap && (!out || !known || !removed))) return PSIM_EINVAL;
+    FmState* f = fm_of(h);
+    if (!f) return PSIM_ESTATE;
+    if (dst >= f->n) return handle_fail(h, PSIM_EINVAL, "take: node %u of %u", dst, f->n);
+    if (cap && words != f->W) return handle_fail(h, PSIM_EINVAL, "want words=%u", f->W);
+    FMCHK(h, hipSetDevice(handle_device(h)));
+    FMCHK(h, hipStreamSynchronize(handle_stream(h)));
+    FmWire w;
+    int rc = fm_download(h, *f, w);
+    if (rc) return rc;
+    const size_t need = fm_collect(*f, w, dst, false, nullptr, nullptr, nullptr, 0);
+    *count = need;
+    if (need > cap) return handle_fail(h, PSIM_EINVAL, "take: %zu messages for node %u, room for %zu", need, dst, cap);
+    fm_collect(*f, w, dst, true, out, known, removed, cap);
+    if (f->S) FMCHK(h, hipMemcpy(f->snap_p[f->par], w.p.data(), w.p.size() * 8, hipMemcpyHostToDevice));
+    return PSIM_OK;
+}
+
+int psim_fm_put(psim_handle* h, const psim_fm_msg* msgs, const uint64_t* known, const uint64_t* removed, size_t k,
+                size_t words) {
+    if (!h || (k && (!msgs || !known || !removed))) return PSIM_EINVAL;
+    FmState* f = fm_of(h);
+    if (!f) return PSIM_ESTATE;
+    if (!k) return PSIM_OK;
+    if (words != f->W) return handle_fail(h, PSIM_EINVAL, "want words=%u", f->W);
+    for (size_t i = 0; i < k; i++) {
+        if (msgs[i].dst >= f->n) return handle_fail(h, PSIM_EINVAL, "put %zu: node %u of %u", i, msgs[i].dst, f->n);
+        for (uint32_t j = 0; j < f->W; j++) {
+            const unsigned long long K = known[i * f->W + j], R = removed[i * f->W + j];
+            // a state over the tokens allocated so far; removed tokens are present ones (state_orset)
+            const uint32_t t0 = 64 * j;
+            const unsigned long long alloc = f->next_tok <= t0 ? 0ull
+                                           : f->next_tok >= t0 + 64 ? ~0ull : (1ull << (f->next_tok - t0)) - 1ull;
+            if ((K & ~alloc) || (R & ~K))
+                return handle_fail(h, PSIM_EINVAL, "put %zu: a token outside the cluster's universe", i);
+        }
+    }
+    FMCHK(h, hipSetDevice(handle_device(h)));
+    FMCHK(h, hipStreamSynchronize(handle_stream(h)));
+    FmWire w;
+    int rc = fm_download(h, *f, w);
+    if (rc) return rc;
+    // merge: storage (= handling) order is (src, seq), a put after existing ties
+    const size_t S0 = f->S, S1 = S0 + k, L = 2 * f->W;
+    std::vector<size_t> add(k);
+    for (size_t i = 0; i < k; i++) add[i] = i;
+    std::stable_sort(add.begin(), add.end(), [&](size_t x, size_t y) {
+        return msgs[x].src != msgs[y].src ? msgs[x].src < msgs[y].src : msgs[x].seq < msgs[y].seq;
+    });
+    FmWire m;
+    m.st.resize(S1 * L);
+    m.p.assign(S1 * f->NW, 0ull);
+    m.src.resize(S1);
+    m.seq.resize(S1);
+    size_t a = 0, b = 0;
+    for (size_t o = 0; o < S1; o++) {
+        const bool old = b == k || (a < S0 && (w.src[a] != msgs[add[b]].src ? w.src[a] < msgs[add[b]].src
+                                                                           : w.seq[a] <= msgs[add[b]].seq));
+        if (old) {
+            std::copy(w.st.begin() + a * L, w.st.begin() + (a + 1) * L, m.st.begin() + o * L);
+            std::copy(w.p.begin() + a * f->NW, w.p.begin() + (a + 1) * f->NW, m.p.begin() + o * f->NW);
+            m.src[o] = w.src[a];
+            m.seq[o] = w.seq[a];
+            a++;
+        } else {
+            const psim_fm_msg& x = msgs[add[b]];
+            for (uint32_t j = 0; j < f->W; j++) {
+                m.st[o * L + j] = known[add[b] * f->W + j];
+                m.st[o * L + f->W + j] = removed[add[b] * f->W + j];
+            }
+            m.p[o * f->NW + (x.dst >> 6)] = 1ull << (x.dst & 63);
+            m.src[o] = x.src;
+            m.seq[o] = x.seq;
+            b++;
+        }
+    }
+    rc = fm_reserve(h, *f, f->par, S1);
+    if (rc) return rc;
+    FMCHK(h, hipMemcpy(f->snap_st[f->par], m.st.data(), m.st.size() * 8, hipMemcpyHostToDevice));
+    FMCHK(h, hipMemcpy(f->snap_p[f->par], m.p.data(), m.p.size() * 8, hipMemcpyHostToDevice));
+    FMCHK(h, hipMemcpy(f->snap_src[f->par], m.src.data(), S1 * 4, hipMemcpyHostToDevice));
+    f->S = (uint32_t)S1;
+    f->hseq = m.seq;
     return PSIM_OK;
 }
 

@@ -1512,6 +1512,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->epoch = 1;
     h->have_root = false;
     h->mono_of.clear();
+    h->next_epoch.clear();
     h->ost_cnt = h->live_rows = 0;
     h->inflight = 0;
     return PSIM_OK;
@@ -1562,7 +1563,6 @@ int psim_plumtree_restart_backend(psim_handle* h, uint32_t v) {
     const auto ne = h->next_epoch.find(v);
     const uint32_t e = (ne == h->next_epoch.end() ? cur : ne->second) + 1u;
     if (e > 0xFFu) return fail(h, PSIM_EOVERFLOW, "vertex %u: 255 backend restarts", v);
-    h->next_epoch[v] = e;
     const uint32_t lv = v - h->sh.v_lo;
     const int focus = h->cur_lane;
     if (!h->lanes.empty()) save_lane(h);
@@ -1583,6 +1583,7 @@ int psim_plumtree_restart_backend(psim_handle* h, uint32_t v) {
     }
     if (!h->lanes.empty()) load_lane(h, focus);
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->next_epoch[v] = e;     // only once every lane forgot: a failed restart leaves the epoch alone
     return PSIM_OK;
 }
 
@@ -2811,10 +2812,21 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
+    int64_t busy = 0;
     for (const auto& l : h->lanes) {
-        if (l.inflight) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
         if (l.win) return fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
+        busy += (int64_t)l.inflight;
     }
+    if (h->sh.world > 1) {
+        // collective: every rank must return the same code, and a shard's own
+        // in-flight count says nothing about the others' (ADVICE r3), so the
+        // decision is taken on the global sum before any state changes
+        if (!h->sh.xport) return fail(h, PSIM_ESTATE, "delay faults on a sharded handle need the in-library exchange");
+        std::string err;
+        const int rc = h->sh.xport->allreduce(&busy, 1, h->stream, &err);
+        if (rc) return fail(h, rc, "delay all-reduce: %s", err.c_str());
+    }
+    if (busy) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
     // every shard installs the table (its own senders' pairs) and the ring,
     // so a delayed word from any shard finds its receiver's inbox ring
     std::vector<uint8_t> dl(h->Ed, 0);
@@ -2871,6 +2883,15 @@ int psim_trace_hash(const psim_handle* h, uint64_t* out) {
     out[1] = r[1];
     out[2] = r[2];
     out[3] = h->round;
+    return PSIM_OK;
+}
+
+int psim_shard_transport_info(const psim_handle* h, int* kind, int* comm_world, int* comm_rank) {
+    if (!h) return PSIM_EINVAL;
+    const psim::Transport* t = h->sh.xport;
+    if (kind) *kind = !t ? 0 : (std::string(t->name()) == "rccl" ? 1 : 2);
+    if (comm_world) *comm_world = t ? t->comm_size() : -1;
+    if (comm_rank) *comm_rank = t ? t->comm_rank() : -1;
     return PSIM_OK;
 }
 

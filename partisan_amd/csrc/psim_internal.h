@@ -539,6 +539,10 @@ struct Transport {
     // host values, in place, summed over ranks (synchronous)
     virtual int allreduce(int64_t* vals, size_t n, hipStream_t s, std::string* err) = 0;
     virtual const char* name() const = 0;
+    // the transport's own view of the job: RCCL asks its communicator
+    // (ncclCommCount / ncclCommUserRank); a callback transport reports -1
+    virtual int comm_size() const { return -1; }
+    virtual int comm_rank() const { return -1; }
 };
 int make_rccl_transport(int device, int rank, int world, const void* id, Transport** out, std::string* err);
 Transport* make_callback_transport(const psim_transport& t);

@@ -45,7 +45,7 @@ struct Ctx {
     PdRow* rows;                   // outstanding rows in HBM
     const uint32_t* pv;            // SCAMP partial view row
     uint32_t npv;
-    unsigned long long sent;       // 12 bits per message kind 1..5 (kind k at bit 12 k)
+    unsigned long long sent;       // 12 bits per message kind 1..5 (kind k at bit 12 (k - 1): 60 bits)
     uint32_t dropped, deliv, err;
 };
 
@@ -60,7 +60,9 @@ __device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t
     if (!connected(c, t)) { c.dropped++; return; }
     const PdArgs& a = *c.a;
     const uint32_t pos = wave_reserve(a.nout);
-    c.sent += 1ull << (12u * type);
+    const uint32_t sh = 12u * (type - 1u);
+    if (((c.sent >> sh) & 0xFFFull) == 0xFFFull) c.err |= 16u;   // a 13th bit would carry into the next kind
+    else c.sent += 1ull << sh;
     if (pos >= a.out_cap) { c.err |= 1u; return; }
     PdMsg m;
     m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.mono = mono;
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
         if (c.h.ntab > kPdTab - 8) tab_compact(c);
         store(c);
 #pragma unroll
-        for (int i = 1; i <= 5; i++) vals[i] = (c.sent >> (12 * i)) & 0xFFFull;
+        for (int i = 1; i <= 5; i++) vals[i] = (c.sent >> (12 * (i - 1))) & 0xFFFull;
         vals[6] = c.dropped;
         vals[7] = c.deliv;
         vals[9] = c.err;
@@ -536,6 +538,8 @@ int pd_check(psim_handle* h, unsigned long long err, uint64_t round) {
                                        (unsigned long long)round, kPdRows);
     if (err & 8ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a heartbeat older than 64 serials is still in flight",
                                        (unsigned long long)round);
+    if (err & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a vertex sent more than 4095 messages of one kind",
+                                        (unsigned long long)round);
     return PSIM_OK;
 }
 

@@ -83,6 +83,14 @@ class RcclTransport : public Transport {
     }
 
     const char* name() const override { return "rccl"; }
+    int comm_size() const override {
+        int c = -1;
+        return comm && ncclCommCount(comm, &c) == ncclSuccess ? c : -1;
+    }
+    int comm_rank() const override {
+        int r = -1;
+        return comm && ncclCommUserRank(comm, &r) == ncclSuccess ? r : -1;
+    }
 };
 
 class CallbackTransport : public Transport {

@@ -12,6 +12,11 @@ Host mirror of what the pluggable peer service manager does with the
   * ``step(rounds)``    -- deliveries to handle_message/2 (:1739-1808) and the
                            periodic/1 timer (:1386-1419)
   * ``members(v)``      -- the manager's `members` (partisan_membership_set:to_list)
+  * ``messages()`` / ``take(v)`` / ``put(msgs)`` -- the gossip on the wire,
+                           {membership_strategy, {NodeSpec, #full_v1{}}}
+                           (gossip_messages/2 :247-267, handle_message/2
+                           :135-166): what the manager sends, what node v's
+                           manager receives, what it hands back to the device
 
 Each node's membership is a state_orset (partisan_membership_set) held on the
 device as two token bitmaps (known / removed); see fullmem.hip.
@@ -20,7 +25,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import FmStats, check, lib
+from ._lib import FmMsg, FmStats, check, lib
 
 _P = C.POINTER
 
@@ -87,3 +92,44 @@ class FullMembershipCluster:
         x = C.c_uint64()
         self._c(lib().psim_fm_inflight(self.sim._h, C.byref(x)))
         return x.value
+
+    # ---------------------------------------------------------------- wire
+    def _unpack(self, m, K, R, k):
+        return [(int(m[i].src), int(m[i].dst), int(m[i].seq), K[i].copy(), R[i].copy()) for i in range(k)]
+
+    def messages(self):
+        """[(src, dst, seq, known[words], removed[words])] the next round delivers, in handling order."""
+        k = C.c_size_t()
+        self._c(lib().psim_fm_messages(self.sim._h, None, None, None, 0, self.words, C.byref(k)))
+        n = k.value
+        m = (FmMsg * max(1, n))()
+        K = np.zeros((max(1, n), self.words), np.uint64)
+        R = np.zeros((max(1, n), self.words), np.uint64)
+        self._c(lib().psim_fm_messages(self.sim._h, m, K.ctypes.data_as(_P(C.c_uint64)),
+                                       R.ctypes.data_as(_P(C.c_uint64)), n, self.words, C.byref(k)))
+        return self._unpack(m, K, R, min(n, k.value))
+
+    def take(self, v):
+        """Node v's messages off the wire (its manager receives them), in handling order."""
+        cap = max(1, self.inflight())
+        k = C.c_size_t()
+        m = (FmMsg * cap)()
+        K = np.zeros((cap, self.words), np.uint64)
+        R = np.zeros((cap, self.words), np.uint64)
+        self._c(lib().psim_fm_take(self.sim._h, v, m, K.ctypes.data_as(_P(C.c_uint64)),
+                                   R.ctypes.data_as(_P(C.c_uint64)), cap, self.words, C.byref(k)))
+        return self._unpack(m, K, R, k.value)
+
+    def put(self, msgs):
+        """[(src, dst, seq, known, removed)] onto the wire for the next round."""
+        k = len(msgs)
+        if not k:
+            return
+        m = (FmMsg * k)()
+        K = np.zeros((k, self.words), np.uint64)
+        R = np.zeros((k, self.words), np.uint64)
+        for i, (src, dst, seq, kn, rm) in enumerate(msgs):
+            m[i].src, m[i].dst, m[i].seq = src, dst, seq
+            K[i], R[i] = kn, rm
+        self._c(lib().psim_fm_put(self.sim._h, m, K.ctypes.data_as(_P(C.c_uint64)),
+                                  R.ctypes.data_as(_P(C.c_uint64)), k, self.words))

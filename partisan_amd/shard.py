@@ -115,6 +115,13 @@ class ShardedPlumtree:
             check(lib().psim_set_stream(self._h, C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)),
                   self._h)
 
+    def transport_info(self):
+        """{"kind", "world", "rank"} of the handle's exchange as the library
+        reports it; for RCCL world / rank come from the communicator itself."""
+        kind, w, r = C.c_int(), C.c_int(), C.c_int()
+        check(lib().psim_shard_transport_info(self._h, C.byref(kind), C.byref(w), C.byref(r)), self._h)
+        return {"kind": {0: "none", 1: "rccl", 2: "callback"}[kind.value], "world": w.value, "rank": r.value}
+
     # -------------------------------------------------------------- exchange
     def _allreduce(self, vals):
         t = torch.tensor(vals, dtype=torch.int64, device=self.dev if self.backend == "nccl" else "cpu")

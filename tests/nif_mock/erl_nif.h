@@ -47,6 +47,7 @@ int enif_get_uint(ErlNifEnv*, ERL_NIF_TERM, unsigned*);
 int enif_get_uint64(ErlNifEnv*, ERL_NIF_TERM, ErlNifUInt64*);
 int enif_inspect_binary(ErlNifEnv*, ERL_NIF_TERM, ErlNifBinary*);
 int enif_get_list_cell(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM*, ERL_NIF_TERM*);
+int enif_get_list_length(ErlNifEnv*, ERL_NIF_TERM, unsigned*);
 int enif_get_tuple(ErlNifEnv*, ERL_NIF_TERM, int*, const ERL_NIF_TERM**);
 ErlNifResourceType* enif_open_resource_type(ErlNifEnv*, const char*, const char*, ErlNifResourceDtor*,
                                             ErlNifResourceFlags, ErlNifResourceFlags*);

@@ -244,6 +244,18 @@ int enif_get_list_cell(ErlNifEnv* env, ERL_NIF_TERM list, ERL_NIF_TERM* head, ER
     return 1;
 }
 
+int enif_get_list_length(ErlNifEnv* env, ERL_NIF_TERM list, unsigned* len) {
+    (void)env;
+    unsigned n = 0;
+    while (T(list)->tag == T_CONS) {
+        n++;
+        list = T(list)->a[1];
+    }
+    if (T(list)->tag != T_NIL) return 0;
+    *len = n;
+    return 1;
+}
+
 int enif_get_tuple(ErlNifEnv* env, ERL_NIF_TERM t, int* arity, const ERL_NIF_TERM** items) {
     (void)env;
     term_t* x = T(t);

@@ -284,6 +284,58 @@ int main(int argc, char** argv) {
         fprintf(g_out, ", \"fullmem\": {\"n\": %u, \"knows_all\": %llu, \"tokens_used\": %llu, \"own_tokens\": %llu}", n,
                (unsigned long long)full, (unsigned long long)mock_int(mock_elem(tk, 2)), (unsigned long long)ident);
     }
+    /* ---- full membership on the wire: {membership_strategy, {Spec, #full_v1{}}} --- */
+    {
+        const uint32_t n = 12;
+        ERL_NIF_TERM sim = new_sim(0x5EED0001ull);
+        want_ok("fm_setup", call("fm_setup", 4, A(sim, mock_uint(n), mock_uint(3), mock_uint(64))));
+        uint32_t v[11], p[11];
+        for (uint32_t i = 1; i < n; i++) {
+            v[i - 1] = i;
+            p[i - 1] = i - 1;
+        }
+        want_ok("fm_join", call("fm_join", 3, A(sim, u32s(v, 11), u32s(p, 11))));
+        fprintf(g_out, ", \"fm_wire\": {\"n\": %u, \"rounds\": [", n);
+        uint64_t taken = 0;
+        for (int r = 0; r < 8; r++) {
+            want_ok_tuple("fm_step", call("fm_step", 2, A(sim, mock_uint(1))));
+            ERL_NIF_TERM ms = mock_elem(want_ok_tuple("fm_messages", call("fm_messages", 1, A(sim))), 1);
+            fprintf(g_out, "%s[", r ? ", " : "");
+            for (size_t i = 0; i < mock_list_len(ms); i++) {
+                ERL_NIF_TERM m = mock_list_nth(ms, i);             /* {Src, Dst, Seq, Known, Removed} */
+                size_t kz, rz;
+                const uint64_t* kw = (const uint64_t*)mock_bin_data(mock_elem(m, 3), &kz);
+                const uint64_t* rw = (const uint64_t*)mock_bin_data(mock_elem(m, 4), &rz);
+                fprintf(g_out, "%s[%llu, %llu, %llu, %llu]", i ? ", " : "", (unsigned long long)mock_int(mock_elem(m, 0)),
+                        (unsigned long long)mock_int(mock_elem(m, 1)), (unsigned long long)kw[0], (unsigned long long)rw[0]);
+            }
+            fprintf(g_out, "]");
+            if (r == 3 && mock_list_len(ms) > 0) {   /* a manager's round trip: take one node's messages, put them back */
+                const uint64_t d = mock_int(mock_elem(mock_list_nth(ms, 0), 1));
+                ERL_NIF_TERM got = mock_elem(want_ok_tuple("fm_take", call("fm_take", 2, A(sim, mock_uint(d)))), 1);
+                taken = mock_list_len(got);
+                want_ok("fm_put", call("fm_put", 2, A(sim, got)));
+            }
+            if (r == 5) {                             /* node 2's state from a node outside the cluster, to node 4 */
+                ERL_NIF_TERM fs = want_ok_tuple("fm_state", call("fm_state", 1, A(sim)));
+                size_t sz;
+                const uint64_t* kn = (const uint64_t*)mock_bin_data(mock_elem(fs, 1), &sz);
+                const uint64_t* rm = (const uint64_t*)mock_bin_data(mock_elem(fs, 2), &sz);
+                ERL_NIF_TERM el[5] = {mock_uint(n), mock_uint(4), mock_uint(0), mock_bin(&kn[2], 8), mock_bin(&rm[2], 8)};
+                ERL_NIF_TERM msg = enif_make_tuple_from_array(NULL, el, 5);
+                want_ok("fm_put", call("fm_put", 2, A(sim, enif_make_list_cell(NULL, msg, enif_make_list(NULL, 0)))));
+            }
+        }
+        ERL_NIF_TERM fs = want_ok_tuple("fm_state", call("fm_state", 1, A(sim)));
+        size_t sz;
+        const uint64_t* kn = (const uint64_t*)mock_bin_data(mock_elem(fs, 1), &sz);
+        const uint64_t* rm = (const uint64_t*)mock_bin_data(mock_elem(fs, 2), &sz);
+        fprintf(g_out, "], \"taken\": %llu, \"known\": [", (unsigned long long)taken);
+        for (uint32_t i = 0; i < n; i++) fprintf(g_out, "%s%llu", i ? ", " : "", (unsigned long long)kn[i]);
+        fprintf(g_out, "], \"removed\": [");
+        for (uint32_t i = 0; i < n; i++) fprintf(g_out, "%s%llu", i ? ", " : "", (unsigned long long)rm[i]);
+        fprintf(g_out, "]}");
+    }
     /* ---- C3: SCAMP v2 churn + Plumtree repair ------------------------------- */
     {
         const uint32_t n = 2000;

@@ -180,3 +180,56 @@ def test_gpu_large_crash_list_resets_every_vertex():
         assert all(pv[x, :npv[x]].tolist() == fpv[x, :fnpv[x]].tolist() for x in v[:2000])
     sim.close()
     fresh.close()
+
+
+def _max_grafts_per_sender(o):
+    """Largest number of grafts one vertex sent in the last round (the oracle's in-flight list)."""
+    import collections
+    c = collections.Counter(s for s, _d, t, _r in o.pt.pending() if t == 5)
+    return max(c.values()) if c else 0
+
+
+@pytest.mark.gpu
+def test_gpu_c3_many_grafts_per_vertex_round():
+    """the per-kind send counters of pd_process are packed 12 bits
+    per kind into one u64; graft used to sit at bit 60 with 4 bits, so a vertex
+    sending more than 15 grafts in one round lost counts.  A heartbeat every
+    round with churn every third round makes vertices answer 16+ i_haves of
+    distinct undelivered serials in one tick (the oracle's in-flight list
+    proves the case is reached); counters and state must stay bit-exact."""
+    import partisan_amd as pa
+    n, periodic = 300, 2
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=periodic)
+    o = O.C3(n, 5, periodic, SEED)
+    r = 0
+    for v, cc in waves(n):
+        g.join(v, cc)
+        for a, b in zip(v, cc):
+            o.join(int(a), int(b))
+        for _ in range(3):
+            _step(g, o, r)
+            r += 1
+    for _ in range(30):
+        _step(g, o, r)
+        r += 1
+    most = 0
+    mono = 0
+    for i in range(60):
+        if i < 50:
+            mono = g.heartbeat(0)
+            assert mono == o.heartbeat(0)
+        _step(g, o, r)
+        r += 1
+        most = max(most, _max_grafts_per_sender(o))
+        if i % 3 == 0:
+            v, cc = churn(n, i, frac=0.1)
+            keep = v != 0
+            v, cc = v[keep], cc[keep]
+            g.crash(v)
+            g.join(v, cc)
+            for a, b in zip(v, cc):
+                o.crash(int(a))
+                o.join(int(a), int(b))
+    _compare(g, o, n, 0, mono)
+    assert most > 15, most

@@ -100,6 +100,41 @@ def test_bench_config_10m_flood_converges():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_config_10m_oracle_parity():
+    """the metric configuration itself against the C oracle --
+    not a property, not GPU vs GPU.  bench.py's overlay (10M peers, random
+    5-peer, seed 0x5EED0001, L = 1): the flood from a fresh tree, then a
+    heartbeat over the pruned tree; after each, the round count, the
+    per-round counts of every message kind and of new deliveries, and every
+    vertex's delivered bit, eager / lazy / outstanding masks and accepted
+    Round equal the oracle's (bench.oracle_parity, the check bench.py runs
+    as `parity_10m`)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    import pyoracle as O
+    import partisan_amd as pa
+    n = 10_000_000
+    rp, col = pa.overlay.random_regular(n, 5, 0x5EED0001)
+    sim = pa.Simulator(lazy_tick_rounds=1, device=0)
+    sim.load_overlay(rp, col)
+    orc = O.Plumtree(rp, col, 1)
+    del rp, col
+    sim.reset_trees()
+    for hb in ("flood", "tree heartbeat"):
+        sim.broadcast(0)
+        gst, gr = sim.run(as_dicts=False)
+        omono = orc.heartbeat(0)
+        ost, orr = orc.run()
+        res = bench.oracle_parity(sim, orc, 0, gst, gr, ost, orr, omono)
+        print(hb, res, flush=True)
+        assert res["ok"], (hb, res)
+    orc.close()
+    sim.close()
+
+
+@pytest.mark.gpu
 def test_bench_config_10m_engines_agree_per_round():
     """The slot-scatter engine (what bench.py times) and the binned engine at
     the bench size, round by round, by psim_trace_hash (state digest,

@@ -188,3 +188,121 @@ def test_gpu_two_words_of_nodes():
     script = {3 * (v - 1): [("join", v, v - 1)] for v in range(1, n)}
     g, f = _drive(n, 7, script, 3 * n + 3)
     assert all(g.members(v) == list(range(n)) for v in range(n))
+
+
+# ------------------------------------------------------------------ the wire
+def _rows_to_bits(rows, words):
+    K = np.zeros(words, np.uint64)
+    R = np.zeros(words, np.uint64)
+    for _, t, act in rows:
+        K[t >> 6] |= np.uint64(1 << (t & 63))
+        if not act:
+            R[t >> 6] |= np.uint64(1 << (t & 63))
+    return K, R
+
+
+def _bits_to_rows(K, R, token_node):
+    rows = []
+    for t in range(64 * len(K)):
+        if (int(K[t >> 6]) >> (t & 63)) & 1:
+            rows.append((int(token_node[t]), t, not (int(R[t >> 6]) >> (t & 63)) & 1))
+    return rows
+
+
+def test_oracle_wire_take_put_round_trip():
+    """A node's manager taking its messages off the wire and handing them
+    back (handle_message/2) changes nothing; the listing is in handling order
+    and each message carries the {NodeSpec, #full_v1{}} state its sender
+    gossiped (gossip_messages/2 :247-267)."""
+    n = 12
+    a, b = O.FullMembership(n, periodic_rounds=3), O.FullMembership(n, periodic_rounds=3)
+    for f in (a, b):
+        cluster_joins(f, n)
+    for r in range(8):
+        for f in (a, b):
+            f.step(1)
+        ms = a.messages()
+        assert ms == b.messages()
+        assert [(d, s, q) for s, d, q, _ in ms] == sorted((d, s, q) for s, d, q, _ in ms)
+        if ms:
+            d = ms[len(ms) // 2][1]
+            got = a.take(d)
+            assert got == [m for m in ms if m[1] == d]
+            assert all(m[1] != d for m in a.messages())
+            a.put(got)
+            assert a.messages() == ms
+    for v in range(n):
+        assert a.payload(v) == b.payload(v)
+
+
+@pytest.mark.gpu
+def test_gpu_wire_messages_take_put_parity():
+    """psim_fm_messages / _take / _put against the oracle's wire: every round
+    the messages the next round delivers -- (src, dst) in handling order and
+    the #full_v1{} state each carries -- equal the oracle's; a manager's round
+    trip (take a node's messages, hand them back) and a message from a node
+    outside the simulated cluster (src = n) go onto both wires, and the states,
+    counters and liveness stay bit-exact through joins, a leave and a failure."""
+    import partisan_amd as pa
+    n = 16
+    sim = pa.Simulator(device=0)
+    g = pa.fullmem.FullMembershipCluster(sim, n, periodic_rounds=4, max_tokens=n + 64)
+    f = O.FullMembership(n, periodic_rounds=4)
+    rng = np.random.default_rng(11)
+    ext = 0
+    took = 0
+    for r in range(24):
+        if r < 6:
+            for _ in range(3):
+                a_, b_ = int(rng.integers(n)), int(rng.integers(n))
+                g.join([a_], [b_]); f.join(a_, b_)
+        if r == 10:
+            g.leave([3], [7]); f.leave(3, 7)
+        if r == 14:
+            al = np.ones(n, np.uint8)
+            al[5] = 0
+            g.set_alive(al); f.set_alive(al)
+        gs, os_ = g.step(1)[0], f.step(1)[0]
+        for k in os_:
+            assert gs[k] == os_[k], (r, k, gs, os_)
+        check_round(g, f, n)
+        gm, om = g.messages(), f.messages()
+        assert len(gm) == len(om), (r, len(gm), len(om))
+        for (s1, d1, _q1, K1, R1), (s2, d2, _q2, rows) in zip(gm, om):
+            K2, R2 = _rows_to_bits(rows, g.words)
+            assert (s1, d1) == (s2, d2) and np.array_equal(K1, K2) and np.array_equal(R1, R2), r
+        if gm and r % 3 == 1:              # a manager's round trip at one node
+            d = gm[(7 * r) % len(gm)][1]
+            gt, ot = g.take(d), f.take(d)
+            assert [(m[0], m[1]) for m in gt] == [(m[0], m[1]) for m in ot]
+            assert all(m[1] != d for m in g.messages())
+            took += len(gt)
+            g.put(gt)
+            f.put(ot)
+        if r % 4 == 2:                     # gossip from a node outside the cluster: node 2's state, to node 9
+            K, R, _ = g.state()
+            tok = g.token_nodes()
+            g.put([(n, 9, ext, K[2], R[2])])
+            f.put([(n, 9, ext, _bits_to_rows(K[2], R[2], tok))])
+            ext += 1
+    assert took > 0 and ext > 0
+    assert all(g.members(v) == f.members(v) for v in range(n) if f.alive(v))
+
+
+@pytest.mark.gpu
+def test_gpu_wire_put_refuses_unknown_tokens():
+    import partisan_amd as pa
+    from partisan_amd._lib import PsimError
+    n = 8
+    sim = pa.Simulator(device=0)
+    g = pa.fullmem.FullMembershipCluster(sim, n, periodic_rounds=4, max_tokens=n + 64)
+    K = np.zeros(g.words, np.uint64)
+    R = np.zeros(g.words, np.uint64)
+    K[0] = np.uint64(1 << 20)                  # token 20: never allocated (8 nodes, no self-leave)
+    with pytest.raises(PsimError):
+        g.put([(n, 1, 0, K, R)])
+    K[0] = np.uint64(1)
+    R[0] = np.uint64(2)                        # removed but not known
+    with pytest.raises(PsimError):
+        g.put([(n, 1, 0, K, R)])
+    assert g.messages() == []

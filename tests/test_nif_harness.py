@@ -45,6 +45,43 @@ def _lcg(s):
     return s, s >> 33
 
 
+def _check_fm_wire(w):
+    """SURVEY 8(f) row 3, full membership: the {Src, Dst, Seq, Known, Removed}
+    records the shim renders (what the cluster module turns into
+    {membership_strategy, {Spec, #full_v1{}}}) equal, round by round, the
+    oracle's messages in flight (src, dst, token bitmaps of the state) in
+    handling order; a node's messages taken off (fm_take) and put back
+    (fm_put), and a state put from a node outside the cluster, leave every
+    node's state equal to the oracle's after the same operations."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    n = w["n"]
+    orc = O.FullMembership(n, periodic_rounds=3)
+    for i in range(1, n):
+        orc.join(i, i - 1)
+
+    def bits(rows):
+        k = r = 0
+        for _, t, act in rows:
+            k |= 1 << t
+            if not act:
+                r |= 1 << t
+        return k, r
+
+    for r, got in enumerate(w["rounds"]):
+        orc.step(1)
+        ms = orc.messages()
+        assert [[s, d, *bits(rows)] for s, d, _q, rows in ms] == got, r
+        if r == 3 and ms:
+            orc.put(orc.take(ms[0][1]))
+        if r == 5:
+            orc.put([(n, 4, 0, orc.payload(2))])
+    assert w["taken"] > 0
+    for v in range(n):
+        assert list(bits(orc.payload(v))) == [w["known"][v], w["removed"][v]], v
+
+
 def _check_scamp_wire(w):
     """the {membership_strategy, Msg} terms the shim renders
     for a SCAMP v2 run, round by round, equal the oracle's messages in
@@ -89,6 +126,7 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rep["fullmem"]["tokens_used"] == rep["fullmem"]["own_tokens"] == rep["fullmem"]["n"]
     assert rep["scamp"]["view_entries"] > rep["scamp"]["n"]
     _check_scamp_wire(rep["scamp_wire"])
+    _check_fm_wire(rep["fm_wire"])
     assert 0 < rep["c3"]["delivered_live"] <= rep["c3"]["live"]
     assert rep["causal"]["delivered"] > 0
     assert rep["vclock_merge"] == [3, 1, 4]

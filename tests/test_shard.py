@@ -195,6 +195,72 @@ def test_sharded_delay_faults_match_oracle(world, n, seed, L, dmax, csr):
         assert res[r] == "ok", res[r]
 
 
+def _delay_busy_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        dist = _init(rank, world, port)
+        import partisan_amd as pa
+        from partisan_amd._lib import PsimError
+        from partisan_amd.shard import ShardedPlumtree
+        import pyoracle as O
+        n, root = 3000, 11                          # the origin's words are counted on rank 0 only
+        rp, col = pa.overlay.random_regular(n, 5, 41)
+        sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=1, transport="callback")
+        orc = O.Plumtree(rp, col, 1)
+        rp64 = np.asarray(rp, dtype=np.int64)
+        src = np.repeat(np.arange(n), np.diff(rp64))
+        pick = np.random.default_rng(41).random(len(src)) < 0.3
+        pairs = np.stack([src[pick], np.asarray(col)[pick]], axis=1).astype(np.uint32)
+        d = np.full(len(pairs), 2, np.uint8)
+        codes = []
+        for stepped in (0, 3):                      # right after the broadcast, then mid-flood
+            mono = sp.broadcast(root) if stepped == 0 else mono
+            if stepped == 0:
+                assert mono == orc.heartbeat(root)
+            else:
+                sp.step(stepped)
+                orc.step(stepped)
+            try:
+                sp.set_delays(pairs, d)
+                codes.append("ok")
+            except PsimError as e:
+                codes.append(e.name)
+        gst, gr = sp.run()
+        ost, orr = orc.run()
+        assert gr == orr
+        sp.set_delays(pairs, d)                     # quiescent everywhere: every rank installs them
+        orc.set_delays(pairs, d)
+        mono = sp.broadcast(root)
+        assert mono == orc.heartbeat(root)
+        gst, gr = sp.run()
+        ost, orr = orc.run()
+        assert gr == orr, (gr, orr)
+        for g, o in zip(gst, ost):
+            for k in KINDS:
+                assert g[k] == o[k], (k, g, o)
+        sp.close()
+        dist.destroy_process_group()
+        q.put((rank, "codes " + ",".join(codes)))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_sharded_set_delays_busy_on_every_rank():
+    """psim_set_delays is collective on a sharded handle; with
+    messages in flight on ONE shard only (the origin's words right after a
+    broadcast are counted by the root's shard) every rank must refuse with
+    PSIM_EBUSY -- a rank that went ahead would switch to the staging ring
+    while the others did not.  The decision is an all-reduce of the shards'
+    in-flight counts; at quiescence every rank installs the delays and the
+    next flood matches the oracle."""
+    res = run_world(_delay_busy_worker, 2)
+    for r in range(2):
+        assert res[r] == "codes PSIM_EBUSY,PSIM_EBUSY", res[r]
+
+
 def _lanes_check(sim, orc, monos, exact):
     """This rank's vertices against the oracle, per root lane: delivered per
     Monotonic, eager / lazy sets; rows and in-flight messages over all lanes
