@@ -413,6 +413,17 @@ int  psim_demers_shard_round(psim_handle* h, void* rm_shadow, void* pull_shadow,
 int  psim_demers_shard_ingest(psim_handle* h, const void* rm_recv, const void* pull_recv, const void* rmx_all,
                               uint32_t tick);
 int  psim_demers_shard_get_seen(const psim_handle* h, uint64_t* seen, size_t n_local);
+/* The same exchange inside the library, on the handle's transport
+ * (psim_shard_init_rccl: RCCL all-to-all-v / all-gather over xGMI on the
+ * handle's stream; psim_shard_set_transport: the caller's callbacks) -- no
+ * caller buffers, no host collectives: the broadcast of every rumor at its
+ * origin, exactly `rounds` rounds, or rounds until every vertex of every
+ * shard holds every rumor.  Collective; stats are GLOBAL (summed over the
+ * shards; kernel_ms this shard's).  world 1 needs no transport. */
+int  psim_demers_shard_broadcast_x(psim_handle* h);
+int  psim_demers_shard_step(psim_handle* h, uint32_t rounds, psim_demers_stats* stats, size_t cap);
+int  psim_demers_shard_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* stats, size_t cap,
+                           uint32_t* rounds_run);
 
 /* --- HyParView view maintenance (partisan_hyparview_peer_service_manager.erl) */
 typedef struct psim_hv_config {

@@ -306,6 +306,18 @@ __global__ __launch_bounds__(kBlock) void dm_ingest_kernel(DmArgs a, const unsig
     }
 }
 
+// the pull slots of this shard as every source shard wrote them: slice g of
+// `in` came from shard g (one writer per slot, so the sum is the one value)
+__global__ __launch_bounds__(kBlock) void dm_sum_slices_kernel(const unsigned long long* __restrict__ in,
+                                                               uint32_t world, size_t len,
+                                                               unsigned long long* __restrict__ out) {
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < len; i += size_t(gridDim.x) * kBlock) {
+        unsigned long long x = 0;
+        for (uint32_t g = 0; g < world; g++) x += in[size_t(g) * len + i];
+        out[i] = x;
+    }
+}
+
 __global__ void dm_origin_kernel(uint2 key, uint32_t n, uint32_t m, uint32_t* __restrict__ origin) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
@@ -329,6 +341,15 @@ hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s)
     uint32_t g = (a.n_global + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(dm_pushscan_kernel, dim3(g), dim3(kBlock), 0, s, a, tick_idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_dm_sum_slices(const unsigned long long* in, uint32_t world, size_t len, unsigned long long* out,
+                                hipStream_t s) {
+    size_t g = (len + kBlock - 1) / kBlock;
+    if (g > 8192) g = 8192;
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(dm_sum_slices_kernel, dim3((uint32_t)g), dim3(kBlock), 0, s, in, world, len, out);
     return hipGetLastError();
 }
 

@@ -186,9 +186,15 @@ struct DmShard : ModuleState {
     std::vector<uint32_t> h_origin;
     uint32_t par = 0;
     uint64_t round = 0;
+    // the in-library exchange (psim_demers_shard_step / _run): the caller-side
+    // buffers of the split-phase entry points, owned here
+    unsigned long long *x_rm_shadow = nullptr, *x_rm_recv = nullptr, *x_pull_shadow = nullptr, *x_pull_all = nullptr,
+                       *x_pull_sum = nullptr, *x_snap_all = nullptr, *x_rmx_all = nullptr;
+    uint64_t complete_g = 0;      // vertices holding every rumor, over all shards, after the last round
     ~DmShard() override {
         void* p[] = {seen, rm[0], rm[1], rm[2], pull, stats, rmnew_prev, ncall_prev, pushcnt[0], pushcnt[1],
-                     pushlist[0], pushlist[1], origin, idbit};
+                     pushlist[0], pushlist[1], origin, idbit, x_rm_shadow, x_rm_recv, x_pull_shadow, x_pull_all,
+                     x_pull_sum, x_snap_all, x_rmx_all};
         for (void* x : p)
             if (x) (void)hipFree(x);
     }
@@ -232,6 +238,78 @@ DmArgs dms_args(const psim_handle* h, const DmShard& d, void* rm_shadow, void* p
     a.pull_nxt = (unsigned long long*)pull_shadow;
     a.stats = d.stats;
     return a;
+}
+
+// ---- the exchange inside the library (the handle's transport) -----------------
+int dms_x_buffers(psim_handle* h, DmShard& d) {
+    if (d.world > 1 && !handle_transport(h))
+        return handle_fail(h, PSIM_ESTATE, "sharded Demers without a transport (psim_shard_init_rccl / _set_transport)");
+    if (d.x_rm_shadow) return PSIM_OK;
+    const size_t NG = size_t(d.world) * d.chunk;
+    auto A = [&](unsigned long long** p, size_t words) { return alloc_zero((void**)p, std::max<size_t>(words, 1) * 8); };
+    if (!A(&d.x_rm_shadow, 3 * NG) || !A(&d.x_rm_recv, 3 * NG) || !A(&d.x_pull_shadow, 2 * NG) ||
+        !A(&d.x_pull_all, 2 * NG) || !A(&d.x_pull_sum, 2 * size_t(d.chunk)) || !A(&d.x_snap_all, NG) ||
+        !A(&d.x_rmx_all, NG + (NG + 1) / 2))
+        return handle_fail(h, PSIM_ENOMEM, "demers exchange buffers for %zu slots", NG);
+    return PSIM_OK;
+}
+
+// The round's exchange (psim.h "vertex-sharded Demers"): all-to-all of the
+// three RM count planes in slices of C, the pull slots as an all-to-all whose
+// slices the receiver sums (one writer per slot), all-gathers of both RM call
+// record planes and, after an AE tick, of the snapshots -- RCCL on the
+// handle's stream, or the caller's transport; the own slices are local copies.
+int dms_exchange(psim_handle* h, DmShard& d, bool tick) {
+    const hipStream_t s = handle_stream(h);
+    const size_t C = d.chunk, NG = size_t(d.world) * C;
+    const int G = (int)d.world, r = (int)d.rank;
+    Transport* T = handle_transport(h);
+    std::string err;
+    std::vector<uint64_t> off1(G + 1), off2(G + 1);
+    for (int g = 0; g <= G; g++) {
+        off1[g] = uint64_t(g) * 2 * C;     // C u64 per slice
+        off2[g] = uint64_t(g) * 4 * C;     // 2C u64 per slice
+    }
+    for (int k = 0; k < 3; k++) {
+        unsigned long long* snd = d.x_rm_shadow + k * NG;
+        unsigned long long* rcv = d.x_rm_recv + k * NG;
+        if (G > 1) {
+            const int rc = T->alltoallv(reinterpret_cast<uint32_t*>(snd), off1.data(), reinterpret_cast<uint32_t*>(rcv),
+                                        off1.data(), r, G, s, &err);
+            if (rc) return handle_fail(h, rc, "demers RM exchange: %s", err.c_str());
+        }
+        DMCHK(h, hipMemcpyAsync(rcv + r * C, snd + r * C, C * 8, hipMemcpyDeviceToDevice, s));
+    }
+    if (G > 1) {
+        const int rc = T->alltoallv(reinterpret_cast<uint32_t*>(d.x_pull_shadow), off2.data(),
+                                    reinterpret_cast<uint32_t*>(d.x_pull_all), off2.data(), r, G, s, &err);
+        if (rc) return handle_fail(h, rc, "demers pull exchange: %s", err.c_str());
+    }
+    DMCHK(h, hipMemcpyAsync(d.x_pull_all + r * 2 * C, d.x_pull_shadow + r * 2 * C, 2 * C * 8, hipMemcpyDeviceToDevice, s));
+    DMCHK(h, launch_dm_sum_slices(d.x_pull_all, d.world, 2 * C, d.x_pull_sum, s));
+    if (G > 1) {
+        uint32_t* rmx = reinterpret_cast<uint32_t*>(d.x_rmx_all);
+        int rc = T->allgather(rmx, 2 * C, r, G, s, &err);                        // rumors called (u64)
+        if (!rc) rc = T->allgather(rmx + 2 * NG, C, r, G, s, &err);               // calls before the round (u32)
+        if (!rc && tick) rc = T->allgather(reinterpret_cast<uint32_t*>(d.x_snap_all), 2 * C, r, G, s, &err);
+        if (rc) return handle_fail(h, rc, "demers all-gather: %s", err.c_str());
+    }
+    DMCHK(h, hipMemsetAsync(d.x_rm_shadow, 0, 3 * NG * 8, s));
+    DMCHK(h, hipMemsetAsync(d.x_pull_shadow, 0, 2 * NG * 8, s));
+    return PSIM_OK;
+}
+
+// per-round stats over every shard (kernel_ms stays this shard's)
+int dms_global(psim_handle* h, const DmShard& d, psim_demers_stats& st) {
+    if (d.world == 1) return PSIM_OK;
+    int64_t v[6] = {(int64_t)st.rm_sent, (int64_t)st.push_sent, (int64_t)st.pull_sent, (int64_t)st.delivered_new,
+                    (int64_t)st.complete, (int64_t)st.algo_bytes};
+    std::string err;
+    const int rc = handle_transport(h)->allreduce(v, 6, handle_stream(h), &err);
+    if (rc) return handle_fail(h, rc, "demers stats all-reduce: %s", err.c_str());
+    st.rm_sent = v[0]; st.push_sent = v[1]; st.pull_sent = v[2]; st.delivered_new = v[3];
+    st.complete = v[4]; st.algo_bytes = v[5];
+    return PSIM_OK;
 }
 
 }  // namespace
@@ -444,6 +522,56 @@ int psim_demers_shard_ingest(psim_handle* h, const void* rm_recv, const void* pu
     if (tick) DMCHK(h, launch_dm_pushscan(a, (uint32_t)(d->round / d->ae_period), s));
     DMCHK(h, hipStreamSynchronize(s));
     d->par ^= 1u;
+    return PSIM_OK;
+}
+
+int psim_demers_shard_broadcast_x(psim_handle* h) {
+    if (!h) return PSIM_EINVAL;
+    DmShard* d = dms_of(h);
+    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    int rc = dms_x_buffers(h, *d);
+    if (!rc) rc = psim_demers_shard_broadcast_all(h, d->x_rm_shadow, d->x_rmx_all);
+    if (!rc) rc = dms_exchange(h, *d, false);
+    if (!rc) rc = psim_demers_shard_ingest(h, d->x_rm_recv, d->x_pull_sum, d->x_rmx_all, 0);
+    return rc;
+}
+
+int psim_demers_shard_step(psim_handle* h, uint32_t rounds, psim_demers_stats* stats, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    DmShard* d = dms_of(h);
+    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    int rc = dms_x_buffers(h, *d);
+    for (uint32_t i = 0; i < rounds && !rc; i++) {
+        psim_demers_stats st;
+        uint32_t tick = 0;
+        rc = psim_demers_shard_round(h, d->x_rm_shadow, d->x_pull_shadow, d->x_snap_all, d->x_rmx_all, &st, &tick);
+        if (!rc) rc = dms_exchange(h, *d, tick != 0);
+        if (!rc) rc = psim_demers_shard_ingest(h, d->x_rm_recv, d->x_pull_sum, d->x_rmx_all, tick);
+        if (!rc) rc = dms_global(h, *d, st);
+        if (!rc) {
+            d->complete_g = st.complete;
+            if (stats && i < cap) stats[i] = st;
+        }
+    }
+    return rc;
+}
+
+int psim_demers_shard_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* stats, size_t cap,
+                          uint32_t* rounds_run) {
+    if (!h) return PSIM_EINVAL;
+    DmShard* d = dms_of(h);
+    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    uint32_t ran = 0;
+    d->complete_g = 0;
+    while (ran < max_rounds) {
+        psim_demers_stats st;
+        const int rc = psim_demers_shard_step(h, 1, &st, 1);
+        if (rc) return rc;
+        if (stats && ran < cap) stats[ran] = st;
+        ran++;
+        if (st.complete == d->n_global) break;      // every vertex holds every rumor (global count)
+    }
+    if (rounds_run) *rounds_run = ran;
     return PSIM_OK;
 }
 

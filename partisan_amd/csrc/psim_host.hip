@@ -1077,6 +1077,7 @@ namespace psim {
 ModuleState*& handle_module(psim_handle* h, int slot) { return h->mods[slot]; }
 const ModuleState* handle_module(const psim_handle* h, int slot) { return h->mods[slot]; }
 hipStream_t handle_stream(const psim_handle* h) { return h->stream; }
+Transport* handle_transport(psim_handle* h) { return h->sh.xport; }
 int handle_device(const psim_handle* h) { return h->device; }
 uint64_t handle_seed(const psim_handle* h) { return h->cfg.seed; }
 int handle_fail(psim_handle* h, int code, const char* fmt, ...) {

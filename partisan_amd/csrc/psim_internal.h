@@ -257,6 +257,9 @@ hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const ui
 hipError_t launch_dm_ingest_rm(const DmArgs& a, const unsigned long long* rm_recv, const unsigned long long* pull_recv,
                                uint32_t world, uint32_t chunk, hipStream_t s);
 hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
+// out[i] = sum over g < world of in[g * len + i] (the pull slots' reduce-scatter)
+hipError_t launch_dm_sum_slices(const unsigned long long* in, uint32_t world, size_t len, unsigned long long* out,
+                                hipStream_t s);
 hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s);
 
 // HyParView (hyparview.hip)
@@ -419,7 +422,7 @@ hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
 
 // C3: Plumtree over the SCAMP engine's changing views (ptdyn.hip)
 constexpr uint32_t kPdTab = 128;      // peer-table ids per vertex (PdBits masks)
-constexpr uint32_t kPdRows = 64;      // outstanding i_have rows per vertex
+constexpr uint32_t kPdRows = 256;     // outstanding i_have rows per vertex (heartbeats every round pile them up)
 constexpr uint32_t kPdSets = 5;       // masks per vertex: members, common eager/lazy, root eager/lazy
 constexpr int kPdNStat = 16;
 struct PdHead {
@@ -538,6 +541,9 @@ struct Transport {
                           int world, hipStream_t s, std::string* err) = 0;
     // host values, in place, summed over ranks (synchronous)
     virtual int allreduce(int64_t* vals, size_t n, hipStream_t s, std::string* err) = 0;
+    // device buffer of world slices of `count` u32 words, in place: rank r's
+    // slice [r count, (r + 1) count) to every rank
+    virtual int allgather(uint32_t* buf, size_t count, int rank, int world, hipStream_t s, std::string* err) = 0;
     virtual const char* name() const = 0;
     // the transport's own view of the job: RCCL asks its communicator
     // (ncclCommCount / ncclCommUserRank); a callback transport reports -1
@@ -561,6 +567,7 @@ ModuleState*& handle_module(psim_handle* h, int slot);
 const ModuleState* handle_module(const psim_handle* h, int slot);
 hipStream_t handle_stream(const psim_handle* h);
 int handle_device(const psim_handle* h);
+Transport* handle_transport(psim_handle* h);                // the exchange of psim_shard_init_rccl / _set_transport
 uint64_t handle_seed(const psim_handle* h);
 int handle_fail(psim_handle* h, int code, const char* fmt, ...);
 void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing totals

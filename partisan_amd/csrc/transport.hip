@@ -82,6 +82,13 @@ class RcclTransport : public Transport {
         return hipStreamSynchronize(s) == hipSuccess ? PSIM_OK : PSIM_EHIP;
     }
 
+    int allgather(uint32_t* buf, size_t count, int rank, int world, hipStream_t s, std::string* e) override {
+        (void)world;
+        if (!count) return PSIM_OK;
+        const ncclResult_t r = ncclAllGather(buf + size_t(rank) * count, buf, count, ncclUint32, comm, s);
+        return r == ncclSuccess ? PSIM_OK : fail_nccl(r, "ncclAllGather", e);
+    }
+
     const char* name() const override { return "rccl"; }
     int comm_size() const override {
         int c = -1;
@@ -121,6 +128,28 @@ class CallbackTransport : public Transport {
         const int rc = t.allreduce(t.ctx, vals, n);
         if (rc && e) *e = "psim_transport.allreduce returned " + std::to_string(rc);
         return rc ? PSIM_ERCCL : PSIM_OK;
+    }
+
+    // through the caller's all-to-all-v: the own slice to every rank (host staged)
+    int allgather(uint32_t* buf, size_t count, int rank, int world, hipStream_t s, std::string* e) override {
+        if (!count) return PSIM_OK;
+        const size_t tot = size_t(world) * count;
+        hs.resize(tot + 1);
+        hr.resize(tot + 1);
+        if (hipMemcpyAsync(hs.data(), buf + size_t(rank) * count, count * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return PSIM_EHIP;
+        for (int d = 1; d < world; d++) memcpy(hs.data() + size_t(d) * count, hs.data(), count * 4);
+        std::vector<uint64_t> off(world + 1);
+        for (int d = 0; d <= world; d++) off[d] = uint64_t(d) * count;
+        const int rc = t.alltoallv(t.ctx, hs.data(), off.data(), hr.data(), off.data(), world);
+        if (rc) {
+            if (e) *e = "psim_transport.alltoallv (allgather) returned " + std::to_string(rc);
+            return PSIM_ERCCL;
+        }
+        memcpy(hr.data() + size_t(rank) * count, hs.data(), count * 4);
+        if (hipMemcpyAsync(buf, hr.data(), tot * 4, hipMemcpyHostToDevice, s) != hipSuccess) return PSIM_EHIP;
+        return hipStreamSynchronize(s) == hipSuccess ? PSIM_OK : PSIM_EHIP;
     }
 
     const char* name() const override { return "callback"; }

@@ -54,18 +54,42 @@ class ShardedDemers:
     round: all-to-all of the RM count-plane slices (summed, saturating, by the
     receiver), reduce-scatter of the pull slots, all-gather of every RM
     process's call records (rumors called, calls before the round), all-gather
-    of the AE snapshots after a tick -- RCCL over xGMI with backend "nccl",
-    host-staged with "gloo"."""
+    of the AE snapshots after a tick.
 
-    def __init__(self, n, m, rank, world, device=0, backend="nccl", ae_period=2, rumor_mongering=True, seed=0):
+    transport: "rccl" (default with backend "nccl") / "callback" (default with
+    "gloo"): the exchange runs inside libpsim on the handle's transport
+    (psim_demers_shard_step: RCCL all-to-all-v / all-gather over xGMI on the
+    library's stream, or gloo callbacks) -- what an Erlang host drives through
+    the NIF; "torch": the split-phase entry points with the collectives issued
+    from Python (the round-1 path, kept for A/B)."""
+
+    def __init__(self, n, m, rank, world, device=0, backend="nccl", ae_period=2, rumor_mongering=True, seed=0,
+                 transport=None):
         import torch
 
         from .sim import Simulator
         self.torch = torch
         self.n, self.m, self.rank, self.world, self.backend = n, m, rank, world, backend
+        self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
+        if backend == "nccl":
+            torch.cuda.set_device(self.dev)
         self.sim = Simulator(device=device, seed=seed)
         self._h = self.sim._h
+        if self.transport == "rccl":
+            from ._lib import PSIM_RCCL_ID_BYTES
+            uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES)()
+            if rank == 0:
+                check(lib().psim_rccl_unique_id(uid))
+            if world > 1:
+                box = [bytes(uid)]
+                self._dist().broadcast_object_list(box, src=0)
+                uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES).from_buffer_copy(box[0])
+            check(lib().psim_shard_init_rccl(self._h, rank, world, uid), self._h)
+        elif self.transport == "callback":
+            from .shard import gloo_transport
+            self._tp, self._keep = gloo_transport()
+            check(lib().psim_shard_set_transport(self._h, C.byref(self._tp)), self._h)
         chunk = C.c_uint64()
         check(lib().psim_demers_shard_setup(self._h, n, m, ae_period, 1 if rumor_mongering else 0, rank, world,
                                             C.byref(chunk)), self._h)
@@ -74,12 +98,13 @@ class ShardedDemers:
         check(lib().psim_demers_shard_info(self._h, C.byref(vlo), C.byref(nl), None), self._h)
         self.v_lo, self.n_local = vlo.value, nl.value
         G = world
-        z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=self.dev)  # noqa: E731
-        self.rm_shadow, self.rm_recv = z(3, G * Cn), z(3, G * Cn)
-        self.pull_shadow, self.pull_recv = z(2 * G * Cn), z(2 * Cn)
-        self.snap_all = z(G * Cn)
-        # RM call records: [G C] u64 rumors called, then [G C] u32 calls before the round
-        self.rmx_all = torch.zeros(3 * G * Cn, dtype=torch.int32, device=self.dev)
+        if self.transport == "torch":    # the caller-side buffers of the split-phase entry points
+            z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=self.dev)  # noqa: E731
+            self.rm_shadow, self.rm_recv = z(3, G * Cn), z(3, G * Cn)
+            self.pull_shadow, self.pull_recv = z(2 * G * Cn), z(2 * Cn)
+            self.snap_all = z(G * Cn)
+            # RM call records: [G C] u64 rumors called, then [G C] u32 calls before the round
+            self.rmx_all = torch.zeros(3 * G * Cn, dtype=torch.int32, device=self.dev)
         self.local_kernel_ms = 0.0
         self.local_algo_bytes = 0
 
@@ -150,11 +175,21 @@ class ShardedDemers:
 
     # -------------------------------------------------------------- protocol
     def broadcast(self):
+        if self.transport != "torch":
+            check(lib().psim_demers_shard_broadcast_x(self._h), self._h)
+            return
         check(lib().psim_demers_shard_broadcast_all(self._h, self._p(self.rm_shadow), self._p(self.rmx_all)), self._h)
         self._exchange(False)
 
     def step(self, rounds=1):
         """Rounds; returns per-round GLOBAL stats (summed over shards)."""
+        if self.transport != "torch":
+            st = (DemersStats * max(1, rounds))()
+            check(lib().psim_demers_shard_step(self._h, rounds, st, rounds), self._h)
+            out = [s_.as_dict() for s_ in st[:rounds]]
+            for d in out:
+                self.local_kernel_ms += d["kernel_ms"]
+            return out
         out = []
         for _ in range(rounds):
             st = DemersStats()
@@ -173,6 +208,14 @@ class ShardedDemers:
         return out
 
     def run(self, max_rounds=10000):
+        if self.transport != "torch":
+            st = (DemersStats * min(max_rounds, 4096))()
+            ran = C.c_uint32()
+            check(lib().psim_demers_shard_run(self._h, max_rounds, st, len(st), C.byref(ran)), self._h)
+            out = [s_.as_dict() for s_ in st[:min(ran.value, len(st))]]
+            for d in out:
+                self.local_kernel_ms += d["kernel_ms"]
+            return out, ran.value
         out = []
         while len(out) < max_rounds:
             out += self.step(1)

@@ -1,7 +1,9 @@
 """Vertex-sharded Demers epidemic (SURVEY 8(e), config C4's exchange).
 
-GPU: world = 2 and 4 processes on ONE GPU (gloo transport), and world = 1
-over RCCL (the nccl code path); every rank checks its vertex range of the
+GPU: world = 2, 3 and 4 processes on ONE GPU, and world = 1 over RCCL (the
+nccl code path).  The exchange runs inside libpsim on the handle's transport
+(psim_demers_shard_step: gloo callbacks / the library's RCCL communicator)
+or, for A/B, from Python (transport "torch"); every rank checks its vertex range of the
 stores against the oracle (oracle/demers.c) after every round, and the
 per-round message counters summed over ranks against the oracle's.
 
@@ -21,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = ("rm_sent", "push_sent", "pull_sent", "delivered_new", "complete")
 
 
-def _gpu_worker(rank, world, port, n, m, ae, rm, backend, q):
+def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, q):
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -37,7 +39,8 @@ def _gpu_worker(rank, world, port, n, m, ae, rm, backend, q):
         from partisan_amd.demers import ShardedDemers
         import pyoracle as O
         seed = 0x5EED0004
-        sd = ShardedDemers(n, m, rank, world, device=0, backend=backend, ae_period=ae, rumor_mongering=rm, seed=seed)
+        sd = ShardedDemers(n, m, rank, world, device=0, backend=backend, ae_period=ae, rumor_mongering=rm, seed=seed,
+                           transport=transport)
         orc = O.Demers(n, m, seed, ae_period=ae, rm_on=rm)
         lo, hi = sd.v_lo, sd.v_lo + sd.n_local
         sd.broadcast()
@@ -60,17 +63,22 @@ def _gpu_worker(rank, world, port, n, m, ae, rm, backend, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n,m,ae,rm", [(2, 3000, 64, 2, True), (4, 5001, 64, 2, True),
-                                              (3, 2000, 17, 3, False), (2, 2500, 64, 0, True)])
-def test_sharded_demers_matches_oracle(world, n, m, ae, rm):
-    res = run_world(_gpu_worker, world, n, m, ae, rm, "gloo")
+@pytest.mark.parametrize("world,n,m,ae,rm,transport", [(2, 3000, 64, 2, True, "callback"),
+                                                        (4, 5001, 64, 2, True, "callback"),
+                                                        (3, 2000, 17, 3, False, "callback"),
+                                                        (2, 2500, 64, 0, True, "callback"),
+                                                        (2, 3000, 64, 2, True, "torch"),
+                                                        (3, 2000, 17, 3, False, "torch")])
+def test_sharded_demers_matches_oracle(world, n, m, ae, rm, transport):
+    res = run_world(_gpu_worker, world, n, m, ae, rm, "gloo", transport)
     for r in range(world):
         assert res[r] == "ok", res[r]
 
 
 @pytest.mark.gpu
-def test_sharded_demers_nccl_world1():
-    res = run_world(_gpu_worker, 1, 4000, 64, 2, True, "nccl")
+@pytest.mark.parametrize("transport", ["rccl", "torch"])
+def test_sharded_demers_nccl_world1(transport):
+    res = run_world(_gpu_worker, 1, 4000, 64, 2, True, "nccl", transport)
     assert res[0] == "ok", res[0]
 
 
