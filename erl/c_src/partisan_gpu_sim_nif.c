@@ -1264,6 +1264,98 @@ static ERL_NIF_TERM nif_shard_init_rccl(ErlNifEnv* env, int argc, const ERL_NIF_
     return rc == PSIM_OK ? mk_atom(env, "ok") : err(env, rc);
 }
 
+/* demers_shard_setup(Sim, N, M, AePeriod, RumorMongering :: boolean(), Rank, World) -> {ok, VLo, NLocal}:
+ * this rank's vertex range of a C4 epidemic sharded over World ranks (after
+ * shard_init_rccl: the exchange runs on the handle's RCCL communicator) */
+static ERL_NIF_TERM nif_demers_shard_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, m, ae, rank, world;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &m) ||
+        !enif_get_uint(env, argv[3], &ae) || !enif_get_uint(env, argv[5], &rank) || !enif_get_uint(env, argv[6], &world))
+        return enif_make_badarg(env);
+    const int rm = enif_is_identical(argv[4], mk_atom(env, "true"));
+    uint32_t vlo = 0, nl = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_demers_shard_setup(r->h, n, m, ae, rm ? 1u : 0u, (int)rank, (int)world, NULL);
+    if (rc == PSIM_OK) rc = psim_demers_shard_info(r->h, &vlo, &nl, NULL);
+    if (rc == PSIM_OK) r->dm_n = nl;
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, vlo), enif_make_uint(env, nl));
+}
+
+/* demers_shard_run(Sim, MaxRounds) -> {ok, Rounds, Seen :: <<u64-little per local vertex>>}:
+ * every rumor from its origin, rounds until every vertex of every shard holds
+ * every rumor (collective: psim_demers_shard_broadcast_x + psim_demers_shard_run) */
+static ERL_NIF_TERM nif_demers_shard_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
+    ERL_NIF_TERM t;
+    unsigned char* seen = enif_make_new_binary(env, (size_t)r->dm_n * 8, &t);
+    uint32_t ran = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_demers_shard_broadcast_x(r->h);
+    if (rc == PSIM_OK) rc = psim_demers_shard_run(r->h, maxr, NULL, 0, &ran);
+    if (rc == PSIM_OK && r->dm_n) rc = psim_demers_shard_get_seen(r->h, (uint64_t*)seen, r->dm_n);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), t);
+}
+
+/* causal_shard_setup(Sim, N, M, Period, DMax, Redeliver, Rank, World) -> {ok, VLo, NLocal}
+ * (after shard_init_rccl) */
+static ERL_NIF_TERM nif_causal_shard_setup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned n, m, per, dmax, red, rank, world;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &n) || !enif_get_uint(env, argv[2], &m) ||
+        !enif_get_uint(env, argv[3], &per) || !enif_get_uint(env, argv[4], &dmax) ||
+        !enif_get_uint(env, argv[5], &red) || !enif_get_uint(env, argv[6], &rank) || !enif_get_uint(env, argv[7], &world))
+        return enif_make_badarg(env);
+    uint32_t vlo = 0, nl = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_causal_shard_setup(r->h, n, m, per, dmax, red, (int)rank, (int)world);
+    if (rc == PSIM_OK) rc = psim_causal_shard_info(r->h, &vlo, &nl);
+    if (rc == PSIM_OK) r->cs_n = nl;
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, vlo), enif_make_uint(env, nl));
+}
+
+/* causal_shard_step(Sim, Rounds) -> {ok, [StatsMap]}   (collective, global counters) */
+static ERL_NIF_TERM nif_causal_shard_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned k;
+    if (!get_res(env, argv[0], &r) || !get_rounds(env, argv[1], &k)) return enif_make_badarg(env);
+    psim_causal_stats* st = (psim_causal_stats*)enif_alloc(k * sizeof(psim_causal_stats));
+    ERL_NIF_TERM* maps = (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM));
+    if (!st || !maps) {
+        if (st) enif_free(st);
+        if (maps) enif_free(maps);
+        return err(env, PSIM_ENOMEM);
+    }
+    enif_mutex_lock(r->mu);
+    int rc = psim_causal_shard_step(r->h, k, st, k);
+    enif_mutex_unlock(r->mu);
+    ERL_NIF_TERM out = err(env, rc);
+    if (rc == PSIM_OK) {
+        static const char* const names[] = {"emitted", "received", "delivered", "checks", "buffered", "kernel_us"};
+        for (unsigned i = 0; i < k; i++) {
+            const uint64_t v[6] = {st[i].emitted, st[i].received, st[i].delivered, st[i].checks, st[i].buffered,
+                                   (uint64_t)(st[i].kernel_ms * 1000.0)};
+            maps[i] = kv_map(env, names, v, 6);
+        }
+        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+    }
+    enif_free(st);
+    enif_free(maps);
+    return out;
+}
+
 /* shard_broadcast(Sim, Root) -> {ok, Monotonic}   (collective over the ranks) */
 static ERL_NIF_TERM nif_shard_broadcast(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
@@ -1470,6 +1562,10 @@ static ErlNifFunc funcs[] = {
     {"shard_init_rccl", 4, nif_shard_init_rccl, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"shard_broadcast", 2, nif_shard_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"shard_run", 2, nif_shard_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"demers_shard_setup", 7, nif_demers_shard_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"demers_shard_run", 2, nif_demers_shard_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"causal_shard_setup", 8, nif_causal_shard_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"causal_shard_step", 2, nif_causal_shard_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

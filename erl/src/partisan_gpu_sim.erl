@@ -18,7 +18,8 @@
          fm_messages/1, fm_take/2, fm_put/2,
          c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
          causal_setup/6, causal_step/2, causal_clocks/1,
-         rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2]).
+         rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2,
+         demers_shard_setup/7, demers_shard_run/2, causal_shard_setup/8, causal_shard_step/2]).
 -export([active_views/1, csr_from_views/1]).
 
 -on_load(init/0).
@@ -254,3 +255,16 @@ csr_from_views(Views) ->
                               {<<0:64/little>>, 0}, Views),
     Col = << <<I:32/little>> || Ids <- Views, I <- Ids >>,
     {RowPtr, Col}.
+
+%% C4 / C5 vertex-sharded over World ranks, the exchange on the handle's RCCL
+%% communicator (shard_init_rccl first; psim_demers_shard_* / psim_causal_shard_step).
+-spec demers_shard_setup(sim(), pos_integer(), pos_integer(), non_neg_integer(), boolean(), non_neg_integer(),
+                         pos_integer()) -> {ok, non_neg_integer(), non_neg_integer()} | error().
+demers_shard_setup(_Sim, _N, _M, _AePeriod, _RumorMongering, _Rank, _World) -> erlang:nif_error(nif_not_loaded).
+-spec demers_shard_run(sim(), pos_integer()) -> {ok, non_neg_integer(), binary()} | error().
+demers_shard_run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
+-spec causal_shard_setup(sim(), pos_integer(), pos_integer(), pos_integer(), pos_integer(), non_neg_integer(),
+                         non_neg_integer(), pos_integer()) -> {ok, non_neg_integer(), non_neg_integer()} | error().
+causal_shard_setup(_Sim, _N, _M, _Period, _DMax, _Redeliver, _Rank, _World) -> erlang:nif_error(nif_not_loaded).
+-spec causal_shard_step(sim(), pos_integer()) -> {ok, [map()]} | error().
+causal_shard_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).

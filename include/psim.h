@@ -510,6 +510,10 @@ int  psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t pe
 int  psim_causal_shard_info(const psim_handle* h, uint32_t* v_lo, uint32_t* n_local);
 int  psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* stats);
 int  psim_causal_shard_ingest(psim_handle* h, const void* slab);
+/* The same exchange inside the library, on the handle's transport
+ * (psim_shard_init_rccl / psim_shard_set_transport; world 1 needs none):
+ * `rounds` rounds, collective, stats GLOBAL (kernel_ms this shard's). */
+int  psim_causal_shard_step(psim_handle* h, uint32_t rounds, psim_causal_stats* stats, size_t cap);
 
 /* --- full-membership strategy (partisan_full_membership_strategy.erl) --
  * Nodes 0..n-1; node v's #full_v1{} membership (a state_orset,

@@ -252,6 +252,7 @@ SIGNATURES = {
     "psim_causal_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32)]),
     "psim_causal_shard_round": (C.c_int, [_H, C.c_void_p, _P(CausalStats)]),
     "psim_causal_shard_ingest": (C.c_int, [_H, C.c_void_p]),
+    "psim_causal_shard_step": (C.c_int, [_H, C.c_uint32, _P(CausalStats), C.c_size_t]),
     "psim_fm_setup": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
     "psim_fm_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_fm_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),

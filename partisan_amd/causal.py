@@ -64,16 +64,42 @@ class ShardedCausal:
     """Causal delivery vertex-sharded over `world` processes, one GPU each
     (SURVEY 8(e), config C5).  Receivers enumerate their own arrivals, so the
     only exchange per round is the 64 x 64 clock slab of the emitters that
-    broadcast: sum-all-reduced (RCCL with backend "nccl", gloo in tests)."""
+    broadcast: sum-all-reduced.
 
-    def __init__(self, n, rank, world, m=64, period=1, dmax=4, redeliver=1, device=0, backend="nccl", seed=0):
+    transport: "rccl" (default with backend "nccl") / "callback" (default
+    with "gloo"): inside libpsim on the handle's transport
+    (psim_causal_shard_step -- what an Erlang host drives through the NIF);
+    "torch": the split-phase entry points with the all-reduce issued from
+    Python."""
+
+    def __init__(self, n, rank, world, m=64, period=1, dmax=4, redeliver=1, device=0, backend="nccl", seed=0,
+                 transport=None):
         import torch
 
         from .sim import Simulator
         self.torch, self.n, self.m, self.rank, self.world, self.backend = torch, n, m, rank, world, backend
+        self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
+        if backend == "nccl":
+            torch.cuda.set_device(self.dev)
         self.sim = Simulator(device=device, seed=seed)
         self._h = self.sim._h
+        if self.transport == "rccl":
+            import torch.distributed as dist
+
+            from ._lib import PSIM_RCCL_ID_BYTES
+            uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES)()
+            if rank == 0:
+                check(lib().psim_rccl_unique_id(uid))
+            if world > 1:
+                box = [bytes(uid)]
+                dist.broadcast_object_list(box, src=0)
+                uid = (C.c_uint8 * PSIM_RCCL_ID_BYTES).from_buffer_copy(box[0])
+            check(lib().psim_shard_init_rccl(self._h, rank, world, uid), self._h)
+        elif self.transport == "callback":
+            from .shard import gloo_transport
+            self._tp, self._keep = gloo_transport()
+            check(lib().psim_shard_set_transport(self._h, C.byref(self._tp)), self._h)
         check(lib().psim_causal_shard_setup(self._h, n, m, period, dmax, redeliver, rank, world), self._h)
         lo, nl = C.c_uint32(), C.c_uint32()
         check(lib().psim_causal_shard_info(self._h, C.byref(lo), C.byref(nl)), self._h)
@@ -91,6 +117,13 @@ class ShardedCausal:
 
     def step(self, rounds=1):
         """Rounds; per-round GLOBAL stats (summed over shards)."""
+        if self.transport != "torch":
+            st = (CausalStats * max(1, rounds))()
+            check(lib().psim_causal_shard_step(self._h, rounds, st, rounds), self._h)
+            out = [s_.as_dict() for s_ in st[:rounds]]
+            for d in out:
+                self.local_kernel_ms += d["kernel_ms"]
+            return out
         import torch.distributed as dist
         out = []
         keys = ["emitted", "received", "delivered", "checks", "buffered", "algo_bytes"]

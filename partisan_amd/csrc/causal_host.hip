@@ -24,9 +24,10 @@ struct CsState : ModuleState {
     uint32_t n_global = 0, v_lo = 0, rank = 0, world = 1;   // vertex shard [v_lo, v_lo + n) of n_global
     uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr;
     unsigned long long *delivered = nullptr, *stats = nullptr, *h_stats = nullptr;
+    uint32_t* x_slab = nullptr;        // the in-library exchange's slab (psim_causal_shard_step)
     uint64_t round = 0;
     ~CsState() override {
-        void* ptrs[] = {clk, self, buf, nbuf, base, delivered, stats};
+        void* ptrs[] = {clk, self, buf, nbuf, base, delivered, stats, x_slab};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (h_stats) (void)hipHostFree(h_stats);
@@ -227,6 +228,45 @@ int psim_causal_shard_ingest(psim_handle* h, const void* slab) {
     uint32_t* sl = c.base + size_t(c.round % kCsWindow) * kCsLanes * kCsLanes;
     HIPCHK(h, hipMemcpyAsync(sl, slab, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, handle_stream(h)));
     HIPCHK(h, hipStreamSynchronize(handle_stream(h)));
+    return PSIM_OK;
+}
+
+int psim_causal_shard_step(psim_handle* h, uint32_t rounds, psim_causal_stats* stats, size_t cap) {
+    if (!h) return PSIM_EINVAL;
+    auto& c = cs_ref(h);
+    if (!c.n_global) return handle_fail(h, PSIM_ESTATE, "psim_causal_shard_setup not called");
+    Transport* T = handle_transport(h);
+    if (c.world > 1 && !T)
+        return handle_fail(h, PSIM_ESTATE, "sharded causal without a transport (psim_shard_init_rccl / _set_transport)");
+    HIPCHK(h, hipSetDevice(handle_device(h)));
+    constexpr size_t kSlab = size_t(kCsLanes) * kCsLanes;
+    if (!c.x_slab && !alloc_zero((void**)&c.x_slab, kSlab * 4)) return handle_fail(h, PSIM_ENOMEM, "causal slab");
+    std::vector<uint32_t> hs(kSlab);
+    std::vector<int64_t> v(kSlab + 6);
+    for (uint32_t i = 0; i < rounds; i++) {
+        psim_causal_stats st;
+        int rc = psim_causal_shard_round(h, c.x_slab, &st);
+        if (rc) return rc;
+        if (c.world > 1) {
+            // the broadcasting emitters' clocks: each row written by its owner,
+            // zero elsewhere -- a sum all-reduce is the gather (16 KB), with the
+            // round's counters in the same call
+            HIPCHK(h, hipMemcpy(hs.data(), c.x_slab, kSlab * 4, hipMemcpyDeviceToHost));
+            for (size_t j = 0; j < kSlab; j++) v[j] = hs[j];
+            const uint64_t loc[6] = {st.emitted, st.received, st.delivered, st.checks, st.buffered, st.algo_bytes};
+            for (int j = 0; j < 6; j++) v[kSlab + j] = (int64_t)loc[j];
+            std::string err;
+            rc = T->allreduce(v.data(), v.size(), handle_stream(h), &err);
+            if (rc) return handle_fail(h, rc, "causal exchange: %s", err.c_str());
+            for (size_t j = 0; j < kSlab; j++) hs[j] = (uint32_t)v[j];
+            HIPCHK(h, hipMemcpy(c.x_slab, hs.data(), kSlab * 4, hipMemcpyHostToDevice));
+            st.emitted = v[kSlab]; st.received = v[kSlab + 1]; st.delivered = v[kSlab + 2];
+            st.checks = v[kSlab + 3]; st.buffered = v[kSlab + 4]; st.algo_bytes = v[kSlab + 5];
+        }
+        rc = psim_causal_shard_ingest(h, c.x_slab);
+        if (rc) return rc;
+        if (stats && i < cap) stats[i] = st;
+    }
     return PSIM_OK;
 }
 

@@ -171,6 +171,22 @@ int main(int argc, char** argv) {
         fprintf(g_out, ", \"demers\": {\"n\": 20000, \"rounds\": %llu, \"complete\": %llu}",
                (unsigned long long)mock_int(mock_elem(r, 1)), (unsigned long long)full);
     }
+    /* ---- the same epidemic vertex-sharded at world 1, exchange on the library's RCCL communicator */
+    {
+        ERL_NIF_TERM sim = new_sim(0x5EED0004ull);
+        ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);
+        want_ok("shard_init_rccl", call("shard_init_rccl", 4, A(sim, mock_uint(0), mock_uint(1), id)));
+        want_ok_tuple("demers_shard_setup", call("demers_shard_setup", 7, A(sim, mock_uint(20000), mock_uint(64),
+                                                                              mock_uint(2), mock_atom("true"),
+                                                                              mock_uint(0), mock_uint(1))));
+        ERL_NIF_TERM r = want_ok_tuple("demers_shard_run", call("demers_shard_run", 2, A(sim, mock_uint(200))));
+        size_t sz;
+        const uint64_t* seen = (const uint64_t*)mock_bin_data(mock_elem(r, 2), &sz);
+        uint64_t full = 0;
+        for (size_t i = 0; i < sz / 8; i++) full += seen[i] == ~0ull;
+        fprintf(g_out, ", \"demers_shard_rccl_world1\": {\"rounds\": %llu, \"complete\": %llu}",
+               (unsigned long long)mock_int(mock_elem(r, 1)), (unsigned long long)full);
+    }
     /* ---- SCAMP v2 join waves ---------------------------------------------- */
     {
         const uint32_t n = 3000;
@@ -379,6 +395,20 @@ int main(int argc, char** argv) {
             if (mock_map_get(mock_list_nth(st, i), "delivered", &x)) delivered += x;
         want_ok_tuple("causal_clocks", call("causal_clocks", 1, A(sim)));
         fprintf(g_out, ", \"causal\": {\"n\": 1000, \"delivered\": %llu}", (unsigned long long)delivered);
+    }
+    /* ---- causal delivery sharded at world 1 over the library's RCCL communicator */
+    {
+        ERL_NIF_TERM sim = new_sim(0x5EED0005ull);
+        ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);
+        want_ok("shard_init_rccl", call("shard_init_rccl", 4, A(sim, mock_uint(0), mock_uint(1), id)));
+        want_ok_tuple("causal_shard_setup", call("causal_shard_setup", 8, A(sim, mock_uint(1000), mock_uint(8),
+                                                                              mock_uint(1), mock_uint(2), mock_uint(1),
+                                                                              mock_uint(0), mock_uint(1))));
+        ERL_NIF_TERM st = mock_elem(want_ok_tuple("causal_shard_step", call("causal_shard_step", 2, A(sim, mock_uint(10)))), 1);
+        uint64_t delivered = 0, x;
+        for (size_t i = 0; i < mock_list_len(st); i++)
+            if (mock_map_get(mock_list_nth(st, i), "delivered", &x)) delivered += x;
+        fprintf(g_out, ", \"causal_shard_rccl_world1\": {\"delivered\": %llu}", (unsigned long long)delivered);
     }
     /* ---- vclock merge on dense lanes ------------------------------------------ */
     {

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = ("emitted", "received", "delivered", "checks", "buffered")
 
 
-def _worker(rank, world, port, n, m, period, dmax, redeliver, backend, q):
+def _worker(rank, world, port, n, m, period, dmax, redeliver, backend, transport, q):
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -33,7 +33,7 @@ def _worker(rank, world, port, n, m, period, dmax, redeliver, backend, q):
         import pyoracle as O
         seed = 0x5EED0005
         g = ShardedCausal(n, rank, world, m=m, period=period, dmax=dmax, redeliver=redeliver, device=0,
-                          backend=backend, seed=seed)
+                          backend=backend, seed=seed, transport=transport)
         o = O.Causal(n, m, period=period, dmax=dmax, redeliver=redeliver, seed=seed)
         assert g.emitters.tolist() == [o.emitter(k) for k in range(m)]
         for _ in range(5):
@@ -57,15 +57,20 @@ def _worker(rank, world, port, n, m, period, dmax, redeliver, backend, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n,m,period,dmax,redeliver", [(2, 600, 16, 1, 4, 1), (4, 1001, 64, 2, 5, 2),
-                                                              (3, 500, 7, 3, 6, 1)])
-def test_sharded_causal_matches_oracle(world, n, m, period, dmax, redeliver):
-    res = run_world(_worker, world, n, m, period, dmax, redeliver, "gloo")
+@pytest.mark.parametrize("world,n,m,period,dmax,redeliver,transport", [(2, 600, 16, 1, 4, 1, "callback"),
+                                                                        (4, 1001, 64, 2, 5, 2, "callback"),
+                                                                        (3, 500, 7, 3, 6, 1, "callback"),
+                                                                        (2, 600, 16, 1, 4, 1, "torch")])
+def test_sharded_causal_matches_oracle(world, n, m, period, dmax, redeliver, transport):
+    """psim_causal_shard_step's exchange inside the library (gloo callbacks)
+    and, for A/B, the split-phase entry points driven from Python."""
+    res = run_world(_worker, world, n, m, period, dmax, redeliver, "gloo", transport)
     for r in range(world):
         assert res[r] == "ok", res[r]
 
 
 @pytest.mark.gpu
-def test_sharded_causal_nccl_world1():
-    res = run_world(_worker, 1, 800, 64, 1, 4, 1, "nccl")
+@pytest.mark.parametrize("transport", ["rccl", "torch"])
+def test_sharded_causal_nccl_world1(transport):
+    res = run_world(_worker, 1, 800, 64, 1, 4, 1, "nccl", transport)
     assert res[0] == "ok", res[0]

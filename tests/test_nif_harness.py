@@ -122,6 +122,8 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rep["shard_rccl_world1"] == {"rounds": rep["c2"]["rounds"], "delivered": n, "step2": 2}
     assert rep["c2_getters"] == {"delivered_mono": n, "messages": 0, "rows0": 0, "is_delivered": n}
     assert rep["demers"]["complete"] == rep["demers"]["n"]
+    # the sharded entry points with the exchange in the library (RCCL, world 1): the same epidemic
+    assert rep["demers_shard_rccl_world1"] == {"rounds": rep["demers"]["rounds"], "complete": rep["demers"]["n"]}
     assert rep["fullmem"]["knows_all"] == rep["fullmem"]["n"]
     assert rep["fullmem"]["tokens_used"] == rep["fullmem"]["own_tokens"] == rep["fullmem"]["n"]
     assert rep["scamp"]["view_entries"] > rep["scamp"]["n"]
@@ -129,6 +131,7 @@ def test_nif_harness_on_gpu(tmp_path):
     _check_fm_wire(rep["fm_wire"])
     assert 0 < rep["c3"]["delivered_live"] <= rep["c3"]["live"]
     assert rep["causal"]["delivered"] > 0
+    assert rep["causal_shard_rccl_world1"]["delivered"] == rep["causal"]["delivered"]
     assert rep["vclock_merge"] == [3, 1, 4]
 
     # the same C2 through the Python binding of the same ABI: bit-identical
