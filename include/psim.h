@@ -424,6 +424,18 @@ int  psim_demers_shard_broadcast_x(psim_handle* h);
 int  psim_demers_shard_step(psim_handle* h, uint32_t rounds, psim_demers_stats* stats, size_t cap);
 int  psim_demers_shard_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats* stats, size_t cap,
                            uint32_t* rounds_run);
+/* How the in-library exchange moves the RM planes and call records: 0 (the
+ * default) sends a round's nonzero RM slots as {slot, any, multi, tri}
+ * records and its callers as {vertex, rumors called, calls before} records
+ * whenever they reach fewer than n/8 slots (counts summed over the shards
+ * first, so every shard picks the same form), the dense slices otherwise;
+ * 1 always dense; 2 always records.  Results are identical.  Collective
+ * setting: every shard must pass the same mode.  *_exchange_stats: bytes
+ * this shard sent to other shards, exchanges run, and how many of them sent
+ * RM records / call records. */
+int  psim_demers_shard_set_exchange(psim_handle* h, int mode);
+int  psim_demers_shard_exchange_stats(const psim_handle* h, uint64_t* bytes_sent, uint32_t* rounds,
+                                      uint32_t* sparse_rm_rounds, uint32_t* sparse_call_rounds);
 
 /* --- HyParView view maintenance (partisan_hyparview_peer_service_manager.erl) */
 typedef struct psim_hv_config {

@@ -231,6 +231,9 @@ SIGNATURES = {
     "psim_demers_shard_broadcast_x": (C.c_int, [_H]),
     "psim_demers_shard_step": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t]),
     "psim_demers_shard_run": (C.c_int, [_H, C.c_uint32, _P(DemersStats), C.c_size_t, _P(C.c_uint32)]),
+    "psim_demers_shard_set_exchange": (C.c_int, [_H, C.c_int]),
+    "psim_demers_shard_exchange_stats": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint32), _P(C.c_uint32),
+                                                   _P(C.c_uint32)]),
     "psim_demers_shard_get_seen": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_hv_setup": (C.c_int, [_H, C.c_uint32, _P(HvConfig)]),
     "psim_hv_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),

@@ -39,197 +39,210 @@ __device__ __forceinline__ uint32_t delay_of(uint2 key, uint32_t v, uint32_t r, 
 // its dependency check can pass again.  A failed `dominates` leaves either a
 // lane j with Local[j] < Dep[j] (recheck once Local[j] >= Dep[j]: the clock
 // only grows) or Local == Dep (recheck after the next delivery, the only thing
-// that changes the clock).  Entries loaded at the start of a round are
-// unchecked.  A fold visits every entry in list order exactly as
-// lists:foldl does; an entry whose watch still holds is not deliverable, so
+// that changes the clock).  A watch is (ja, x): ja = 4 j, the ds_bpermute
+// address of clock lane j, and the entry is rechecked once c[j] >= x; ja =
+// kWatchAny rechecks once the delivery count reaches x.  An unchecked entry
+// (loaded at the start of the round, or just received) has (0, 0), which
+// always holds; register lanes past the buffer hold (kWatchAny, kNever),
+// which never does.  A fold visits every entry in list order exactly as
+// lists:foldl does; an entry whose watch is closed is not deliverable, so
 // skipping its full check changes nothing but the work (it still counts as
 // one dependency check).
-constexpr uint32_t kWatchAny = 64;      // Local == Dep: recheck after a delivery
-constexpr uint32_t kWatchNone = 65;     // not checked this round
+constexpr uint32_t kWatchAny = 256u;
+constexpr uint32_t kNever = 0xFFFFFFFFu;
 
 struct Wave {
     const CsArgs* a;
     uint32_t v, lane, c, self, nb;
-    uint32_t eid;                       // lane k: emitter_id(k)
-    int ke;
+    uint32_t rk;                        // lane k: raise of emitter k's messages to v (rank(v) + 1)
+    uint32_t inc;                       // 1 at v's own emitter lane: a delivery increments it
+    uint32_t self_inc;                  // 1 when v is no emitter: a delivery increments its own entry
     uint32_t* sbuf;                     // entries (k << 24 | round), list order
-    uint32_t* wj;                       // watch lane / kWatchAny / kWatchNone
-    uint32_t* wx;                       // watch value (clock entry or delivery count)
+    uint32_t* wj;                       // watch address
+    uint32_t* wx;                       // watch threshold
     // while nb <= 64 the buffer lives in registers, entry l at lane l
-    uint32_t rent, rjw, rxw;
-    unsigned long long pend;            // register entries whose watch no longer holds
+    uint32_t rent, rja, rxw;
+    unsigned long long pend;            // register entries whose watch is open
     uint32_t inreg;                     // 1 while the buffer is in registers
-    bool old_any;                       // a loaded entry is older than the clock window
     uint32_t received, delivered, checks, err;
 };
-
-// the clocks entry (k, r) is checked against, at this lane: the message's
-// (ml) and its order-buffer dependency's (dl, only used when r > period)
-struct Clocks { uint32_t ml, dl; };
-__device__ __forceinline__ Clocks load_clocks(const Wave& w, uint32_t k, uint32_t r) {
-    const CsArgs& a = *w.a;
-    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)w.eid, (int)k);
-    const uint32_t raise = w.lane == k ? w.v - (w.v > e ? 1u : 0u) + 1u : 0u;
-    const uint32_t* row = a.base + k * kCsLanes + w.lane;
-    Clocks q;
-    q.ml = row[(r % kCsWindow) * kCsLanes * kCsLanes] + raise;
-    q.dl = r > a.period ? row[((r - a.period) % kCsWindow) * kCsLanes * kCsLanes] + raise : 0u;
-    return q;
-}
 
 // a wave-uniform value, moved to a scalar register (the compiler cannot
 // always prove uniformity through the fold's loops)
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-
-// internal_receive_message/2 (:309-344) + deliver/5 (:265-300) for (k, r);
-// on failure (jw, xw) is the entry's new watch
-__device__ bool try_deliver(Wave& w, uint32_t r, const Clocks& q, uint32_t& jw, uint32_t& xw) {
-    const CsArgs& a = *w.a;
-    bool ok = true;
-    if (r > a.period) {                                   // orddict:find(MyNode, IncomingOrderBuffer) -> {ok, Dep}
-        const uint32_t dl = q.dl;
-        w.checks = uni(w.checks + 1u);
-        // dominates(Local, Dep) = descends(Local, Dep) andalso not descends(Dep, Local)
-        const unsigned long long f1 = __ballot(!(dl == 0u || w.c >= dl));
-        const unsigned long long f2 = __ballot(!(w.c == 0u || dl >= w.c));
-        if (f1) {
-            jw = uni((uint32_t)__ffsll((long long)f1) - 1u);
-            xw = uni((uint32_t)__builtin_amdgcn_readlane((int)dl, (int)jw));
-            ok = false;
-        } else if (f2 == 0ull && w.self == 0u) {
-            jw = kWatchAny;
-            xw = w.delivered;
-            ok = false;
-        }
-    }
-    if (ok) {
-        w.c = max(w.c, q.ml);                             // merge([LocalClock, MessageClock])
-        if (w.ke >= 0) w.c += w.lane == (uint32_t)w.ke ? 1u : 0u;   // increment(MyNode, ...)
-        else w.self = uni(w.self + 1u);
-        w.delivered = uni(w.delivered + 1u);
-    }
-    return ok;
-}
-
-// the fold over one 64-entry slice (lane l holds the slice's entry l; lanes
-// outside `vmask` hold none): every entry in list order, full dependency
-// checks only where the watch no longer holds; returns the delivered lanes
-__device__ unsigned long long fold_slice(Wave& w, uint32_t ent, uint32_t& jw, uint32_t& xw,
-                                         unsigned long long vmask) {
-    const bool valid = (vmask >> w.lane) & 1ull;
-    unsigned long long gone = 0, seen = 0;
-    uint32_t from = 0;                                    // first lane not yet visited
-    for (;;) {
-        const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(jw & 63u), 64);
-        const bool cand = (jw == kWatchNone) | ((jw == kWatchAny) & (w.delivered > xw)) | ((jw < 64u) & (cj >= xw));
-        const unsigned long long m = __ballot(valid & cand) & (~0ull << from);
-        if (!m) break;
-        const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
-        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)ent, (int)l));
-        uint32_t nj = 0, nx = 0;
-        seen |= 1ull << l;
-        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) gone |= 1ull << l;
-        else {
-            jw = w.lane == l ? nj : jw;
-            xw = w.lane == l ? nx : xw;
-        }
-        if (l == 63u) break;
-        from = l + 1u;
-    }
-    w.checks = uni(w.checks + (uint32_t)__popcll(vmask & ~seen));   // watched entries: checks that cannot pass
-    return gone;
-}
-
-__device__ __forceinline__ unsigned long long first_n(uint32_t n) { return n >= 64u ? ~0ull : (1ull << n) - 1ull; }
 __device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
     return ((unsigned long long)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
+// lane l of `old` replaced by the wave-uniform x (a compare shared by the
+// writes to one lane and a v_cndmask each: VALU, where the scalar unit is the
+// busier one)
+__device__ __forceinline__ uint32_t wlane(uint32_t x, uint32_t l, uint32_t old) {
+    return (uint32_t)(threadIdx.x & 63u) == l ? x : old;
+}
+__device__ __forceinline__ unsigned long long first_n(uint32_t n) { return n >= 64u ? ~0ull : (1ull << n) - 1ull; }
 
-// the register entries whose watch no longer holds (clock or delivery count moved)
-__device__ __forceinline__ unsigned long long pending(const Wave& w) {
-    const uint32_t cj = (uint32_t)__shfl((int)w.c, (int)(w.rjw & 63u), 64);
-    const bool cand = (w.rjw == kWatchNone) | ((w.rjw == kWatchAny) & (w.delivered > w.rxw)) |
-                      ((w.rjw < 64u) & (cj >= w.rxw));
-    return uni64(__ballot(cand) & first_n(w.nb));
+__device__ __forceinline__ bool watch_open(const Wave& w, uint32_t ja, uint32_t x) {
+    const uint32_t cj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)ja, (int)w.c);
+    return (ja == kWatchAny ? w.delivered : cj) >= x;
 }
 
-// the fold over the register entries: only pending entries are checked;
-// the pending set is recomputed after each delivery (the only event that
-// moves the clock), so a fold in which nothing is delivered costs one check
-// per pending entry
-__device__ void fold_reg(Wave& w) {
+// the base-clock rows entry (k, r) is checked against, at this lane: the
+// message's (round r) and its order-buffer dependency's (round r - period;
+// only used when r > period, so an earlier round's slot is harmless)
+struct Rows { uint32_t ml, dl; };
+__device__ __forceinline__ Rows load_rows(const Wave& w, uint32_t e) {
+    const CsArgs& a = *w.a;
+    const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
+    const uint32_t* pm = a.base + ((r % kCsWindow) * kCsLanes + k) * kCsLanes;
+    const uint32_t* pd = a.base + (((r - a.period) % kCsWindow) * kCsLanes + k) * kCsLanes;
+    Rows q;
+    q.ml = pm[w.lane];
+    q.dl = pd[w.lane];
+    return q;
+}
+
+// internal_receive_message/2 (:309-344) + deliver/5 (:265-300) for entry e
+// whose rows are q; on failure (ja, x) is the entry's new watch
+__device__ __forceinline__ bool try_deliver(Wave& w, uint32_t e, const Rows& q, uint32_t& ja, uint32_t& x) {
+    const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
+    const uint32_t rs = w.lane == k ? w.rk : 0u;          // lane k raised by rank(v) + 1
+    if (r > w.a->period) {                                // orddict:find(MyNode, IncomingOrderBuffer) -> {ok, Dep}
+        const uint32_t dl = q.dl + rs;
+        w.checks++;
+        // dominates(Local, Dep) = descends(Local, Dep) andalso not descends(Dep, Local)
+        const unsigned long long f1 = __ballot(w.c < dl);
+        if (f1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(f1);
+            ja = 4u * j;
+            x = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
+            return false;
+        }
+        if (w.self == 0u && __ballot(dl < w.c) == 0ull) {
+            ja = kWatchAny;
+            x = w.delivered + 1u;
+            return false;
+        }
+    }
+    w.c = max(w.c, q.ml + rs) + w.inc;                    // merge([LocalClock, MessageClock]), increment(MyNode, ...)
+    w.self += w.self_inc;
+    w.delivered++;
+    return true;
+}
+
+// the register entries whose watch is open
+__device__ __forceinline__ unsigned long long pending(const Wave& w) {
+    return uni64(__ballot(watch_open(w, w.rja, w.rxw)));
+}
+
+// the fold over the register entries: only open entries are checked; the
+// open set is recomputed after each delivery (the only event that moves the
+// clock), so a fold in which nothing is delivered costs one check per open
+// entry.  (he, hq): the entry just appended and its rows, loaded ahead.
+__device__ void fold_reg(Wave& w, bool hinted, uint32_t he, const Rows& hq) {
     const uint32_t n0 = uni(w.nb);
     if (n0 == 0u) return;
-    if (uni64(w.pend) == 1ull << (n0 - 1u)) {
+    const uint32_t last = n0 - 1u;
+    if (w.pend == 1ull << last) {
         // the common fold: only the entry just appended can pass (the others'
         // watches hold); it leaves from the end, so nothing moves
-        const uint32_t l = n0 - 1u;
-        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)l));
-        uint32_t nj = 0, nx = 0;
-        w.checks = uni(w.checks + l);
-        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) {
-            w.nb = l;
+        const uint32_t e = hinted ? he : uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)last));
+        const Rows q = hinted ? hq : load_rows(w, e);
+        uint32_t ja = 0, x = 0;
+        w.checks += last;
+        if (try_deliver(w, e, q, ja, x)) {
+            w.nb = last;
+            w.rja = wlane(kWatchAny, last, w.rja);
+            w.rxw = wlane(kNever, last, w.rxw);
             w.pend = pending(w);
         } else {
-            w.rjw = w.lane == l ? nj : w.rjw;
-            w.rxw = w.lane == l ? nx : w.rxw;
+            w.rja = wlane(ja, last, w.rja);
+            w.rxw = wlane(x, last, w.rxw);
             w.pend = 0ull;
         }
         return;
     }
     unsigned long long gone = 0;
     uint32_t tried = 0;
-    unsigned long long m = uni64(w.pend);
+    unsigned long long m = w.pend;
     while (m) {
-        const uint32_t l = uni((uint32_t)__ffsll((long long)m) - 1u);
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
         const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)l));
-        uint32_t nj = 0, nx = 0;
+        const Rows q = hinted && l == last ? hq : load_rows(w, e);
+        uint32_t ja = 0, x = 0;
         tried++;
-        if (try_deliver(w, e & 0xFFFFFFu, load_clocks(w, e >> 24, e & 0xFFFFFFu), nj, nx)) {
+        if (try_deliver(w, e, q, ja, x)) {
             gone |= 1ull << l;
-            w.pend = uni64(pending(w) & ~gone);
+            w.rja = wlane(kWatchAny, l, w.rja);
+            w.rxw = wlane(kNever, l, w.rxw);
+            w.pend = pending(w);
         } else {
-            w.rjw = w.lane == l ? nj : w.rjw;
-            w.rxw = w.lane == l ? nx : w.rxw;
-            w.pend = uni64(w.pend & ~(1ull << l));
+            w.rja = wlane(ja, l, w.rja);
+            w.rxw = wlane(x, l, w.rxw);
+            w.pend &= ~(1ull << l);
         }
         if (l == 63u) break;
-        m = uni64(w.pend & (~0ull << (l + 1u)));
+        m = w.pend & (~0ull << (l + 1u));
     }
-    w.checks = uni(w.checks + n0 - tried);                // watched entries: checks that cannot pass
+    w.checks += n0 - tried;                               // watched entries: checks that cannot pass
     if (!gone) return;
-    const uint32_t nk = uni(n0 - (uint32_t)__popcll(gone));
-    if (gone != 1ull << (n0 - 1u)) {
+    const uint32_t nk = n0 - (uint32_t)__popcll(gone);
+    if (gone != 1ull << last) {
         // compact: kept entries to the front in order, the rest behind them
         // (a permutation of the 64 lanes, so ds_permute moves every value)
         const unsigned long long kept = first_n(n0) & ~gone, lt = (1ull << w.lane) - 1ull;
         const uint32_t o = 4u * ((kept >> w.lane) & 1ull ? (uint32_t)__popcll(kept & lt)
                                                           : nk + (uint32_t)__popcll(~kept & lt));
         w.rent = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rent);
-        w.rjw = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rjw);
+        w.rja = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rja);
         w.rxw = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)w.rxw);
-        const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_permute((int)o, (int)((w.pend >> w.lane) & 1ull));
         w.nb = nk;
-        w.pend = uni64(__ballot(pb != 0u) & first_n(nk));
+        w.pend = pending(w);                              // removed lanes hold (kWatchAny, kNever)
     } else {
         w.nb = nk;                                        // the last entry left: nothing moves
     }
 }
 
+// the fold over one 64-entry slice of the LDS buffer (lane l holds the
+// slice's entry l; lanes outside `vmask` hold none): every entry in list
+// order, full dependency checks only where the watch is open; returns the
+// delivered lanes
+__device__ unsigned long long fold_slice(Wave& w, uint32_t ent, uint32_t& jw, uint32_t& xw,
+                                         unsigned long long vmask) {
+    const bool valid = (vmask >> w.lane) & 1ull;
+    unsigned long long gone = 0, seen = 0;
+    uint32_t from = 0;                                    // first lane not yet visited
+    for (;;) {
+        const bool open = watch_open(w, jw, xw);         // every lane takes part in the ds_bpermute
+        const unsigned long long m = __ballot(valid & open) & (~0ull << from);
+        if (!m) break;
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)ent, (int)l));
+        uint32_t ja = 0, x = 0;
+        seen |= 1ull << l;
+        if (try_deliver(w, e, load_rows(w, e), ja, x)) gone |= 1ull << l;
+        else {
+            jw = wlane(ja, l, jw);
+            xw = wlane(x, l, xw);
+        }
+        if (l == 63u) break;
+        from = l + 1u;
+    }
+    w.checks += (uint32_t)__popcll(vmask & ~seen);       // watched entries: checks that cannot pass
+    return gone;
+}
+
 // one lists:foldl over the buffer snapshot; delivered entries leave the
-// buffer, the others keep their order.  An old entry is visited by every
-// fold, so the window error is raised by the first fold of the round.
-__device__ void fold(Wave& w) {
-    if (w.old_any) w.err = uni(w.err | 2u);
-    if (uni(w.inreg)) {
-        fold_reg(w);
+// buffer, the others keep their order
+__device__ void fold(Wave& w, bool hinted, uint32_t he, const Rows& hq) {
+    if (w.inreg) {
+        fold_reg(w, hinted, he, hq);
         return;
     }
-    const uint32_t n0 = uni(w.nb);
+    const uint32_t n0 = w.nb;
     uint32_t keep = 0;
-    for (uint32_t s0 = 0; s0 < n0; s0 = uni(s0 + 64u)) {
+    for (uint32_t s0 = 0; s0 < n0; s0 += 64u) {
         const uint32_t i = s0 + w.lane;
-        uint32_t ent = 0, jw = kWatchNone, xw = 0;
+        uint32_t ent = 0, jw = kWatchAny, xw = kNever;
         if (i < n0) { ent = w.sbuf[i]; jw = w.wj[i]; xw = w.wx[i]; }
         const unsigned long long vmask = __ballot(i < n0);
         const unsigned long long kept = vmask & ~fold_slice(w, ent, jw, xw, vmask);
@@ -239,38 +252,39 @@ __device__ void fold(Wave& w) {
             w.wj[o] = jw;
             w.wx[o] = xw;
         }
-        keep = uni(keep + (uint32_t)__popcll(kept));
+        keep += (uint32_t)__popcll(kept);
         __builtin_amdgcn_wave_barrier();
     }
     w.nb = keep;
     if (keep <= 64u) {                                    // back to registers
         w.inreg = 1u;
         w.rent = w.lane < keep ? w.sbuf[w.lane] : 0u;
-        w.rjw = w.lane < keep ? w.wj[w.lane] : kWatchNone;
-        w.rxw = w.lane < keep ? w.wx[w.lane] : 0u;
+        w.rja = w.lane < keep ? w.wj[w.lane] : kWatchAny;
+        w.rxw = w.lane < keep ? w.wx[w.lane] : kNever;
         w.pend = pending(w);
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-// append a received entry at the end of the buffer
-__device__ void append(Wave& w, uint32_t e) {
-    w.nb = uni(w.nb);
-    w.inreg = uni(w.inreg);
+// append a received entry, unchecked, at the end of the buffer
+__device__ __forceinline__ void append(Wave& w, uint32_t e) {
     if (w.inreg && w.nb == 64u) {                         // spill the registers
         w.sbuf[w.lane] = w.rent;
-        w.wj[w.lane] = w.rjw;
+        w.wj[w.lane] = w.rja;
         w.wx[w.lane] = w.rxw;
         w.inreg = 0u;
     }
     if (w.inreg) {
-        if (w.lane == w.nb) { w.rent = e; w.rjw = kWatchNone; }
-        w.pend = uni64(w.pend | (1ull << w.nb));
+        w.rent = wlane(e, w.nb, w.rent);
+        w.rja = wlane(0u, w.nb, w.rja);
+        w.rxw = wlane(0u, w.nb, w.rxw);
+        w.pend |= 1ull << w.nb;
     } else if (w.lane == 0) {
         w.sbuf[w.nb] = e;
-        w.wj[w.nb] = kWatchNone;
+        w.wj[w.nb] = 0u;
+        w.wx[w.nb] = 0u;
     }
-    w.nb = uni(w.nb + 1u);
+    w.nb++;
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -278,6 +292,7 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
     __shared__ uint32_t sbuf[kWavesPerBlock][kCsBufCap];
     __shared__ uint32_t wj[kWavesPerBlock][kCsBufCap];
     __shared__ uint32_t wx[kWavesPerBlock][kCsBufCap];
+    __shared__ uint32_t alist[kWavesPerBlock][64];
     __shared__ unsigned long long red[kWavesPerBlock][4];
     // wave-uniform values are read into scalar registers explicitly, so the
     // fold's control flow stays scalar (no exec-mask bookkeeping)
@@ -294,14 +309,17 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         w.wj = wj[wv];
         w.wx = wx[wv];
         w.c = a.clk[(size_t)lv * kCsLanes + lane];
-        w.self = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.self[lv]);
-        w.eid = lane < a.m ? emitter_id(lane, a.n_global, a.m) : 0xFFFFFFFFu;
-        w.ke = (int)uni((uint32_t)emitter_index(w.v, a.n_global, a.m));
+        w.self = uni(a.self[lv]);
+        const uint32_t eid = lane < a.m ? emitter_id(lane, a.n_global, a.m) : 0xFFFFFFFFu;
+        const int ke = (int)uni((uint32_t)emitter_index(w.v, a.n_global, a.m));
+        w.rk = w.v - (w.v > eid ? 1u : 0u) + 1u;
+        w.inc = ke >= 0 && lane == (uint32_t)ke ? 1u : 0u;
+        w.self_inc = ke < 0 ? 1u : 0u;
         w.nb = uni(a.nbuf[lv]);
         w.inreg = w.nb <= 64u ? 1u : 0u;
         w.rent = 0;
-        w.rjw = kWatchNone;
-        w.rxw = 0;
+        w.rja = w.lane < w.nb ? 0u : kWatchAny;           // loaded entries are unchecked
+        w.rxw = w.lane < w.nb ? 0u : kNever;
         w.pend = w.inreg ? first_n(w.nb) : 0ull;
         bool old = false;
         for (uint32_t i = lane; i < w.nb; i += 64) {
@@ -310,33 +328,74 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
             if (w.inreg) w.rent = e;
             else {
                 w.sbuf[i] = e;
-                w.wj[i] = kWatchNone;
+                w.wj[i] = 0u;
+                w.wx[i] = 0u;
             }
         }
-        w.old_any = __ballot(old) != 0ull;
+        const bool old_any = __ballot(old) != 0ull;
         __builtin_amdgcn_wave_barrier();
         // arrivals of round t: lane k marks bit d if k's round-(t-d) message lands now
         uint32_t am = 0;
-        if (lane < a.m && w.eid != w.v) {
+        if (lane < a.m && eid != w.v) {
             const uint32_t ph = lane % a.period;
             for (uint32_t d = 1; d <= a.dmax && d < a.t; d++) {
                 const uint32_t r = a.t - d;
                 if (r % a.period == ph && delay_of(a.key, w.v, r, lane, a.dmax) == d) am |= 1u << d;
             }
         }
-        // receive_message (:205-220) in (src, seq) order: emitter id, then oldest round first
-        for (;;) {
-            const unsigned long long any = __ballot(am != 0u);
-            if (!any) break;
-            const uint32_t k = uni((uint32_t)__ffsll((long long)any) - 1u);
-            const uint32_t d = uni(31u - __clz((uint32_t)__builtin_amdgcn_readlane((int)am, (int)k)));
-            if (lane == k) am &= ~(1u << d);
-            w.received = uni(w.received + 1u);
-            if (w.nb >= kCsBufCap) { w.err = uni(w.err | 1u); continue; }
-            append(w, (k << 24) | (a.t - d));
-            fold(w);
+        // receive_message (:205-220) in (src, seq) order: emitter id, then
+        // oldest round first.  Arrival i sits at position pre(k) + (bits of
+        // lane k above d); the list is staged 64 arrivals at a time.
+        uint32_t pre = 0, total = 0;
+        for (uint32_t d = 1; d <= a.dmax; d++) {
+            const unsigned long long b = __ballot((am >> d) & 1u);
+            pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            total += (uint32_t)__popcll(b);
         }
-        if (a.redeliver && a.t % a.redeliver == 0) fold(w);   // handle_info(deliver) (:233-248)
+        uint32_t* al = alist[wv];
+        auto chunk = [&](uint32_t base) -> uint32_t {
+            for (uint32_t d = 1; d <= a.dmax; d++) {
+                if ((am >> d) & 1u) {
+                    const uint32_t p = pre + (uint32_t)__popc(am >> (d + 1u)) - base;
+                    if (p < 64u) al[p] = (lane << 24) | (a.t - d);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t x = al[lane];
+            __builtin_amdgcn_wave_barrier();
+            return x;
+        };
+        bool folded = false;
+        if (total) {
+            uint32_t lst = chunk(0);
+            uint32_t ecur = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, 0));
+            Rows qcur = load_rows(w, ecur);
+            for (uint32_t i = 0; i < total; i++) {
+                uint32_t enext = 0;
+                Rows qnext = qcur;
+                if (i + 1u < total) {                     // the next arrival's rows, loaded ahead
+                    if (((i + 1u) & 63u) == 0u) lst = chunk(i + 1u);
+                    enext = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)((i + 1u) & 63u)));
+                    qnext = load_rows(w, enext);
+                }
+                w.received++;
+                if (w.nb >= kCsBufCap) w.err |= 1u;
+                else {
+                    append(w, ecur);
+                    fold(w, true, ecur, qcur);
+                    folded = true;
+                }
+                ecur = enext;
+                qcur = qnext;
+            }
+        }
+        if (a.redeliver && a.t % a.redeliver == 0) {     // handle_info(deliver) (:233-248)
+            fold(w, false, 0u, Rows{0u, 0u});
+            folded = true;
+        }
+        // an old entry is visited by every fold, so the window error is
+        // raised by the first fold of the round
+        if (old_any && folded) w.err |= 2u;
         a.clk[(size_t)lv * kCsLanes + lane] = w.c;
         if (lane == 0) {
             a.self[lv] = w.self;

@@ -318,6 +318,113 @@ __global__ __launch_bounds__(kBlock) void dm_sum_slices_kernel(const unsigned lo
     }
 }
 
+// ---- sparse exchange records (psim.h "vertex-sharded Demers") -------------
+// A round whose RM messages reach few slots sends {slot, any, multi, tri}
+// records (7 words) instead of the three dense 8 B x C slices per peer, and
+// its RM call records as {vertex, rumors called, calls before} (4 words)
+// instead of the all-gathered 12 B x C planes.
+
+// per destination shard g != rank: slots of slice g with an RM bit (any is
+// the superset plane); cnt[world]: this shard's vertices that called select
+__global__ __launch_bounds__(kBlock) void dm_xcount_kernel(const unsigned long long* __restrict__ any, uint32_t world,
+                                                           uint32_t rank, uint32_t chunk,
+                                                           const unsigned long long* __restrict__ rn_own,
+                                                           uint32_t n_own, uint32_t* __restrict__ cnt) {
+    const size_t total = size_t(world) * chunk;
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < total + n_own; i += stride) {
+        bool hit;
+        uint32_t g;
+        if (i < total) {
+            g = (uint32_t)(i / chunk);
+            hit = g != rank && any[i] != 0ull;
+        } else {
+            g = world;
+            hit = rn_own[i - total] != 0ull;
+        }
+        // one atomic per wave and destination: the lanes of a wave share g
+        // except where a slice boundary falls inside the wave (lane 0, the
+        // lowest index, is active whenever any lane is)
+        const uint32_t g0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+        const unsigned long long same = __ballot(hit && g == g0);
+        if ((threadIdx.x & 63) == 0 && same) atomicAdd(&cnt[g0], (uint32_t)__popcll(same));
+        if (hit && g != g0) atomicAdd(&cnt[g], 1u);
+    }
+}
+
+// records of the RM slots for shard g at rec + 7 (off[g] + k), k from cursor[g]
+__global__ __launch_bounds__(kBlock) void dm_xpack_rm_kernel(const unsigned long long* __restrict__ rm, size_t plane,
+                                                             uint32_t world, uint32_t rank, uint32_t chunk,
+                                                             const uint32_t* __restrict__ off,
+                                                             uint32_t* __restrict__ cursor, uint32_t* __restrict__ rec) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < plane; i += stride) {
+        const uint32_t g = (uint32_t)(i / chunk);
+        const unsigned long long a = rm[i];
+        if (g == rank || a == 0ull) continue;
+        const unsigned long long m = rm[plane + i], t = rm[2 * plane + i];
+        uint32_t* o = rec + 7 * (size_t)(off[g] + atomicAdd(&cursor[g], 1u));
+        o[0] = (uint32_t)(i - size_t(g) * chunk);
+        o[1] = (uint32_t)a;
+        o[2] = (uint32_t)(a >> 32);
+        o[3] = (uint32_t)m;
+        o[4] = (uint32_t)(m >> 32);
+        o[5] = (uint32_t)t;
+        o[6] = (uint32_t)(t >> 32);
+    }
+}
+
+// received RM records into the dense receive planes (slice s = records from
+// shard s, off[s] .. off[s+1]; the slices were zeroed)
+__global__ __launch_bounds__(kBlock) void dm_xunpack_rm_kernel(const uint32_t* __restrict__ rec,
+                                                               const uint32_t* __restrict__ off, uint32_t world,
+                                                               uint32_t chunk, size_t plane,
+                                                               unsigned long long* __restrict__ rm) {
+    const uint32_t total = off[world];
+    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < total; j += gridDim.x * kBlock) {
+        uint32_t s = 0;
+        while (off[s + 1] <= j) s++;
+        const uint32_t* x = rec + 7 * (size_t)j;
+        const size_t i = size_t(s) * chunk + x[0];
+        rm[i] = (unsigned long long)x[1] | ((unsigned long long)x[2] << 32);
+        rm[plane + i] = (unsigned long long)x[3] | ((unsigned long long)x[4] << 32);
+        rm[2 * plane + i] = (unsigned long long)x[5] | ((unsigned long long)x[6] << 32);
+    }
+}
+
+// this shard's RM call records {global vertex, rumors called, calls before},
+// written once per other shard (regions of `per` records, own region skipped)
+__global__ __launch_bounds__(kBlock) void dm_xpack_rmx_kernel(const unsigned long long* __restrict__ rn,
+                                                              const uint32_t* __restrict__ ncall, uint32_t v_lo,
+                                                              uint32_t n_own, uint32_t world, uint32_t rank,
+                                                              uint32_t per, uint32_t* __restrict__ cursor,
+                                                              uint32_t* __restrict__ rec) {
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_own; i += gridDim.x * kBlock) {
+        const unsigned long long x = rn[v_lo + i];
+        if (x == 0ull) continue;
+        const uint32_t k = atomicAdd(cursor, 1u);
+        for (uint32_t g = 0, q = 0; g < world; g++) {
+            if (g == rank) continue;
+            uint32_t* o = rec + 4 * ((size_t)q * per + k);
+            o[0] = v_lo + i;
+            o[1] = (uint32_t)x;
+            o[2] = (uint32_t)(x >> 32);
+            o[3] = ncall[v_lo + i];
+            q++;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void dm_xunpack_rmx_kernel(const uint32_t* __restrict__ rec, uint32_t nrec,
+                                                                unsigned long long* __restrict__ rn,
+                                                                uint32_t* __restrict__ ncall) {
+    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < nrec; j += gridDim.x * kBlock) {
+        const uint32_t* x = rec + 4 * (size_t)j;
+        rn[x[0]] = (unsigned long long)x[1] | ((unsigned long long)x[2] << 32);
+        ncall[x[0]] = x[3];
+    }
+}
+
 __global__ void dm_origin_kernel(uint2 key, uint32_t n, uint32_t m, uint32_t* __restrict__ origin) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
@@ -359,6 +466,50 @@ hipError_t launch_dm_ingest_rm(const DmArgs& a, const unsigned long long* rm_rec
     if (g > 8192) g = 8192;
     if (g == 0) return hipSuccess;
     hipLaunchKernelGGL(dm_ingest_kernel, dim3(g), dim3(kBlock), 0, s, a, rm_recv, pull_recv, world, chunk);
+    return hipGetLastError();
+}
+
+static uint32_t dm_grid(size_t n) {
+    size_t g = (n + kBlock - 1) / kBlock;
+    return (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
+}
+
+hipError_t launch_dm_xcount(const unsigned long long* any, uint32_t world, uint32_t rank, uint32_t chunk,
+                            const unsigned long long* rn_own, uint32_t n_own, uint32_t* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(dm_xcount_kernel, dim3(dm_grid(size_t(world) * chunk + n_own)), dim3(kBlock), 0, s, any, world,
+                       rank, chunk, rn_own, n_own, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_dm_xpack_rm(const unsigned long long* rm, uint32_t world, uint32_t rank, uint32_t chunk,
+                              const uint32_t* off, uint32_t* cursor, uint32_t* rec, hipStream_t s) {
+    const size_t plane = size_t(world) * chunk;
+    hipLaunchKernelGGL(dm_xpack_rm_kernel, dim3(dm_grid(plane)), dim3(kBlock), 0, s, rm, plane, world, rank, chunk, off,
+                       cursor, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_dm_xunpack_rm(const uint32_t* rec, const uint32_t* off, uint32_t world, uint32_t chunk,
+                                uint32_t nrec, unsigned long long* rm, hipStream_t s) {
+    if (nrec == 0) return hipSuccess;
+    hipLaunchKernelGGL(dm_xunpack_rm_kernel, dim3(dm_grid(nrec)), dim3(kBlock), 0, s, rec, off, world, chunk,
+                       size_t(world) * chunk, rm);
+    return hipGetLastError();
+}
+
+hipError_t launch_dm_xpack_rmx(const unsigned long long* rn, const uint32_t* ncall, uint32_t v_lo, uint32_t n_own,
+                               uint32_t world, uint32_t rank, uint32_t per, uint32_t* cursor, uint32_t* rec,
+                               hipStream_t s) {
+    if (n_own == 0) return hipSuccess;
+    hipLaunchKernelGGL(dm_xpack_rmx_kernel, dim3(dm_grid(n_own)), dim3(kBlock), 0, s, rn, ncall, v_lo, n_own, world,
+                       rank, per, cursor, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_dm_xunpack_rmx(const uint32_t* rec, uint32_t nrec, unsigned long long* rn, uint32_t* ncall,
+                                 hipStream_t s) {
+    if (nrec == 0) return hipSuccess;
+    hipLaunchKernelGGL(dm_xunpack_rmx_kernel, dim3(dm_grid(nrec)), dim3(kBlock), 0, s, rec, nrec, rn, ncall);
     return hipGetLastError();
 }
 

@@ -191,12 +191,21 @@ struct DmShard : ModuleState {
     unsigned long long *x_rm_shadow = nullptr, *x_rm_recv = nullptr, *x_pull_shadow = nullptr, *x_pull_all = nullptr,
                        *x_pull_sum = nullptr, *x_snap_all = nullptr, *x_rmx_all = nullptr;
     uint64_t complete_g = 0;      // vertices holding every rumor, over all shards, after the last round
+    // sparse records (dms_exchange): per-destination counts, record offsets
+    // (device and pinned host: [cnt G+1][send G+1][recv G+1]), cursors, buffers
+    int xmode = 0;                // 0 auto, 1 dense, 2 sparse (psim_demers_shard_set_exchange)
+    uint32_t *x_cnt = nullptr, *x_off = nullptr, *x_cur = nullptr, *h_x = nullptr, *x_sp_send = nullptr,
+             *x_sp_recv = nullptr;
+    size_t x_cap_send = 0, x_cap_recv = 0;      // words
+    uint64_t x_bytes = 0;                       // bytes this shard sent to other shards
+    uint32_t x_rounds = 0, x_sparse_rm = 0, x_sparse_rmx = 0;
     ~DmShard() override {
         void* p[] = {seen, rm[0], rm[1], rm[2], pull, stats, rmnew_prev, ncall_prev, pushcnt[0], pushcnt[1],
                      pushlist[0], pushlist[1], origin, idbit, x_rm_shadow, x_rm_recv, x_pull_shadow, x_pull_all,
-                     x_pull_sum, x_snap_all, x_rmx_all};
+                     x_pull_sum, x_snap_all, x_rmx_all, x_cnt, x_off, x_cur, x_sp_send, x_sp_recv};
         for (void* x : p)
             if (x) (void)hipFree(x);
+        if (h_x) (void)hipHostFree(h_x);
     }
 };
 
@@ -247,18 +256,129 @@ int dms_x_buffers(psim_handle* h, DmShard& d) {
     if (d.x_rm_shadow) return PSIM_OK;
     const size_t NG = size_t(d.world) * d.chunk;
     auto A = [&](unsigned long long** p, size_t words) { return alloc_zero((void**)p, std::max<size_t>(words, 1) * 8); };
+    const size_t G1 = size_t(d.world) + 1;
     if (!A(&d.x_rm_shadow, 3 * NG) || !A(&d.x_rm_recv, 3 * NG) || !A(&d.x_pull_shadow, 2 * NG) ||
         !A(&d.x_pull_all, 2 * NG) || !A(&d.x_pull_sum, 2 * size_t(d.chunk)) || !A(&d.x_snap_all, NG) ||
-        !A(&d.x_rmx_all, NG + (NG + 1) / 2))
+        !A(&d.x_rmx_all, NG + (NG + 1) / 2) || !alloc_zero((void**)&d.x_cnt, G1 * 4) ||
+        !alloc_zero((void**)&d.x_off, 2 * G1 * 4) || !alloc_zero((void**)&d.x_cur, G1 * 4) ||
+        hipHostMalloc((void**)&d.h_x, 3 * G1 * 4, 0) != hipSuccess)
         return handle_fail(h, PSIM_ENOMEM, "demers exchange buffers for %zu slots", NG);
     return PSIM_OK;
 }
 
+// grow a record buffer to `words` u32 (contents not kept)
+int dms_grow(psim_handle* h, uint32_t** p, size_t* cap, size_t words) {
+    if (words <= *cap) return PSIM_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t w = std::max<size_t>(words + words / 4, 1024);
+    if (hipMalloc((void**)p, w * 4) != hipSuccess) {
+        *p = nullptr;
+        return handle_fail(h, PSIM_ENOMEM, "demers sparse exchange buffer of %zu words", w);
+    }
+    *cap = w;
+    return PSIM_OK;
+}
+
+// How the round's RM planes and call records travel: counts of this shard's
+// RM slots per destination and of its vertices that called select, summed
+// over the shards by the transport's host all-reduce (M[s G + g]: slots shard
+// s sends shard g; M[G G + s]: shard s's call records).  Records when the
+// round's traffic reaches fewer than n/8 slots (or always / never, xmode).
+int dms_plan(psim_handle* h, DmShard& d, std::vector<int64_t>& M, bool& sp_rm, bool& sp_x) {
+    const hipStream_t s = handle_stream(h);
+    const int G = (int)d.world, r = (int)d.rank;
+    sp_rm = sp_x = false;
+    M.assign(size_t(G) * G + G, 0);
+    if (d.xmode == 1) return PSIM_OK;
+    DMCHK(h, hipMemsetAsync(d.x_cnt, 0, (G + 1) * 4, s));
+    DMCHK(h, launch_dm_xcount(d.x_rm_shadow, d.world, d.rank, d.chunk, d.x_rmx_all + d.v_lo, d.n, d.x_cnt, s));
+    DMCHK(h, hipMemcpyAsync(d.h_x, d.x_cnt, (G + 1) * 4, hipMemcpyDeviceToHost, s));
+    DMCHK(h, hipStreamSynchronize(s));
+    for (int g = 0; g < G; g++) M[size_t(r) * G + g] = d.h_x[g];
+    M[size_t(G) * G + r] = d.h_x[G];
+    std::string err;
+    const int rc = handle_transport(h)->allreduce(M.data(), M.size(), s, &err);
+    if (rc) return handle_fail(h, rc, "demers exchange plan all-reduce: %s", err.c_str());
+    int64_t rm = 0, x = 0;
+    for (int i = 0; i < G * G; i++) rm += M[i];
+    for (int i = 0; i < G; i++) x += M[size_t(G) * G + i];
+    sp_rm = d.xmode == 2 || rm * 8 < int64_t(d.n_global);
+    sp_x = d.xmode == 2 || x * 8 < int64_t(d.n_global);
+    return PSIM_OK;
+}
+
+// RM slots as records: pack per destination, all-to-all-v, scatter into the
+// zeroed receive slices (the own slice is copied by the caller)
+int dms_sparse_rm(psim_handle* h, DmShard& d, const std::vector<int64_t>& M, std::string& err) {
+    const hipStream_t s = handle_stream(h);
+    const int G = (int)d.world, r = (int)d.rank;
+    const size_t C = d.chunk, NG = size_t(G) * C;
+    std::vector<uint64_t> so(G + 1, 0), ro(G + 1, 0);
+    uint32_t* hs = d.h_x + (G + 1);
+    uint32_t* hr = d.h_x + 2 * (G + 1);
+    for (int g = 0; g < G; g++) {
+        hs[g] = (uint32_t)(so[g] / 7);
+        hr[g] = (uint32_t)(ro[g] / 7);
+        so[g + 1] = so[g] + 7 * uint64_t(g == r ? 0 : M[size_t(r) * G + g]);
+        ro[g + 1] = ro[g] + 7 * uint64_t(g == r ? 0 : M[size_t(g) * G + r]);
+    }
+    hs[G] = (uint32_t)(so[G] / 7);
+    hr[G] = (uint32_t)(ro[G] / 7);
+    int rc = dms_grow(h, &d.x_sp_send, &d.x_cap_send, so[G]);
+    if (!rc) rc = dms_grow(h, &d.x_sp_recv, &d.x_cap_recv, ro[G]);
+    if (rc) return rc;
+    DMCHK(h, hipMemcpyAsync(d.x_off, hs, 2 * (G + 1) * 4, hipMemcpyHostToDevice, s));
+    DMCHK(h, hipMemsetAsync(d.x_cur, 0, (G + 1) * 4, s));
+    DMCHK(h, launch_dm_xpack_rm(d.x_rm_shadow, d.world, d.rank, d.chunk, d.x_off, d.x_cur, d.x_sp_send, s));
+    rc = handle_transport(h)->alltoallv(d.x_sp_send, so.data(), d.x_sp_recv, ro.data(), r, G, s, &err);
+    if (rc) return rc;
+    DMCHK(h, hipMemsetAsync(d.x_rm_recv, 0, 3 * NG * 8, s));
+    DMCHK(h, launch_dm_xunpack_rm(d.x_sp_recv, d.x_off + (G + 1), d.world, d.chunk, hr[G], d.x_rm_recv, s));
+    d.x_bytes += so[G] * 4;
+    d.x_sparse_rm++;
+    return PSIM_OK;
+}
+
+// RM call records as {vertex, rumors called, calls before} to every other
+// shard; their slices of the rumors-called plane are zeroed first (a call
+// count is only read where a rumor bit is set; the own slice is intact)
+int dms_sparse_rmx(psim_handle* h, DmShard& d, const std::vector<int64_t>& M, std::string& err) {
+    const hipStream_t s = handle_stream(h);
+    const int G = (int)d.world, r = (int)d.rank;
+    const size_t C = d.chunk, NG = size_t(G) * C;
+    const uint32_t per = (uint32_t)M[size_t(G) * G + r];
+    std::vector<uint64_t> so(G + 1, 0), ro(G + 1, 0);
+    for (int g = 0; g < G; g++) {
+        so[g + 1] = so[g] + (g == r ? 0 : 4 * uint64_t(per));
+        ro[g + 1] = ro[g] + (g == r ? 0 : 4 * uint64_t(M[size_t(G) * G + g]));
+    }
+    int rc = dms_grow(h, &d.x_sp_send, &d.x_cap_send, so[G]);
+    if (!rc) rc = dms_grow(h, &d.x_sp_recv, &d.x_cap_recv, ro[G]);
+    if (rc) return rc;
+    unsigned long long* rn = d.x_rmx_all;
+    uint32_t* nc = reinterpret_cast<uint32_t*>(d.x_rmx_all + NG);
+    DMCHK(h, hipMemsetAsync(d.x_cur + G, 0, 4, s));
+    DMCHK(h, launch_dm_xpack_rmx(rn, nc, d.v_lo, d.n, d.world, d.rank, per, d.x_cur + G, d.x_sp_send, s));
+    rc = handle_transport(h)->alltoallv(d.x_sp_send, so.data(), d.x_sp_recv, ro.data(), r, G, s, &err);
+    if (rc) return rc;
+    if (r > 0) DMCHK(h, hipMemsetAsync(rn, 0, size_t(r) * C * 8, s));
+    if (size_t(r + 1) * C < NG) DMCHK(h, hipMemsetAsync(rn + size_t(r + 1) * C, 0, (NG - size_t(r + 1) * C) * 8, s));
+    DMCHK(h, launch_dm_xunpack_rmx(d.x_sp_recv, (uint32_t)(ro[G] / 4), rn, nc, s));
+    d.x_bytes += so[G] * 4;
+    d.x_sparse_rmx++;
+    return PSIM_OK;
+}
+
 // The round's exchange (psim.h "vertex-sharded Demers"): all-to-all of the
-// three RM count planes in slices of C, the pull slots as an all-to-all whose
-// slices the receiver sums (one writer per slot), all-gathers of both RM call
-// record planes and, after an AE tick, of the snapshots -- RCCL on the
+// three RM count planes in slices of C (or their nonzero slots as records,
+// dms_plan), the pull slots as an all-to-all whose slices the receiver sums
+// (one writer per slot), all-gathers of both RM call record planes (or the
+// callers' records) and, after an AE tick, of the snapshots -- RCCL on the
 // handle's stream, or the caller's transport; the own slices are local copies.
+// Without rumor mongering the RM planes and call records stay zero and do not
+// travel.
 int dms_exchange(psim_handle* h, DmShard& d, bool tick) {
     const hipStream_t s = handle_stream(h);
     const size_t C = d.chunk, NG = size_t(d.world) * C;
@@ -270,32 +390,57 @@ int dms_exchange(psim_handle* h, DmShard& d, bool tick) {
         off1[g] = uint64_t(g) * 2 * C;     // C u64 per slice
         off2[g] = uint64_t(g) * 4 * C;     // 2C u64 per slice
     }
-    for (int k = 0; k < 3; k++) {
-        unsigned long long* snd = d.x_rm_shadow + k * NG;
-        unsigned long long* rcv = d.x_rm_recv + k * NG;
-        if (G > 1) {
-            const int rc = T->alltoallv(reinterpret_cast<uint32_t*>(snd), off1.data(), reinterpret_cast<uint32_t*>(rcv),
-                                        off1.data(), r, G, s, &err);
-            if (rc) return handle_fail(h, rc, "demers RM exchange: %s", err.c_str());
+    const uint64_t peers = uint64_t(G - 1);
+    std::vector<int64_t> M;
+    bool sp_rm = false, sp_x = false;
+    if (G > 1 && d.rm_on) {
+        const int rc = dms_plan(h, d, M, sp_rm, sp_x);
+        if (rc) return rc;
+    }
+    if (d.rm_on) {
+        if (G > 1 && sp_rm) {
+            const int rc = dms_sparse_rm(h, d, M, err);
+            if (rc) return handle_fail(h, rc, "demers RM records: %s", err.c_str());
         }
-        DMCHK(h, hipMemcpyAsync(rcv + r * C, snd + r * C, C * 8, hipMemcpyDeviceToDevice, s));
+        for (int k = 0; k < 3; k++) {
+            unsigned long long* snd = d.x_rm_shadow + k * NG;
+            unsigned long long* rcv = d.x_rm_recv + k * NG;
+            if (G > 1 && !sp_rm) {
+                const int rc = T->alltoallv(reinterpret_cast<uint32_t*>(snd), off1.data(),
+                                            reinterpret_cast<uint32_t*>(rcv), off1.data(), r, G, s, &err);
+                if (rc) return handle_fail(h, rc, "demers RM exchange: %s", err.c_str());
+                d.x_bytes += peers * C * 8;
+            }
+            DMCHK(h, hipMemcpyAsync(rcv + r * C, snd + r * C, C * 8, hipMemcpyDeviceToDevice, s));
+        }
     }
     if (G > 1) {
         const int rc = T->alltoallv(reinterpret_cast<uint32_t*>(d.x_pull_shadow), off2.data(),
                                     reinterpret_cast<uint32_t*>(d.x_pull_all), off2.data(), r, G, s, &err);
         if (rc) return handle_fail(h, rc, "demers pull exchange: %s", err.c_str());
+        d.x_bytes += peers * C * 16;
     }
     DMCHK(h, hipMemcpyAsync(d.x_pull_all + r * 2 * C, d.x_pull_shadow + r * 2 * C, 2 * C * 8, hipMemcpyDeviceToDevice, s));
     DMCHK(h, launch_dm_sum_slices(d.x_pull_all, d.world, 2 * C, d.x_pull_sum, s));
     if (G > 1) {
         uint32_t* rmx = reinterpret_cast<uint32_t*>(d.x_rmx_all);
-        int rc = T->allgather(rmx, 2 * C, r, G, s, &err);                        // rumors called (u64)
-        if (!rc) rc = T->allgather(rmx + 2 * NG, C, r, G, s, &err);               // calls before the round (u32)
-        if (!rc && tick) rc = T->allgather(reinterpret_cast<uint32_t*>(d.x_snap_all), 2 * C, r, G, s, &err);
+        int rc = 0;
+        if (d.rm_on && sp_x) {
+            rc = dms_sparse_rmx(h, d, M, err);
+        } else if (d.rm_on) {
+            rc = T->allgather(rmx, 2 * C, r, G, s, &err);                             // rumors called (u64)
+            if (!rc) rc = T->allgather(rmx + 2 * NG, C, r, G, s, &err);               // calls before the round (u32)
+            d.x_bytes += peers * C * 12;
+        }
+        if (!rc && tick) {
+            rc = T->allgather(reinterpret_cast<uint32_t*>(d.x_snap_all), 2 * C, r, G, s, &err);
+            d.x_bytes += peers * C * 8;
+        }
         if (rc) return handle_fail(h, rc, "demers all-gather: %s", err.c_str());
     }
     DMCHK(h, hipMemsetAsync(d.x_rm_shadow, 0, 3 * NG * 8, s));
     DMCHK(h, hipMemsetAsync(d.x_pull_shadow, 0, 2 * NG * 8, s));
+    d.x_rounds++;
     return PSIM_OK;
 }
 
@@ -572,6 +717,26 @@ int psim_demers_shard_run(psim_handle* h, uint32_t max_rounds, psim_demers_stats
         if (st.complete == d->n_global) break;      // every vertex holds every rumor (global count)
     }
     if (rounds_run) *rounds_run = ran;
+    return PSIM_OK;
+}
+
+int psim_demers_shard_set_exchange(psim_handle* h, int mode) {
+    if (!h || mode < 0 || mode > 2) return PSIM_EINVAL;
+    DmShard* d = dms_of(h);
+    if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    d->xmode = mode;
+    return PSIM_OK;
+}
+
+int psim_demers_shard_exchange_stats(const psim_handle* h, uint64_t* bytes_sent, uint32_t* rounds,
+                                     uint32_t* sparse_rm_rounds, uint32_t* sparse_call_rounds) {
+    if (!h) return PSIM_EINVAL;
+    const DmShard* d = dms_of(h);
+    if (!d) return PSIM_ESTATE;
+    if (bytes_sent) *bytes_sent = d->x_bytes;
+    if (rounds) *rounds = d->x_rounds;
+    if (sparse_rm_rounds) *sparse_rm_rounds = d->x_sparse_rm;
+    if (sparse_call_rounds) *sparse_call_rounds = d->x_sparse_rmx;
     return PSIM_OK;
 }
 

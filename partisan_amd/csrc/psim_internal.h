@@ -261,6 +261,17 @@ hipError_t launch_dm_round(const DmArgs& a, hipStream_t s);
 hipError_t launch_dm_sum_slices(const unsigned long long* in, uint32_t world, size_t len, unsigned long long* out,
                                 hipStream_t s);
 hipError_t launch_dm_pushscan(const DmArgs& a, uint32_t tick_idx, hipStream_t s);
+hipError_t launch_dm_xcount(const unsigned long long* any, uint32_t world, uint32_t rank, uint32_t chunk,
+                            const unsigned long long* rn_own, uint32_t n_own, uint32_t* cnt, hipStream_t s);
+hipError_t launch_dm_xpack_rm(const unsigned long long* rm, uint32_t world, uint32_t rank, uint32_t chunk,
+                              const uint32_t* off, uint32_t* cursor, uint32_t* rec, hipStream_t s);
+hipError_t launch_dm_xunpack_rm(const uint32_t* rec, const uint32_t* off, uint32_t world, uint32_t chunk,
+                                uint32_t nrec, unsigned long long* rm, hipStream_t s);
+hipError_t launch_dm_xpack_rmx(const unsigned long long* rn, const uint32_t* ncall, uint32_t v_lo, uint32_t n_own,
+                               uint32_t world, uint32_t rank, uint32_t per, uint32_t* cursor, uint32_t* rec,
+                               hipStream_t s);
+hipError_t launch_dm_xunpack_rmx(const uint32_t* rec, uint32_t nrec, unsigned long long* rn, uint32_t* ncall,
+                                 hipStream_t s);
 
 // HyParView (hyparview.hip)
 constexpr uint32_t kHvX = 8;          // exchange list capacity (1 + k_active + k_passive)

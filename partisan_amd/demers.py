@@ -112,6 +112,20 @@ class ShardedDemers:
     def _p(t):
         return C.c_void_p(t.data_ptr())
 
+    def set_exchange(self, mode):
+        """In-library exchange form of the RM planes and call records: "auto"
+        (records below n/8 slots), "dense" or "records" (psim.h
+        psim_demers_shard_set_exchange); every shard must pass the same."""
+        check(lib().psim_demers_shard_set_exchange(self._h, {"auto": 0, "dense": 1, "records": 2}[mode]), self._h)
+
+    def exchange_stats(self):
+        """(bytes this shard sent to other shards, exchanges, exchanges that
+        sent RM records, exchanges that sent call records)."""
+        b, n, s1, s2 = C.c_uint64(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().psim_demers_shard_exchange_stats(self._h, C.byref(b), C.byref(n), C.byref(s1), C.byref(s2)),
+              self._h)
+        return b.value, n.value, s1.value, s2.value
+
     # -------------------------------------------------------------- exchange
     def _exchange(self, tick):
         dist, torch = self._dist(), self.torch

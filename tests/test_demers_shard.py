@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = ("rm_sent", "push_sent", "pull_sent", "delivered_new", "complete")
 
 
-def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, q):
+def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, *rest):
+    q, xmode = rest[-1], (rest[0] if len(rest) > 1 else "auto")      # run_world appends the queue
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -41,6 +42,8 @@ def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, q):
         seed = 0x5EED0004
         sd = ShardedDemers(n, m, rank, world, device=0, backend=backend, ae_period=ae, rumor_mongering=rm, seed=seed,
                            transport=transport)
+        if transport != "torch":
+            sd.set_exchange(xmode)
         orc = O.Demers(n, m, seed, ae_period=ae, rm_on=rm)
         lo, hi = sd.v_lo, sd.v_lo + sd.n_local
         sd.broadcast()
@@ -54,6 +57,15 @@ def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, q):
             assert np.array_equal(sd.seen(), orc.seen()[lo:hi]), r
             if o["complete"] == n:
                 break
+        if transport != "torch" and world > 1:
+            nbytes, ex, sp_rm, sp_calls = sd.exchange_stats()
+            assert ex == r + 2 and nbytes > 0, (ex, r, nbytes)      # the broadcast's exchange + one per round
+            if xmode == "records":
+                assert sp_rm == ex and sp_calls == ex, (ex, sp_rm, sp_calls)
+            elif xmode == "dense" or not rm:
+                assert sp_rm == 0 and sp_calls == 0, (sp_rm, sp_calls)
+            else:     # auto: the first and last rounds reach few slots, the middle ones most
+                assert 0 < sp_rm < ex and 0 < sp_calls < ex, (ex, sp_rm, sp_calls)
         sd.close()
         dist.destroy_process_group()
         q.put((rank, "ok"))
@@ -71,6 +83,16 @@ def _gpu_worker(rank, world, port, n, m, ae, rm, backend, transport, q):
                                                         (3, 2000, 17, 3, False, "torch")])
 def test_sharded_demers_matches_oracle(world, n, m, ae, rm, transport):
     res = run_world(_gpu_worker, world, n, m, ae, rm, "gloo", transport)
+    for r in range(world):
+        assert res[r] == "ok", res[r]
+
+
+# the same rounds with the RM planes and call records always as records, and
+# always dense: both equal the oracle (auto, above, mixes the two)
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,xmode", [(2, "records"), (3, "records"), (2, "dense")])
+def test_sharded_demers_exchange_forms(world, xmode):
+    res = run_world(_gpu_worker, world, 3000, 64, 2, True, "gloo", "callback", xmode)
     for r in range(world):
         assert res[r] == "ok", res[r]
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
 # Round-4 session D: batched candidate loads (PT_BATCH=2, default build) vs
 # PT_BATCH=1 (exp_b1.so) vs the committed head (exp_head.so); the 3-pass
-# transport micro-benchmark; session C's tests.
+# transport micro-benchmark; the rewritten causal round kernel (lockstep
+# parity, then C5 against the committed head's kernel).
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -15,8 +16,8 @@ for rep in 1 2; do
 done
 step rp_b2 300 python tools/round_profile.py --steps 2
 PSIM_LIB_PATH=$PWD/partisan_amd/exp_head.so step rp_head 300 python tools/round_profile.py --steps 2
-step mbb2 180 tools/mb_binned
-step t_c 1200 python -u -m pytest -v --timeout 900 --timeout-method thread -m gpu \
-    tests/test_causal_shard.py tests/test_nif_harness.py tests/test_shard.py::test_sharded_set_delays_busy_on_every_rank \
-    tests/test_c3.py::test_gpu_c3_many_grafts_per_vertex_round tests/test_configs_at_scale.py::test_bench_config_10m_oracle_parity
+step t_causal 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_causal.py
+step c5_new 200 python tools/config_bench.py C5
+PSIM_LIB_PATH=$PWD/partisan_amd/exp_head.so step c5_head 200 python tools/config_bench.py C5
+step mbb2 120 tools/mb_binned
 echo done
