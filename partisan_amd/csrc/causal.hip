@@ -336,7 +336,20 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         __builtin_amdgcn_wave_barrier();
         // arrivals of round t: lane k marks bit d if k's round-(t-d) message lands now
         uint32_t am = 0;
-        if (lane < a.m && eid != w.v) {
+        if (a.dring) {
+            // the delay of k's round-(t-1) message is drawn now and kept in
+            // its 4-bit slot (r % 8) until it lands: one draw per message
+            uint32_t* rp = a.dring + (size_t)lv * kCsLanes + lane;
+            uint32_t ring = *rp;
+            if (lane < a.m && eid != w.v && a.t >= 2u) {
+                const uint32_t r = a.t - 1u, sh = 4u * (r % 8u);
+                const uint32_t dv = r % a.period == lane % a.period ? delay_of(a.key, w.v, r, lane, a.dmax) : 0u;
+                ring = (ring & ~(0xFu << sh)) | (dv << sh);
+                for (uint32_t d = 1; d <= a.dmax && d < a.t; d++)
+                    if (((ring >> (4u * ((a.t - d) % 8u))) & 0xFu) == d) am |= 1u << d;
+                *rp = ring;
+            }
+        } else if (lane < a.m && eid != w.v) {
             const uint32_t ph = lane % a.period;
             for (uint32_t d = 1; d <= a.dmax && d < a.t; d++) {
                 const uint32_t r = a.t - d;

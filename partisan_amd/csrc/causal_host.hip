@@ -22,12 +22,12 @@ namespace {
 struct CsState : ModuleState {
     uint32_t n = 0, m = 0, period = 1, dmax = 1, redeliver = 1;
     uint32_t n_global = 0, v_lo = 0, rank = 0, world = 1;   // vertex shard [v_lo, v_lo + n) of n_global
-    uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr;
+    uint32_t *clk = nullptr, *self = nullptr, *buf = nullptr, *nbuf = nullptr, *base = nullptr, *dring = nullptr;
     unsigned long long *delivered = nullptr, *stats = nullptr, *h_stats = nullptr;
     uint32_t* x_slab = nullptr;        // the in-library exchange's slab (psim_causal_shard_step)
     uint64_t round = 0;
     ~CsState() override {
-        void* ptrs[] = {clk, self, buf, nbuf, base, delivered, stats, x_slab};
+        void* ptrs[] = {clk, self, buf, nbuf, base, delivered, stats, x_slab, dring};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (h_stats) (void)hipHostFree(h_stats);
@@ -74,6 +74,7 @@ CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
     a.delivered = c.delivered;
     a.base = c.base;
     a.stats = c.stats;
+    a.dring = c.dring;
     return a;
 }
 
@@ -103,7 +104,14 @@ int psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t per
                     A((void**)&c.base, size_t(kCsWindow) * kCsLanes * kCsLanes * 4) &&
                     A((void**)&c.delivered, N * 8) && A((void**)&c.stats, kStatShards * kCsNStat * 8) &&
                     hipHostMalloc((void**)&c.h_stats, kStatShards * kCsNStat * 8, 0) == hipSuccess;
-    if (!ok) {
+#ifndef CS_NO_DELAY_RING
+    // each message's delay drawn once, in the round after its broadcast, and
+    // kept until it lands, instead of redrawn in each round of its window
+    const bool ring_ok = !ok || dmax > kCsRingMax || A((void**)&c.dring, N * kCsLanes * 4);
+#else
+    const bool ring_ok = true;
+#endif
+    if (!ok || !ring_ok) {
         cs_reset(h);
         return handle_fail(h, PSIM_ENOMEM, "causal state for n=%u", n);
     }

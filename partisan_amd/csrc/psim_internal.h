@@ -342,7 +342,10 @@ struct CsArgs {
     unsigned long long* __restrict__ delivered;   // [n]
     uint32_t* __restrict__ base;          // [kCsWindow][64][64] emitter clocks at their broadcasts
     unsigned long long* __restrict__ stats;
+    uint32_t* __restrict__ dring;         // [n][64] or null: lane k = the delays of k's messages of the
+                                          // last 8 rounds, 4 bits at r % 8 (dmax <= kCsRingMax)
 };
+constexpr uint32_t kCsRingMax = 8;
 hipError_t launch_cs_round(const CsArgs& a, hipStream_t s);
 hipError_t launch_cs_broadcast(const CsArgs& a, hipStream_t s);
 

@@ -18,6 +18,7 @@ step rp_b2 300 python tools/round_profile.py --steps 2
 PSIM_LIB_PATH=$PWD/partisan_amd/exp_head.so step rp_head 300 python tools/round_profile.py --steps 2
 step t_causal 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_causal.py
 step c5_new 200 python tools/config_bench.py C5
+PSIM_LIB_PATH=$PWD/partisan_amd/exp_cs_noring.so step c5_noring 200 python tools/config_bench.py C5
 PSIM_LIB_PATH=$PWD/partisan_amd/exp_head.so step c5_head 200 python tools/config_bench.py C5
 step mbb2 120 tools/mb_binned
 echo done
