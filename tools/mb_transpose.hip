@@ -62,6 +62,16 @@ __global__ __launch_bounds__(256) void k_direct(const uint32_t* __restrict__ wor
     }
 }
 
+// destination-range split: one pass of P writes only the
+// words whose receiver slot lies in [lo, lo + span)
+__global__ __launch_bounds__(256) void k_range(const uint32_t* __restrict__ word, const uint32_t* __restrict__ tgt,
+                                               uint32_t E, uint32_t lo, uint32_t span, uint32_t* __restrict__ inbox) {
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+        const uint32_t w = word[e], t = tgt[e];
+        if (w && t - lo < span) inbox[t] = w;
+    }
+}
+
 // pass 1, dense: image position of slot e = segbase[c][b(e)] + rank8[e]
 __global__ __launch_bounds__(256) void k_p1_dense(const uint32_t* __restrict__ word, const uint32_t* __restrict__ tgt,
                                                   const uint8_t* __restrict__ rank8, const uint16_t* __restrict__ segbase,
@@ -242,6 +252,18 @@ int main(int argc, char** argv) {
     printf("direct scatter                %7.1f us  (%.1f G words/s)\n", td, M / td / 1e3);
     std::vector<uint32_t> ref(E, 0);
     for (uint32_t e = 0; e < E; e++) if (word[e]) ref[tgt[e]] = word[e];
+    for (uint32_t P : {2u, 4u, 8u}) {
+        const uint32_t span = (E + P - 1) / P;
+        CK(hipMemset(d_inbox, 0, E * 4ull));
+        const float tp = timeit([&] {
+            for (uint32_t p = 0; p < P; p++)
+                hipLaunchKernelGGL(k_range, dim3(cus * 8), dim3(256), 0, 0, d_word, d_tgt, E, p * span, span, d_inbox);
+        });
+        std::vector<uint32_t> got(E);
+        CK(hipMemcpy(got.data(), d_inbox, E * 4ull, hipMemcpyDeviceToHost));
+        printf("range split P=%u (%.0f MB windows)  %7.1f us  (%.1f G words/s)  %s\n", P, span * 4.0 / 1e6, tp,
+               M / tp / 1e3, got == ref ? "ok" : "MISMATCH");
+    }
     for (uint32_t bshift : {22u, 21u, 20u, 19u}) {
         const uint32_t B = (E + (1u << bshift) - 1) >> bshift;
         if (B > kMaxB || B > 256) continue;      // bof is u8
