@@ -9,9 +9,9 @@ step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" >
 step t_dm 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_demers_shard.py
 step t_cs 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_causal_shard.py tests/test_nif_harness.py
 step c4 200 python tools/config_bench.py C4
+step mbt 240 tools/mb_transpose
 step pmc_c5 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     --kernel-include-regex cs_round -d gpurun_out/pmc_c5 -o run --output-format csv -- python3 tools/c5_probe.py
 step pmc_c4 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
     --kernel-include-regex dm_round -d gpurun_out/pmc_c4 -o run --output-format csv -- python3 tools/config_bench.py C4
-step mbt 240 tools/mb_transpose
 echo done
