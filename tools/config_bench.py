@@ -64,10 +64,17 @@ def c4(n=10_000_000, m=64):
     ms = sum(s["kernel_ms"] for s in st)
     b = sum(s["algo_bytes"] for s in st)
     gbs = b / 1e6 / ms
+    # the round is a stream of random 8-byte accesses: an RM send is one
+    # atomicOr (its cascade rarely goes further), an AE push an atomicAdd on
+    # the target's count plus the list store, a pull reply a snapshot load plus
+    # the reply store -- priced against the chip's random 4-byte scatter rate
+    # into a 200 MB target (54.24 G ops/s, profiles/r01/microbench2.txt:3)
+    rnd = sum(s["rm_sent"] + 2 * s["push_sent"] + 2 * s["pull_sent"] for s in st)
     line("C4", n=n, rumors=m, rounds=r, complete=int(st[-1]["complete"]), kernel_ms=round(ms, 3),
          ms_per_round=round(ms / r, 4), wall_s=round(wall, 3), peer_rounds_per_s=n * r / (ms / 1e3),
          algo_GBps=round(gbs, 1), hbm_frac=round(gbs / HBM, 4),
-         messages=int(sum(s["rm_sent"] + s["push_sent"] + s["pull_sent"] for s in st)))
+         messages=int(sum(s["rm_sent"] + s["push_sent"] + s["pull_sent"] for s in st)),
+         random_ops=int(rnd), random_Gops=round(rnd / ms / 1e6, 2), random_frac=round(rnd / ms / 1e6 / 54.24, 3))
     sim.close()
 
 
