@@ -218,9 +218,10 @@ int  psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst
  * (ingress) delay of a node is its out- (in-) edges.  PSIM_EBUSY while any
  * message is in flight (a change could reorder a pair); PSIM_ESTATE for the
  * binned engine.  Sharded handles: collective (every rank passes the same
- * global pairs and installs its own senders'), one heartbeat root at a time,
- * driven by psim_shard_run / psim_shard_step (PSIM_ESTATE with several lanes
- * or async rounds pending).  Pairs that are not overlay edges are ignored.
+ * global pairs and installs its own senders'), driven by psim_shard_run /
+ * psim_shard_step, several heartbeat roots at once (each lane stages its
+ * cross-shard delayed words in its own ring); PSIM_ESTATE with a window lane
+ * or async rounds pending.  Pairs that are not overlay edges are ignored.
  * psim_run / psim_shard_run end only when no delayed message is pending. */
 #define PSIM_MAX_DELAY 14u
 int  psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k);

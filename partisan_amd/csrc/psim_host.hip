@@ -147,6 +147,7 @@ struct psim_handle {
         int* ost_total = nullptr;
         uint32_t* ring = nullptr;
         uint8_t* pring = nullptr;
+        uint32_t* srg = nullptr;          // sharded + delays: the lane's staging ring (Sh::srg while focused)
         uint64_t due[kRing] = {};
         Win* win = nullptr;
         // sharded handles: the lane's GLOBAL state after the last collective
@@ -252,7 +253,7 @@ void free_graph(psim_handle* h) {
         swap_lane(h, 0);
         for (size_t j = 1; j < h->lanes.size(); j++) {
             auto& l = h->lanes[j];
-            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost, l.ring, l.pring};
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost, l.ring, l.pring, l.srg};
             for (void* p : lp)
                 if (p) (void)hipFree(p);
             delete l.win;
@@ -587,7 +588,7 @@ void save_lane(psim_handle* h) {
     l.ost = h->ost; l.ost_total = h->ost_total; l.par = h->par; l.serial = h->serial; l.root = h->root;
     l.have_root = h->have_root; l.ost_cnt = h->ost_cnt; l.live_rows = h->live_rows; l.inflight = h->inflight;
     l.scrub = h->scrub;
-    l.ring = h->ring; l.pring = h->pring;
+    l.ring = h->ring; l.pring = h->pring; l.srg = h->sh.srg;
     memcpy(l.due, h->due, sizeof l.due);
     l.win = h->win;
 }
@@ -597,7 +598,7 @@ void load_lane(psim_handle* h, int j) {
     h->ost = l.ost; h->ost_total = l.ost_total; h->par = l.par; h->serial = l.serial; h->root = l.root;
     h->have_root = l.have_root; h->ost_cnt = l.ost_cnt; h->live_rows = l.live_rows; h->inflight = l.inflight;
     h->scrub = l.scrub;
-    h->ring = l.ring; h->pring = l.pring;
+    h->ring = l.ring; h->pring = l.pring; h->sh.srg = l.srg;
     memcpy(h->due, l.due, sizeof h->due);
     h->win = l.win;
     h->cur_lane = j;
@@ -723,8 +724,9 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
                 if (p) (void)hipFree(p);
             return fail(h, PSIM_ENOMEM, "heartbeat lane %zu for n=%u", L.size(), h->n);
         }
-        if (h->dly && alloc_ring(h, l.ring, l.pring) != PSIM_OK) {
-            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost};
+        if (h->dly && (alloc_ring(h, l.ring, l.pring) != PSIM_OK ||
+                       (h->sh.world > 1 && !alloc_zero((void**)&l.srg, size_t(kRing) * h->Ed * 4)))) {
+            void* lp[] = {l.vs, l.in[0], l.in[1], l.pend[0], l.pend[1], l.ost, l.ring, l.pring};
             for (void* p : lp)
                 if (p) (void)hipFree(p);
             return fail(h, PSIM_ENOMEM, "delay ring of heartbeat lane %zu", L.size());
@@ -2137,7 +2139,10 @@ int lane_globals(psim_handle* h) {
 
 // Rounds of a sharded handle with several lanes or a window lane: each round
 // runs every lane with a root (round kernel, then its exchange), one
-// all-reduce of every lane's counters per round.
+// all-reduce of every lane's counters per round.  Delay faults: each static
+// lane stages its cross-shard delayed words in its own ring (Lane::srg), the
+// exchange after round R carries that ring's slot R, and a lane's in-flight
+// count is what its delay histogram still has pending (summed over shards).
 int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
                       uint32_t* ran_out, psim_exchange_stats* xs) {
     if (h) h->sh.plan_ok = false;       // outside shard_drive_fast's record bound
@@ -2149,7 +2154,8 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
         ~Refocus() { load_lane(h, f); }
     } refocus{h, focus};
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
-    constexpr int NK = 10;    // 5 kinds, delivered_new, senders, degree sum, live rows, row holders
+    constexpr int NK = 11;    // 5 kinds, delivered_new, senders, degree sum, live rows, row holders,
+                              // messages still pending (delay faults)
     uint32_t ran = 0;
     auto quiet = [&]() {
         for (const auto& l : h->lanes)
@@ -2184,7 +2190,10 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
                     HIPCHK(h, launch_pt_pack_dense(a, h->sh.rem, (uint32_t)h->sh.send_base[h->sh.world], h->sh.xsend,
                                                    h->stream));
                 h->par ^= 1u;
+                // delays: the ingest files the words into the ring by the round just run
+                if (h->dly) h->round++;
                 rc = x_exchange(h, 0, xs);
+                if (h->dly) h->round--;
             }
             if (rc) return rc;
             save_lane(h);
@@ -2211,7 +2220,13 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
             for (int t = 1; t <= 5; t++) lm += r[t];
             l.ost_cnt += (int64_t)r[S_OST_DELTA];
             l.live_rows += (int64_t)r[S_LIVE_DELTA];
-            if (!l.win) l.inflight = lm;
+            if (h->dly && !l.win) {      // round R consumed its arrivals; its sends are pending until R + 1 + d
+                const uint64_t R = h->round;
+                l.due[R & (kRing - 1)] = 0;
+                l.inflight = add_due(l.due, R, h->h_stats + q * kStatsRow + size_t(kStatShards) * kNStat);
+            } else if (!l.win) {
+                l.inflight = lm;
+            }
             int64_t* f = flat.data() + q * NK;
             for (int t = 1; t <= 5; t++) f[t - 1] = (int64_t)r[t];
             f[5] = (int64_t)r[S_DELIV];
@@ -2219,6 +2234,7 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
             f[7] = (int64_t)r[S_DEGSUM];
             f[8] = l.live_rows;
             f[9] = l.ost_cnt;
+            f[10] = h->dly ? (int64_t)l.inflight : 0;
             for (int t = 0; t < kNStat; t++) loc[t] += r[t];
         }
         if (h->sh.world > 1) {
@@ -2230,10 +2246,10 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
         for (size_t q = 0; q < A; q++) {
             auto& l = h->lanes[act[q]];
             const int64_t* f = flat.data() + q * NK;
-            l.g_inflight = f[0] + f[1] + f[2] + f[3] + f[4];
+            l.g_inflight = h->dly ? f[10] : f[0] + f[1] + f[2] + f[3] + f[4];   // delays: what is still on the wire
             l.g_live = f[8];
             l.g_ost = f[9];
-            for (int t = 0; t < NK; t++) tot[t] += f[t];
+            for (int t = 0; t < NK - 1; t++) tot[t] += f[t];
         }
         if (out && ran < cap) {
             psim_round_stats& o = out[ran];
@@ -2272,8 +2288,6 @@ int shard_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size
     if (rc) return rc;
     if (xs) memset(xs, 0, sizeof *xs);
     if (h->lanes.size() > 1 || h->win) {
-        if (h->dly && h->sh.world > 1)
-            return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: one heartbeat root at a time");
         if (!h->sh.pending) HIPCHK(h, seed_hold_rings(h, h->round + 1));
         return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
     }
@@ -2808,8 +2822,8 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
 int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
     if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
     if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "delay faults need the slot-scatter engine (not the binned one)");
-    if (h->sh.world > 1 && (h->lanes.size() > 1 || h->win || h->sh.pending))
-        return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: one heartbeat lane, no async rounds pending");
+    if (h->sh.world > 1 && (h->win || h->sh.pending))
+        return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: no window lane, no async rounds pending");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
@@ -2847,21 +2861,21 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     if (!h->dly) {
         // switch every lane to the ring; nothing is in flight, so no word moves
         if (hipMalloc((void**)&h->dly, h->Ed) != hipSuccess) return fail(h, PSIM_ENOMEM, "delay table");
-        if (h->sh.world > 1) {
-            if (!alloc_zero((void**)&h->sh.srg, size_t(kRing) * h->Ed * 4))
-                return fail(h, PSIM_ENOMEM, "staging ring of the delay faults");
-            h->sh.plan_ok = false;
-        }
+        // (sharded: each lane also stages its cross-shard delayed words in a ring of its own)
+        if (h->sh.world > 1) h->sh.plan_ok = false;
         const int focus = h->cur_lane;
         for (int j = 0; j < (int)h->lanes.size(); j++) {
             auto& l = h->lanes[j];
-            if (alloc_ring(h, l.ring, l.pring) != PSIM_OK) {
+            if (alloc_ring(h, l.ring, l.pring) != PSIM_OK ||
+                (h->sh.world > 1 && !alloc_zero((void**)&l.srg, size_t(kRing) * h->Ed * 4))) {
                 load_lane(h, focus);
                 return fail(h, PSIM_ENOMEM, "delay ring of heartbeat lane %d", j);
             }
             for (auto& x : l.due) x = 0;
         }
-        load_lane(h, focus);
+        if (h->lanes.empty() && h->sh.world > 1 && !alloc_zero((void**)&h->sh.srg, size_t(kRing) * h->Ed * 4))
+            return fail(h, PSIM_ENOMEM, "staging ring of the delay faults");
+        if (!h->lanes.empty()) load_lane(h, focus);
     }
     HIPCHK(h, hipMemcpy(h->dly, dl.data(), h->Ed, hipMemcpyHostToDevice));
     return PSIM_OK;
