@@ -450,31 +450,22 @@ constexpr bool kNtState = true;
 constexpr bool kNtState = false;
 #endif
 
-// kPk (ELL packed rows): the reverse slots are kept as 3-bit positions in one
-// register and derived on use (rev = col * W + position) -- a thread holding
-// the loads of several vertices at once needs the registers
-template <uint32_t kCap, bool kPk = false>
+template <uint32_t kCap>
 struct VLoad {
     uint4 st;
     uint32_t aw;
-    uint32_t cl[kCap];
-    uint32_t rvv[kPk ? 1 : kCap];
-    uint32_t pos;
+    uint32_t cl[kCap], rv[kCap];
     bool rows;   // cl / rv were loaded
     bool has_mb; // mb = memb[v] was loaded with the rest
     uint32_t mb;
-    __device__ __forceinline__ uint32_t rv(uint32_t s, uint32_t W) const {
-        if constexpr (kPk) return cl[s] * W + ((pos >> (3u * s)) & 7u);
-        else return rvv[s];
-    }
 };
 
 // `rows` false: the vertex's words hold only prunes and no row is due, so it
 // sends nothing and never tests a peer's liveness -- its peer ids and
 // reverse slots (2 x 4 B per slot, most of a sparse round's row bytes) are
 // not loaded.
-template <uint32_t kCap, bool kNtSt = kNtState, bool kPk = false>
-__device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, VLoad<kCap, kPk>& L,
+template <uint32_t kCap, bool kNtSt = kNtState>
+__device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, VLoad<kCap>& L,
                                       bool rows = true) {
     L.aw = a.alive[(a.v_lo + v) >> 5];
 #ifndef PT_MEMB_LAZY
@@ -493,31 +484,20 @@ __device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, 
         L.st = a.vs[v];
     }
     L.rows = rows;
-    if constexpr (kPk) {         // ELL packed rows (a.ecol), positions kept packed
-        L.pos = 0;
-#pragma unroll
-        for (uint32_t s = 0; s < kCap; s++) {
-            const uint32_t p = (rows && s < deg) ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
-            L.cl[s] = p == kNoPeer ? kNoPeer : p >> 3;
-            L.pos |= (p == kNoPeer ? 0u : (p & 7u)) << (3u * s);
-        }
-        return;
-    } else {
     if (a.ecol) {                // ELL packed rows: half the row bytes
         const uint32_t W = a.ell;
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) {
             const uint32_t p = (rows && s < deg) ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
             L.cl[s] = p == kNoPeer ? kNoPeer : p >> 3;
-            L.rvv[s] = p == kNoPeer ? 0u : (p >> 3) * W + (p & 7u);
+            L.rv[s] = p == kNoPeer ? 0u : (p >> 3) * W + (p & 7u);
         }
         return;
     }
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         L.cl[s] = (rows && s < deg) ? a.col[rs + s] : 0u;
-        L.rvv[s] = (rows && s < deg) ? a.rev[rs + s] : 0u;
-    }
+        L.rv[s] = (rows && s < deg) ? a.rev[rs + s] : 0u;
     }
 }
 
@@ -579,12 +559,13 @@ struct GroupSink {
 };
 
 // Returns the change in "holds outstanding rows" (vst_store).
-template <bool kFault, uint32_t kCap, class Sink, class VL>
+template <bool kFault, uint32_t kCap, class Sink>
 __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
-                                              const uint32_t (&w)[kCap], const VL& L, Ctr& c, Sink& sink) {
+                                              const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, Sink& sink) {
     const uint32_t aw = L.aw;
     const uint4 st = L.st;
     const uint32_t(&cl)[kCap] = L.cl;
+    const uint32_t(&rv)[kCap] = L.rv;
     if (!((aw >> ((a.v_lo + v) & 31)) & 1u)) return 0;   // a dead vertex receives nothing
     c.active++;
     VSt x;
@@ -628,12 +609,12 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         if (!wo[s]) continue;
         const uint32_t u = cl[s] - a.v_lo;
         if (kFault && a.dly && u < a.n) {
-            put_delayed(a, rs + s, L.rv(s, a.ell) - a.slot_base, u, wo[s], delay_hist());
+            put_delayed(a, rs + s, rv[s] - a.slot_base, u, wo[s], delay_hist());
         } else if (u < a.n) {
 #ifdef PT_NT_STORE
-            __builtin_nontemporal_store(wo[s], &a.in_nxt[L.rv(s, a.ell) - a.slot_base]);
+            __builtin_nontemporal_store(wo[s], &a.in_nxt[rv[s] - a.slot_base]);
 #else
-            a.in_nxt[L.rv(s, a.ell) - a.slot_base] = wo[s];
+            a.in_nxt[rv[s] - a.slot_base] = wo[s];
 #endif
 #ifndef PT_CLAIMS_FIRST
             sink.word(s, u);
@@ -661,9 +642,9 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     return vst_store(a, v, st, x, c);
 }
 
-template <bool kFault, uint32_t kCap, class VL>
+template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
-                                               const uint32_t (&w)[kCap], const VL& L, Ctr& c, uint32_t mark,
+                                               const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, uint32_t mark,
                                                WlLds* wl) {
     GroupSink<kCap> sink{a, mark, wl};
     (void)pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, sink);
@@ -695,38 +676,6 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
 #endif
     vload(a, v, rs, deg, L, rows);
     pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, mark, wl);
-}
-
-// pt_vertex_fast (kLdsWords) in two steps, so that a thread can issue the
-// loads of several vertices before it stores anything: ell_issue reads the
-// vertex's words from LDS and issues its global loads (false: nothing to do);
-// ell_finish runs the handlers and the stores.
-template <uint32_t kCap>
-__device__ __forceinline__ bool ell_issue(const PtArgs& a, uint32_t v, uint32_t deg, bool pend, bool due,
-                                          const uint32_t* lw, VLoad<kCap, true>& L) {
-    uint32_t any = 0;
-    bool rows = due;
-#pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) {
-        const uint32_t w = (pend && s < deg) ? lw[s] : 0u;
-        any |= w;
-        rows |= word_non_prune(w);
-    }
-    if (!any && !due) return false;
-#ifdef PT_ROWS_ALWAYS
-    rows = true;
-#endif
-    vload<kCap, kNtState, true>(a, v, v * deg, deg, L, rows);
-    return true;
-}
-
-template <bool kFault, uint32_t kCap>
-__device__ __forceinline__ void ell_finish(const PtArgs& a, uint32_t v, uint32_t deg, bool pend, const uint32_t* lw,
-                                           const VLoad<kCap, true>& L, Ctr& c, uint32_t mark, WlLds* wl) {
-    uint32_t w[kCap];
-#pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) w[s] = (pend && s < deg) ? lw[s] : 0u;
-    pt_vertex_core<kFault, kCap>(a, v, v * deg, deg, w, L, c, mark, wl);
 }
 
 template <bool kFault>
@@ -1119,43 +1068,10 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         }
         __syncthreads();
         const uint32_t nc = ncand;
-#ifndef PT_BATCH
-#define PT_BATCH 2
-#endif
-        // kBatch candidates of a thread at once: every load of the batch is
-        // issued, and waited for, before any of the batch's stores.  vmcnt
-        // counts loads and stores together in issue order, so a vertex whose
-        // loads were issued after the previous vertex's word stores waited for
-        // those stores to complete as well as for its own loads.
-        constexpr uint32_t kBatch = PT_BATCH;
-        if (!a.ecol) {                                 // unpacked ELL rows (n >= 2^29 - 1): one at a time
-            for (uint32_t i = t; i < nc; i += kBlock) {
-                const uint32_t x = cand[i], lv = x >> 2;
-                const uint32_t v = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
-                pt_vertex_fast<kFault, true, kCap>(a, v, v * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W], md.mark,
-                                                   &wl);
-            }
-        } else
-        for (uint32_t i0 = t; i0 < nc; i0 += kBatch * kBlock) {
-            VLoad<kCap, true> L[kBatch];
-            uint32_t vb[kBatch], lb[kBatch];
-            bool go[kBatch], pb[kBatch], db[kBatch];
-#pragma unroll
-            for (uint32_t b = 0; b < kBatch; b++) {
-                const uint32_t i = i0 + b * kBlock;
-                go[b] = false;
-                if (i >= nc) continue;
-                const uint32_t x = cand[i], lv = x >> 2;
-                vb[b] = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
-                lb[b] = lv;
-                pb[b] = (x >> 1) & 1u;
-                db[b] = x & 1u;
-                go[b] = ell_issue<kCap>(a, vb[b], W, pb[b], db[b], &wbuf[lv * W], L[b]);
-            }
-            if (kBatch > 1) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the batch's loads, before its stores
-#pragma unroll
-            for (uint32_t b = 0; b < kBatch; b++)
-                if (go[b]) ell_finish<kFault, kCap>(a, vb[b], W, pb[b], &wbuf[lb[b] * W], L[b], c, md.mark, &wl);
+        for (uint32_t i = t; i < nc; i += kBlock) {
+            const uint32_t x = cand[i], lv = x >> 2;
+            const uint32_t v = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
+            pt_vertex_fast<kFault, true, kCap>(a, v, v * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W], md.mark, &wl);
         }
         __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
     }
@@ -1287,7 +1203,7 @@ __device__ __forceinline__ int fr_vertex(const PtArgs& a, FrLds& S, uint32_t nxt
     for (uint32_t s = 0; s < kCap; s++) {
         const uint32_t q = s < W ? pk[s] : kNoPeer;
         L.cl[s] = q == kNoPeer ? kNoPeer : q >> 3;
-        L.rvv[s] = q == kNoPeer ? 0u : (q >> 3) * W + (q & 7u);
+        L.rv[s] = q == kNoPeer ? 0u : (q >> 3) * W + (q & 7u);
     }
     FrontierSink sink{a, S, nxt};
     return pt_vertex_core<kFault, kCap>(a, v, v * W, W, w, L, c, sink);

@@ -8,6 +8,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -3 "gpurun_out/$name.log"; [ $rc -le 1 ] || exit $rc; }
 step t_dm 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_demers_shard.py
 step t_cs 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_causal_shard.py tests/test_nif_harness.py
+step t_dly 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_shard.py -k "delay or overlapping" tests/test_plumtree_gpu.py
 step c4 200 python tools/config_bench.py C4
 step mbt 240 tools/mb_transpose
 step pmc_c5 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
