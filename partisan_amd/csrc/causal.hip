@@ -92,12 +92,15 @@ __device__ __forceinline__ bool watch_open(const Wave& w, uint32_t ja, uint32_t 
 struct Rows { uint32_t ml, dl; };
 __device__ __forceinline__ Rows load_rows(const Wave& w, uint32_t e) {
     const CsArgs& a = *w.a;
-    const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
-    const uint32_t* pm = a.base + ((r % kCsWindow) * kCsLanes + k) * kCsLanes;
-    const uint32_t* pd = a.base + (((r - a.period) % kCsWindow) * kCsLanes + k) * kCsLanes;
+    // the row offsets in vector registers: the scalar unit is the busier pipe
+    // (round r's slot at (r % 64) * 4096 words, emitter k's row at k * 64)
+    uint32_t ev = e;
+    asm volatile("" : "+v"(ev));
+    const uint32_t kk = (ev >> 18) & 0xFC0u;
+    const uint32_t im = ((ev & 63u) << 12) | kk, id = (((ev - a.period) & 63u) << 12) | kk;
     Rows q;
-    q.ml = pm[w.lane];
-    q.dl = pd[w.lane];
+    q.ml = a.base[im + w.lane];
+    q.dl = a.base[id + w.lane];
     return q;
 }
 
@@ -129,9 +132,43 @@ __device__ __forceinline__ bool try_deliver(Wave& w, uint32_t e, const Rows& q, 
     return true;
 }
 
+
 // the register entries whose watch is open
 __device__ __forceinline__ unsigned long long pending(const Wave& w) {
     return uni64(__ballot(watch_open(w, w.rja, w.rxw)));
+}
+
+// receive_message + the fold it triggers when the buffer is in registers
+// with room and no entry's watch is open, so that only the entry just
+// received can pass: append, dependency check, delivery, new watch and open
+// set without a branch (try_deliver and fold_reg's fast path, predicated)
+__device__ __forceinline__ void arrive_fast(Wave& w, uint32_t e, const Rows& q) {
+    const uint32_t l = w.nb;
+    const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
+    const uint32_t rs = w.lane == k ? w.rk : 0u;
+    const uint32_t ml = q.ml + rs, dl = q.dl + rs;
+    const unsigned long long f1 = __ballot(w.c < dl);
+    const unsigned long long f2 = __ballot(dl < w.c);
+    const bool chk = r > w.a->period;
+    const bool fail1 = chk && f1 != 0ull;
+    const bool failA = chk && f1 == 0ull && f2 == 0ull && w.self == 0u;
+    const bool ok = !(fail1 || failA);
+    w.checks += l + (chk ? 1u : 0u);                      // the others' watches hold: checks that cannot pass
+    const uint32_t c2 = max(w.c, ml) + w.inc;
+    w.c = ok ? c2 : w.c;
+    w.self += ok ? w.self_inc : 0u;
+    const uint32_t j = (uint32_t)__builtin_ctzll(f1 | (1ull << 63));
+    const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
+    const uint32_t ja = fail1 ? 4u * j : kWatchAny;
+    const uint32_t x = fail1 ? xj : failA ? w.delivered + 1u : kNever;   // delivered: the lane is free again
+    w.delivered += ok ? 1u : 0u;
+    const bool me = w.lane == l;
+    w.rent = me ? e : w.rent;
+    w.rja = me ? ja : w.rja;
+    w.rxw = me ? x : w.rxw;
+    w.nb = ok ? l : l + 1u;
+    const unsigned long long op = pending(w);
+    w.pend = ok ? op : 0ull;
 }
 
 // the fold over the register entries: only open entries are checked; the
@@ -383,23 +420,45 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
             uint32_t lst = chunk(0);
             uint32_t ecur = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, 0));
             Rows qcur = load_rows(w, ecur);
-            for (uint32_t i = 0; i < total; i++) {
+            uint32_t i = 0;
+            // each step loads the next arrival's entry and rows ahead of handling the current one
+            while (i < total) {
+                // a run of arrivals on the branch-free path (one loop, one
+                // register assignment: no copies between paths)
+                while (i < total && w.inreg && w.nb < 64u && w.pend == 0ull) {
+                    uint32_t enext = 0;
+                    Rows qnext = qcur;
+                    if (i + 1u < total) {
+                        if (((i + 1u) & 63u) == 0u) lst = chunk(i + 1u);
+                        enext = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)((i + 1u) & 63u)));
+                        qnext = load_rows(w, enext);
+                    }
+                    w.received++;
+                    arrive_fast(w, ecur, qcur);
+                    folded = true;
+                    ecur = enext;
+                    qcur = qnext;
+                    i++;
+                }
+                if (i >= total) break;
                 uint32_t enext = 0;
                 Rows qnext = qcur;
-                if (i + 1u < total) {                     // the next arrival's rows, loaded ahead
+                if (i + 1u < total) {
                     if (((i + 1u) & 63u) == 0u) lst = chunk(i + 1u);
                     enext = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)((i + 1u) & 63u)));
                     qnext = load_rows(w, enext);
                 }
                 w.received++;
-                if (w.nb >= kCsBufCap) w.err |= 1u;
-                else {
+                if (w.nb >= kCsBufCap) {
+                    w.err |= 1u;
+                } else {
                     append(w, ecur);
                     fold(w, true, ecur, qcur);
                     folded = true;
                 }
                 ecur = enext;
                 qcur = qnext;
+                i++;
             }
         }
         if (a.redeliver && a.t % a.redeliver == 0) {     // handle_info(deliver) (:233-248)
