@@ -65,6 +65,9 @@ struct Wave {
     unsigned long long pend;            // register entries whose watch is open
     uint32_t inreg;                     // 1 while the buffer is in registers
     uint32_t received, delivered, checks, err;
+#ifdef CS_PROF
+    uint32_t pf, pt;                    // diagnostics: fast-path arrivals, general-fold checks
+#endif
 };
 
 // a wave-uniform value, moved to a scalar register (the compiler cannot
@@ -140,35 +143,41 @@ __device__ __forceinline__ unsigned long long pending(const Wave& w) {
 
 // receive_message + the fold it triggers when the buffer is in registers
 // with room and no entry's watch is open, so that only the entry just
-// received can pass: append, dependency check, delivery, new watch and open
-// set without a branch (try_deliver and fold_reg's fast path, predicated)
+// received can pass (try_deliver and fold_reg's fast path for that case):
+// the dependency check is branch-free, then one uniform branch on its
+// outcome -- a delivery leaves lane l as it was (lanes past the buffer never
+// open) and recomputes the open set, a failure appends the entry with its
+// watch
 __device__ __forceinline__ void arrive_fast(Wave& w, uint32_t e, const Rows& q) {
+#ifdef CS_PROF
+    w.pf++;
+#endif
     const uint32_t l = w.nb;
     const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
     const uint32_t rs = w.lane == k ? w.rk : 0u;
     const uint32_t ml = q.ml + rs, dl = q.dl + rs;
     const unsigned long long f1 = __ballot(w.c < dl);
     const unsigned long long f2 = __ballot(dl < w.c);
-    const bool chk = r > w.a->period;
-    const bool fail1 = chk && f1 != 0ull;
-    const bool failA = chk && f1 == 0ull && f2 == 0ull && w.self == 0u;
-    const bool ok = !(fail1 || failA);
-    w.checks += l + (chk ? 1u : 0u);                      // the others' watches hold: checks that cannot pass
-    const uint32_t c2 = max(w.c, ml) + w.inc;
-    w.c = ok ? c2 : w.c;
-    w.self += ok ? w.self_inc : 0u;
-    const uint32_t j = (uint32_t)__builtin_ctzll(f1 | (1ull << 63));
-    const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
-    const uint32_t ja = fail1 ? 4u * j : kWatchAny;
-    const uint32_t x = fail1 ? xj : failA ? w.delivered + 1u : kNever;   // delivered: the lane is free again
-    w.delivered += ok ? 1u : 0u;
-    const bool me = w.lane == l;
-    w.rent = me ? e : w.rent;
-    w.rja = me ? ja : w.rja;
-    w.rxw = me ? x : w.rxw;
-    w.nb = ok ? l : l + 1u;
-    const unsigned long long op = pending(w);
-    w.pend = ok ? op : 0ull;
+    const uint32_t chk = r > w.a->period ? 1u : 0u;
+    // dominates(Local, Dep) fails: a lane below Dep (f1), or Local == Dep (no
+    // lane above it either, and no own-actor entry outside the 64 lanes)
+    const uint32_t fail1 = chk & (f1 != 0ull ? 1u : 0u);
+    const uint32_t failA = chk & (f1 == 0ull ? 1u : 0u) & (f2 == 0ull ? 1u : 0u) & (w.self == 0u ? 1u : 0u);
+    w.checks += l + chk;                                  // the others' watches hold: checks that cannot pass
+    if ((fail1 | failA) == 0u) {
+        w.c = max(w.c, ml) + w.inc;                       // merge + increment(MyNode)
+        w.self += w.self_inc;
+        w.delivered++;
+        w.pend = l ? pending(w) : 0ull;
+    } else {
+        const uint32_t j = (uint32_t)__builtin_ctzll(f1 | (1ull << 63));
+        const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
+        const bool me = w.lane == l;
+        w.rent = me ? e : w.rent;
+        w.rja = me ? (fail1 ? 4u * j : kWatchAny) : w.rja;
+        w.rxw = me ? (fail1 ? xj : w.delivered + 1u) : w.rxw;
+        w.nb = l + 1u;
+    }
 }
 
 // the fold over the register entries: only open entries are checked; the
@@ -207,6 +216,9 @@ __device__ void fold_reg(Wave& w, bool hinted, uint32_t he, const Rows& hq) {
         const Rows q = hinted && l == last ? hq : load_rows(w, e);
         uint32_t ja = 0, x = 0;
         tried++;
+#ifdef CS_PROF
+        w.pt++;
+#endif
         if (try_deliver(w, e, q, ja, x)) {
             gone |= 1ull << l;
             w.rja = wlane(kWatchAny, l, w.rja);
@@ -329,14 +341,17 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
     __shared__ uint32_t sbuf[kWavesPerBlock][kCsBufCap];
     __shared__ uint32_t wj[kWavesPerBlock][kCsBufCap];
     __shared__ uint32_t wx[kWavesPerBlock][kCsBufCap];
-    __shared__ uint32_t alist[kWavesPerBlock][64];
-    __shared__ unsigned long long red[kWavesPerBlock][4];
+    __shared__ uint32_t alist[kWavesPerBlock][3][64];
+    __shared__ unsigned long long red[kWavesPerBlock][6];
     // wave-uniform values are read into scalar registers explicitly, so the
     // fold's control flow stays scalar (no exec-mask bookkeeping)
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const uint32_t lv = blockIdx.x * kWavesPerBlock + wv;
     Wave w;
     w.received = w.delivered = w.checks = w.err = 0;
+#ifdef CS_PROF
+    w.pf = w.pt = 0;
+#endif
     w.nb = 0;
     if (lv < a.n) {
         w.a = &a;
@@ -402,53 +417,88 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
             pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             total += (uint32_t)__popcll(b);
         }
-        uint32_t* al = alist[wv];
-        auto chunk = [&](uint32_t base) -> uint32_t {
+        // the staged list: entry (k << 24 | r) and the word offsets of its
+        // two base rows (message round r, dependency round r - period), so
+        // the per-arrival loads take scalar offsets (buffer loads, soffset)
+        uint32_t* al = alist[wv][0];
+        uint32_t* am_ = alist[wv][1];
+        uint32_t* ad = alist[wv][2];
+        auto chunk = [&](uint32_t base, uint32_t& lm, uint32_t& ld) -> uint32_t {
             for (uint32_t d = 1; d <= a.dmax; d++) {
                 if ((am >> d) & 1u) {
                     const uint32_t p = pre + (uint32_t)__popc(am >> (d + 1u)) - base;
-                    if (p < 64u) al[p] = (lane << 24) | (a.t - d);
+                    if (p < 64u) {
+                        const uint32_t r = a.t - d;
+                        al[p] = (lane << 24) | r;
+                        am_[p] = 4u * (((r % kCsWindow) * kCsLanes + lane) * kCsLanes);
+                        ad[p] = 4u * ((((r - a.period) % kCsWindow) * kCsLanes + lane) * kCsLanes);
+                    }
                 }
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t x = al[lane];
+            lm = am_[lane];
+            ld = ad[lane];
             __builtin_amdgcn_wave_barrier();
             return x;
         };
+        const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a.base, (short)0, (int)(kCsWindow * kCsLanes * kCsLanes * 4), 0x00020000);
+        const int lane4 = (int)(4u * lane);
+        auto rows_at = [&](uint32_t j, uint32_t lm, uint32_t ld) {
+            Rows q;
+            q.ml = __builtin_amdgcn_raw_buffer_load_b32(brs, lane4, __builtin_amdgcn_readlane((int)lm, (int)j), 0);
+            q.dl = __builtin_amdgcn_raw_buffer_load_b32(brs, lane4, __builtin_amdgcn_readlane((int)ld, (int)j), 0);
+            return q;
+        };
         bool folded = false;
+        w.received = total;                               // receive_message for every arrival
         if (total) {
-            uint32_t lst = chunk(0);
+            uint32_t lm = 0, ld = 0;
+            uint32_t lst = chunk(0, lm, ld);
             uint32_t ecur = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, 0));
-            Rows qcur = load_rows(w, ecur);
+            Rows qcur = rows_at(0, lm, ld);
             uint32_t i = 0;
             // each step loads the next arrival's entry and rows ahead of handling the current one
+            auto next = [&](uint32_t& en, Rows& qn) {
+                if (i + 1u < total) {
+                    const uint32_t j = (i + 1u) & 63u;
+                    if (j == 0u) lst = chunk(i + 1u, lm, ld);
+                    en = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)j));
+                    qn = rows_at(j, lm, ld);
+                }
+            };
             while (i < total) {
-                // a run of arrivals on the branch-free path (one loop, one
-                // register assignment: no copies between paths)
-                while (i < total && w.inreg && w.nb < 64u && w.pend == 0ull) {
-                    uint32_t enext = 0;
-                    Rows qnext = qcur;
-                    if (i + 1u < total) {
-                        if (((i + 1u) & 63u) == 0u) lst = chunk(i + 1u);
-                        enext = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)((i + 1u) & 63u)));
-                        qnext = load_rows(w, enext);
+                // a run of arrivals on the fast path, two per iteration so
+                // that the rows loaded ahead alternate between two register
+                // sets instead of being copied
+                if (w.inreg) {
+                    uint32_t eb = 0;
+                    Rows qb = qcur;
+                    for (;;) {
+                        if (!(i < total && w.nb < 64u && w.pend == 0ull)) break;
+                        eb = 0;
+                        qb = qcur;
+                        next(eb, qb);
+                        arrive_fast(w, ecur, qcur);
+                        folded = true;
+                        i++;
+                        if (!(i < total && w.nb < 64u && w.pend == 0ull)) {
+                            ecur = eb;
+                            qcur = qb;
+                            break;
+                        }
+                        ecur = 0;
+                        qcur = qb;
+                        next(ecur, qcur);
+                        arrive_fast(w, eb, qb);
+                        i++;
                     }
-                    w.received++;
-                    arrive_fast(w, ecur, qcur);
-                    folded = true;
-                    ecur = enext;
-                    qcur = qnext;
-                    i++;
                 }
                 if (i >= total) break;
                 uint32_t enext = 0;
                 Rows qnext = qcur;
-                if (i + 1u < total) {
-                    if (((i + 1u) & 63u) == 0u) lst = chunk(i + 1u);
-                    enext = uni((uint32_t)__builtin_amdgcn_readlane((int)lst, (int)((i + 1u) & 63u)));
-                    qnext = load_rows(w, enext);
-                }
-                w.received++;
+                next(enext, qnext);
                 if (w.nb >= kCsBufCap) {
                     w.err |= 1u;
                 } else {
@@ -485,6 +535,10 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         red[wv][1] = w.delivered;
         red[wv][2] = w.checks;
         red[wv][3] = ((unsigned long long)w.err << 32) | w.nb;
+#ifdef CS_PROF
+        red[wv][4] = w.pf;
+        red[wv][5] = w.pt;
+#endif
     }
     __syncthreads();
     if (threadIdx.x < 4) {
@@ -497,6 +551,14 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         if (s) atomicAdd(&st[1 + threadIdx.x], s);
         if (e) atomicOr(&st[5], e);
     }
+#ifdef CS_PROF
+    if (threadIdx.x == 4 || threadIdx.x == 5) {
+        unsigned long long s = 0;
+        for (uint32_t i = 0; i < kWavesPerBlock; i++) s += red[i][threadIdx.x];
+        unsigned long long* st = a.stats + (blockIdx.x & (kStatShards - 1)) * kCsNStat;
+        if (s) atomicAdd(&st[threadIdx.x == 4 ? 0 : 7], s);
+    }
+#endif
 }
 
 // end of round t: emitters due to broadcast record their clock, then

@@ -5,6 +5,7 @@
 #include "../../include/psim.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -152,6 +153,10 @@ int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, si
                 if (q == 5) err |= c.h_stats[sh * kCsNStat + q];
                 else r[q] += c.h_stats[sh * kCsNStat + q];
             }
+#ifdef CS_PROF
+        fprintf(stderr, "cs_prof round %llu received %llu fast %llu general-fold checks %llu\n", (unsigned long long)t,
+                r[1], r[0], r[7]);
+#endif
         if (err & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
                                     (unsigned long long)t, kCsBufCap);
         if (err & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
