@@ -147,8 +147,10 @@ __device__ __forceinline__ unsigned long long pending(const Wave& w) {
 // the dependency check is branch-free, then one uniform branch on its
 // outcome -- a delivery leaves lane l as it was (lanes past the buffer never
 // open) and recomputes the open set, a failure appends the entry with its
-// watch
-__device__ __forceinline__ void arrive_fast(Wave& w, uint32_t e, const Rows& q) {
+// watch.  The entry's own dependency check was counted with the round's
+// arrivals (Wave::checks, kernel).  Returns whether the next arrival can
+// take this path too.
+__device__ __forceinline__ bool arrive_fast(Wave& w, uint32_t e, const Rows& q) {
 #ifdef CS_PROF
     w.pf++;
 #endif
@@ -156,28 +158,36 @@ __device__ __forceinline__ void arrive_fast(Wave& w, uint32_t e, const Rows& q) 
     const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
     const uint32_t rs = w.lane == k ? w.rk : 0u;
     const uint32_t ml = q.ml + rs, dl = q.dl + rs;
-    const unsigned long long f1 = __ballot(w.c < dl);
-    const unsigned long long f2 = __ballot(dl < w.c);
-    const uint32_t chk = r > w.a->period ? 1u : 0u;
-    // dominates(Local, Dep) fails: a lane below Dep (f1), or Local == Dep (no
-    // lane above it either, and no own-actor entry outside the 64 lanes)
-    const uint32_t fail1 = chk & (f1 != 0ull ? 1u : 0u);
-    const uint32_t failA = chk & (f1 == 0ull ? 1u : 0u) & (f2 == 0ull ? 1u : 0u) & (w.self == 0u ? 1u : 0u);
-    w.checks += l + chk;                                  // the others' watches hold: checks that cannot pass
-    if ((fail1 | failA) == 0u) {
-        w.c = max(w.c, ml) + w.inc;                       // merge + increment(MyNode)
-        w.self += w.self_inc;
-        w.delivered++;
-        w.pend = l ? pending(w) : 0ull;
-    } else {
-        const uint32_t j = (uint32_t)__builtin_ctzll(f1 | (1ull << 63));
-        const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
-        const bool me = w.lane == l;
-        w.rent = me ? e : w.rent;
-        w.rja = me ? (fail1 ? 4u * j : kWatchAny) : w.rja;
-        w.rxw = me ? (fail1 ? xj : w.delivered + 1u) : w.rxw;
-        w.nb = l + 1u;
+    w.checks += l;                                        // the others' watches hold: checks that cannot pass
+    if (r > w.a->period) {
+        // dominates(Local, Dep) fails on a lane below Dep ...
+        const unsigned long long f1 = __ballot(w.c < dl);
+        if (f1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(f1);
+            const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
+            const bool me = w.lane == l;
+            w.rent = me ? e : w.rent;
+            w.rja = me ? 4u * j : w.rja;
+            w.rxw = me ? xj : w.rxw;
+            w.nb = l + 1u;
+            return w.nb < 64u;
+        }
+        // ... or on Local == Dep (no lane above it either, no own-actor entry outside the 64 lanes)
+        if (w.self == 0u && __ballot(dl < w.c) == 0ull) {
+            const bool me = w.lane == l;
+            w.rent = me ? e : w.rent;
+            w.rja = me ? kWatchAny : w.rja;
+            w.rxw = me ? w.delivered + 1u : w.rxw;
+            w.nb = l + 1u;
+            return w.nb < 64u;
+        }
     }
+    w.c = max(w.c, ml) + w.inc;                           // merge + increment(MyNode)
+    w.self += w.self_inc;
+    w.delivered++;
+    if (l == 0u) return true;
+    w.pend = pending(w);
+    return w.pend == 0ull;
 }
 
 // the fold over the register entries: only open entries are checked; the
@@ -411,12 +421,16 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
         // receive_message (:205-220) in (src, seq) order: emitter id, then
         // oldest round first.  Arrival i sits at position pre(k) + (bits of
         // lane k above d); the list is staged 64 arrivals at a time.
-        uint32_t pre = 0, total = 0;
+        uint32_t pre = 0, total = 0, nchk = 0;
         for (uint32_t d = 1; d <= a.dmax; d++) {
             const unsigned long long b = __ballot((am >> d) & 1u);
             pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             total += (uint32_t)__popcll(b);
+            if (a.t - d > a.period) nchk += (uint32_t)__popcll(b);   // arrivals with a dependency to check
         }
+        // each arrival's own first dependency check (orddict:find ... {ok, Dep})
+        // is counted here; the folds count every other check
+        w.checks += nchk;
         // the staged list: entry (k << 24 | r) and the word offsets of its
         // two base rows (message round r, dependency round r - period), so
         // the per-arrival loads take scalar offsets (buffer loads, soffset)
@@ -472,18 +486,17 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
                 // a run of arrivals on the fast path, two per iteration so
                 // that the rows loaded ahead alternate between two register
                 // sets instead of being copied
-                if (w.inreg) {
+                if (w.inreg && w.nb < 64u && w.pend == 0ull) {
                     uint32_t eb = 0;
                     Rows qb = qcur;
+                    folded = true;
                     for (;;) {
-                        if (!(i < total && w.nb < 64u && w.pend == 0ull)) break;
                         eb = 0;
                         qb = qcur;
                         next(eb, qb);
-                        arrive_fast(w, ecur, qcur);
-                        folded = true;
+                        const bool c1 = arrive_fast(w, ecur, qcur);
                         i++;
-                        if (!(i < total && w.nb < 64u && w.pend == 0ull)) {
+                        if (!c1 || i >= total) {
                             ecur = eb;
                             qcur = qb;
                             break;
@@ -491,14 +504,17 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
                         ecur = 0;
                         qcur = qb;
                         next(ecur, qcur);
-                        arrive_fast(w, eb, qb);
+                        const bool c2 = arrive_fast(w, eb, qb);
                         i++;
+                        if (!c2 || i >= total) break;
                     }
                 }
                 if (i >= total) break;
                 uint32_t enext = 0;
                 Rows qnext = qcur;
                 next(enext, qnext);
+                // the fold below counts this entry's check itself (none on overflow)
+                w.checks -= (ecur & 0xFFFFFFu) > a.period ? 1u : 0u;
                 if (w.nb >= kCsBufCap) {
                     w.err |= 1u;
                 } else {
