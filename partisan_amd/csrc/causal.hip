@@ -190,6 +190,41 @@ __device__ __forceinline__ bool arrive_fast(Wave& w, uint32_t e, const Rows& q) 
     return w.pend == 0ull;
 }
 
+// A fold's dependency check of register entry l (entry e, rows q), as
+// try_deliver with nested uniform branches: deliver it (the lane is freed,
+// the open set recomputed) or give it its new watch (it leaves the open set)
+__device__ __forceinline__ bool try_lane(Wave& w, uint32_t l, uint32_t e, const Rows& q) {
+    const uint32_t k = e >> 24, r = e & 0xFFFFFFu;
+    const uint32_t rs = w.lane == k ? w.rk : 0u;
+    const uint32_t dl = q.dl + rs;
+    const bool me = w.lane == l;
+    if (r > w.a->period) {
+        w.checks++;
+        const unsigned long long f1 = __ballot(w.c < dl);
+        if (f1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(f1);
+            const uint32_t xj = (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)j);
+            w.rja = me ? 4u * j : w.rja;
+            w.rxw = me ? xj : w.rxw;
+            w.pend &= ~(1ull << l);
+            return false;
+        }
+        if (w.self == 0u && __ballot(dl < w.c) == 0ull) {
+            w.rja = me ? kWatchAny : w.rja;
+            w.rxw = me ? w.delivered + 1u : w.rxw;
+            w.pend &= ~(1ull << l);
+            return false;
+        }
+    }
+    w.c = max(w.c, q.ml + rs) + w.inc;
+    w.self += w.self_inc;
+    w.delivered++;
+    w.rja = me ? kWatchAny : w.rja;
+    w.rxw = me ? kNever : w.rxw;
+    w.pend = pending(w);
+    return true;
+}
+
 // the fold over the register entries: only open entries are checked; the
 // open set is recomputed after each delivery (the only event that moves the
 // clock), so a fold in which nothing is delivered costs one check per open
@@ -203,18 +238,8 @@ __device__ void fold_reg(Wave& w, bool hinted, uint32_t he, const Rows& hq) {
         // watches hold); it leaves from the end, so nothing moves
         const uint32_t e = hinted ? he : uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)last));
         const Rows q = hinted ? hq : load_rows(w, e);
-        uint32_t ja = 0, x = 0;
         w.checks += last;
-        if (try_deliver(w, e, q, ja, x)) {
-            w.nb = last;
-            w.rja = wlane(kWatchAny, last, w.rja);
-            w.rxw = wlane(kNever, last, w.rxw);
-            w.pend = pending(w);
-        } else {
-            w.rja = wlane(ja, last, w.rja);
-            w.rxw = wlane(x, last, w.rxw);
-            w.pend = 0ull;
-        }
+        if (try_lane(w, last, e, q)) w.nb = last;
         return;
     }
     unsigned long long gone = 0;
@@ -224,21 +249,11 @@ __device__ void fold_reg(Wave& w, bool hinted, uint32_t he, const Rows& hq) {
         const uint32_t l = (uint32_t)__builtin_ctzll(m);
         const uint32_t e = uni((uint32_t)__builtin_amdgcn_readlane((int)w.rent, (int)l));
         const Rows q = hinted && l == last ? hq : load_rows(w, e);
-        uint32_t ja = 0, x = 0;
         tried++;
 #ifdef CS_PROF
         w.pt++;
 #endif
-        if (try_deliver(w, e, q, ja, x)) {
-            gone |= 1ull << l;
-            w.rja = wlane(kWatchAny, l, w.rja);
-            w.rxw = wlane(kNever, l, w.rxw);
-            w.pend = pending(w);
-        } else {
-            w.rja = wlane(ja, l, w.rja);
-            w.rxw = wlane(x, l, w.rxw);
-            w.pend &= ~(1ull << l);
-        }
+        if (try_lane(w, l, e, q)) gone |= 1ull << l;
         if (l == 63u) break;
         m = w.pend & (~0ull << (l + 1u));
     }
