@@ -597,9 +597,13 @@ __device__ __forceinline__ In load_msg(const HvArgs& a, uint32_t i) {
     return m;
 }
 
-// One wave per vertex: a wave takes 64 consecutive vertices at a time, keeps
-// those with messages (or every live one on a timer round), and runs each of
-// them with all its lanes.
+// One wave per vertex: a wave takes a.group consecutive vertices at a time,
+// keeps those with messages (or every live one on a timer round), and runs
+// each of them with all its lanes.  The vertices of a group run one after
+// another (each a chain of dependent loads and draws), so the group shrinks
+// until a timer round -- where every live vertex runs -- has about as many
+// waves as the chip holds (hv_group): at 10k vertices 64-vertex groups made
+// 157 waves of 64 vertices each.
 #ifndef HV_WAVES_PER_EU
 #define HV_WAVES_PER_EU 4
 #endif
@@ -610,12 +614,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HV_WAVES
     uint32_t* stage = stage_all[threadIdx.x >> 6];
     uint32_t nstage = 0;
     uint32_t err = 0;
-    for (uint32_t base = gw * 64; base < a.n; base += nw * 64) {
+    const uint32_t G = a.group;
+    for (uint32_t base = gw * G; base < a.n; base += nw * G) {
         uint64_t k0 = 0, k1 = 0, k2 = 0;     // this group's counters (flushed per group: no field overflows)
         uint32_t ndraw = 0, nproc = 0, act1 = 0;
         const uint32_t u = base + l;
         bool want = false;
-        if (u < a.n && alive_of(a, u)) {
+        if (l < G && u < a.n && alive_of(a, u)) {
             // a random_promotion-only round leaves a vertex with >= active_min_size
             // active peers and an empty inbox untouched (no draw, no send)
             want = (a.timers & 2u) || a.off[u + 1] > a.off[u] ||
@@ -776,10 +781,23 @@ __global__ __launch_bounds__(kBlock) void hv_init_kernel(HvArgs a) {
 }
 
 inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
-// hv_process: one 64-vertex group per wave (the waves are latency-bound:
-// as many as the chip holds), grid-striding beyond 64K workgroups
-inline uint32_t hv_blocks(uint32_t n) {
-    const uint32_t groups = (n + 63) / 64;
+// hv_process: vertices per wave -- the smallest power of two that leaves at
+// most HV_WAVE_TARGET waves, so that a timer round at 10k vertices runs 1250
+// waves of 8 vertices (0.082 ms per C2 round against 0.247 with groups of
+// 64 and 0.136 with groups of 2: each wave also pays its staging flush and
+// counter atomics) and one above 128k vertices keeps groups of 64 (groups of
+// 8 measured 2.4x slower at 1M, where the chip is full anyway)
+#ifndef HV_WAVE_TARGET
+#define HV_WAVE_TARGET 2048
+#endif
+inline uint32_t hv_group(uint32_t n) {
+    uint32_t g = 1;
+    while (g < 64 && uint64_t(g) * HV_WAVE_TARGET < n) g <<= 1;
+    return g;
+}
+// grid-striding beyond 64K workgroups
+inline uint32_t hv_blocks(uint32_t n, uint32_t group) {
+    const uint32_t groups = (n + group - 1) / group;
     const uint32_t b = (groups + kHvWaves - 1) / kHvWaves;
     return b < 1 ? 1 : (b > 65535 ? 65535 : b);
 }
@@ -806,7 +824,9 @@ hipError_t launch_hv_round(const HvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(hv_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
     hipLaunchKernelGGL(hv_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(hv_scatter, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(hv_process, dim3(hv_blocks(a.n)), dim3(kBlock), 0, s, a);
+    HvArgs b = a;
+    b.group = hv_group(a.n);
+    hipLaunchKernelGGL(hv_process, dim3(hv_blocks(a.n, b.group)), dim3(kBlock), 0, s, b);
     return hipGetLastError();
 }
 

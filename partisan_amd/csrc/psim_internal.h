@@ -298,6 +298,7 @@ struct HvArgs {
     HvCfg cfg;
     uint2 key;
     uint32_t timers;                      // bit0 random_promotion, bit1 passive_view_maintenance
+    uint32_t group;                       // hv_process: consecutive vertices per wave (1..64, launch_hv_round)
     const uint32_t* __restrict__ alive;   // [ceil(n/32)]
     HvHead* __restrict__ head;            // [n]
     uint32_t* __restrict__ act;           // [n][8], 0xFFFFFFFF padded
