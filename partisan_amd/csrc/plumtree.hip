@@ -381,6 +381,30 @@ __device__ __forceinline__ uint32_t pt_out(uint32_t s, uint32_t r, const VSt& x,
     return fifo | (wtag << kTagShift) | (x.myround << kRoundShift);
 }
 
+// pt_out for replies of at most one message (every reply of a flood's
+// single-message words): the FIFO assembled with selects -- push before the
+// reply on slots after the delivering one, after it on slots before, then the
+// i_have; at most three entries, so no overflow -- and the kinds counted in
+// one add, instead of fifo_append's per-kind walk.
+template <bool kCount>
+__device__ __forceinline__ uint32_t pt_out1(uint32_t s, uint32_t r, const VSt& x, uint32_t ihave, uint32_t wtag,
+                                            Ctr& c) {
+    const uint32_t b = 1u << s;
+    const bool p = (x.push_mask & b) != 0, ih = (ihave & b) != 0;
+    const uint32_t k1 = p && s > x.push_pos ? (uint32_t)PSIM_MSG_BROADCAST : 0u;
+    const uint32_t k3 = p && s < x.push_pos ? (uint32_t)PSIM_MSG_BROADCAST : 0u;
+    const uint32_t k4 = ih ? (uint32_t)PSIM_MSG_IHAVE : 0u;
+    uint32_t fifo = k1, n = k1 ? 1u : 0u;
+    fifo |= r << (kKindBits * n);
+    n += r ? 1u : 0u;
+    fifo |= k3 << (kKindBits * n);
+    n += k3 ? 1u : 0u;
+    fifo |= k4 << (kKindBits * n);
+    if (kCount)
+        c.kinds += (p ? 1ull : 0ull) + (r ? 1ull << (12 * (r - 1u)) : 0ull) + (ih ? 1ull << 24 : 0ull);
+    return (fifo | k4) ? fifo | (wtag << kTagShift) | (x.myround << kRoundShift) : 0u;
+}
+
 // Write back the state record and the outstanding flag; returns the change
 // in "holds outstanding rows" (-1, 0, +1).
 __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint4& st, const VSt& x, Ctr& c) {
@@ -570,15 +594,72 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     c.active++;
     VSt x;
     vst_load(a, v, st, x, L.has_mb ? &L.mb : nullptr);
+    auto peer = [&](uint32_t q) {                        // ids from the registers (select chain)
+        uint32_t id = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kCap; k++) id = k == q ? cl[k] : id;
+        return L.rows ? id : a.col[rs + q];
+    };
     uint32_t r[kCap];
+#ifndef PT_WORD_LOOP
+    // A flood's words carry one message each, a broadcast or a prune: those
+    // vertices take pt_word's clauses over slot masks at once, in the same
+    // slot order -- prunes below the first broadcast, its delivery
+    // (handle_broadcast(true)), then the later broadcasts' prunes and the later
+    // prunes (set operations on distinct slots commute) -- instead of a
+    // divergent per-slot FIFO walk.  Any other word: the general walk.
+    uint32_t bm = 0, pm = 0, om = 0;
 #pragma unroll
-    for (uint32_t s = 0; s < kCap; s++)
-        r[s] = w[s] ? pt_word(a, s, w[s], x, c, [&](uint32_t q) {   // ids from the registers (select chain)
-                   uint32_t id = 0;
+    for (uint32_t s = 0; s < kCap; s++) {
+        const uint32_t f = w[s] & kFifoMask;
+        bm |= (f == PSIM_MSG_BROADCAST ? 1u : 0u) << s;
+        pm |= (f == PSIM_MSG_PRUNE ? 1u : 0u) << s;
+        om |= (f != 0u && f != PSIM_MSG_BROADCAST && f != PSIM_MSG_PRUNE ? 1u : 0u) << s;
+    }
+    if (om == 0u) {
+        uint32_t rep = 0;                                // slots answering a broadcast with a prune
+        if (!x.rcv && bm) {
+            const uint32_t s0 = (uint32_t)__ffs(bm) - 1u, b0 = 1u << s0;
+            const uint32_t pre = pm & (b0 - 1u);
+            x.eager &= ~pre;
+            x.lazy |= pre;
+            uint32_t w0 = 0;
 #pragma unroll
-                   for (uint32_t k = 0; k < kCap; k++) id = k == q ? cl[k] : id;
-                   return L.rows ? id : a.col[rs + q];
-               }) : 0u;
+            for (uint32_t k = 0; k < kCap; k++) w0 = k == s0 ? w[k] : w0;
+            x.rcv = true;                                // merge/2 -> true; handle_broadcast(true) :852-857
+            x.rseq = a.mono8;
+            x.myround = (w0 >> kRoundShift) + 1u;
+            if (x.myround > kMaxRound) { c.overflow |= 2u; x.myround = kMaxRound; }
+            c.deliv++;
+            x.eager |= b0;                               // add_eager(From, Root)
+            x.lazy &= ~b0;
+            x.push_mask = x.eager & ~b0;                 // eager_push(.., Round+1, Root, From)
+            x.push_pos = s0;
+            if (x.outst) c.overflow |= 4u;
+            uint32_t add = x.lazy & ~b0 & ~x.outst;      // schedule_lazy_push(.., Round+1, Root, From)
+            x.outst |= x.lazy & ~b0;
+            while (add) {
+                const uint32_t q = __ffs(add) - 1;
+                add &= add - 1;
+                x.live_delta += bit_alive(a.alive, peer(q));
+            }
+            const uint32_t later = (bm & ~b0) | (pm & ~pre);
+            x.eager &= ~later;                           // add_lazy(From, Root) / prune
+            x.lazy |= later;
+            rep = bm & ~b0;
+        } else {
+            x.eager &= ~(bm | pm);
+            x.lazy |= bm | pm;
+            rep = x.rcv ? bm : 0u;                       // handle_broadcast(false) :843-850
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) r[s] = ((rep >> s) & 1u) ? PSIM_MSG_PRUNE : 0u;
+    } else
+#endif
+    {
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) r[s] = w[s] ? pt_word(a, s, w[s], x, c, peer) : 0u;
+    }
     uint32_t ihave = 0;                                  // pt_ihave over the registers
     if (a.tick && x.outst) {
         // rows held but not due cannot happen (ost mirrors them); still, never test id 0's liveness
@@ -591,7 +672,12 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     uint32_t wo[kCap];
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
+#ifndef PT_WORD_LOOP
+        wo[s] = s >= deg ? 0u : r[s] < 8u ? pt_out1<true>(s, r[s], x, ihave, a.wtag, c)
+                                           : pt_out<true>(s, r[s], x, ihave, a.wtag, c);
+#else
         wo[s] = s < deg ? pt_out<true>(s, r[s], x, ihave, a.wtag, c) : 0u;
+#endif
         sent |= wo[s] != 0u;
         if (kFault && wo[s] && omitted(a, rs + s)) wo[s] = 0u;   // sent (counted) and lost
     }
