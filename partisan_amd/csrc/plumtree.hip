@@ -996,8 +996,14 @@ constexpr uint32_t kVpt = kEllChunk / kBlock;
 static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) <= 65536,
               "ELL chunk: 1-8 vertices per thread, candidates fit 16 bits");
 
+// x / W for x < 2^13 and 1 <= W <= 8: x * ceil(2^18 / W) >> 18 (the rounding
+// error stays below 2^13 / 2^18 of one, under the 1/8 a fraction of x/W
+// leaves to the next integer)
+__device__ __forceinline__ uint32_t div_w(uint32_t x, uint32_t wmag) { return (x * wmag) >> 18; }
+
 template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
+    static_assert(kEllChunk * kEllMax <= (1u << 13), "div_w is exact below 2^13");
     extern __shared__ uint32_t wbuf[];                 // [kEllChunk * W] the live words of the groups read
     __shared__ uint32_t actm[kEllChunk / 32];          // vertices with live words
     __shared__ uint32_t duem[kEllChunk / 32];          // vertices holding outstanding rows on a tick round
@@ -1035,6 +1041,9 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     c.zero();
     const uint32_t nW = a.n * W;                       // words that exist
     const uint32_t gw = kGV * W;
+    // x / W by one multiply (a runtime divide is a ~20-instruction sequence,
+    // and the sweep divided once per quad and once per live word)
+    const uint32_t wmag = ((1u << 18) + W - 1u) / W;
     for (uint32_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
         const uint32_t base = ch * kEllChunk;
         const uint32_t nv = list ? 0u : min(kEllChunk, a.n - base);
@@ -1087,7 +1096,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             if (!live_word(w, a.ctag)) w = 0u;
             wbuf[lwi] = w;
             if (w) {
-                const uint32_t lv = lwi / W;
+                const uint32_t lv = div_w(lwi, wmag);
                 atomicOr(&actm[lv >> 5], 1u << (lv & 31));
             }
         };
@@ -1108,7 +1117,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
 #pragma unroll
                 for (uint32_t k = 0; k < kSweepU; k++) {
                     const uint32_t q = q0 + k * kBlock + t;
-                    const uint32_t i = q / gq, r = (q % gq) * 4u;
+                    const uint32_t i = div_w(q >> 2, wmag), r = (q - i * gq) * 4u;   // gq = 4 W
                     li[k] = q < nq ? pos(i) * gw + r : 0xFFFFFFFFu;
                     gi[k] = q < nq ? gv(i) * W + r : nW;
                     if (gi[k] + 4 <= nW) {
