@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-4 session K: runtime divisions of the sweep as magic multiplies (default)
+# Round-4 session K: the A/B of the working tree (default) against the last commit
 # vs the per-slot FIFO walk (exp_prevhead.so): parity, bench A/B, per-round.
 set -u
 mkdir -p gpurun_out
