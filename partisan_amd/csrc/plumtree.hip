@@ -1004,7 +1004,7 @@ __device__ __forceinline__ uint32_t div_w(uint32_t x, uint32_t wmag) { return (x
 template <bool kFault, uint32_t kCap>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     static_assert(kEllChunk * kEllMax <= (1u << 13), "div_w is exact below 2^13");
-    extern __shared__ uint32_t wbuf[];                 // [kEllChunk * W] the live words of the groups read
+    extern __shared__ __attribute__((aligned(16))) uint32_t wbuf[];   // [kEllChunk * W] the live words of the groups read
     __shared__ uint32_t actm[kEllChunk / 32];          // vertices with live words
     __shared__ uint32_t duem[kEllChunk / 32];          // vertices holding outstanding rows on a tick round
     __shared__ uint16_t cand[kEllChunk];
@@ -1100,8 +1100,41 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
                 atomicOr(&actm[lv >> 5], 1u << (lv & 31));
             }
         };
+        // A chunk whose 64 groups are all read (every dense round: all_in, or
+        // every flag set) holds its words contiguously, in LDS as in HBM: the
+        // sweep is a straight copy of kEllChunk W words, quad k of the chunk to
+        // LDS quad k, and which vertices hold live words is read back from LDS
+        // by the candidate pass -- no per-word group lookup, division or LDS
+        // atomic (the general sweep below spends ~100 VALU per quad on those).
+#if !defined(PT_GROUP_SWEEP_ONLY) && !defined(PT_SCALAR_SWEEP)
+        const bool full = !list && ng == kGroups && nv == kEllChunk &&
+                          (reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0;   // uniform
+#else
+        constexpr bool full = false;
+#endif
 #ifndef PT_SCALAR_SWEEP
-        if ((reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0) {   // group g's words start at 64 W g bytes
+        if (full) {
+            constexpr uint32_t kSweepF = (kEllChunk * kCap / 4 + kBlock - 1) / kBlock;   // W <= kCap
+            const u32x4_t* src = reinterpret_cast<const u32x4_t*>(a.in_cur + size_t(base) * W);
+            static_assert(kEllChunk == 4 * kBlock, "quad k * kBlock + t exists iff k < W");
+            u32x4_t wv[kSweepF];
+#pragma unroll
+            for (uint32_t k = 0; k < kSweepF; k++) {     // k < W: uniform
+                const u32x4_t z = {0u, 0u, 0u, 0u};
+                wv[k] = k < W ? ld_stream<kNtSweep>(src + k * kBlock + t) : z;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kSweepF; k++) {
+                const uint32_t q = k * kBlock + t;
+                if (k >= W) continue;
+                u32x4_t x = wv[k];
+                x.x = live_word(x.x, a.ctag) ? x.x : 0u;
+                x.y = live_word(x.y, a.ctag) ? x.y : 0u;
+                x.z = live_word(x.z, a.ctag) ? x.z : 0u;
+                x.w = live_word(x.w, a.ctag) ? x.w : 0u;
+                reinterpret_cast<u32x4_t*>(wbuf)[q] = x;
+            }
+        } else if ((reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0) {   // group g's words start at 64 W g bytes
             // A group's 16 W words start on a 16-byte boundary: read them as
             // quads, kSweepU quads per thread in flight before any is used (the
             // word-at-a-time loop waited out one load latency per word).
@@ -1152,7 +1185,19 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         {
             constexpr uint32_t kMask = (1u << kVpt) - 1u;
             const uint32_t v4 = kVpt * t;
-            const uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & kMask, dm = (duem[v4 >> 5] >> (v4 & 31)) & kMask;
+            uint32_t am = (actm[v4 >> 5] >> (v4 & 31)) & kMask;
+            if (full) {                                  // live words read back from LDS
+                am = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kVpt; i++) {
+                    uint32_t o = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < kCap; s++)
+                        if (s < W) o |= wbuf[(v4 + i) * W + s];
+                    am |= (o != 0u ? 1u : 0u) << i;
+                }
+            }
+            const uint32_t dm = (duem[v4 >> 5] >> (v4 & 31)) & kMask;
             const uint32_t m = am | dm;
             if (m) {
                 uint32_t k = atomicAdd(&ncand, (uint32_t)__popc(m));
@@ -1177,11 +1222,13 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
 }
 
 template <bool kFault, uint32_t kCap>
-#ifdef PT_WAVES_PER_EU
-#define PT_ELL_ATTR __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU, PT_WAVES_PER_EU)))
-#else
-#define PT_ELL_ATTR
+// At least 5 waves per SIMD (<= 96 VGPRs): the LDS holds 5-6 workgroups per
+// CU at W = 5-6, and the contiguous sweep's quads in flight would otherwise
+// take the kernel to 99 VGPRs, 4 waves (no spills at 96).
+#ifndef PT_WAVES_PER_EU
+#define PT_WAVES_PER_EU 5
 #endif
+#define PT_ELL_ATTR __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU)))
 __global__ __launch_bounds__(kBlock) PT_ELL_ATTR void pt_round_ell_kernel(PtArgs a) {
     pt_round_ell_body<kFault, kCap>(a);
 }
