@@ -384,6 +384,36 @@ hipError_t launch_fm_alive_bm(const uint8_t* alive, uint32_t n, unsigned long lo
 
 // SCAMP v1 / v2 membership strategies (scamp.hip)
 constexpr uint32_t kScPv = 128;       // partial view capacity per vertex
+static_assert(kScPv % 8 == 0, "row_has / row_find read rows as quad pairs");
+// Whether t is among row[0, n) -- a 16-byte aligned row of capacity a
+// multiple of 8 (the SCAMP partial view): quads, two in flight, instead of a
+// dependent load per entry (the connection test of every SCAMP and C3 send).
+__device__ __forceinline__ bool row_has(const uint32_t* __restrict__ row, uint32_t n, uint32_t t) {
+    const uint4* q = reinterpret_cast<const uint4*>(row);
+    for (uint32_t i = 0; i < n; i += 8) {
+        const uint32_t k = n - i;                  // entries left, >= 1
+        const uint4 x = q[i >> 2];
+        const uint4 y = k > 4 ? q[(i >> 2) + 1] : make_uint4(0u, 0u, 0u, 0u);
+        const bool h = (x.x == t) | (k > 1 && x.y == t) | (k > 2 && x.z == t) | (k > 3 && x.w == t) |
+                       (k > 4 && y.x == t) | (k > 5 && y.y == t) | (k > 6 && y.z == t) | (k > 7 && y.w == t);
+        if (h) return true;
+    }
+    return false;
+}
+// The first index of t in row[0, n), or -1 (same layout rules as row_has).
+__device__ __forceinline__ int row_find(const uint32_t* __restrict__ row, uint32_t n, uint32_t t) {
+    const uint4* q = reinterpret_cast<const uint4*>(row);
+    for (uint32_t i = 0; i < n; i += 8) {
+        const uint32_t k = n - i;
+        const uint4 x = q[i >> 2];
+        const uint4 y = k > 4 ? q[(i >> 2) + 1] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t m = (x.x == t ? 1u : 0u) | (k > 1 && x.y == t ? 2u : 0u) | (k > 2 && x.z == t ? 4u : 0u) |
+                           (k > 3 && x.w == t ? 8u : 0u) | (k > 4 && y.x == t ? 16u : 0u) | (k > 5 && y.y == t ? 32u : 0u) |
+                           (k > 6 && y.z == t ? 64u : 0u) | (k > 7 && y.w == t ? 128u : 0u);
+        if (m) return int(i) + __ffs(m) - 1;
+    }
+    return -1;
+}
 constexpr uint32_t kScIv = 64;        // in-view capacity per vertex
 struct ScMsg {                        // one 24-byte record
     uint32_t type, src, dst, seq;     // seq: emission index at src (schedule order key)

@@ -49,12 +49,7 @@ struct Ctx {
     uint32_t dropped, deliv, err;
 };
 
-__device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) {
-    if (t == c.v) return false;
-    for (uint32_t i = 0; i < c.npv; i++)
-        if (c.pv[i] == t) return true;
-    return false;
-}
+__device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) { return t != c.v && row_has(c.pv, c.npv, t); }
 
 __device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     if (!connected(c, t)) { c.dropped++; return; }
@@ -69,11 +64,8 @@ __device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t
     a.out[pos] = m;
 }
 
-__device__ __forceinline__ int tab_find(const Ctx& c, uint32_t x) {
-    for (uint32_t i = 0; i < c.h.ntab; i++)
-        if (c.tab[i] == x) return (int)i;
-    return -1;
-}
+static_assert(kPdTab % 8 == 0, "row_find reads the peer table as quad pairs");
+__device__ __forceinline__ int tab_find(const Ctx& c, uint32_t x) { return row_find(c.tab, c.h.ntab, x); }
 
 // drop ids no set refers to (keeps the masks aligned with the row)
 __device__ __forceinline__ void tab_compact(Ctx& c) {

@@ -57,11 +57,7 @@ __device__ uint64_t draw64(Ctx& c) {
     return (uint64_t)r.x | ((uint64_t)r.y << 32);
 }
 
-__device__ __forceinline__ bool in_pv(const Ctx& c, uint32_t t) {
-    for (uint32_t i = 0; i < c.h.npv; i++)
-        if (c.pv[i] == t) return true;
-    return false;
-}
+__device__ __forceinline__ bool in_pv(const Ctx& c, uint32_t t) { return row_has(c.pv, c.h.npv, t); }
 
 // select_random_sublist(L, K) = lists:sublist(shuffle(L), K): one uniform()
 // per element in list order, then the K smallest (r >> 11, N) in order
@@ -90,9 +86,12 @@ __device__ uint32_t select_sublist(Ctx& c, uint32_t k, uint32_t* out) {
     return got;
 }
 
-__device__ void emit(Ctx& c, uint32_t t, uint32_t type, uint32_t x, uint32_t y, uint32_t extra) {
+// `member`: the caller took t from the live partial view (a member now), so
+// the connection rule needs no scan of the row -- every send but
+// bootstrap_remove's, whose targets come from the in-view
+__device__ void emit(Ctx& c, uint32_t t, uint32_t type, uint32_t x, uint32_t y, uint32_t extra, bool member = false) {
     const ScArgs& a = *c.a;
-    const bool conn = t != c.v && a.alive0[t] && (t == extra || in_pv(c, t));
+    const bool conn = t != c.v && a.alive0[t] && (member || t == extra || in_pv(c, t));
     if (!conn) { c.dropped++; return; }
     const uint32_t pos = wave_reserve(a.nout);
     c.sent[type]++;
@@ -142,15 +141,15 @@ __device__ void do_join(Ctx& c, uint32_t node) {
         const uint32_t t = c.pv[i];
         if (c.a->ver == 2) { if (i == 0) continue; }
         else if (t == node && c.h.npv != n0) continue;
-        emit(c, t, SC_FWD, node, 0, node);
+        emit(c, t, SC_FWD, node, 0, node, true);
     }
-    for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, node);
+    for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, node, true);   // drawn from the row, which only grew
 }
 
 // leave/2 (v2 :140-146, v1 :122-142)
 __device__ void do_leave(Ctx& c, uint32_t node) {
     if (c.a->ver == 2) {
-        for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_BOOT, node, 0, 0xFFFFFFFFu);
+        for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_BOOT, node, 0, 0xFFFFFFFFu, true);
         return;
     }
     // members(State0) in id order, `node` deleted from the set first
@@ -160,7 +159,8 @@ __device__ void do_leave(Ctx& c, uint32_t node) {
     for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
     if (had) pv_del_first(c, node);
     if (had) record_update(c, 0xFFFFFFFFu, node);
-    for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu);
+    for (uint32_t i = 0; i < n0; i++)   // snap minus node is still in the row; node itself is `extra`
+        emit(c, snap[i], SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu, snap[i] != node);
 }
 
 // periodic/1 (v2 :180-221, v1 :174-216); isolation per Q19
@@ -170,9 +170,9 @@ __device__ void do_periodic(Ctx& c) {
         uint32_t sel[1];
         const uint32_t ns = select_sublist(c, 1, sel);
         c.resub++;
-        for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, c.v, 0, 0xFFFFFFFFu);
+        for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, c.v, 0, 0xFFFFFFFFu, true);
     }
-    for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_PING, c.v, 0, 0xFFFFFFFFu);
+    for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_PING, c.v, 0, 0xFFFFFFFFu, true);
 }
 
 // handle_message/2; returns false when the manager stops (:1791-1803)
@@ -198,7 +198,7 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         } else {
             uint32_t sel[1];
             const uint32_t ns = select_sublist(c, 1, sel);
-            for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, 0xFFFFFFFFu);
+            for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, 0xFFFFFFFFu, true);
         }
         break;
     }
@@ -217,7 +217,7 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
         pv_del_first(c, node);
         if (!in_pv(c, node)) record_update(c, 0xFFFFFFFFu, node);   // a duplicate keeps it a member
-        for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, node);
+        for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, node, snap[i] != node);
         break;
     }
     case SC_REPLACE: {                                        // v2 :275-294
