@@ -470,6 +470,19 @@ constexpr uint32_t kPdTab = 128;      // peer-table ids per vertex (PdBits masks
 constexpr uint32_t kPdRows = 256;     // outstanding i_have rows per vertex (heartbeats every round pile them up)
 constexpr uint32_t kPdSets = 5;       // masks per vertex: members, common eager/lazy, root eager/lazy
 constexpr int kPdNStat = 16;
+// SCAMP / C3 round counters are kept in kRoundStatShards copies (workgroup
+// b adds into copy b mod kRoundStatShards; the host folds them): one copy took
+// an atomic from every wave of the 1M-thread grid on the same few words, a
+// ~0.2 ms serial floor under every round whatever it carried.
+constexpr int kRoundStatShards = 64;
+inline void fold_stat_shards(const unsigned long long* raw, unsigned long long* r, int nstat, int or_idx) {
+    for (int i = 0; i < nstat; i++) r[i] = 0;
+    for (int k = 0; k < kRoundStatShards; k++)
+        for (int i = 0; i < nstat; i++) {
+            const unsigned long long x = raw[size_t(k) * nstat + i];
+            r[i] = i == or_idx ? (r[i] | x) : r[i] + x;
+        }
+}
 struct PdHead {
     uint32_t ntab, flags;             // flags: bit0 root's eager/lazy map entries exist, bit1 restarted
     uint32_t myround, seq;            // pushed Round of the current heartbeat; emission counter

@@ -327,12 +327,12 @@ __device__ __forceinline__ void reduce_stats(const PdArgs& a, const unsigned lon
         if (i == 9) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
-            if ((threadIdx.x & 63) == 0 && x) atomicOr(&a.stats[i], x);
+            if ((threadIdx.x & 63) == 0 && x) atomicOr(&a.stats[(blockIdx.x % kRoundStatShards) * kPdNStat + i], x);
             continue;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[i], x);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[(blockIdx.x % kRoundStatShards) * kPdNStat + i], x);
     }
 }
 
@@ -556,7 +556,7 @@ int psim_c3_setup(psim_handle* h, uint32_t n, uint32_t c, uint32_t periodic_roun
     const uint32_t nb = (n + kBlock - 1) / kBlock;
     const bool ok = pd_alloc((void**)&s->head, N * sizeof(PdHead)) && pd_alloc((void**)&s->tab, N * kPdTab * 4) &&
                     pd_alloc((void**)&s->mask, N * kPdSets * sizeof(PdBits)) &&
-                    pd_alloc((void**)&s->rows, N * kPdRows * sizeof(PdRow)) && pd_alloc((void**)&s->stats, kPdNStat * 8) &&
+                    pd_alloc((void**)&s->rows, N * kPdRows * sizeof(PdRow)) && pd_alloc((void**)&s->stats, kRoundStatShards * kPdNStat * 8) &&
                     pd_alloc((void**)&s->msg[0], size_t(s->cap) * sizeof(PdMsg)) &&
                     pd_alloc((void**)&s->msg[1], size_t(s->cap) * sizeof(PdMsg)) && pd_alloc((void**)&s->nmsg, 16) &&
                     pd_alloc((void**)&s->cnt, N * 4) && pd_alloc((void**)&s->cur, N * 4) &&
@@ -612,11 +612,12 @@ int psim_c3_heartbeat(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     if (rc) return rc;
     a.out = s->msg[s->par];          // the origin's pushes are read by the next round
     a.nout = s->nmsg + s->par;
-    PDCHK(h, hipMemsetAsync(s->stats, 0, kPdNStat * 8, handle_stream(h)));
+    PDCHK(h, hipMemsetAsync(s->stats, 0, kRoundStatShards * kPdNStat * 8, handle_stream(h)));
     PDCHK(h, launch_pd_origin(a, root, handle_stream(h)));
-    unsigned long long r[kPdNStat];
-    PDCHK(h, hipMemcpyAsync(r, s->stats, sizeof r, hipMemcpyDeviceToHost, handle_stream(h)));
+    unsigned long long raw[kRoundStatShards * kPdNStat], r[kPdNStat];
+    PDCHK(h, hipMemcpyAsync(raw, s->stats, sizeof raw, hipMemcpyDeviceToHost, handle_stream(h)));
     PDCHK(h, hipStreamSynchronize(handle_stream(h)));
+    fold_stat_shards(raw, r, kPdNStat, 9);
     if (mono_out) *mono_out = s->mono;
     return pd_check(h, r[9], s->round);
 }
@@ -633,14 +634,15 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         PdArgs a;
         rc = pd_args(h, *s, a);
         if (rc) return rc;
-        PDCHK(h, hipMemsetAsync(s->stats, 0, kPdNStat * 8, st));
+        PDCHK(h, hipMemsetAsync(s->stats, 0, kRoundStatShards * kPdNStat * 8, st));
         PDCHK(h, hipMemsetAsync(s->nmsg + (s->par ^ 1), 0, 4, st));
         PDCHK(h, hipEventRecord(handle_event(h, 2), st));
         PDCHK(h, launch_pd_round(a, st));
         PDCHK(h, hipEventRecord(handle_event(h, 3), st));
-        unsigned long long r[kPdNStat];
-        PDCHK(h, hipMemcpyAsync(r, s->stats, sizeof r, hipMemcpyDeviceToHost, st));
+        unsigned long long raw[kRoundStatShards * kPdNStat], r[kPdNStat];
+        PDCHK(h, hipMemcpyAsync(raw, s->stats, sizeof raw, hipMemcpyDeviceToHost, st));
         PDCHK(h, hipStreamSynchronize(st));
+        fold_stat_shards(raw, r, kPdNStat, 9);
         float ms = 0.f;
         PDCHK(h, hipEventElapsedTime(&ms, handle_event(h, 2), handle_event(h, 3)));
         s->par ^= 1u;

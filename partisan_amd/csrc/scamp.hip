@@ -373,12 +373,12 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         unsigned long long x = vals[i];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[i], x);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&a.stats[(blockIdx.x % kRoundStatShards) * 16 + i], x);
     }
     unsigned long long e = err;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) e |= __shfl_xor(e, o, 64);
-    if ((threadIdx.x & 63) == 0 && e) atomicOr(&a.stats[11], e);
+    if ((threadIdx.x & 63) == 0 && e) atomicOr(&a.stats[(blockIdx.x % kRoundStatShards) * 16 + 11], e);
 }
 
 // init/1 (v2 :75-85, v1 :56-66) for every vertex, or crash-restart of a list
@@ -523,15 +523,16 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     s.cx.clear();
     SCCHK(h, hipMemcpyAsync(s.alive0, s.alive, s.n, hipMemcpyDeviceToDevice, st));
     if (s.ev_cnt) SCCHK(h, hipMemsetAsync(s.ev_cnt, 0, size_t(s.n) * 4, st));
-    SCCHK(h, hipMemsetAsync(s.stats, 0, 16 * 8, st));
+    SCCHK(h, hipMemsetAsync(s.stats, 0, kRoundStatShards * 16 * 8, st));
     SCCHK(h, hipMemsetAsync(s.nmsg + (s.par ^ 1), 0, 4, st));
     ScArgs a = sc_args(h, s);
     SCCHK(h, hipEventRecord(handle_event(h, 0), st));
     SCCHK(h, launch_sc_round(a, st));
     SCCHK(h, hipEventRecord(handle_event(h, 1), st));
-    unsigned long long r[16];
-    SCCHK(h, hipMemcpyAsync(r, s.stats, sizeof r, hipMemcpyDeviceToHost, st));
+    unsigned long long raw[kRoundStatShards * 16], r[16];
+    SCCHK(h, hipMemcpyAsync(raw, s.stats, sizeof raw, hipMemcpyDeviceToHost, st));
     SCCHK(h, hipStreamSynchronize(st));
+    fold_stat_shards(raw, r, 16, 11);
     float ms = 0.f;
     SCCHK(h, hipEventElapsedTime(&ms, handle_event(h, 0), handle_event(h, 1)));
     handle_add_round(h, ms);
@@ -621,7 +622,7 @@ int psim_scamp_setup(psim_handle* h, uint32_t n, uint32_t version, uint32_t c, u
                     sc_alloc((void**)&s->cnt, N * 4) && sc_alloc((void**)&s->cur, N * 4) &&
                     sc_alloc((void**)&s->off, (N + 1) * 4) && sc_alloc((void**)&s->idx, size_t(s->cap) * 4) &&
                     sc_alloc((void**)&s->bsum, size_t(nb) * 4) && sc_alloc((void**)&s->call_off, (N + 1) * 4) &&
-                    sc_alloc((void**)&s->stats, 16 * 8);
+                    sc_alloc((void**)&s->stats, kRoundStatShards * 16 * 8);
     if (!ok) {
         delete s;
         return handle_fail(h, PSIM_ENOMEM, "scamp state for n=%u", n);
