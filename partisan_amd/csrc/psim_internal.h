@@ -39,6 +39,26 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter) {
     base = __shfl(base, (int)leader, 64);
     return base + rank;
 }
+// k < 2^10 consecutive slots for each calling lane, ONE atomicAdd per wave:
+// the wave's exclusive prefix of k is assembled from one ballot per bit of k
+// (ballots see exactly the active lanes, so it holds in divergent code).
+__device__ __forceinline__ uint32_t wave_reserve_n(uint32_t* counter, uint32_t k) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)act) - 1;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 10; b++) {
+        const unsigned long long m = __ballot((k >> b) & 1u);
+        pre += (uint32_t)__popcll(m & lt) << b;
+        tot += (uint32_t)__popcll(m) << b;
+    }
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, tot);
+    base = __shfl(base, (int)leader, 64);
+    return base + pre;
+}
 // Per-lane round-count area (PtArgs::mcnt), u32 words:
 //   [0, 256)    messages sent per round, [4 rounds][64 shards]
 //   [256, 512)  worklist entries per round, [4][64] (PtArgs::wlcnt)

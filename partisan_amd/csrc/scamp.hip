@@ -172,7 +172,25 @@ __device__ void do_periodic(Ctx& c) {
         c.resub++;
         for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, c.v, 0, 0xFFFFFFFFu, true);
     }
-    for (uint32_t i = 0; i < c.h.npv; i++) emit(c, c.pv[i], SC_PING, c.v, 0, 0xFFFFFFFFu, true);
+    // the pings (one per live member but self, in list order): one wave
+    // reservation for all of them instead of one per emit
+    const ScArgs& a = *c.a;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < c.h.npv; i++) {
+        const uint32_t t = c.pv[i];
+        if (t != c.v && a.alive0[t]) k++;
+        else c.dropped++;
+    }
+    uint32_t pos = wave_reserve_n(a.nout, k);                // k <= kScPv < 2^10
+    c.sent[SC_PING] += k;
+    for (uint32_t i = 0; i < c.h.npv && k; i++) {
+        const uint32_t t = c.pv[i];
+        if (t == c.v || !a.alive0[t]) continue;
+        if (pos >= a.out_cap) { c.err |= 1u; break; }
+        ScMsg m;
+        m.type = SC_PING; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.a = c.v; m.b = 0;
+        a.out[pos++] = m;
+    }
 }
 
 // handle_message/2; returns false when the manager stops (:1791-1803)
