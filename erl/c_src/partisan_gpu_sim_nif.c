@@ -545,13 +545,19 @@ static ERL_NIF_TERM nif_demers_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
     (void)argc;
     sim_res* r;
     unsigned maxr;
-    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr) || !r->dm_n) return enif_make_badarg(env);
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
     ERL_NIF_TERM t;
-    unsigned char* seen = enif_make_new_binary(env, (size_t)r->dm_n * 8, &t);
     uint32_t ran = 0;
     enif_mutex_lock(r->mu);
+    /* dm_n is read under the lock: a concurrent demers_setup may change it */
+    const uint32_t nl = r->dm_n;
+    if (!nl) {
+        enif_mutex_unlock(r->mu);
+        return enif_make_badarg(env);
+    }
+    unsigned char* seen = enif_make_new_binary(env, (size_t)nl * 8, &t);
     int rc = psim_demers_run(r->h, maxr, NULL, 0, &ran);
-    if (rc == PSIM_OK) rc = psim_demers_get_seen(r->h, (uint64_t*)seen, r->dm_n);
+    if (rc == PSIM_OK) rc = psim_demers_get_seen(r->h, (uint64_t*)seen, nl);
     enif_mutex_unlock(r->mu);
     if (rc != PSIM_OK) return err(env, rc);
     return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), t);
@@ -559,8 +565,13 @@ static ERL_NIF_TERM nif_demers_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
 
 /* ---- vclock (dense 64-lane clocks, u32-little lanes, 0 = absent) ----------- */
 
-/* vclock(Sim, Op :: descends | dominates | merge | increment, A, B) ->
- *   {ok, <<0|1 per clock>>} | {ok, Clocks}   (B = actor ids for increment) */
+/* vclock(Sim, Op, A, B) -> {ok, Binary} | {error, _}
+ *   Op :: descends | dominates | equal              -> <<0|1 per clock>>
+ *       | merge | glb | subtract_dots               -> Clocks   (B = clocks)
+ *       | increment                                 -> Clocks   (B = u32 actor lanes)
+ *       | get_counter                               -> <<u32 per clock>> (B = actor lanes)
+ * partisan_vclock descends/2, dominates/2, equal/2, merge/1, glb/2,
+ * subtract_dots/2, increment/2, get_counter/2 (src/partisan_vclock.erl:58-198) */
 static ERL_NIF_TERM nif_vclock(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
     sim_res* r;
@@ -570,26 +581,31 @@ static ERL_NIF_TERM nif_vclock(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
         !enif_inspect_binary(env, argv[3], &b) || a.size % cb)
         return enif_make_badarg(env);
     const size_t n = a.size / cb;
-    const int inc = enif_is_identical(argv[1], mk_atom(env, "increment"));
-    if (inc ? b.size != n * 4 : b.size != a.size) return enif_make_badarg(env);
+    static const char* ops[] = {"descends", "dominates", "equal", "merge", "glb", "subtract_dots", "increment",
+                                "get_counter"};
+    int op = -1;
+    for (int i = 0; i < 8 && op < 0; i++)
+        if (enif_is_identical(argv[1], mk_atom(env, ops[i]))) op = i;
+    if (op < 0) return enif_make_badarg(env);
+    const int by_actor = op >= 6;
+    if (by_actor ? b.size != n * 4 : b.size != a.size) return enif_make_badarg(env);
+    const uint32_t* pa = (const uint32_t*)a.data;
+    const uint32_t* pb = (const uint32_t*)b.data;
     ERL_NIF_TERM t;
-    int rc;
-    if (enif_is_identical(argv[1], mk_atom(env, "descends")) || enif_is_identical(argv[1], mk_atom(env, "dominates"))) {
-        unsigned char* o = enif_make_new_binary(env, n, &t);
-        enif_mutex_lock(r->mu);
-        rc = enif_is_identical(argv[1], mk_atom(env, "descends"))
-                 ? psim_vclock_descends(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, o, n)
-                 : psim_vclock_dominates(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, o, n);
-        enif_mutex_unlock(r->mu);
-    } else if (inc || enif_is_identical(argv[1], mk_atom(env, "merge"))) {
-        unsigned char* o = enif_make_new_binary(env, a.size, &t);
-        enif_mutex_lock(r->mu);
-        rc = inc ? psim_vclock_increment(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, (uint32_t*)o, n)
-                 : psim_vclock_merge(r->h, (const uint32_t*)a.data, (const uint32_t*)b.data, (uint32_t*)o, n);
-        enif_mutex_unlock(r->mu);
-    } else {
-        return enif_make_badarg(env);
+    int rc = PSIM_OK;
+    unsigned char* o = enif_make_new_binary(env, op <= 2 ? n : op == 7 ? n * 4 : a.size, &t);
+    enif_mutex_lock(r->mu);
+    switch (op) {
+    case 0: rc = psim_vclock_descends(r->h, pa, pb, o, n); break;
+    case 1: rc = psim_vclock_dominates(r->h, pa, pb, o, n); break;
+    case 2: rc = psim_vclock_equal(r->h, pa, pb, o, n); break;
+    case 3: rc = psim_vclock_merge(r->h, pa, pb, (uint32_t*)o, n); break;
+    case 4: rc = psim_vclock_glb(r->h, pa, pb, (uint32_t*)o, n); break;
+    case 5: rc = psim_vclock_subtract_dots(r->h, pa, pb, (uint32_t*)o, n); break;
+    case 6: rc = psim_vclock_increment(r->h, pa, pb, (uint32_t*)o, n); break;
+    default: rc = psim_vclock_get_counter(r->h, pa, pb, (uint32_t*)o, n); break;
     }
+    enif_mutex_unlock(r->mu);
     return rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"), t) : err(env, rc);
 }
 
@@ -791,6 +807,29 @@ static ERL_NIF_TERM nif_scamp_messages(ErlNifEnv* env, int argc, const ERL_NIF_T
     enif_mutex_unlock(r->mu);
     if (rc != PSIM_OK) { enif_free(m); return err(env, rc); }
     ERL_NIF_TERM list = sc_msg_list(env, m, k);
+    enif_free(m);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), list);
+}
+
+/* scamp_messages_from(Sim, Src) -> {ok, [...]}: scamp_messages/1 keeping only
+ * Src's messages, filtered before any term is built (the Erlang cluster's
+ * outgoing/1 renders one node's sends: ADVICE r4) */
+static ERL_NIF_TERM nif_scamp_messages_from(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned src;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &src)) return enif_make_badarg(env);
+    size_t k = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_scamp_messages(r->h, NULL, 0, &k);
+    psim_scamp_msg* m = rc == PSIM_OK ? (psim_scamp_msg*)enif_alloc((k ? k : 1) * sizeof(psim_scamp_msg)) : NULL;
+    if (rc == PSIM_OK) rc = m ? psim_scamp_messages(r->h, m, k, &k) : PSIM_ENOMEM;
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(m); return err(env, rc); }
+    size_t j = 0;
+    for (size_t i = 0; i < k; i++)
+        if (m[i].src == src) m[j++] = m[i];
+    ERL_NIF_TERM list = sc_msg_list(env, m, j);
     enif_free(m);
     return enif_make_tuple2(env, mk_atom(env, "ok"), list);
 }
@@ -1010,6 +1049,8 @@ static ERL_NIF_TERM fm_msg_list(ErlNifEnv* env, const psim_fm_msg* m, const uint
 
 /* fm_messages(Sim) / fm_take(Sim, Dst) -> {ok, [{Src, Dst, Seq, Known, Removed}]}
  * in handling order (psim_fm_messages / psim_fm_take) */
+/* take: 0 every message, 1 take Dst's, 2 every message from Src (argv[1]),
+ * filtered before the terms are built (fm_messages_from/2) */
 static ERL_NIF_TERM fm_wire(ErlNifEnv* env, const ERL_NIF_TERM argv[], int take) {
     sim_res* r;
     unsigned dst = 0;
@@ -1024,9 +1065,22 @@ static ERL_NIF_TERM fm_wire(ErlNifEnv* env, const ERL_NIF_TERM argv[], int take)
     uint64_t* kw = rc == PSIM_OK ? (uint64_t*)enif_alloc(2 * cap * w * 8) : NULL;
     if (rc == PSIM_OK && (!m || !kw)) rc = PSIM_ENOMEM;
     if (rc == PSIM_OK)
-        rc = take ? psim_fm_take(r->h, dst, m, kw, kw + cap * w, cap, w, &k)
-                  : psim_fm_messages(r->h, m, kw, kw + cap * w, cap, w, &k);
+        rc = take == 1 ? psim_fm_take(r->h, dst, m, kw, kw + cap * w, cap, w, &k)
+                       : psim_fm_messages(r->h, m, kw, kw + cap * w, cap, w, &k);
     enif_mutex_unlock(r->mu);
+    if (rc == PSIM_OK && take == 2) {      /* keep Src = argv[1]'s messages, in order */
+        size_t j = 0;
+        for (size_t i = 0; i < k && i < cap; i++) {
+            if (m[i].src != dst) continue;
+            if (j != i) {
+                m[j] = m[i];
+                memmove(kw + j * w, kw + i * w, w * 8);
+                memmove(kw + cap * w + j * w, kw + cap * w + i * w, w * 8);
+            }
+            j++;
+        }
+        k = j;
+    }
     ERL_NIF_TERM out = rc == PSIM_OK ? enif_make_tuple2(env, mk_atom(env, "ok"),
                                                         fm_msg_list(env, m, kw, kw + cap * w, k < cap ? k : cap, w))
                                      : err(env, rc);
@@ -1041,6 +1095,10 @@ static ERL_NIF_TERM nif_fm_messages(ErlNifEnv* env, int argc, const ERL_NIF_TERM
 static ERL_NIF_TERM nif_fm_take(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
     return fm_wire(env, argv, 1);
+}
+static ERL_NIF_TERM nif_fm_messages_from(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return fm_wire(env, argv, 2);
 }
 
 /* fm_put(Sim, [{Src, Dst, Seq, Known, Removed}]) -> ok: what a simulated node's
@@ -1294,12 +1352,14 @@ static ERL_NIF_TERM nif_demers_shard_run(ErlNifEnv* env, int argc, const ERL_NIF
     unsigned maxr;
     if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
     ERL_NIF_TERM t;
-    unsigned char* seen = enif_make_new_binary(env, (size_t)r->dm_n * 8, &t);
     uint32_t ran = 0;
     enif_mutex_lock(r->mu);
+    /* dm_n read once under the lock: the binary and get_seen agree */
+    const uint32_t nl = r->dm_n;
+    unsigned char* seen = enif_make_new_binary(env, (size_t)nl * 8, &t);
     int rc = psim_demers_shard_broadcast_x(r->h);
     if (rc == PSIM_OK) rc = psim_demers_shard_run(r->h, maxr, NULL, 0, &ran);
-    if (rc == PSIM_OK && r->dm_n) rc = psim_demers_shard_get_seen(r->h, (uint64_t*)seen, r->dm_n);
+    if (rc == PSIM_OK && nl) rc = psim_demers_shard_get_seen(r->h, (uint64_t*)seen, nl);
     enif_mutex_unlock(r->mu);
     if (rc != PSIM_OK) return err(env, rc);
     return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), t);
@@ -1539,6 +1599,7 @@ static ErlNifFunc funcs[] = {
     {"scamp_step", 2, nif_scamp_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_views", 1, nif_scamp_views, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_messages", 1, nif_scamp_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"scamp_messages_from", 2, nif_scamp_messages_from, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_take", 2, nif_scamp_take, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"scamp_put", 2, nif_scamp_put, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_setup", 4, nif_fm_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -1548,6 +1609,7 @@ static ErlNifFunc funcs[] = {
     {"fm_state", 1, nif_fm_state, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_tokens", 1, nif_fm_tokens, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_messages", 1, nif_fm_messages, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"fm_messages_from", 2, nif_fm_messages_from, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_take", 2, nif_fm_take, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fm_put", 2, nif_fm_put, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_setup", 4, nif_c3_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},

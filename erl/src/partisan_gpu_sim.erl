@@ -13,9 +13,9 @@
          demers_setup/5, demers_run/2,
          vclock/4,
          scamp_setup/5, scamp_join/3, scamp_leave/3, scamp_crash/2, scamp_step/2, scamp_views/1,
-         scamp_messages/1, scamp_take/2, scamp_put/2,
+         scamp_messages/1, scamp_messages_from/2, scamp_take/2, scamp_put/2,
          fm_setup/4, fm_join/3, fm_leave/3, fm_step/2, fm_state/1, fm_tokens/1,
-         fm_messages/1, fm_take/2, fm_put/2,
+         fm_messages/1, fm_messages_from/2, fm_take/2, fm_put/2,
          c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
          causal_setup/6, causal_step/2, causal_clocks/1,
          rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2,
@@ -140,7 +140,11 @@ demers_setup(_Sim, _N, _M, _AePeriod, _RumorMongering) -> erlang:nif_error(nif_n
 -spec demers_run(sim(), pos_integer()) -> {ok, non_neg_integer(), binary()} | error().
 demers_run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 
--spec vclock(sim(), descends | dominates | merge | increment, binary(), binary()) -> {ok, binary()} | error().
+%% partisan_vclock on dense 64-lane clocks: B is a clock binary, or u32 actor
+%% lanes for increment / get_counter; descends / dominates / equal return one
+%% byte per clock, get_counter one u32 per clock, the others clocks.
+-spec vclock(sim(), descends | dominates | equal | merge | glb | subtract_dots | increment | get_counter,
+             binary(), binary()) -> {ok, binary()} | error().
 vclock(_Sim, _Op, _A, _B) -> erlang:nif_error(nif_not_loaded).
 
 %% ---- SCAMP v1 / v2 (psim_scamp_*): joins / leaves / crashes are u32 binaries,
@@ -166,6 +170,10 @@ scamp_views(_Sim) -> erlang:nif_error(nif_not_loaded).
 %% the next round's messages in handling order (dst, src, seq)
 -spec scamp_messages(sim()) -> {ok, [wire_msg()]} | error().
 scamp_messages(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% scamp_messages/1 restricted to the messages sent by Src (filtered in the NIF).
+-spec scamp_messages_from(sim(), non_neg_integer()) -> {ok, [wire_msg()]} | error().
+scamp_messages_from(_Sim, _Src) -> erlang:nif_error(nif_not_loaded).
 %% takes Dst's messages off the wire (the next round does not deliver them)
 -spec scamp_take(sim(), non_neg_integer()) -> {ok, [wire_msg()]} | error().
 scamp_take(_Sim, _Dst) -> erlang:nif_error(nif_not_loaded).
@@ -192,6 +200,10 @@ fm_tokens(_Sim) -> erlang:nif_error(nif_not_loaded).
 %% message's state_orset as little-endian u64 token bitmaps.
 -spec fm_messages(sim()) -> {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]} | error().
 fm_messages(_Sim) -> erlang:nif_error(nif_not_loaded).
+
+%% fm_messages/1 restricted to the messages sent by Src (filtered in the NIF).
+-spec fm_messages_from(sim(), non_neg_integer()) -> {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]} | error().
+fm_messages_from(_Sim, _Src) -> erlang:nif_error(nif_not_loaded).
 -spec fm_take(sim(), non_neg_integer()) ->
           {ok, [{non_neg_integer(), non_neg_integer(), non_neg_integer(), binary(), binary()}]} | error().
 fm_take(_Sim, _Dst) -> erlang:nif_error(nif_not_loaded).

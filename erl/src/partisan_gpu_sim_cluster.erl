@@ -46,9 +46,14 @@ start(#{n := N, strategy := Strategy} = Opts) ->
                     Calls = atomics:new(3, []),
                     catch ets:delete(?HIST),
                     ?HIST = ets:new(?HIST, [named_table, public, set]),
+                    %% token words of a full-membership state (psim_fm_setup:
+                    %% ceil(max_tokens / 64)), kept here so deliver/2 never
+                    %% downloads the cluster's states to learn it (ADVICE r4)
+                    FmWords = (maps:get(max_tokens, Opts, 2 * N) + 63) div 64,
                     persistent_term:put(?KEY, #{sim => Sim, n => N, strategy => Strategy,
                                                 periodic => Periodic, calls => Calls,
-                                                live => maps:get(live, Opts, N)}),
+                                                live => maps:get(live, Opts, N),
+                                                fm_words => FmWords}),
                     {ok, Sim};
                 Err ->
                     Err
@@ -237,13 +242,13 @@ snapshot_latest(Sim, Origin) ->
 outgoing(V) ->
     case strategy() of
         full ->
-            {ok, Msgs} = partisan_gpu_sim:fm_messages(sim()),
+            {ok, Msgs} = partisan_gpu_sim:fm_messages_from(sim(), V),
             [{node_spec(Dst), {membership_strategy, {node_spec(Src), full_state(Src, K, R)}}}
-             || {Src, Dst, _Seq, K, R} <- Msgs, Src =:= V];
+             || {Src, Dst, _Seq, K, R} <- Msgs];
         _ ->
-            {ok, Msgs} = partisan_gpu_sim:scamp_messages(sim()),
+            {ok, Msgs} = partisan_gpu_sim:scamp_messages_from(sim(), V),
             [{node_spec(Dst), {membership_strategy, spec_msg(M)}}
-             || {Src, Dst, _Seq, {membership_strategy, M}} <- Msgs, Src =:= V]
+             || {_Src, Dst, _Seq, {membership_strategy, M}} <- Msgs]
     end.
 
 %% The messages for V the next round would deliver, taken off the device:
@@ -325,9 +330,7 @@ full_bits(_) ->
     {error, foreign_state}.
 
 fm_words() ->
-    #{sim := Sim, n := N} = persistent_term:get(?KEY),
-    {ok, Known, _Removed, _Alive} = partisan_gpu_sim:fm_state(Sim),
-    byte_size(Known) div (N * 8).
+    maps:get(fm_words, persistent_term:get(?KEY)).
 
 spec_msg({replace_subscription, A, B}) -> {replace_subscription, node_spec(A), node_spec(B)};
 spec_msg({Tag, A}) -> {Tag, node_spec(A)}.

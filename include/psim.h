@@ -354,6 +354,18 @@ int  psim_vclock_dominates(psim_handle* h, const uint32_t* a, const uint32_t* b,
 int  psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
 /* partisan_vclock:increment(Actor, A) (:140-153) */
 int  psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n);
+/* partisan_vclock:equal/2 (:163-164): lists:sort(A) =:= lists:sort(B), i.e.
+ * lane-wise equality (a dense clock has one entry per actor) */
+int  psim_vclock_equal(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n);
+/* partisan_vclock:glb/2 (:183-198): actors of both, the smaller counter,
+ * sorted = lane-wise min (absent = 0 drops out) */
+int  psim_vclock_glb(psim_handle* h, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
+/* partisan_vclock:subtract_dots(Dots, Clock) (:85-99, drop_dots): a dot
+ * {Actor, C} survives iff get_counter(Actor, Clock) < C; sorted */
+int  psim_vclock_subtract_dots(psim_handle* h, const uint32_t* dots, const uint32_t* clock, uint32_t* out, size_t n);
+/* partisan_vclock:get_counter(Actor, A) (:132-137): out[i] = counter of lane
+ * actor[i] in clock i, 0 when absent (one u32 per clock) */
+int  psim_vclock_get_counter(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n);
 
 /* --- Demers epidemics (protocols/demers_*.erl) ------------------------ */
 typedef struct psim_demers_stats {

@@ -429,6 +429,22 @@ def vc_equal(a, b):
     return bool(lib().orc_vc_equal(_to_dots(a), len(a), _to_dots(b), len(b)))
 
 
+def vc_glb(a, b):
+    cap = max(1, len(a))
+    out = (Dot * cap)()
+    n = C.c_size_t(0)
+    lib().orc_vc_glb(_to_dots(a), len(a), _to_dots(b), len(b), out, cap, C.byref(n))
+    return _from_dots(out, n.value)
+
+
+def vc_subtract_dots(dots, clock):
+    cap = max(1, len(dots))
+    out = (Dot * cap)()
+    n = C.c_size_t(0)
+    lib().orc_vc_subtract_dots(_to_dots(dots), len(dots), _to_dots(clock), len(clock), out, cap, C.byref(n))
+    return _from_dots(out, n.value)
+
+
 def vc_all_nodes(clock):
     cap = max(1, len(clock))
     out = (C.c_uint32 * cap)()

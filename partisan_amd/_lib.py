@@ -294,6 +294,10 @@ SIGNATURES = {
     "psim_vclock_dominates": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_vclock_merge": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_vclock_increment": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_vclock_equal": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
+    "psim_vclock_glb": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_vclock_subtract_dots": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
+    "psim_vclock_get_counter": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_relay_run": (C.c_int64, [_H, C.c_uint32, _P(C.c_uint64), _P(C.c_uint32), C.c_uint64, _P(C.c_uint64),
                                    _P(C.c_uint32), C.c_uint64, _P(C.c_uint8), C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), C.c_uint32,
                                    _P(C.c_uint64), _P(C.c_uint32), _P(RelayStats), C.c_size_t, C.c_size_t]),

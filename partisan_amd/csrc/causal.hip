@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kBlock) void cs_round_kernel(CsArgs a) {
                 next(enext, qnext);
                 // the fold below counts this entry's check itself (none on overflow)
                 w.checks -= (ecur & 0xFFFFFFu) > a.period ? 1u : 0u;
-                if (w.nb >= kCsBufCap) {
+                if (w.nb >= a.bufcap) {
                     w.err |= 1u;
                 } else {
                     append(w, ecur);

@@ -76,6 +76,7 @@ CsArgs make_cs_args(const psim_handle* h, uint32_t t) {
     a.base = c.base;
     a.stats = c.stats;
     a.dring = c.dring;
+    a.bufcap = env_cap("PSIM_CS_BUFCAP", kCsBufCap);
     return a;
 }
 
@@ -212,7 +213,7 @@ int psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* out) 
             else r[q] += c.h_stats[sh * kCsNStat + q];
         }
     if (err & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "causal round %llu: more than %u buffered messages at a vertex",
-                                (unsigned long long)t, kCsBufCap);
+                                (unsigned long long)t, a.bufcap);
     if (err & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "causal round %llu: a buffered message outlived the %u-round "
                                 "clock window", (unsigned long long)t, kCsWindow);
     if (err & 4ull) return handle_fail(h, PSIM_EOVERFLOW, "causal round %llu: a u32 clock entry overflowed",
@@ -255,22 +256,32 @@ int psim_causal_shard_step(psim_handle* h, uint32_t rounds, psim_causal_stats* s
     constexpr size_t kSlab = size_t(kCsLanes) * kCsLanes;
     if (!c.x_slab && !alloc_zero((void**)&c.x_slab, kSlab * 4)) return handle_fail(h, PSIM_ENOMEM, "causal slab");
     std::vector<uint32_t> hs(kSlab);
-    std::vector<int64_t> v(kSlab + 6);
+    std::vector<int64_t> v(kSlab + 6 + kNCodes);
     for (uint32_t i = 0; i < rounds; i++) {
         psim_causal_stats st;
+        memset(&st, 0, sizeof st);
         int rc = psim_causal_shard_round(h, c.x_slab, &st);
-        if (rc) return rc;
+        if (c.world == 1 && rc) return rc;
         if (c.world > 1) {
             // the broadcasting emitters' clocks: each row written by its owner,
             // zero elsewhere -- a sum all-reduce is the gather (16 KB), with the
-            // round's counters in the same call
-            HIPCHK(h, hipMemcpy(hs.data(), c.x_slab, kSlab * 4, hipMemcpyDeviceToHost));
-            for (size_t j = 0; j < kSlab; j++) v[j] = hs[j];
-            const uint64_t loc[6] = {st.emitted, st.received, st.delivered, st.checks, st.buffered, st.algo_bytes};
-            for (int j = 0; j < 6; j++) v[kSlab + j] = (int64_t)loc[j];
+            // round's counters and every shard's error flags in the same call: a
+            // shard whose round failed (buffer cap, clock window, u32 overflow)
+            // still joins it, so no peer waits forever, and all return alike
+            std::fill(v.begin(), v.end(), 0);
+            if (!rc && hipMemcpy(hs.data(), c.x_slab, kSlab * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = handle_fail(h, PSIM_EHIP, "causal slab read-back");
+            if (!rc) {
+                for (size_t j = 0; j < kSlab; j++) v[j] = hs[j];
+                const uint64_t loc[6] = {st.emitted, st.received, st.delivered, st.checks, st.buffered, st.algo_bytes};
+                for (int j = 0; j < 6; j++) v[kSlab + j] = (int64_t)loc[j];
+            }
+            put_code(v.data() + kSlab + 6, rc);
             std::string err;
-            rc = T->allreduce(v.data(), v.size(), handle_stream(h), &err);
-            if (rc) return handle_fail(h, rc, "causal exchange: %s", err.c_str());
+            const int trc = T->allreduce(v.data(), v.size(), handle_stream(h), &err);
+            if (trc) return handle_fail(h, trc, "causal exchange: %s", err.c_str());
+            rc = finish_code(h, v.data() + kSlab + 6, rc, "causal shard step");
+            if (rc) return rc;
             for (size_t j = 0; j < kSlab; j++) hs[j] = (uint32_t)v[j];
             HIPCHK(h, hipMemcpy(c.x_slab, hs.data(), kSlab * 4, hipMemcpyHostToDevice));
             st.emitted = v[kSlab]; st.received = v[kSlab + 1]; st.delivered = v[kSlab + 2];

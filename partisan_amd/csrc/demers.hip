@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
         if (np) {
             a.pushcnt_cur[i] = 0;
             const uint32_t cnt = np < kDmPushCap ? np : kDmPushCap;
-            if (np > kDmPushCap) c.overflow |= 1u;
+            if (np > a.push_cap) c.overflow |= 1u;
             const uint32_t* lst = a.pushlist_cur + (size_t)i * kDmPushCap;
 #ifndef DM_NO_FAST_AE
             if (cnt <= kDmFastPush) {

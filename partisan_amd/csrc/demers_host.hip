@@ -110,6 +110,7 @@ DmArgs dm_args(const psim_handle* h, const DmState& d, uint32_t par) {
     a.n_global = d.n;
     a.sharded = 0;
     a.key = key_of(h);
+    a.push_cap = env_cap("PSIM_DM_PUSHCAP", kDmPushCap);
     a.rm_on = d.rm_on == 1u;
     a.dpc = dm_draws_per_call(d.n);
     a.full = d.full;
@@ -222,6 +223,7 @@ DmArgs dms_args(const psim_handle* h, const DmShard& d, void* rm_shadow, void* p
     a.n_global = d.n_global;
     a.sharded = 1;
     a.key = key_of(h);
+    a.push_cap = env_cap("PSIM_DM_PUSHCAP", kDmPushCap);
     a.rm_on = d.rm_on;
     a.dpc = dm_draws_per_call(d.n_global);
     a.full = d.full;
@@ -286,27 +288,59 @@ int dms_grow(psim_handle* h, uint32_t** p, size_t* cap, size_t words) {
 // over the shards by the transport's host all-reduce (M[s G + g]: slots shard
 // s sends shard g; M[G G + s]: shard s's call records).  Records when the
 // round's traffic reaches fewer than n/8 slots (or always / never, xmode).
-int dms_plan(psim_handle* h, DmShard& d, std::vector<int64_t>& M, bool& sp_rm, bool& sp_x) {
+int dms_plan(psim_handle* h, DmShard& d, std::vector<int64_t>& M, bool& sp_rm, bool& sp_x, int lrc) {
     const hipStream_t s = handle_stream(h);
     const int G = (int)d.world, r = (int)d.rank;
     sp_rm = sp_x = false;
-    M.assign(size_t(G) * G + G, 0);
-    if (d.xmode == 1) return PSIM_OK;
-    DMCHK(h, hipMemsetAsync(d.x_cnt, 0, (G + 1) * 4, s));
-    DMCHK(h, launch_dm_xcount(d.x_rm_shadow, d.world, d.rank, d.chunk, d.x_rmx_all + d.v_lo, d.n, d.x_cnt, s));
-    DMCHK(h, hipMemcpyAsync(d.h_x, d.x_cnt, (G + 1) * 4, hipMemcpyDeviceToHost, s));
-    DMCHK(h, hipStreamSynchronize(s));
-    for (int g = 0; g < G; g++) M[size_t(r) * G + g] = d.h_x[g];
-    M[size_t(G) * G + r] = d.h_x[G];
+    // [G G] slot counts, [G] call records, [kNCodes] error flags: a shard whose
+    // round failed still joins this all-reduce (its peers wait in it) and every
+    // shard leaves with the same code
+    M.assign(size_t(G) * G + G + kNCodes, 0);
+    if (!lrc && d.xmode != 1) {
+        if (hipMemsetAsync(d.x_cnt, 0, (G + 1) * 4, s) != hipSuccess ||
+            launch_dm_xcount(d.x_rm_shadow, d.world, d.rank, d.chunk, d.x_rmx_all + d.v_lo, d.n, d.x_cnt, s) !=
+                hipSuccess ||
+            hipMemcpyAsync(d.h_x, d.x_cnt, (G + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            lrc = handle_fail(h, PSIM_EHIP, "demers exchange plan: counting kernel failed");
+        } else {
+            for (int g = 0; g < G; g++) M[size_t(r) * G + g] = d.h_x[g];
+            M[size_t(G) * G + r] = d.h_x[G];
+        }
+    }
+    put_code(M.data() + size_t(G) * G + G, lrc);
     std::string err;
     const int rc = handle_transport(h)->allreduce(M.data(), M.size(), s, &err);
     if (rc) return handle_fail(h, rc, "demers exchange plan all-reduce: %s", err.c_str());
+    const int code = finish_code(h, M.data() + size_t(G) * G + G, lrc, "demers shard round");
+    if (code) return code;
+    if (d.xmode == 1) return PSIM_OK;
     int64_t rm = 0, x = 0;
     for (int i = 0; i < G * G; i++) rm += M[i];
     for (int i = 0; i < G; i++) x += M[size_t(G) * G + i];
     sp_rm = d.xmode == 2 || rm * 8 < int64_t(d.n_global);
     sp_x = d.xmode == 2 || x * 8 < int64_t(d.n_global);
     return PSIM_OK;
+}
+
+// Record regions of this round's sparse forms, grown before any of them is
+// exchanged: a shard that cannot grow them tells the others in one more
+// all-reduce instead of leaving them in an all-to-all-v.
+int dms_sparse_grow(psim_handle* h, DmShard& d, const std::vector<int64_t>& M, bool sp_rm, bool sp_x) {
+    const int G = (int)d.world, r = (int)d.rank;
+    uint64_t rm_s = 0, rm_r = 0, x_s = 0, x_r = 0;
+    for (int g = 0; g < G; g++) {
+        if (g == r) continue;
+        rm_s += 7 * uint64_t(M[size_t(r) * G + g]);
+        rm_r += 7 * uint64_t(M[size_t(g) * G + r]);
+        x_s += 4 * uint64_t(M[size_t(G) * G + r]);
+        x_r += 4 * uint64_t(M[size_t(G) * G + g]);
+    }
+    const uint64_t snd = std::max(sp_rm ? rm_s : 0, sp_x ? x_s : 0);
+    const uint64_t rcv = std::max(sp_rm ? rm_r : 0, sp_x ? x_r : 0);
+    int lrc = dms_grow(h, &d.x_sp_send, &d.x_cap_send, snd);
+    if (!lrc) lrc = dms_grow(h, &d.x_sp_recv, &d.x_cap_recv, rcv);
+    return agree_rc(h, handle_transport(h), lrc, "demers sparse exchange buffers");
 }
 
 // RM slots as records: pack per destination, all-to-all-v, scatter into the
@@ -379,7 +413,9 @@ int dms_sparse_rmx(psim_handle* h, DmShard& d, const std::vector<int64_t>& M, st
 // handle's stream, or the caller's transport; the own slices are local copies.
 // Without rumor mongering the RM planes and call records stay zero and do not
 // travel.
-int dms_exchange(psim_handle* h, DmShard& d, bool tick) {
+// lrc: this shard's round result -- with several shards it is agreed on in the
+// round's first collective (every shard fails with the same code, none waits).
+int dms_exchange(psim_handle* h, DmShard& d, bool tick, int lrc = PSIM_OK) {
     const hipStream_t s = handle_stream(h);
     const size_t C = d.chunk, NG = size_t(d.world) * C;
     const int G = (int)d.world, r = (int)d.rank;
@@ -394,8 +430,14 @@ int dms_exchange(psim_handle* h, DmShard& d, bool tick) {
     std::vector<int64_t> M;
     bool sp_rm = false, sp_x = false;
     if (G > 1 && d.rm_on) {
-        const int rc = dms_plan(h, d, M, sp_rm, sp_x);
+        int rc = dms_plan(h, d, M, sp_rm, sp_x, lrc);
+        if (!rc && (sp_rm || sp_x)) rc = dms_sparse_grow(h, d, M, sp_rm, sp_x);
         if (rc) return rc;
+    } else if (G > 1) {
+        const int rc = agree_rc(h, T, lrc, "demers shard round");
+        if (rc) return rc;
+    } else if (lrc) {
+        return lrc;
     }
     if (d.rm_on) {
         if (G > 1 && sp_rm) {
@@ -675,8 +717,8 @@ int psim_demers_shard_broadcast_x(psim_handle* h) {
     DmShard* d = dms_of(h);
     if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
     int rc = dms_x_buffers(h, *d);
-    if (!rc) rc = psim_demers_shard_broadcast_all(h, d->x_rm_shadow, d->x_rmx_all);
-    if (!rc) rc = dms_exchange(h, *d, false);
+    if (rc) return rc;
+    rc = dms_exchange(h, *d, false, psim_demers_shard_broadcast_all(h, d->x_rm_shadow, d->x_rmx_all));
     if (!rc) rc = psim_demers_shard_ingest(h, d->x_rm_recv, d->x_pull_sum, d->x_rmx_all, 0);
     return rc;
 }
@@ -685,12 +727,18 @@ int psim_demers_shard_step(psim_handle* h, uint32_t rounds, psim_demers_stats* s
     if (!h) return PSIM_EINVAL;
     DmShard* d = dms_of(h);
     if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    const bool fresh = !d->x_rm_shadow;
     int rc = dms_x_buffers(h, *d);
+    // the first call allocates the exchange buffers: a shard that cannot must
+    // not leave the others in the round's collectives
+    if (fresh && d->world > 1 && handle_transport(h)) rc = agree_rc(h, handle_transport(h), rc, "demers exchange buffers");
     for (uint32_t i = 0; i < rounds && !rc; i++) {
         psim_demers_stats st;
         uint32_t tick = 0;
-        rc = psim_demers_shard_round(h, d->x_rm_shadow, d->x_pull_shadow, d->x_snap_all, d->x_rmx_all, &st, &tick);
-        if (!rc) rc = dms_exchange(h, *d, tick != 0);
+        memset(&st, 0, sizeof st);
+        const int lrc =
+            psim_demers_shard_round(h, d->x_rm_shadow, d->x_pull_shadow, d->x_snap_all, d->x_rmx_all, &st, &tick);
+        rc = dms_exchange(h, *d, tick != 0, lrc);
         if (!rc) rc = psim_demers_shard_ingest(h, d->x_rm_recv, d->x_pull_sum, d->x_rmx_all, tick);
         if (!rc) rc = dms_global(h, *d, st);
         if (!rc) {

@@ -2742,12 +2742,16 @@ void* scratch(psim_handle* h, size_t bytes) {
     return h->scratch_buf;
 }
 
-// one batched vclock op over host buffers: A, B (or actor ids), outputs
+// one batched vclock op over host buffers: A, B (or actor ids), outputs.
+// op (launch_vc): 0 descends, 1 dominates, 4 equal -> outb[n]; 2 merge,
+// 3 increment, 5 glb, 6 subtract_dots -> out[n][64]; 7 get_counter -> out[n]
 int vc_op(psim_handle* h, int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
           uint8_t* outb, size_t n) {
     if (!h || !a || n == 0) return n == 0 ? PSIM_OK : PSIM_EINVAL;
-    if ((op <= 2 && !b) || (op == 3 && !actor) || (op >= 2 && !out) || (op <= 1 && !outb)) return PSIM_EINVAL;
-    if (op == 3)
+    const bool use_b = op != 3 && op != 7, use_act = op == 3 || op == 7;
+    const bool bool_out = op == 0 || op == 1 || op == 4, clock_out = op == 2 || op == 3 || op == 5 || op == 6;
+    if ((use_b && !b) || (use_act && !actor) || (!bool_out && !out) || (bool_out && !outb)) return PSIM_EINVAL;
+    if (use_act)
         for (size_t i = 0; i < n; i++)
             if (actor[i] >= PSIM_VC_LANES) return fail(h, PSIM_EINVAL, "actor %u >= %d", actor[i], PSIM_VC_LANES);
     const size_t cb = n * PSIM_VC_LANES * 4;
@@ -2760,11 +2764,11 @@ int vc_op(psim_handle* h, int op, const uint32_t* a, const uint32_t* b, const ui
     uint8_t* doutb = (uint8_t*)(base + 3 * cb + n * 4);
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemcpyAsync(da, a, cb, hipMemcpyHostToDevice, h->stream));
-    if (op <= 2) HIPCHK(h, hipMemcpyAsync(db, b, cb, hipMemcpyHostToDevice, h->stream));
-    if (op == 3) HIPCHK(h, hipMemcpyAsync(dact, actor, n * 4, hipMemcpyHostToDevice, h->stream));
+    if (use_b) HIPCHK(h, hipMemcpyAsync(db, b, cb, hipMemcpyHostToDevice, h->stream));
+    if (use_act) HIPCHK(h, hipMemcpyAsync(dact, actor, n * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, launch_vc(op, da, db, dact, dout, doutb, n, h->stream));
-    if (op >= 2) HIPCHK(h, hipMemcpyAsync(out, dout, cb, hipMemcpyDeviceToHost, h->stream));
-    else HIPCHK(h, hipMemcpyAsync(outb, doutb, n, hipMemcpyDeviceToHost, h->stream));
+    if (bool_out) HIPCHK(h, hipMemcpyAsync(outb, doutb, n, hipMemcpyDeviceToHost, h->stream));
+    else HIPCHK(h, hipMemcpyAsync(out, dout, clock_out ? cb : n * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PSIM_OK;
 }
@@ -2784,6 +2788,18 @@ int psim_vclock_merge(psim_handle* h, const uint32_t* a, const uint32_t* b, uint
 }
 int psim_vclock_increment(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n) {
     return vc_op(h, 3, a, nullptr, actor, out, nullptr, n);
+}
+int psim_vclock_equal(psim_handle* h, const uint32_t* a, const uint32_t* b, uint8_t* out, size_t n) {
+    return vc_op(h, 4, a, b, nullptr, nullptr, out, n);
+}
+int psim_vclock_glb(psim_handle* h, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
+    return vc_op(h, 5, a, b, nullptr, out, nullptr, n);
+}
+int psim_vclock_subtract_dots(psim_handle* h, const uint32_t* dots, const uint32_t* clock, uint32_t* out, size_t n) {
+    return vc_op(h, 6, dots, clock, nullptr, out, nullptr, n);
+}
+int psim_vclock_get_counter(psim_handle* h, const uint32_t* a, const uint32_t* actor, uint32_t* out, size_t n) {
+    return vc_op(h, 7, a, nullptr, actor, out, nullptr, n);
 }
 
 int psim_plumtree_focus(psim_handle* h, uint32_t root) {
@@ -2827,20 +2843,28 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
-    int64_t busy = 0;
+    int64_t v[1 + kNCodes];
+    int64_t& busy = v[0];
+    busy = 0;
+    int lrc = PSIM_OK;
     for (const auto& l : h->lanes) {
-        if (l.win) return fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
+        if (l.win && !lrc) lrc = fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
         busy += (int64_t)l.inflight;
     }
     if (h->sh.world > 1) {
         // collective: every rank must return the same code, and a shard's own
         // in-flight count says nothing about the others' (ADVICE r3), so the
-        // decision is taken on the global sum before any state changes
+        // decision is taken on the global sum before any state changes; a
+        // rank's own refusal (a window lane) travels in the same all-reduce
+        //  instead of leaving the others in it
         if (!h->sh.xport) return fail(h, PSIM_ESTATE, "delay faults on a sharded handle need the in-library exchange");
+        put_code(v + 1, lrc);
         std::string err;
-        const int rc = h->sh.xport->allreduce(&busy, 1, h->stream, &err);
+        const int rc = h->sh.xport->allreduce(v, 1 + kNCodes, h->stream, &err);
         if (rc) return fail(h, rc, "delay all-reduce: %s", err.c_str());
+        lrc = finish_code(h, v + 1, lrc, "psim_set_delays");
     }
+    if (lrc) return lrc;
     if (busy) return fail(h, PSIM_EBUSY, "messages in flight: a delay change could reorder a pair");
     // every shard installs the table (its own senders' pairs) and the ring,
     // so a delayed word from any shard finds its receiver's inbox ring

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 
 typedef struct psim_handle psim_handle;
@@ -270,6 +271,8 @@ struct DmArgs {
     unsigned long long* __restrict__ pull_cur;   // [n][2]
     unsigned long long* __restrict__ pull_nxt;   // [n_global][2]
     unsigned long long* __restrict__ stats;      // [kStatShards][kNStat]: 1 rm, 2 push, 3 pull, 4 deliv, 5 complete, 6 overflow
+    uint32_t push_cap;                    // AE pushes per vertex and tick before PSIM_EOVERFLOW (<= kDmPushCap;
+                                          // PSIM_DM_PUSHCAP lowers it to test the overflow path)
 };
 hipError_t launch_dm_origins(uint2 key, uint32_t n, uint32_t m, uint32_t* origin, hipStream_t s);
 hipError_t launch_dm_broadcast(const DmArgs& a, const uint32_t* origin, const uint32_t* idbit, hipStream_t s);
@@ -365,6 +368,8 @@ struct CsArgs {
     unsigned long long* __restrict__ stats;
     uint32_t* __restrict__ dring;         // [n][64] or null: lane k = the delays of k's messages of the
                                           // last 8 rounds, 4 bits at r % 8 (dmax <= kCsRingMax)
+    uint32_t bufcap;                      // buffered messages per vertex before PSIM_EOVERFLOW (<= kCsBufCap;
+                                          // PSIM_CS_BUFCAP lowers it to test the overflow path)
 };
 constexpr uint32_t kCsRingMax = 8;
 hipError_t launch_cs_round(const CsArgs& a, hipStream_t s);
@@ -629,6 +634,31 @@ struct Transport {
     virtual int comm_rank() const { return -1; }
 };
 int make_rccl_transport(int device, int rank, int world, const void* id, Transport** out, std::string* err);
+// A capacity knob for tests: getenv(name) clipped to [1, cap], default cap.
+inline uint32_t env_cap(const char* name, uint32_t cap) {
+    const char* e = getenv(name);
+    if (!e) return cap;
+    const unsigned long v = strtoul(e, nullptr, 10);
+    return v < 1 ? 1u : v > cap ? cap : (uint32_t)v;
+}
+
+// Collective error agreement: a rank whose local step fails must
+// still enter the collective its peers wait in, and every rank must then
+// return the same code.  A local code travels as one flag per PSIM_E* code
+// inside an all-reduce that runs anyway (or on its own, agree_rc); the common
+// code is the lowest-numbered flag set.
+constexpr int kNCodes = 12;            // PSIM_EINVAL (-1) .. -12; other nonzero codes use the last slot
+inline void put_code(int64_t* v, int rc) {
+    for (int k = 0; k < kNCodes; k++) v[k] = 0;
+    if (rc < 0 && rc >= -kNCodes) v[-rc - 1] = 1;
+    else if (rc) v[kNCodes - 1] = 1;
+}
+inline int common_code(const int64_t* v) {
+    for (int k = 0; k < kNCodes; k++)
+        if (v[k]) return -(k + 1);
+    return 0;
+}
+
 Transport* make_callback_transport(const psim_transport& t);
 int rccl_unique_id(void* out);
 
@@ -650,12 +680,30 @@ uint64_t handle_seed(const psim_handle* h);
 int handle_fail(psim_handle* h, int code, const char* fmt, ...);
 void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing totals
 hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
+// The agreed code of a collective step (all-reduced flags v, this rank's
+// local code lrc): 0, or the common code -- a rank that did not fail itself
+// names the failure as another shard's.
+inline int finish_code(psim_handle* h, const int64_t* v, int lrc, const char* what) {
+    const int c = common_code(v);
+    if (!c) return 0;
+    if (lrc) return c;
+    return handle_fail(h, c, "%s: another shard failed (code %d)", what, c);
+}
+// ... over an all-reduce of its own
+inline int agree_rc(psim_handle* h, Transport* T, int lrc, const char* what) {
+    int64_t v[kNCodes];
+    put_code(v, lrc);
+    std::string err;
+    const int trc = T->allreduce(v, kNCodes, handle_stream(h), &err);
+    if (trc) return handle_fail(h, trc, "%s: error agreement all-reduce: %s", what, err.c_str());
+    return finish_code(h, v, lrc, what);
+}
 
 hipError_t launch_pt_round(const PtArgs& a, hipStream_t s);   // binned when a.rec_c is set
 uint32_t ell_round_grid(uint32_t W, int device);              // resident workgroups of the ELL kernel
 // one slot-scatter round for nlanes heartbeat lanes (d_args[0..nlanes) on device; a0 = d_args[0] on host)
 hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_t nlanes, hipStream_t s);
-// op: 0 descends, 1 dominates, 2 merge, 3 increment
+// op: 0 descends, 1 dominates, 2 merge, 3 increment, 4 equal, 5 glb, 6 subtract_dots, 7 get_counter
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
                      uint8_t* outb, size_t n, hipStream_t s);
 hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);

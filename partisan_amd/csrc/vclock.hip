@@ -9,6 +9,12 @@
 //   dominates(A, B) (:75-77)  <=> descends(A, B) and not descends(B, A)
 //   merge([A, B])   (:102-129) = lane-wise max (absent < any present)
 //   increment(N, A) (:140-153): lane N := max(A[N], 1) + 1
+//   get_counter(N, A) (:132-137) = A[N] - 1, 0 when absent
+//   equal(A, B)     (:163-164)  <=> A == B lane-wise (sorted sets)
+//   glb(A, B)       (:183-198)  = lane-wise min: an actor absent from
+//       either clock (0) drops out, else the smaller counter
+//   subtract_dots(D, C) (:85-99): dot lane k survives iff present and
+//       get_counter(k, C) < its counter, i.e. D[k] > max(C[k], 1)
 // Clocks are compared as sorted sets (equal/2 sorts, Q23), which is the only
 // order a dense form has.
 #include "psim_internal.h"
@@ -52,6 +58,26 @@ __global__ __launch_bounds__(kBlock) void vc_kernel(int op, const uint32_t* __re
     case 3: {  // increment
         const uint32_t who = actor[c];
         out[i] = lane == who ? (sa > 1u ? sa : 1u) + 1u : sa;
+        break;
+    }
+    case 4: {  // equal
+        const bool e = __all(sa == b[i]);
+        if (lane == 0) outb[c] = e;
+        break;
+    }
+    case 5: {  // glb
+        const uint32_t sb = b[i];
+        out[i] = sa < sb ? sa : sb;
+        break;
+    }
+    case 6: {  // subtract_dots(A = dots, B = clock)
+        const uint32_t sb = b[i];
+        out[i] = sa > (sb > 1u ? sb : 1u) ? sa : 0u;
+        break;
+    }
+    case 7: {  // get_counter: out[c] = counter of actor[c] in A (one word per clock)
+        const uint32_t x = __shfl(sa, (int)actor[c], 64);
+        if (lane == 0) out[c] = x ? x - 1u : 0u;
         break;
     }
     default:

@@ -78,6 +78,47 @@ class VClockOps:
                                       out.ctypes.data_as(P(C.c_uint32)), len(a)), self.sim._h)
         return out
 
+    def _bool(self, fn, a, b):
+        a, b = self._pair(a, b)
+        out = np.zeros(len(a), np.uint8)
+        P = C.POINTER
+        check(fn(self.sim._h, a.ctypes.data_as(P(C.c_uint32)), b.ctypes.data_as(P(C.c_uint32)),
+                 out.ctypes.data_as(P(C.c_uint8)), len(a)), self.sim._h)
+        return out.astype(bool)
+
+    def _clock(self, fn, a, b):
+        a, b = self._pair(a, b)
+        out = np.zeros_like(a)
+        P = C.POINTER
+        check(fn(self.sim._h, a.ctypes.data_as(P(C.c_uint32)), b.ctypes.data_as(P(C.c_uint32)),
+                 out.ctypes.data_as(P(C.c_uint32)), len(a)), self.sim._h)
+        return out
+
+    def equal(self, a, b):
+        """equal/2 (:163-164)."""
+        return self._bool(lib().psim_vclock_equal, a, b)
+
+    def glb(self, a, b):
+        """glb/2 (:183-198): lane-wise min."""
+        return self._clock(lib().psim_vclock_glb, a, b)
+
+    def subtract_dots(self, dots, clock):
+        """subtract_dots(DotList, VClock) (:85-99)."""
+        return self._clock(lib().psim_vclock_subtract_dots, dots, clock)
+
+    def get_counter(self, a, actor_lanes):
+        """get_counter(Actor, VClock) (:132-137), one actor lane per clock."""
+        a = _u32(a)
+        act = _u32(actor_lanes)
+        if act.shape != (len(a),):
+            raise ValueError("one actor lane per clock")
+        out = np.zeros(len(a), np.uint32)
+        P = C.POINTER
+        check(lib().psim_vclock_get_counter(self.sim._h, a.ctypes.data_as(P(C.c_uint32)),
+                                            act.ctypes.data_as(P(C.c_uint32)), out.ctypes.data_as(P(C.c_uint32)),
+                                            len(a)), self.sim._h)
+        return out
+
     def increment(self, a, actor_lanes):
         a = _u32(a)
         act = _u32(actor_lanes)

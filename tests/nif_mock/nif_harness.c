@@ -255,6 +255,23 @@ int main(int argc, char** argv) {
                         (unsigned long long)b);
             }
             fprintf(g_out, "]");
+            if (mock_list_len(ms) > 0) {             /* scamp_messages_from/2 = the Src-filtered list, in order */
+                const uint64_t src = mock_int(mock_elem(mock_list_nth(ms, mock_list_len(ms) / 2), 0));
+                ERL_NIF_TERM f = mock_elem(want_ok_tuple("scamp_messages_from",
+                                                         call("scamp_messages_from", 2, A(sim, mock_uint((uint32_t)src)))), 1);
+                size_t j = 0;
+                for (size_t i = 0; i < mock_list_len(ms); i++) {
+                    ERL_NIF_TERM m = mock_list_nth(ms, i);
+                    if ((uint64_t)mock_int(mock_elem(m, 0)) != src) continue;
+                    if (j >= mock_list_len(f) || mock_int(mock_elem(mock_list_nth(f, j), 1)) != mock_int(mock_elem(m, 1)) ||
+                        mock_int(mock_elem(mock_list_nth(f, j), 2)) != mock_int(mock_elem(m, 2))) {
+                        fprintf(stderr, "scamp_messages_from differs at %zu\n", j);
+                        return 1;
+                    }
+                    j++;
+                }
+                if (j != mock_list_len(f)) { fprintf(stderr, "scamp_messages_from: %zu vs %zu\n", j, mock_list_len(f)); return 1; }
+            }
             if (r == 5 && mock_list_len(ms) > 0) {   /* a manager's round trip: take one node's messages, put them back */
                 const uint64_t d = mock_int(mock_elem(mock_list_nth(ms, 0), 1));
                 ERL_NIF_TERM got = mock_elem(want_ok_tuple("scamp_take", call("scamp_take", 2, A(sim, mock_uint(d)))), 1);
@@ -326,6 +343,26 @@ int main(int argc, char** argv) {
                         (unsigned long long)mock_int(mock_elem(m, 1)), (unsigned long long)kw[0], (unsigned long long)rw[0]);
             }
             fprintf(g_out, "]");
+            if (mock_list_len(ms) > 0) {             /* fm_messages_from/2 = the Src-filtered list, in order */
+                const uint64_t src = mock_int(mock_elem(mock_list_nth(ms, mock_list_len(ms) / 2), 0));
+                ERL_NIF_TERM f = mock_elem(want_ok_tuple("fm_messages_from",
+                                                         call("fm_messages_from", 2, A(sim, mock_uint((uint32_t)src)))), 1);
+                size_t j = 0;
+                for (size_t i = 0; i < mock_list_len(ms); i++) {
+                    ERL_NIF_TERM m = mock_list_nth(ms, i);
+                    if ((uint64_t)mock_int(mock_elem(m, 0)) != src) continue;
+                    size_t z1, z2;
+                    const uint64_t* a = (const uint64_t*)mock_bin_data(mock_elem(m, 3), &z1);
+                    const uint64_t* b = j < mock_list_len(f) ? (const uint64_t*)mock_bin_data(mock_elem(mock_list_nth(f, j), 3), &z2) : NULL;
+                    if (!b || z1 != z2 || memcmp(a, b, z1) != 0 ||
+                        mock_int(mock_elem(mock_list_nth(f, j), 1)) != mock_int(mock_elem(m, 1))) {
+                        fprintf(stderr, "fm_messages_from differs at %zu\n", j);
+                        return 1;
+                    }
+                    j++;
+                }
+                if (j != mock_list_len(f)) { fprintf(stderr, "fm_messages_from: %zu vs %zu\n", j, mock_list_len(f)); return 1; }
+            }
             if (r == 3 && mock_list_len(ms) > 0) {   /* a manager's round trip: take one node's messages, put them back */
                 const uint64_t d = mock_int(mock_elem(mock_list_nth(ms, 0), 1));
                 ERL_NIF_TERM got = mock_elem(want_ok_tuple("fm_take", call("fm_take", 2, A(sim, mock_uint(d)))), 1);

@@ -74,3 +74,38 @@ def test_sharded_causal_matches_oracle(world, n, m, period, dmax, redeliver, tra
 def test_sharded_causal_nccl_world1(transport):
     res = run_world(_worker, 1, 800, 64, 1, 4, 1, "nccl", transport)
     assert res[0] == "ok", res[0]
+
+
+def _overflow_worker(rank, world, port, q):
+    """Only rank 1 lowers its buffer cap (PSIM_CS_BUFCAP, read when a round's
+    arguments are built), so only its shard overflows; both ranks must leave
+    psim_causal_shard_step with PSIM_EOVERFLOW (the failing shard
+    used to return before the all-reduce, leaving rank 0 in it forever)."""
+    try:
+        sys.path.insert(0, ROOT)
+        if rank == 1:
+            os.environ["PSIM_CS_BUFCAP"] = "1"
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import partisan_amd as pa
+        from partisan_amd.causal import ShardedCausal
+        g = ShardedCausal(600, rank, world, m=16, period=1, dmax=4, redeliver=1, device=0, backend="gloo",
+                          seed=0x5EED0005, transport="callback")
+        try:
+            g.step(12)
+            q.put((rank, "no error"))
+        except pa.PsimError as e:
+            q.put((rank, e.name))
+        g.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_sharded_causal_one_shard_overflows():
+    res = run_world(_overflow_worker, 2, timeout=240)
+    assert res[0] == "PSIM_EOVERFLOW" and res[1] == "PSIM_EOVERFLOW", res

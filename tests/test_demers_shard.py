@@ -177,3 +177,40 @@ def test_demers_exchange_routing_gloo_cpu(world):
     res = run_world(_cpu_worker, world, timeout=120)
     for r in range(world):
         assert res[r] == "ok", res[r]
+
+
+def _overflow_worker(rank, world, port, q):
+    """Only rank 1 lowers the anti-entropy push cap (PSIM_DM_PUSHCAP=1: any
+    vertex pushed to twice in a tick overflows), so only its shard fails the
+    round; every rank must leave psim_demers_shard_step with PSIM_EOVERFLOW
+    instead of waiting in the exchange's collectives."""
+    try:
+        sys.path.insert(0, ROOT)
+        if rank == 1:
+            os.environ["PSIM_DM_PUSHCAP"] = "1"
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import partisan_amd as pa
+        from partisan_amd.demers import ShardedDemers
+        sd = ShardedDemers(3000, 64, rank, world, device=0, backend="gloo", ae_period=2, rumor_mongering=True,
+                           seed=0x5EED0004, transport="callback")
+        sd.broadcast()
+        try:
+            sd.step(8)
+            q.put((rank, "no error"))
+        except pa.PsimError as e:
+            q.put((rank, e.name))
+        sd.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "FAIL " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_demers_one_shard_overflows(world):
+    res = run_world(_overflow_worker, world, timeout=240)
+    assert all(res[r] == "PSIM_EOVERFLOW" for r in range(world)), res

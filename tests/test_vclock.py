@@ -81,6 +81,53 @@ def test_dense_encoding_matches_oracle():
         assert sorted_clock(to_sparse(m[i:i + 1], ACTORS)[0]) == sorted_clock(O.vc_merge([A[i], B[i]]))
 
 
+def np_glb(a, b):
+    return np.minimum(a, b)
+
+
+def np_subtract_dots(d, c):
+    return np.where(d > np.maximum(c, 1), d, 0).astype(np.uint32)
+
+
+def np_get_counter(a, act):
+    x = a[np.arange(len(a)), act].astype(np.int64)
+    return np.where(x > 0, x - 1, 0)
+
+
+def test_dense_encoding_rest_matches_oracle():
+    """glb/2, subtract_dots/2, get_counter/2 and equal/2 as lane ops (the
+    kernels' statement) against the oracle's list restatement."""
+    A, B = pairs(600, 4)
+    da, db = to_dense(A, ACTORS), to_dense(B, ACTORS)
+    g = np_glb(da, db)
+    sd = np_subtract_dots(da, db)
+    eq = (da == db).all(axis=1)
+    rng = np.random.default_rng(5)
+    act = rng.integers(0, LANES, len(A))
+    gc = np_get_counter(da, act)
+    for i in range(len(A)):
+        assert to_sparse(g[i:i + 1], ACTORS)[0] == O.vc_glb(A[i], B[i]), i
+        assert to_sparse(sd[i:i + 1], ACTORS)[0] == O.vc_subtract_dots(A[i], B[i]), i
+        assert eq[i] == O.vc_equal(A[i], B[i]), i
+        assert gc[i] == O.vc_get_counter(ACTORS[act[i]], A[i]), i
+    # equal/2 compares sorted lists: a permuted clock is equal
+    assert O.vc_equal([[101, 2], [100, 1]], [[100, 1], [101, 2]])
+
+
+# the example in subtract_dots/2's doc comment (src/partisan_vclock.erl:81-83):
+# [{a,3},{b,2},{d,14},{g,22}] minus [{a,4},{b,1},{c,1},{d,14},{e,5},{f,2}] = [{b,2},{g,22}]
+SUBTRACT_DOC = ([[1, 3], [2, 2], [4, 14], [7, 22]], [[1, 4], [2, 1], [3, 1], [4, 14], [5, 5], [6, 2]],
+                [[2, 2], [7, 22]])
+
+
+def test_subtract_dots_doc_example():
+    dots, clock, want = SUBTRACT_DOC
+    assert O.vc_subtract_dots(dots, clock) == want
+    actors = list(range(1, 8))
+    d = np_subtract_dots(to_dense([dots], actors), to_dense([clock], actors))
+    assert to_sparse(d, actors)[0] == want
+
+
 def test_dense_encoding_kats(golden_dir):
     kat = json.load(open(os.path.join(golden_dir, "vclock_kat.json")))
     actors = list(range(1, 8))
@@ -151,3 +198,39 @@ def test_large_batch_properties(ops):
     assert np.array_equal(m, np.maximum(a, b))
     assert ops.descends(m, a).all() and ops.descends(m, b).all()
     assert np.array_equal(ops.descends(a, b), (a >= b).all(axis=1))
+
+
+@pytest.mark.gpu
+def test_kernels_rest_match_oracle(ops):
+    """Device glb / subtract_dots / get_counter / equal against the oracle,
+    plus the accessor KAT (src/partisan_vclock.erl:212-220) and the
+    subtract_dots doc example."""
+    A, B = pairs(5000, 6)
+    A += [[[100, 3], [101, 1]], [[100, 0]]]
+    B += [[[101, 1], [100, 3]], [[100, 0]]]      # permuted equal; zero counters equal
+    da, db = to_dense(A, ACTORS), to_dense(B, ACTORS)
+    g = ops.glb(da, db)
+    sd = ops.subtract_dots(da, db)
+    eq = ops.equal(da, db)
+    rng = np.random.default_rng(7)
+    act = rng.integers(0, LANES, len(A)).astype(np.uint32)
+    gc = ops.get_counter(da, act)
+    for i in range(len(A)):
+        assert to_sparse(g[i:i + 1], ACTORS)[0] == O.vc_glb(A[i], B[i]), i
+        assert to_sparse(sd[i:i + 1], ACTORS)[0] == O.vc_subtract_dots(A[i], B[i]), i
+        assert bool(eq[i]) == O.vc_equal(A[i], B[i]), i
+        assert int(gc[i]) == O.vc_get_counter(ACTORS[act[i]], A[i]), i
+    assert eq[-1] and eq[-2]
+    actors = list(range(1, 8))
+    dots, clock, want = SUBTRACT_DOC
+    assert to_sparse(ops.subtract_dots(to_dense([dots], actors), to_dense([clock], actors)), actors)[0] == want
+
+
+@pytest.mark.gpu
+def test_accessor_kat_on_device(ops, golden_dir):
+    kat = json.load(open(os.path.join(golden_dir, "vclock_kat.json")))["accessor"]
+    actors = list(range(1, 8))
+    clk = to_dense([kat["clock"]] * len(kat["get_counter"]), actors)
+    act = np.array([actors.index(a) for a, _ in kat["get_counter"]], np.uint32)
+    got = ops.get_counter(clk, act)
+    assert got.tolist() == [c for _, c in kat["get_counter"]]
