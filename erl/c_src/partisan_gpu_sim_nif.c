@@ -75,7 +75,9 @@ static unsigned map_u32(ErlNifEnv* env, ERL_NIF_TERM m, const char* key, unsigne
     return dflt;
 }
 
-/* new(#{lazy_tick_rounds, exchange_tick_rounds, device, seed}) -> {ok, Sim} */
+/* new(#{lazy_tick_rounds, exchange_tick_rounds, device, seed, max_roots}) -> {ok, Sim}
+ * max_roots: heartbeat roots whose trees the handle keeps (every node of the
+ * cluster heartbeats, partisan_plumtree_backend:341-368); 0 / absent = 16 */
 static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
     if (!enif_is_map(env, argv[0])) return enif_make_badarg(env);
@@ -85,6 +87,7 @@ static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[])
     cfg.device = (int32_t)map_u32(env, argv[0], "device", (unsigned)-1);
     cfg.lazy_tick_rounds = map_u32(env, argv[0], "lazy_tick_rounds", 1);
     cfg.exchange_tick_rounds = map_u32(env, argv[0], "exchange_tick_rounds", 10);
+    cfg.max_roots = map_u32(env, argv[0], "max_roots", 0);
     {
         ERL_NIF_TERM v;
         ErlNifUInt64 seed = 0;

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 2u   /* 2: psim_load_csr takes the col length */
+#define PSIM_ABI_VERSION 3u   /* 2: psim_load_csr takes the col length; 3: psim_config.max_roots, psim_round_stats.words_stored */
 
 #define PSIM_OK         0
 #define PSIM_EINVAL    (-1)   /* bad argument / shape                        */
@@ -37,6 +37,7 @@ extern "C" {
 #define PSIM_EOVERFLOW (-6)   /* a fixed-capacity structure overflowed       */
 #define PSIM_EBUSY     (-7)   /* previous broadcast has not reached quiescence */
 #define PSIM_ENODEV    (-8)   /* no HIP device / kernel image for this GPU   */
+#define PSIM_ENOSPC    (-9)   /* every heartbeat-root slot holds a root's state */
 
 /* Message kinds of the Plumtree protocol (partisan_plumtree_broadcast.erl
  * send sites); index of psim_round_stats.sent[]. */
@@ -58,7 +59,8 @@ typedef struct psim_config {
     uint32_t lazy_tick_rounds;     /* lazy tick every k rounds (>= 1)          */
     uint32_t exchange_tick_rounds; /* accepted for config parity; no effect */
     uint32_t flags;                /* PSIM_CFG_* bits                          */
-    uint32_t _reserved;
+    uint32_t max_roots;            /* heartbeat roots whose per-root state the handle keeps (0 = 16); a
+                                    * new root beyond them is PSIM_ENOSPC, never a silent eviction */
     uint64_t seed;                 /* Philox key for the protocols that draw   */
 } psim_config;
 
@@ -90,6 +92,8 @@ typedef struct psim_round_stats {
     uint64_t outstanding_vertices; /* vertices holding outstanding i_have rows */
     uint64_t algo_bytes;           /* SURVEY 8(d) bytes: 16N + sum(8+4deg) + 32 msgs */
     double   kernel_ms;            /* device time of this round's kernel (hipEvent) */
+    uint64_t words_stored;         /* inbox words (4-byte random stores) the round wrote; a word carries
+                                    * the <= 4 messages of one sender to one receiver */
 } psim_round_stats;
 
 /* --- lifecycle -------------------------------------------------------- */
@@ -731,10 +735,6 @@ int64_t psim_relay_run(psim_handle* h, uint32_t n, const uint64_t* act_ptr, cons
 
 /* Totals since creation: device ms spent in round kernels and rounds run. */
 int  psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rounds);
-/* Totals since creation of the frontier kernel: rounds it ran
- * (one workgroup running a chunk's leading sparse rounds back to back) and the
- * chunks it was launched for.  Diagnostic; no reference counterpart. */
-int  psim_get_frontier(const psim_handle* h, uint64_t* rounds, uint64_t* launches);
 /* Switch PSIM_CFG_CHUNK_TIMING on (chunk != 0) or off after creation: one event
  * pair per chunk (round kernels back to back; on a sharded handle the chunk's
  * time includes its exchanges) or a pair per round kernel (kernel-only times,

@@ -10,13 +10,13 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSIM_LIB_PATH") or os.path.join(HERE, "libpsim.so")   # override: kernel experiments
 
-PSIM_ABI_VERSION = 2
+PSIM_ABI_VERSION = 3
 PSIM_CFG_BINNED = 1   # psim_config.flags: binned Plumtree engine on one GPU
 PSIM_CFG_CSR = 2      # slot-scatter engine keeps CSR rows instead of ELL rows
 PSIM_CFG_CHUNK_TIMING = 4   # one hipEvent pair per chunk of rounds instead of per round
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EHIP", -4: "PSIM_ERCCL",
-    -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV",
+    -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV", -9: "PSIM_ENOSPC",
 }
 MSG_KINDS = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
 
@@ -34,21 +34,22 @@ class FmMsg(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("lazy_tick_rounds", C.c_uint32),
-                ("exchange_tick_rounds", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32),
+                ("exchange_tick_rounds", C.c_uint32), ("flags", C.c_uint32), ("max_roots", C.c_uint32),
                 ("seed", C.c_uint64)]
 
 
 class RoundStats(C.Structure):
     _fields_ = [("sent", C.c_uint64 * 6), ("delivered_new", C.c_uint64), ("active", C.c_uint64),
                 ("senders", C.c_uint64), ("sender_degree_sum", C.c_uint64),
-                ("outstanding_vertices", C.c_uint64), ("algo_bytes", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("outstanding_vertices", C.c_uint64), ("algo_bytes", C.c_uint64), ("kernel_ms", C.c_double),
+                ("words_stored", C.c_uint64)]
 
     def as_dict(self):
         d = {MSG_KINDS[t]: int(self.sent[t]) for t in range(1, 6)}
         d.update(delivered_new=int(self.delivered_new), active=int(self.active), senders=int(self.senders),
                  sender_degree_sum=int(self.sender_degree_sum),
                  outstanding_vertices=int(self.outstanding_vertices), algo_bytes=int(self.algo_bytes),
-                 kernel_ms=float(self.kernel_ms))
+                 kernel_ms=float(self.kernel_ms), words_stored=int(self.words_stored))
         return d
 
 
@@ -192,7 +193,6 @@ SIGNATURES = {
     "psim_get_delivered_mono": (C.c_int, [_H, C.c_uint32, _P(C.c_uint8), C.c_size_t]),
     "psim_get_delivered_range": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_size_t, _P(C.c_uint8)]),
     "psim_get_timing": (C.c_int, [_H, _P(C.c_double), _P(C.c_uint64)]),
-    "psim_get_frontier": (C.c_int, [_H, _P(C.c_uint64), _P(C.c_uint64)]),
     "psim_set_chunk_timing": (C.c_int, [_H, C.c_int]),
     "psim_shard_init": (C.c_int, [_H, C.c_int, C.c_int]),
     "psim_shard_info": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),

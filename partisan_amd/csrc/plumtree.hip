@@ -41,9 +41,9 @@ __device__ __forceinline__ bool bit_alive(const uint32_t* __restrict__ alive, ui
 // time (that would spill the array to scratch).
 struct Ctr {
     unsigned long long kinds;   // field t (t = 1..5) at bits [12(t-1), 12t): 60 bits, no field truncated
-    uint32_t deliv, active, senders, degsum, ost_delta, live_delta, overflow;
+    uint32_t deliv, active, senders, degsum, ost_delta, live_delta, overflow, words;
     __device__ __forceinline__ void zero() {
-        kinds = 0; deliv = active = senders = degsum = ost_delta = live_delta = overflow = 0;
+        kinds = 0; deliv = active = senders = degsum = ost_delta = live_delta = overflow = words = 0;
     }
     __device__ __forceinline__ void kind(uint32_t t) { kinds += 1ull << (12 * (t - 1)); }
     __device__ __forceinline__ unsigned long long get(int i) const {
@@ -56,6 +56,7 @@ struct Ctr {
         case S_OST_DELTA: return (unsigned long long)(long long)(int32_t)ost_delta;
         case S_LIVE_DELTA: return (unsigned long long)(long long)(int32_t)live_delta;
         case S_OVERFLOW: return overflow;
+        case S_WORDS: return words;
         default: return 0;
         }
     }
@@ -224,11 +225,7 @@ __device__ __forceinline__ void deliver_word(const PtArgs& a, uint32_t e, uint32
             put_delayed(a, e, a.rev[e] - a.slot_base, u, w, hist ? hist : delay_hist());
             return;
         }
-#ifdef PT_NT_STORE
-        __builtin_nontemporal_store(w, &a.in_nxt[a.rev[e] - a.slot_base]);
-#else
         a.in_nxt[a.rev[e] - a.slot_base] = w;
-#endif
         mark_group(a, u >> kGroupShift, mark, wl);
     } else if (kFault && a.srg) {
         put_delayed_remote(a, e, w, hist ? hist : delay_hist());
@@ -245,8 +242,8 @@ struct VSt {
     bool rcv;
 };
 
-// `mb`: memb[v] when the caller already loaded it (the frontier kernel issues
-// every load of a vertex at once), else it is read here on an epoch mismatch.
+// `mb`: memb[v] when the caller already loaded it (vload issues it with the
+// state record), else it is read here on an epoch mismatch.
 __device__ __forceinline__ void vst_load(const PtArgs& a, uint32_t v, const uint4& st, VSt& x,
                                          const uint32_t* mb = nullptr) {
     x.eager = st.x;
@@ -410,12 +407,8 @@ __device__ __forceinline__ uint32_t pt_out1(uint32_t s, uint32_t r, const VSt& x
 __device__ __forceinline__ int vst_store(const PtArgs& a, uint32_t v, const uint4& st, const VSt& x, Ctr& c) {
     const uint32_t nw = x.myround | (x.rseq << 16) | (x.ep << 24);
     if (x.eager != st.x || x.lazy != st.y || x.outst != st.z || nw != st.w) {
-#ifndef PT_TEMPORAL_STATE_STORE     // the record is not read again this round: 2.34 -> 2.27 ms per 10M flood
         u32x4_t q = {x.eager, x.lazy, x.outst, nw};
         __builtin_nontemporal_store(q, reinterpret_cast<u32x4_t*>(a.vs) + v);
-#else
-        a.vs[v] = make_uint4(x.eager, x.lazy, x.outst, nw);
-#endif
     }
     c.live_delta += (uint32_t)x.live_delta;
     if ((x.outst0 != 0) != (x.outst != 0)) {
@@ -451,28 +444,16 @@ constexpr uint32_t kFastDeg = 8;
 // after it, so the sweep loads them non-temporally and they do not displace
 // the lines the round scatters its own words into (2.43 -> 2.33 ms per 10M
 // flood, profiles/r02/experiments/ab_nt_loads.txt).  Rows and state records
-// are re-read every round: non-temporal loads of those were slower (A/B
-// macros PT_NT_ROWS, PT_NT_STATE).
+// are re-read every round: non-temporal loads of those were slower or
+// neutral (profiles/r02/experiments/ab_nt_*.txt).
 template <bool kNt, class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
     if constexpr (kNt) return __builtin_nontemporal_load(p);
     else return *p;
 }
-#ifdef PT_NT_ROWS
-constexpr bool kNtRows = true;
-#else
 constexpr bool kNtRows = false;
-#endif
-#ifndef PT_TEMPORAL_SWEEP      // A/B: 2.43 -> 2.33 ms per 10M flood with the sweep non-temporal
 constexpr bool kNtSweep = true;
-#else
-constexpr bool kNtSweep = false;
-#endif
-#ifdef PT_NT_STATE
-constexpr bool kNtState = true;
-#else
 constexpr bool kNtState = false;
-#endif
 
 template <uint32_t kCap>
 struct VLoad {
@@ -492,15 +473,11 @@ template <uint32_t kCap, bool kNtSt = kNtState>
 __device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, VLoad<kCap>& L,
                                       bool rows = true) {
     L.aw = a.alive[(a.v_lo + v) >> 5];
-#ifndef PT_MEMB_LAZY
     // common_eagers, needed when the vertex has no map entry for the root (a
     // fresh tree: every vertex's first round after reset_peers): loaded with
     // the state, not after it -- one dependent round trip less per vertex
     L.mb = a.memb[v];
     L.has_mb = true;
-#else
-    L.has_mb = false;
-#endif
     if constexpr (kNtSt) {
         const u32x4_t q = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.vs) + v);
         L.st = make_uint4(q.x, q.y, q.z, q.w);
@@ -533,8 +510,7 @@ __device__ __forceinline__ bool word_non_prune(uint32_t w) {
 }
 
 // What happens to a local receiver u after its word over slot s was stored:
-// the round kernels flag its group (and list it in a sparse round); the
-// frontier kernel claims it for its own next round (pt_frontier_kernel).
+// the round kernels flag its group (and list it in a sparse round).
 // Mark 2 (flag + worklist) claims a flag with a RETURNING atomicOr: the
 // claims of a vertex's words are all issued before any result is used, so the
 // vertex waits for one atomic round trip instead of one per word (a wave's
@@ -547,10 +523,7 @@ struct GroupSink {
     uint32_t m = 0;
     uint32_t g[kCap];
     __device__ __forceinline__ void word(uint32_t s, uint32_t u) {
-#ifndef PT_SERIAL_CLAIMS                // A/B: each claim's result used before the next word is sent
-        if (mark != 2)
-#endif
-        {
+        if (mark != 2) {
             mark_group(a, u >> kGroupShift, mark, wl);
             return;
         }
@@ -558,10 +531,9 @@ struct GroupSink {
         m |= 1u << s;
     }
     uint32_t old[kCap];
-    // the claims of a vertex, issued together (after its word stores by
-    // default; PT_CLAIMS_FIRST issues them before the stores, so their results
-    // do not wait behind the stores in vmcnt -- measured neutral, round 4:
-    // 2.248 / 2.251 vs 2.239 / 2.229 ms per step, profiles/r04/experiments)
+    // the claims of a vertex, issued together after its word stores (issuing
+    // them before the stores, so their results do not wait behind the stores
+    // in vmcnt, measured neutral in round 4: profiles/r04/experiments)
     __device__ __forceinline__ void issue() {
         if (!m) return;
 #pragma unroll
@@ -601,7 +573,6 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         return L.rows ? id : a.col[rs + q];
     };
     uint32_t r[kCap];
-#ifndef PT_WORD_LOOP
     // A flood's words carry one message each, a broadcast or a prune: those
     // vertices take pt_word's clauses over slot masks at once, in the same
     // slot order -- prunes below the first broadcast, its delivery
@@ -655,7 +626,6 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) r[s] = ((rep >> s) & 1u) ? PSIM_MSG_PRUNE : 0u;
     } else
-#endif
     {
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) r[s] = w[s] ? pt_word(a, s, w[s], x, c, peer) : 0u;
@@ -670,26 +640,16 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     }
     bool sent = false;
     uint32_t wo[kCap];
+    uint32_t nstored = 0;
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
-#ifndef PT_WORD_LOOP
         wo[s] = s >= deg ? 0u : r[s] < 8u ? pt_out1<true>(s, r[s], x, ihave, a.wtag, c)
                                            : pt_out<true>(s, r[s], x, ihave, a.wtag, c);
-#else
-        wo[s] = s < deg ? pt_out<true>(s, r[s], x, ihave, a.wtag, c) : 0u;
-#endif
         sent |= wo[s] != 0u;
         if (kFault && wo[s] && omitted(a, rs + s)) wo[s] = 0u;   // sent (counted) and lost
+        nstored += wo[s] != 0u ? 1u : 0u;
     }
-#ifdef PT_CLAIMS_FIRST
-    // local receivers' group flags / claims first (GroupSink::issue), then the words
-#pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) {
-        const uint32_t u = cl[s] - a.v_lo;
-        if (wo[s] && u < a.n && !(kFault && a.dly)) sink.word(s, u);
-    }
-    sink.issue();
-#endif
+    c.words += nstored;
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         if (!wo[s]) continue;
@@ -697,23 +657,15 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         if (kFault && a.dly && u < a.n) {
             put_delayed(a, rs + s, rv[s] - a.slot_base, u, wo[s], delay_hist());
         } else if (u < a.n) {
-#ifdef PT_NT_STORE
-            __builtin_nontemporal_store(wo[s], &a.in_nxt[rv[s] - a.slot_base]);
-#else
             a.in_nxt[rv[s] - a.slot_base] = wo[s];
-#endif
-#ifndef PT_CLAIMS_FIRST
             sink.word(s, u);
-#endif
         } else if (kFault && a.srg) {
             put_delayed_remote(a, rs + s, wo[s], delay_hist());
         } else {
             a.stage[rs + s] = wo[s];
         }
     }
-#ifndef PT_CLAIMS_FIRST
     sink.issue();
-#endif
     sink.done();
     if (sent) {
         c.senders++;
@@ -757,9 +709,6 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
     pend = any != 0;
     if (!pend && !due) return;
     VLoad<kCap> L;
-#ifdef PT_ROWS_ALWAYS
-    rows = true;
-#endif
     vload(a, v, rs, deg, L, rows);
     pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, mark, wl);
 }
@@ -783,12 +732,10 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
     }
     const uint32_t rs = a.rowp[v];
     const uint32_t deg = a.rowp[v + 1] - rs;
-#ifndef PT_NO_FAST
     if (deg <= kFastDeg) {
         pt_vertex_fast<kFault>(a, v, rs, deg, pend, due, c, nullptr, mark);
         return;
     }
-#endif
     if (pend) {
         bool any = false;
         for (uint32_t s = 0; s < deg; s++) any |= live_word(a.in_cur[rs + s], a.ctag);
@@ -814,6 +761,7 @@ __device__ __forceinline__ void pt_vertex(const PtArgs& a, uint32_t v, bool pend
         const uint32_t w = pt_out<true>(s, pend ? rep[s * kBlock] : 0u, x, ihave, a.wtag, c);
         if (!w) continue;
         deliver_word<kFault>(a, rs + s, w, nullptr, mark);
+        c.words += (kFault && omitted(a, rs + s)) ? 0u : 1u;
         sent = true;
     }
     if (sent) {
@@ -918,7 +866,6 @@ __device__ __forceinline__ void pt_round_body(const PtArgs& a) {
     static_assert(kChunkV == 4 * kBlock && (kChunkV << 2) <= 65536, "candidate encoding");
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
-    if (a.fr_done && a.fr_idx < *a.fr_done) return;    // run by the frontier kernel
     RoundMode md;
     if (!round_counts(a, md)) return;
     const bool all_in = md.all_in;
@@ -988,10 +935,7 @@ __global__ __launch_bounds__(kBlock) void pt_round_kernel(PtArgs a) {
 // (a flagged group typically has one or two receivers in the sparse rounds).
 // kEllChunk vertices per workgroup (kVpt per thread): the words buffer is
 // kEllChunk * W * 4 bytes of LDS, which is what bounds workgroups per CU.
-#ifndef PT_ELL_CHUNK
-#define PT_ELL_CHUNK 1024
-#endif
-constexpr uint32_t kEllChunk = PT_ELL_CHUNK;
+constexpr uint32_t kEllChunk = 1024;   // 512 / 256 / 2048 measured slower
 constexpr uint32_t kVpt = kEllChunk / kBlock;
 static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) <= 65536,
               "ELL chunk: 1-8 vertices per thread, candidates fit 16 bits");
@@ -1015,7 +959,6 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     __shared__ uint32_t ncand, ngrp;
     constexpr uint32_t kGroups = kEllChunk >> kGroupShift, kGV = 1u << kGroupShift;
     const uint32_t t = threadIdx.x;
-    if (a.fr_done && a.fr_idx < *a.fr_done) return;    // run by the frontier kernel
     RoundMode md;
     if (!round_counts(a, md, wl_off)) return;
     const uint32_t W = a.ell;
@@ -1106,13 +1049,8 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         // LDS quad k, and which vertices hold live words is read back from LDS
         // by the candidate pass -- no per-word group lookup, division or LDS
         // atomic (the general sweep below spends ~100 VALU per quad on those).
-#if !defined(PT_GROUP_SWEEP_ONLY) && !defined(PT_SCALAR_SWEEP)
         const bool full = !list && ng == kGroups && nv == kEllChunk &&
                           (reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0;   // uniform
-#else
-        constexpr bool full = false;
-#endif
-#ifndef PT_SCALAR_SWEEP
         if (full) {
             constexpr uint32_t kSweepF = (kEllChunk * kCap / 4 + kBlock - 1) / kBlock;   // W <= kCap
             const u32x4_t* src = reinterpret_cast<const u32x4_t*>(a.in_cur + size_t(base) * W);
@@ -1138,11 +1076,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             // A group's 16 W words start on a 16-byte boundary: read them as
             // quads, kSweepU quads per thread in flight before any is used (the
             // word-at-a-time loop waited out one load latency per word).
-#ifndef PT_SWEEP_U
             constexpr uint32_t kSweepU = 8;   // a dense round's 5 quads per thread all in flight at once
-#else
-            constexpr uint32_t kSweepU = PT_SWEEP_U;
-#endif
             const uint32_t gq = gw >> 2, nq = ng * gq;
             for (uint32_t q0 = 0; q0 < nq; q0 += kBlock * kSweepU) {
                 uint4 wv[kSweepU];
@@ -1174,7 +1108,6 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
                 }
             }
         } else
-#endif
         {
             for (uint32_t q = t; q < ng * gw; q += kBlock) {
                 const uint32_t i = q / gw, r = q % gw;
@@ -1225,11 +1158,7 @@ template <bool kFault, uint32_t kCap>
 // At least 5 waves per SIMD (<= 96 VGPRs): the LDS holds 5-6 workgroups per
 // CU at W = 5-6, and the contiguous sweep's quads in flight would otherwise
 // take the kernel to 99 VGPRs, 4 waves (no spills at 96).
-#ifndef PT_WAVES_PER_EU
-#define PT_WAVES_PER_EU 5
-#endif
-#define PT_ELL_ATTR __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU)))
-__global__ __launch_bounds__(kBlock) PT_ELL_ATTR void pt_round_ell_kernel(PtArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void pt_round_ell_kernel(PtArgs a) {
     pt_round_ell_body<kFault, kCap>(a);
 }
 
@@ -1245,375 +1174,6 @@ __global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __
 template <bool kFault, uint32_t kCap>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs* __restrict__ args) {
     pt_round_ell_body<kFault, kCap>(args[blockIdx.y]);
-}
-
-// ---------------------------------------------------------------------------
-// Frontier kernel (FrArgs, psim_internal.h; DESIGN.md 5 "Sparse rounds: the
-// frontier kernel").  A sparse round in the round kernel costs 18-36 us
-// whatever it carries: its launch and a chain of dependent global operations
-// that cross workgroups (the counts, the list entry, the words, the state,
-// the flag claim, the list reservation, the counters).  Here ONE workgroup
-// runs the chunk's rounds args[0..k) back to back while the frontier -- the
-// vertex pairs that received words -- stays at most f.thr entries:
-//   * the frontier is a list of vertex pairs in LDS; a word for receiver u is
-//     stored as in the round kernel, sets the bit of u's pair in u's group
-//     flag byte (atomicOr, nothing returned) and appends u's pair to the next
-//     list -- a pair may be listed more than once;
-//   * round i's reader of an entry clears the pair's bit (atomicAnd) in the
-//     same round trip as the loads of both vertices' words, state and row;
-//     only the entry that found the bit set handles the pair, through the
-//     round kernel's own handlers (pt_vertex_core: same clauses, same slot
-//     order) -- one dependent round trip per entry, plus the stores;
-//   * vertices that gain rows are kept in f.hl and claimed for the next tick
-//     round, so rows are due exactly as in the round kernel's ost scan;
-//   * each round leaves the group flags, the message counts and the holder
-//     ring a round kernel would leave; the last round run also leaves the
-//     worklist of its receivers' groups (deduplicated through f.gtag), so a
-//     round kernel -- or the next launch -- takes over after any round.  The
-//     round kernels of the rounds run here return at once (PtArgs::fr_done).
-// Everything handed from one round to the next stays in one workgroup (one
-// CU): a barrier orders it, and data written in this launch is loaded
-// non-temporally (L2-served, never a stale L1 line).
-static_assert(kGroupShift == 4, "frontier claims: the 8 vertex pairs of a 16-vertex group are its flag byte's bits");
-constexpr uint32_t kFrWaves = kFrBlock / 64;
-
-template <class T>
-__device__ __forceinline__ T ld_fresh(const T* p) { return __builtin_nontemporal_load(p); }
-
-// flag word and bit of vertex pair p (vertices 2p, 2p + 1; group p >> 3)
-__device__ __forceinline__ uint32_t* fr_word(uint8_t* pend, uint32_t p) {
-    return reinterpret_cast<uint32_t*>(pend) + (p >> 5);
-}
-__device__ __forceinline__ uint32_t fr_bit(uint32_t p) { return 1u << (8u * ((p >> 3) & 3u) + (p & 7u)); }
-
-struct FrLds {
-    uint32_t lst[2][kFrCap];   // frontier lists: vertex pairs (kNoPeer: padding past the last vertex)
-    uint32_t nfr[2];           // entries appended (past kFrCap too: the kernel then stops)
-    uint32_t ngl, nhl, found;
-    int hold0, hd;
-    uint32_t wl_off[65];
-    uint32_t red[kFrWaves][16];
-};
-
-__device__ __forceinline__ void fr_append(FrLds& S, uint32_t which, uint32_t p) {
-    const uint32_t k = atomicAdd(&S.nfr[which], 1u);
-    if (k < kFrCap) S.lst[which][k] = p;
-}
-
-// a local receiver u: its pair is flagged for the next round and listed
-struct FrontierSink {
-    const PtArgs& a;
-    FrLds& S;
-    uint32_t nxt;
-    __device__ __forceinline__ void word(uint32_t, uint32_t u) {
-        atomicOr(fr_word(a.pend_nxt, u >> 1), fr_bit(u >> 1));
-        fr_append(S, nxt, u >> 1);
-    }
-    __device__ __forceinline__ void issue() {}
-    __device__ __forceinline__ void done() {}
-};
-
-// the 8 pairs of group g into list `which`
-__device__ __forceinline__ void fr_push_group(const PtArgs& a, FrLds& S, uint32_t which, uint32_t g) {
-    const uint32_t npair = (a.n + 1) >> 1;
-    const uint32_t k = atomicAdd(&S.nfr[which], 8u);
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) {
-        const uint32_t p = 8 * g + j;
-        if (k + j < kFrCap) S.lst[which][k + j] = p < npair ? p : kNoPeer;
-    }
-}
-
-// one vertex of an entry: its words (live ones only), rows due, and the raw
-// packed row already loaded
-template <bool kFault, uint32_t kCap>
-__device__ __forceinline__ int fr_vertex(const PtArgs& a, FrLds& S, uint32_t nxt, uint32_t v, const uint32_t (&w)[kCap],
-                                         bool due, const uint4& st, uint32_t aw, const uint32_t (&pk)[kCap], uint32_t mb,
-                                         Ctr& c) {
-    uint32_t any = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) any |= w[s];
-    if (!any && !due) return 0;
-    const uint32_t W = a.ell;
-    VLoad<kCap> L;
-    L.st = st;
-    L.aw = aw;
-    L.rows = true;
-    L.has_mb = true;      // no load after this vertex's stores: a later load would wait for them (vmcnt is in order)
-    L.mb = mb;
-#pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) {
-        const uint32_t q = s < W ? pk[s] : kNoPeer;
-        L.cl[s] = q == kNoPeer ? kNoPeer : q >> 3;
-        L.rv[s] = q == kNoPeer ? 0u : (q >> 3) * W + (q & 7u);
-    }
-    FrontierSink sink{a, S, nxt};
-    return pt_vertex_core<kFault, kCap>(a, v, v * W, W, w, L, c, sink);
-}
-
-template <bool kFault, uint32_t kCap>
-__global__ __launch_bounds__(kFrBlock) void pt_frontier_kernel(const PtArgs* __restrict__ args, FrArgs f) {
-    __shared__ FrLds S;
-    const uint32_t t = threadIdx.x;
-    const uint32_t lane = t & 63u, wv = t >> 6;
-    // diagnostic phase stamps (PSIM_FR_PROFILE): slot q of round i at prof[kFrProf i + q]
-    auto stamp = [&](uint32_t i, uint32_t q) {
-        if (f.prof && t == 0) f.prof[kFrProf * i + q] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0, 0);
-    if (f.prof && t == 0) f.prof[7] = __builtin_amdgcn_s_memtime();   // shader clock (its rate vs realtime)
-    // ---- the first round's frontier: the groups the last round listed (or flagged)
-    {
-        const PtArgs& a = args[0];
-        if (t == 0) {
-            S.nfr[0] = S.nfr[1] = 0;
-            S.nhl = S.found = 0;
-            S.hold0 = int(a.mcnt[kMcntHold + a.m_r]) + int(a.mcnt[kMcntHoldD + a.m_s]);
-        }
-        if (t < 64) {
-            uint32_t c2 = a.mcnt[a.m_r * 64 + t];
-            uint32_t l = a.wlcnt[a.m_s * 64 + t];
-            const bool ovf = __ballot(l > a.wl_cap) != 0ull;
-            l = min(l, a.wl_cap);
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(l, off, 64);
-                if (t >= (uint32_t)off) l += y;
-            }
-            S.wl_off[t + 1] = l;
-            if (t == 0) S.wl_off[0] = 0;
-            c2 = __ockl_wfred_add_u32(c2);
-            if (t == 0) {
-                S.red[0][0] = c2;
-                S.red[0][1] = ovf;
-            }
-        }
-        __syncthreads();
-        const uint32_t prev2 = S.red[0][0];
-        // the last round's senders wrote no flags (a dense round): nothing to find the receivers by;
-        // rows held by vertices this kernel cannot name: their tick visits need the round kernel's scan
-        bool decline = prev2 >= a.dense || S.hold0 > (f.hold_v != kNoPeer ? 1 : 0);
-        const bool list = prev2 < a.wl_thr && !S.red[0][1];
-        const uint32_t hg = f.hold_v != kNoPeer ? f.hold_v >> kGroupShift : kNoPeer;
-        const uint32_t ng = (a.n + (1u << kGroupShift) - 1) >> kGroupShift;
-        const uint32_t nw = (ng + 3) >> 2;
-        const uint32_t* pw = reinterpret_cast<const uint32_t*>(a.pend_cur);
-        if (!decline && !list) {                       // count the flagged groups first
-            uint32_t k = 0;
-            for (uint32_t i = t; i < nw; i += kFrBlock) {
-                const uint32_t x = pw[i];
-                for (uint32_t b = 0; b < 4; b++) k += (4 * i + b < ng && ((x >> (8 * b)) & 0xFFu)) ? 1u : 0u;
-            }
-            if (k) atomicAdd(&S.nfr[1], k);
-            __syncthreads();
-        }
-        stamp(0, 1);
-        const uint32_t groups = list ? S.wl_off[64] : S.nfr[1];
-        if (f.prof && t == 0) f.prof[6] = list ? 1u : 2u;
-        decline |= 8ull * groups + 1 > kFrCap;
-        if (decline) {                                 // uniform: the round kernels run every round
-            if (t == 0) *f.done = 0;
-            return;
-        }
-        if (list) {
-            const uint32_t total = S.wl_off[64];
-            for (uint32_t idx = t; idx < total; idx += kFrBlock) {
-                uint32_t lo = 0, hi = 64;              // shard: wl_off[lo] <= idx < wl_off[lo + 1]
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (S.wl_off[mid] <= idx) lo = mid; else hi = mid;
-                }
-                const uint32_t g = a.wl_cur[size_t(lo) * a.wl_cap + (idx - S.wl_off[lo])];
-                a.pend_cur[g] = 0;
-                if (g == hg) S.found = 1;
-                fr_push_group(a, S, 0, g);
-            }
-        } else {
-            for (uint32_t i = t; i < nw; i += kFrBlock) {
-                const uint32_t x = pw[i];
-                if (!x) continue;
-                for (uint32_t b = 0; b < 4; b++) {
-                    const uint32_t g = 4 * i + b;
-                    if (g >= ng || !((x >> (8 * b)) & 0xFFu)) continue;
-                    a.pend_cur[g] = 0;
-                    if (g == hg) S.found = 1;
-                    fr_push_group(a, S, 0, g);
-                }
-            }
-        }
-        __syncthreads();
-        if (t == 0 && f.hold_v != kNoPeer) {          // the holding origin: due on a tick round
-            f.hl[0] = f.hold_v;
-            S.nhl = 1;
-            if (a.tick && !S.found) fr_append(S, 0, f.hold_v >> 1);
-        }
-        S.nfr[1] = 0;                                  // (every thread read its count before the barrier)
-        __syncthreads();
-        stamp(0, 2);
-    }
-    int H = S.hold0;                                   // row holders when round i starts
-    uint32_t cur = 0, ran = 0;
-    for (uint32_t i = 0; i < f.k; i++) {
-        const PtArgs& a = args[i];
-        const uint32_t nxt = cur ^ 1u;
-        const uint32_t nf = min(S.nfr[cur], kFrCap);
-        __syncthreads();                               // nf read everywhere before the counters restart
-        if (t == 0) {
-            S.nfr[nxt] = 0;
-            a.mcnt[kMcntHold + a.m_s] = uint32_t(H);   // round_counts' ring, as its block 0 would
-            a.mcnt[kMcntHoldD + a.m_z] = 0u;
-        }
-        if (t < 64) {
-            a.mcnt[a.m_z * 64 + t] = 0u;
-            a.wlcnt[a.m_z * 64 + t] = 0u;
-        }
-        __syncthreads();
-        stamp(i + 1, 0);
-        Ctr c;
-        c.zero();
-        const uint32_t W = a.ell;
-        const bool due_any = a.tick && H > 0;
-        const bool uniq = i == 0;                      // the entry lists each pair once; later lists may repeat
-        for (uint32_t j = t; j < nf; j += kFrBlock) {
-            const uint32_t p = S.lst[cur][j];
-            if (p == kNoPeer) continue;
-            const uint32_t v0 = 2 * p;
-            const bool has1 = v0 + 1 < a.n;
-            // the claim and every load of both vertices in one round trip
-            const uint32_t bit = fr_bit(p);
-            const uint32_t old = uniq ? bit : atomicAnd(fr_word(a.pend_cur, p), ~bit);
-            uint32_t w0[kCap], w1[kCap], k0[kCap], k1[kCap];
-#pragma unroll
-            for (uint32_t s = 0; s < kCap; s++) {
-                w0[s] = s < W ? ld_fresh(a.in_cur + size_t(v0) * W + s) : 0u;
-                w1[s] = (has1 && s < W) ? ld_fresh(a.in_cur + size_t(v0 + 1) * W + s) : 0u;
-                k0[s] = s < W ? a.ecol[size_t(v0) * W + s] : kNoPeer;
-                k1[s] = (has1 && s < W) ? a.ecol[size_t(v0 + 1) * W + s] : kNoPeer;
-            }
-            const u32x4_t q0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.vs) + v0);
-            const u32x4_t q1 = has1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.vs) + v0 + 1)
-                                    : u32x4_t{0u, 0u, 0u, 0u};
-            const uint32_t aw = a.alive[(a.v_lo + v0) >> 5];   // both vertices: one 32-vertex word
-            const uint2 mb = *reinterpret_cast<const uint2*>(a.memb + v0);   // (memb has n + 1 words at least)
-            const bool d0 = due_any && ld_fresh(a.ost + v0) != 0;
-            const bool d1 = due_any && has1 && ld_fresh(a.ost + v0 + 1) != 0;
-#ifdef PT_FR_STAMPS
-            if (j == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stamp(i + 1, 5);
-            }
-#endif
-            if (!(old & bit)) continue;                // another entry of this pair ran it
-#pragma unroll
-            for (uint32_t s = 0; s < kCap; s++) {
-                if (!live_word(w0[s], a.ctag)) w0[s] = 0u;
-                if (!live_word(w1[s], a.ctag)) w1[s] = 0u;
-            }
-            if (fr_vertex<kFault, kCap>(a, S, nxt, v0, w0, d0, make_uint4(q0.x, q0.y, q0.z, q0.w), aw, k0, mb.x, c) > 0) {
-                const uint32_t k = atomicAdd(&S.nhl, 1u);
-                if (k < f.hcap) f.hl[k] = v0;
-            }
-#ifdef PT_FR_STAMPS
-            if (j == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stamp(i + 1, 6);
-            }
-#endif
-            if (has1 &&
-                fr_vertex<kFault, kCap>(a, S, nxt, v0 + 1, w1, d1, make_uint4(q1.x, q1.y, q1.z, q1.w), aw, k1, mb.y, c) > 0) {
-                const uint32_t k = atomicAdd(&S.nhl, 1u);
-                if (k < f.hcap) f.hl[k] = v0 + 1;
-            }
-#ifdef PT_FR_STAMPS
-            if (j == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stamp(i + 1, 7);
-            }
-#endif
-        }
-        __syncthreads();
-        stamp(i + 1, 1);
-        // rows due next round: the holders are claimed like receivers
-        if (i + 1 < f.k && args[i + 1].tick && S.nhl) {
-            const uint32_t nh = min(S.nhl, f.hcap);
-            for (uint32_t j = t; j < nh; j += kFrBlock) {
-                const uint32_t v = ld_fresh(&f.hl[j]);
-                if (ld_fresh(a.ost + v)) {
-                    atomicOr(fr_word(a.pend_nxt, v >> 1), fr_bit(v >> 1));
-                    fr_append(S, nxt, v >> 1);
-                }
-            }
-            __syncthreads();
-        }
-        stamp(i + 1, 2);
-        // this round's counters into its stats row (shard 0), its count and holder change into the rings
-#pragma unroll
-        for (int q = 1; q < kNStat; q++) {
-            const uint32_t x = uint32_t(c.get(q));     // per-thread values fit 32 bits; sums are taken in 64
-            const uint32_t y = q == S_OVERFLOW ? __ockl_wfred_or_u32(x) : __ockl_wfred_add_u32(x);
-            if (lane == 0) S.red[wv][q] = y;
-        }
-        __syncthreads();
-        if (t >= 1 && t < (uint32_t)kNStat) {
-            unsigned long long s = 0;
-            if (t == S_OVERFLOW) {
-                for (uint32_t w = 0; w < kFrWaves; w++) s |= S.red[w][t];
-            } else if (t == S_OST_DELTA || t == S_LIVE_DELTA) {   // two's complement changes
-                long long d = 0;
-                for (uint32_t w = 0; w < kFrWaves; w++) d += int32_t(S.red[w][t]);
-                s = (unsigned long long)d;
-            } else {
-                for (uint32_t w = 0; w < kFrWaves; w++) s += S.red[w][t];
-            }
-            if (s) a.stats[t] = s;                     // the host zeroed the row; no round kernel writes it
-            if (t == S_OST_DELTA) S.hd = int(s);
-        }
-        if (t == 0) {
-            unsigned long long m = 0;
-            for (int q = 1; q <= 5; q++)
-                for (uint32_t w = 0; w < kFrWaves; w++) m += S.red[w][q];
-            if (m) atomicAdd(&a.mcnt[a.m_w * 64], uint32_t(m));
-        }
-        __syncthreads();
-        const int hd = S.hd;
-        if (t == 0 && hd) {
-            atomicAdd(a.ost_total, hd);
-            atomicAdd(reinterpret_cast<int*>(a.mcnt + kMcntHoldD + a.m_w), hd);
-        }
-        H += hd;
-        ran = i + 1;
-        stamp(i + 1, 3);
-        if (f.prof && t == 0) f.prof[kFrProf * (i + 1) + 4] = nf;
-        const uint32_t next = S.nfr[nxt];
-        if (i + 1 == f.k || next > f.thr || S.nhl > f.hcap) {   // uniform: the last round run
-            // its receivers' groups as the worklist of the round that reads them (one entry per group:
-            // f.gtag[g] takes this launch's serial once); more entries than the LDS list holds -> the
-            // count says "overflowed" and the reader takes the flags
-            if (t == 0) S.ngl = 0;
-            __syncthreads();
-            const bool full = next > kFrCap;
-            if (!full)
-                for (uint32_t j = t; j < next; j += kFrBlock) {
-                    const uint32_t g = S.lst[nxt][j] >> 3;
-                    if (atomicExch(&f.gtag[g], f.serial) != f.serial) {
-                        const uint32_t k = atomicAdd(&S.ngl, 1u);
-                        if ((k >> 6) < a.wl_cap) a.wl_nxt[size_t(k & 63u) * a.wl_cap + (k >> 6)] = g;
-                    }
-                }
-            __syncthreads();
-            if (t < 64) {
-                const uint32_t ngl = S.ngl;
-                a.wlcnt[a.m_w * 64 + t] = full ? a.wl_cap + 1u : (ngl >> 6) + (t < (ngl & 63u) ? 1u : 0u);
-            }
-            break;
-        }
-        cur = nxt;
-    }
-    if (t == 0) *f.done = ran;
-    if (f.prof && t == 0) {
-        f.prof[3] = __builtin_amdgcn_s_memtime();
-        f.prof[4] = __builtin_amdgcn_s_memrealtime();
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1819,6 +1379,7 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
                 const uint32_t pos = base[cb] + atomicAdd(&hist[cb], 1u);
                 if (pos < a.csub[cb * kCoarseShards + sh + 1]) a.rec_c[pos] = make_uint2(a.rev[rs + s], w);
                 else c.overflow |= 8u;
+                c.words++;                            // one record per word
             }
             if (sent) {
                 c.senders++;
@@ -1847,11 +1408,12 @@ __global__ void pt_origin_kernel(PtArgs a) {
     unsigned long long add_live = 0, flags = 0;
     if (outst) flags |= 4u;
     const uint32_t outst0 = outst;
-    uint32_t nmsg = 0;
+    uint32_t nmsg = 0, nword = 0;
     for (uint32_t s = 0; s < deg; s++) {
         const uint32_t b = 1u << s;
         const uint32_t e = rs + s;
         if (eager & b) {
+            nword += omitted(a, e) ? 0u : 1u;
             if (omitted(a, e)) {
                 // sent and lost
             } else if (a.rec_c) {                    // binned: a record for the next route
@@ -1879,6 +1441,7 @@ __global__ void pt_origin_kernel(PtArgs a) {
     }
     if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
     if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);
+    if (nword) atomicAdd(&a.stats[S_WORDS], (unsigned long long)nword);
     if (nmsg && a.mcnt) atomicAdd(&a.mcnt[a.m_s * 64], nmsg);   // read by the next round
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
 }
@@ -2201,16 +1764,6 @@ hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_
         hipLaunchKernelGGL(pt_round_lanes_kernel<true>, grid, dim3(kBlock), 0, s, d_args);
     else
         hipLaunchKernelGGL(pt_round_lanes_kernel<false>, grid, dim3(kBlock), 0, s, d_args);
-    return hipGetLastError();
-}
-
-hipError_t launch_pt_frontier(const PtArgs* d_args, const PtArgs& a0, const FrArgs& f, hipStream_t s) {
-    if (!a0.ell || a0.ell > kEllMax || a0.dly || !a0.mcnt || !a0.wl_nxt) return hipErrorInvalidValue;
-    const bool x = a0.omit != nullptr;
-    const auto k = a0.ell <= 4 ? (x ? pt_frontier_kernel<true, 4> : pt_frontier_kernel<false, 4>)
-                 : a0.ell <= 6 ? (x ? pt_frontier_kernel<true, 6> : pt_frontier_kernel<false, 6>)
-                               : (x ? pt_frontier_kernel<true, 8> : pt_frontier_kernel<false, 8>);
-    hipLaunchKernelGGL(k, dim3(1), dim3(kFrBlock), 0, s, d_args, f);
     return hipGetLastError();
 }
 

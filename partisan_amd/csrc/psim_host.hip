@@ -101,23 +101,6 @@ struct psim_handle {
     uint32_t wl_gpc = 0;                     // listed groups per ELL chunk, 0: spread (PSIM_WL_GPC A/B knob)
     uint32_t ell_grid = 0;                   // grid of the ELL round kernel (resident workgroups)
     hipEvent_t ev[2 * kChunk] = {};
-    // frontier kernel (plumtree.hip pt_frontier_kernel): frontier lists, holder
-    // list, rounds-run word (device, allocated on first use) and its mirror
-    struct Fr {
-        uint32_t* buf = nullptr;        // [hcap] holders, [1] rounds run, [groups] worklist dedup tags
-        uint32_t* h_done = nullptr;     // pinned
-        unsigned long long* prof = nullptr;   // PSIM_FR_PROFILE: phase stamps (device), printed per chunk
-        uint32_t hcap = 0, thr = 0, serial = 0, ngrp = 0;
-        bool off = false;               // not PSIM_FRONTIER=1 (A/B)
-        hipEvent_t ev[2] = {};
-        // a broadcast that left only the origin's words (and maybe the origin's
-        // rows) on its lane: the next chunk of that lane may skip the round
-        // kernels of its first rounds (drive())
-        uint64_t bcast = 0, fresh_bcast = ~0ull, fresh_round = 0;
-        int fresh_lane = -1;
-        uint32_t hold_v = kNoPeer;
-        uint64_t rounds = 0, chunks = 0;   // rounds run by it / chunks it was launched for (psim_get_timing)
-    } fr;
 
     uint32_t par = 0;          // inbox buffer the next round reads
     uint64_t round = 0;        // rounds completed (lazy-tick schedule)
@@ -156,11 +139,10 @@ struct psim_handle {
         uint32_t par = 0, serial = 0, root = 0;
         bool have_root = false;
         int64_t ost_cnt = 0, live_rows = 0;
-        uint64_t inflight = 0, last_use = 0, scrub = 0;
+        uint64_t inflight = 0, scrub = 0;
     };
     std::vector<Lane> lanes;
     int cur_lane = 0;
-    uint64_t use_clock = 0;
     void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
     size_t scratch_cap = 0;
 
@@ -246,9 +228,6 @@ void save_lane(psim_handle* h);
 void load_lane(psim_handle* h, int j);
 
 void free_graph(psim_handle* h) {
-    if (h->fr.buf) (void)hipFree(h->fr.buf);      // sized by the overlay: fr_ready reallocates
-    h->fr.buf = nullptr;
-    h->fr.fresh_lane = -1;
     if (!h->lanes.empty()) {
         swap_lane(h, 0);
         for (size_t j = 1; j < h->lanes.size(); j++) {
@@ -700,8 +679,13 @@ uint64_t add_due(uint64_t* due, uint64_t R, const unsigned long long* hist) {
 }
 
 // Focus the lane of heartbeat root `root`; with `create`, give a new root a
-// lane (a fresh one while fewer than kMaxLanes exist, else the least recently
-// used quiescent lane, whose root's per-root sets are then forgotten).
+// lane while fewer than kMaxLanes hold a root.  A lane keeps its root's
+// per-root eager / lazy sets and the backend's timestamps for that origin
+// (partisan_plumtree_broadcast.erl:1240-1248, 1278-1282; backend :400-417)
+// for the life of the handle: a 17th root is PSIM_ENOSPC -- reusing a
+// quiescent lane would silently forget those sets.  Handles
+// created with psim_config.max_roots > 16 keep every root in the forest
+// (forest.hip) instead.
 int focus_root(psim_handle* h, uint32_t root, bool create) {
     save_lane(h);
     auto& L = h->lanes;
@@ -736,12 +720,9 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
         pick = (int)L.size() - 1;
         fresh = true;
     }
-    if (pick < 0) {                                 // evict the least recently used quiescent lane
-        for (int j = 0; j < (int)L.size(); j++)
-            if (lane_quiescent(h, L[j]) && (pick < 0 || L[j].last_use < L[pick].last_use)) pick = j;
-        if (pick < 0) return fail(h, PSIM_EBUSY, "all %d heartbeat lanes are in flight", kMaxLanes);
-        fresh = true;
-    }
+    if (pick < 0)
+        return fail(h, PSIM_ENOSPC, "root %u: all %d heartbeat lanes hold a root's trees (psim_config.max_roots "
+                                    "keeps more)", root, kMaxLanes);
     if (fresh) {                                    // start_link/0 state for this lane
         auto& l = L[pick];
         const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
@@ -772,73 +753,7 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
     } else {
         load_lane(h, pick);
     }
-    L[pick].last_use = ++h->use_clock;
     return PSIM_OK;
-}
-
-// ---- frontier kernel (plumtree.hip pt_frontier_kernel) ---------------------
-// Its buffers on first use.  PSIM_FRONTIER=1 switches it on (A/B),
-// PSIM_FR_THR sets the frontier (vertex pairs) up to which it keeps running.
-int fr_ready(psim_handle* h) {
-    auto& f = h->fr;
-    if (f.buf || f.off) return PSIM_OK;
-    // opt-in until it measures faster than the round kernels' sparse rounds
-    const char* on = getenv("PSIM_FRONTIER");
-    if (!on || strcmp(on, "1") != 0) {
-        f.off = true;
-        return PSIM_OK;
-    }
-    f.hcap = 1u << 16;
-    f.thr = 8192;
-    if (const char* e = getenv("PSIM_FR_THR")) f.thr = std::min<uint32_t>(kFrCap, uint32_t(strtoul(e, nullptr, 10)));
-    f.ngrp = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
-    if (!alloc_zero((void**)&f.buf, (size_t(f.hcap) + 1 + f.ngrp) * sizeof(uint32_t)))
-        return fail(h, PSIM_ENOMEM, "frontier kernel buffers");
-    if (!f.h_done) HIPCHK(h, hipHostMalloc((void**)&f.h_done, sizeof(uint32_t)));
-    if (!f.prof && getenv("PSIM_FR_PROFILE")) {
-        HIPCHK(h, hipMalloc((void**)&f.prof, kFrProf * (kChunk + 1) * 8));
-        HIPCHK(h, hipMemset(f.prof, 0, kFrProf * (kChunk + 1) * 8));
-    }
-    for (auto& e : f.ev)
-        if (!e) HIPCHK(h, hipEventCreate(&e));
-    return PSIM_OK;
-}
-
-// Whether the focused lane's next chunk starts in the frontier kernel: -1 no;
-// else the number P of leading rounds it is SURE to run (their round kernels
-// are not launched; the later ones are, and return at once for the rounds it
-// did run).  P > 0 only right after a broadcast on this lane, when the only
-// words in flight are the origin's M0 and at most the origin holds rows:
-// round i's frontier then has at most `pairs` entries -- 8 M0 + 1 for the
-// first (listed groups, the origin), and after a round with `recv`
-// receivers and H holders at most D (recv + H) words (D = row width) to as
-// many new receivers, plus the holders claimed for the next tick -- and the
-// kernel only stops once a frontier exceeds f.thr pairs.
-int fr_plan(psim_handle* h, uint32_t k, uint32_t& hold_v) {
-    const auto& f = h->fr;
-    hold_v = kNoPeer;
-    if (f.off || !f.buf || f.ngrp != ((h->n + (1u << kGroupShift) - 1) >> kGroupShift) || !h->ell || h->ell > kEllMax || h->dly || h->bin.rec_c || h->sh.world != 1 || h->win ||
-        !h->wl_cap)
-        return -1;
-    const uint64_t M0 = h->inflight;
-    const bool fresh = f.fresh_bcast == f.bcast && f.fresh_round == h->round && f.fresh_lane == h->cur_lane;
-    if (h->ost_cnt == 1 && fresh && f.hold_v != kNoPeer) hold_v = f.hold_v;
-    else if (h->ost_cnt != 0) return -1;
-    if (M0 == 0 || M0 > f.thr || 8 * M0 + 1 > kFrCap) return -1;
-    if (!fresh) return 0;
-    const uint64_t D = h->ell;
-    uint64_t recv = M0, H = uint64_t(h->ost_cnt), hl = H, pairs = 8 * M0 + 1;
-    uint32_t P = 0;
-    for (uint32_t i = 0; i < k; i++) {
-        if (i > 0 && (pairs > f.thr || hl > f.hcap)) break;
-        P = i + 1;
-        const uint64_t words = D * (recv + H);
-        H += recv;
-        hl += recv;
-        pairs = words + H;
-        recv = words;
-    }
-    return int(P);
 }
 
 // Launch up to max_rounds rounds in chunks; with stop_q, stop after the first
@@ -904,52 +819,6 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             if (e != hipSuccess) return e;
             return launch_win_round(a, h->w_cnt, h->w_cur, h->w_bsum, h->stream);
         };
-        // one static lane: its first rounds may run in the frontier kernel
-        int fr_first = -1;
-        uint32_t fr_hold = kNoPeer;
-        if (A == 1 && !any_win) {
-            load_lane(h, act[0]);
-            const int rc = fr_ready(h);
-            if (rc) return rc;
-            fr_first = fr_plan(h, k, fr_hold);
-        }
-        uint32_t* fr_done = fr_first >= 0 ? h->fr.buf + h->fr.hcap : nullptr;
-        if (fr_first >= 0) {
-            for (uint32_t i = 0; i < k; i++) {
-                const uint32_t tick = ((h->round + i + 1) % L) == 0;
-                PtArgs a = lane_args(0, i, tick);
-                a.fr_done = fr_done;
-                a.fr_idx = i;
-                h->h_lane_args[i] = a;
-            }
-            HIPCHK(h, hipMemcpyAsync(h->lane_args, h->h_lane_args, k * sizeof(PtArgs), hipMemcpyHostToDevice,
-                                     h->stream));
-            FrArgs f{};
-            f.k = k;
-            f.thr = h->fr.thr;
-            f.hl = h->fr.buf;
-            f.hcap = h->fr.hcap;
-            f.hold_v = fr_hold;
-            f.done = fr_done;
-            f.gtag = h->fr.buf + h->fr.hcap + 1;
-            if (++h->fr.serial == 0) {             // the tags could alias after 2^32 launches: start over
-                HIPCHK(h, hipMemsetAsync(f.gtag, 0, size_t(h->fr.ngrp) * 4, h->stream));
-                h->fr.serial = 1;
-            }
-            f.serial = h->fr.serial;
-            f.prof = h->fr.prof;
-            HIPCHK(h, hipEventRecord(per_round ? h->fr.ev[0] : h->ev[0], h->stream));
-            HIPCHK(h, launch_pt_frontier(h->lane_args, h->h_lane_args[0], f, h->stream));
-            if (per_round) HIPCHK(h, hipEventRecord(h->fr.ev[1], h->stream));
-            for (uint32_t i = uint32_t(fr_first); i < k; i++) {
-                if (per_round) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-                HIPCHK(h, launch_pt_round(h->h_lane_args[i], h->stream));
-                if (per_round) HIPCHK(h, hipEventRecord(h->ev[2 * i + 1], h->stream));
-            }
-            if (!per_round) HIPCHK(h, hipEventRecord(h->ev[1], h->stream));
-            HIPCHK(h, hipMemcpyAsync(h->fr.h_done, fr_done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-        } else
-#ifndef PT_LANE_LAUNCHES
         if (A > 1 && !any_win) {
             // several lanes: one launch per round over all of them (blockIdx.y = lane)
             for (uint32_t i = 0; i < k; i++) {
@@ -963,16 +832,16 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
                 HIPCHK(h, launch_pt_round_lanes(h->lane_args + i * A, h->h_lane_args[i * A], (uint32_t)A, h->stream));
                 if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
             }
-        } else
-#endif
-        for (uint32_t i = 0; i < k; i++) {
-            const uint32_t tick = ((h->round + i + 1) % L) == 0;
-            if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
-            for (size_t q = 0; q < A; q++) {
-                if (h->lanes[act[q]].win) HIPCHK(h, win_round(q, i, tick));
-                else HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
+        } else {
+            for (uint32_t i = 0; i < k; i++) {
+                const uint32_t tick = ((h->round + i + 1) % L) == 0;
+                if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+                for (size_t q = 0; q < A; q++) {
+                    if (h->lanes[act[q]].win) HIPCHK(h, win_round(q, i, tick));
+                    else HIPCHK(h, launch_pt_round(lane_args(q, i, tick), h->stream));
+                }
+                if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
             }
-            if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
         }
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
@@ -980,44 +849,9 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         HIPCHK(h, hipStreamSynchronize(h->stream));
         float chunk_ms = 0.f;
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
-        uint32_t fr_ran = 0;
-        float fr_ms = 0.f;
-        if (fr_first >= 0) {
-            fr_ran = *h->fr.h_done;
-            if (fr_ran < uint32_t(fr_first) || fr_ran > k)
-                return fail(h, PSIM_EHIP, "frontier kernel ran %u rounds, %d were left to it alone", fr_ran, fr_first);
-            if (per_round) HIPCHK(h, hipEventElapsedTime(&fr_ms, h->fr.ev[0], h->fr.ev[1]));
-            if (h->fr.prof) {                   // diagnostic: phase times in us from the kernel's stamps
-                unsigned long long p[kFrProf * (kChunk + 1)];
-                HIPCHK(h, hipMemcpy(p, h->fr.prof, sizeof p, hipMemcpyDeviceToHost));
-                fprintf(stderr, "frontier: ran %u, first %d, mode %llu, entry %.2f %.2f us, shader clock %.0f MHz\n",
-                        fr_ran, fr_first, p[6], (p[1] - p[0]) * 0.01, (p[2] - p[0]) * 0.01,
-                        double(p[3] - p[7]) / (double(p[4] - p[0]) * 0.01));
-                for (uint32_t i = 1; i <= fr_ran; i++) {
-                    const unsigned long long* q = p + kFrProf * i;
-                    fprintf(stderr, "  round %u: pairs %llu  start %.2f  process %.2f  claims %.2f  flush %.2f us", i,
-                            q[4], (q[0] - p[0]) * 0.01, (q[1] - q[0]) * 0.01, (q[2] - q[1]) * 0.01, (q[3] - q[2]) * 0.01);
-                    if (q[5] > q[0] && q[7] > q[6] && q[6] > q[5])   // PT_FR_STAMPS builds: thread 0's first entry
-                        fprintf(stderr, "  [t0: loads %.2f  v0 %.2f  v1 %.2f]", (q[5] - q[0]) * 0.01, (q[6] - q[5]) * 0.01,
-                                (q[7] - q[6]) * 0.01);
-                    fprintf(stderr, "\n");
-                }
-            }
-            h->fr.rounds += fr_ran;
-            h->fr.chunks++;
-        }
         for (uint32_t i = 0; i < k; i++) {
             float ms = chunk_ms / float(k);
-            if (per_round) {
-                // per-round events: the frontier kernel's time split over its rounds, plus
-                // the round kernel's own launch (a no-op for a round the frontier ran)
-                ms = i < fr_ran ? fr_ms / float(fr_ran) : 0.f;
-                if (fr_first < 0 || i >= uint32_t(fr_first)) {
-                    float e = 0.f;
-                    HIPCHK(h, hipEventElapsedTime(&e, h->ev[2 * i], h->ev[2 * i + 1]));
-                    ms += e;
-                }
-            }
+            if (per_round) HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
             unsigned long long tot[kNStat] = {0};
             uint64_t msgs = 0;
             for (size_t q = 0; q < A; q++) {
@@ -1061,6 +895,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
                 for (const auto& l : h->lanes) ov += l.ost_cnt;
                 o.outstanding_vertices = (uint64_t)ov;
                 o.algo_bytes = 16ull * h->n * A + 8ull * tot[S_SENDERS] + 4ull * tot[S_DEGSUM] + 32ull * msgs;
+                o.words_stored = tot[S_WORDS];
                 o.kernel_ms = ms;
             }
             ran++;
@@ -1114,6 +949,7 @@ const char* psim_strerror(int code) {
     case PSIM_EOVERFLOW: return "fixed-capacity structure overflowed";
     case PSIM_EBUSY: return "previous broadcast not quiescent";
     case PSIM_ENODEV: return "no usable HIP device";
+    case PSIM_ENOSPC: return "no slot left for another heartbeat root";
     default: return "unknown error";
     }
 }
@@ -1189,11 +1025,6 @@ int psim_destroy(psim_handle* h) {
     if (h->ost_total_base) (void)hipFree(h->ost_total_base);
     if (h->mcnt_base) (void)hipFree(h->mcnt_base);
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);
-    if (h->fr.buf) (void)hipFree(h->fr.buf);
-    if (h->fr.h_done) (void)hipHostFree(h->fr.h_done);
-    if (h->fr.prof) (void)hipFree(h->fr.prof);
-    for (auto& e : h->fr.ev)
-        if (e) (void)hipEventDestroy(e);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : h->sh.rev_)
@@ -1690,14 +1521,6 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
             return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat; "
                         "window lanes: 32: > 32 rows, 64: > 4 timestamp intervals)", r[S_OVERFLOW]);
     }
-    h->fr.bcast++;
-    if (!h->win && !h->dly && lr < h->n && h->sh.world == 1 && h->ost_cnt == 0) {
-        // the frontier kernel may plan on this lane's next chunk (fr_plan)
-        h->fr.fresh_bcast = h->fr.bcast;
-        h->fr.fresh_round = h->round;
-        h->fr.fresh_lane = h->lanes.empty() ? 0 : h->cur_lane;
-        h->fr.hold_v = r[S_OST_DELTA] == 1 ? lr : kNoPeer;
-    }
     h->ost_cnt += (int64_t)r[S_OST_DELTA];
     h->live_rows += (int64_t)r[S_LIVE_DELTA];
     h->inflight = (h->win ? h->inflight : 0) + r[PSIM_MSG_BROADCAST];
@@ -1966,6 +1789,7 @@ int psim_shard_collect(psim_handle* h, psim_round_stats* out, size_t cap, uint32
             o.sender_degree_sum = r[S_DEGSUM];
             o.outstanding_vertices = (uint64_t)h->ost_cnt;
             o.algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+            o.words_stored = r[S_WORDS];
             o.kernel_ms = ms;
         }
         if (local_live && i < cap) local_live[i] = h->live_rows;
@@ -2263,6 +2087,7 @@ int shard_drive_lanes(psim_handle* h, uint32_t max_rounds, psim_round_stats* out
             uint64_t lm = 0;
             for (int t = 1; t <= 5; t++) lm += loc[t];
             o.algo_bytes = 16ull * h->n * A + 8ull * loc[S_SENDERS] + 4ull * loc[S_DEGSUM] + 32ull * lm;
+            o.words_stored = loc[S_WORDS];
             o.kernel_ms = ms;
         }
         if (xs) {
@@ -2424,6 +2249,7 @@ int shard_drive_fast(psim_handle* h, uint32_t max_rounds, psim_round_stats* out,
                 o.active = st[j].active;                        // this rank's
                 o.outstanding_vertices = (uint64_t)f[9];
                 o.algo_bytes = st[j].algo_bytes;                // this rank's (its kernel's bytes)
+                o.words_stored = st[j].words_stored;            // this rank's
                 o.kernel_ms = kms;
             }
             ran++;
@@ -2946,13 +2772,6 @@ int psim_get_timing(const psim_handle* h, double* round_kernel_ms, uint64_t* rou
     if (!h) return PSIM_EINVAL;
     if (round_kernel_ms) *round_kernel_ms = h->kernel_ms_total;
     if (rounds) *rounds = h->rounds_total;
-    return PSIM_OK;
-}
-
-int psim_get_frontier(const psim_handle* h, uint64_t* rounds, uint64_t* launches) {
-    if (!h) return PSIM_EINVAL;
-    if (rounds) *rounds = h->fr.rounds;
-    if (launches) *launches = h->fr.chunks;
     return PSIM_OK;
 }
 

@@ -75,10 +75,7 @@ constexpr size_t kMcntLane = 520;
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard
-#ifndef PT_GROUP_SHIFT
-#define PT_GROUP_SHIFT 4
-#endif
-constexpr int kGroupShift = PT_GROUP_SHIFT;   // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
+constexpr int kGroupShift = 4;       // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
 static_assert(kGroupShift >= 2 && kGroupShift <= 8, "a group spans whole 4-vertex thread quads");
 constexpr uint32_t kChunkV = 1024;   // vertices owned by one round-kernel workgroup
 // binned engine (single GPU): messages travel as {receiver
@@ -99,6 +96,7 @@ enum Stat : int {
     S_OST_DELTA = 10,   // change in #vertices with outstanding rows (two's complement)
     S_LIVE_DELTA = 11,  // change in #outstanding rows to live peers (two's complement)
     S_OVERFLOW = 12,    // bit0: per-edge FIFO > 4 ; bit1: Round > 4095 ; bit2: rows of an older heartbeat
+    S_WORDS = 13,       // inbox words stored (random 4-byte stores; omitted words are not stored)
 };
 
 // Slot-scatter inbox word (one per receiver slot):
@@ -171,10 +169,6 @@ struct PtArgs {
     uint32_t ell_grid;                     // ELL kernel grid = resident workgroups (0: one per chunk)
     uint32_t force_flags;                  // this round writes group flags whatever its count (the last round
                                            // of a sharded psim_shard_step: readers without counts come next)
-    // frontier kernel (FrArgs): the rounds it ran of this chunk; a round kernel
-    // whose index fr_idx is below that returns at once (null: not launched)
-    const uint32_t* fr_done;
-    uint32_t fr_idx;
     unsigned long long* __restrict__ stats;  // [kStatShards][kNStat]
     uint32_t tick;                         // lazy tick fires at the end of this round
     uint32_t mono8;                        // current heartbeat Monotonic (low 8 bits)
@@ -208,30 +202,6 @@ struct PtArgs {
     uint32_t fv_shift, cv_shift;           // fine bin = 2^fv_shift vertices, coarse = 2^cv_shift
     uint32_t nf, nc, chunks;               // bins; route chunks per sub-region
 };
-
-// Frontier kernel (plumtree.hip pt_frontier_kernel): ONE
-// workgroup runs the leading sparse rounds of a chunk back to back -- the
-// receivers of a round are kept as a list of vertex pairs claimed in the group
-// flag bytes (bit = pair within the 16-vertex group), so a round costs its
-// few dependent memory round trips and no launch, no cross-workgroup count,
-// no list reservation.  It leaves every round's flags, worklist, counts and
-// holder ring exactly as the round kernel would, so a round kernel can take
-// over after any round.
-constexpr uint32_t kFrBlock = 1024;
-constexpr uint32_t kFrCap = 16384;   // frontier list entries (LDS, two lists)
-struct FrArgs {
-    uint32_t k;                 // rounds of this chunk (their PtArgs on device)
-    uint32_t thr;               // the next round runs here only while its frontier list is <= thr (<= kFrCap)
-    uint32_t* hl;               // vertices that gained outstanding rows in this launch (tick candidates)
-    uint32_t hcap;
-    uint32_t hold_v;            // the one local vertex holding rows at entry (an origin), kNoPeer: none
-    uint32_t* done;             // out: rounds run
-    uint32_t* gtag;             // [groups] worklist dedup of the last round: the serial of the launch that listed g
-    uint32_t serial;            // this launch's (never 0; gtag starts zeroed)
-    unsigned long long* prof;   // diagnostic (PSIM_FR_PROFILE): s_memrealtime stamps per phase, or null
-};
-constexpr uint32_t kFrProf = 8;   // stamps per round (+ kFrProf at entry)
-hipError_t launch_pt_frontier(const PtArgs* d_args, const PtArgs& a0, const FrArgs& f, hipStream_t s);
 
 // Demers rumor mongering + anti-entropy (demers.hip)
 constexpr uint32_t kDmPushCap = 24;   // AE pushes one vertex can receive per tick (Poisson(2) in-degree)

@@ -18,7 +18,8 @@ _u64p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
 
 _ROUND_DTYPE = np.dtype([("sent", np.uint64, 6), ("delivered_new", np.uint64), ("active", np.uint64),
                          ("senders", np.uint64), ("sender_degree_sum", np.uint64),
-                         ("outstanding_vertices", np.uint64), ("algo_bytes", np.uint64), ("kernel_ms", np.float64)])
+                         ("outstanding_vertices", np.uint64), ("algo_bytes", np.uint64), ("kernel_ms", np.float64),
+                         ("words_stored", np.uint64)])
 assert _ROUND_DTYPE.itemsize == C.sizeof(RoundStats)
 
 
@@ -26,17 +27,21 @@ class Simulator:
     """Round-synchronous simulator of Partisan's gossip hot path."""
 
     def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0, rank=0, world=1,
-                 binned=False, csr=False, chunk_timing=False):
+                 binned=False, csr=False, chunk_timing=False, max_roots=0):
         """binned: route Plumtree messages through receiver bins on a single
         GPU instead of scattering receiver-slot words (PSIM_CFG_BINNED; same
         results).  csr: keep CSR slot rows in the slot-scatter
         engine instead of fixed-width ELL rows (PSIM_CFG_CSR; same results).
         chunk_timing: one hipEvent pair per chunk of rounds (PSIM_CFG_CHUNK_TIMING;
-        kernel_ms of a round = the chunk's device time / its rounds)."""
+        kernel_ms of a round = the chunk's device time / its rounds).
+        max_roots: heartbeat roots whose per-root trees the handle keeps
+        (psim_config.max_roots; 0 = 16 lanes).  Above 16 the roots live in one
+        forest launched together; a root beyond max_roots is
+        PSIM_ENOSPC."""
         flags = ((PSIM_CFG_BINNED if binned else 0) | (PSIM_CFG_CSR if csr else 0)
                  | (PSIM_CFG_CHUNK_TIMING if chunk_timing else 0))
         cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
-                     exchange_tick_rounds=exchange_tick_rounds, flags=flags, _reserved=0, seed=seed)
+                     exchange_tick_rounds=exchange_tick_rounds, flags=flags, max_roots=max_roots, seed=seed)
         h = C.c_void_p()
         check(lib().psim_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -248,14 +253,6 @@ class Simulator:
         self._c(lib().psim_get_timing(self._h, C.byref(ms), C.byref(r)))
         return ms.value, r.value
 
-    def frontier_stats(self):
-        """psim_get_frontier: (rounds run by the frontier kernel, chunks it was launched for)."""
-        r = C.c_uint64()
-        k = C.c_uint64()
-        self._c(lib().psim_get_frontier(self._h, C.byref(r), C.byref(k)))
-        return r.value, k.value
-
-    # ---------------------------------------------------------------- helpers
     def mask_to_peers(self, v, mask):
         """Decode a per-vertex slot mask into the sorted list of peer ids."""
         lo = int(self.slot_row_ptr[v])

@@ -425,20 +425,35 @@ def test_multi_root_heartbeats_lockstep():
     sim.close()
 
 
-def test_multi_root_lane_reuse():
-    """More roots than lanes: the least recently used quiescent lane is reused
-    (its root's sets forgotten, as after reset_peers for that root)."""
+def test_multi_root_lanes_full_is_enospc():
+    """More roots than lanes: a 17th root is PSIM_ENOSPC (VERDICT r4 -- the
+    least recently used lane used to be reused silently, forgetting its root's
+    trees); the 16 roots keep their trees and another heartbeat of any of
+    them still runs on its own lane."""
     import partisan_amd as pa
     rp, col = pa.overlay.random_regular(400, 5, 131)
     sim = pa.Simulator()
     sim.load_overlay(rp, col)
-    for root in range(20):
-        sim.broadcast(root)
+    orc = O.Plumtree(rp, col, lazy_tick_rounds=1)
+    monos = {}
+    for root in range(16):
+        monos[root] = sim.broadcast(root)
+        assert monos[root] == orc.heartbeat(root)
         sim.run()
+        orc.run()
         assert sim.delivered().all()
-    sim.focus(19)
-    with pytest.raises(pa.PsimError):
-        sim.focus(0)                 # evicted
+    with pytest.raises(pa.PsimError) as ei:
+        sim.broadcast(16)
+    assert ei.value.name == "PSIM_ENOSPC"
+    monos[0] = sim.broadcast(0)            # root 0's pruned tree, not a fresh flood
+    assert monos[0] == orc.heartbeat(0)
+    lockstep(sim, orc, 0, monos[0])
+    for root in (0, 7, 15):
+        sim.focus(root)
+        eager, lazy, _, _ = sim.plumtree_state()
+        for v in range(0, 400, 13):
+            assert sim.mask_to_peers(v, eager[v]) == orc.peers(v, root)[0], (root, v)
+            assert sim.mask_to_peers(v, lazy[v]) == orc.peers(v, root)[1], (root, v)
     sim.close()
 
 
