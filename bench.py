@@ -10,12 +10,22 @@ value = n_peers * rounds / step time, summed over ranks.  The overlay is
 resident in HBM before the timed region; nothing crosses PCIe inside it
 except the per-chunk 8 KB counter read-back the round driver needs.
 
-Roofline: dominant kernel pt_round_ell_kernel, HBM-bound; achieved = SURVEY
-8(d) algorithmic bytes of the timed rounds / their summed hipEvent durations
+Roofline: dominant kernel pt_round_ell_kernel, HBM-bound.  achieved = the
+algorithmic bytes of the timed rounds / their summed hipEvent durations
 (events on the library's own stream: one pair per 16-round chunk, so the
-average launch includes the dispatch gaps between round kernels); traffic =
-rocprofv3 PMC bytes per launch from profiles/pmc_traffic.json, reported only
-when that profile was taken on the very libpsim.so this run loaded (sha256).
+average launch includes the dispatch gaps between round kernels), with the
+state bytes of the vertices each round TOUCHED (16 B per vertex that
+processed a word or a tick) -- SURVEY 8(d)'s model charges 16 B for all N
+vertices every round, which credits a sparse round with state it never
+reads (1.4x peak in the shortest launch); that figure stays as
+frac_dense_model.  roofline.random_access puts the stored inbox words (one
+random 4-byte store each) against the chip's measured scatter rate, the roof
+the dense rounds actually hit.  roofline.per_round: one more step, untimed,
+with an event pair per round kernel -- each round's bytes, words and
+fractions (and PMC bytes when profiles/pmc_traffic.json has them for this
+build).  traffic = rocprofv3 PMC bytes per launch from
+profiles/pmc_traffic.json, reported only when that profile was taken on the
+very libpsim.so this run loaded (sha256).
 cpu_baseline: the C oracle (a scalar port of the reference modules) running
 one flood of the benchmark's own configuration single-threaded, rank 0 only
 (plus the 1M-peer sample and the 16-process all-core figure beside it).
@@ -37,6 +47,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "simulated peer-rounds/sec + HBM GB/s at 10M-peer plumtree broadcast, 1–8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# random 4-byte stores into a 200 MB inbox, the round-12 shape (27.0M words
+# into 50M slots), measured on MI355X: profiles/r04/experiments/mb_transpose_range.txt
+# ("direct scatter 494 us, 54.7 G words/s"; tools/mb_transpose.hip)
+SCATTER_PEAK_WPS = 54.7e9
+
+
+def touched_bytes(st):
+    """Algorithmic bytes of one round (a numpy record of psim_run) with 16 B
+    of state per vertex the round touched: 16 active + 8 senders + 4 deg-sum
+    + 32 messages (SURVEY 8(d) with the 16 N term replaced)."""
+    msgs = int(st["sent"][1:6].sum())
+    return 16 * int(st["active"]) + 8 * int(st["senders"]) + 4 * int(st["sender_degree_sum"]) + 32 * msgs
 
 
 def parse():
@@ -369,6 +391,7 @@ def main():
 
     algo_bytes = 0
     active_bytes = 0
+    words = 0
     round_ms = 0.0
     rounds_per_step = []
     if sp is not None:
@@ -385,7 +408,8 @@ def main():
             algo_bytes += int(stats["algo_bytes"].sum())
             round_ms += float(stats["kernel_ms"].sum())
             # the same model crediting the state bytes of the vertices a round touched, not of all N
-            active_bytes += int((stats["algo_bytes"] - np.uint64(16 * args.n) + np.uint64(16) * stats["active"]).sum())
+            active_bytes += sum(touched_bytes(x) for x in stats)
+            words += int(stats["words_stored"].sum())
     # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
     barrier(pg)
     t1 = time.perf_counter()
@@ -393,6 +417,13 @@ def main():
         algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
 
     verified = verify(sim, pg, args.n, rounds_per_step)
+    per_round_stats = None
+    if sp is None:
+        # one more step, outside the timed region, with an event pair around
+        # every round kernel: the per-round table of roofline.per_round
+        sim.set_chunk_timing(False)
+        per_round_stats, _ = one_step(sim, root)
+        sim.set_chunk_timing(not args.round_events)
     exchange = None
     counted = sum(rounds_per_step)
     if sp is not None:   # the in-library exchange (psim_shard_run): fabric bytes and device time per step
@@ -415,6 +446,10 @@ def main():
         else:
             kernel_ms_step = chunk_ms
             exchange_ms_step = float(xt.get("exchange_ms", 0.0)) / args.steps
+        comm_world = sp.transport_info()["world"]
+        if args.transport == "nccl" and comm_world != world:
+            # the RCCL communicator inside libpsim must span exactly the launched ranks
+            raise SystemExit(f"bench: libpsim's RCCL communicator has {comm_world} ranks but WORLD_SIZE={world}")
         exchange = {
             "transport": sp.transport,
             # the library's own view of the job (RCCL: ncclCommCount / ncclCommUserRank of its communicator)
@@ -438,13 +473,15 @@ def main():
     # per-launch figures over the rounds up to quiescence (the no-op tail of a
     # step's last chunk is not counted): hipEvent durations of each launch
     avg_launch_ms = round_ms / max(1, counted)
-    achieved_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
+    dense_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
+    touched_gbs = (active_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9 if sp is None else None
 
     # ELL rows (every degree of the whole overlay <= 8) run the sweep kernel
     max_deg = int(max_over_ranks(pg, float(sim.max_degree())))
     kernel = "pt_round_kernel" if (args.csr or max_deg > 8) else "pt_round_ell_kernel"
     if rank == 0:
         traffic = traffic_fetch = traffic_write = None
+        tj = {}
         traffic_note = "no PMC profile for this workload"
         fp = lib_fingerprint()
         try:
@@ -464,6 +501,27 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
         launch_s = avg_launch_ms * 1e-3
+        per_round = None
+        if per_round_stats is not None:
+            pmc_rounds = None
+            if traffic is not None:
+                pmc_rounds = tj.get("per_round")
+            per_round = []
+            for i, x in enumerate(per_round_stats):
+                ms = float(x["kernel_ms"])
+                tb, db, w = touched_bytes(x), int(x["algo_bytes"]), int(x["words_stored"])
+                row = {"round": i + 1, "us": round(ms * 1e3, 2), "messages": int(x["sent"][1:6].sum()),
+                       "words": w, "active": int(x["active"]), "bytes_touched": tb, "bytes_dense_model": db,
+                       "frac": tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None,
+                       "frac_dense_model": db / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None,
+                       "frac_random_access": w / (ms * 1e-3) / SCATTER_PEAK_WPS if ms > 0 else None}
+                if pmc_rounds and i < len(pmc_rounds):
+                    pb = pmc_rounds[i]["fetch"] + pmc_rounds[i]["write"]
+                    row["pmc_bytes"] = pb
+                    row["frac_pmc"] = pb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None
+                per_round.append(row)
+        words_s = (words / (round_ms * 1e-3)) if (sp is None and round_ms > 0) else None
+        achieved_gbs = touched_gbs if touched_gbs is not None else dense_gbs
         out = {
             "metric": METRIC,
             "value": value,
@@ -497,6 +555,20 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
+                "model": ("bytes per launch = 16 B per vertex the round touched + (8 + 4 deg) per sender + "
+                          "32 per message (SURVEY 8(d) with its 16 N term charged only for touched vertices)"
+                          if touched_gbs is not None else "SURVEY 8(d): 16 N + sum(8 + 4 deg) + 32 msgs"),
+                "achieved_dense_model": dense_gbs,
+                "frac_dense_model": dense_gbs / HBM_PEAK_GBS,
+                "random_access": ({"achieved": words_s, "peak": SCATTER_PEAK_WPS, "unit": "words/s",
+                                   "frac": words_s / SCATTER_PEAK_WPS,
+                                   "words_per_step": words / args.steps,
+                                   "peak_source": "profiles/r04/experiments/mb_transpose_range.txt (direct "
+                                                  "random 4-byte scatter, round-12 shape)"}
+                                  if words_s is not None else None),
+                "per_round": per_round,
+                "max_round_frac": max((r["frac"] for r in per_round if r["frac"] is not None), default=None)
+                                  if per_round else None,
                 "traffic": traffic,
                 "traffic_note": traffic_note,
                 # the same launch time against the PMC-measured bytes (tools/pmc_traffic.py): what
@@ -510,12 +582,6 @@ def main():
                 "kernel": kernel,
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "algo_bytes_per_launch": algo_bytes / max(1, counted),
-                # SURVEY 8(d)'s model credits 16 B of state for all N vertices every round; this
-                # variant credits only the vertices the round touched (sparse rounds get no credit
-                # for the vertices they skip)
-                "achieved_active_state": ((active_bytes / max(1, counted)) / launch_s / 1e9) if sp is None else None,
-                "frac_active_state": ((active_bytes / max(1, counted)) / launch_s / 1e9 / HBM_PEAK_GBS)
-                                     if sp is None else None,
                 "lib_sha256": fp,
             },
         }

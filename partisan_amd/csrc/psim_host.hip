@@ -1044,7 +1044,10 @@ int psim_device_info(const psim_handle* h, char* buf, size_t cap) {
     if (!h || !buf || !cap) return PSIM_EINVAL;
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, h->device) != hipSuccess) return PSIM_EHIP;
-    snprintf(buf, cap, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+    // the marketing name is empty on some ROCm installs (the r04 bench line
+    // printed " (gfx950...)"): the arch, CU count and HBM size name the part
+    snprintf(buf, cap, "%s (%s, %d CUs, %.0f GB HBM)", p.name[0] ? p.name : "AMD Instinct GPU", p.gcnArchName,
+             p.multiProcessorCount, double(p.totalGlobalMem) / 1e9);
     return PSIM_OK;
 }
 

@@ -47,12 +47,21 @@ def main():
     counted = a.rounds_per_step * a.steps
     fetch = sum(f) / counted
     write = sum(w) / counted
+    # per round of a step: launch i of every step (the run repeats the same
+    # deterministic flood, so launch k * rounds_per_step + i is round i + 1)
+    per_round = []
+    if len(f) == counted and len(w) == counted:
+        R = a.rounds_per_step
+        for i in range(R):
+            per_round.append({"round": i + 1, "fetch": sum(f[k * R + i] for k in range(a.steps)) / a.steps,
+                              "write": sum(w[k * R + i] for k in range(a.steps)) / a.steps})
     out = {
         "n": a.n, "peers": a.peers, "kernel": a.kernel,
         "launches_profiled": len(f), "counted_launches": counted,
         "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
         "hbm_bytes_per_launch_read_doubled": 2 * fetch + write,
+        "per_round": per_round,
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB*1024, "
                   "summed over all launches of the kernel / counted rounds",
         "lib_sha256": lib_sha,
