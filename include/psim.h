@@ -156,6 +156,14 @@ int  psim_plumtree_restart_backend(psim_handle* h, uint32_t v);
  * sets, per-message ids -- from then until the lane is reused.  Sharded,
  * binned and delay-fault handles keep one heartbeat per root: PSIM_EBUSY. */
 int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
+/* Heartbeats from k roots at once -- backend handle_info(heartbeat) at each
+ * of them, as every node's timer fires (partisan_plumtree_backend.erl:341-368,
+ * 421-428).  monos_out[i] = roots[i]'s id (may be NULL).  On a forest
+ * (max_roots > 16) one origin launch for all of them, all or nothing:
+ * PSIM_ENOSPC when new roots exceed max_roots, PSIM_EBUSY when a root's last
+ * heartbeat is still in flight or holds rows, PSIM_EINVAL on a root listed
+ * twice; otherwise psim_plumtree_broadcast per root, in order. */
+int  psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos_out);
 /* Several roots: on one GPU without PSIM_CFG_BINNED each
  * heartbeat root gets a lane of its own (per-root eager / lazy sets, rows,
  * delivered serials, in-flight words; up to 16 lanes, then the least

@@ -1177,6 +1177,41 @@ __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs
 }
 
 // ---------------------------------------------------------------------------
+// The forest (FoArgs, psim_internal.h): lane L's arguments
+// are lane 0's shifted by L slices -- built in registers from one kernel
+// argument block, so a round over 10^4 roots uploads nothing per lane.
+__device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
+    PtArgs a = f.a;
+    a.vs += lane * f.s_vs;
+    a.in_cur += lane * f.s_in;
+    a.in_nxt += lane * f.s_in;
+    a.pend_cur += lane * f.s_pend;
+    a.pend_nxt += lane * f.s_pend;
+    a.ost += lane * f.s_ost;
+    a.ost_total += 4 * lane;
+    if (a.mcnt) {
+        a.mcnt += size_t(lane) * kMcntLane;
+        if (a.wlcnt) a.wlcnt = a.mcnt + 256;
+    }
+    if (a.wl_cur) a.wl_cur = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_cur) + lane * f.s_pend);
+    if (a.wl_nxt) a.wl_nxt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_nxt) + lane * f.s_pend);
+    const uint2 li = f.info[lane];
+    a.mono8 = li.x;
+    a.root = li.y;
+    return a;
+}
+
+template <bool kFault, uint32_t kCap>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void pt_forest_ell_kernel(FoArgs f) {
+    pt_round_ell_body<kFault, kCap>(fo_lane(f, f.lane0 + blockIdx.y));
+}
+
+template <bool kFault>
+__global__ __launch_bounds__(kBlock) void pt_forest_kernel(FoArgs f) {
+    pt_round_body<kFault>(fo_lane(f, f.lane0 + blockIdx.y));
+}
+
+// ---------------------------------------------------------------------------
 // Binned engine (single GPU).  A round is two launches:
 //   pb_route_kernel: the records emitted last round sit in coarse receiver
 //     bins (2^cv_shift vertices); each workgroup moves <= kRouteK of one
@@ -1394,8 +1429,7 @@ __global__ __launch_bounds__(kBlock) void pb_round_kernel(PtArgs a) {
 // The origin's {broadcast, Id, Payload, Mod} cast (:565-569): eager_push/4
 // and schedule_lazy_push/3 with Round 0, Root = From = the origin; the
 // backend already did add_timestamp (backend :341-368).
-__global__ void pt_origin_kernel(PtArgs a) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ void pt_origin_body(const PtArgs& a) {
     const uint32_t v = a.root;   // local index of the origin (only its owner launches this)
     PtArgs ao = a;               // listed groups count as the round the next round reads as previous
     ao.m_w = a.m_s;
@@ -1444,6 +1478,85 @@ __global__ void pt_origin_kernel(PtArgs a) {
     if (nword) atomicAdd(&a.stats[S_WORDS], (unsigned long long)nword);
     if (nmsg && a.mcnt) atomicAdd(&a.mcnt[a.m_s * 64], nmsg);   // read by the next round
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
+}
+
+__global__ void pt_origin_kernel(PtArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    pt_origin_body(a);
+}
+
+// The forest's origins: one thread per heartbeat, each on its own lane.
+__global__ __launch_bounds__(64) void fo_origin_kernel(FoArgs f, const uint32_t* __restrict__ lanes, uint32_t k) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i < k) pt_origin_body(fo_lane(f, lanes[i]));
+}
+
+// A lane is busy while its last round (count slot `slot`, origins included)
+// sent messages or some vertex holds rows of its heartbeat.
+__global__ __launch_bounds__(64) void fo_busy_kernel(FoArgs f, const uint32_t* __restrict__ lanes, uint32_t k,
+                                                     uint32_t slot, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= k) return;
+    const uint32_t lane = lanes[i];
+    const uint32_t* m = f.a.mcnt + size_t(lane) * kMcntLane + slot * 64;
+    uint32_t msgs = 0;
+    for (int q = 0; q < 64; q++) msgs += m[q];
+    out[i] = (msgs != 0u || f.a.ost_total[4 * lane] != 0) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void fo_seed_kernel(FoArgs f) {
+    const uint32_t lane = blockIdx.x * kBlock + threadIdx.x;
+    if (lane >= f.nl) return;
+    uint32_t* m = f.a.mcnt + size_t(lane) * kMcntLane;
+    m[kMcntHold + f.a.m_r] = uint32_t(f.a.ost_total[4 * lane]);
+    m[kMcntHoldD + f.a.m_s] = 0u;
+}
+
+// (lane, vertex) pairs, flattened: lane i of lanes[] (or lane i itself)
+__global__ __launch_bounds__(kBlock) void fo_renorm_kernel(FoArgs f, const uint32_t* __restrict__ lanes, uint32_t k) {
+    const unsigned long long total = (unsigned long long)k * f.a.n;
+    const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+    for (unsigned long long x = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; x < total; x += stride) {
+        const uint32_t i = uint32_t(x / f.a.n), v = uint32_t(x % f.a.n);
+        const uint32_t lane = lanes ? lanes[i] : i;
+        const uint32_t mono8 = f.info[lane].x;
+        uint4* vs = f.a.vs + lane * f.s_vs;
+        uint4 st = vs[v];
+        uint32_t rseq = (st.w >> 16) & 0xFFu, ep = st.w >> 24;
+        if (rseq != mono8) rseq = (mono8 - 1u) & 0xFFu;
+        if (ep != f.a.epoch8) ep = (f.a.epoch8 - 1u) & 0xFFu;
+        st.w = (st.w & 0xFFFFu) | (rseq << 16) | (ep << 24);
+        vs[v] = st;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fo_count_live_kernel(FoArgs f, unsigned long long* out) {
+    const PtArgs& a = f.a;
+    const unsigned long long total = (unsigned long long)f.nl * a.n;
+    const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+    unsigned long long cnt = 0;
+    for (unsigned long long x = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; x < total; x += stride) {
+        const uint32_t lane = uint32_t(x / a.n), v = uint32_t(x % a.n);
+        if (!a.ost[lane * f.s_ost + v] || !bit_alive(a.alive, a.v_lo + v)) continue;
+        uint32_t m = a.vs[lane * f.s_vs + v].z;
+        const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
+        while (m) {
+            const uint32_t q = __ffs(m) - 1;
+            m &= m - 1;
+            cnt += bit_alive(a.alive, a.col[rs + q]);
+        }
+    }
+    cnt = wave_sum(cnt);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, cnt);
+}
+
+__global__ __launch_bounds__(kBlock) void fo_forget_kernel(FoArgs f, uint32_t v) {
+    const uint32_t lane = blockIdx.x * kBlock + threadIdx.x;
+    if (lane >= f.nl) return;
+    uint4* p = f.a.vs + lane * f.s_vs + v;
+    uint4 st = *p;
+    st.w = (st.w & 0xFF00FFFFu) | (((f.info[lane].x - 1u) & 0xFFu) << 16);
+    *p = st;
 }
 
 // Outstanding rows to live peers, counted densely (after psim_set_alive).
@@ -1764,6 +1877,74 @@ hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_
         hipLaunchKernelGGL(pt_round_lanes_kernel<true>, grid, dim3(kBlock), 0, s, d_args);
     else
         hipLaunchKernelGGL(pt_round_lanes_kernel<false>, grid, dim3(kBlock), 0, s, d_args);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_round(FoArgs f, uint32_t gx, hipStream_t s) {
+    const PtArgs& a0 = f.a;
+    const bool flt = a0.omit || a0.dly;
+    const uint32_t nl = f.nl;
+    for (uint32_t l0 = 0; l0 < nl; l0 += 65535u) {
+        f.lane0 = l0;
+        const uint32_t ny = std::min<uint32_t>(65535u, nl - l0);
+        if (a0.ell) {
+            // resident workgroups spread over the lanes, at least one per lane
+            const uint32_t g = gx ? gx : std::max<uint32_t>(1u, (a0.ell_grid ? a0.ell_grid : 1536u) / ny);
+            const dim3 grid(std::min(g, grid_ell(a0.n)), ny);
+            const size_t lds = size_t(kEllChunk) * a0.ell * 4;
+            const auto k = a0.ell <= 4 ? (flt ? pt_forest_ell_kernel<true, 4> : pt_forest_ell_kernel<false, 4>)
+                         : a0.ell <= 6 ? (flt ? pt_forest_ell_kernel<true, 6> : pt_forest_ell_kernel<false, 6>)
+                                       : (flt ? pt_forest_ell_kernel<true, 8> : pt_forest_ell_kernel<false, 8>);
+            hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, f);
+        } else {
+            const dim3 grid(grid_chunks(a0.n), ny);
+            if (flt) hipLaunchKernelGGL(pt_forest_kernel<true>, grid, dim3(kBlock), 0, s, f);
+            else hipLaunchKernelGGL(pt_forest_kernel<false>, grid, dim3(kBlock), 0, s, f);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_fo_origin(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(fo_origin_kernel, dim3((k + 63) / 64), dim3(64), 0, s, f, lanes, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_busy(const FoArgs& f, const uint32_t* lanes, uint32_t k, uint32_t slot, uint32_t* out,
+                          hipStream_t s) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(fo_busy_kernel, dim3((k + 63) / 64), dim3(64), 0, s, f, lanes, k, slot, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_seed(const FoArgs& f, hipStream_t s) {
+    if (!f.nl || !f.a.mcnt) return hipSuccess;
+    hipLaunchKernelGGL(fo_seed_kernel, dim3((f.nl + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s) {
+    if (!k || !f.a.n) return hipSuccess;
+    const unsigned long long total = (unsigned long long)k * f.a.n;
+    const uint32_t g = uint32_t(std::min<unsigned long long>(65535ull * 8, (total + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(fo_renorm_kernel, dim3(g), dim3(kBlock), 0, s, f, lanes, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_count_live(const FoArgs& f, unsigned long long* out, hipStream_t s) {
+    if (!f.nl || !f.a.n) return hipSuccess;
+    const unsigned long long total = (unsigned long long)f.nl * f.a.n;
+    const uint32_t g = uint32_t(std::min<unsigned long long>(65535ull * 8, (total + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(fo_count_live_kernel, dim3(g), dim3(kBlock), 0, s, f, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s) {
+    if (!f.nl) return hipSuccess;
+    hipLaunchKernelGGL(fo_forget_kernel, dim3((f.nl + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, v);
     return hipGetLastError();
 }
 

@@ -143,6 +143,33 @@ struct psim_handle {
     };
     std::vector<Lane> lanes;
     int cur_lane = 0;
+
+    // The forest (psim_config.max_roots > kMaxLanes): every
+    // root's arrays in one slab each (lane L = root L's slice), all lanes
+    // launched together every round on the handle's round clock (par, round,
+    // tags); the fields above (vs, in, pend, ost, ost_total, serial, root)
+    // alias the focused lane's slices, and inflight / live_rows / ost_cnt
+    // are the totals over every lane.
+    struct Forest {
+        bool on = false;
+        uint32_t cap = 0, nl = 0;                // lanes the slabs hold / lanes holding a root
+        uint4* vs = nullptr;
+        uint32_t* in[2] = {nullptr, nullptr};
+        uint8_t* pend[2] = {nullptr, nullptr};
+        uint8_t* ost = nullptr;
+        int* ost_total = nullptr;                // [cap][4]
+        uint32_t* mcnt = nullptr;                // [cap][kMcntLane]
+        uint2* info = nullptr;                   // [cap] {Monotonic tag, local root} (device)
+        uint32_t* d_list = nullptr;              // [cap] lane lists for the origin / busy / renorm kernels
+        uint32_t* d_busy = nullptr;              // [cap]
+        uint64_t s_in = 0, s_pend = 0, s_ost = 0;
+        std::vector<uint2> h_info;
+        std::vector<uint32_t> serial;            // lane -> heartbeats so far (the lane's tag source)
+        std::vector<uint32_t> root_of;           // lane -> root
+        std::unordered_map<uint32_t, uint32_t> lane_of;
+        int focus = -1;
+        uint32_t gx = 0;                         // workgroups per lane (PSIM_FOREST_GX A/B knob; 0: auto)
+    } fo;
     void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
     size_t scratch_cap = 0;
 
@@ -226,8 +253,38 @@ int fail(psim_handle* h, int code, const char* fmt, ...) {
 void swap_lane(psim_handle* h, int j);
 void save_lane(psim_handle* h);
 void load_lane(psim_handle* h, int j);
+int forest_renorm_all(psim_handle* h);
+int forest_alloc(psim_handle* h);
+
+void free_forest(psim_handle* h) {
+    auto& f = h->fo;
+    if (!f.on) return;
+    // the handle's single-lane pointers alias the focused lane's slices
+    h->vs = nullptr;
+    h->in[0] = h->in[1] = nullptr;
+    h->pend[0] = h->pend[1] = nullptr;
+    h->ost = nullptr;
+    h->ost_total = h->ost_total_base;
+    void* fp[] = {f.vs, f.in[0], f.in[1], f.pend[0], f.pend[1], f.ost, f.ost_total, f.mcnt, f.info, f.d_list, f.d_busy};
+    for (void* x : fp)
+        if (x) (void)hipFree(x);
+    f.vs = nullptr;
+    f.in[0] = f.in[1] = nullptr;
+    f.pend[0] = f.pend[1] = nullptr;
+    f.ost = nullptr;
+    f.ost_total = nullptr;
+    f.mcnt = nullptr;
+    f.info = nullptr;
+    f.d_list = f.d_busy = nullptr;
+    f.nl = 0;
+    f.h_info.clear();
+    f.root_of.clear();
+    f.lane_of.clear();
+    f.focus = -1;
+}
 
 void free_graph(psim_handle* h) {
+    free_forest(h);
     if (!h->lanes.empty()) {
         swap_lane(h, 0);
         for (size_t j = 1; j < h->lanes.size(); j++) {
@@ -643,6 +700,7 @@ int64_t rows_held(const psim_handle* h) {
 }
 
 int renorm_if_needed(psim_handle* h) {
+    if (h->fo.on) return forest_renorm_all(h);
     const int focus = h->cur_lane;
     for (int j = 0; j < (int)h->lanes.size(); j++) {   // every lane's tags
         swap_lane(h, j);
@@ -907,6 +965,311 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     return PSIM_OK;
 }
 
+// ---- the forest: every node's heartbeat tree ---------------
+// partisan_plumtree_backend heartbeats from every node on a timer
+// (:341-368, :421-428) and the broadcast server keeps each root's eager /
+// lazy sets in its eager_sets / lazy_sets maps for good
+// (partisan_plumtree_broadcast.erl:1240-1248, 1278-1282; only reset_peers
+// drops them, :1320-1328).  A forest handle keeps up to max_roots roots:
+// lane L of every slab is one root's copy of the single-lane arrays, a
+// round is one launch over every lane, and nothing per lane crosses PCIe
+// per round (the counters of all lanes add into the round's one stats row).
+
+// bytes one lane takes in the slabs
+uint64_t fo_lane_bytes(const psim_handle* h, uint64_t s_in) {
+    const auto& f = h->fo;
+    return uint64_t(h->n) * 16 + 2 * s_in * 4 + 2 * f.s_pend + f.s_ost + 4 * sizeof(int) + kMcntLane * 4 + 8 + 8;
+}
+
+int forest_alloc(psim_handle* h) {
+    auto& f = h->fo;
+    if (!h->ell && !h->E) return fail(h, PSIM_EINVAL, "empty overlay");
+    // lane slices aligned to 256 B: the ELL sweep reads a chunk's words as quads
+    const uint64_t s_in = (h->Ed + 63) & ~uint64_t(63);
+    f.s_pend = (h->pend_bytes + 255) & ~uint64_t(255);
+    f.s_ost = (uint64_t(h->n) + 4 + 255) & ~uint64_t(255);
+    const uint64_t per = fo_lane_bytes(h, s_in), total = per * f.cap;
+    size_t fr = 0, tot = 0;
+    HIPCHK(h, hipMemGetInfo(&fr, &tot));
+    if (total + (uint64_t(1) << 30) > fr)
+        return fail(h, PSIM_ENOMEM, "max_roots=%u needs %.2f GB of slabs (%.2f MB per root); %.2f GB free", f.cap,
+                    double(total) / 1e9, double(per) / 1e6, double(fr) / 1e9);
+    const uint64_t C = f.cap;
+    if (!alloc_zero((void**)&f.vs, C * h->n * 16) || !alloc_zero((void**)&f.in[0], C * s_in * 4) ||
+        !alloc_zero((void**)&f.in[1], C * s_in * 4) || !alloc_zero((void**)&f.pend[0], C * f.s_pend) ||
+        !alloc_zero((void**)&f.pend[1], C * f.s_pend) || !alloc_zero((void**)&f.ost, C * f.s_ost) ||
+        !alloc_zero((void**)&f.ost_total, C * 4 * sizeof(int)) || !alloc_zero((void**)&f.mcnt, C * kMcntLane * 4) ||
+        !alloc_zero((void**)&f.info, C * 8) || !alloc_zero((void**)&f.d_list, C * 4) ||
+        !alloc_zero((void**)&f.d_busy, C * 4)) {
+        free_forest(h);
+        return fail(h, PSIM_ENOMEM, "forest slabs for %u roots (%.2f GB)", f.cap, double(total) / 1e9);
+    }
+    f.s_in = s_in;
+    f.nl = 0;
+    f.focus = -1;
+    f.h_info.assign(f.cap, make_uint2(0u, 0u));
+    f.serial.assign(f.cap, 0u);
+    f.root_of.clear();
+    f.lane_of.clear();
+    return PSIM_OK;
+}
+
+// The arguments of round R (tags R, counts ring R mod 4) for every lane: lane
+// 0's slices here, the kernels shift them by the lane (fo_lane in plumtree.hip).
+FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats, uint64_t R) {
+    const auto& f = h->fo;
+    PtArgs a = make_args(h, par, tick, stats);
+    a.vs = f.vs;
+    a.in_cur = f.in[par];
+    a.in_nxt = f.in[par ^ 1];
+    a.pend_cur = f.pend[par];
+    a.pend_nxt = f.pend[par ^ 1];
+    a.ost = f.ost;
+    a.ost_total = f.ost_total;
+    set_round_tags(a, R);
+    a.mcnt = f.mcnt;
+    a.m_w = uint32_t(R % 4);
+    a.m_s = uint32_t((R + 3) % 4);
+    a.m_r = uint32_t((R + 2) % 4);
+    a.m_z = uint32_t((R + 1) % 4);
+    a.dense = std::max<uint32_t>(1u, h->n / 4);
+    const uint32_t thr = list_threshold(h);
+    if (thr) {
+        a.wlcnt = a.mcnt + 256;
+        a.wl_cur = reinterpret_cast<uint32_t*>(a.pend_cur + h->wl_off);
+        a.wl_nxt = reinterpret_cast<uint32_t*>(a.pend_nxt + h->wl_off);
+        a.wl_cap = h->wl_cap;
+        a.wl_thr = thr;
+        a.wl_gpc = h->wl_gpc;
+    }
+    FoArgs fa{};
+    fa.a = a;
+    fa.s_vs = h->n;
+    fa.s_in = f.s_in;
+    fa.s_pend = f.s_pend;
+    fa.s_ost = f.s_ost;
+    fa.info = f.info;
+    fa.nl = f.nl;
+    return fa;
+}
+
+// The getters' view: the handle's single-lane fields alias lane `lane`.
+void forest_focus(psim_handle* h, int lane) {
+    auto& f = h->fo;
+    const uint64_t l = uint64_t(lane);
+    h->vs = f.vs + l * h->n;
+    for (int b = 0; b < 2; b++) {
+        h->in[b] = f.in[b] + l * f.s_in;
+        h->pend[b] = f.pend[b] + l * f.s_pend;
+    }
+    h->ost = f.ost + l * f.s_ost;
+    h->ost_total = f.ost_total + 4 * l;
+    h->serial = f.serial[lane];
+    h->root = f.root_of[lane];
+    h->have_root = true;
+    f.focus = lane;
+}
+
+int forest_upload_info(psim_handle* h) {
+    auto& f = h->fo;
+    if (f.nl) HIPCHK(h, hipMemcpyAsync(f.info, f.h_info.data(), size_t(f.nl) * 8, hipMemcpyHostToDevice, h->stream));
+    return PSIM_OK;
+}
+
+// The backend's heartbeat id of root's next heartbeat (broadcast_common's
+// rule): *commit = false only checks it.
+int next_mono(psim_handle* h, uint32_t root, uint32_t* out, bool commit) {
+    uint32_t mono = 0;
+    const auto it = h->mono_of.find(root);
+    if (it != h->mono_of.end()) mono = it->second;
+    const auto ne = h->next_epoch.find(root);
+    if (ne != h->next_epoch.end()) {
+        mono = (ne->second << 24) | 1u;
+        if (commit) h->next_epoch.erase(ne);
+    } else {
+        if ((mono & 0xFFFFFFu) >= 0xFFFFFEu) return fail(h, PSIM_EOVERFLOW, "root %u: 2^24-2 heartbeats in one epoch", root);
+        mono++;
+    }
+    if (commit) h->mono_of[root] = mono;
+    if (out) *out = mono;
+    return PSIM_OK;
+}
+
+// Heartbeats from roots[0, k) at once (backend handle_info(heartbeat) at each
+// of them).  All or nothing: a root past max_roots is PSIM_ENOSPC, a root
+// whose previous heartbeat is in flight or holds rows PSIM_EBUSY, before any
+// state changes.
+int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos) {
+    auto& f = h->fo;
+    if (!h->n) return PSIM_ESTATE;
+    if (!k) return PSIM_OK;
+    if (!roots) return PSIM_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    std::vector<uint32_t> lanes(k), old;
+    std::unordered_map<uint32_t, int> seen;
+    uint32_t fresh = 0;
+    for (size_t i = 0; i < k; i++) {
+        if (roots[i] >= h->n) return fail(h, PSIM_EINVAL, "root %u >= n", roots[i]);
+        if (!seen.emplace(roots[i], 1).second)
+            return fail(h, PSIM_EINVAL, "root %u heartbeats twice in one call", roots[i]);
+        const auto it = f.lane_of.find(roots[i]);
+        if (it == f.lane_of.end()) {
+            lanes[i] = kNoPeer;
+            fresh++;
+        } else {
+            lanes[i] = it->second;
+            old.push_back(it->second);
+        }
+        const int rc = next_mono(h, roots[i], nullptr, false);
+        if (rc) return rc;
+    }
+    if (uint64_t(f.nl) + fresh > f.cap)
+        return fail(h, PSIM_ENOSPC, "%u roots hold trees, %u new ones exceed max_roots=%u", f.nl, fresh, f.cap);
+    if (!old.empty()) {                          // every heartbeating root's last one is done
+        FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+        HIPCHK(h, hipMemcpyAsync(f.d_list, old.data(), old.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, launch_fo_busy(fa, f.d_list, uint32_t(old.size()), uint32_t(h->round % 4), f.d_busy, h->stream));
+        std::vector<uint32_t> busy(old.size());
+        HIPCHK(h, hipMemcpyAsync(busy.data(), f.d_busy, old.size() * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (size_t i = 0; i < old.size(); i++)
+            if (busy[i])
+                return fail(h, PSIM_EBUSY, "root %u: its last heartbeat is in flight or holds rows (a forest keeps one "
+                                           "heartbeat per root)", f.root_of[old[i]]);
+    }
+    std::vector<uint32_t> wrap;
+    for (size_t i = 0; i < k; i++) {
+        if (lanes[i] == kNoPeer) {
+            lanes[i] = f.nl++;
+            f.root_of.push_back(roots[i]);
+            f.lane_of[roots[i]] = lanes[i];
+        }
+        const uint32_t l = lanes[i];
+        f.serial[l]++;
+        if ((f.serial[l] & 0x7Fu) == 0) wrap.push_back(l);
+        f.h_info[l] = make_uint2(f.serial[l] & 0xFFu, roots[i]);
+        uint32_t mono = 0;
+        (void)next_mono(h, roots[i], &mono, true);
+        if (monos) monos[i] = mono;
+    }
+    int rc = forest_upload_info(h);
+    if (rc) return rc;
+    if (!wrap.empty()) {                         // 8-bit Monotonic tags of these lanes re-based
+        FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+        HIPCHK(h, hipMemcpyAsync(f.d_list, wrap.data(), wrap.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, launch_fo_renorm(fa, f.d_list, uint32_t(wrap.size()), h->stream));
+    }
+    // the origins emit into the buffers the next round reads (broadcast_common)
+    HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
+    FoArgs fa = forest_args(h, h->par ^ 1u, 0, h->stats, h->round + 1);
+    fa.a.wtag = uint32_t(h->round + 1) & 0xFFu;
+    HIPCHK(h, hipMemcpyAsync(f.d_list, lanes.data(), k * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, launch_fo_origin(fa, f.d_list, uint32_t(k), h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    unsigned long long r[kNStat];
+    reduce_row(h->h_stats, r);
+    forest_focus(h, int(lanes[k - 1]));
+    if (r[S_OVERFLOW])
+        return fail(h, PSIM_EOVERFLOW, "origins: overflow flags 0x%llx", r[S_OVERFLOW]);
+    h->ost_cnt += (int64_t)r[S_OST_DELTA];
+    h->live_rows += (int64_t)r[S_LIVE_DELTA];
+    h->inflight += r[PSIM_MSG_BROADCAST];
+    return PSIM_OK;
+}
+
+int forest_scrub_if_needed(psim_handle* h, uint64_t last) {
+    if (last + 1 < h->scrub + kTagSpan) return PSIM_OK;
+    const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
+    for (int b = 0; b < 2 && h->fo.nl; b++)
+        HIPCHK(h, launch_pt_scrub(h->fo.in[b], uint64_t(h->fo.nl) * h->fo.s_in, keep, 1, h->stream));
+    h->scrub = h->round;
+    return PSIM_OK;
+}
+
+int forest_renorm_all(psim_handle* h) {
+    FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+    HIPCHK(h, launch_fo_renorm(fa, nullptr, h->fo.nl, h->stream));
+    return PSIM_OK;
+}
+
+// psim_step / psim_run on a forest: every lane runs every round (a lane with
+// nothing in flight and no row due leaves in its first instructions).
+int forest_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
+                 uint32_t* ran_out) {
+    auto& f = h->fo;
+    uint32_t ran = 0;
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    const bool per_round = !(h->cfg.flags & PSIM_CFG_CHUNK_TIMING);
+    auto quiet = [&]() { return h->inflight == 0 && h->live_rows == 0; };
+    {   // every lane's row-holder ring from its exact count (seed_hold_ring)
+        FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+        HIPCHK(h, launch_fo_seed(fa, h->stream));
+    }
+    bool done = stop_q && quiet();
+    while (!done && ran < max_rounds) {
+        const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
+        int rc = forest_scrub_if_needed(h, h->round + k);
+        if (rc) return rc;
+        HIPCHK(h, hipMemsetAsync(h->stats, 0, k * kStatsRow * sizeof(unsigned long long), h->stream));
+        uint32_t par = h->par;
+        for (uint32_t i = 0; i < k; i++) {
+            const uint32_t tick = ((h->round + i + 1) % L) == 0;
+            const FoArgs fa = forest_args(h, par, tick, h->stats + i * kStatsRow, h->round + i + 1);
+            if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
+            if (f.nl) HIPCHK(h, launch_fo_round(fa, f.gx, h->stream));
+            if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
+            par ^= 1u;
+        }
+        h->par = par;
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * kStatsRow * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        float chunk_ms = 0.f;
+        if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
+        for (uint32_t i = 0; i < k; i++) {
+            float ms = chunk_ms / float(k);
+            if (per_round) HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
+            unsigned long long r[kNStat];
+            reduce_row(h->h_stats + i * kStatsRow, r);
+            if (r[S_OVERFLOW])
+                return fail(h, PSIM_EOVERFLOW, "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > "
+                            "4095, 4: outstanding rows of an older heartbeat)", (unsigned long long)(h->round + 1),
+                            r[S_OVERFLOW]);
+            uint64_t msgs = 0;
+            for (int t = 1; t <= 5; t++) msgs += r[t];
+            h->ost_cnt += (int64_t)r[S_OST_DELTA];
+            h->live_rows += (int64_t)r[S_LIVE_DELTA];
+            h->inflight = msgs;
+            h->round++;
+            h->kernel_ms_total += ms;
+            h->rounds_total++;
+            if (out && ran < cap) {
+                psim_round_stats& o = out[ran];
+                memset(&o, 0, sizeof o);
+                for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
+                o.delivered_new = r[S_DELIV];
+                o.active = r[S_ACTIVE];
+                o.senders = r[S_SENDERS];
+                o.sender_degree_sum = r[S_DEGSUM];
+                o.outstanding_vertices = (uint64_t)h->ost_cnt;
+                o.algo_bytes = 16ull * h->n * f.nl + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
+                o.words_stored = r[S_WORDS];
+                o.kernel_ms = ms;
+            }
+            ran++;
+            if (stop_q && quiet()) {
+                done = true;
+                break;
+            }
+        }
+    }
+    if (ran_out) *ran_out = ran;
+    return PSIM_OK;
+}
+
 }  // namespace
 
 namespace psim {
@@ -970,6 +1333,16 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     if (!h) return PSIM_ENOMEM;
     h->cfg = *cfg;
     if (!h->cfg.lazy_tick_rounds) h->cfg.lazy_tick_rounds = 1;
+    if (cfg->max_roots > uint32_t(kMaxLanes)) {          // the forest: every root's trees
+        if (cfg->flags & PSIM_CFG_BINNED) {
+            g_create_err = "max_roots > 16 needs the slot-scatter engine (not PSIM_CFG_BINNED)";
+            delete h;
+            return PSIM_EINVAL;
+        }
+        h->fo.on = true;
+        h->fo.cap = cfg->max_roots;
+        if (const char* e = getenv("PSIM_FOREST_GX")) h->fo.gx = uint32_t(strtoul(e, nullptr, 10));
+    }
     h->device = cfg->device >= 0 ? cfg->device : 0;
     if (cfg->device < 0) (void)hipGetDevice(&h->device);
     if (h->device >= ndev) { delete h; return PSIM_EINVAL; }
@@ -1246,13 +1619,15 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         bn.h_fslot.resize(size_t(bn.nf) + 1);
         for (uint32_t f = 0; f <= bn.nf; f++) bn.h_fslot[f] = rpl[std::min<uint64_t>(nl, uint64_t(f) << bn.fv_shift)];
     }
+    const bool forest = h->fo.on;       // the per-lane arrays live in the forest's slabs
+    if (forest && W > 1) return fail(h, PSIM_ESTATE, "max_roots > 16 (the forest) runs on one GPU");
     if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, Ed * 4) != hipSuccess ||
         alloc((void**)&h->rev, Ed * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl + 1) * 4) != hipSuccess ||
         (!ep.empty() && alloc((void**)&h->ecol, Ed * 4) != hipSuccess) ||
-        alloc((void**)&h->alive, nw * 4) != hipSuccess || alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess ||
-        (!binned && (alloc((void**)&h->in[0], Ed * 4) != hipSuccess || alloc((void**)&h->in[1], Ed * 4) != hipSuccess ||
-                     alloc((void**)&h->pend[0], pend_bytes) != hipSuccess ||
-                     alloc((void**)&h->pend[1], pend_bytes) != hipSuccess)) ||
+        alloc((void**)&h->alive, nw * 4) != hipSuccess || (!forest && alloc((void**)&h->vs, size_t(nl) * 16) != hipSuccess) ||
+        (!binned && !forest &&
+         (alloc((void**)&h->in[0], Ed * 4) != hipSuccess || alloc((void**)&h->in[1], Ed * 4) != hipSuccess ||
+          alloc((void**)&h->pend[0], pend_bytes) != hipSuccess || alloc((void**)&h->pend[1], pend_bytes) != hipSuccess)) ||
         (binned && (alloc((void**)&bn.rec_c, El * 8) != hipSuccess || alloc((void**)&bn.rec_f, El * 8) != hipSuccess ||
                     alloc((void**)&bn.cnt_c[0], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
                     alloc((void**)&bn.cnt_c[1], size_t(bn.nc) * kCoarseShards * 4) != hipSuccess ||
@@ -1260,7 +1635,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
                     alloc((void**)&bn.csub, bn.h_csub.size() * 4) != hipSuccess ||
                     alloc((void**)&bn.fslot, (size_t(bn.nf) + 1) * 4) != hipSuccess ||
                     alloc((void**)&bn.obin, size_t(bn.nf) * 4) != hipSuccess)) ||
-        alloc((void**)&h->ost, size_t(nl) + 4) != hipSuccess ||
+        (!forest && alloc((void**)&h->ost, size_t(nl) + 4) != hipSuccess) ||
         (W > 1 && (alloc((void**)&sh.stage, Ed * 4) != hipSuccess ||
                    alloc((void**)&sh.rem, remflat.size() * 4) != hipSuccess ||
                    alloc((void**)&sh.blk, blks.size() * 16) != hipSuccess ||
@@ -1300,7 +1675,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     HIPCHK(h, hipMemcpy(h->memb, mbl.data(), size_t(nl) * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemset(h->alive, 0xFF, nw * 4));
     // state: epoch tag 0 != h->epoch -> common sets; delivered tag never matches serial 1..
-    HIPCHK(h, hipMemset(h->vs, 0, size_t(nl) * 16));
+    if (!forest) HIPCHK(h, hipMemset(h->vs, 0, size_t(nl) * 16));
     if (binned) {
         HIPCHK(h, hipMemset(bn.cnt_c[0], 0, size_t(bn.nc) * kCoarseShards * 4));
         HIPCHK(h, hipMemset(bn.cnt_c[1], 0, size_t(bn.nc) * kCoarseShards * 4));
@@ -1308,17 +1683,17 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         HIPCHK(h, hipMemset(bn.obin, 0, size_t(bn.nf) * 4));
         HIPCHK(h, hipMemcpy(bn.csub, bn.h_csub.data(), bn.h_csub.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(bn.fslot, bn.h_fslot.data(), (size_t(bn.nf) + 1) * 4, hipMemcpyHostToDevice));
-    } else {
+    } else if (!forest) {
         HIPCHK(h, hipMemset(h->in[0], 0, Ed * 4));
         HIPCHK(h, hipMemset(h->in[1], 0, Ed * 4));
         HIPCHK(h, hipMemset(h->pend[0], 0, ng));
         HIPCHK(h, hipMemset(h->pend[1], 0, ng));
     }
-    HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
+    if (!forest) HIPCHK(h, hipMemset(h->ost, 0, size_t(nl) + 4));
     HIPCHK(h, hipMemset(h->ost_total_base, 0, kMaxLanes * 4 * sizeof(int)));
     HIPCHK(h, hipMemset(h->mcnt_base, 0, kMaxLanes * kMcntLane * sizeof(uint32_t)));
     h->ost_total = h->ost_total_base;
-    h->lanes.assign(1, psim_handle::Lane());
+    h->lanes.assign(forest ? 0 : 1, psim_handle::Lane());
     h->cur_lane = 0;
     if (W > 1) {
         std::vector<uint32_t> sb32(W);
@@ -1352,6 +1727,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->next_epoch.clear();
     h->ost_cnt = h->live_rows = 0;
     h->inflight = 0;
+    if (forest) return forest_alloc(h);
     return PSIM_OK;
 }
 
@@ -1375,6 +1751,16 @@ int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
         if (alive[v]) bm[v >> 5] |= 1u << (v & 31);
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemcpyAsync(h->alive, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, h->stream));
+    if (h->fo.on) {                  // outstanding rows to live peers, over every root's lane
+        HIPCHK(h, hipMemsetAsync(h->scratch, 0, 8, h->stream));
+        const FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+        HIPCHK(h, launch_fo_count_live(fa, h->scratch, h->stream));
+        unsigned long long live = 0;
+        HIPCHK(h, hipMemcpyAsync(&live, h->scratch, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->live_rows = (int64_t)live;
+        return PSIM_OK;
+    }
     const int focus = h->cur_lane;
     for (int j = 0; j < (int)h->lanes.size(); j++) {   // outstanding rows to live peers, per lane
         swap_lane(h, j);
@@ -1401,6 +1787,17 @@ int psim_plumtree_restart_backend(psim_handle* h, uint32_t v) {
     const uint32_t e = (ne == h->next_epoch.end() ? cur : ne->second) + 1u;
     if (e > 0xFFu) return fail(h, PSIM_EOVERFLOW, "vertex %u: 255 backend restarts", v);
     const uint32_t lv = v - h->sh.v_lo;
+    if (h->fo.on) {
+        // a static lane keeps one heartbeat per vertex: v may not forget one
+        // that is still in flight (the ≤ 16-lane handles turn the lane into a
+        // window lane instead)
+        if (!quiescent(h)) return fail(h, PSIM_EBUSY, "forest: backend restart while heartbeats are in flight");
+        const FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
+        HIPCHK(h, launch_fo_forget(fa, lv, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->next_epoch[v] = e;
+        return PSIM_OK;
+    }
     const int focus = h->cur_lane;
     if (!h->lanes.empty()) save_lane(h);
     const int nl = h->lanes.empty() ? 1 : (int)h->lanes.size();
@@ -1557,13 +1954,28 @@ extern "C" {
 
 int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     if (h && h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast");
+    if (h && h->fo.on) return forest_broadcast(h, &root, 1, mono_out);
     unsigned long long r[kNStat];
     return broadcast_common(h, root, mono_out, r);
+}
+
+int psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos_out) {
+    if (!h) return PSIM_EINVAL;
+    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast_x per root");
+    if (k && !roots) return PSIM_EINVAL;
+    if (h->fo.on) return forest_broadcast(h, roots, k, monos_out);
+    for (size_t i = 0; i < k; i++) {
+        unsigned long long r[kNStat];
+        const int rc = broadcast_common(h, roots[i], monos_out ? monos_out + i : nullptr, r);
+        if (rc) return rc;
+    }
+    return PSIM_OK;
 }
 
 int psim_shard_init(psim_handle* h, int rank, int world) {
     if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
     if (h->n) return fail(h, PSIM_ESTATE, "psim_shard_init must precede psim_load_csr");
+    if (h->fo.on && world > 1) return fail(h, PSIM_ESTATE, "max_roots > 16 (the forest) runs on one GPU");
     h->sh.rank = rank;
     h->sh.world = world;
     return PSIM_OK;
@@ -2331,6 +2743,7 @@ int psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t c
     if (!h) return PSIM_EINVAL;
     if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: drive rounds with psim_shard_round");
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->fo.on) return forest_drive(h, rounds, stats, cap, false, nullptr);
     return drive(h, rounds, stats, cap, false, nullptr);
 }
 
@@ -2338,12 +2751,14 @@ int psim_run(psim_handle* h, uint32_t max_rounds, psim_round_stats* stats, size_
     if (!h) return PSIM_EINVAL;
     if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: drive rounds with psim_shard_round");
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->fo.on) return forest_drive(h, max_rounds, stats, cap, true, rounds_run);
     return drive(h, max_rounds, stats, cap, true, rounds_run);
 }
 
 int psim_get_plumtree(const psim_handle* h, uint32_t* eager, uint32_t* lazy, uint32_t* outstanding,
                       uint16_t* recv_round, size_t n) {
     if (!h || n != h->n || !h->n) return PSIM_EINVAL;
+    if (!h->vs) return fail(const_cast<psim_handle*>(h), PSIM_ESTATE, "forest: no root heartbeated yet (no lane to read)");
     psim_handle* hh = const_cast<psim_handle*>(h);
     std::vector<uint4> vs(n);
     HIPCHK(hh, hipSetDevice(h->device));
@@ -2475,6 +2890,7 @@ int psim_get_delivered_mono(const psim_handle* h, uint32_t mono, uint8_t* delive
 
 int psim_get_delivered_range(const psim_handle* h, uint32_t mono, uint32_t v0, size_t count, uint8_t* delivered) {
     if (!h || !h->n || (count && !delivered) || v0 > h->n || count > h->n - v0) return PSIM_EINVAL;
+    if (!h->vs) return fail(const_cast<psim_handle*>(h), PSIM_ESTATE, "forest: no root heartbeated yet (no lane to read)");
     psim_handle* hh = const_cast<psim_handle*>(h);
     if (!count) return PSIM_OK;
     const uint32_t cm = cur_mono(h);
@@ -2506,6 +2922,7 @@ int psim_get_delivered_range(const psim_handle* h, uint32_t mono, uint32_t v0, s
 
 int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
     if (!h || !delivered || n != h->n || !h->n) return PSIM_EINVAL;
+    if (!h->vs) return fail(const_cast<psim_handle*>(h), PSIM_ESTATE, "forest: no root heartbeated yet (no lane to read)");
     psim_handle* hh = const_cast<psim_handle*>(h);
     std::vector<uint4> vs(n);
     HIPCHK(hh, hipSetDevice(h->device));
@@ -2518,6 +2935,7 @@ int psim_get_delivered(const psim_handle* h, uint8_t* delivered, size_t n) {
 
 int psim_get_inflight(const psim_handle* h, uint32_t* words, uint64_t n_words) {
     if (!h || !words || n_words != h->E) return PSIM_EINVAL;
+    if (!h->vs) return fail(const_cast<psim_handle*>(h), PSIM_ESTATE, "forest: no root heartbeated yet (no lane to read)");
     psim_handle* hh = const_cast<psim_handle*>(h);
     if (h->win) return fail(hh, PSIM_ESTATE, "window lane (several heartbeats in flight): use psim_get_messages");
     HIPCHK(hh, hipSetDevice(h->device));
@@ -2633,6 +3051,12 @@ int psim_vclock_get_counter(psim_handle* h, const uint32_t* a, const uint32_t* a
 
 int psim_plumtree_focus(psim_handle* h, uint32_t root) {
     if (!h || !h->n) return PSIM_ESTATE;
+    if (h->fo.on) {
+        const auto it = h->fo.lane_of.find(root);
+        if (it == h->fo.lane_of.end()) return fail(h, PSIM_EINVAL, "root %u has no heartbeat lane", root);
+        forest_focus(h, int(it->second));
+        return PSIM_OK;
+    }
     if (!lanes_enabled(h)) return h->have_root && h->root == root ? PSIM_OK : PSIM_EINVAL;
     return focus_root(h, root, false);
 }
@@ -2665,6 +3089,7 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
 }
 
 int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
+    if (h && h->fo.on) return fail(h, PSIM_ESTATE, "delay faults are not supported on a forest (max_roots > 16)");
     if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
     if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "delay faults need the slot-scatter engine (not the binned one)");
     if (h->sh.world > 1 && (h->win || h->sh.pending))
@@ -2736,6 +3161,7 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
 
 int psim_trace_hash(const psim_handle* h, uint64_t* out) {
     if (!h || !out || !h->n) return PSIM_EINVAL;
+    if (!h->vs) return fail(const_cast<psim_handle*>(h), PSIM_ESTATE, "forest: no root heartbeated yet (no lane to read)");
     psim_handle* hh = const_cast<psim_handle*>(h);
     HIPCHK(hh, hipSetDevice(h->device));
     PtArgs a = make_args(h, h->par, 0, h->stats);

@@ -203,6 +203,34 @@ struct PtArgs {
     uint32_t nf, nc, chunks;               // bins; route chunks per sub-region
 };
 
+// The forest (psim_config.max_roots > 16): every node's
+// heartbeat tree (partisan_plumtree_backend.erl:341-368, 421-428) in one
+// slab per array -- lane L of a slab is root L's copy of the single-lane
+// array -- and one launch per round over every lane (blockIdx.y = lane).
+// All lanes share the round clock: one inbox parity, one set of round tags,
+// one count-ring position; each keeps its own counts, worklist and holders.
+struct FoArgs {
+    PtArgs a;                              // this round's arguments at lane 0's slices
+    uint64_t s_vs, s_in, s_pend, s_ost;    // per-lane strides: uint4 records, u32 words, bytes, bytes
+    const uint2* __restrict__ info;        // [lanes] {Monotonic tag (low 8 bits), local root}
+    uint32_t lane0, nl;                    // this launch: lanes [lane0, lane0 + gridDim.y) of [0, nl)
+};
+// one round over lanes [0, f.nl): gx workgroups per lane (0: the round kernel's own choice)
+hipError_t launch_fo_round(FoArgs f, uint32_t gx, hipStream_t s);
+// the origins of lanes[0, k) (one root each; a.mono8 / a.root from f.info)
+hipError_t launch_fo_origin(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s);
+// out[i] = lane lanes[i] has messages of its last round (count slot `slot`) or rows
+hipError_t launch_fo_busy(const FoArgs& f, const uint32_t* lanes, uint32_t k, uint32_t slot, uint32_t* out,
+                          hipStream_t s);
+// every lane's row-holder ring from its exact count (a.m_r, a.m_s as PtArgs)
+hipError_t launch_fo_seed(const FoArgs& f, hipStream_t s);
+// tag re-base of lanes[0, k) (lanes == null: all f.nl lanes)
+hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s);
+// outstanding rows to live peers over every lane -> *out (added)
+hipError_t launch_fo_count_live(const FoArgs& f, unsigned long long* out, hipStream_t s);
+// a backend restart at local vertex v: v forgets every origin (each lane's delivered tag)
+hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s);
+
 // Demers rumor mongering + anti-entropy (demers.hip)
 constexpr uint32_t kDmPushCap = 24;   // AE pushes one vertex can receive per tick (Poisson(2) in-degree)
 constexpr uint32_t kDmFastPush = 8;   // pushes handled in registers (the rest: the generic walk)

@@ -111,6 +111,14 @@ class Simulator:
         self._c(lib().psim_plumtree_broadcast(self._h, root, C.byref(mono)))
         return mono.value
 
+    def broadcast_many(self, roots):
+        """Heartbeats from every root in `roots` at once (psim_plumtree_broadcast_many):
+        the backend's timer firing at each node.  Returns their ids."""
+        r = np.ascontiguousarray(np.asarray(roots, dtype=np.uint32).reshape(-1))
+        monos = np.zeros(len(r), np.uint32)
+        self._c(lib().psim_plumtree_broadcast_many(self._h, _u32p(r), len(r), _u32p(monos)))
+        return monos
+
     def step(self, rounds=1):
         st = (RoundStats * max(1, rounds))()
         self._c(lib().psim_step(self._h, rounds, st, rounds))

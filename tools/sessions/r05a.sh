@@ -12,7 +12,8 @@ step() {  # name seconds cmd...
     echo "=== $name rc=$rc"; tail -3 "gpurun_out/$name.log"
     [ $rc -le 1 ] || exit $rc
 }
-step pytest_gpu 1100 python -u -m pytest tests -m gpu -q -x --timeout 400 --timeout-method thread -p no:cacheprovider
+step pytest_forest 400 python -u -m pytest tests/test_forest.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider
+step pytest_gpu 1100 python -u -m pytest tests -m gpu --ignore=tests/test_forest.py -q -x --timeout 400 --timeout-method thread -p no:cacheprovider
 step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python bench.py --steps 20 --warmup 3
 step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline
