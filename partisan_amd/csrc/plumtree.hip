@@ -23,6 +23,7 @@
 //     added to one of 64 shards so atomics never pile onto one address.
 #include "psim_internal.h"
 #include <algorithm>
+#include <type_traits>
 #include "../../include/psim.h"
 
 namespace psim {
@@ -88,15 +89,18 @@ __device__ __forceinline__ void flush_counters(const Ctr& c, unsigned long long*
         if (lane == 0) red[wv][i] = x;
     }
     __syncthreads();
+    // shard by the workgroup's x and y index: the forest's lanes (blockIdx.y)
+    // must not all add into shard 0
+    const uint32_t sh = (blockIdx.x + blockIdx.y) & (kStatShards - 1);
     if (threadIdx.x < kNStat && threadIdx.x >= 1) {
         const int i = threadIdx.x;
         unsigned long long s = 0;
         if (i == S_OVERFLOW) {
             for (int w = 0; w < kBlock / 64; w++) s |= red[w][i];
-            if (s) atomicOr(&stats[(blockIdx.x & (kStatShards - 1)) * kNStat + i], s);
+            if (s) atomicOr(&stats[sh * kNStat + i], s);
         } else {
             for (int w = 0; w < kBlock / 64; w++) s += red[w][i];
-            if (s) atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kNStat + i], s);
+            if (s) atomicAdd(&stats[sh * kNStat + i], s);
             if (s && i == S_OST_DELTA && ost_total) atomicAdd(ost_total, (int)(long long)s);
             if (s && i == S_OST_DELTA && hold_d) atomicAdd(hold_d, (int)(long long)s);   // kMcntHoldD ring
         }
@@ -515,7 +519,13 @@ __device__ __forceinline__ bool word_non_prune(uint32_t w) {
 // claims of a vertex's words are all issued before any result is used, so the
 // vertex waits for one atomic round trip instead of one per word (a wave's
 // dependent random memory operations are what a sparse round costs).
-template <uint32_t kCap>
+// kMark: the round's mark when the caller resolved it at compile time (it is
+// uniform over a launch: RoundMode::mark), -1 = read `mark` at run time.  A
+// dense round (mark 0) then stores its words and nothing else -- no flag
+// store, no branch per slot, and the flag / worklist pointers need no
+// registers in the candidate loop (they were spilled to VGPR lanes and
+// reloaded with v_readlane per word: VERDICT r4 #4).
+template <uint32_t kCap, int kMark = -1>
 struct GroupSink {
     const PtArgs& a;
     uint32_t mark;
@@ -523,9 +533,16 @@ struct GroupSink {
     uint32_t m = 0;
     uint32_t g[kCap];
     __device__ __forceinline__ void word(uint32_t s, uint32_t u) {
-        if (mark != 2) {
-            mark_group(a, u >> kGroupShift, mark, wl);
+        if constexpr (kMark == 0) {
             return;
+        } else if constexpr (kMark == 1) {
+            a.pend_nxt[u >> kGroupShift] = 1;
+            return;
+        } else if constexpr (kMark == -1) {
+            if (mark != 2) {
+                mark_group(a, u >> kGroupShift, mark, wl);
+                return;
+            }
         }
         g[s] = u >> kGroupShift;
         m |= 1u << s;
@@ -535,6 +552,7 @@ struct GroupSink {
     // them before the stores, so their results do not wait behind the stores
     // in vmcnt, measured neutral in round 4: profiles/r04/experiments)
     __device__ __forceinline__ void issue() {
+        if constexpr (kMark == 0 || kMark == 1) return;
         if (!m) return;
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++)
@@ -543,6 +561,7 @@ struct GroupSink {
                          : 0u;
     }
     __device__ __forceinline__ void done() {
+        if constexpr (kMark == 0 || kMark == 1) return;
         if (!m) return;
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) {
@@ -555,7 +574,9 @@ struct GroupSink {
 };
 
 // Returns the change in "holds outstanding rows" (vst_store).
-template <bool kFault, uint32_t kCap, class Sink>
+// kLocal: one GPU, not sharded (no staging of remote words, v_lo = slot_base
+// = 0) -- the store of a word is the store, with no receiver-range test.
+template <bool kFault, uint32_t kCap, class Sink, bool kLocal = false>
 __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
                                               const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, Sink& sink) {
     const uint32_t aw = L.aw;
@@ -650,6 +671,14 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         nstored += wo[s] != 0u ? 1u : 0u;
     }
     c.words += nstored;
+    if constexpr (kLocal && !kFault) {
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) {
+            if (!wo[s]) continue;
+            a.in_nxt[rv[s]] = wo[s];
+            sink.word(s, cl[s]);
+        }
+    } else
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         if (!wo[s]) continue;
@@ -680,15 +709,15 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     return vst_store(a, v, st, x, c);
 }
 
-template <bool kFault, uint32_t kCap>
+template <bool kFault, uint32_t kCap, int kMark = -1, bool kLocal = false>
 __device__ __forceinline__ void pt_vertex_core(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg,
                                                const uint32_t (&w)[kCap], const VLoad<kCap>& L, Ctr& c, uint32_t mark,
                                                WlLds* wl) {
-    GroupSink<kCap> sink{a, mark, wl};
-    (void)pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, sink);
+    GroupSink<kCap, kMark> sink{a, mark, wl};
+    (void)pt_vertex_core<kFault, kCap, GroupSink<kCap, kMark>, kLocal>(a, v, rs, deg, w, L, c, sink);
 }
 
-template <bool kFault, bool kLdsWords = false, uint32_t kCap = kFastDeg>
+template <bool kFault, bool kLdsWords = false, uint32_t kCap = kFastDeg, int kMark = -1, bool kLocal = false>
 __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint32_t rs, uint32_t deg, bool pend,
                                                bool due, Ctr& c, const uint32_t* lw = nullptr, uint32_t mark = 1,
                                                WlLds* wl = nullptr) {
@@ -710,7 +739,7 @@ __device__ __forceinline__ void pt_vertex_fast(const PtArgs& a, uint32_t v, uint
     if (!pend && !due) return;
     VLoad<kCap> L;
     vload(a, v, rs, deg, L, rows);
-    pt_vertex_core<kFault, kCap>(a, v, rs, deg, w, L, c, mark, wl);
+    pt_vertex_core<kFault, kCap, kMark, kLocal>(a, v, rs, deg, w, L, c, mark, wl);
 }
 
 template <bool kFault>
@@ -945,7 +974,7 @@ static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) 
 // leaves to the next integer)
 __device__ __forceinline__ uint32_t div_w(uint32_t x, uint32_t wmag) { return (x * wmag) >> 18; }
 
-template <bool kFault, uint32_t kCap>
+template <bool kFault, uint32_t kCap, bool kLocal = false>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     static_assert(kEllChunk * kEllMax <= (1u << 13), "div_w is exact below 2^13");
     extern __shared__ __attribute__((aligned(16))) uint32_t wbuf[];   // [kEllChunk * W] the live words of the groups read
@@ -1141,11 +1170,20 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         }
         __syncthreads();
         const uint32_t nc = ncand;
-        for (uint32_t i = t; i < nc; i += kBlock) {
-            const uint32_t x = cand[i], lv = x >> 2;
-            const uint32_t v = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
-            pt_vertex_fast<kFault, true, kCap>(a, v, v * W, W, (x >> 1) & 1u, x & 1u, c, &wbuf[lv * W], md.mark, &wl);
-        }
+        // the round's mark is uniform over the launch: the dense rounds' (mark 0,
+        // no flags) get a candidate loop of their own
+        auto cand_loop = [&](auto mk) {
+            constexpr int M = decltype(mk)::value;
+            for (uint32_t i = t; i < nc; i += kBlock) {
+                const uint32_t x = cand[i], lv = x >> 2;
+                const uint32_t v = list ? (gl[lv >> kGroupShift] << kGroupShift) + (lv & (kGV - 1u)) : base + lv;
+                pt_vertex_fast<kFault, true, kCap, M, kLocal && M == 0>(a, v, v * W, W, (x >> 1) & 1u, x & 1u, c,
+                                                                        &wbuf[lv * W], md.mark, &wl);
+            }
+        };
+        const uint32_t mark = __builtin_amdgcn_readfirstlane(md.mark);
+        if (mark == 0) cand_loop(std::integral_constant<int, 0>{});
+        else cand_loop(std::integral_constant<int, -1>{});
         __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
     }
     if (md.mark == 2) wl_flush(a, &wl);
@@ -1154,12 +1192,12 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     flush_delays<kFault>(a);
 }
 
-template <bool kFault, uint32_t kCap>
+template <bool kFault, uint32_t kCap, bool kLocal>
 // At least 5 waves per SIMD (<= 96 VGPRs): the LDS holds 5-6 workgroups per
 // CU at W = 5-6, and the contiguous sweep's quads in flight would otherwise
 // take the kernel to 99 VGPRs, 4 waves (no spills at 96).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void pt_round_ell_kernel(PtArgs a) {
-    pt_round_ell_body<kFault, kCap>(a);
+    pt_round_ell_body<kFault, kCap, kLocal>(a);
 }
 
 // Multi-root rounds: one launch runs the round of every
@@ -1171,9 +1209,9 @@ __global__ __launch_bounds__(kBlock) void pt_round_lanes_kernel(const PtArgs* __
     pt_round_body<kFault>(args[blockIdx.y]);
 }
 
-template <bool kFault, uint32_t kCap>
+template <bool kFault, uint32_t kCap, bool kLocal>
 __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs* __restrict__ args) {
-    pt_round_ell_body<kFault, kCap>(args[blockIdx.y]);
+    pt_round_ell_body<kFault, kCap, kLocal>(args[blockIdx.y]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1203,7 +1241,7 @@ __device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
 
 template <bool kFault, uint32_t kCap>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void pt_forest_ell_kernel(FoArgs f) {
-    pt_round_ell_body<kFault, kCap>(fo_lane(f, f.lane0 + blockIdx.y));
+    pt_round_ell_body<kFault, kCap, true>(fo_lane(f, f.lane0 + blockIdx.y));   // one GPU, never sharded
 }
 
 template <bool kFault>
@@ -1827,8 +1865,10 @@ uint32_t ell_round_grid(uint32_t W, int device) {
     int cus = 0, o0 = 0, o1 = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
     const size_t lds = size_t(kEllChunk) * W * 4;
-    const auto k0 = W <= 4 ? pt_round_ell_kernel<false, 4> : W <= 6 ? pt_round_ell_kernel<false, 6> : pt_round_ell_kernel<false, 8>;
-    const auto k1 = W <= 4 ? pt_round_ell_kernel<true, 4> : W <= 6 ? pt_round_ell_kernel<true, 6> : pt_round_ell_kernel<true, 8>;
+    const auto k0 = W <= 4 ? pt_round_ell_kernel<false, 4, false> : W <= 6 ? pt_round_ell_kernel<false, 6, false>
+                                                                    : pt_round_ell_kernel<false, 8, false>;
+    const auto k1 = W <= 4 ? pt_round_ell_kernel<true, 4, false> : W <= 6 ? pt_round_ell_kernel<true, 6, false>
+                                                                   : pt_round_ell_kernel<true, 8, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, k0, kBlock, lds) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k1, kBlock, lds) != hipSuccess)
         return 0;
@@ -1846,9 +1886,14 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
     if (a.ell) {
         const size_t lds = size_t(kEllChunk) * a.ell * 4;
         const bool f = a.omit || a.dly;
-        const auto k = a.ell <= 4 ? (f ? pt_round_ell_kernel<true, 4> : pt_round_ell_kernel<false, 4>)
-                     : a.ell <= 6 ? (f ? pt_round_ell_kernel<true, 6> : pt_round_ell_kernel<false, 6>)
-                                  : (f ? pt_round_ell_kernel<true, 8> : pt_round_ell_kernel<false, 8>);
+        // kLocal: one GPU, not sharded (no staging ring, no staged remote words)
+        const bool loc = !a.stage && !a.srg;
+        const auto k = a.ell <= 4 ? (f ? pt_round_ell_kernel<true, 4, false>
+                                       : loc ? pt_round_ell_kernel<false, 4, true> : pt_round_ell_kernel<false, 4, false>)
+                     : a.ell <= 6 ? (f ? pt_round_ell_kernel<true, 6, false>
+                                       : loc ? pt_round_ell_kernel<false, 6, true> : pt_round_ell_kernel<false, 6, false>)
+                                  : (f ? pt_round_ell_kernel<true, 8, false>
+                                       : loc ? pt_round_ell_kernel<false, 8, true> : pt_round_ell_kernel<false, 8, false>);
         hipLaunchKernelGGL(k, dim3(a.ell_grid ? min(a.ell_grid, grid_ell(a.n)) : grid_ell(a.n)), dim3(kBlock), lds, s,
                            a);
         return hipGetLastError();
@@ -1867,9 +1912,16 @@ hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_
         const dim3 grid(std::min(gx, grid_ell(a0.n)), nlanes);
         const size_t lds = size_t(kEllChunk) * a0.ell * 4;
         const bool f = a0.omit || a0.dly;
-        const auto k = a0.ell <= 4 ? (f ? pt_round_ell_lanes_kernel<true, 4> : pt_round_ell_lanes_kernel<false, 4>)
-                     : a0.ell <= 6 ? (f ? pt_round_ell_lanes_kernel<true, 6> : pt_round_ell_lanes_kernel<false, 6>)
-                                   : (f ? pt_round_ell_lanes_kernel<true, 8> : pt_round_ell_lanes_kernel<false, 8>);
+        const bool loc = !a0.stage && !a0.srg;
+        const auto k = a0.ell <= 4 ? (f ? pt_round_ell_lanes_kernel<true, 4, false>
+                                        : loc ? pt_round_ell_lanes_kernel<false, 4, true>
+                                              : pt_round_ell_lanes_kernel<false, 4, false>)
+                     : a0.ell <= 6 ? (f ? pt_round_ell_lanes_kernel<true, 6, false>
+                                        : loc ? pt_round_ell_lanes_kernel<false, 6, true>
+                                              : pt_round_ell_lanes_kernel<false, 6, false>)
+                                   : (f ? pt_round_ell_lanes_kernel<true, 8, false>
+                                        : loc ? pt_round_ell_lanes_kernel<false, 8, true>
+                                              : pt_round_ell_lanes_kernel<false, 8, false>);
         hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, d_args);
         return hipGetLastError();
     }

@@ -640,6 +640,19 @@ inline uint32_t env_cap(const char* name, uint32_t cap) {
     return v < 1 ? 1u : v > cap ? cap : (uint32_t)v;
 }
 
+// C3_PROF diagnostic builds (tools/c3_prof.py): the SCAMP and C3 Plumtree
+// kernels clock their phases per wave (s_memtime at reconvergence points)
+// and count handled messages by kind into kProfSlots device counters per
+// kernel; the host folds them after every round and prints the running
+// totals to stderr.  Off in the product build (no code, no counters).
+#ifdef C3_PROF
+constexpr int kProfSlots = 24;
+__device__ __forceinline__ void prof_add(unsigned long long* p, int i, unsigned long long x) {
+    const unsigned long long act = __ballot(1);
+    if (__lane_id() == uint32_t(__ffsll((long long)act) - 1)) atomicAdd(&p[i], x);
+}
+#endif
+
 // Collective error agreement: a rank whose local step fails must
 // still enter the collective its peers wait in, and every rank must then
 // return the same code.  A local code travels as one flag per PSIM_E* code

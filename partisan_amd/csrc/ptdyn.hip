@@ -24,6 +24,7 @@
 // the destination must be a member of the sender (its SCAMP partial view);
 // otherwise it is dropped.
 #include "psim_internal.h"
+#include <cstdio>
 #include "../../include/psim.h"
 
 namespace psim {
@@ -338,14 +339,28 @@ __device__ __forceinline__ void reduce_stats(const PdArgs& a, const unsigned lon
 
 // stats: [1..5] sent by kind, 6 dropped, 7 delivered_new, 8 active, 9 error bits,
 // 10 updates applied, 11 delivered_live, 12 live, 13 outstanding rows to connected live peers
+#ifdef C3_PROF
+// [0..5) cycles of load+updates / sort / inbox / lazy tick / store (per wave),
+// [5..11) messages handled by kind, [11] i_have rows walked, [12] waves,
+// [13] load cycles alone, [14] update events
+__device__ unsigned long long g_pd_prof[kProfSlots];
+#endif
+
 __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
     unsigned long long vals[kPdNStat];
 #pragma unroll
     for (int i = 0; i < kPdNStat; i++) vals[i] = 0;
     if (v < a.n && a.alive[v]) {
+#ifdef C3_PROF
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        unsigned long long kinds = 0;
+#endif
         Ctx c;
         load(c, a, v);
+#ifdef C3_PROF
+        const unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
         const bool fresh = (c.h.flags & 2u) != 0;
         c.h.flags &= ~2u;
         // 1. the manager's update casts of this round, in order
@@ -355,6 +370,9 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
             apply_update(c, e.x, e.y);
         }
         vals[10] = ne;
+#ifdef C3_PROF
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
         // 2. the inbox in (src, seq) order (a restarted vertex drops it)
         const uint32_t lo = a.off[v], hi = a.off[v + 1];
         if (!fresh && hi > lo) {
@@ -365,9 +383,22 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
                 while (j > lo && msg_less(mx, a.in[a.idx[j - 1]])) { a.idx[j] = a.idx[j - 1]; j--; }
                 a.idx[j] = x;
             }
-            for (uint32_t i = lo; i < hi; i++) handle(c, a.in[a.idx[i]]);
+        }
+#ifdef C3_PROF
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+#endif
+        if (!fresh && hi > lo) {
+            for (uint32_t i = lo; i < hi; i++) {
+#ifdef C3_PROF
+                kinds += 1ull << (10 * (a.in[a.idx[i]].type % 6));
+#endif
+                handle(c, a.in[a.idx[i]]);
+            }
             vals[8] = 1;
         }
+#ifdef C3_PROF
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+#endif
         // 3. handle_info(lazy_tick): send_lazy/0, rows persist
         unsigned long long live_rows = 0;
         const uint32_t nr = c.h.nrow;
@@ -377,8 +408,25 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
             live_rows++;
             if (a.tick) send(c, r.peer, PD_IHAVE, r.mono, r.round);
         }
+#ifdef C3_PROF
+        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+#endif
         if (c.h.ntab > kPdTab - 8) tab_compact(c);
         store(c);
+#ifdef C3_PROF
+        const unsigned long long t5 = __builtin_amdgcn_s_memtime();
+        prof_add(g_pd_prof, 0, t1 - t0);
+        prof_add(g_pd_prof, 1, t2 - t1);
+        prof_add(g_pd_prof, 2, t3 - t2);
+        prof_add(g_pd_prof, 3, t4 - t3);
+        prof_add(g_pd_prof, 4, t5 - t4);
+        prof_add(g_pd_prof, 12, 1);
+        prof_add(g_pd_prof, 13, tl - t0);
+        atomicAdd(&g_pd_prof[11], (unsigned long long)nr);
+        atomicAdd(&g_pd_prof[14], (unsigned long long)ne);
+        for (int k = 0; k < 6; k++)
+            if ((kinds >> (10 * k)) & 1023ull) atomicAdd(&g_pd_prof[5 + k], (kinds >> (10 * k)) & 1023ull);
+#endif
 #pragma unroll
         for (int i = 1; i <= 5; i++) vals[i] = (c.sent >> (12 * (i - 1))) & 0xFFFull;
         vals[6] = c.dropped;
@@ -643,6 +691,18 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         PDCHK(h, hipMemcpyAsync(raw, s->stats, sizeof raw, hipMemcpyDeviceToHost, st));
         PDCHK(h, hipStreamSynchronize(st));
         fold_stat_shards(raw, r, kPdNStat, 9);
+#ifdef C3_PROF
+        {
+            static unsigned long long tot[kProfSlots];
+            unsigned long long x[kProfSlots];
+            PDCHK(h, hipMemcpyFromSymbol(x, HIP_SYMBOL(g_pd_prof), sizeof x));
+            const unsigned long long z[kProfSlots] = {};
+            PDCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_pd_prof), z, sizeof z));
+            fprintf(stderr, "pd_prof");
+            for (int i = 0; i < kProfSlots; i++) fprintf(stderr, " %llu", tot[i] += x[i]);
+            fprintf(stderr, "\n");
+        }
+#endif
         float ms = 0.f;
         PDCHK(h, hipEventElapsedTime(&ms, handle_event(h, 2), handle_event(h, 3)));
         s->par ^= 1u;

@@ -20,6 +20,7 @@
 // node), and bootstrap_remove sends before it clears the row.
 #include "psim_internal.h"
 #include "philox.h"
+#include <cstdio>
 #include "../../include/psim.h"
 
 namespace psim {
@@ -328,6 +329,13 @@ __global__ __launch_bounds__(kBlock) void sc_scatter(ScArgs a) {
     }
 }
 
+#ifdef C3_PROF
+// [0..4) cycles of the phases calls / sort / inbox / periodic (per wave),
+// [4..11) messages handled by kind, [11] draws in calls, [12] draws in the
+// inbox, [13] draws in periodic, [14] waves, [15] vertices with calls
+__device__ unsigned long long g_sc_prof[kProfSlots];
+#endif
+
 __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
     uint32_t sent[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -346,12 +354,21 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         const bool fresh = c.h.fresh != 0;
         c.h.fresh = 0;
         bool up = true;
+#ifdef C3_PROF
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const uint32_t d0 = c.ndraw;
+        unsigned long long kinds = 0;
+#endif
         // leave calls, then join calls (made since the last round, in call order)
         for (uint32_t i = a.call_off[v]; i < a.call_off[v + 1]; i++) {
             const uint32_t x = a.calls[i];
             if (x >> 31) do_leave(c, x & 0x7FFFFFFFu);
             else if (x != v && a.alive0[x]) do_join(c, x);   // connect/1 succeeds iff the peer is up
         }
+#ifdef C3_PROF
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const uint32_t d1 = c.ndraw;
+#endif
         // inbox in (src, seq) order; a restarted vertex drops what was sent to its old incarnation
         const uint32_t lo = a.off[v], hi = a.off[v + 1];
         if (!fresh && hi > lo) {
@@ -362,12 +379,38 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
                 while (j > lo && msg_less(mx, a.in[a.idx[j - 1]])) { a.idx[j] = a.idx[j - 1]; j--; }
                 a.idx[j] = x;
             }
+        }
+#ifdef C3_PROF
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+#endif
+        if (!fresh && hi > lo) {
             for (uint32_t i = lo; i < hi && up; i++) {
                 nproc++;
+#ifdef C3_PROF
+                kinds += 1ull << (9 * (a.in[a.idx[i]].type % 7));       // 9-bit fields by kind
+#endif
                 if (!do_message(c, a.in[a.idx[i]])) up = false;
             }
         }
+#ifdef C3_PROF
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        const uint32_t d3 = c.ndraw;
+#endif
         if (up && a.periodic) do_periodic(c);
+#ifdef C3_PROF
+        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+        prof_add(g_sc_prof, 0, t1 - t0);
+        prof_add(g_sc_prof, 1, t2 - t1);
+        prof_add(g_sc_prof, 2, t3 - t2);
+        prof_add(g_sc_prof, 3, t4 - t3);
+        atomicAdd(&g_sc_prof[11], (unsigned long long)(d1 - d0));
+        atomicAdd(&g_sc_prof[12], (unsigned long long)(d3 - d1));
+        atomicAdd(&g_sc_prof[13], (unsigned long long)(c.ndraw - d3));
+        prof_add(g_sc_prof, 14, 1);
+        if (a.call_off[v + 1] > a.call_off[v]) atomicAdd(&g_sc_prof[15], 1ull);
+        for (int k = 0; k < 7; k++)
+            if ((kinds >> (9 * k)) & 511ull) atomicAdd(&g_sc_prof[4 + k], (kinds >> (9 * k)) & 511ull);
+#endif
         if (!up) {
             a.alive[v] = 0;
             stopped = 1;
@@ -551,6 +594,18 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     SCCHK(h, hipMemcpyAsync(raw, s.stats, sizeof raw, hipMemcpyDeviceToHost, st));
     SCCHK(h, hipStreamSynchronize(st));
     fold_stat_shards(raw, r, 16, 11);
+#ifdef C3_PROF
+    {
+        static unsigned long long tot[kProfSlots];
+        unsigned long long x[kProfSlots];
+        SCCHK(h, hipMemcpyFromSymbol(x, HIP_SYMBOL(g_sc_prof), sizeof x));
+        const unsigned long long z[kProfSlots] = {};
+        SCCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_sc_prof), z, sizeof z));
+        fprintf(stderr, "sc_prof");
+        for (int i = 0; i < kProfSlots; i++) fprintf(stderr, " %llu", tot[i] += x[i]);
+        fprintf(stderr, "\n");
+    }
+#endif
     float ms = 0.f;
     SCCHK(h, hipEventElapsedTime(&ms, handle_event(h, 0), handle_event(h, 1)));
     handle_add_round(h, ms);

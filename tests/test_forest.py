@@ -219,9 +219,10 @@ def test_c2_all_roots_interval_properties():
         assert tot["delivered_new"] == n * (n - 1), (interval, tot)
         assert tot["i_have"] == tot["ignored_i_have"] + tot["graft"], tot   # every i_have answered once
         if interval == 1:
-            # the trees carry the second heartbeat: n - 1 eager pushes per root,
-            # plus the re-sends of the (rare) grafts
-            assert tot["broadcast"] == n * (n - 1) + tot["graft"], tot
+            # the trees carry the second heartbeat: n - 1 eager pushes per root
+            # (the origins' own <= 5 are counted by broadcast_many, not the
+            # rounds), plus the re-sends of the (rare) grafts
+            assert n * (n - 1) - 5 * n <= tot["broadcast"] - tot["graft"] <= n * (n - 1), tot
         for r in range(0, n, 997):
             sim.focus(r)
             eager, lazy, outst, rr = sim.plumtree_state()

@@ -7,6 +7,8 @@ GPU box:  python tools/config_bench.py > profiles/rNN/configs.jsonl
   C3  1M-peer SCAMP v2, 5 % churn per round + Plumtree repair (tools/probe_engines.py c3)
   C4  10M-peer Demers rumor mongering (fanout 2) + anti-entropy (fanout 2, every 2 rounds), 64 rumors, 1 GPU
   C5  1M-peer causal broadcast, 64 emitters with 64-lane vclocks, 1 GPU
+  C2ALL  every node heartbeats: the C2 overlay (10k HyParView peers) with all
+         10k roots heartbeating at once, two intervals, on a forest handle (max_roots = 10k)
   RELAY  10M-peer transitive relay: 100k random sends, relay_ttl 3,
          5-peer views, out-links = members (no per-root entry), 1 GPU
 """
@@ -52,6 +54,49 @@ def c2():
          plumtree_rounds=rounds, plumtree_kernel_ms=round(pt_ms, 3), delivered=int(sim.delivered().sum()),
          note="latency-bound at 10k peers: one join per round, as the sequential-join schedule prescribes")
     sim.close()
+
+
+def c2_overlay(n=10_000):
+    sim = pa.Simulator(seed=0x5EED0002)
+    hv = pa.hyparview.HyParViewCluster(sim, n)
+    from partisan_amd.overlay import philox_uniform
+    for v in range(1, n):
+        c = philox_uniform(0x5EED0002, np.array([v], np.uint32), 0xC200, v)
+        hv.join_many(np.array([v], np.uint32), np.asarray(c, np.uint32))
+        hv.step(1)
+    hv.step(10 * 10)
+    rp, col = hv.overlay()
+    sim.close()
+    return rp, col
+
+
+def c2_all_roots(n=10_000, intervals=2):
+    """Every node's heartbeat tree at once: all n roots heartbeat, rounds to
+    quiescence, twice (the second interval travels the pruned trees).
+    root-peer-rounds/s = roots x peers x rounds / device time; bytes = the
+    touched-state model of bench.py summed over every root's lane."""
+    rp, col = c2_overlay(n)
+    sim = pa.Simulator(seed=0x5EED0002, max_roots=n, chunk_timing=True)
+    sim.load_overlay(rp, col)
+    out = []
+    for it in range(intervals):
+        t0 = time.time()
+        sim.broadcast_many(np.arange(n, dtype=np.uint32))
+        bc_s = time.time() - t0
+        st, rounds = sim.run()
+        ms = sum(s["kernel_ms"] for s in st)
+        msgs = sum(sum(s[k] for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft")) for s in st)
+        tb = sum(16 * s["active"] + 8 * s["senders"] + 4 * s["sender_degree_sum"] +
+                 32 * sum(s[k] for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft")) for s in st)
+        words = sum(s["words_stored"] for s in st)
+        out.append(dict(interval=it + 1, rounds=rounds, kernel_ms=round(ms, 3), broadcast_call_s=round(bc_s, 4),
+                        messages=msgs, words=words, delivered_new=sum(s["delivered_new"] for s in st),
+                        root_peer_rounds_per_s=n * n * rounds / (ms / 1e3),
+                        touched_GBps=round(tb / 1e6 / ms, 1), hbm_frac=round(tb / 1e6 / ms / HBM, 4),
+                        words_per_s=words / (ms / 1e3), random_frac=round(words / (ms / 1e3) / 54.7e9, 4),
+                        per_round_ms=[round(s["kernel_ms"], 3) for s in st]))
+    sim.close()
+    line("C2ALL", n=n, roots=n, engine="forest (max_roots)", intervals=out)
 
 
 def c4(n=10_000_000, m=64):
@@ -136,3 +181,5 @@ if __name__ == "__main__":
             c5()
         elif w == "RELAY":
             relay()
+        elif w == "C2ALL":
+            c2_all_roots()
