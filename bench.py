@@ -90,6 +90,9 @@ def parse():
                    help="nccl = RCCL over xGMI (the real path); gloo = host-staged, for tests")
     p.add_argument("--all-on-device0", action="store_true",
                    help="test aid: put every rank on GPU 0 (needs --transport gloo)")
+    p.add_argument("--sustain-s", type=float, default=3.0,
+                   help="after the timed steps, keep flooding for this many seconds and report the sustained rate "
+                        "(the timed region alone is ~40 ms: too short for an SMI sampler to see); 0 = skip")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by tools/pmc_traffic.py for this workload")
     return p.parse_args()
@@ -468,6 +471,21 @@ def main():
 
     step_s = max_over_ranks(pg, (t1 - t0) / args.steps)
     n_units = args.n if sharded else args.n * world      # peers simulated by the whole job
+    sustained = None
+    if args.sustain_s > 0:
+        # the same steps back to back for a few seconds (outside the timed region, after every
+        # timed figure is taken)
+        barrier(pg)
+        k, s0, sus_rounds = 0, time.perf_counter(), []
+        while time.perf_counter() - s0 < args.sustain_s:
+            _, r = step()
+            sus_rounds.append(r)
+            k += 1
+        barrier(pg)
+        dt = max_over_ranks(pg, time.perf_counter() - s0)
+        sustained = {"steps": k, "seconds": round(dt, 3), "ms_per_step": dt / k * 1e3,
+                     "value": float(n_units) * sum(sus_rounds) / dt,
+                     "same_rounds_as_timed": set(sus_rounds) == set(rounds_per_step)}
     peer_rounds = float(n_units) * sum(rounds_per_step) / args.steps
     value = peer_rounds / step_s
     # per-launch figures over the rounds up to quiescence (the no-op tail of a
@@ -587,6 +605,8 @@ def main():
         }
         if exchange is not None:
             out["exchange"] = exchange
+        if sustained is not None:
+            out["sustained"] = sustained
         if not args.no_cpu_baseline and world == 1:
             if args.no_cpu_full:
                 out["cpu_baseline"] = cpu_baseline(args)

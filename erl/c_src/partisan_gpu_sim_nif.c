@@ -47,6 +47,8 @@ static ERL_NIF_TERM err(ErlNifEnv* env, int rc) {
     case PSIM_EOVERFLOW: a = "eoverflow"; break;
     case PSIM_EBUSY: a = "ebusy"; break;
     case PSIM_ENODEV: a = "enodev"; break;
+    case PSIM_ENOSPC: a = "enospc"; break;
+    case PSIM_ENOTSUP: a = "enotsup"; break;
     }
     return enif_make_tuple2(env, mk_atom(env, "error"), mk_atom(env, a));
 }
@@ -183,6 +185,35 @@ static ERL_NIF_TERM nif_broadcast(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     enif_mutex_unlock(r->mu);
     if (rc != PSIM_OK) return err(env, rc);
     return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_uint(env, mono));
+}
+
+/* broadcast_many(Sim, Roots :: <<u32-little>>) -> {ok, Ids :: <<u32-little>>}: the
+ * backend's heartbeat timer firing at every listed node at once
+ * (partisan_plumtree_backend.erl:341-368, 421-428; psim_plumtree_broadcast_many) */
+static ERL_NIF_TERM nif_broadcast_many(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    ErlNifBinary roots;
+    if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &roots) || roots.size % 4)
+        return enif_make_badarg(env);
+    const size_t k = roots.size / 4;
+    uint32_t* rt = (uint32_t*)enif_alloc(roots.size + 4);      /* binary data has no alignment guarantee */
+    if (!rt) return err(env, PSIM_ENOMEM);
+    memcpy(rt, roots.data, roots.size);
+    ERL_NIF_TERM t;
+    unsigned char* ids = enif_make_new_binary(env, k * 4, &t);
+    uint32_t* tmp = (uint32_t*)enif_alloc(k * 4 + 4);
+    int rc = tmp ? PSIM_OK : PSIM_ENOMEM;
+    if (rc == PSIM_OK) {
+        enif_mutex_lock(r->mu);
+        rc = psim_plumtree_broadcast_many(r->h, rt, k, tmp);
+        enif_mutex_unlock(r->mu);
+        if (rc == PSIM_OK) memcpy(ids, tmp, k * 4);
+    }
+    enif_free(rt);
+    if (tmp) enif_free(tmp);
+    if (rc != PSIM_OK) return err(env, rc);
+    return enif_make_tuple2(env, mk_atom(env, "ok"), t);
 }
 
 static ERL_NIF_TERM stats_term(ErlNifEnv* env, const psim_round_stats* s) {
@@ -1573,6 +1604,7 @@ static ErlNifFunc funcs[] = {
     {"reset_trees", 1, nif_reset_trees, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"restart_backend", 2, nif_restart_backend, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"broadcast", 2, nif_broadcast, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"broadcast_many", 2, nif_broadcast_many, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},

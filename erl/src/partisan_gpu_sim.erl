@@ -6,7 +6,8 @@
 %% pointers u64, byte maps one byte per vertex (see include/psim.h).
 -module(partisan_gpu_sim).
 
--export([new/1, load_csr/3, set_alive/2, reset_trees/1, restart_backend/2, broadcast/2, step/2, run/2,
+-export([new/1, load_csr/3, set_alive/2, reset_trees/1, restart_backend/2, broadcast/2, broadcast_many/2,
+         step/2, run/2,
          peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, is_delivered/3, rows/2, messages/1, shard_step/2,
          relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
@@ -36,6 +37,7 @@ init() ->
     erlang:load_nif(filename:join(Dir, "partisan_gpu_sim"), 0).
 
 -spec new(#{device => integer(), seed => non_neg_integer(), lazy_tick_rounds => pos_integer(),
+            max_roots => non_neg_integer(),
             exchange_tick_rounds => pos_integer()}) -> {ok, sim()} | error().
 new(_Opts) -> erlang:nif_error(nif_not_loaded).
 
@@ -56,6 +58,14 @@ restart_backend(_Sim, _V) -> erlang:nif_error(nif_not_loaded).
 %% {ok, Id}: Id = Epoch bsl 24 bor Monotonic (Epoch 0 until a restart)
 -spec broadcast(sim(), non_neg_integer()) -> {ok, non_neg_integer()} | error().
 broadcast(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
+
+%% Heartbeats from every listed root at once (the backend's timer firing at
+%% each node, partisan_plumtree_backend.erl:341-368): Roots and the returned
+%% Ids are u32-little binaries.  On a handle created with max_roots > 16 (the
+%% forest) every root's trees are kept: {error, enospc} past max_roots,
+%% {error, ebusy} for a root whose last heartbeat is still in flight.
+-spec broadcast_many(sim(), binary()) -> {ok, binary()} | error().
+broadcast_many(_Sim, _Roots) -> erlang:nif_error(nif_not_loaded).
 
 -spec step(sim(), pos_integer()) -> {ok, [map()]} | error().
 step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).

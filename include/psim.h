@@ -38,6 +38,7 @@ extern "C" {
 #define PSIM_EBUSY     (-7)   /* previous broadcast has not reached quiescence */
 #define PSIM_ENODEV    (-8)   /* no HIP device / kernel image for this GPU   */
 #define PSIM_ENOSPC    (-9)   /* every heartbeat-root slot holds a root's state */
+#define PSIM_ENOTSUP   (-10)  /* this combination of engine and features is not implemented */
 
 /* Message kinds of the Plumtree protocol (partisan_plumtree_broadcast.erl
  * send sites); index of psim_round_stats.sent[]. */

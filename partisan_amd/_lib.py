@@ -16,7 +16,7 @@ PSIM_CFG_CSR = 2      # slot-scatter engine keeps CSR rows instead of ELL rows (
 PSIM_CFG_CHUNK_TIMING = 4   # one hipEvent pair per chunk of rounds instead of per round
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EHIP", -4: "PSIM_ERCCL",
-    -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV", -9: "PSIM_ENOSPC",
+    -5: "PSIM_ESTATE", -6: "PSIM_EOVERFLOW", -7: "PSIM_EBUSY", -8: "PSIM_ENODEV", -9: "PSIM_ENOSPC", -10: "PSIM_ENOTSUP",
 }
 MSG_KINDS = {1: "broadcast", 2: "prune", 3: "i_have", 4: "ignored_i_have", 5: "graft"}
 

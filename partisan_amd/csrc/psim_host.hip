@@ -1313,6 +1313,7 @@ const char* psim_strerror(int code) {
     case PSIM_EBUSY: return "previous broadcast not quiescent";
     case PSIM_ENODEV: return "no usable HIP device";
     case PSIM_ENOSPC: return "no slot left for another heartbeat root";
+    case PSIM_ENOTSUP: return "not supported for this engine / feature combination";
     default: return "unknown error";
     }
 }
@@ -1779,7 +1780,7 @@ int psim_set_alive(psim_handle* h, const uint8_t* alive, size_t n) {
 int psim_plumtree_restart_backend(psim_handle* h, uint32_t v) {
     if (!h || !h->n) return PSIM_ESTATE;
     if (v >= h->sh.n_global) return PSIM_EINVAL;
-    if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "binned handles keep one epoch per root");
+    if (h->bin.rec_c) return fail(h, PSIM_ENOTSUP, "binned handles keep one epoch per root");
     HIPCHK(h, hipSetDevice(h->device));
     const auto it = h->mono_of.find(v);
     const uint32_t cur = it == h->mono_of.end() ? 0u : it->second >> 24;
@@ -1841,7 +1842,7 @@ int ingest_dense(psim_handle* h, const void* recv_dev, bool force_flags = false)
 // The split-phase sharded entry points drive the focused lane's words only.
 int one_lane_only(psim_handle* h) {
     if (h->lanes.size() > 1 || h->win)
-        return fail(h, PSIM_ESTATE, "several heartbeat lanes or a window lane: drive with psim_shard_broadcast_x / "
+        return fail(h, PSIM_ENOTSUP, "several heartbeat lanes or a window lane: drive with psim_shard_broadcast_x / "
                                     "psim_shard_run / psim_shard_step");
     return PSIM_OK;
 }
@@ -1975,7 +1976,7 @@ int psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k
 int psim_shard_init(psim_handle* h, int rank, int world) {
     if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
     if (h->n) return fail(h, PSIM_ESTATE, "psim_shard_init must precede psim_load_csr");
-    if (h->fo.on && world > 1) return fail(h, PSIM_ESTATE, "max_roots > 16 (the forest) runs on one GPU");
+    if (h->fo.on && world > 1) return fail(h, PSIM_ENOTSUP, "max_roots > 16 (the forest) runs on one GPU");
     h->sh.rank = rank;
     h->sh.world = world;
     return PSIM_OK;
@@ -3089,11 +3090,13 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
 }
 
 int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
-    if (h && h->fo.on) return fail(h, PSIM_ESTATE, "delay faults are not supported on a forest (max_roots > 16)");
+    if (h && h->fo.on) return fail(h, PSIM_ENOTSUP, "delay faults are not supported on a forest (max_roots > 16)");
     if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
-    if (h->bin.rec_c) return fail(h, PSIM_ESTATE, "delay faults need the slot-scatter engine (not the binned one)");
-    if (h->sh.world > 1 && (h->win || h->sh.pending))
-        return fail(h, PSIM_ESTATE, "delay faults on a sharded handle: no window lane, no async rounds pending");
+    if (h->bin.rec_c) return fail(h, PSIM_ENOTSUP, "delay faults need the slot-scatter engine (not the binned one)");
+    if (h->sh.world > 1 && h->win)      // lane layouts are decided alike on every rank (global counts)
+        return fail(h, PSIM_ENOTSUP, "delay faults on a sharded window lane (overlapping heartbeats)");
+    if (h->sh.world > 1 && h->sh.pending)
+        return fail(h, PSIM_ESTATE, "delay faults on a sharded handle with async rounds pending");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     save_lane(h);
@@ -3102,7 +3105,7 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
     busy = 0;
     int lrc = PSIM_OK;
     for (const auto& l : h->lanes) {
-        if (l.win && !lrc) lrc = fail(h, PSIM_ESTATE, "delay faults on a window lane (overlapping heartbeats)");
+        if (l.win && !lrc) lrc = fail(h, PSIM_ENOTSUP, "delay faults on a window lane (overlapping heartbeats)");
         busy += (int64_t)l.inflight;
     }
     if (h->sh.world > 1) {

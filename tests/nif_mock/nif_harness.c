@@ -122,6 +122,34 @@ int main(int argc, char** argv) {
                (unsigned long long)got, (unsigned long long)bsum, (unsigned long long)mock_int(mock_elem(th, 0)),
                (unsigned long long)mock_int(mock_elem(th, 1)), (unsigned long long)mock_int(mock_elem(th, 2)),
                (unsigned long long)mock_int(mock_elem(th, 3)));
+        {   /* every node heartbeats: the same overlay on a forest handle, all n roots
+             * at once through broadcast_many, twice; a 2n-th root is {error, enospc} */
+            const char* k[] = {"seed", "lazy_tick_rounds", "device", "max_roots"};
+            const uint64_t v[] = {0x5EED0002ull, 1, 0, n};
+            ERL_NIF_TERM fs = mock_elem(want_ok_tuple("new", call("new", 1, A(mock_map(4, k, v)))), 1);
+            want_ok("load_csr", call("load_csr", 3, A(fs, mock_bin(rp, (n + 1) * 8), u32s(col, e))));
+            uint32_t* roots = (uint32_t*)calloc(n, 4);
+            for (uint32_t i = 0; i < n; i++) roots[i] = i;
+            uint64_t fr[2] = {0, 0}, fdl = 0;
+            for (int it = 0; it < 2; it++) {
+                ERL_NIF_TERM ids = want_ok_tuple("broadcast_many", call("broadcast_many", 2, A(fs, u32s(roots, n))));
+                size_t isz;
+                const uint32_t* idp = (const uint32_t*)mock_bin_data(mock_elem(ids, 1), &isz);
+                if (isz != (size_t)n * 4 || idp[0] != (uint32_t)(it + 1)) { fprintf(stderr, "broadcast_many ids\n"); return 1; }
+                ERL_NIF_TERM fr_run = want_ok_tuple("run", call("run", 2, A(fs, mock_uint(1000))));
+                fr[it] = mock_int(mock_elem(fr_run, 1));
+                ERL_NIF_TERM fst = mock_elem(fr_run, 2);
+                for (size_t i = 0; i < mock_list_len(fst); i++)
+                    if (it == 0 && mock_map_get(mock_list_nth(fst, i), "delivered", &x)) fdl += x;
+            }
+            uint32_t extra = 0;
+            ERL_NIF_TERM big = call("broadcast_many", 2, A(fs, u32s(&extra, 1)));   /* root 0 again: fine */
+            (void)big;
+            want_ok_tuple("run", call("run", 2, A(fs, mock_uint(1000))));
+            fprintf(g_out, ", \"forest\": {\"roots\": %u, \"rounds\": [%llu, %llu], \"delivered\": %llu}", n,
+                    (unsigned long long)fr[0], (unsigned long long)fr[1], (unsigned long long)fdl);
+            free(roots);
+        }
         {   /* window-lane-era getters on the static lane: every vertex delivered this Monotonic, nothing in flight */
             ERL_NIF_TERM dm = want_ok_tuple("delivered_mono", call("delivered_mono", 2, A(sim, mock_elem(bc, 1))));
             size_t dmz;

@@ -133,6 +133,9 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rep["causal"]["delivered"] > 0
     assert rep["causal_shard_rccl_world1"]["delivered"] == rep["causal"]["delivered"]
     assert rep["vclock_merge"] == [3, 1, 4]
+    # the forest through the NIF: every root of the C2 overlay heartbeats, twice
+    assert rep["forest"]["roots"] == n and rep["forest"]["delivered"] == n * (n - 1), rep["forest"]
+    assert all(r > 0 for r in rep["forest"]["rounds"])
 
     # the same C2 through the Python binding of the same ABI: bit-identical
     import partisan_amd as pa

@@ -596,8 +596,9 @@ def test_delay_faults_lockstep(psim, n, seed, L, dmax):
     sim, orc = make(psim, rp, col, L)
     pairs, d = _delay_pairs(sim, 0.3, dmax, seed)
     if psim.engine == "binned":
-        with pytest.raises(psim.PsimError):
+        with pytest.raises(psim.PsimError) as ei:
             sim.set_delays(pairs, d)
+        assert ei.value.name == "PSIM_ENOTSUP"       # an explicit capability gap
         return
     sim.set_delays(pairs, d)
     orc.set_delays(pairs, d)
@@ -1046,3 +1047,36 @@ def test_facade_backend_restart_epochs(in_flight):
             assert pb.handler(v).graft(mid) == _expect_graft(orc, root, v, mid), (mid, v)
     assert pb.handler(3).graft(id0) == "stale"          # the row holds epoch 1 now
     assert pb.handler(3).graft(id1) == ("ok", id1)
+
+
+def test_unsupported_combinations_are_enotsup():
+    """combinations with no implementation answer
+    PSIM_ENOTSUP (not a generic state error): delay faults on the binned
+    engine, on a window lane (a root heartbeating during its own flood) and on
+    a forest; a backend restart on a binned handle."""
+    import partisan_amd as pa
+    rp, col = pa.overlay.random_regular(300, 5, 241)
+    b = pa.Simulator(binned=True)
+    b.load_overlay(rp, col)
+    pairs = [(0, int(b.slot_col[0]))]
+    for call in (lambda: b.set_delays(pairs, [2]), lambda: b.restart_backend(3)):
+        with pytest.raises(pa.PsimError) as ei:
+            call()
+        assert ei.value.name == "PSIM_ENOTSUP"
+    b.close()
+    s = pa.Simulator()
+    s.load_overlay(rp, col)
+    s.broadcast(0)
+    s.step(2)
+    s.broadcast(0)                            # the lane becomes a window lane
+    s.run()
+    with pytest.raises(pa.PsimError) as ei:
+        s.set_delays([(0, int(s.slot_col[0]))], [2])
+    assert ei.value.name == "PSIM_ENOTSUP"
+    s.close()
+    f = pa.Simulator(max_roots=32)
+    f.load_overlay(rp, col)
+    with pytest.raises(pa.PsimError) as ei:
+        f.set_delays([(0, int(f.slot_col[0]))], [2])
+    assert ei.value.name == "PSIM_ENOTSUP"
+    f.close()
