@@ -194,8 +194,11 @@ def sum_over_ranks(pg, x):
 
 def one_step(sim, root):
     sim.reset_trees()
-    sim.broadcast(root)
-    return sim.run(as_dicts=False)     # a numpy record array: no per-round Python dicts in the timed loop
+    # broadcast + run in one call (psim_plumtree_broadcast_run): the origin's
+    # counters come back with the first chunk; a numpy record array, no
+    # per-round Python dicts in the timed loop
+    _, st, rounds = sim.broadcast_run(root, as_dicts=False)
+    return st, rounds
 
 
 def verify(sim, pg, n, rounds_per_step):

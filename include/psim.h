@@ -165,6 +165,15 @@ int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
  * heartbeat is still in flight or holds rows, PSIM_EINVAL on a root listed
  * twice; otherwise psim_plumtree_broadcast per root, in order. */
 int  psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos_out);
+/* One heartbeat interval of one root: psim_plumtree_broadcast(root) then
+ * psim_run(max_rounds) -- the same state, ids, per-round stats and codes --
+ * in one call whose origin is not read back on its own: its counters come
+ * back with the first chunk of rounds (one host round trip fewer).  An
+ * origin overflow (PSIM_EOVERFLOW) is then reported after that chunk ran.
+ * Delay-fault and window-lane heartbeats read the origin first, as the two
+ * calls do; sharded handles: PSIM_ESTATE. */
+int  psim_plumtree_broadcast_run(psim_handle* h, uint32_t root, uint32_t* mono_out, uint32_t max_rounds,
+                                 psim_round_stats* stats, size_t cap, uint32_t* rounds_run);
 /* Several roots: on one GPU without PSIM_CFG_BINNED each
  * heartbeat root gets a lane of its own (per-root eager / lazy sets, rows,
  * delivered serials, in-flight words; up to 16 lanes, then the least

@@ -1518,9 +1518,32 @@ __device__ __forceinline__ void pt_origin_body(const PtArgs& a) {
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
 }
 
-__global__ void pt_origin_kernel(PtArgs a) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// prep != 0: first the fills the host used to enqueue before an origin, by
+// this block -- the stats row (prep words) zeroed, the lane's count area
+// zeroed and its hold ring seeded with `hold` (psim_host.hip seed_hold_ring)
+// -- one launch instead of four
+__global__ void pt_origin_kernel(PtArgs a, uint32_t prep, uint32_t hold) {
+    if (blockIdx.x != 0) return;
+    if (prep) {
+        for (uint32_t i = threadIdx.x; i < prep; i += blockDim.x) a.stats[i] = 0ull;
+        if (a.mcnt)
+            for (uint32_t i = threadIdx.x; i < kMcntLane; i += blockDim.x) a.mcnt[i] = i == kMcntHold + a.m_r ? hold : 0u;
+        __threadfence();
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
     pt_origin_body(a);
+}
+
+// The fills before a chunk of rounds (psim_host.hip drive): its stats rows
+// zeroed and every lane's hold ring seeded, in one launch.
+__global__ __launch_bounds__(kBlock) void pt_prep_kernel(PtPrep p) {
+    const uint64_t i0 = blockIdx.x * uint64_t(kBlock) + threadIdx.x, st = uint64_t(gridDim.x) * kBlock;
+    for (uint64_t i = i0; i < p.nz; i += st) p.z[i] = 0ull;
+    if (i0 < p.k) {
+        *p.hold[i0] = p.hv[i0];
+        *p.holdd[i0] = 0u;
+    }
 }
 
 // The forest's origins: one thread per heartbeat, each on its own lane.
@@ -2000,8 +2023,14 @@ hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pt_origin_kernel, dim3(1), dim3(64), 0, s, a);
+hipError_t launch_pt_prep(const PtPrep& p, hipStream_t s) {
+    const uint64_t b = (p.nz + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(pt_prep_kernel, dim3(uint32_t(b < 1 ? 1 : b > 64 ? 64 : b)), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s, uint32_t prep, uint32_t hold) {
+    hipLaunchKernelGGL(pt_origin_kernel, dim3(1), dim3(64), 0, s, a, prep, hold);
     return hipGetLastError();
 }
 

@@ -84,8 +84,9 @@ struct psim_handle {
         uint32_t fv_shift = 0, cv_shift = 0, nf = 0, nc = 0, chunks = 0;
         std::vector<uint32_t> h_csub, h_fslot;
     } bin;
-    unsigned long long* stats = nullptr;     // [kChunk][kStatShards][kNStat]
+    unsigned long long* stats = nullptr;     // [kChunk * kMaxLanes + 1][kStatsRow]; the last row: a deferred origin's
     unsigned long long* h_stats = nullptr;   // pinned mirror
+    bool origin_pend = false;                // psim_plumtree_broadcast_run: the origin's row not read back yet
     psim::PtArgs* lane_args = nullptr;       // [kChunk][kMaxLanes] per-round lane arguments (device)
     psim::PtArgs* h_lane_args = nullptr;     // pinned staging
     unsigned long long* scratch = nullptr;   // 1 counter
@@ -583,6 +584,33 @@ hipError_t seed_hold_rings(psim_handle* h, uint64_t R) {
     return e;
 }
 
+// seed_hold_rings as (address, value) pairs for pt_prep_kernel, every lane
+// but `skip` (a lane whose origin kernel seeded it for this round already)
+void prep_seeds(psim_handle* h, uint64_t R, PtPrep& p, int skip) {
+    static_assert(kMaxLanes <= (int)kMaxPrep, "one seed per lane");
+    auto one = [&]() {
+        PtArgs a = make_args(h, h->par, 0, h->stats);
+        set_round_slots(h, a, R);
+        if (!a.mcnt) return;
+        p.hold[p.k] = a.mcnt + kMcntHold + a.m_r;
+        p.holdd[p.k] = a.mcnt + kMcntHoldD + a.m_s;
+        p.hv[p.k] = uint32_t(h->ost_cnt);
+        p.k++;
+    };
+    if (h->lanes.empty()) {
+        if (skip < 0) one();
+        return;
+    }
+    const int focus = h->cur_lane;
+    save_lane(h);
+    for (int j = 0; j < (int)h->lanes.size(); j++) {
+        if (j == skip) continue;
+        load_lane(h, j);
+        one();
+    }
+    load_lane(h, focus);
+}
+
 // Round tags (psim_internal.h): a slot-scatter inbox word carries the round
 // that reads it, mod 256, and consumed words stay in place.  Before a lane
 // runs round `last`, every word older than 256 rounds must be gone, or its
@@ -836,8 +864,12 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             if (!lane_quiescent(h, l)) return false;
         return true;
     };
-    bool done = stop_q && all_quiet();
-    HIPCHK(h, seed_hold_rings(h, h->round + 1));
+    // psim_plumtree_broadcast_run: the origin's counters arrive with the
+    // first chunk's (its kernel seeded the focused lane's hold ring)
+    bool pend = h->origin_pend;
+    h->origin_pend = false;
+    bool done = !pend && stop_q && all_quiet();
+    bool seeded = false;
     while (!done && ran < max_rounds) {
         const uint32_t k = std::min<uint32_t>(kChunk, max_rounds - ran);
         const bool per_round = !(h->cfg.flags & PSIM_CFG_CHUNK_TIMING);   // events between round kernels
@@ -865,7 +897,14 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             par[q] ^= 1u;
             return a;
         };
-        HIPCHK(h, hipMemsetAsync(h->stats, 0, k * A * kStatsRow * sizeof(unsigned long long), h->stream));
+        {   // the chunk's stats rows zeroed and (first chunk) every lane's hold ring seeded: one launch
+            PtPrep pp{};
+            pp.z = h->stats;
+            pp.nz = uint64_t(k) * A * kStatsRow;
+            if (!seeded) prep_seeds(h, h->round + 1, pp, pend ? focus : -1);
+            seeded = true;
+            HIPCHK(h, launch_pt_prep(pp, h->stream));
+        }
         bool any_win = false;
         for (size_t q = 0; q < A; q++) any_win |= h->lanes[act[q]].win != nullptr;
         // a window lane's round: bucket its records, handle them (ptwin.hip)
@@ -907,6 +946,20 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         HIPCHK(h, hipStreamSynchronize(h->stream));
         float chunk_ms = 0.f;
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
+        if (pend) {     // the origin's row (broadcast_common), then the rounds as if it had been read first
+            pend = false;
+            unsigned long long r[kNStat];
+            reduce_row(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, r);
+            if (r[S_OVERFLOW])
+                return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older "
+                            "heartbeat)", r[S_OVERFLOW]);
+            auto& l = h->lanes[focus];
+            l.ost_cnt += (int64_t)r[S_OST_DELTA];
+            l.live_rows += (int64_t)r[S_LIVE_DELTA];
+            l.inflight = r[PSIM_MSG_BROADCAST];
+            // a quiet origin (no live eager peer): the chunk's rounds were no-ops
+            if (stop_q && all_quiet()) break;
+        }
         for (uint32_t i = 0; i < k; i++) {
             float ms = chunk_ms / float(k);
             if (per_round) HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
@@ -1362,8 +1415,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
         for (auto& e : h->sh.xev)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
-        if (hipMalloc(&h->stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
-        if (hipHostMalloc(&h->h_stats, kChunk * kMaxLanes * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipMalloc(&h->stats, (kChunk * kMaxLanes + 1) * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
+        if (hipHostMalloc(&h->h_stats, (kChunk * kMaxLanes + 1) * kStatsRow * sizeof(unsigned long long)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess ||
             hipHostMalloc(&h->h_lane_args, kChunk * kMaxLanes * sizeof(PtArgs)) != hipSuccess) { rc = PSIM_ENOMEM; break; }
         if (hipMalloc(&h->scratch, 64) != hipSuccess) { rc = PSIM_ENOMEM; break; }
@@ -1850,7 +1903,7 @@ int one_lane_only(psim_handle* h) {
 // Shared by psim_plumtree_broadcast and psim_shard_broadcast: every shard
 // advances the same serial / epoch / Monotonic; only the root's owner runs
 // the origin kernel.  Returns the origin's emitted-message stats row.
-int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned long long* r) {
+int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned long long* r, bool defer = false) {
     if (!h || !h->n) return PSIM_ESTATE;
     if (root >= h->sh.n_global) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
@@ -1896,23 +1949,28 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
     for (int i = 0; i < kNStat; i++) r[i] = 0;
     const uint32_t lr = root - h->sh.v_lo;
     if (lr < h->n) {
-        HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
         if (h->win) {                           // window lane: records for the next round
+            HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
             WinArgs a = make_win_args(h, h->par, 0, h->stats);
             a.out = h->win->msg[h->par];
             a.nout = h->win->nmsg + h->par;
             HIPCHK(h, launch_win_origin(a, lr, h->stream));
         } else {
-            // origin emits into the buffer the next round reads
-            PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);
+            // origin emits into the buffer the next round reads; its kernel
+            // first zeroes its stats row and the lane's count area and seeds
+            // the hold ring with the holders before the origin's own change
+            unsigned long long* row = defer ? h->stats + size_t(kChunk) * kMaxLanes * kStatsRow : h->stats;
+            PtArgs a = make_args(h, h->par ^ 1u, 0, row);
             set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
-            if (a.mcnt) {
-                HIPCHK(h, hipMemsetAsync(a.mcnt, 0, kMcntLane * sizeof(uint32_t), h->stream));
-                HIPCHK(h, seed_hold_ring(h, h->round + 1));   // holders before the origin's own change
-            }
             a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
             a.root = lr;
-            HIPCHK(h, launch_pt_origin(a, h->stream));
+            HIPCHK(h, launch_pt_origin(a, h->stream, uint32_t(kStatsRow), uint32_t(h->ost_cnt)));
+            if (defer) {                        // read back with the first chunk of rounds (drive)
+                HIPCHK(h, hipMemcpyAsync(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, row,
+                                         kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+                h->origin_pend = true;
+                return PSIM_OK;
+            }
         }
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
@@ -1971,6 +2029,23 @@ int psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k
         if (rc) return rc;
     }
     return PSIM_OK;
+}
+
+int psim_plumtree_broadcast_run(psim_handle* h, uint32_t root, uint32_t* mono_out, uint32_t max_rounds,
+                                psim_round_stats* stats, size_t cap, uint32_t* rounds_run) {
+    if (!h) return PSIM_EINVAL;
+    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast_x + psim_shard_run");
+    if (h->fo.on) {
+        const int rc = forest_broadcast(h, &root, 1, mono_out);
+        if (rc) return rc;
+        return forest_drive(h, max_rounds, stats, cap, true, rounds_run);
+    }
+    unsigned long long r[kNStat];
+    // delay faults account the origin's words in the due ring: read it now
+    const int rc = broadcast_common(h, root, mono_out, r, !h->dly);
+    if (rc) return rc;
+    HIPCHK(h, hipSetDevice(h->device));
+    return drive(h, max_rounds, stats, cap, true, rounds_run);
 }
 
 int psim_shard_init(psim_handle* h, int rank, int world) {

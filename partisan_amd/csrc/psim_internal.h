@@ -60,6 +60,62 @@ __device__ __forceinline__ uint32_t wave_reserve_n(uint32_t* counter, uint32_t k
     base = __shfl(base, (int)leader, 64);
     return base + pre;
 }
+// A wave's send buffer in LDS (the SCAMP and C3 handlers, which send one
+// record at a time from divergent code).  A send reserves records of its
+// wave's buffer with ONE LDS atomic per wave (wave_reserve's shape, on LDS)
+// and stores its record there; at the kernel's end the wave moves the buffer
+// to the global queue with one global atomicAdd of its exact count and
+// coalesced stores.  wave_reserve cost a device-scope atomic per send call,
+// whose return every sending lane waited for, on one counter every wave of
+// the chip hit.  A buffer past kWq records sends straight to the global
+// queue (wave_reserve).  No holes: the queue stays dense.
+// Only read-modify-writes hand records out: lanes in the two arms of a branch
+// run one arm after the other, and the compiler may sink an arm's plain LDS
+// stores past the other arm (tools/mb/mb_wq.hip caught a count kept that way).
+constexpr uint32_t kWq = 256;
+template <class Rec>
+struct WaveQ {
+    Rec* buf;          // LDS [kWq]
+    uint32_t* n;       // LDS: records reserved (may pass kWq)
+};
+__device__ __forceinline__ void wq_init(uint32_t* n) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <class Rec>
+__device__ __forceinline__ void wq_send(WaveQ<Rec> q, uint32_t* counter, Rec* __restrict__ out, uint32_t cap,
+                                        uint32_t& err, const Rec& r) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)act) - 1;
+    const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+    uint32_t k = 0;
+    if (lane == leader)
+        k = __hip_atomic_fetch_add(q.n, (uint32_t)__popcll(act), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    k = __shfl(k, (int)leader, 64) + rank;
+    if (k < kWq) {
+        q.buf[k] = r;
+        return;
+    }
+    const uint32_t pos = wave_reserve(counter);     // the buffer is full: the global queue directly
+    if (pos < cap) out[pos] = r;
+    else err |= 1u;
+}
+// At the kernel's end, by all 64 lanes of the wave (converged).
+template <class Rec>
+__device__ __forceinline__ void wq_flush(WaveQ<Rec> q, uint32_t* counter, Rec* __restrict__ out, uint32_t cap,
+                                         uint32_t& err) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // every lane's records are in LDS
+    uint32_t n = __hip_atomic_load(q.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    n = n < kWq ? n : kWq;
+    if (n == 0) return;
+    const uint32_t lane = __lane_id();
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(counter, n);
+    base = __shfl(base, 0, 64);
+    if (base + n > cap) err |= 1u;
+    for (uint32_t i = lane; i < n; i += 64)
+        if (base + i < cap) out[base + i] = q.buf[i];
+}
 // Per-lane round-count area (PtArgs::mcnt), u32 words:
 //   [0, 256)    messages sent per round, [4 rounds][64 shards]
 //   [256, 512)  worklist entries per round, [4][64] (PtArgs::wlcnt)
@@ -717,7 +773,18 @@ hipError_t launch_pt_round_lanes(const PtArgs* d_args, const PtArgs& a0, uint32_
 // op: 0 descends, 1 dominates, 2 merge, 3 increment, 4 equal, 5 glb, 6 subtract_dots, 7 get_counter
 hipError_t launch_vc(int op, const uint32_t* a, const uint32_t* b, const uint32_t* actor, uint32_t* out,
                      uint8_t* outb, size_t n, hipStream_t s);
-hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s);
+hipError_t launch_pt_origin(const PtArgs& a, hipStream_t s, uint32_t prep = 0, uint32_t hold = 0);
+// the fills before a chunk of rounds: stats rows zeroed, hold rings seeded
+constexpr uint32_t kMaxPrep = 16;
+struct PtPrep {
+    unsigned long long* z;
+    uint64_t nz;
+    uint32_t* hold[kMaxPrep];
+    uint32_t* holdd[kMaxPrep];
+    uint32_t hv[kMaxPrep];
+    uint32_t k;
+};
+hipError_t launch_pt_prep(const PtPrep& p, hipStream_t s);
 hipError_t launch_pt_count_live(const PtArgs& a, unsigned long long* out, hipStream_t s);
 hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s);
 // zero every inbox word whose round tag is not `keep` (psim_internal.h word format)

@@ -48,6 +48,7 @@ struct Ctx {
     uint32_t npv;
     unsigned long long sent;       // 12 bits per message kind 1..5 (kind k at bit 12 (k - 1): 60 bits)
     uint32_t dropped, deliv, err;
+    WaveQ<PdMsg> q;                // this wave's send buffer (LDS)
 };
 
 __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) { return t != c.v && row_has(c.pv, c.npv, t); }
@@ -55,14 +56,10 @@ __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) { return t !
 __device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     if (!connected(c, t)) { c.dropped++; return; }
     const PdArgs& a = *c.a;
-    const uint32_t pos = wave_reserve(a.nout);
     const uint32_t sh = 12u * (type - 1u);
     if (((c.sent >> sh) & 0xFFFull) == 0xFFFull) c.err |= 16u;   // a 13th bit would carry into the next kind
     else c.sent += 1ull << sh;
-    if (pos >= a.out_cap) { c.err |= 1u; return; }
-    PdMsg m;
-    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.round = round; m.mono = mono;
-    a.out[pos] = m;
+    wq_send(c.q, a.nout, a.out, a.out_cap, c.err, PdMsg{type, c.v, t, c.h.seq++, round, mono});
 }
 
 static_assert(kPdTab % 8 == 0, "row_find reads the peer table as quad pairs");
@@ -246,8 +243,11 @@ __device__ __forceinline__ uint32_t n_in(const PdArgs& a) { return *a.nin < a.ou
 
 __global__ __launch_bounds__(kBlock) void pd_count(PdArgs a) {
     const uint32_t k = n_in(a);
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock)
-        atomicAdd(&a.cnt[a.in[i].dst - a.v_lo], 1u);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock) {
+        const uint32_t d = a.in[i].dst - a.v_lo;
+        if (d < a.n) atomicAdd(&a.cnt[d], 1u);
+        else if (a.stats) atomicOr(&a.stats[9], 32ull);   // a record off this range: reported, never indexed
+    }
 }
 __global__ __launch_bounds__(kBlock) void pd_scan_blocks(PdArgs a) {
     __shared__ uint32_t ws[kBlock / 64];
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void pd_scatter(PdArgs a) {
     const uint32_t k = n_in(a);
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kPdStrideBlocks * kBlock) {
         const uint32_t d = a.in[i].dst - a.v_lo;
-        a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
+        if (d < a.n) a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
     }
 }
 
@@ -347,7 +347,12 @@ __device__ unsigned long long g_pd_prof[kProfSlots];
 #endif
 
 __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
+    __shared__ PdMsg qbuf[kBlock / 64][kWq];
+    __shared__ uint32_t qn[kBlock / 64];
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    const WaveQ<PdMsg> q{qbuf[threadIdx.x >> 6], &qn[threadIdx.x >> 6]};
+    wq_init(q.n);
+    uint32_t qerr = 0;
     unsigned long long vals[kPdNStat];
 #pragma unroll
     for (int i = 0; i < kPdNStat; i++) vals[i] = 0;
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
 #endif
         Ctx c;
         load(c, a, v);
+        c.q = q;
 #ifdef C3_PROF
         const unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
@@ -436,23 +442,34 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
         vals[12] = 1;
         vals[13] = live_rows;
     }
+    wq_flush(q, a.nout, a.out, a.out_cap, qerr);          // every lane of the wave: what is still staged
+    vals[9] |= qerr;
     reduce_stats(a, vals);
 }
 
 // heartbeat at the root: the backend's add_timestamp + the plumtree cast
 // {broadcast, Id, Payload, Mod} (:565-569) -> eager_push/4, schedule_lazy_push/3
 __global__ void pd_origin(PdArgs a, uint32_t root) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    unsigned long long vals[kPdNStat];
-    Ctx c;
-    load(c, a, root);
-    mark_delivered(c, a.mono);
-    c.h.myround = 0;
-    push(c, PdBits::none(), a.mono, 0u);
-    store(c);
-    (void)vals;
-    if (c.err) atomicOr(&a.stats[9], (unsigned long long)c.err);
-    atomicAdd(&a.stats[6], (unsigned long long)c.dropped);
+    // one thread sends; the wave's 64 lanes move its buffer (wq_flush)
+    __shared__ PdMsg qbuf[kWq];
+    __shared__ uint32_t qn;
+    if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+    wq_init(&qn);
+    const WaveQ<PdMsg> q{qbuf, &qn};
+    uint32_t err = 0;
+    if (threadIdx.x == 0) {
+        Ctx c;
+        load(c, a, root);
+        c.q = q;
+        mark_delivered(c, a.mono);
+        c.h.myround = 0;
+        push(c, PdBits::none(), a.mono, 0u);
+        store(c);
+        err = c.err;
+        atomicAdd(&a.stats[6], (unsigned long long)c.dropped);
+    }
+    wq_flush(q, a.nout, a.out, a.out_cap, err);
+    if (threadIdx.x == 0 && err) atomicOr(&a.stats[9], (unsigned long long)err);   // lane 0 holds every bit
 }
 
 // start_link/0 with members = {self}: fresh state (every vertex, or a crash list)
@@ -579,6 +596,8 @@ int pd_check(psim_handle* h, unsigned long long err, uint64_t round) {
     if (err & 8ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a heartbeat older than 64 serials is still in flight",
                                        (unsigned long long)round);
     if (err & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "c3 round %llu: a vertex sent more than 4095 messages of one kind",
+                                        (unsigned long long)round);
+    if (err & 32ull) return handle_fail(h, PSIM_EHIP, "c3 round %llu: a message record addressed off the cluster",
                                         (unsigned long long)round);
     return PSIM_OK;
 }

@@ -40,6 +40,7 @@ struct Ctx {
     uint32_t sent[7];
     uint32_t dropped, ndraw, err, resub;
     uint32_t nev;      // update events recorded this round
+    WaveQ<ScMsg> q;    // this wave's send buffer (LDS)
 };
 
 // partisan_peer_service_events:update(Members) after a handler that changed
@@ -61,30 +62,52 @@ __device__ uint64_t draw64(Ctx& c) {
 __device__ __forceinline__ bool in_pv(const Ctx& c, uint32_t t) { return row_has(c.pv, c.h.npv, t); }
 
 // select_random_sublist(L, K) = lists:sublist(shuffle(L), K): one uniform()
-// per element in list order, then the K smallest (r >> 11, N) in order
-__device__ uint32_t select_sublist(Ctx& c, uint32_t k, uint32_t* out) {
+// per element in list order, then the K smallest (r >> 11, N) in order.
+// The top-k list is kept by a carry pass over compile-time slots (registers;
+// a run-time-indexed array would live in scratch).
+template <uint32_t K>
+__device__ uint32_t select_top(Ctx& c, uint32_t k, uint32_t* out) {
     const uint32_t m = c.h.npv;
-    unsigned long long key[kScMaxSel];
-    uint32_t val[kScMaxSel];
-    uint32_t got = 0;
+    unsigned long long key[K];
+    uint32_t val[K];
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++) { key[j] = ~0ull; val[j] = 0xFFFFFFFFu; }
+    for (uint32_t i = 0; i < m; i++) {
+        unsigned long long r = draw64(c) >> 11;     // < 2^53: never the empty-slot key
+        uint32_t e = c.pv[i];
+#pragma unroll
+        for (uint32_t j = 0; j < K; j++) {
+            const bool lt = r < key[j] || (r == key[j] && e < val[j]);
+            const unsigned long long kr = lt ? key[j] : r;
+            const uint32_t ke = lt ? val[j] : e;
+            if (lt) { key[j] = r; val[j] = e; }
+            r = kr;
+            e = ke;
+        }
+    }
+    const uint32_t got = m < k ? m : k;
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++)
+        if (j < got) out[j] = val[j];
+    return got;
+}
+__device__ uint32_t select_sublist(Ctx& c, uint32_t k, uint32_t* out) {
+    return k <= 4 ? select_top<4>(c, k, out) : select_top<kScMaxSel>(c, k, out);
+}
+
+// select_random_sublist(L, 1): the same draws, the smallest (r >> 11, N) kept
+// in registers (the top-k arrays above are indexed at run time: scratch)
+__device__ uint32_t select_one(Ctx& c, uint32_t* out) {
+    const uint32_t m = c.h.npv;
+    unsigned long long best = ~0ull;
+    uint32_t bv = 0;
     for (uint32_t i = 0; i < m; i++) {
         const unsigned long long r = draw64(c) >> 11;
         const uint32_t e = c.pv[i];
-        // insert (r, e) into the sorted top-k
-        uint32_t j = got < k ? got : k;
-        if (j == k && !(r < key[k - 1] || (r == key[k - 1] && e < val[k - 1]))) continue;
-        if (j == k) j = k - 1;
-        while (j > 0 && (r < key[j - 1] || (r == key[j - 1] && e < val[j - 1]))) {
-            key[j] = key[j - 1];
-            val[j] = val[j - 1];
-            j--;
-        }
-        key[j] = r;
-        val[j] = e;
-        if (got < k) got++;
+        if (i == 0 || r < best || (r == best && e < bv)) { best = r; bv = e; }
     }
-    for (uint32_t i = 0; i < got; i++) out[i] = val[i];
-    return got;
+    out[0] = bv;
+    return m ? 1u : 0u;
 }
 
 // `member`: the caller took t from the live partial view (a member now), so
@@ -94,12 +117,9 @@ __device__ void emit(Ctx& c, uint32_t t, uint32_t type, uint32_t x, uint32_t y, 
     const ScArgs& a = *c.a;
     const bool conn = t != c.v && a.alive0[t] && (member || t == extra || in_pv(c, t));
     if (!conn) { c.dropped++; return; }
-    const uint32_t pos = wave_reserve(a.nout);
-    c.sent[type]++;
-    if (pos >= a.out_cap) { c.err |= 1u; return; }
-    ScMsg m;
-    m.type = type; m.src = c.v; m.dst = t; m.seq = c.h.seq++; m.a = x; m.b = y;
-    a.out[pos] = m;
+#pragma unroll
+    for (uint32_t k = 1; k < 7; k++) c.sent[k] += type == k ? 1u : 0u;   // compile-time slots: registers
+    wq_send(c.q, a.nout, a.out, a.out_cap, c.err, ScMsg{type, c.v, t, c.h.seq++, x, y});
 }
 
 __device__ void pv_push_front(Ctx& c, uint32_t x) {
@@ -116,13 +136,19 @@ __device__ void pv_set_add(Ctx& c, uint32_t x) {     // v1: sets, id order
     c.pv[i] = x;
     c.h.npv++;
 }
-__device__ void pv_del_first(Ctx& c, uint32_t x) {
+// deletes the first x; returns its index (npv before the call if absent)
+__device__ uint32_t pv_del_first(Ctx& c, uint32_t x) {
     for (uint32_t i = 0; i < c.h.npv; i++)
         if (c.pv[i] == x) {
             for (uint32_t j = i + 1; j < c.h.npv; j++) c.pv[j - 1] = c.pv[j];
             c.h.npv--;
-            return;
+            return i;
         }
+    return c.h.npv;
+}
+// entry i of the row as it was before pv_del_first(x) returned `at`
+__device__ __forceinline__ uint32_t pv_before(const Ctx& c, uint32_t i, uint32_t at, uint32_t x) {
+    return i < at ? c.pv[i] : (i == at ? x : c.pv[i - 1]);
 }
 
 // join/3 (v2 :89-137, v1 :69-119)
@@ -144,7 +170,9 @@ __device__ void do_join(Ctx& c, uint32_t node) {
         else if (t == node && c.h.npv != n0) continue;
         emit(c, t, SC_FWD, node, 0, node, true);
     }
-    for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, node, true);   // drawn from the row, which only grew
+#pragma unroll
+    for (uint32_t i = 0; i < kScMaxSel; i++)         // drawn from the row, which only grew
+        if (i < ns) emit(c, sel[i], SC_FWD, node, 0, node, true);
 }
 
 // leave/2 (v2 :140-146, v1 :122-142)
@@ -155,23 +183,23 @@ __device__ void do_leave(Ctx& c, uint32_t node) {
     }
     // members(State0) in id order, `node` deleted from the set first
     const bool had = in_pv(c, node);
-    uint32_t snap[kScPv];
     const uint32_t n0 = c.h.npv;
-    for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
-    if (had) pv_del_first(c, node);
+    const uint32_t at = had ? pv_del_first(c, node) : n0;
     if (had) record_update(c, 0xFFFFFFFFu, node);
-    for (uint32_t i = 0; i < n0; i++)   // snap minus node is still in the row; node itself is `extra`
-        emit(c, snap[i], SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu, snap[i] != node);
+    for (uint32_t i = 0; i < n0; i++) {   // the old row minus node is still in the row; node itself is `extra`
+        const uint32_t t = pv_before(c, i, at, node);
+        emit(c, t, SC_REMOVE, node, 0, had ? node : 0xFFFFFFFFu, t != node);
+    }
 }
 
 // periodic/1 (v2 :180-221, v1 :174-216); isolation per Q19
 __device__ void do_periodic(Ctx& c) {
     const bool isolated = c.h.last_ping >= 0 && (uint32_t)c.h.last_ping < c.a->round;
     if (isolated) {
-        uint32_t sel[1];
-        const uint32_t ns = select_sublist(c, 1, sel);
+        uint32_t sel;
+        const uint32_t ns = select_one(c, &sel);
         c.resub++;
-        for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, c.v, 0, 0xFFFFFFFFu, true);
+        if (ns) emit(c, sel, SC_FWD, c.v, 0, 0xFFFFFFFFu, true);
     }
     // the pings (one per live member but self, in list order): one wave
     // reservation for all of them instead of one per emit
@@ -215,9 +243,9 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
                 record_update(c, node, 0xFFFFFFFFu);
             }
         } else {
-            uint32_t sel[1];
-            const uint32_t ns = select_sublist(c, 1, sel);
-            for (uint32_t i = 0; i < ns; i++) emit(c, sel[i], SC_FWD, node, 0, 0xFFFFFFFFu, true);
+            uint32_t sel;
+            const uint32_t ns = select_one(c, &sel);
+            if (ns) emit(c, sel, SC_FWD, node, 0, 0xFFFFFFFFu, true);
         }
         break;
     }
@@ -231,12 +259,13 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         const uint32_t node = m.a;
         if (!in_pv(c, node)) break;
         if (a.ver == 1) { c.err |= 8u; return false; }       // Q17: the manager stops
-        uint32_t snap[kScPv];
         const uint32_t n0 = c.h.npv;
-        for (uint32_t i = 0; i < n0; i++) snap[i] = c.pv[i];
-        pv_del_first(c, node);
+        const uint32_t at = pv_del_first(c, node);
         if (!in_pv(c, node)) record_update(c, 0xFFFFFFFFu, node);   // a duplicate keeps it a member
-        for (uint32_t i = 0; i < n0; i++) emit(c, snap[i], SC_REMOVE, node, 0, node, snap[i] != node);
+        for (uint32_t i = 0; i < n0; i++) {
+            const uint32_t t = pv_before(c, i, at, node);
+            emit(c, t, SC_REMOVE, node, 0, node, t != node);
+        }
         break;
     }
     case SC_REPLACE: {                                        // v2 :275-294
@@ -279,8 +308,11 @@ __device__ __forceinline__ uint32_t n_in(const ScArgs& a) { return *a.nin < a.ou
 
 __global__ __launch_bounds__(kBlock) void sc_count(ScArgs a) {
     const uint32_t k = n_in(a);
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kScStrideBlocks * kBlock)
-        atomicAdd(&a.cnt[a.in[i].dst], 1u);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kScStrideBlocks * kBlock) {
+        const uint32_t d = a.in[i].dst;
+        if (d < a.n) atomicAdd(&a.cnt[d], 1u);
+        else atomicOr(&a.stats[11], 32ull);           // a record off the cluster: reported, never indexed
+    }
 }
 __global__ __launch_bounds__(kBlock) void sc_scan_blocks(ScArgs a) {
     __shared__ uint32_t ws[kBlock / 64];
@@ -325,7 +357,7 @@ __global__ __launch_bounds__(kBlock) void sc_scatter(ScArgs a) {
     const uint32_t k = n_in(a);
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < k; i += kScStrideBlocks * kBlock) {
         const uint32_t d = a.in[i].dst;
-        a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
+        if (d < a.n) a.idx[a.off[d] + atomicAdd(&a.cur[d], 1u)] = i;
     }
 }
 
@@ -337,7 +369,11 @@ __device__ unsigned long long g_sc_prof[kProfSlots];
 #endif
 
 __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
+    __shared__ ScMsg qbuf[kBlock / 64][kWq];
+    __shared__ uint32_t qn[kBlock / 64];
     const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    const WaveQ<ScMsg> q{qbuf[threadIdx.x >> 6], &qn[threadIdx.x >> 6]};
+    wq_init(q.n);
     uint32_t sent[7] = {0, 0, 0, 0, 0, 0, 0};
     uint32_t dropped = 0, ndraw = 0, err = 0, resub = 0, nproc = 0, stopped = 0, npv = 0, niv = 0;
     if (v < a.n && !a.alive0[v] && a.head[v].fresh) a.head[v].fresh = 0;
@@ -351,6 +387,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         for (int i = 0; i < 7; i++) c.sent[i] = 0;
         c.dropped = c.ndraw = c.err = c.resub = 0;
         c.nev = 0;
+        c.q = q;
         const bool fresh = c.h.fresh != 0;
         c.h.fresh = 0;
         bool up = true;
@@ -423,6 +460,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         for (int i = 0; i < 7; i++) sent[i] = c.sent[i];
         dropped = c.dropped; ndraw = c.ndraw; err = c.err; resub = c.resub;
     }
+    wq_flush(q, a.nout, a.out, a.out_cap, err);           // every lane of the wave: what is still staged
     // counters: [1..6] sent by kind, 7 dropped, 8 processed, 9 draws, 10 stopped,
     // 11 error bits (OR), 12 pv_sum, 13 inview_sum, 14 resub
     unsigned long long vals[15];
@@ -617,6 +655,8 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
                                          (unsigned long long)s.round, kScPv, kScIv);
     if (r[11] & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: > %u membership updates at a vertex",
                                           (unsigned long long)s.round, kScEv);
+    if (r[11] & 32ull) return handle_fail(h, PSIM_EHIP, "scamp round %llu: a message record addressed off the cluster",
+                                          (unsigned long long)s.round);
     if (out) {
         memset(out, 0, sizeof *out);
         uint64_t emitted = 0;

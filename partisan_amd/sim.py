@@ -138,6 +138,20 @@ class Simulator:
             return np.frombuffer(st, dtype=_ROUND_DTYPE, count=k).copy(), ran.value
         return [s.as_dict() for s in st[:k]], ran.value
 
+    def broadcast_run(self, root, max_rounds=100000, cap=4096, as_dicts=True):
+        """broadcast(root) then run() in one call (psim_plumtree_broadcast_run):
+        the origin's counters come back with the first chunk of rounds.
+        Returns (id, per-round stats, rounds)."""
+        st = getattr(self, "_run_buf", None)
+        if st is None or len(st) < cap:
+            st = self._run_buf = (RoundStats * cap)()
+        mono, ran = C.c_uint32(), C.c_uint32()
+        self._c(lib().psim_plumtree_broadcast_run(self._h, root, C.byref(mono), max_rounds, st, cap, C.byref(ran)))
+        k = min(ran.value, cap)
+        if not as_dicts:
+            return mono.value, np.frombuffer(st, dtype=_ROUND_DTYPE, count=k).copy(), ran.value
+        return mono.value, [s.as_dict() for s in st[:k]], ran.value
+
     def plumtree_state(self):
         n = self.n
         eager = np.zeros(n, np.uint32)

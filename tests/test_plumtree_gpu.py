@@ -1080,3 +1080,102 @@ def test_unsupported_combinations_are_enotsup():
         f.set_delays([(0, int(f.slot_col[0]))], [2])
     assert ei.value.name == "PSIM_ENOTSUP"
     f.close()
+
+
+def _nt(st):
+    """per-round stats without the timing field"""
+    return [{k: v for k, v in x.items() if k != "kernel_ms"} for x in st]
+
+
+def _same(a, b):
+    for x, y in zip(a.plumtree_state(), b.plumtree_state()):
+        assert np.array_equal(x, y)
+    assert np.array_equal(a.delivered(), b.delivered())
+    assert a.decode_inflight() == b.decode_inflight()
+    assert a.trace_hash() == b.trace_hash()
+
+
+def test_broadcast_run_matches_broadcast_then_run(psim):
+    """psim_plumtree_broadcast_run (the origin's counters read back with the
+    first chunk) = psim_plumtree_broadcast + psim_run: ids, per-round stats,
+    round counts and every vertex's state -- floods, tree heartbeats, dead
+    peers, a root change, a root with no peers (a quiet origin: zero rounds),
+    a root whose every peer is dead, and a second root heartbeating while the first is in flight
+    (several lanes, the pending origin on one of them)."""
+    n = 2000
+    rp, col = psim.overlay.random_regular(n - 1, 5, 77)
+    rp = np.append(rp, rp[-1]).astype(rp.dtype)      # vertex n - 1 has no peers: its origin is quiet
+    a = psim.Simulator()
+    a.load_overlay(rp, col)
+    b = psim.Simulator()
+    b.load_overlay(rp, col)
+
+    def both(root):
+        ma = a.broadcast(root)
+        sa, ra = a.run()
+        mb, sb, rb = b.broadcast_run(root)
+        assert (ma, ra) == (mb, rb)
+        assert _nt(sa) == _nt(sb)
+        _same(a, b)
+        return ra
+
+    assert both(5) > 3
+    assert both(5) > 3
+    dead = np.ones(n, np.uint8)
+    dead[np.random.default_rng(1).choice(n, 100, replace=False)] = 0
+    a.set_alive(dead)
+    b.set_alive(dead)
+    both(9)
+    both(9)
+    assert both(n - 1) == 0                   # nothing sent: zero rounds
+    # a root whose every peer is dead: its pushes are lost on arrival
+    r = 1234
+    nb = col[rp[r]:rp[r + 1]]
+    alive = np.ones(n, np.uint8)
+    alive[nb] = 0
+    a.set_alive(alive)
+    b.set_alive(alive)
+    both(r)
+    a.set_alive(np.ones(n, np.uint8))
+    b.set_alive(np.ones(n, np.uint8))
+    both(r)
+    if psim.engine != "binned":       # binned handles keep one root
+        a.broadcast(17)
+        b.broadcast(17)
+        a.step(2)
+        b.step(2)
+        ma = a.broadcast(400)
+        sa, ra = a.run()
+        mb, sb, rb = b.broadcast_run(400)
+        assert (ma, ra, _nt(sa)) == (mb, rb, _nt(sb))
+        for root in (17, 400):
+            a.focus(root)
+            b.focus(root)
+            _same(a, b)
+    a.close()
+    b.close()
+
+
+def test_broadcast_run_with_delays_matches():
+    """Delay faults: the origin's words go to the due ring, so broadcast_run
+    reads the origin first (as the two calls do); same results."""
+    import partisan_amd as pa
+    n = 1500
+    rp, col = pa.overlay.random_regular(n, 5, 78)
+    sims = []
+    for _ in range(2):
+        s = pa.Simulator()
+        s.load_overlay(rp, col)
+        src = np.repeat(np.arange(n), np.diff(rp.astype(np.int64)))
+        pick = np.random.default_rng(3).random(len(src)) < 0.1
+        s.set_delays(np.stack([src[pick], col[pick]], axis=1), np.full(int(pick.sum()), 2))
+        sims.append(s)
+    a, b = sims
+    for _ in range(2):
+        ma = a.broadcast(3)
+        sa, ra = a.run()
+        mb, sb, rb = b.broadcast_run(3)
+        assert (ma, ra, _nt(sa)) == (mb, rb, _nt(sb))
+        _same(a, b)
+    a.close()
+    b.close()
