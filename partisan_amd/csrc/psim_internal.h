@@ -519,8 +519,15 @@ struct ScArgs {
     uint32_t* nout;
     uint32_t out_cap;
     uint32_t *cnt, *cur, *off, *idx, *bsum;
-    const uint32_t* __restrict__ call_off;    // [n+1] calls of each vertex
-    const uint32_t* __restrict__ calls;       // bit31 = leave, low bits = node / contact
+    // the join / leave calls made since the last round, sorted by vertex
+    // (leaves first, then joins, each in call order): call_v[i] their vertex,
+    // calls[i] bit31 = leave | node / contact; call_start[v] = 1 + index of
+    // v's first call, 0 = none (set by sc_prep, cleared by sc_process)
+    uint32_t* __restrict__ call_start;        // [n]
+    const uint32_t* __restrict__ call_v;      // [ncalls]
+    const uint32_t* __restrict__ calls;       // [ncalls]
+    uint32_t ncalls;
+    const uint8_t* __restrict__ alive_now;    // [n] alive, copied to alive0 by sc_prep
     unsigned long long* __restrict__ stats;   // [16]
     // partisan_peer_service_events:update(Members) as set deltas, per vertex in
     // firing order (C3: consumed by the Plumtree engine); null = not recorded
@@ -609,7 +616,7 @@ struct PdArgs {
     unsigned long long* __restrict__ stats;   // [kPdNStat]
 };
 // messages of a.in bucketed by destination: off[n+1], idx[] (order inside a bucket unspecified)
-hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s);
+hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s, bool zeroed);
 hipError_t launch_pd_init(const PdArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s);
 hipError_t launch_pd_round(const PdArgs& a, hipStream_t s);

@@ -444,6 +444,10 @@ __global__ __launch_bounds__(kBlock) void pd_process(PdArgs a) {
     }
     wq_flush(q, a.nout, a.out, a.out_cap, qerr);          // every lane of the wave: what is still staged
     vals[9] |= qerr;
+    if (v < a.n) {          // zero for the next round's bucket pass (instead of host fills)
+        a.cnt[v] = 0;
+        a.cur[v] = 0;
+    }
     reduce_stats(a, vals);
 }
 
@@ -506,10 +510,11 @@ hipError_t launch_pd_origin(const PdArgs& a, uint32_t root, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s) {
+// zeroed: cnt / cur are known zero (pd_process leaves them so for the next round)
+hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s, bool zeroed) {
     hipError_t e;
-    if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    if (!zeroed && (e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    if (!zeroed && (e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(pd_count, dim3(kPdStrideBlocks), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(pd_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(pd_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
@@ -518,8 +523,16 @@ hipError_t launch_pd_bucket(const PdArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// the round's stats rows and outgoing count zeroed: one launch instead of two fills
+__global__ __launch_bounds__(kBlock) void pd_prep(PdArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < kRoundStatShards * kPdNStat) a.stats[i] = 0ull;
+    if (i == 0) *a.nout = 0u;
+}
+
 hipError_t launch_pd_round(const PdArgs& a, hipStream_t s) {
-    const hipError_t e = launch_pd_bucket(a, s);
+    hipLaunchKernelGGL(pd_prep, dim3(nblk(kRoundStatShards * kPdNStat)), dim3(kBlock), 0, s, a);
+    const hipError_t e = launch_pd_bucket(a, s, true);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(pd_process, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
@@ -701,8 +714,6 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         PdArgs a;
         rc = pd_args(h, *s, a);
         if (rc) return rc;
-        PDCHK(h, hipMemsetAsync(s->stats, 0, kRoundStatShards * kPdNStat * 8, st));
-        PDCHK(h, hipMemsetAsync(s->nmsg + (s->par ^ 1), 0, 4, st));
         PDCHK(h, hipEventRecord(handle_event(h, 2), st));
         PDCHK(h, launch_pd_round(a, st));
         PDCHK(h, hipEventRecord(handle_event(h, 3), st));

@@ -487,7 +487,7 @@ hipError_t launch_win_round(const WinArgs& a, uint32_t* cnt, uint32_t* cur, uint
     b.off = const_cast<uint32_t*>(a.off);
     b.idx = a.idx;
     b.bsum = bsum;
-    hipError_t e = launch_pd_bucket(b, s);
+    hipError_t e = launch_pd_bucket(b, s, false);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(win_round_kernel, dim3(blocks(a.n)), dim3(kBlock), 0, s, a);
     return hipGetLastError();

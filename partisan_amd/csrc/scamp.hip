@@ -361,6 +361,22 @@ __global__ __launch_bounds__(kBlock) void sc_scatter(ScArgs a) {
     }
 }
 
+// Before a round's passes, in one launch: the stats rows and the outgoing
+// queue's count zeroed, alive copied to alive0 (up at the start of the
+// round), and each vertex's first call indexed (call_start).
+__global__ __launch_bounds__(kBlock) void sc_prep(ScArgs a) {
+    const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x, st = gridDim.x * kBlock;
+    for (uint32_t i = i0; i < kRoundStatShards * 16; i += st) a.stats[i] = 0ull;
+    if (i0 == 0) *a.nout = 0u;
+    uint8_t* a0 = const_cast<uint8_t*>(a.alive0);
+    const uint32_t n16 = a.n / 16;
+    for (uint32_t q = i0; q < n16; q += st)
+        reinterpret_cast<uint4*>(a0)[q] = reinterpret_cast<const uint4*>(a.alive_now)[q];
+    for (uint32_t j = n16 * 16 + i0; j < a.n; j += st) a0[j] = a.alive_now[j];
+    for (uint32_t c = i0; c < a.ncalls; c += st)
+        if (c == 0 || a.call_v[c] != a.call_v[c - 1]) a.call_start[a.call_v[c]] = c + 1;
+}
+
 #ifdef C3_PROF
 // [0..4) cycles of the phases calls / sort / inbox / periodic (per wave),
 // [4..11) messages handled by kind, [11] draws in calls, [12] draws in the
@@ -375,7 +391,8 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
     const WaveQ<ScMsg> q{qbuf[threadIdx.x >> 6], &qn[threadIdx.x >> 6]};
     wq_init(q.n);
     uint32_t sent[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t dropped = 0, ndraw = 0, err = 0, resub = 0, nproc = 0, stopped = 0, npv = 0, niv = 0;
+    uint32_t dropped = 0, ndraw = 0, err = 0, resub = 0, nproc = 0, stopped = 0, npv = 0, niv = 0, nev = 0;
+    const uint32_t j0 = v < a.n ? a.call_start[v] : 0u;
     if (v < a.n && !a.alive0[v] && a.head[v].fresh) a.head[v].fresh = 0;
     if (v < a.n && a.alive0[v]) {
         Ctx c;
@@ -397,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         unsigned long long kinds = 0;
 #endif
         // leave calls, then join calls (made since the last round, in call order)
-        for (uint32_t i = a.call_off[v]; i < a.call_off[v + 1]; i++) {
+        for (uint32_t i = j0 ? j0 - 1 : a.ncalls; i < a.ncalls && a.call_v[i] == v; i++) {
             const uint32_t x = a.calls[i];
             if (x >> 31) do_leave(c, x & 0x7FFFFFFFu);
             else if (x != v && a.alive0[x]) do_join(c, x);   // connect/1 succeeds iff the peer is up
@@ -444,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         atomicAdd(&g_sc_prof[12], (unsigned long long)(d3 - d1));
         atomicAdd(&g_sc_prof[13], (unsigned long long)(c.ndraw - d3));
         prof_add(g_sc_prof, 14, 1);
-        if (a.call_off[v + 1] > a.call_off[v]) atomicAdd(&g_sc_prof[15], 1ull);
+        if (j0) atomicAdd(&g_sc_prof[15], 1ull);
         for (int k = 0; k < 7; k++)
             if ((kinds >> (9 * k)) & 511ull) atomicAdd(&g_sc_prof[4 + k], (kinds >> (9 * k)) & 511ull);
 #endif
@@ -456,11 +473,17 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
             niv = c.h.niv;
         }
         a.head[v] = c.h;
-        if (a.ev_cnt) a.ev_cnt[v] = c.nev;
+        nev = c.nev;
         for (int i = 0; i < 7; i++) sent[i] = c.sent[i];
         dropped = c.dropped; ndraw = c.ndraw; err = c.err; resub = c.resub;
     }
     wq_flush(q, a.nout, a.out, a.out_cap, err);           // every lane of the wave: what is still staged
+    if (v < a.n) {          // what the next round expects zero (instead of host fills before it)
+        if (j0) a.call_start[v] = 0;
+        a.cnt[v] = 0;
+        a.cur[v] = 0;
+        if (a.ev_cnt) a.ev_cnt[v] = nev;
+    }
     // counters: [1..6] sent by kind, 7 dropped, 8 processed, 9 draws, 10 stopped,
     // 11 error bits (OR), 12 pv_sum, 13 inview_sum, 14 resub
     unsigned long long vals[15];
@@ -514,9 +537,10 @@ hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hip
 }
 
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s) {
-    hipError_t e;
-    if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+    // cnt / cur / call_start / ev_cnt were left zero by the last sc_process
+    uint32_t w = a.n / 16 > a.ncalls ? a.n / 16 : a.ncalls;
+    if (w < kRoundStatShards * 16) w = kRoundStatShards * 16;
+    hipLaunchKernelGGL(sc_prep, dim3(nblk(w) < 2048u ? nblk(w) : 2048u), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sc_count, dim3(kScStrideBlocks), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sc_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sc_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
@@ -547,7 +571,7 @@ struct ScState : ModuleState {
     ScMsg* msg[2] = {nullptr, nullptr};
     uint32_t* nmsg = nullptr;
     uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
-    uint32_t *call_off = nullptr, *calls = nullptr, *list = nullptr;
+    uint32_t *call_start = nullptr, *call_v = nullptr, *calls = nullptr, *list = nullptr;
     size_t calls_cap = 0, list_cap = 0;
     unsigned long long* stats = nullptr;
     uint32_t* ev_cnt = nullptr;     // update events (C3), allocated on demand
@@ -556,8 +580,8 @@ struct ScState : ModuleState {
     uint64_t round = 0;
     std::vector<uint32_t> cv, cx;   // calls since the last round: vertex, (bit31 = leave) | target
     ~ScState() override {
-        void* p[] = {head, pv, iv, alive, alive0, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, call_off, calls,
-                     list, stats, ev_cnt, ev};
+        void* p[] = {head, pv, iv, alive, alive0, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, call_start, call_v,
+                     calls, list, stats, ev_cnt, ev};
         for (void* x : p)
             if (x) (void)hipFree(x);
     }
@@ -590,7 +614,9 @@ ScArgs sc_args(const psim_handle* h, const ScState& s) {
     a.out = s.msg[s.par ^ 1]; a.nout = s.nmsg + (s.par ^ 1);
     a.out_cap = s.cap;
     a.cnt = s.cnt; a.cur = s.cur; a.off = s.off; a.idx = s.idx; a.bsum = s.bsum;
-    a.call_off = s.call_off; a.calls = s.calls;
+    a.call_start = s.call_start; a.call_v = s.call_v; a.calls = s.calls;
+    a.ncalls = 0;
+    a.alive_now = s.alive;
     a.stats = s.stats;
     a.ev_cnt = s.ev_cnt;
     a.ev = s.ev;
@@ -599,32 +625,32 @@ ScArgs sc_args(const psim_handle* h, const ScState& s) {
 
 int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     const hipStream_t st = handle_stream(h);
-    // calls grouped by vertex: leaves first, then joins, each in call order
-    std::vector<uint32_t> off(s.n + 1, 0);
-    for (uint32_t v : s.cv) off[v + 1]++;
-    for (uint32_t v = 0; v < s.n; v++) off[v + 1] += off[v];
-    std::vector<uint32_t> lst(s.cv.size());
-    {
-        std::vector<uint32_t> fill(off.begin(), off.end() - 1);
-        for (int pass = 0; pass < 2; pass++)
-            for (size_t i = 0; i < s.cv.size(); i++)
-                if ((s.cx[i] >> 31) == (pass == 0 ? 1u : 0u)) lst[fill[s.cv[i]]++] = s.cx[i];
-    }
-    if (lst.size() > s.calls_cap) {
+    // calls sorted by vertex: leaves first, then joins, each in call order
+    // (sc_prep indexes each vertex's first one on the device)
+    const size_t k = s.cv.size();
+    std::vector<uint32_t> ord(k), cv(k), cx(k);
+    for (size_t i = 0; i < k; i++) ord[i] = uint32_t(i);
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t jx = (s.cx[x] >> 31) ^ 1u, jy = (s.cx[y] >> 31) ^ 1u;   // leave (bit31) first
+        return s.cv[x] != s.cv[y] ? s.cv[x] < s.cv[y] : jx < jy;
+    });
+    for (size_t i = 0; i < k; i++) { cv[i] = s.cv[ord[i]]; cx[i] = s.cx[ord[i]]; }
+    if (k > s.calls_cap) {
         if (s.calls) (void)hipFree(s.calls);
-        s.calls = nullptr;
-        s.calls_cap = std::max<size_t>(lst.size(), 2 * s.calls_cap);
-        if (!sc_alloc((void**)&s.calls, s.calls_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "scamp: call list");
+        if (s.call_v) (void)hipFree(s.call_v);
+        s.calls = s.call_v = nullptr;
+        s.calls_cap = std::max<size_t>(k, 2 * s.calls_cap);
+        if (!sc_alloc((void**)&s.calls, s.calls_cap * 4) || !sc_alloc((void**)&s.call_v, s.calls_cap * 4))
+            return handle_fail(h, PSIM_ENOMEM, "scamp: call list");
     }
-    SCCHK(h, hipMemcpyAsync(s.call_off, off.data(), (s.n + 1) * 4, hipMemcpyHostToDevice, st));
-    if (!lst.empty()) SCCHK(h, hipMemcpyAsync(s.calls, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, st));
+    if (k) {
+        SCCHK(h, hipMemcpyAsync(s.call_v, cv.data(), k * 4, hipMemcpyHostToDevice, st));
+        SCCHK(h, hipMemcpyAsync(s.calls, cx.data(), k * 4, hipMemcpyHostToDevice, st));
+    }
     s.cv.clear();
     s.cx.clear();
-    SCCHK(h, hipMemcpyAsync(s.alive0, s.alive, s.n, hipMemcpyDeviceToDevice, st));
-    if (s.ev_cnt) SCCHK(h, hipMemsetAsync(s.ev_cnt, 0, size_t(s.n) * 4, st));
-    SCCHK(h, hipMemsetAsync(s.stats, 0, kRoundStatShards * 16 * 8, st));
-    SCCHK(h, hipMemsetAsync(s.nmsg + (s.par ^ 1), 0, 4, st));
     ScArgs a = sc_args(h, s);
+    a.ncalls = uint32_t(k);
     SCCHK(h, hipEventRecord(handle_event(h, 0), st));
     SCCHK(h, launch_sc_round(a, st));
     SCCHK(h, hipEventRecord(handle_event(h, 1), st));
@@ -734,7 +760,7 @@ int psim_scamp_setup(psim_handle* h, uint32_t n, uint32_t version, uint32_t c, u
                     sc_alloc((void**)&s->msg[1], size_t(s->cap) * sizeof(ScMsg)) && sc_alloc((void**)&s->nmsg, 16) &&
                     sc_alloc((void**)&s->cnt, N * 4) && sc_alloc((void**)&s->cur, N * 4) &&
                     sc_alloc((void**)&s->off, (N + 1) * 4) && sc_alloc((void**)&s->idx, size_t(s->cap) * 4) &&
-                    sc_alloc((void**)&s->bsum, size_t(nb) * 4) && sc_alloc((void**)&s->call_off, (N + 1) * 4) &&
+                    sc_alloc((void**)&s->bsum, size_t(nb) * 4) && sc_alloc((void**)&s->call_start, N * 4) &&
                     sc_alloc((void**)&s->stats, kRoundStatShards * 16 * 8);
     if (!ok) {
         delete s;
