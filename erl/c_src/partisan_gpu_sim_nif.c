@@ -242,6 +242,7 @@ static ERL_NIF_TERM nif_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[])
     if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &maxr)) return enif_make_badarg(env);
     enum { CAP = 4096 };
     psim_round_stats* st = (psim_round_stats*)enif_alloc(CAP * sizeof(psim_round_stats));
+    if (!st) return err(env, PSIM_ENOMEM);
     uint32_t ran = 0;
     enif_mutex_lock(r->mu);
     int rc = psim_run(r->h, maxr, st, CAP, &ran);
@@ -253,6 +254,29 @@ static ERL_NIF_TERM nif_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[])
     return enif_make_tuple3(env, mk_atom(env, "ok"), enif_make_uint(env, ran), list);
 }
 
+/* broadcast_run(Sim, Root, MaxRounds) -> {ok, Id, Rounds, [StatsMap]}: one heartbeat
+ * interval of one root, broadcast then rounds to quiescence in one call
+ * (psim_plumtree_broadcast_run) */
+static ERL_NIF_TERM nif_broadcast_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root, maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root) || !enif_get_uint(env, argv[2], &maxr))
+        return enif_make_badarg(env);
+    enum { CAP = 4096 };
+    psim_round_stats* st = (psim_round_stats*)enif_alloc(CAP * sizeof(psim_round_stats));
+    if (!st) return err(env, PSIM_ENOMEM);
+    uint32_t ran = 0, mono = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_broadcast_run(r->h, root, &mono, maxr, st, CAP, &ran);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (uint32_t i = ran < CAP ? ran : CAP; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    return enif_make_tuple4(env, mk_atom(env, "ok"), enif_make_uint(env, mono), enif_make_uint(env, ran), list);
+}
+
 /* step(Sim, Rounds) -> {ok, [StatsMap]} */
 static ERL_NIF_TERM nif_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
@@ -261,6 +285,7 @@ static ERL_NIF_TERM nif_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &k) || k == 0 || k > 65536)
         return enif_make_badarg(env);
     psim_round_stats* st = (psim_round_stats*)enif_alloc(k * sizeof(psim_round_stats));
+    if (!st) return err(env, PSIM_ENOMEM);
     enif_mutex_lock(r->mu);
     int rc = psim_step(r->h, k, st, k);
     enif_mutex_unlock(r->mu);
@@ -1607,6 +1632,7 @@ static ErlNifFunc funcs[] = {
     {"broadcast_many", 2, nif_broadcast_many, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"broadcast_run", 3, nif_broadcast_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},

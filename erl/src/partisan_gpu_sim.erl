@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, restart_backend/2, broadcast/2, broadcast_many/2,
-         step/2, run/2,
+         step/2, run/2, broadcast_run/3,
          peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, is_delivered/3, rows/2, messages/1, shard_step/2,
          relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
@@ -72,6 +72,10 @@ step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 
 -spec run(sim(), pos_integer()) -> {ok, non_neg_integer(), [map()]} | error().
 run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
+%% one heartbeat interval of one root: broadcast/2 then run/2 in one call
+-spec broadcast_run(sim(), non_neg_integer(), pos_integer()) ->
+    {ok, non_neg_integer(), non_neg_integer(), [map()]} | error().
+broadcast_run(_Sim, _Root, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 
 -spec peers(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
 peers(_Sim) -> erlang:nif_error(nif_not_loaded).

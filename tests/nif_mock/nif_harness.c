@@ -169,6 +169,20 @@ int main(int argc, char** argv) {
                     (unsigned long long)dmsum, mock_list_len(mock_elem(ms, 1)), mock_list_len(mock_elem(rw, 1)),
                     (unsigned long long)one);
         }
+        {   /* root 0's second heartbeat in one call: broadcast_run (broadcast + run to quiescence) */
+            ERL_NIF_TERM br = want_ok_tuple("broadcast_run", call("broadcast_run", 3, A(sim, mock_uint(0), mock_uint(1000))));
+            ERL_NIF_TERM st2 = mock_elem(br, 3);
+            uint64_t b2 = 0, y;
+            for (size_t i = 0; i < mock_list_len(st2); i++)
+                if (mock_map_get(mock_list_nth(st2, i), "broadcast", &y)) b2 += y;
+            ERL_NIF_TERM th2 = mock_elem(want_ok_tuple("trace_hash", call("trace_hash", 1, A(sim))), 1);
+            fprintf(g_out, ", \"c2_hb2\": {\"mono\": %llu, \"rounds\": %llu, \"broadcasts\": %llu, "
+                    "\"trace\": [\"%llu\", \"%llu\", \"%llu\", \"%llu\"]}",
+                    (unsigned long long)mock_int(mock_elem(br, 1)), (unsigned long long)mock_int(mock_elem(br, 2)),
+                    (unsigned long long)b2, (unsigned long long)mock_int(mock_elem(th2, 0)),
+                    (unsigned long long)mock_int(mock_elem(th2, 1)), (unsigned long long)mock_int(mock_elem(th2, 2)),
+                    (unsigned long long)mock_int(mock_elem(th2, 3)));
+        }
         /* the same overlay, vertex-sharded at world 1 with the library's own RCCL communicator */
         ERL_NIF_TERM sim7 = new_sim(0x5EED0002ull);
         ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);

@@ -159,4 +159,10 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rounds == rep["c2"]["rounds"]
     assert sum(x["broadcast"] for x in stats) == rep["c2"]["broadcasts"]
     assert [str(x) for x in sim.trace_hash()] == rep["c2"]["trace"]
+    # root 0's second heartbeat: the NIF's broadcast_run = broadcast + run here
+    assert sim.broadcast(0) == rep["c2_hb2"]["mono"]
+    stats, rounds = sim.run(1000)
+    assert rounds == rep["c2_hb2"]["rounds"]
+    assert sum(x["broadcast"] for x in stats) == rep["c2_hb2"]["broadcasts"]
+    assert [str(x) for x in sim.trace_hash()] == rep["c2_hb2"]["trace"]
     sim.close()
