@@ -868,6 +868,19 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     // first chunk's (its kernel seeded the focused lane's hold ring)
     bool pend = h->origin_pend;
     h->origin_pend = false;
+    // the origin's counters into the focused lane (after the stream synchronised)
+    auto settle_origin = [&]() -> int {
+        unsigned long long r[kNStat];
+        reduce_row(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, r);
+        if (r[S_OVERFLOW])
+            return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat)",
+                        r[S_OVERFLOW]);
+        auto& l = h->lanes[focus];
+        l.ost_cnt += (int64_t)r[S_OST_DELTA];
+        l.live_rows += (int64_t)r[S_LIVE_DELTA];
+        l.inflight = r[PSIM_MSG_BROADCAST];
+        return PSIM_OK;
+    };
     bool done = !pend && stop_q && all_quiet();
     bool seeded = false;
     while (!done && ran < max_rounds) {
@@ -948,15 +961,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
         if (pend) {     // the origin's row (broadcast_common), then the rounds as if it had been read first
             pend = false;
-            unsigned long long r[kNStat];
-            reduce_row(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, r);
-            if (r[S_OVERFLOW])
-                return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older "
-                            "heartbeat)", r[S_OVERFLOW]);
-            auto& l = h->lanes[focus];
-            l.ost_cnt += (int64_t)r[S_OST_DELTA];
-            l.live_rows += (int64_t)r[S_LIVE_DELTA];
-            l.inflight = r[PSIM_MSG_BROADCAST];
+            if (const int rc = settle_origin()) return rc;
             // a quiet origin (no live eager peer): the chunk's rounds were no-ops
             if (stop_q && all_quiet()) break;
         }
@@ -1012,6 +1017,10 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             ran++;
             if (stop_q && all_quiet()) { done = true; break; }
         }
+    }
+    if (pend) {         // max_rounds 0: the origin's row is still to be read
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (const int rc = settle_origin()) return rc;
     }
     load_lane(h, focus);
     if (ran_out) *ran_out = ran;

@@ -1139,6 +1139,14 @@ def test_broadcast_run_matches_broadcast_then_run(psim):
     a.set_alive(np.ones(n, np.uint8))
     b.set_alive(np.ones(n, np.uint8))
     both(r)
+    # max_rounds 0: the origin alone (its counters are read without a chunk), then the rounds
+    ma = a.broadcast(r)
+    mb, sb0, rb0 = b.broadcast_run(r, max_rounds=0)
+    assert (ma, rb0, sb0) == (mb, 0, [])
+    sa, ra = a.run()
+    sb, rb = b.run()
+    assert (ra, _nt(sa)) == (rb, _nt(sb))
+    _same(a, b)
     if psim.engine != "binned":       # binned handles keep one root
         a.broadcast(17)
         b.broadcast(17)
