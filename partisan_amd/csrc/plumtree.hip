@@ -1518,6 +1518,65 @@ __device__ __forceinline__ void pt_origin_body(const PtArgs& a) {
     if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
 }
 
+// One root's origin by the 64 lanes of a wave, lane s on peer slot s (rows of
+// <= 64 slots: every row, kMaxDeg = 32): its pushes are issued together, where
+// pt_origin_body walks the slots one after another (a store, a flag claim and
+// a list push per slot, each waiting on the last: ~14 us of the step).  The
+// same counts and state as pt_origin_body; worklist and bin record order
+// differ, which no consumer reads.
+__device__ __forceinline__ void pt_origin_wave(const PtArgs& a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t v = a.root;
+    PtArgs ao = a;
+    ao.m_w = a.m_s;
+    const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
+    const uint32_t deg = a.ell ? a.ell : a.rowp[v + 1] - rs;
+    const uint4 st = a.vs[v];
+    uint32_t eager = st.x, lazy = st.y, outst = st.z;
+    uint32_t ep = st.w >> 24;
+    if (ep != a.epoch8) { eager = a.memb[v]; lazy = 0; ep = a.epoch8; }
+    const uint32_t outst0 = outst;
+    const uint32_t b = lane < 32u ? 1u << lane : 0u;
+    bool sent = false, stored = false, live = false;
+    if (lane < deg) {
+        const uint32_t e = rs + lane;
+        if (eager & b) {
+            sent = true;
+            if (!omitted(a, e)) {
+                stored = true;
+                if (a.rec_c) {                           // binned: a record for the next route
+                    const uint32_t cs = (a.col[e] >> a.cv_shift) * kCoarseShards + ((v >> a.fv_shift) & (kCoarseShards - 1));
+                    a.rec_c[a.csub[cs] + atomicAdd(&a.cnt_c_nxt[cs], 1u)] =
+                        make_uint2(a.rev[e], PSIM_MSG_BROADCAST | (a.wtag << kTagShift));
+                } else {
+                    deliver_word(ao, e, PSIM_MSG_BROADCAST | (a.wtag << kTagShift), a.dhist,   // Round 0
+                                 a.wl_nxt ? 2u : 1u);
+                }
+            }
+        }
+        if ((lazy & b) && !(outst & b)) live = bit_alive(a.alive, a.col[e]);
+    }
+    const uint32_t nmsg = (uint32_t)__popcll(__ballot(sent)), nword = (uint32_t)__popcll(__ballot(stored));
+    const unsigned long long add_live = (unsigned long long)__popcll(__ballot(live));
+    const uint32_t dm = deg >= 32u ? ~0u : (1u << deg) - 1u;
+    outst |= lazy & dm;                                  // schedule_lazy_push: a row per lazy peer
+    if (lane != 0) return;
+    unsigned long long flags = outst0 ? 4ull : 0ull;
+    a.vs[v] = make_uint4(eager, lazy, outst, 0u | (a.mono8 << 16) | (ep << 24));
+    if ((outst0 != 0) != (outst != 0)) {
+        a.ost[v] = 1;
+        if (a.obin) a.obin[v >> a.fv_shift] += 1u;
+        atomicAdd(&a.stats[S_OST_DELTA], 1ull);
+        atomicAdd(a.ost_total, 1);
+        if (int* d = hold_delta(ao)) atomicAdd(d, 1);
+    }
+    if (add_live) atomicAdd(&a.stats[S_LIVE_DELTA], add_live);
+    if (nmsg) atomicAdd(&a.stats[PSIM_MSG_BROADCAST], (unsigned long long)nmsg);
+    if (nword) atomicAdd(&a.stats[S_WORDS], (unsigned long long)nword);
+    if (nmsg && a.mcnt) atomicAdd(&a.mcnt[a.m_s * 64], nmsg);
+    if (flags) atomicOr(&a.stats[S_OVERFLOW], flags);
+}
+
 // prep != 0: first the fills the host used to enqueue before an origin, by
 // this block -- the stats row (prep words) zeroed, the lane's count area
 // zeroed and its hold ring seeded with `hold` (psim_host.hip seed_hold_ring)
@@ -1531,8 +1590,8 @@ __global__ void pt_origin_kernel(PtArgs a, uint32_t prep, uint32_t hold) {
         __threadfence();
         __syncthreads();
     }
-    if (threadIdx.x != 0) return;
-    pt_origin_body(a);
+    if (threadIdx.x >= 64) return;
+    pt_origin_wave(a);
 }
 
 // The fills before a chunk of rounds (psim_host.hip drive): its stats rows

@@ -84,7 +84,7 @@ struct psim_handle {
         uint32_t fv_shift = 0, cv_shift = 0, nf = 0, nc = 0, chunks = 0;
         std::vector<uint32_t> h_csub, h_fslot;
     } bin;
-    unsigned long long* stats = nullptr;     // [kChunk * kMaxLanes + 1][kStatsRow]; the last row: a deferred origin's
+    unsigned long long* stats = nullptr;     // [kChunk * kMaxLanes + 1][kStatsRow] (+1: a deferred origin's row 0)
     unsigned long long* h_stats = nullptr;   // pinned mirror
     bool origin_pend = false;                // psim_plumtree_broadcast_run: the origin's row not read back yet
     psim::PtArgs* lane_args = nullptr;       // [kChunk][kMaxLanes] per-round lane arguments (device)
@@ -871,7 +871,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
     // the origin's counters into the focused lane (after the stream synchronised)
     auto settle_origin = [&]() -> int {
         unsigned long long r[kNStat];
-        reduce_row(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, r);
+        reduce_row(h->h_stats, r);                                   // row 0: the origin's
         if (r[S_OVERFLOW])
             return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat)",
                         r[S_OVERFLOW]);
@@ -892,6 +892,9 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         for (int j = 0; j < (int)h->lanes.size(); j++)
             if (j == focus || !lane_quiescent(h, h->lanes[j])) act.push_back(j);
         const size_t A = act.size();
+        // the first chunk after a deferred origin keeps its rows behind the
+        // origin's (row 0), so one copy brings both back
+        const size_t r0 = pend ? 1u : 0u;
         // inbox parities advance on a copy, committed once every launch of the
         // chunk is enqueued (a failed launch leaves the lanes' parities alone)
         std::vector<uint32_t> par(A);
@@ -903,7 +906,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         }
         auto lane_args = [&](size_t q, uint32_t i, uint32_t tick) {
             load_lane(h, act[q]);
-            PtArgs a = make_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
+            PtArgs a = make_args(h, par[q], tick, h->stats + (r0 + i * A + q) * kStatsRow);
             set_round_slots(h, a, h->round + i + 1);
             set_round_tags(a, h->round + i + 1);
             if (h->dly) set_round_ring(h, a, h->round + i + 1);
@@ -912,7 +915,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         };
         {   // the chunk's stats rows zeroed and (first chunk) every lane's hold ring seeded: one launch
             PtPrep pp{};
-            pp.z = h->stats;
+            pp.z = h->stats + r0 * kStatsRow;
             pp.nz = uint64_t(k) * A * kStatsRow;
             if (!seeded) prep_seeds(h, h->round + 1, pp, pend ? focus : -1);
             seeded = true;
@@ -923,7 +926,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         // a window lane's round: bucket its records, handle them (ptwin.hip)
         auto win_round = [&](size_t q, uint32_t i, uint32_t tick) -> hipError_t {
             load_lane(h, act[q]);
-            const WinArgs a = make_win_args(h, par[q], tick, h->stats + (i * A + q) * kStatsRow);
+            const WinArgs a = make_win_args(h, par[q], tick, h->stats + (r0 + i * A + q) * kStatsRow);
             par[q] ^= 1u;
             const hipError_t e = hipMemsetAsync(a.nout, 0, 4, h->stream);
             if (e != hipSuccess) return e;
@@ -954,7 +957,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             }
         }
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
-        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * A * kStatsRow * sizeof(unsigned long long),
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, (r0 + k * A) * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         float chunk_ms = 0.f;
@@ -972,7 +975,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
             uint64_t msgs = 0;
             for (size_t q = 0; q < A; q++) {
                 unsigned long long r[kNStat];
-                reduce_row(h->h_stats + (i * A + q) * kStatsRow, r);
+                reduce_row(h->h_stats + (r0 + i * A + q) * kStatsRow, r);
                 if (r[S_OVERFLOW]) {
                     load_lane(h, focus);
                     return fail(h, PSIM_EOVERFLOW,
@@ -991,7 +994,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
                 if (h->dly) {                   // round R consumed its arrivals; the sends are pending
                     const uint64_t R = h->round + 1;
                     l.due[R & (kRing - 1)] = 0;
-                    l.inflight = add_due(l.due, R, h->h_stats + (i * A + q) * kStatsRow + size_t(kStatShards) * kNStat);
+                    l.inflight = add_due(l.due, R, h->h_stats + (r0 + i * A + q) * kStatsRow + size_t(kStatShards) * kNStat);
                 }
                 msgs += lm;
                 for (int t = 0; t < kNStat; t++) tot[t] += r[t];
@@ -1019,6 +1022,8 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         }
     }
     if (pend) {         // max_rounds 0: the origin's row is still to be read
+        HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         if (const int rc = settle_origin()) return rc;
     }
@@ -1968,15 +1973,12 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
             // origin emits into the buffer the next round reads; its kernel
             // first zeroes its stats row and the lane's count area and seeds
             // the hold ring with the holders before the origin's own change
-            unsigned long long* row = defer ? h->stats + size_t(kChunk) * kMaxLanes * kStatsRow : h->stats;
-            PtArgs a = make_args(h, h->par ^ 1u, 0, row);
+            PtArgs a = make_args(h, h->par ^ 1u, 0, h->stats);      // row 0 (a deferred one: drive reads it)
             set_round_slots(h, a, h->round + 1);     // the origin's pushes count as round h->round's
             a.wtag = uint32_t(h->round + 1) & 0xFFu; // read by the next round
             a.root = lr;
             HIPCHK(h, launch_pt_origin(a, h->stream, uint32_t(kStatsRow), uint32_t(h->ost_cnt)));
             if (defer) {                        // read back with the first chunk of rounds (drive)
-                HIPCHK(h, hipMemcpyAsync(h->h_stats + size_t(kChunk) * kMaxLanes * kStatsRow, row,
-                                         kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
                 h->origin_pend = true;
                 return PSIM_OK;
             }
