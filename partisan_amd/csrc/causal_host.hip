@@ -106,13 +106,9 @@ int psim_causal_shard_setup(psim_handle* h, uint32_t n, uint32_t m, uint32_t per
                     A((void**)&c.base, size_t(kCsWindow) * kCsLanes * kCsLanes * 4) &&
                     A((void**)&c.delivered, N * 8) && A((void**)&c.stats, kStatShards * kCsNStat * 8) &&
                     hipHostMalloc((void**)&c.h_stats, kStatShards * kCsNStat * 8, 0) == hipSuccess;
-#ifndef CS_NO_DELAY_RING
     // each message's delay drawn once, in the round after its broadcast, and
     // kept until it lands, instead of redrawn in each round of its window
     const bool ring_ok = !ok || dmax > kCsRingMax || A((void**)&c.dring, N * kCsLanes * 4);
-#else
-    const bool ring_ok = true;
-#endif
     if (!ok || !ring_ok) {
         cs_reset(h);
         return handle_fail(h, PSIM_ENOMEM, "causal state for n=%u", n);

@@ -104,11 +104,8 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
             const unsigned long long rn_prev = a.rmnew_prev[v];
             const uint32_t calls0 = a.ncall_prev[v] + (uint32_t)__popcll(rn_prev);   // calls before this round
             unsigned long long rn = 0;
-#ifndef DM_TEMPORAL_INBOX   // the inbox planes are read once (then cleared): non-temporal, ~1-3 % per C4 round
+            // the inbox planes are read once (then cleared): non-temporal, ~1-3 % per C4 round
             const unsigned long long any = __builtin_nontemporal_load(a.rm_cur_any + i);
-#else
-            const unsigned long long any = a.rm_cur_any[i];
-#endif
             if (any) {
                 const unsigned long long multi = a.rm_cur_multi[i], tri = a.rm_cur_tri[i];
                 a.rm_cur_any[i] = 0;
@@ -146,7 +143,6 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
             const uint32_t cnt = np < kDmPushCap ? np : kDmPushCap;
             if (np > a.push_cap) c.overflow |= 1u;
             const uint32_t* lst = a.pushlist_cur + (size_t)i * kDmPushCap;
-#ifndef DM_NO_FAST_AE
             if (cnt <= kDmFastPush) {
                 // the usual case (Poisson(2) in-degree): the list in registers,
                 // sorted there, and every pusher's snapshot requested at once --
@@ -174,9 +170,7 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
                     a.pull_nxt[2 * (size_t)x[j] + (sp.x == v ? 0u : 1u)] = s;   // {pull, MyNode, OurMessages}
                     c.pull++;
                 }
-            } else
-#endif
-            {
+            } else {
             uint32_t last = 0;
             bool first = true;
             for (uint32_t k = 0; k < cnt; k++) {                     // senders in id order
@@ -198,12 +192,9 @@ __global__ __launch_bounds__(kBlock) void dm_round_kernel(DmArgs a) {
         }
 
         // ---- anti-entropy pull: handle_info({pull, _, Messages}) :178-195
-#ifndef DM_TEMPORAL_INBOX   // the inbox sets are read once (then cleared): non-temporal, ~1-3 % per C4 round
+        // the inbox sets are read once (then cleared): non-temporal, ~1-3 % per C4 round
         const unsigned long long p0 = __builtin_nontemporal_load(a.pull_cur + 2 * (size_t)i),
                                  p1 = __builtin_nontemporal_load(a.pull_cur + 2 * (size_t)i + 1);
-#else
-        const unsigned long long p0 = a.pull_cur[2 * (size_t)i], p1 = a.pull_cur[2 * (size_t)i + 1];
-#endif
         if (p0 | p1) {
             s |= p0 | p1;
             if (p0) a.pull_cur[2 * (size_t)i] = 0;

@@ -33,10 +33,7 @@ __device__ __forceinline__ bool alive_of(const HvArgs& a, uint32_t v) { return (
 // set operations of the reference (ordsets add / del / member, pick_random's
 // filter, the exchange list's usort) are ballots, popcounts and shuffles.
 // Nothing is indexed at run time from a private array, so nothing spills.
-#ifndef HV_STAGE
-#define HV_STAGE 32
-#endif
-constexpr uint32_t kHvStage = HV_STAGE;   // records a wave stages in LDS before one reservation
+constexpr uint32_t kHvStage = 32;   // records a wave stages in LDS before one reservation
 struct W {
     const HvArgs* a;
     uint32_t* stage;               // this wave's LDS staging: kHvStage records of 16 dwords
@@ -604,10 +601,7 @@ __device__ __forceinline__ In load_msg(const HvArgs& a, uint32_t i) {
 // until a timer round -- where every live vertex runs -- has about as many
 // waves as the chip holds (hv_group): at 10k vertices 64-vertex groups made
 // 157 waves of 64 vertices each.
-#ifndef HV_WAVES_PER_EU
-#define HV_WAVES_PER_EU 4
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HV_WAVES_PER_EU))) void hv_process(HvArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void hv_process(HvArgs a) {
     __shared__ uint32_t stage_all[kHvWaves][kHvStage * 16];
     const uint32_t l = lane_id();
     const uint32_t gw = blockIdx.x * kHvWaves + (threadIdx.x >> 6), nw = gridDim.x * kHvWaves;
@@ -782,17 +776,15 @@ __global__ __launch_bounds__(kBlock) void hv_init_kernel(HvArgs a) {
 
 inline uint32_t nblk(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 // hv_process: vertices per wave -- the smallest power of two that leaves at
-// most HV_WAVE_TARGET waves, so that a timer round at 10k vertices runs 1250
+// most kHvWaveTarget waves, so that a timer round at 10k vertices runs 1250
 // waves of 8 vertices (0.082 ms per C2 round against 0.247 with groups of
 // 64 and 0.136 with groups of 2: each wave also pays its staging flush and
 // counter atomics) and one above 128k vertices keeps groups of 64 (groups of
 // 8 measured 2.4x slower at 1M, where the chip is full anyway)
-#ifndef HV_WAVE_TARGET
-#define HV_WAVE_TARGET 2048
-#endif
+constexpr uint32_t kHvWaveTarget = 2048;
 inline uint32_t hv_group(uint32_t n) {
     uint32_t g = 1;
-    while (g < 64 && uint64_t(g) * HV_WAVE_TARGET < n) g <<= 1;
+    while (g < 64 && uint64_t(g) * kHvWaveTarget < n) g <<= 1;
     return g;
 }
 // grid-striding beyond 64K workgroups
