@@ -141,7 +141,7 @@ int psim_causal_step(psim_handle* h, uint32_t rounds, psim_causal_stats* out, si
         HIPCHK(h, launch_cs_broadcast(a, handle_stream(h)));
         HIPCHK(h, hipEventRecord(handle_event(h, 1), handle_stream(h)));
         HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, handle_stream(h)));
-        HIPCHK(h, hipStreamSynchronize(handle_stream(h)));
+        HIPCHK(h, handle_wait(h));
         c.round = t;
         unsigned long long r[kCsNStat] = {0};
         unsigned long long err = 0;
@@ -199,7 +199,7 @@ int psim_causal_shard_round(psim_handle* h, void* slab, psim_causal_stats* out) 
     HIPCHK(h, hipEventRecord(handle_event(h, 1), handle_stream(h)));
     HIPCHK(h, hipMemcpyAsync(slab, sl, kCsLanes * kCsLanes * 4, hipMemcpyDeviceToDevice, handle_stream(h)));
     HIPCHK(h, hipMemcpyAsync(c.h_stats, c.stats, kStatShards * kCsNStat * 8, hipMemcpyDeviceToHost, handle_stream(h)));
-    HIPCHK(h, hipStreamSynchronize(handle_stream(h)));
+    HIPCHK(h, handle_wait(h));
     c.round = t;
     unsigned long long r[kCsNStat] = {0};
     unsigned long long err = 0;

@@ -672,7 +672,7 @@ int psim_demers_shard_round(psim_handle* h, void* rm_shadow, void* pull_shadow, 
     DMCHK(h, hipEventRecord(handle_event(h, 1), s));
     std::vector<unsigned long long> hs(size_t(kStatShards) * kNStat);
     DMCHK(h, hipMemcpyAsync(hs.data(), d->stats, hs.size() * 8, hipMemcpyDeviceToHost, s));
-    DMCHK(h, hipStreamSynchronize(s));
+    DMCHK(h, handle_wait(h));
     unsigned long long r[kNStat];
     reduce_stats(hs.data(), r);
     float ms = 0.f;

@@ -217,7 +217,7 @@ int psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* out, size_t cap
             v.par ^= 1u;
         }
         HIPCHK(h, hipMemcpyAsync(v.h_stats, v.stats, size_t(k) * kHvNStat * 8, hipMemcpyDeviceToHost, handle_stream(h)));
-        HIPCHK(h, hipStreamSynchronize(handle_stream(h)));
+        HIPCHK(h, handle_wait(h));
         for (uint32_t i = 0; i < k; i++) {
             const unsigned long long* r = v.h_stats + size_t(i) * kHvNStat;
             const uint64_t t = v.round + i + 1;

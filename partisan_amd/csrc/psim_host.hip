@@ -102,6 +102,7 @@ struct psim_handle {
     uint32_t wl_gpc = 0;                     // listed groups per ELL chunk, 0: spread (PSIM_WL_GPC A/B knob)
     uint32_t ell_grid = 0;                   // grid of the ELL round kernel (resident workgroups)
     hipEvent_t ev[2 * kChunk] = {};
+    hipEvent_t ev_done = nullptr;            // end of a chunk's work, polled (chunk_wait)
 
     uint32_t par = 0;          // inbox buffer the next round reads
     uint64_t round = 0;        // rounds completed (lazy-tick schedule)
@@ -845,6 +846,18 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
 // Launch up to max_rounds rounds in chunks; with stop_q, stop after the first
 // round that leaves the system quiescent (trailing rounds of the chunk were
 // no-ops and are not counted: they change no state).
+// The end of a chunk's work, by polling an event instead of a blocking
+// stream synchronisation: the host learns of it within a microsecond or so,
+// where the blocking wait's wake-up was part of the idle time between two
+// heartbeat intervals on the device.
+hipError_t chunk_wait(psim_handle* h) {
+    hipError_t e = hipEventRecord(h->ev_done, h->stream);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(h->ev_done)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
 int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
           uint32_t* ran_out) {
     uint32_t ran = 0;
@@ -959,7 +972,7 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
         for (size_t q = 0; q < A; q++) h->lanes[act[q]].par = par[q];
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, (r0 + k * A) * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, chunk_wait(h));
         float chunk_ms = 0.f;
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
         if (pend) {     // the origin's row (broadcast_common), then the rounds as if it had been read first
@@ -1293,7 +1306,7 @@ int forest_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, siz
         h->par = par;
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, k * kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, chunk_wait(h));
         float chunk_ms = 0.f;
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
         for (uint32_t i = 0; i < k; i++) {
@@ -1363,6 +1376,7 @@ void handle_add_round(psim_handle* h, double kernel_ms) {
     h->rounds_total++;
 }
 hipEvent_t handle_event(psim_handle* h, int i) { return h->ev[i]; }
+hipError_t handle_wait(psim_handle* h) { return chunk_wait(h); }
 
 }  // namespace psim
 
@@ -1442,6 +1456,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         h->ost_total = h->ost_total_base;
         for (auto& e : h->ev)
             if (hipEventCreate(&e) != hipSuccess) { rc = PSIM_EHIP; break; }
+        if (hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) != hipSuccess) { rc = PSIM_EHIP; break; }
     } while (0);
     if (rc != PSIM_OK) { psim_destroy(h); return rc; }
     *out = h;
@@ -1468,6 +1483,7 @@ int psim_destroy(psim_handle* h) {
     if (h->scratch_buf) (void)hipFree(h->scratch_buf);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    if (h->ev_done) (void)hipEventDestroy(h->ev_done);
     for (auto& e : h->sh.rev_)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : h->sh.xev)
@@ -1985,7 +2001,7 @@ int broadcast_common(psim_handle* h, uint32_t root, uint32_t* mono_out, unsigned
         }
         HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, chunk_wait(h));
         reduce_row(h->h_stats, r);
         if (r[S_OVERFLOW])
             return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat; "

@@ -753,7 +753,9 @@ Transport* handle_transport(psim_handle* h);                // the exchange of p
 uint64_t handle_seed(const psim_handle* h);
 int handle_fail(psim_handle* h, int code, const char* fmt, ...);
 void handle_add_round(psim_handle* h, double kernel_ms);   // psim_get_timing totals
-hipEvent_t handle_event(psim_handle* h, int i);            // i < 8
+hipEvent_t handle_event(psim_handle* h, int i);
+// wait for the handle's stream by polling an event (psim_host.hip chunk_wait)
+hipError_t handle_wait(psim_handle* h);            // i < 8
 // The agreed code of a collective step (all-reduced flags v, this rank's
 // local code lrc): 0, or the common code -- a rank that did not fail itself
 // names the failure as another shard's.

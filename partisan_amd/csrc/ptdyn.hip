@@ -719,7 +719,7 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         PDCHK(h, hipEventRecord(handle_event(h, 3), st));
         unsigned long long raw[kRoundStatShards * kPdNStat], r[kPdNStat];
         PDCHK(h, hipMemcpyAsync(raw, s->stats, sizeof raw, hipMemcpyDeviceToHost, st));
-        PDCHK(h, hipStreamSynchronize(st));
+        PDCHK(h, handle_wait(h));
         fold_stat_shards(raw, r, kPdNStat, 9);
 #ifdef C3_PROF
         {

@@ -664,7 +664,7 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     SCCHK(h, hipEventRecord(handle_event(h, 1), st));
     unsigned long long raw[kRoundStatShards * 16], r[16];
     SCCHK(h, hipMemcpyAsync(raw, s.stats, sizeof raw, hipMemcpyDeviceToHost, st));
-    SCCHK(h, hipStreamSynchronize(st));
+    SCCHK(h, handle_wait(h));
     fold_stat_shards(raw, r, 16, 11);
 #ifdef C3_PROF
     {

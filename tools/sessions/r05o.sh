@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# Round-5: the chunk wait by polling an event (new) vs a blocking stream sync (old): parity, bench A/B, a trace.
+# Round-5: every per-round host wait by polling an event (new) vs blocking
+# stream syncs (old = exp_pre_spin.so): parity of the engines, config lines A/B.
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -14,12 +15,10 @@ step() {  # name seconds cmd...  (stops the session on a GPU fault, abort, kill 
     [ $rc -le 1 ] || exit $rc
 }
 OLD=$PWD/partisan_amd/exp_pre_spin.so
-step parity 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_plumtree_gpu.py
+step parity 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_hyparview.py tests/test_scamp.py tests/test_c3.py tests/test_demers.py tests/test_causal.py tests/test_forest.py tests/test_fullmem.py
 grep -q " passed" gpurun_out/parity.log && ! grep -q "failed" gpurun_out/parity.log || { echo "=== parity not green: stopping"; exit 4; }
-B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --sustain-s 2"
-for rep in 1 2 3; do
-  step b_new_$rep 200 $B
-  PSIM_LIB_PATH=$OLD step b_old_$rep 200 $B
+for rep in 1 2; do
+  step cfg_new_$rep 400 python tools/config_bench.py C2 C3 C4 C5
+  PSIM_LIB_PATH=$OLD step cfg_old_$rep 400 python tools/config_bench.py C2 C3 C4 C5
 done
-step trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/trace -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --sustain-s 0
 echo "=== session done"
