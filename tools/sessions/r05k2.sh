@@ -21,4 +21,5 @@ python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --n 100000
 step bench 600 python bench.py --steps 20 --warmup 3 --traffic-json gpurun_out/pmc_traffic.json
 step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --sustain-s 0
 step configs 700 python tools/config_bench.py C2 C3 C4 C5 RELAY C2ALL
+step tr_w2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --transport gloo --all-on-device0 --no-cpu-baseline --sustain-s 1
 echo "=== session done"
