@@ -85,7 +85,8 @@ def _compare(g, o, n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,period,dmax,redeliver", [
     (300, 8, 1, 4, 1), (500, 16, 2, 5, 3), (700, 64, 1, 6, 2), (257, 3, 3, 8, 1),
-    (300, 64, 1, 8, 1), (300, 48, 1, 10, 2)])
+    (300, 64, 1, 8, 1), (300, 48, 1, 10, 2),
+    (1000, 64, 1, 4, 1)])   # C5's own parameters (64 emitters, P=1, D=4, R=1): the batched fast path
 def test_lockstep_vs_oracle(n, m, period, dmax, redeliver):
     sim, g, o = _pair(n, m, period, dmax, redeliver, 0x5EED0005)
     for _ in range(6):

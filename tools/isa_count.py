@@ -3,7 +3,11 @@
 opcodes, v_readlane / v_writelane (SGPR spill traffic), 64-bit address math,
 and per basic block (label) counts so the hot loop can be located.
 
-usage: python tools/isa_count.py <file.s> <kernel-substring> [--blocks]"""
+--loops: the same per loop (LLVM's "Loop: Header=... Depth=" block notes),
+innermost loop of each block, with its memory operations -- which candidate
+or arrival loop holds the spill reloads.
+
+usage: python tools/isa_count.py <file.s> <kernel-substring> [--blocks] [--loops]"""
 import re
 import sys
 from collections import Counter
@@ -63,6 +67,25 @@ def main():
                                                    "v_addc_co_u32_e32", "v_addc_co_u32_e64", "v_add_u64",
                                                    "v_lshlrev_b64", "v_mad_u64_u32")))
     print("  top opcodes:", ops.most_common(30))
+    if "--loops" in sys.argv:
+        per, mem, cur = {}, {}, (0, "-")
+        for raw in b.split("\n"):
+            st = raw.strip()
+            if (raw[:1] not in (" ", "\t") and st.endswith(":")) or st.startswith("; %bb") or \
+                    (st.startswith(".LBB") and ":" in st):
+                import re
+                m = re.search(r"Loop: Header=(\S+) Depth=(\d+)", raw)
+                cur = (int(m.group(2)), m.group(1)) if m else (0, "-")
+                continue
+            line = raw.split(";")[0].strip()
+            if not line or line.startswith(".") or line.endswith(":"):
+                continue
+            op = line.split()[0]
+            per.setdefault(cur, Counter())[cls(op)] += 1
+            if cls(op) in ("VMEM", "LDS") or "readlane" in op or "writelane" in op:
+                mem.setdefault(cur, Counter())[op] += 1
+        for k in sorted(per, key=lambda k: (k[0], k[1])):
+            print(f"  depth {k[0]} {k[1]:>12} {dict(per[k])} {dict(mem.get(k, {}))}")
     if "--blocks" in sys.argv:
         for lab, bl in blocks:
             bc = Counter(cls(l.split()[0]) for l in bl)
