@@ -696,7 +696,10 @@ int  psim_scamp_put(psim_handle* h, const psim_scamp_msg* msgs, size_t k);
  * the SCAMP round, then the Plumtree round (the round's updates in order,
  * the inbox in (src, seq) order, the lazy tick).  A crash restarts both
  * processes (start_link/0 with members = {self}).  psim_scamp_get_views /
- * _get_nodes read the membership side. */
+ * _get_nodes read the membership side.  crash / join return without waiting
+ * for the device (their work is ordered before the next round and every
+ * read-back); an error of a round (PSIM_EOVERFLOW) leaves the C3 state spent:
+ * set it up again. */
 typedef struct psim_c3_stats {
     psim_scamp_stats scamp;        /* the membership round                      */
     uint64_t pt_sent[6];           /* [k] Plumtree messages of PSIM_MSG_* kind k */

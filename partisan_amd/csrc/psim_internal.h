@@ -539,6 +539,7 @@ constexpr uint32_t kScEv = 32;                // update events per vertex and ro
 // The SCAMP engine's device state, for the C3 Plumtree engine (ptdyn.hip)
 struct ScView {
     uint32_t n;
+    const uint32_t* list;                 // the last psim_scamp_crash list (device)
     const uint32_t* pv;                   // [n][kScPv]
     const ScHead* head;
     uint8_t* alive;
@@ -548,6 +549,11 @@ struct ScView {
 int scamp_view(psim_handle* h, ScView* out, bool want_events);   // PSIM_ESTATE without psim_scamp_setup
 int scamp_round(psim_handle* h, psim_scamp_stats* out);          // one SCAMP round (calls made so far)
 int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k);
+// a round in two halves: launch (calls uploaded, round launched, stats copy
+// enqueued; no wait) and finish (after the stream passed it: stats folded,
+// errors raised) -- psim_c3_step waits once for both engines' rounds
+int scamp_round_launch(psim_handle* h);
+int scamp_round_finish(psim_handle* h, psim_scamp_stats* out);
 hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
 

@@ -560,14 +560,15 @@ struct PdState : ModuleState {
     PdRow* rows = nullptr;
     PdMsg* msg[2] = {nullptr, nullptr};
     uint32_t* nmsg = nullptr;
-    uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr, *list = nullptr;
-    size_t list_cap = 0;
+    uint32_t *cnt = nullptr, *cur = nullptr, *off = nullptr, *idx = nullptr, *bsum = nullptr;
     uint32_t par = 0;
     uint64_t round = 0;
+    unsigned long long* h_stats = nullptr;   // pinned: a round's stats rows
     ~PdState() override {
-        void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, list};
+        void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum};
         for (void* x : p)
             if (x) (void)hipFree(x);
+        if (h_stats) (void)hipHostFree(h_stats);
     }
 };
 
@@ -663,20 +664,16 @@ int psim_c3_crash(psim_handle* h, const uint32_t* v, size_t k) {
     if (!h || (k && !v)) return PSIM_EINVAL;
     PdState* s = pd_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
-    int rc = scamp_crash_list(h, v, k);     // validates the list, restarts the SCAMP side
+    int rc = scamp_crash_list(h, v, k);     // validates the list, uploads it, restarts the SCAMP side
     if (rc || !k) return rc;
-    if (k > s->list_cap) {
-        if (s->list) (void)hipFree(s->list);
-        s->list = nullptr;
-        s->list_cap = std::max<size_t>(k, 2 * s->list_cap);
-        if (!pd_alloc((void**)&s->list, s->list_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "c3 crash list");
-    }
-    PDCHK(h, hipMemcpyAsync(s->list, v, k * 4, hipMemcpyHostToDevice, handle_stream(h)));
+    ScView sv;
+    rc = scamp_view(h, &sv, true);
+    if (rc) return rc;
     PdArgs a;
     rc = pd_args(h, *s, a);
     if (rc) return rc;
-    PDCHK(h, launch_pd_init(a, s->list, (uint32_t)k, handle_stream(h)));
-    PDCHK(h, hipStreamSynchronize(handle_stream(h)));
+    // the same device list, on the same stream: nothing is copied twice and nothing waits
+    PDCHK(h, launch_pd_init(a, sv.list, (uint32_t)k, handle_stream(h)));
     return PSIM_OK;
 }
 
@@ -707,9 +704,16 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
     PdState* s = pd_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
     const hipStream_t st = handle_stream(h);
+    if (!s->h_stats && hipHostMalloc((void**)&s->h_stats, kRoundStatShards * kPdNStat * 8) != hipSuccess) {
+        s->h_stats = nullptr;
+        return handle_fail(h, PSIM_ENOMEM, "c3: pinned stats rows");
+    }
     for (uint32_t i = 0; i < rounds; i++) {
         psim_c3_stats* o = out && i < cap ? &out[i] : nullptr;
-        int rc = scamp_round(h, o ? &o->scamp : nullptr);
+        // the SCAMP round and the Plumtree round that reads its updates are
+        // enqueued back to back and the host waits once for both; a SCAMP
+        // error is still reported first (the handle's C3 state is then spent)
+        int rc = scamp_round_launch(h);
         if (rc) return rc;
         PdArgs a;
         rc = pd_args(h, *s, a);
@@ -717,10 +721,12 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         PDCHK(h, hipEventRecord(handle_event(h, 2), st));
         PDCHK(h, launch_pd_round(a, st));
         PDCHK(h, hipEventRecord(handle_event(h, 3), st));
-        unsigned long long raw[kRoundStatShards * kPdNStat], r[kPdNStat];
-        PDCHK(h, hipMemcpyAsync(raw, s->stats, sizeof raw, hipMemcpyDeviceToHost, st));
+        unsigned long long r[kPdNStat];
+        PDCHK(h, hipMemcpyAsync(s->h_stats, s->stats, kRoundStatShards * kPdNStat * 8, hipMemcpyDeviceToHost, st));
         PDCHK(h, handle_wait(h));
-        fold_stat_shards(raw, r, kPdNStat, 9);
+        rc = scamp_round_finish(h, o ? &o->scamp : nullptr);
+        if (rc) return rc;
+        fold_stat_shards(s->h_stats, r, kPdNStat, 9);
 #ifdef C3_PROF
         {
             static unsigned long long tot[kProfSlots];

@@ -581,11 +581,22 @@ struct ScState : ModuleState {
     std::vector<uint32_t> cv, cx;   // calls since the last round: vertex, (bit31 = leave) | target
     std::vector<uint32_t> stamp;    // psim_scamp_crash's duplicate test
     uint32_t stamp_gen = 0;
+    // host -> device uploads (crash lists, a round's calls) go through pinned
+    // staging, so the copies are asynchronous and no call waits for the
+    // device; `up_ev` marks the last upload, awaited before the buffer is reused
+    uint32_t* h_up = nullptr;
+    size_t h_up_cap = 0;
+    hipEvent_t up_ev = nullptr;
+    bool up_pending = false;
+    unsigned long long* h_stats = nullptr;   // pinned: a round's stats rows
     ~ScState() override {
         void* p[] = {head, pv, iv, alive, alive0, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, call_start, call_v,
                      calls, list, stats, ev_cnt, ev};
         for (void* x : p)
             if (x) (void)hipFree(x);
+        if (h_up) (void)hipHostFree(h_up);
+        if (h_stats) (void)hipHostFree(h_stats);
+        if (up_ev) (void)hipEventDestroy(up_ev);
     }
 };
 
@@ -625,24 +636,58 @@ ScArgs sc_args(const psim_handle* h, const ScState& s) {
     return a;
 }
 
-int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
+// A pinned staging area of `words` u32 for the next upload (waits for the
+// previous upload out of it, long finished in practice)
+uint32_t* sc_stage(psim_handle* h, ScState& s, size_t words) {
+    if (s.up_pending) {
+        if (hipEventSynchronize(s.up_ev) != hipSuccess) return nullptr;
+        s.up_pending = false;
+    }
+    if (!s.up_ev && hipEventCreateWithFlags(&s.up_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (words > s.h_up_cap) {
+        if (s.h_up) (void)hipHostFree(s.h_up);
+        s.h_up = nullptr;
+        s.h_up_cap = std::max<size_t>(words, 2 * s.h_up_cap);
+        if (hipHostMalloc((void**)&s.h_up, s.h_up_cap * 4) != hipSuccess) {
+            s.h_up_cap = 0;
+            return nullptr;
+        }
+    }
+    (void)h;
+    return s.h_up;
+}
+
+// A round's first half: the calls made since the last round sorted and
+// uploaded, the round launched, its stats rows copied to the pinned mirror --
+// nothing waits; sc_round_finish reads them once the stream got there.
+int sc_round_launch(psim_handle* h, ScState& s) {
     const hipStream_t st = handle_stream(h);
     // calls sorted by vertex: leaves first, then joins, each in call order
     // (sc_prep indexes each vertex's first one on the device)
     // (an LSD radix sort of key 2 v + join, stable: O(k) per 11-bit digit,
-    // where a comparison sort of 50k calls took milliseconds of host time)
+    // where a comparison sort of 50k calls took milliseconds of host time;
+    // calls already in key order -- a churn batch's joins -- skip it)
     const size_t k = s.cv.size();
-    std::vector<uint32_t> ord(k), tmp(k), cv(k), cx(k);
-    for (size_t i = 0; i < k; i++) ord[i] = uint32_t(i);
     auto key = [&](uint32_t i) -> uint64_t { return 2ull * s.cv[i] + ((s.cx[i] >> 31) ^ 1u); };   // leave first
-    for (uint32_t shift = 0; shift < 64 && (2ull * s.n) >> shift; shift += 11) {
-        uint32_t cnt[2049] = {0};
-        for (size_t i = 0; i < k; i++) cnt[((key(ord[i]) >> shift) & 2047u) + 1]++;
-        for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
-        for (size_t i = 0; i < k; i++) tmp[cnt[(key(ord[i]) >> shift) & 2047u]++] = ord[i];
-        ord.swap(tmp);
+    bool sorted = true;
+    for (size_t i = 1; i < k && sorted; i++) sorted = key(uint32_t(i - 1)) <= key(uint32_t(i));
+    uint32_t* up = k ? sc_stage(h, s, 2 * k) : nullptr;
+    if (k && !up) return handle_fail(h, PSIM_ENOMEM, "scamp: pinned staging for %zu calls", k);
+    if (k && sorted) {
+        memcpy(up, s.cv.data(), k * 4);
+        memcpy(up + k, s.cx.data(), k * 4);
+    } else if (k) {
+        std::vector<uint32_t> ord(k), tmp(k);
+        for (size_t i = 0; i < k; i++) ord[i] = uint32_t(i);
+        for (uint32_t shift = 0; shift < 64 && (2ull * s.n) >> shift; shift += 11) {
+            uint32_t cnt[2049] = {0};
+            for (size_t i = 0; i < k; i++) cnt[((key(ord[i]) >> shift) & 2047u) + 1]++;
+            for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+            for (size_t i = 0; i < k; i++) tmp[cnt[(key(ord[i]) >> shift) & 2047u]++] = ord[i];
+            ord.swap(tmp);
+        }
+        for (size_t i = 0; i < k; i++) { up[i] = s.cv[ord[i]]; up[k + i] = s.cx[ord[i]]; }
     }
-    for (size_t i = 0; i < k; i++) { cv[i] = s.cv[ord[i]]; cx[i] = s.cx[ord[i]]; }
     if (k > s.calls_cap) {
         if (s.calls) (void)hipFree(s.calls);
         if (s.call_v) (void)hipFree(s.call_v);
@@ -652,20 +697,30 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
             return handle_fail(h, PSIM_ENOMEM, "scamp: call list");
     }
     if (k) {
-        SCCHK(h, hipMemcpyAsync(s.call_v, cv.data(), k * 4, hipMemcpyHostToDevice, st));
-        SCCHK(h, hipMemcpyAsync(s.calls, cx.data(), k * 4, hipMemcpyHostToDevice, st));
+        SCCHK(h, hipMemcpyAsync(s.call_v, up, k * 4, hipMemcpyHostToDevice, st));
+        SCCHK(h, hipMemcpyAsync(s.calls, up + k, k * 4, hipMemcpyHostToDevice, st));
+        SCCHK(h, hipEventRecord(s.up_ev, st));
+        s.up_pending = true;
     }
     s.cv.clear();
     s.cx.clear();
+    if (!s.h_stats && hipHostMalloc((void**)&s.h_stats, kRoundStatShards * 16 * 8) != hipSuccess) {
+        s.h_stats = nullptr;
+        return handle_fail(h, PSIM_ENOMEM, "scamp: pinned stats rows");
+    }
     ScArgs a = sc_args(h, s);
     a.ncalls = uint32_t(k);
     SCCHK(h, hipEventRecord(handle_event(h, 0), st));
     SCCHK(h, launch_sc_round(a, st));
     SCCHK(h, hipEventRecord(handle_event(h, 1), st));
-    unsigned long long raw[kRoundStatShards * 16], r[16];
-    SCCHK(h, hipMemcpyAsync(raw, s.stats, sizeof raw, hipMemcpyDeviceToHost, st));
-    SCCHK(h, handle_wait(h));
-    fold_stat_shards(raw, r, 16, 11);
+    SCCHK(h, hipMemcpyAsync(s.h_stats, s.stats, kRoundStatShards * 16 * 8, hipMemcpyDeviceToHost, st));
+    return PSIM_OK;
+}
+
+// A round's second half, after the stream passed sc_round_launch's copy
+int sc_round_finish(psim_handle* h, ScState& s, psim_scamp_stats* out) {
+    unsigned long long r[16];
+    fold_stat_shards(s.h_stats, r, 16, 11);
 #ifdef C3_PROF
     {
         static unsigned long long tot[kProfSlots];
@@ -705,6 +760,13 @@ int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
     return PSIM_OK;
 }
 
+int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
+    int rc = sc_round_launch(h, s);
+    if (rc) return rc;
+    SCCHK(h, handle_wait(h));
+    return sc_round_finish(h, s, out);
+}
+
 int sc_upload_list(psim_handle* h, ScState& s, const uint32_t* v, size_t k) {
     if (k > s.list_cap) {
         if (s.list) (void)hipFree(s.list);
@@ -712,7 +774,12 @@ int sc_upload_list(psim_handle* h, ScState& s, const uint32_t* v, size_t k) {
         s.list_cap = std::max<size_t>(k, 2 * s.list_cap);
         if (!sc_alloc((void**)&s.list, s.list_cap * 4)) return handle_fail(h, PSIM_ENOMEM, "scamp: vertex list");
     }
-    SCCHK(h, hipMemcpyAsync(s.list, v, k * 4, hipMemcpyHostToDevice, handle_stream(h)));
+    uint32_t* up = sc_stage(h, s, k);
+    if (!up) return handle_fail(h, PSIM_ENOMEM, "scamp: pinned staging for %zu vertices", k);
+    memcpy(up, v, k * 4);
+    SCCHK(h, hipMemcpyAsync(s.list, up, k * 4, hipMemcpyHostToDevice, handle_stream(h)));
+    SCCHK(h, hipEventRecord(s.up_ev, handle_stream(h)));
+    s.up_pending = true;
     return PSIM_OK;
 }
 
@@ -728,6 +795,7 @@ int scamp_view(psim_handle* h, ScView* out, bool want_events) {
             return handle_fail(h, PSIM_ENOMEM, "scamp: update event arrays");
     }
     out->n = s->n;
+    out->list = s->list;
     out->pv = s->pv;
     out->head = s->head;
     out->alive = s->alive;
@@ -740,6 +808,18 @@ int scamp_round(psim_handle* h, psim_scamp_stats* out) {
     ScState* s = sc_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
     return sc_round(h, *s, out);
+}
+
+int scamp_round_launch(psim_handle* h) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    return sc_round_launch(h, *s);
+}
+
+int scamp_round_finish(psim_handle* h, psim_scamp_stats* out) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    return sc_round_finish(h, *s, out);
 }
 
 int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k) { return psim_scamp_crash(h, v, k); }
@@ -832,8 +912,8 @@ int psim_scamp_crash(psim_handle* h, const uint32_t* v, size_t k) {
     SCCHK(h, hipSetDevice(handle_device(h)));
     int rc = sc_upload_list(h, *s, v, k);
     if (rc) return rc;
+    // no wait: the restart is ordered before every later round and read-back on the stream
     SCCHK(h, launch_sc_init(sc_args(h, *s), s->list, (uint32_t)k, handle_stream(h)));
-    SCCHK(h, hipStreamSynchronize(handle_stream(h)));
     return PSIM_OK;
 }
 

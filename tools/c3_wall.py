@@ -1,0 +1,60 @@
+"""C3 wall-time split (diagnostic): per churn round, the host time of each
+driver call (crash, join, step, heartbeat) against the device time of the
+round's SCAMP and Plumtree kernels -- where a C3 round's wall time goes.
+
+usage: python tools/c3_wall.py [n] [rounds]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import partisan_amd as pa  # noqa: E402
+from partisan_amd.scamp import churn_batch, join_waves  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    seed = 0x5EED0003
+    sim = pa.Simulator(seed=seed)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=10)
+    for v, cc in join_waves(n, seed):
+        g.join(v, cc)
+        g.step(3)
+    g.step(5)
+    t = {"heartbeat": 0.0, "churn_draw": 0.0, "crash": 0.0, "join": 0.0, "step": 0.0}
+    sc_ms = pt_ms = 0.0
+    t0 = time.perf_counter()
+    for i in range(rounds):
+        a = time.perf_counter()
+        if i % 10 == 0:
+            g.heartbeat(0)
+        b = time.perf_counter()
+        v, cc = churn_batch(n, seed, i)
+        keep = v != 0
+        c = time.perf_counter()
+        g.crash(v[keep])
+        d = time.perf_counter()
+        g.join(v[keep], cc[keep])
+        e = time.perf_counter()
+        st = g.step(1)
+        f = time.perf_counter()
+        t["heartbeat"] += b - a
+        t["churn_draw"] += c - b
+        t["crash"] += d - c
+        t["join"] += e - d
+        t["step"] += f - e
+        sc_ms += st[0]["scamp"]["kernel_ms"]
+        pt_ms += st[0]["pt_kernel_ms"]
+    wall = time.perf_counter() - t0
+    out = {k: round(1e3 * x / rounds, 4) for k, x in t.items()}
+    out.update(n=n, rounds=rounds, wall_ms_per_round=round(1e3 * wall / rounds, 4),
+               wall_ms_per_round_excl_draw=round(1e3 * (wall - t["churn_draw"]) / rounds, 4),
+               scamp_kernel_ms=round(sc_ms / rounds, 4), plumtree_kernel_ms=round(pt_ms / rounds, 4))
+    print(json.dumps(out), flush=True)
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()
