@@ -6,6 +6,10 @@ A step = one heartbeat broadcast from a fresh tree to quiescence:
   -> psim_plumtree_broadcast(root)  (origin eager push, round 0)
   -> psim_run                       (rounds until nothing is in flight and no
                                       outstanding i_have row to a live peer)
+On one GPU the W warmup and the K timed steps are each one
+psim_plumtree_broadcast_run_n call: the same heartbeats as K reset_trees +
+broadcast_run calls (tests/test_run_n.py), without a return to Python between
+them.
 value = n_peers * rounds / step time, summed over ranks.  The overlay is
 resident in HBM before the timed region; nothing crosses PCIe inside it
 except the per-chunk 8 KB counter read-back the round driver needs.
@@ -392,8 +396,20 @@ def main():
             return sp.run()
         return one_step(sim, root)
 
-    for _ in range(args.warmup):
-        step()
+    def steps(k):
+        """k steps; on one GPU in one call (psim_plumtree_broadcast_run_n: the
+        same heartbeats as k reset_trees + broadcast_run calls, without a return
+        to Python between them).  Returns [(round records, rounds)] per step."""
+        if sp is not None or k == 0:
+            return [step() for _ in range(k)]
+        _, st, rounds = sim.broadcast_run_n(root, k, reset_trees=True)
+        out, o = [], 0
+        for r in rounds.tolist():
+            out.append((st[o:o + r], r))
+            o += r
+        return out
+
+    steps(args.warmup)
 
     algo_bytes = 0
     active_bytes = 0
@@ -405,20 +421,22 @@ def main():
         sp.exchange_total = {}
     barrier(pg)
     t0 = time.perf_counter()
-    last_stats = None
-    for _ in range(args.steps):
-        stats, rounds = step()
-        rounds_per_step.append(rounds)
-        last_stats = stats
-        if sp is None:
+    done = steps(args.steps)
+    # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
+    barrier(pg)
+    t1 = time.perf_counter()
+    step_stats = [st for st, _ in done]
+    rounds_per_step = [r for _, r in done]
+    # the per-step bookkeeping after the timed region (a Python pass over each
+    # step's round records cost ~3 % of a step inside it)
+    last_stats = step_stats[-1] if step_stats else None
+    if sp is None:
+        for stats in step_stats:
             algo_bytes += int(stats["algo_bytes"].sum())
             round_ms += float(stats["kernel_ms"].sum())
             # the same model crediting the state bytes of the vertices a round touched, not of all N
             active_bytes += sum(touched_bytes(x) for x in stats)
             words += int(stats["words_stored"].sum())
-    # psim_run / psim_shard_round return after hipStreamSynchronize on the library stream
-    barrier(pg)
-    t1 = time.perf_counter()
     if sp is not None:   # this GPU's own bytes and launch times
         algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
 
@@ -481,9 +499,9 @@ def main():
         barrier(pg)
         k, s0, sus_rounds = 0, time.perf_counter(), []
         while time.perf_counter() - s0 < args.sustain_s:
-            _, r = step()
-            sus_rounds.append(r)
-            k += 1
+            for _, r in steps(max(1, args.steps)):
+                sus_rounds.append(r)
+                k += 1
         barrier(pg)
         dt = max_over_ranks(pg, time.perf_counter() - s0)
         sustained = {"steps": k, "seconds": round(dt, 3), "ms_per_step": dt / k * 1e3,

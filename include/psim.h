@@ -174,10 +174,21 @@ int  psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t 
  * calls do; sharded handles: PSIM_ESTATE. */
 int  psim_plumtree_broadcast_run(psim_handle* h, uint32_t root, uint32_t* mono_out, uint32_t max_rounds,
                                  psim_round_stats* stats, size_t cap, uint32_t* rounds_run);
+/* `count` heartbeat intervals of one root back to back: each is
+ * psim_plumtree_reset_trees (when reset_trees != 0) then
+ * psim_plumtree_broadcast_run(root, max_rounds) -- the same state, ids,
+ * per-round stats and codes as those calls in a loop, without a return to
+ * the caller between intervals.  stats: the per-round rows of every interval
+ * in order (up to cap rows in all); rounds[i] / monos[i] (either may be
+ * null): the rounds interval i ran and its heartbeat id; *done: the
+ * intervals completed (those before the first error). */
+int  psim_plumtree_broadcast_run_n(psim_handle* h, uint32_t root, uint32_t count, uint32_t reset_trees,
+                                   uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds,
+                                   uint32_t* monos, uint32_t* done);
 /* Several roots: on one GPU without PSIM_CFG_BINNED each
  * heartbeat root gets a lane of its own (per-root eager / lazy sets, rows,
- * delivered serials, in-flight words; up to 16 lanes, then the least
- * recently used quiescent lane is reused and its root's sets forgotten), so
+ * delivered serials, in-flight words; up to 16 lanes -- a 17th root is
+ * PSIM_ENOSPC; psim_config.max_roots keeps every root, the forest), so
  * heartbeats of different roots run concurrently and PSIM_EBUSY is per
  * root; rounds advance every lane and their stats are summed.  Sharded and
  * binned handles keep one lane: a heartbeat from a new root drops the old

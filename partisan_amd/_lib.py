@@ -179,6 +179,8 @@ SIGNATURES = {
     "psim_plumtree_broadcast_many": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t, _P(C.c_uint32)]),
     "psim_plumtree_broadcast_run": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), C.c_uint32, _P(RoundStats), C.c_size_t,
                                               _P(C.c_uint32)]),
+    "psim_plumtree_broadcast_run_n": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P(RoundStats),
+                                                C.c_size_t, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
     "psim_step": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t]),
     "psim_run": (C.c_int, [_H, C.c_uint32, _P(RoundStats), C.c_size_t, _P(C.c_uint32)]),
     "psim_get_plumtree": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint16),

@@ -827,7 +827,7 @@ __device__ __forceinline__ int* hold_delta(const PtArgs& a) {
 // list -- a listed vertex that gained rows this round was then visited again
 // as "due" and sent a second i_have (the 1M world-2 mismatch of round 2).
 __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint32_t* wl_off = nullptr) {
-    __shared__ uint32_t cnt2[4];
+    __shared__ uint32_t cnt2[5];
     m.mark = 1;
     m.all_in = m.list_in = false;
     if (!a.mcnt) {
@@ -840,10 +840,8 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
     if (t == 0) {                                         // holders at the start of this round
         const int hold = int(a.mcnt[kMcntHold + a.m_r]) + int(a.mcnt[kMcntHoldD + a.m_s]);
         cnt2[3] = uint32_t(hold);
-        if (blockIdx.x == 0) {
-            a.mcnt[kMcntHold + a.m_s] = uint32_t(hold);  // = holders at the end of round R-1
-            a.mcnt[kMcntHoldD + a.m_z] = 0u;             // the round after next adds into it
-        }
+        // an abandoned pipelined interval (PtArgs::spec), loaded with the counts
+        cnt2[4] = a.spec ? a.spec[0] : 0u;
     }
     if (t < 64) {
         uint32_t c1 = a.mcnt[a.m_s * 64 + t], c2 = a.mcnt[a.m_r * 64 + t];
@@ -865,12 +863,20 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
             c2 += __shfl_xor(c2, off, 64);
         }
         if (t == 0) { cnt2[0] = c1; cnt2[1] = c2; cnt2[2] = ovf; }
-        if (blockIdx.x == 0) {                            // the round after next starts empty
+    }
+    __syncthreads();
+    // nothing of an abandoned interval runs, not even the rings' upkeep below
+    if (cnt2[4]) return false;
+    if (blockIdx.x == 0) {        // (no workgroup of this launch reads these slots)
+        if (t == 0) {
+            a.mcnt[kMcntHold + a.m_s] = cnt2[3];          // = holders at the end of round R-1
+            a.mcnt[kMcntHoldD + a.m_z] = 0u;              // the round after next adds into it
+        }
+        if (t < 64) {                                     // the round after next starts empty
             a.mcnt[a.m_z * 64 + t] = 0;
             if (a.wl_cur) a.wlcnt[a.m_z * 64 + t] = 0;
         }
     }
-    __syncthreads();
     const uint32_t prev = cnt2[0], prev2 = cnt2[1];
     const bool rows_due = a.tick && int(cnt2[3]) > 0;
     m.rows_due = rows_due;
@@ -1583,6 +1589,25 @@ __device__ __forceinline__ void pt_origin_wave(const PtArgs& a) {
 // -- one launch instead of four
 __global__ void pt_origin_kernel(PtArgs a, uint32_t prep, uint32_t hold) {
     if (blockIdx.x != 0) return;
+    if (a.spec) {
+        // pipelined: run only if the previous heartbeat ended exactly at its
+        // predicted last round (PtArgs::spec); the host reads the decision
+        const uint32_t t = threadIdx.x & 63u, rl = a.spec_rl & 3u, rp = (rl + 3u) & 3u;
+        unsigned long long last = threadIdx.x < 64 ? a.mcnt[rl * 64 + t] : 0u;
+        unsigned long long before = threadIdx.x < 64 ? a.mcnt[rp * 64 + t] : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            last += __shfl_xor(last, off, 64);
+            before += __shfl_xor(before, off, 64);
+        }
+        const int holders = int(a.mcnt[kMcntHold + rp]) + int(a.mcnt[kMcntHoldD + rl]);
+        const bool run = last == 0ull && before != 0ull && holders == 0;
+        if (threadIdx.x == 0) {
+            a.spec[0] = run ? 0u : 1u;
+            a.spec[1] = run ? 1u : 2u;
+        }
+        if (!run) return;
+    }
     if (prep) {
         for (uint32_t i = threadIdx.x; i < prep; i += blockDim.x) a.stats[i] = 0ull;
         if (a.mcnt)

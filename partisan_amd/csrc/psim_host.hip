@@ -222,6 +222,7 @@ struct psim_handle {
         hipEvent_t xev[2 * 16] = {};                   // exchange start / end per pending round
     } sh;
     hipStream_t own_stream = nullptr;         // the handle's stream (psim_set_stream may override `stream`)
+    hipStream_t cstream = nullptr;            // psim_plumtree_broadcast_run_n: read-back copies beside the rounds
 
 
 
@@ -1493,6 +1494,10 @@ int psim_destroy(psim_handle* h) {
     h->sh.xport = nullptr;
     if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    if (h->cstream) {
+        (void)hipStreamSynchronize(h->cstream);
+        (void)hipStreamDestroy(h->cstream);
+    }
     delete h;
     return PSIM_OK;
 }
@@ -2034,6 +2039,260 @@ int shard_pack(psim_handle* h, void* send_dev, uint64_t send_cap, uint64_t* coun
     return PSIM_OK;
 }
 
+// ---- heartbeat intervals back to back (psim_plumtree_broadcast_run_n) ------
+// Between two calls of psim_plumtree_broadcast_run the device idles while the
+// host reads the interval back, returns to its caller and launches the next
+// origin (~60 us a 10M-peer interval of ~2 ms, profiles/r05/experiments).
+// Here interval i + 1 is enqueued BEFORE interval i is read back, on the
+// prediction that i ends exactly after as many rounds as i - 1 did: its
+// kernels carry a guard (PtArgs::spec) and its origin runs it only if the
+// previous interval's last predicted round sent nothing, the one before sent
+// something and no vertex holds a row -- the host's own quiescence test on
+// the same counts.  The host repeats the test when it reads interval i back:
+// on a miss the device has abandoned i + 1 (every kernel of it returned at
+// once), the host undoes i + 1's bookkeeping, finishes i with the plain
+// driver if it needs more rounds, and goes on.  Only the plain single-root
+// handle pipelines (one lane on one GPU, no delays, no window lane, chunk
+// timing); an interval that would renormalise tags or scrub the inbox, and
+// every other handle, take the plain calls.
+constexpr uint32_t kPipeRegion = 32;   // stats rows per interval slot: the origin's, then <= kChunk rounds'
+static_assert(2 * kPipeRegion <= kChunk * kMaxLanes + 1, "two interval slots fit the stats rows");
+static_assert(kDelayHist >= 2, "the spec words live in the origin row's delay histogram (no delays here)");
+
+struct PipeRec {
+    uint32_t region = 0, k = 0, mono = 0;
+    uint64_t round0 = 0;     // h->round before the interval's first round
+    bool guarded = false;
+};
+struct PipeSnap {
+    uint32_t epoch = 0, serial = 0, mono = 0, par = 0;
+};
+
+unsigned long long* pipe_rows(psim_handle* h, uint32_t r) { return h->stats + size_t(r) * kPipeRegion * kStatsRow; }
+unsigned long long* pipe_hrows(psim_handle* h, uint32_t r) { return h->h_stats + size_t(r) * kPipeRegion * kStatsRow; }
+// the guard's words: the origin row's delay histogram, unused without delay
+// faults -- read back with the rows, never zeroed by the origin's prep
+uint32_t* pipe_spec(unsigned long long* rows) { return reinterpret_cast<uint32_t*>(rows + size_t(kStatShards) * kNStat); }
+
+// the interval starting after round round0 with k rounds can be enqueued
+// without a wait (`guarded`: before the previous one is read back)
+bool pipe_ok(const psim_handle* h, uint32_t root, bool reset, uint64_t round0, uint32_t k, bool guarded) {
+    if (h->sh.world != 1 || h->fo.on || h->dly || h->bin.rec_c || h->win || !h->mcnt_base) return false;
+    if (!(h->cfg.flags & PSIM_CFG_CHUNK_TIMING)) return false;
+    if (h->lanes.size() != 1 || h->cur_lane != 0 || !h->have_root || h->root != root) return false;
+    if (root - h->sh.v_lo >= h->n || h->next_epoch.count(root)) return false;
+    if (k == 0 || k > kChunk) return false;
+    const uint32_t ep = h->epoch + (reset ? 1u : 0u);
+    if (((h->serial + 1u) & 0x7Fu) == 0 || (ep & 0x7Fu) == 0) return false;        // would renormalise tags
+    const auto it = h->mono_of.find(root);
+    if (it == h->mono_of.end() || (it->second & 0xFFFFFFu) >= 0xFFFFFEu) return false;
+    if (round0 + k + 1 >= h->scrub + kTagSpan) return false;                         // would scrub the inbox
+    return guarded || (h->inflight == 0 && h->live_rows == 0 && h->ost_cnt == 0);   // exact state: quiescent
+}
+
+// reset_trees + the origin + k rounds + the read-back copies, with no wait
+int pipe_enqueue(psim_handle* h, uint32_t root, bool reset, uint32_t k, uint32_t region, bool guarded,
+                 uint64_t round0, PipeRec& rec) {
+    if (reset) h->epoch++;
+    h->serial++;
+    uint32_t& mono = h->mono_of[root];
+    mono++;
+    rec.mono = mono;
+    rec.region = region;
+    rec.k = k;
+    rec.round0 = round0;
+    rec.guarded = guarded;
+    unsigned long long* rows = pipe_rows(h, region);
+    uint32_t* spec = pipe_spec(rows);                    // the origin writes both words (no memset)
+    if (!h->cstream && hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
+        h->cstream = nullptr;
+        return fail(h, PSIM_EHIP, "run_n: copy stream");
+    }
+    const uint64_t round_now = h->round;
+    h->round = round0;                                   // make_args / slots / tags of the interval's rounds
+    struct Back {
+        psim_handle* h;
+        uint64_t r;
+        ~Back() { h->round = r; }
+    } back{h, round_now};
+    PtArgs a = make_args(h, h->par ^ 1u, 0, rows);       // the origin: row 0, pushes for round round0 + 1
+    set_round_slots(h, a, round0 + 1);
+    a.wtag = uint32_t(round0 + 1) & 0xFFu;
+    a.root = root - h->sh.v_lo;
+    if (guarded) {
+        a.spec = spec;
+        a.spec_rl = uint32_t(round0 % 4);
+    }
+    // the interval starts with no row holder (guarded: the origin checks it);
+    // its prep zeroes the row's counters, not the guard's words after them
+    HIPCHK(h, launch_pt_origin(a, h->stream, uint32_t(kStatShards * kNStat), 0u));
+    PtPrep pp{};
+    pp.z = rows + kStatsRow;                             // the rounds' rows (the origin zeroed its own)
+    pp.nz = uint64_t(k) * kStatsRow;
+    HIPCHK(h, launch_pt_prep(pp, h->stream));
+    const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
+    HIPCHK(h, hipEventRecord(h->ev[2 * region], h->stream));
+    for (uint32_t i = 0; i < k; i++) {
+        const uint64_t R = round0 + i + 1;
+        PtArgs ra = make_args(h, h->par, (R % L) == 0, rows + size_t(1 + i) * kStatsRow);
+        set_round_slots(h, ra, R);
+        set_round_tags(ra, R);
+        if (guarded) ra.spec = spec;
+        HIPCHK(h, launch_pt_round(ra, h->stream));
+        h->par ^= 1u;
+    }
+    HIPCHK(h, hipEventRecord(h->ev[2 * region + 1], h->stream));
+    // the read-back on a stream of its own, after the interval's last round:
+    // the next interval's origin follows that round directly
+    HIPCHK(h, hipStreamWaitEvent(h->cstream, h->ev[2 * region + 1], 0));
+    HIPCHK(h, hipMemcpyAsync(pipe_hrows(h, region), rows, size_t(1 + k) * kStatsRow * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, h->cstream));
+    HIPCHK(h, hipEventRecord(h->ev[4 + region], h->cstream));
+    return PSIM_OK;
+}
+
+// Wait for an interval and read it back as drive() does: the origin's row,
+// then its rounds up to the first quiescent one (the rest were no-ops).
+// `before`: messages of the round before the last one counted (the origin's
+// for a one-round interval) -- the guard's test, repeated on the host.
+int pipe_collect(psim_handle* h, const PipeRec& rec, psim_round_stats* out, size_t cap, uint32_t& ran, bool& quiet,
+                 uint64_t& before) {
+    hipError_t e;
+    while ((e = hipEventQuery(h->ev[4 + rec.region])) == hipErrorNotReady) {
+    }
+    HIPCHK(h, e);
+    const unsigned long long* hr = pipe_hrows(h, rec.region);
+    if (rec.guarded && pipe_spec(const_cast<unsigned long long*>(hr))[1] != 1u)
+        return fail(h, PSIM_ESTATE, "pipelined heartbeat %u: the device abandoned an interval the host ran "
+                                    "(guard 0x%x)", rec.mono, pipe_spec(const_cast<unsigned long long*>(hr))[1]);
+    float chunk_ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[2 * rec.region], h->ev[2 * rec.region + 1]));
+    unsigned long long r[kNStat];
+    reduce_row(hr, r);
+    if (r[S_OVERFLOW])
+        return fail(h, PSIM_EOVERFLOW, "origin: overflow flags 0x%llx (4: outstanding rows of an older heartbeat)",
+                    r[S_OVERFLOW]);
+    h->ost_cnt += (int64_t)r[S_OST_DELTA];
+    h->live_rows += (int64_t)r[S_LIVE_DELTA];
+    h->inflight = r[PSIM_MSG_BROADCAST];
+    ran = 0;
+    quiet = quiescent(h);
+    uint64_t prev = h->inflight;
+    before = 0;
+    for (uint32_t i = 0; i < rec.k && !quiet; i++) {
+        reduce_row(hr + size_t(1 + i) * kStatsRow, r);
+        if (r[S_OVERFLOW])
+            return fail(h, PSIM_EOVERFLOW,
+                        "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > 4095, "
+                        "4: outstanding rows of an older heartbeat)", (unsigned long long)(h->round + 1), r[S_OVERFLOW]);
+        uint64_t lm = 0;
+        for (int t = 1; t <= 5; t++) lm += r[t];
+        h->ost_cnt += (int64_t)r[S_OST_DELTA];
+        h->live_rows += (int64_t)r[S_LIVE_DELTA];
+        h->inflight = lm;
+        const float ms = chunk_ms / float(rec.k);
+        h->round++;
+        h->kernel_ms_total += ms;
+        h->rounds_total++;
+        if (out && ran < cap) {
+            psim_round_stats& o = out[ran];
+            memset(&o, 0, sizeof o);
+            for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
+            o.delivered_new = r[S_DELIV];
+            o.active = r[S_ACTIVE];
+            o.senders = r[S_SENDERS];
+            o.sender_degree_sum = r[S_DEGSUM];
+            o.outstanding_vertices = (uint64_t)h->ost_cnt;
+            o.algo_bytes = 16ull * h->n + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * lm;
+            o.words_stored = r[S_WORDS];
+            o.kernel_ms = ms;
+        }
+        ran++;
+        before = prev;
+        prev = lm;
+        quiet = quiescent(h);
+    }
+    return PSIM_OK;
+}
+
+int run_n(psim_handle* h, uint32_t root, uint32_t count, bool reset, uint32_t max_rounds, psim_round_stats* stats,
+          size_t cap, uint32_t* rounds, uint32_t* monos, uint32_t* done) {
+    if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
+    HIPCHK(h, hipSetDevice(h->device));
+    size_t used = 0;
+    uint32_t pred = 0;             // rounds the last interval ran (the next one's prediction)
+    bool have_next = false;        // interval i + 1 enqueued, guarded, before interval i was read back
+    PipeRec cur, next;
+    PipeSnap snap;
+    struct Sync {                  // the focused lane's record follows the handle's fields on every exit
+        psim_handle* h;
+        ~Sync() { if (!h->lanes.empty()) save_lane(h); }
+    } sync{h};
+    for (uint32_t i = 0; i < count; i++) {
+        psim_round_stats* out = stats ? stats + used : nullptr;
+        const size_t room = stats ? cap - used : 0;
+        uint32_t ran = 0;
+        if (have_next) {
+            cur = next;
+            have_next = false;
+        } else if (pred && pred <= max_rounds && pipe_ok(h, root, reset, h->round, pred, false)) {
+            const int rc = pipe_enqueue(h, root, reset, pred, i & 1u, false, h->round, cur);
+            if (rc) return rc;
+        } else {
+            // the plain calls (the first interval, and any the pipeline does not cover)
+            if (!h->lanes.empty()) save_lane(h);
+            if (reset) {
+                const int rc = psim_plumtree_reset_trees(h);
+                if (rc) return rc;
+            }
+            uint32_t mono = 0;
+            const int rc = psim_plumtree_broadcast_run(h, root, &mono, max_rounds, out, room, &ran);
+            if (rc) return rc;
+            used += std::min<size_t>(ran, room);
+            if (rounds) rounds[i] = ran;
+            if (monos) monos[i] = mono;
+            if (done) *done = i + 1;
+            pred = ran;
+            continue;
+        }
+        // the next interval, on the prediction that this one takes cur.k rounds
+        if (i + 1 < count && pipe_ok(h, root, reset, cur.round0 + cur.k, cur.k, true)) {
+            const auto it = h->mono_of.find(root);
+            snap = PipeSnap{h->epoch, h->serial, it->second, h->par};
+            const int rc = pipe_enqueue(h, root, reset, cur.k, cur.region ^ 1u, true, cur.round0 + cur.k, next);
+            if (rc) return rc;
+            have_next = true;
+        }
+        bool quiet = false;
+        uint64_t before = 0;
+        int rc = pipe_collect(h, cur, out, room, ran, quiet, before);
+        if (rc) return rc;
+        if (have_next && !(quiet && ran == cur.k && before != 0 && h->ost_cnt == 0)) {
+            // the device abandoned interval i + 1 (its guard saw the same counts): undo its bookkeeping
+            h->epoch = snap.epoch;
+            h->serial = snap.serial;
+            h->mono_of[root] = snap.mono;
+            h->par = snap.par;
+            have_next = false;
+            // its read-back (copy stream) lands before anything later writes those host rows
+            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev[4 + next.region], 0));
+        }
+        if (!quiet && ran < max_rounds) {   // more rounds than predicted: the plain driver, chunk by chunk
+            uint32_t more = 0;
+            rc = drive(h, max_rounds - ran, out ? out + std::min<size_t>(ran, room) : nullptr,
+                       room > ran ? room - ran : 0, true, &more);
+            if (rc) return rc;
+            ran += more;
+        }
+        used += std::min<size_t>(ran, room);
+        if (rounds) rounds[i] = ran;
+        if (monos) monos[i] = cur.mono;
+        if (done) *done = i + 1;
+        pred = ran;
+    }
+    return PSIM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2073,6 +2332,14 @@ int psim_plumtree_broadcast_run(psim_handle* h, uint32_t root, uint32_t* mono_ou
     if (rc) return rc;
     HIPCHK(h, hipSetDevice(h->device));
     return drive(h, max_rounds, stats, cap, true, rounds_run);
+}
+
+int psim_plumtree_broadcast_run_n(psim_handle* h, uint32_t root, uint32_t count, uint32_t reset_trees,
+                                  uint32_t max_rounds, psim_round_stats* stats, size_t cap, uint32_t* rounds,
+                                  uint32_t* monos, uint32_t* done) {
+    if (done) *done = 0;
+    if (!h) return PSIM_EINVAL;
+    return run_n(h, root, count, reset_trees != 0, max_rounds, stats, stats ? cap : 0, rounds, monos, done);
 }
 
 int psim_shard_init(psim_handle* h, int rank, int world) {

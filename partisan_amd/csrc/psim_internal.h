@@ -257,6 +257,15 @@ struct PtArgs {
     uint32_t* __restrict__ obin;           // [nf] vertices of the fine bin holding outstanding rows
     uint32_t fv_shift, cv_shift;           // fine bin = 2^fv_shift vertices, coarse = 2^cv_shift
     uint32_t nf, nc, chunks;               // bins; route chunks per sub-region
+    // a heartbeat enqueued before the previous one was read back
+    // (psim_plumtree_broadcast_run_n, psim_host.hip): spec[0] = 1 makes every
+    // kernel of it return at once, spec[1] = its origin's decision (1 run,
+    // 2 abandoned).  The origin runs it only if the previous heartbeat ended
+    // exactly at its predicted last round, ring slot spec_rl (mod 4): no
+    // message in that round, some in the one before, no row holder left.
+    // null: no guard (every other launch).
+    uint32_t* spec;
+    uint32_t spec_rl;
 };
 
 // The forest (psim_config.max_roots > 16): every node's

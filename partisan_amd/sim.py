@@ -152,6 +152,23 @@ class Simulator:
             return mono.value, np.frombuffer(st, dtype=_ROUND_DTYPE, count=k).copy(), ran.value
         return mono.value, [s.as_dict() for s in st[:k]], ran.value
 
+    def broadcast_run_n(self, root, count, reset_trees=True, max_rounds=100000, cap=None):
+        """`count` heartbeat intervals of `root` back to back in one call
+        (psim_plumtree_broadcast_run_n): each reset_trees() (when asked) then
+        broadcast_run(root).  Returns (ids, per-round stats of every interval
+        as one numpy record array, rounds per interval)."""
+        cap = cap if cap is not None else 64 * max(1, count)
+        st = getattr(self, "_runn_buf", None)
+        if st is None or len(st) < cap:
+            st = self._runn_buf = (RoundStats * cap)()
+        rounds = np.zeros(count, np.uint32)
+        monos = np.zeros(count, np.uint32)
+        done = C.c_uint32()
+        self._c(lib().psim_plumtree_broadcast_run_n(self._h, root, count, 1 if reset_trees else 0, max_rounds, st, cap,
+                                                    _u32p(rounds), _u32p(monos), C.byref(done)))
+        k = min(int(rounds.astype(np.int64).sum()), cap)
+        return monos, np.frombuffer(st, dtype=_ROUND_DTYPE, count=k).copy(), rounds
+
     def plumtree_state(self):
         n = self.n
         eager = np.zeros(n, np.uint32)

@@ -41,6 +41,14 @@ def main():
         big = sorted(((g, seg[k][2], seg[k + 1][2]) for k, g in enumerate(gaps)), reverse=True)[:4]
         print(f"step {si}: span {span:.1f} us, kernels {busy:.1f} us, ops {len(seg)}, gaps sum {sum(gaps):.1f} us, "
               f"largest {[(round(g, 1), a, b) for g, a, b in big]}")
+        if si + 1 < len(starts):   # between steps: the step's last operation (its stats copy) to the next origin
+            tail = ops[i:j]
+            t_end = max(o[1] for o in tail)
+            after = [o for o in tail if o[0] >= seg[-1][1]]
+            print(f"   between steps: {len(after)} ops after the last round "
+                  f"({', '.join(f'{a[2]} {(a[1] - a[0]) / 1e3:.1f} us' for a in after)}), "
+                  f"device idle until the next origin {(ops[j][0] - t_end) / 1e3:.1f} us, "
+                  f"last round end to next origin {(ops[j][0] - seg[-1][1]) / 1e3:.1f} us")
         if si == 0:
             for o in seg:
                 print(f"   {(o[0] - seg[0][0]) / 1e3:9.1f} {(o[1] - o[0]) / 1e3:8.1f}  {o[2]}")
