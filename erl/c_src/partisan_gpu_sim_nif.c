@@ -277,6 +277,52 @@ static ERL_NIF_TERM nif_broadcast_run(ErlNifEnv* env, int argc, const ERL_NIF_TE
     return enif_make_tuple4(env, mk_atom(env, "ok"), enif_make_uint(env, mono), enif_make_uint(env, ran), list);
 }
 
+/* broadcast_run_n(Sim, Root, Count, Reset, MaxRounds) -> {ok, [{Id, Rounds}], [StatsMap]}:
+ * Count heartbeat intervals of one root back to back, reset_trees before
+ * each when Reset is 1 -- the same as Count reset_trees/1 + broadcast_run/3
+ * calls (psim_plumtree_broadcast_run_n) */
+static ERL_NIF_TERM nif_broadcast_run_n(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned root, count, reset, maxr;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &root) || !enif_get_uint(env, argv[2], &count) ||
+        !enif_get_uint(env, argv[3], &reset) || !enif_get_uint(env, argv[4], &maxr) || count == 0 || count > 4096 ||
+        reset > 1)
+        return enif_make_badarg(env);
+    enum { CAP = 65536 };
+    psim_round_stats* st = (psim_round_stats*)enif_alloc(CAP * sizeof(psim_round_stats));
+    uint32_t* rounds = (uint32_t*)enif_alloc(count * sizeof(uint32_t));
+    uint32_t* monos = (uint32_t*)enif_alloc(count * sizeof(uint32_t));
+    if (!st || !rounds || !monos) {
+        if (st) enif_free(st);
+        if (rounds) enif_free(rounds);
+        if (monos) enif_free(monos);
+        return err(env, PSIM_ENOMEM);
+    }
+    uint32_t done = 0;
+    enif_mutex_lock(r->mu);
+    int rc = psim_plumtree_broadcast_run_n(r->h, root, count, reset, maxr, st, CAP, rounds, monos, &done);
+    enif_mutex_unlock(r->mu);
+    if (rc != PSIM_OK) {
+        enif_free(st);
+        enif_free(rounds);
+        enif_free(monos);
+        return err(env, rc);
+    }
+    uint64_t total = 0;
+    ERL_NIF_TERM ivs = enif_make_list(env, 0);
+    for (uint32_t i = count; i > 0; i--)
+        ivs = enif_make_list_cell(env, enif_make_tuple2(env, enif_make_uint(env, monos[i - 1]),
+                                                        enif_make_uint(env, rounds[i - 1])), ivs);
+    for (uint32_t i = 0; i < count; i++) total += rounds[i];
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (uint64_t i = total < CAP ? total : CAP; i > 0; i--) list = enif_make_list_cell(env, stats_term(env, &st[i - 1]), list);
+    enif_free(st);
+    enif_free(rounds);
+    enif_free(monos);
+    return enif_make_tuple3(env, mk_atom(env, "ok"), ivs, list);
+}
+
 /* step(Sim, Rounds) -> {ok, [StatsMap]} */
 static ERL_NIF_TERM nif_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
@@ -1633,6 +1679,7 @@ static ErlNifFunc funcs[] = {
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"run", 2, nif_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"broadcast_run", 3, nif_broadcast_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"broadcast_run_n", 5, nif_broadcast_run_n, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"peers", 1, nif_peers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"slots", 1, nif_slots, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"delivered", 1, nif_delivered, ERL_NIF_DIRTY_JOB_CPU_BOUND},

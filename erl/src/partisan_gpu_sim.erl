@@ -7,7 +7,7 @@
 -module(partisan_gpu_sim).
 
 -export([new/1, load_csr/3, set_alive/2, reset_trees/1, restart_backend/2, broadcast/2, broadcast_many/2,
-         step/2, run/2, broadcast_run/3,
+         step/2, run/2, broadcast_run/3, broadcast_run_n/5,
          peers/1, slots/1, delivered/1, trace_hash/1, focus/2, set_omissions/3, set_delays/4, delivered_mono/2, is_delivered/3, rows/2, messages/1, shard_step/2,
          relay_run/10,
          hv_setup/3, hv_join/3, hv_step/2, hv_views/1,
@@ -76,6 +76,11 @@ run(_Sim, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 -spec broadcast_run(sim(), non_neg_integer(), pos_integer()) ->
     {ok, non_neg_integer(), non_neg_integer(), [map()]} | error().
 broadcast_run(_Sim, _Root, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
+%% Count heartbeat intervals of one root back to back (reset_trees/1 before
+%% each when Reset is 1): the same as Count broadcast_run/3 calls
+-spec broadcast_run_n(sim(), non_neg_integer(), pos_integer(), 0 | 1, pos_integer()) ->
+    {ok, [{non_neg_integer(), non_neg_integer()}], [map()]} | error().
+broadcast_run_n(_Sim, _Root, _Count, _Reset, _MaxRounds) -> erlang:nif_error(nif_not_loaded).
 
 -spec peers(sim()) -> {ok, binary(), binary(), binary(), binary()} | error().
 peers(_Sim) -> erlang:nif_error(nif_not_loaded).

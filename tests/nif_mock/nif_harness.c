@@ -183,6 +183,25 @@ int main(int argc, char** argv) {
                     (unsigned long long)mock_int(mock_elem(th2, 1)), (unsigned long long)mock_int(mock_elem(th2, 2)),
                     (unsigned long long)mock_int(mock_elem(th2, 3)));
         }
+        {   /* three more heartbeats of root 0 over its tree in one call: broadcast_run_n */
+            ERL_NIF_TERM bn = want_ok_tuple("broadcast_run_n", call("broadcast_run_n", 5,
+                                            A(sim, mock_uint(0), mock_uint(3), mock_uint(0), mock_uint(1000))));
+            ERL_NIF_TERM ivs = mock_elem(bn, 1), st3 = mock_elem(bn, 2);
+            uint64_t b3 = 0, y;
+            for (size_t i = 0; i < mock_list_len(st3); i++)
+                if (mock_map_get(mock_list_nth(st3, i), "broadcast", &y)) b3 += y;
+            ERL_NIF_TERM th3 = mock_elem(want_ok_tuple("trace_hash", call("trace_hash", 1, A(sim))), 1);
+            fprintf(g_out, ", \"c2_hb345\": {\"intervals\": [");
+            for (size_t i = 0; i < mock_list_len(ivs); i++) {
+                ERL_NIF_TERM iv = mock_list_nth(ivs, i);
+                fprintf(g_out, "%s[%llu, %llu]", i ? ", " : "", (unsigned long long)mock_int(mock_elem(iv, 0)),
+                        (unsigned long long)mock_int(mock_elem(iv, 1)));
+            }
+            fprintf(g_out, "], \"rows\": %zu, \"broadcasts\": %llu, \"trace\": [\"%llu\", \"%llu\", \"%llu\", \"%llu\"]}",
+                    mock_list_len(st3), (unsigned long long)b3, (unsigned long long)mock_int(mock_elem(th3, 0)),
+                    (unsigned long long)mock_int(mock_elem(th3, 1)), (unsigned long long)mock_int(mock_elem(th3, 2)),
+                    (unsigned long long)mock_int(mock_elem(th3, 3)));
+        }
         /* the same overlay, vertex-sharded at world 1 with the library's own RCCL communicator */
         ERL_NIF_TERM sim7 = new_sim(0x5EED0002ull);
         ERL_NIF_TERM id = mock_elem(want_ok_tuple("rccl_unique_id", call("rccl_unique_id", 0, A(0))), 1);

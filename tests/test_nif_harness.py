@@ -165,4 +165,16 @@ def test_nif_harness_on_gpu(tmp_path):
     assert rounds == rep["c2_hb2"]["rounds"]
     assert sum(x["broadcast"] for x in stats) == rep["c2_hb2"]["broadcasts"]
     assert [str(x) for x in sim.trace_hash()] == rep["c2_hb2"]["trace"]
+    # three more over the tree in one NIF call (broadcast_run_n) = three broadcast + run here
+    got, bsum, nrows = [], 0, 0
+    for _ in range(3):
+        m = sim.broadcast(0)
+        stats, rounds = sim.run(1000)
+        got.append([m, rounds])
+        bsum += sum(x["broadcast"] for x in stats)
+        nrows += len(stats)
+    assert got == rep["c2_hb345"]["intervals"]
+    assert nrows == rep["c2_hb345"]["rows"]
+    assert bsum == rep["c2_hb345"]["broadcasts"]
+    assert [str(x) for x in sim.trace_hash()] == rep["c2_hb345"]["trace"]
     sim.close()
