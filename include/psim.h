@@ -518,6 +518,15 @@ int  psim_hv_set_alive(psim_handle* h, const uint8_t* alive, size_t n);
  * between rounds (delivered by the next round).  The v[i] must be distinct. */
 int  psim_hv_join(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k);
 int  psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* stats, size_t cap);
+/* Sequential joins (config C2's schedule): vertex v[i] joins contact[i],
+ * then `rounds` rounds run, for i = 0..k-1 -- the same state, draws and
+ * per-round stats (k * rounds rows, up to cap) as k psim_hv_join(v + i,
+ * contact + i, 1) + psim_hv_step(rounds) calls, with one host wait per 16
+ * rounds instead of two per join.  An error is reported with the round it
+ * happened in, after the rounds enqueued with it ran (the state is then
+ * spent: set up again). */
+int  psim_hv_join_seq(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k, uint32_t rounds,
+                      psim_hv_stats* stats, size_t cap);
 /* act[n*8], pas[n*32] padded with 0xFFFFFFFF; na/np = view sizes (active
  * includes self, as sets:to_list(Active) does). */
 int  psim_hv_get_views(const psim_handle* h, uint32_t* act, uint8_t* na, uint32_t* pas, uint8_t* np, size_t n);

@@ -244,6 +244,7 @@ SIGNATURES = {
     "psim_hv_set_alive": (C.c_int, [_H, _P(C.c_uint8), C.c_size_t]),
     "psim_hv_join": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_hv_step": (C.c_int, [_H, C.c_uint32, _P(HvStats), C.c_size_t]),
+    "psim_hv_join_seq": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t, C.c_uint32, _P(HvStats), C.c_size_t]),
     "psim_hv_get_views": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint8), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_hv_get_draws": (C.c_int, [_H, _P(C.c_uint64), C.c_size_t]),
     "psim_hv_get_idmap": (C.c_int, [_H, C.c_uint32, C.c_int, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),

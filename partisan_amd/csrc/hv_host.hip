@@ -39,12 +39,16 @@ struct HvState : ModuleState {
     hipEvent_t ev[2 * 16] = {};
     uint32_t par = 0;                         // queue the next round reads
     uint64_t round = 0;
+    // psim_hv_join_seq: a chunk's join rows and round rows (device, pinned)
+    unsigned long long* seq_stats = nullptr;
+    unsigned long long* h_seq_stats = nullptr;
     ~HvState() override {
         void* ptrs[] = {head, act, pas, skey, sval, rkey, rval, alive, msg[0], msg[1], nmsg,
-                        cnt, cur, off, idx, bsum, joinbuf, stats, idx2};
+                        cnt, cur, off, idx, bsum, joinbuf, stats, idx2, seq_stats};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (h_stats) (void)hipHostFree(h_stats);
+        if (h_seq_stats) (void)hipHostFree(h_seq_stats);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
     }
@@ -242,6 +246,102 @@ int psim_hv_step(psim_handle* h, uint32_t rounds, psim_hv_stats* out, size_t cap
         }
         v.round += k;
         done += k;
+    }
+    return PSIM_OK;
+}
+
+int psim_hv_join_seq(psim_handle* h, const uint32_t* v, const uint32_t* contact, size_t k, uint32_t rounds,
+                     psim_hv_stats* out, size_t cap) {
+    if (!h || (k && (!v || !contact))) return PSIM_EINVAL;
+    auto& hv = hv_ref(h);
+    if (!hv.n) return handle_fail(h, PSIM_ESTATE, "psim_hv_setup not called");
+    if (k > hv.n) return handle_fail(h, PSIM_EINVAL, "%zu joins for %u vertices", k, hv.n);
+    for (size_t i = 0; i < k; i++)
+        if (v[i] >= hv.n || contact[i] >= hv.n) return handle_fail(h, PSIM_EINVAL, "join %zu: vertex out of range", i);
+    if (!k) return PSIM_OK;
+    HIPCHK(h, hipSetDevice(handle_device(h)));
+    const hipStream_t st = handle_stream(h);
+    // every join pair uploaded once (join i reads entry i)
+    HIPCHK(h, hipMemcpyAsync(hv.joinbuf, v, k * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(hv.joinbuf + hv.n, contact, k * 4, hipMemcpyHostToDevice, st));
+    // a chunk: J joins, each followed by `rounds` rounds, with an event pair per
+    // round (the handle's 2 x 16 events) -- one host wait per chunk
+    const uint32_t per = 1u + rounds;
+    const uint32_t J = rounds ? std::max<uint32_t>(1u, kHvChunk / std::max<uint32_t>(1u, rounds)) : kHvChunk;
+    if (rounds > kHvChunk) {
+        // long waits between joins: one join at a time through the plain calls
+        size_t used = 0;
+        for (size_t i = 0; i < k; i++) {
+            int rc = psim_hv_join(h, v + i, contact + i, 1);
+            if (rc) return rc;
+            std::vector<psim_hv_stats> tmp(rounds);
+            rc = psim_hv_step(h, rounds, tmp.data(), rounds);
+            if (rc) return rc;
+            for (uint32_t r = 0; r < rounds && out && used < cap; r++) out[used++] = tmp[r];
+        }
+        return PSIM_OK;
+    }
+    const size_t rows = size_t(J) * per;
+    if (!hv.seq_stats) {
+        if (!alloc_zero((void**)&hv.seq_stats, rows * kHvNStat * 8) ||
+            hipHostMalloc((void**)&hv.h_seq_stats, rows * kHvNStat * 8, 0) != hipSuccess) {
+            hv.h_seq_stats = nullptr;
+            return handle_fail(h, PSIM_ENOMEM, "hyparview join sequence rows");
+        }
+    }
+    size_t used = 0;
+    for (size_t j0 = 0; j0 < k; j0 += J) {
+        const uint32_t nj = (uint32_t)std::min<size_t>(J, k - j0);
+        HIPCHK(h, hipMemsetAsync(hv.seq_stats, 0, size_t(nj) * per * kHvNStat * 8, st));
+        for (uint32_t j = 0; j < nj; j++) {
+            unsigned long long* jr = hv.seq_stats + size_t(j) * per * kHvNStat;
+            // psim_hv_join: the join messages go to the queue the next round reads
+            HvArgs a = make_hv_args(h, hv.par ^ 1u, jr);
+            HIPCHK(h, launch_hv_join(a, hv.joinbuf + j0 + j, hv.joinbuf + hv.n + j0 + j, 1u, st));
+            // psim_hv_step(rounds)
+            for (uint32_t i = 0; i < rounds; i++) {
+                HvArgs b = make_hv_args(h, hv.par, jr + size_t(1 + i) * kHvNStat);
+                const uint64_t t = hv.round + uint64_t(j) * rounds + i + 1;
+                b.timers = (hv.cfg.promotion_rounds && t % hv.cfg.promotion_rounds == 0 ? 1u : 0u) |
+                           (hv.cfg.shuffle_rounds && t % hv.cfg.shuffle_rounds == 0 ? 2u : 0u);
+                HIPCHK(h, hipMemsetAsync(hv.nmsg + (hv.par ^ 1u), 0, 4, st));
+                HIPCHK(h, hipEventRecord(hv.ev[2 * (j * rounds + i)], st));
+                HIPCHK(h, launch_hv_round(b, st));
+                HIPCHK(h, hipEventRecord(hv.ev[2 * (j * rounds + i) + 1], st));
+                hv.par ^= 1u;
+            }
+        }
+        HIPCHK(h, hipMemcpyAsync(hv.h_seq_stats, hv.seq_stats, size_t(nj) * per * kHvNStat * 8, hipMemcpyDeviceToHost,
+                                 st));
+        HIPCHK(h, handle_wait(h));
+        for (uint32_t j = 0; j < nj; j++) {
+            const unsigned long long* jr = hv.h_seq_stats + size_t(j) * per * kHvNStat;
+            int rc = hv_check_err(h, jr[11], hv.round);             // the join, as psim_hv_join reports it
+            if (rc != PSIM_OK) { hv.round += uint64_t(nj - j) * rounds; return rc; }
+            for (uint32_t i = 0; i < rounds; i++) {
+                const unsigned long long* r = jr + size_t(1 + i) * kHvNStat;
+                const uint64_t t = hv.round + 1;
+                rc = hv_check_err(h, r[11], t);
+                if (rc != PSIM_OK) { hv.round += uint64_t(nj - j) * rounds - i; return rc; }
+                float ms = 0.f;
+                HIPCHK(h, hipEventElapsedTime(&ms, hv.ev[2 * (j * rounds + i)], hv.ev[2 * (j * rounds + i) + 1]));
+                handle_add_round(h, ms);
+                if (out && used < cap) {
+                    psim_hv_stats& o = out[used];
+                    memset(&o, 0, sizeof o);
+                    uint64_t emitted = 0;
+                    for (int q = 1; q < 10; q++) { o.sent[q] = r[q]; emitted += r[q]; }
+                    o.draws = r[10];
+                    o.error = r[11];
+                    o.processed = r[12];
+                    o.active = r[13];
+                    o.algo_bytes = 64ull * (r[12] + emitted) + 2ull * 176ull * r[13] + 12ull * hv.n;
+                    o.kernel_ms = ms;
+                }
+                used++;
+                hv.round++;
+            }
+        }
     }
     return PSIM_OK;
 }

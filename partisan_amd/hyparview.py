@@ -53,6 +53,20 @@ class HyParViewCluster:
             raise ValueError("vs and contacts differ in length")
         self._c(lib().psim_hv_join(self.sim._h, _u32p(v), _u32p(c), len(v)))
 
+    def join_seq(self, vs, contacts, rounds=1):
+        """Sequential joins (C2's schedule) in one call (psim_hv_join_seq):
+        vs[i] joins contacts[i], then `rounds` rounds -- the same as
+        join(vs[i], contacts[i]) + step(rounds) per i.  Returns the rounds'
+        stats (len(vs) * rounds dicts)."""
+        v = np.ascontiguousarray(vs, dtype=np.uint32)
+        c = np.ascontiguousarray(contacts, dtype=np.uint32)
+        if v.shape != c.shape:
+            raise ValueError("vs and contacts differ in length")
+        k = len(v) * rounds
+        st = (HvStats * max(1, k))()
+        self._c(lib().psim_hv_join_seq(self.sim._h, _u32p(v), _u32p(c), len(v), rounds, st, k))
+        return [s.as_dict() for s in st[:k]]
+
     def step(self, rounds=1):
         st = (HvStats * max(1, rounds))()
         self._c(lib().psim_hv_step(self.sim._h, rounds, st, rounds))

@@ -130,6 +130,35 @@ def test_lockstep_sequential_joins_small():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rounds", [0, 1, 3, 20])
+def test_join_seq_equals_join_and_step(rounds):
+    """psim_hv_join_seq = psim_hv_join + psim_hv_step(rounds) per joiner:
+    per-round stats, views, draws and id maps (rounds 20: the plain calls)."""
+    import partisan_amd as pa
+    n = 600
+    c = contacts(n)
+    out = []
+    for seq in (False, True):
+        sim = pa.Simulator(seed=SEED)
+        g = pa.hyparview.HyParViewCluster(sim, n, shuffle_rounds=4, promotion_rounds=3)
+        if seq:
+            st = g.join_seq(np.arange(1, n, dtype=np.uint32), c[1:], rounds=rounds)
+        else:
+            st = []
+            for i in range(1, n):
+                g.join(i, int(c[i]))
+                if rounds:
+                    st += g.step(rounds)
+        st += g.step(7)
+        act, na, pas, np_ = g.views()
+        out.append(([{k: x[k] for k in ("sent", "draws", "error", "processed", "active")} for x in st],
+                    act.tolist(), na.tolist(), pas.tolist(), np_.tolist(), g.draws().tolist(),
+                    [sorted(g.idmap(v, w)) for v in range(0, n, 37) for w in (0, 1)], g.inflight()))
+        sim.close()
+    assert out[0] == out[1]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,cfg", [(3000, {}), (2000, dict(active_max_size=5, passive_max_size=12,
                                                             shuffle_rounds=4, promotion_rounds=3))])
 def test_mass_join_then_shuffles(n, cfg):
@@ -187,13 +216,14 @@ def test_c2_hyparview_overlay_then_plumtree():
     n = 10000
     sim, g, o = _pair(n)
     c = contacts(n)
-    gt, ot = np.zeros(9, np.int64), np.zeros(9, np.int64)
+    # the device's joins in one call (psim_hv_join_seq: the same schedule as
+    # a join + step(1) per vertex), round by round against the oracle's loop
+    gs = g.join_seq(np.arange(1, n, dtype=np.uint32), c[1:], rounds=1)
+    os_ = []
     for i in range(1, n):
-        g.join(i, int(c[i]))
         o.join(i, int(c[i]))
-        gt += np.array(g.step(1)[0]["sent"])
-        ot += np.array(o.step(1)[0]["sent"])
-    assert gt.tolist() == ot.tolist()
+        os_ += o.step(1)
+    _same_stats(gs, os_)
     _same_stats(g.step(100), o.step(100))
     _compare(g, o, n, maps=False)
     act, na, _, _ = g.views()

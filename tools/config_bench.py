@@ -36,11 +36,10 @@ def c2():
     hv = pa.hyparview.HyParViewCluster(sim, n)
     from partisan_amd.overlay import philox_uniform
     t0 = time.time()
-    st = []
-    for v in range(1, n):                        # vertex v joins a Philox contact in [0, v)
-        c = philox_uniform(0x5EED0002, np.array([v], np.uint32), 0xC200, v)
-        hv.join_many(np.array([v], np.uint32), np.asarray(c, np.uint32))
-        st += hv.step(1)
+    # vertex v joins a Philox contact in [0, v), one join per round: the whole
+    # sequence in one call (psim_hv_join_seq = join + step(1) per vertex)
+    vs = np.arange(1, n, dtype=np.uint32)
+    st = hv.join_seq(vs, philox_uniform(0x5EED0002, vs, 0xC200, vs), rounds=1)
     st += hv.step(10 * 10)                       # 10 shuffle periods (shuffle every 10 rounds)
     wall = time.time() - t0
     rp, col = hv.overlay()
@@ -60,10 +59,8 @@ def c2_overlay(n=10_000):
     sim = pa.Simulator(seed=0x5EED0002)
     hv = pa.hyparview.HyParViewCluster(sim, n)
     from partisan_amd.overlay import philox_uniform
-    for v in range(1, n):
-        c = philox_uniform(0x5EED0002, np.array([v], np.uint32), 0xC200, v)
-        hv.join_many(np.array([v], np.uint32), np.asarray(c, np.uint32))
-        hv.step(1)
+    vs = np.arange(1, n, dtype=np.uint32)
+    hv.join_seq(vs, philox_uniform(0x5EED0002, vs, 0xC200, vs), rounds=1)
     hv.step(10 * 10)
     rp, col = hv.overlay()
     sim.close()
