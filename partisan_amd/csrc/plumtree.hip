@@ -594,30 +594,38 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         return L.rows ? id : a.col[rs + q];
     };
     uint32_t r[kCap];
-    // A flood's words carry one message each, a broadcast or a prune: those
+    // A flood's words carry a broadcast, a prune, or both (a sender's prune
+    // reply and its eager push over the same slot, in either order): those
     // vertices take pt_word's clauses over slot masks at once, in the same
-    // slot order -- prunes below the first broadcast, its delivery
-    // (handle_broadcast(true)), then the later broadcasts' prunes and the later
-    // prunes (set operations on distinct slots commute) -- instead of a
-    // divergent per-slot FIFO walk.  Any other word: the general walk.
+    // slot order -- prunes below the first broadcast (and a prune ahead of it
+    // in its own word), its delivery (handle_broadcast(true)), then the later
+    // broadcasts' prunes and the later prunes (set operations on distinct
+    // slots commute; within a later slot both leave the peer lazy) -- instead
+    // of a divergent per-slot FIFO walk.  Any other word: the general walk.
+    constexpr uint32_t kBP = PSIM_MSG_BROADCAST | (PSIM_MSG_PRUNE << kKindBits);   // [broadcast, prune]
+    constexpr uint32_t kPB = PSIM_MSG_PRUNE | (PSIM_MSG_BROADCAST << kKindBits);   // [prune, broadcast]
     uint32_t bm = 0, pm = 0, om = 0;
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         const uint32_t f = w[s] & kFifoMask;
-        bm |= (f == PSIM_MSG_BROADCAST ? 1u : 0u) << s;
-        pm |= (f == PSIM_MSG_PRUNE ? 1u : 0u) << s;
-        om |= (f != 0u && f != PSIM_MSG_BROADCAST && f != PSIM_MSG_PRUNE ? 1u : 0u) << s;
+        const bool pair = f == kBP || f == kPB;
+        const bool b = f == PSIM_MSG_BROADCAST || pair;
+        const bool p = f == PSIM_MSG_PRUNE || pair;
+        bm |= (b ? 1u : 0u) << s;
+        pm |= (p ? 1u : 0u) << s;
+        om |= (f != 0u && !b && !p ? 1u : 0u) << s;
     }
     if (om == 0u) {
         uint32_t rep = 0;                                // slots answering a broadcast with a prune
         if (!x.rcv && bm) {
             const uint32_t s0 = (uint32_t)__ffs(bm) - 1u, b0 = 1u << s0;
-            const uint32_t pre = pm & (b0 - 1u);
-            x.eager &= ~pre;
-            x.lazy |= pre;
             uint32_t w0 = 0;
 #pragma unroll
             for (uint32_t k = 0; k < kCap; k++) w0 = k == s0 ? w[k] : w0;
+            // the delivering word's own prune counts as earlier when it came first
+            const uint32_t pre = (pm & (b0 - 1u)) | ((w0 & kFifoMask) == kPB ? b0 : 0u);
+            x.eager &= ~pre;
+            x.lazy |= pre;
             x.rcv = true;                                // merge/2 -> true; handle_broadcast(true) :852-857
             x.rseq = a.mono8;
             x.myround = (w0 >> kRoundShift) + 1u;
