@@ -2003,8 +2003,11 @@ hipError_t launch_pt_round(const PtArgs& a, hipStream_t s) {
         const bool f = a.omit || a.dly;
         // kLocal: one GPU, not sharded (no staging ring, no staged remote words)
         const bool loc = !a.stage && !a.srg;
+        // rows of exactly 5 slots (HyParView's active view, the bench overlay):
+        // a kernel unrolled for 5, not 6 -- one slot fewer in every per-slot loop
         const auto k = a.ell <= 4 ? (f ? pt_round_ell_kernel<true, 4, false>
                                        : loc ? pt_round_ell_kernel<false, 4, true> : pt_round_ell_kernel<false, 4, false>)
+                     : a.ell == 5 && !f ? (loc ? pt_round_ell_kernel<false, 5, true> : pt_round_ell_kernel<false, 5, false>)
                      : a.ell <= 6 ? (f ? pt_round_ell_kernel<true, 6, false>
                                        : loc ? pt_round_ell_kernel<false, 6, true> : pt_round_ell_kernel<false, 6, false>)
                                   : (f ? pt_round_ell_kernel<true, 8, false>

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-5 (session 2): a flood's broadcast + prune pair words on the
+# Round-5 (session 2): A/B of the round kernel (see the commit): first the
 # round kernel's slot-mask path (new) vs the per-slot FIFO walk for them
 # (old = exp_head.so): Plumtree lockstep parity, bench A/B, per-round SQ
 # counters.
