@@ -442,8 +442,10 @@ constexpr uint32_t kFastDeg = 8;
 // kLdsWords: the round kernel already gathered the vertex's live inbox words
 // into LDS (pt_round_ell_body) and `lw` points at them.
 // kCap (>= deg): the register arrays' size.  The ELL kernel is instantiated
-// per row-width class (4 / 6 / 8) so a 5-wide HyParView row holds 6 slots in
-// registers, not 8: fewer VGPRs, more waves per SIMD to hide the chain.
+// per row-width class (4 / 6 / 8, and 5 for rows of exactly 5 slots without
+// faults: HyParView's active view) so a row holds as few slots in registers
+// as it has: fewer VGPRs (kCap 6 spilled 3 to scratch once the pair words
+// joined the mask path), one slot fewer in every unrolled loop.
 // Streaming loads: the inbox words a round sweeps are read once and are stale
 // after it, so the sweep loads them non-temporally and they do not displace
 // the lines the round scatters its own words into (2.43 -> 2.33 ms per 10M
