@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
-# Round-5: every per-round host wait by polling an event (new) vs blocking
-# stream syncs (old = exp_pre_spin.so): parity of the engines, config lines A/B.
+# Round-5 (session 5): the bench round kernel at six waves per SIMD
+# (PSIM_OCC6=1, 80 VGPRs, 13 spilled) vs five: parity of the variant, then the
+# bench's per-round table for both, to see which rounds (if any) gain.
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -8,17 +9,29 @@ step() {  # name seconds cmd...  (stops the session on a GPU fault, abort, kill 
     local name=$1 secs=$2; shift 2
     echo "=== $name" ; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
-    echo "=== $name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-300
+    echo "=== $name rc=$rc"; tail -1 "gpurun_out/$name.log" | cut -c1-300
     if grep -qiE "illegal memory|memory access fault|HSA_STATUS_ERROR|hipErrorLaunchFailure|core dumped" "gpurun_out/$name.log"; then
         echo "=== GPU fault in $name: stopping"; exit 3
     fi
     [ $rc -le 1 ] || exit $rc
 }
-OLD=$PWD/partisan_amd/exp_pre_spin.so
-step parity 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_hyparview.py tests/test_scamp.py tests/test_c3.py tests/test_demers.py tests/test_causal.py tests/test_forest.py tests/test_fullmem.py
+PSIM_OCC6=1 step parity 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_run_n.py tests/test_worklist_parity.py
 grep -q " passed" gpurun_out/parity.log && ! grep -q "failed" gpurun_out/parity.log || { echo "=== parity not green: stopping"; exit 4; }
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-s 1"
 for rep in 1 2; do
-  step cfg_new_$rep 400 python tools/config_bench.py C2 C3 C4 C5
-  PSIM_LIB_PATH=$OLD step cfg_old_$rep 400 python tools/config_bench.py C2 C3 C4 C5
+  PSIM_OCC6=1 step o_new_$rep 200 $B
+  step o_old_$rep 200 $B
 done
+python3 - <<'PY'
+import json, glob
+rows = {}
+for f in sorted(glob.glob("gpurun_out/o_*.log")):
+    for l in open(f):
+        if l.startswith("{"):
+            d = json.loads(l)
+            print(f, round(d["ms_per_step"], 4), round(d["sustained"]["ms_per_step"], 4))
+            rows[f] = [r["us"] for r in d["roofline"]["per_round"]]
+for f, r in rows.items():
+    print(f.split("/")[-1], " ".join("%6.1f" % x for x in r))
+PY
 echo "=== session done"
