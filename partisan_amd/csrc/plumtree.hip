@@ -1014,13 +1014,16 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     // 64 c + 64) of the groups the last round listed -- so a sparse round
     // costs one dispatch of the resident grid, not of n / 1024 workgroups
     // whose LDS must be allocated before each can find it has nothing to do.
-    // list mode: the listed groups are spread over every resident workgroup (gpc groups per chunk,
-    // PtArgs::wl_gpc or total / grid): a chunk of 64 groups loaded one CU with ~64 receivers' random
-    // loads per dependent step, and one CU sustains only ~0.45 G random loads/s (tools/mb_latency.hip)
+    // list mode: the listed groups are spread over the resident workgroups (gpc groups per chunk,
+    // PtArgs::wl_gpc or total / min(grid, wl_wgs)): a chunk of 64 groups loaded one CU with ~64
+    // receivers' random loads per dependent step, and one CU sustains only ~0.45 G random loads/s
+    // (tools/mb_latency.hip); spread over all 1,280, a round of 1-20k groups paid every busy
+    // workgroup's fixed costs (counts, claims, counter flushes) -- 256 measured best
     const uint32_t total = wl_off[64];
+    const uint32_t lwg = a.wl_wgs ? min(a.wl_wgs, gridDim.x) : gridDim.x;
     const uint32_t gpc = !list ? kGroups
                        : a.wl_gpc ? min(a.wl_gpc, kGroups)
-                                  : max(1u, min(kGroups, (total + gridDim.x - 1) / gridDim.x));
+                                  : max(1u, min(kGroups, (total + lwg - 1) / lwg));
     const uint32_t nchunks = list ? (total + gpc - 1) / gpc : (a.n + kEllChunk - 1) / kEllChunk;
     if (blockIdx.x >= nchunks) return;                 // uniform
     if (t == 0) wl.n = 0;

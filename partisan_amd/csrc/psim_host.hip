@@ -100,6 +100,12 @@ struct psim_handle {
     uint32_t wl_cap = 0;
     uint32_t wl_thr = 0;                     // 0: ng / 8 (PSIM_WL_THR test knob: list mode up to that count)
     uint32_t wl_gpc = 0;                     // listed groups per ELL chunk, 0: spread (PSIM_WL_GPC A/B knob)
+    // list mode: the listed groups spread over at most wl_wgs workgroups (0:
+    // the whole resident grid; PSIM_WL_WGS A/B knob).  A flood's rounds 5-7
+    // (1-20k listed groups) take 19 / 20 / 26 us at 128-512 against 27 / 28 /
+    // 31 us over all 1,280: the busy workgroups' fixed costs (counts, flag
+    // claims, counter flushes) outweigh the spread (profiles/r05/experiments/ab_wl_wgs.txt)
+    uint32_t wl_wgs = 256;
     uint32_t ell_grid = 0;                   // grid of the ELL round kernel (resident workgroups)
     hipEvent_t ev[2 * kChunk] = {};
     hipEvent_t ev_done = nullptr;            // end of a chunk's work, polled (chunk_wait)
@@ -554,6 +560,7 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
         a.wl_cap = h->wl_cap;
         a.wl_thr = thr;
         a.wl_gpc = h->wl_gpc;
+        a.wl_wgs = h->wl_wgs;
     }
 }
 
@@ -1122,6 +1129,7 @@ FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned l
         a.wl_cap = h->wl_cap;
         a.wl_thr = thr;
         a.wl_gpc = h->wl_gpc;
+        a.wl_wgs = h->wl_wgs;
     }
     FoArgs fa{};
     fa.a = a;
@@ -1751,6 +1759,7 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->pend_bytes = pend_bytes;
     h->wl_thr = getenv("PSIM_WL_THR") ? uint32_t(strtoul(getenv("PSIM_WL_THR"), nullptr, 10)) : 0u;
     h->wl_gpc = getenv("PSIM_WL_GPC") ? uint32_t(strtoul(getenv("PSIM_WL_GPC"), nullptr, 10)) : 0u;
+    h->wl_wgs = getenv("PSIM_WL_WGS") ? uint32_t(strtoul(getenv("PSIM_WL_WGS"), nullptr, 10)) : 256u;
     h->wl_off = wl_off;
     h->wl_cap = wl_cap;
     sh.n_global = n;

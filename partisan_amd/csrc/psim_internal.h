@@ -222,6 +222,8 @@ struct PtArgs {
     uint32_t* wl_nxt;
     uint32_t wl_cap, wl_thr;
     uint32_t wl_gpc;                       // listed groups per ELL chunk (0: spread over the grid; A/B knob)
+    uint32_t wl_wgs;                       // list mode: groups spread over at most this many workgroups (0: the
+                                           // grid; psim_host.hip psim_handle::wl_wgs)
     uint32_t ell_grid;                     // ELL kernel grid = resident workgroups (0: one per chunk)
     uint32_t force_flags;                  // this round writes group flags whatever its count (the last round
                                            // of a sharded psim_shard_step: readers without counts come next)
