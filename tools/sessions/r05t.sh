@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# Round-5 (session 2): psim_plumtree_broadcast_run_n (pipelined intervals inside the
-# library) vs the loop; bench with the timed steps in one call (new) vs the
-# head's bench.py loop (bench_old.py), same library; a trace of the steps.
+# Round-5 (session 10): with list-mode rounds on 256 workgroups, the list
+# threshold (PSIM_WL_THR; default ng / 8 = 78,125 at 10M) raised so that
+# round 8 (81,785 words read) also reads a list: per-round tables.
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -15,20 +15,24 @@ step() {  # name seconds cmd...  (stops the session on a GPU fault, abort, kill 
     fi
     [ $rc -le 1 ] || exit $rc
 }
-step runn 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_run_n.py tests/test_plumtree_gpu.py tests/test_worklist_parity.py tests/test_forest.py tests/test_shard.py tests/test_golden_traces.py
-grep -q " passed" gpurun_out/runn.log && ! grep -q "failed" gpurun_out/runn.log || { echo "=== parity not green: stopping"; exit 4; }
-for rep in 1 2 3; do
-  step b_new_$rep 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-s 2
-  step b_old_$rep 200 python bench_old.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-s 2
+echo "=== session 10"
+
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-s 1"
+for rep in 1 2; do
+for g in 78125 160000 320000; do
+  PSIM_WL_THR=$g step t_${g}_$rep 200 $B
 done
-step trace 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/trace_t -o run --output-format csv -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --sustain-s 0
-python3 tools/trace_gaps.py "$(dirname $(find gpurun_out/trace_t -name 'run_kernel_trace.csv' | head -1))" > gpurun_out/trace_t_gaps.txt 2>&1
+done
 python3 - <<'PY'
 import json, glob
-for f in sorted(glob.glob("gpurun_out/b_*.log")):
+rows = {}
+for f in sorted(glob.glob("gpurun_out/t_*.log")):
     for l in open(f):
         if l.startswith("{"):
-            d = json.loads(l); print(f, round(d["ms_per_step"], 4), round(d["sustained"]["ms_per_step"], 4), d["config"]["verified_after_timing"])
+            d = json.loads(l)
+            print(f, round(d["ms_per_step"], 4), round(d["sustained"]["ms_per_step"], 4))
+            rows[f] = [r["us"] for r in d["roofline"]["per_round"]]
+for f, r in rows.items():
+    print(f.split("/")[-1], " ".join("%6.1f" % x for x in r))
 PY
-grep -E "between" gpurun_out/trace_t_gaps.txt | head -8
 echo "=== session done"
