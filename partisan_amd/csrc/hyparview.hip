@@ -574,6 +574,49 @@ __global__ __launch_bounds__(kBlock) void hv_scatter(HvArgs a) {
     }
 }
 
+// Small overlays (C2: 10k peers, one join per round): a round's bucketing --
+// counts, exclusive scan, scatter -- by ONE workgroup with the counts in LDS,
+// instead of two fills and five launches that each cost a few microseconds
+// of a round moving a handful of messages.  The same off[] and the same
+// indices per bucket (their order within a bucket is free: hv_process sorts
+// each bucket by (src, seq)).
+constexpr uint32_t kHvSmallN = 12288;                // 48 KB of LDS counts
+__global__ __launch_bounds__(1024) void hv_bucket_small(HvArgs a) {
+    __shared__ uint32_t c[kHvSmallN];
+    __shared__ uint32_t ws[1024 / 64];
+    const uint32_t t = threadIdx.x, n = a.n, k = n_in(a);
+    for (uint32_t i = t; i < n; i += 1024) c[i] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < k; i += 1024) atomicAdd(&c[a.in[i].dst], 1u);
+    __syncthreads();
+    // exclusive scan: thread t sums its run of counts, the runs' sums are
+    // scanned over the workgroup, then each run is written out
+    const uint32_t per = (n + 1023) / 1024, lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; i++) s += c[i];
+    const uint32_t lane = t & 63, wv = t >> 6;
+    uint32_t x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wv; w++) pre += ws[w];
+    uint32_t run = pre + x - s;
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t y = c[i];
+        c[i] = run;                                   // the bucket's cursor
+        a.off[i] = run;
+        run += y;
+    }
+    if (t == 1023) a.off[n] = pre + x;
+    __syncthreads();
+    for (uint32_t i = t; i < k; i += 1024) a.idx[atomicAdd(&c[a.in[i].dst], 1u)] = i;
+}
+
 constexpr uint32_t kHvWaves = kBlock / 64;
 
 // the message with index i, fields made wave-uniform, x[] one per lane
@@ -808,14 +851,18 @@ hipError_t launch_hv_join(const HvArgs& a, const uint32_t* v, const uint32_t* co
 
 // one round: bucket the input messages by destination, then process
 hipError_t launch_hv_round(const HvArgs& a, hipStream_t s) {
-    hipError_t e;
-    if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(hv_count, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(hv_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(hv_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
-    hipLaunchKernelGGL(hv_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(hv_scatter, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
+    if (a.n <= kHvSmallN) {
+        hipLaunchKernelGGL(hv_bucket_small, dim3(1), dim3(1024), 0, s, a);
+    } else {
+        hipError_t e;
+        if ((e = hipMemsetAsync(a.cnt, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(a.cur, 0, size_t(a.n) * 4, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(hv_count, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(hv_scan_blocks, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(hv_scan_sums, dim3(1), dim3(1024), 0, s, a, nblk(a.n));
+        hipLaunchKernelGGL(hv_scan_add, dim3(nblk(a.n)), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(hv_scatter, dim3(kStrideBlocks), dim3(kBlock), 0, s, a);
+    }
     HvArgs b = a;
     b.group = hv_group(a.n);
     hipLaunchKernelGGL(hv_process, dim3(hv_blocks(a.n, b.group)), dim3(kBlock), 0, s, b);

@@ -1,6 +1,10 @@
 #!/usr/bin/env bash
-# Round-5 session H: C3 with the device call index and round prep kernels:
-# SCAMP / C3 parity, C3 lines, the phase split, rocprof stats.
+# Round-5 (session 11, final): small-overlay HyParView rounds bucket their
+# messages in one workgroup (hv_bucket_small) instead of two fills + five
+# launches: the C2 line new vs old (= exp_head.so) twice each; then on this
+# build the whole GPU suite (HyParView parity on both paths: <= 12,288 and
+# larger overlays) and smoke, PMC FETCH / WRITE keyed to its sha256, the
+# bench and rocprof kernel stats.
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -8,17 +12,23 @@ step() {  # name seconds cmd...  (stops the session on a GPU fault, abort, kill 
     local name=$1 secs=$2; shift 2
     echo "=== $name" ; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
-    echo "=== $name rc=$rc"; tail -4 "gpurun_out/$name.log" | cut -c1-600
+    echo "=== $name rc=$rc"; tail -1 "gpurun_out/$name.log" | cut -c1-400
     if grep -qiE "illegal memory|memory access fault|HSA_STATUS_ERROR|hipErrorLaunchFailure|core dumped" "gpurun_out/$name.log"; then
         echo "=== GPU fault in $name: stopping"; exit 3
     fi
     [ $rc -le 1 ] || exit $rc
 }
-step sc_parity 500 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_scamp.py tests/test_c3.py
-grep -q " passed" gpurun_out/sc_parity.log && ! grep -q "failed" gpurun_out/sc_parity.log || { echo "=== parity not green: stopping"; exit 4; }
-step win_parity 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_plumtree_gpu.py -k "overlapping or window"
-step c3_1 200 python tools/config_bench.py C3
-step c3_2 200 python tools/config_bench.py C3
-step c3prof 300 python tools/c3_prof.py 1000000 30
-step prof_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/config_bench.py C3
+OLD=$PWD/partisan_amd/exp_head.so
+for rep in 1 2; do
+  step c2h_new_$rep 300 python tools/config_bench.py C2
+  PSIM_LIB_PATH=$OLD step c2h_old_$rep 300 python tools/config_bench.py C2
+done
+step gpu_suite 1500 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
+grep -q " passed" gpurun_out/gpu_suite.log && ! grep -q "failed" gpurun_out/gpu_suite.log || { echo "=== suite not green: stopping"; exit 4; }
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sustain-s 0
+step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sustain-s 0
+python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --n 10000000 --peers 5 --rounds-per-step 16 --steps 4 --source profiles/r05 --out gpurun_out/pmc_traffic.json > gpurun_out/pmc_traffic.log 2>&1 || exit 5
+step bench 600 python bench.py --steps 20 --warmup 5 --traffic-json gpurun_out/pmc_traffic.json
+step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-s 0
 echo "=== session done"
