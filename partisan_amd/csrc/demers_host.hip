@@ -263,8 +263,22 @@ int dms_x_buffers(psim_handle* h, DmShard& d) {
         !A(&d.x_pull_all, 2 * NG) || !A(&d.x_pull_sum, 2 * size_t(d.chunk)) || !A(&d.x_snap_all, NG) ||
         !A(&d.x_rmx_all, NG + (NG + 1) / 2) || !alloc_zero((void**)&d.x_cnt, G1 * 4) ||
         !alloc_zero((void**)&d.x_off, 2 * G1 * 4) || !alloc_zero((void**)&d.x_cur, G1 * 4) ||
-        hipHostMalloc((void**)&d.h_x, 3 * G1 * 4, 0) != hipSuccess)
+        hipHostMalloc((void**)&d.h_x, 3 * G1 * 4, 0) != hipSuccess) {
+        // all or nothing: x_rm_shadow is the "present" test of every later call
+        unsigned long long** dev64[] = {&d.x_rm_shadow, &d.x_rm_recv, &d.x_pull_shadow, &d.x_pull_all,
+                                        &d.x_pull_sum, &d.x_snap_all, &d.x_rmx_all};
+        for (auto** p : dev64) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+        }
+        uint32_t** dev32[] = {&d.x_cnt, &d.x_off, &d.x_cur};
+        for (auto** p : dev32) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+        }
+        d.h_x = nullptr;      // hipHostMalloc is the last allocation: it is the one that failed, if any
         return handle_fail(h, PSIM_ENOMEM, "demers exchange buffers for %zu slots", NG);
+    }
     return PSIM_OK;
 }
 
@@ -716,7 +730,11 @@ int psim_demers_shard_broadcast_x(psim_handle* h) {
     if (!h) return PSIM_EINVAL;
     DmShard* d = dms_of(h);
     if (!d) return handle_fail(h, PSIM_ESTATE, "psim_demers_shard_setup not called");
+    const bool fresh = !d->x_rm_shadow;
     int rc = dms_x_buffers(h, *d);
+    // as in psim_demers_shard_step: a shard that cannot allocate must not leave the
+    // others waiting in dms_exchange's collectives
+    if (fresh && d->world > 1 && handle_transport(h)) rc = agree_rc(h, handle_transport(h), rc, "demers exchange buffers");
     if (rc) return rc;
     rc = dms_exchange(h, *d, false, psim_demers_shard_broadcast_all(h, d->x_rm_shadow, d->x_rmx_all));
     if (!rc) rc = psim_demers_shard_ingest(h, d->x_rm_recv, d->x_pull_sum, d->x_rmx_all, 0);

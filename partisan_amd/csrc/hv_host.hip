@@ -281,11 +281,18 @@ int psim_hv_join_seq(psim_handle* h, const uint32_t* v, const uint32_t* contact,
         }
         return PSIM_OK;
     }
+    // rows = J·(rounds+1) <= (kHvChunk/r)·(r+1) <= 2·kHvChunk for every rounds <= kHvChunk
+    // (rounds = 1 is the worst, rounds = 0 needs kHvChunk): the buffers are sized once for
+    // that bound, so a later call with another `rounds` on the same handle never outgrows them
     const size_t rows = size_t(J) * per;
+    constexpr size_t kSeqRows = 2 * size_t(kHvChunk);
+    if (rows > kSeqRows) return handle_fail(h, PSIM_ESTATE, "join sequence rows %zu > %zu", rows, kSeqRows);
     if (!hv.seq_stats) {
-        if (!alloc_zero((void**)&hv.seq_stats, rows * kHvNStat * 8) ||
-            hipHostMalloc((void**)&hv.h_seq_stats, rows * kHvNStat * 8, 0) != hipSuccess) {
+        if (!alloc_zero((void**)&hv.seq_stats, kSeqRows * kHvNStat * 8) ||
+            hipHostMalloc((void**)&hv.h_seq_stats, kSeqRows * kHvNStat * 8, 0) != hipSuccess) {
             hv.h_seq_stats = nullptr;
+            if (hv.seq_stats) (void)hipFree(hv.seq_stats);   // both or neither: the next call retries
+            hv.seq_stats = nullptr;
             return handle_fail(h, PSIM_ENOMEM, "hyparview join sequence rows");
         }
     }

@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
+#include <sched.h>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -858,12 +860,29 @@ int focus_root(psim_handle* h, uint32_t root, bool create) {
 // stream synchronisation: the host learns of it within a microsecond or so,
 // where the blocking wait's wake-up was part of the idle time between two
 // heartbeat intervals on the device.
+// The poll spins for at most kSpinUs of wall time (a heartbeat interval's chunk
+// is 0.1-3 ms: the spin covers the bench's waits), then yields the core between
+// polls, so a long run -- or a NIF call on a dirty scheduler -- does not pin a
+// core for its whole length.
+hipError_t event_wait(hipEvent_t ev) {
+    constexpr long kSpinUs = 5000;
+    hipError_t e;
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint32_t i = 0; (e = hipEventQuery(ev)) == hipErrorNotReady; i++) {
+        if ((i & 63) != 63) continue;
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        const long us = (t.tv_sec - t0.tv_sec) * 1000000L + (t.tv_nsec - t0.tv_nsec) / 1000L;
+        if (us > kSpinUs) sched_yield();
+    }
+    return e;
+}
+
 hipError_t chunk_wait(psim_handle* h) {
     hipError_t e = hipEventRecord(h->ev_done, h->stream);
     if (e != hipSuccess) return e;
-    while ((e = hipEventQuery(h->ev_done)) == hipErrorNotReady) {
-    }
-    return e;
+    return event_wait(h->ev_done);
 }
 
 int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap, bool stop_q,
@@ -2166,10 +2185,7 @@ int pipe_enqueue(psim_handle* h, uint32_t root, bool reset, uint32_t k, uint32_t
 // for a one-round interval) -- the guard's test, repeated on the host.
 int pipe_collect(psim_handle* h, const PipeRec& rec, psim_round_stats* out, size_t cap, uint32_t& ran, bool& quiet,
                  uint64_t& before) {
-    hipError_t e;
-    while ((e = hipEventQuery(h->ev[4 + rec.region])) == hipErrorNotReady) {
-    }
-    HIPCHK(h, e);
+    HIPCHK(h, event_wait(h->ev[4 + rec.region]));
     const unsigned long long* hr = pipe_hrows(h, rec.region);
     if (rec.guarded && pipe_spec(const_cast<unsigned long long*>(hr))[1] != 1u)
         return fail(h, PSIM_ESTATE, "pipelined heartbeat %u: the device abandoned an interval the host ran "
@@ -2283,8 +2299,15 @@ int run_n(psim_handle* h, uint32_t root, uint32_t count, bool reset, uint32_t ma
             h->mono_of[root] = snap.mono;
             h->par = snap.par;
             have_next = false;
-            // its read-back (copy stream) lands before anything later writes those host rows
-            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev[4 + next.region], 0));
+            // the device must have made the same decision (spec[1] = 2: abandoned); a device
+            // that ran the interval the host rolled back would leave the two states apart
+            // (ADVICE r5).  Waiting for its read-back also orders it before anything later
+            // writes those host rows.
+            HIPCHK(h, event_wait(h->ev[4 + next.region]));
+            const uint32_t dec = pipe_spec(pipe_hrows(h, next.region))[1];
+            if (dec != 2u)
+                return fail(h, PSIM_ESTATE, "pipelined heartbeat %u: the device ran an interval the host rolled back "
+                                            "(guard 0x%x)", next.mono, dec);
         }
         if (!quiet && ran < max_rounds) {   // more rounds than predicted: the plain driver, chunk by chunk
             uint32_t more = 0;

@@ -159,6 +159,36 @@ def test_join_seq_equals_join_and_step(rounds):
 
 
 @pytest.mark.gpu
+def test_join_seq_mixed_rounds_one_handle():
+    """join_seq calls with rounds 16, then 1, then 0, then 5 on the SAME handle
+    (the row buffers are sized once: rounds = 1 needs the most rows)
+    equal the plain join + step calls."""
+    import partisan_amd as pa
+    n = 400
+    c = contacts(n)
+    plan = [(1, 40, 16), (40, 140, 1), (140, 200, 0), (200, n, 5)]
+    out = []
+    for seq in (False, True):
+        sim = pa.Simulator(seed=SEED)
+        g = pa.hyparview.HyParViewCluster(sim, n, shuffle_rounds=4, promotion_rounds=3)
+        st = []
+        for lo, hi, rounds in plan:
+            if seq:
+                st += g.join_seq(np.arange(lo, hi, dtype=np.uint32), c[lo:hi], rounds=rounds)
+            else:
+                for i in range(lo, hi):
+                    g.join(i, int(c[i]))
+                    if rounds:
+                        st += g.step(rounds)
+        st += g.step(6)
+        act, na, pas, np_ = g.views()
+        out.append(([{k: x[k] for k in ("sent", "draws", "error", "processed", "active")} for x in st],
+                    act.tolist(), na.tolist(), pas.tolist(), np_.tolist(), g.draws().tolist(), g.inflight()))
+        sim.close()
+    assert out[0] == out[1]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,cfg", [(3000, {}), (2000, dict(active_max_size=5, passive_max_size=12,
                                                             shuffle_rounds=4, promotion_rounds=3))])
 def test_mass_join_then_shuffles(n, cfg):
