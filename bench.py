@@ -65,6 +65,26 @@ def touched_bytes(st):
     return 16 * int(st["active"]) + 8 * int(st["senders"]) + 4 * int(st["sender_degree_sum"]) + 32 * msgs
 
 
+def shard_touched_bytes(d, n_local):
+    """touched_bytes for one shard's round (a psim_shard_run row, a dict):
+    its algo_bytes are this shard's 16 n_local + 8 senders + 4 deg-sum + 32
+    messages (psim_host.hip shard rows), so replacing 16 n_local by 16 B per
+    vertex the shard touched gives the same model per GPU."""
+    return int(d["algo_bytes"]) - 16 * int(n_local) + 16 * int(d["active"])
+
+
+def gather_floats(pg, vals):
+    """[rank][i] = vals[i] of every rank (all-gather; one rank: [vals])."""
+    if pg is None:
+        return [list(vals)]
+    import torch
+    dev = "cuda" if pg.get_backend() == "nccl" else "cpu"
+    mine = torch.tensor(vals, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(mine) for _ in range(pg.get_world_size())]
+    pg.all_gather(out, mine)
+    return [t.cpu().tolist() for t in out]
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None,
@@ -81,6 +101,9 @@ def parse():
                    help="skip the single-thread C-oracle flood of the full --num-peers config (~25 s at 10M)")
     p.add_argument("--cpu-sample-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip parity_10m: the C oracle's flood of the same overlay against the last step's per-round "
+                        "counts and final state (gathered from every shard at N > 1; ~30 s of rank-0 CPU at 10M)")
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes for the all-core CPU baseline (the box's CPU share is 16 per GPU); 0 = skip")
     p.add_argument("--mode", choices=["sharded", "replicas"], default="sharded")
@@ -227,32 +250,87 @@ def verify(sim, pg, n, rounds_per_step):
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-def oracle_parity(sim, orc, root, gpu_stats, gpu_rounds, ost, orr, omono):
+def local_state(sim):
+    """This handle's final Plumtree state and slot layout (its own vertices)."""
+    import numpy as np
+    e, l, o, rr = sim.plumtree_state()
+    return {"delivered": sim.delivered(), "eager": e, "lazy": l, "outstanding": o, "Round": rr,
+            "slot_row_ptr": np.asarray(sim.slot_row_ptr, dtype=np.uint64), "slot_col": np.asarray(sim.slot_col)}
+
+
+def gather_state(pg, sim):
+    """Every shard's final state and slot rows (local_state) gathered in rank
+    order, i.e. global vertex order (shards own contiguous ranges): the whole
+    overlay's delivered set, eager / lazy / outstanding masks, accepted Round
+    and slot layout, as one GPU's handle reports them.  Collective (every
+    rank calls it); every rank gets the result, rank 0 uses it."""
+    import numpy as np
+    import torch
+    st = local_state(sim)
+    n_l, e_l = len(st["eager"]), len(st["slot_col"])
+    sizes = gather_floats(pg, [float(n_l), float(e_l)])
+    nmax, emax = int(max(x[0] for x in sizes)), int(max(x[1] for x in sizes))
+    dev = "cuda" if pg.get_backend() == "nccl" else "cpu"
+    per_v = np.zeros((6, nmax), np.int32)
+    per_v[0, :n_l] = st["eager"].view(np.int32)
+    per_v[1, :n_l] = st["lazy"].view(np.int32)
+    per_v[2, :n_l] = st["outstanding"].view(np.int32)
+    per_v[3, :n_l] = st["Round"]
+    per_v[4, :n_l] = st["delivered"]
+    per_v[5, :n_l] = np.diff(st["slot_row_ptr"].astype(np.int64))
+    cols = np.zeros(max(1, emax), np.int32)
+    cols[:e_l] = st["slot_col"].view(np.int32)
+    out = {}
+    for name, arr in (("v", per_v), ("c", cols)):
+        mine = torch.from_numpy(arr).to(dev)
+        got = [torch.zeros_like(mine) for _ in sizes]
+        pg.all_gather(got, mine)
+        out[name] = [g.cpu().numpy() for g in got]
+        del mine, got
+    v = np.concatenate([out["v"][r][:, :int(sizes[r][0])] for r in range(len(sizes))], axis=1)
+    c = np.concatenate([out["c"][r][:int(sizes[r][1])] for r in range(len(sizes))]).view(np.uint32)
+    return {"delivered": v[4].astype(np.uint8), "eager": v[0].view(np.uint32), "lazy": v[1].view(np.uint32),
+            "outstanding": v[2].view(np.uint32), "Round": v[3].astype(np.uint16),
+            "slot_row_ptr": np.concatenate([[0], np.cumsum(v[5].astype(np.int64))]).astype(np.uint64),
+            "slot_col": c}
+
+
+def _row_counts(g):
+    """(messages by kind, new deliveries) of one round: a psim_run record
+    (numpy) or a psim_shard_run row (dict; global counts)."""
+    if isinstance(g, dict):
+        return [int(g[k]) for k in KINDS], int(g["delivered_new"])
+    return [int(g["sent"][i + 1]) for i in range(len(KINDS))], int(g["delivered_new"])
+
+
+def oracle_parity(state, orc, root, gpu_stats, gpu_rounds, ost, orr, omono):
     """The GPU's last heartbeat against the C oracle's heartbeat of the same
     overlay (outside any timed region): round count, per-round message counts
     by kind and new deliveries, and at the end every vertex's delivered bit,
     eager / lazy / outstanding sets and accepted Round (orc_pt_dump_state over
-    the handle's slot layout).  gpu_stats: psim_run's rows (numpy records).
+    the handle's slot layout).  state: local_state / gather_state (the whole
+    overlay); gpu_stats: psim_run's rows or psim_shard_run's GLOBAL rows.
     Returns {"ok": bool, ...} with the first mismatch named."""
     import numpy as np
-    res = {"n_peers": int(sim.n), "rounds_gpu": int(gpu_rounds), "rounds_oracle": int(orr), "ok": False}
+    res = {"n_peers": int(len(state["eager"])), "rounds_gpu": int(gpu_rounds), "rounds_oracle": int(orr),
+           "ok": False}
     if gpu_rounds != orr:
         res["mismatch"] = "round count"
         return res
     for r in range(orr):
-        g, o = gpu_stats[r], ost[r]
+        (gk, gd), o = _row_counts(gpu_stats[r]), ost[r]
         for i, k in enumerate(KINDS):
-            if int(g["sent"][i + 1]) != o[k]:
-                res["mismatch"] = f"round {r + 1} {k}: gpu {int(g['sent'][i + 1])} oracle {o[k]}"
+            if gk[i] != o[k]:
+                res["mismatch"] = f"round {r + 1} {k}: gpu {gk[i]} oracle {o[k]}"
                 return res
-        if int(g["delivered_new"]) != o["delivered_new"]:
+        if gd != o["delivered_new"]:
             res["mismatch"] = f"round {r + 1} delivered_new"
             return res
-    if not np.array_equal(sim.delivered(), orc.delivered(root, omono)):
+    if not np.array_equal(state["delivered"], orc.delivered(root, omono)):
         res["mismatch"] = "delivered set"
         return res
-    ge, gl, go, grr = sim.plumtree_state()
-    oe, ol, oo, orrs = orc.dump_state(root, omono, sim.slot_row_ptr, sim.slot_col)
+    ge, gl, go, grr = state["eager"], state["lazy"], state["outstanding"], state["Round"]
+    oe, ol, oo, orrs = orc.dump_state(root, omono, state["slot_row_ptr"], state["slot_col"])
     for name, g, o in (("eager", ge, oe), ("lazy", gl, ol), ("outstanding", go, oo), ("Round", grr, orrs)):
         bad = np.flatnonzero(g != o)
         if len(bad):
@@ -265,7 +343,7 @@ def oracle_parity(sim, orc, root, gpu_stats, gpu_rounds, ost, orr, omono):
     return res
 
 
-def cpu_baseline_full(args, sim=None, gpu_stats=None, gpu_rounds=None):
+def cpu_baseline_full(args, state=None, gpu_stats=None, gpu_rounds=None):
     """One single-thread C-oracle flood of the benchmark's own configuration
     (the same --num-peers overlay, seed and root), timed from heartbeat to
     quiescence (the 10M config itself, beside the 1M sample).
@@ -283,9 +361,9 @@ def cpu_baseline_full(args, sim=None, gpu_stats=None, gpu_rounds=None):
     ost, rounds = orc.run()
     dt = time.perf_counter() - t0
     parity = None
-    if sim is not None:
+    if state is not None:
         t1 = time.perf_counter()
-        parity = oracle_parity(sim, orc, 0, gpu_stats, gpu_rounds, ost, rounds, omono)
+        parity = oracle_parity(state, orc, 0, gpu_stats, gpu_rounds, ost, rounds, omono)
         parity["check_s"] = round(time.perf_counter() - t1, 1)
     orc.close()
     return {
@@ -332,27 +410,40 @@ def cpu_baseline(args):
 
 
 def cpu_baseline_allcores(args):
-    """W single-thread oracle floods at once, one spawned process each (no
-    fork of this GPU-initialised process); value = the sum of the workers'
-    own rates (peer-rounds / time inside their floods, which overlap)."""
-    import multiprocessing as mp
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import cpu_flood
+    """W single-thread oracle floods at once, one child process each (a
+    fresh interpreter started by subprocess: no fork of this GPU-initialised
+    process, and no multiprocessing pool whose resource tracker outlives the
+    bench); value = the sum of the workers' own rates (peer-rounds / time
+    inside their floods, which overlap).  Every child is waited for before
+    this returns."""
+    import subprocess
     w = args.cpu_workers
-    jobs = [(args.cpu_sample_n, args.peers, args.seed + i, args.cpu_sample_reps, args.lazy_tick_rounds)
-            for i in range(w)]
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(w) as pool:
-        pool.map(cpu_flood.flood, [(1000, args.peers, 1, 1, 1)] * w)   # interpreters up, oracle loaded
-        t0 = time.perf_counter()
-        res = pool.map(cpu_flood.flood, jobs)
-        wall = time.perf_counter() - t0
+    worker = os.path.join(ROOT, "oracle", "cpu_flood.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([sys.executable, worker, str(args.cpu_sample_n), str(args.peers), str(args.seed + i),
+                               str(args.cpu_sample_reps), str(args.lazy_tick_rounds)],
+                              stdout=subprocess.PIPE, text=True, env=env) for i in range(w)]
+    res = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=600)
+            if p.returncode != 0:
+                raise RuntimeError(f"cpu_flood worker exited with {p.returncode}")
+            res.append(json.loads(out.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    wall = time.perf_counter() - t0
     rate = sum(r[0] / r[1] for r in res)
     return {
         "value": rate, "unit": "peer-rounds/s", "cores": w, "kind": "port",
         "sample": (f"{w} processes at once, each the single-thread C oracle running {args.cpu_sample_reps} "
                    f"floods of its own {args.cpu_sample_n}-peer random {args.peers}-peer overlay "
-                   f"({res[0][2]} rounds); sum of per-process rates, {wall:.1f} s wall incl. overlay builds"),
+                   f"({res[0][2]} rounds); sum of per-process rates, {wall:.1f} s wall incl. interpreter starts "
+                   f"and overlay builds"),
     }
 
 
@@ -439,6 +530,8 @@ def main():
             words += int(stats["words_stored"].sum())
     if sp is not None:   # this GPU's own bytes and launch times
         algo_bytes, round_ms = sp.local_algo_bytes, sp.local_kernel_ms
+        for stats in step_stats:
+            active_bytes += sum(shard_touched_bytes(x, sim.n) for x in stats)
 
     verified = verify(sim, pg, args.n, rounds_per_step)
     per_round_stats = None
@@ -462,8 +555,9 @@ def main():
             # own launch time for the roofline and the exchange time
             sp.sim.set_chunk_timing(False)
             sp.local_algo_bytes, sp.local_kernel_ms, sp.exchange_total = 0, 0.0, {}
-            _, r_inst = step()
+            inst_rows, r_inst = step()
             algo_bytes, round_ms, counted = sp.local_algo_bytes, sp.local_kernel_ms, r_inst
+            active_bytes = sum(shard_touched_bytes(x, sim.n) for x in inst_rows[:r_inst])
             xi = sp.exchange_total
             kernel_ms_step, exchange_ms_step = float(xi.get("kernel_ms", 0.0)), float(xi.get("exchange_ms", 0.0))
             sp.sim.set_chunk_timing(True)
@@ -513,11 +607,36 @@ def main():
     # step's last chunk is not counted): hipEvent durations of each launch
     avg_launch_ms = round_ms / max(1, counted)
     dense_gbs = (algo_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
-    touched_gbs = (active_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9 if sp is None else None
+    per_rank = None
+    rep_steps = 1 if (sp is not None and not args.round_events) else args.steps   # steps the bytes / ms cover
+    if sp is None:
+        touched_gbs = (active_bytes / max(1, counted)) / (avg_launch_ms * 1e-3) / 1e9
+    else:
+        # every shard's touched-state bytes over its own round-kernel time
+        # (hipEvents on its stream): the mean per-GPU rate = all shards' bytes
+        # over all shards' kernel time, each GPU against its own 8 TB/s
+        rk = gather_floats(pg, [float(active_bytes), float(round_ms), float(sim.n)])
+        per_rank = [{"rank": i, "n_local": int(x[2]), "touched_bytes_per_step": x[0] / rep_steps,
+                     "kernel_ms_per_step": x[1] / rep_steps,
+                     "frac": (x[0] / (x[1] * 1e-3) / 1e9 / HBM_PEAK_GBS) if x[1] > 0 else None}
+                    for i, x in enumerate(rk)]
+        tot_ms = sum(x[1] for x in rk)
+        touched_gbs = sum(x[0] for x in rk) / (tot_ms * 1e-3) / 1e9 if tot_ms > 0 else 0.0
 
     # ELL rows (every degree of the whole overlay <= 8) run the sweep kernel
     max_deg = int(max_over_ranks(pg, float(sim.max_degree())))
     kernel = "pt_round_kernel" if (args.csr or max_deg > 8) else "pt_round_ell_kernel"
+    # parity_10m: the final state of the last flood -- at N > 1
+    # every shard's, gathered to rank 0 in global vertex order -- for the C
+    # oracle's flood of the same overlay, after every timed figure
+    gstate = None
+    if not args.no_parity:
+        if sp is not None and world > 1:
+            gstate = gather_state(pg, sim)
+            if rank != 0:
+                gstate = None
+        elif rank == 0:
+            gstate = local_state(sim)
     if rank == 0:
         traffic = traffic_fetch = traffic_write = None
         tj = {}
@@ -552,7 +671,6 @@ def main():
                 row = {"round": i + 1, "us": round(ms * 1e3, 2), "messages": int(x["sent"][1:6].sum()),
                        "words": w, "active": int(x["active"]), "bytes_touched": tb, "bytes_dense_model": db,
                        "frac": tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None,
-                       "frac_dense_model": db / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None,
                        "frac_random_access": w / (ms * 1e-3) / SCATTER_PEAK_WPS if ms > 0 else None}
                 if pmc_rounds and i < len(pmc_rounds):
                     pb = pmc_rounds[i]["fetch"] + pmc_rounds[i]["write"]
@@ -596,9 +714,15 @@ def main():
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "model": ("bytes per launch = 16 B per vertex the round touched + (8 + 4 deg) per sender + "
                           "32 per message (SURVEY 8(d) with its 16 N term charged only for touched vertices)"
-                          if touched_gbs is not None else "SURVEY 8(d): 16 N + sum(8 + 4 deg) + 32 msgs"),
+                          + ("" if sp is None else
+                             "; per GPU: every shard's bytes over its own round-kernel time, summed over shards "
+                             "(per_rank)")),
+                "per_rank": per_rank,
+                # SURVEY 8(d)'s 16 N-per-round model credits state a sparse round never
+                # reads (above 1.0 of peak in rounds 2-5): a model, not evidence
                 "achieved_dense_model": dense_gbs,
                 "frac_dense_model": dense_gbs / HBM_PEAK_GBS,
+                "dense_model_note": "SURVEY 8(d) 16 N per round: model, not evidence (credits unread state)",
                 "random_access": ({"achieved": words_s, "peak": SCATTER_PEAK_WPS, "unit": "words/s",
                                    "frac": words_s / SCATTER_PEAK_WPS,
                                    "words_per_step": words / args.steps,
@@ -633,11 +757,18 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args)
             else:
                 out["cpu_baseline"], out["parity_10m"] = cpu_baseline_full(
-                    args, sim if sp is None else None, last_stats, rounds_per_step[-1])
+                    args, gstate, last_stats, rounds_per_step[-1])
                 out["cpu_baseline_sample_1m"] = cpu_baseline(args)
             if args.cpu_workers > 1:
                 out["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
+        if gstate is not None and "parity_10m" not in out:
+            # the oracle flood only as the checker here (cpu_baseline is rank 0 at N = 1)
+            _, out["parity_10m"] = cpu_baseline_full(args, gstate, last_stats, rounds_per_step[-1])
+        if gstate is not None and out.get("parity_10m"):
+            out["parity_10m"]["shards"] = world if sp is not None else 1
         print(json.dumps(out), flush=True)
+    del gstate
+    barrier(pg)          # the other ranks wait for rank 0's oracle check before tearing down
     sim.close()
     if pg is not None:
         pg.destroy_process_group()

@@ -163,7 +163,12 @@ int  psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out);
  * (max_roots > 16) one origin launch for all of them, all or nothing:
  * PSIM_ENOSPC when new roots exceed max_roots, PSIM_EBUSY when a root's last
  * heartbeat is still in flight or holds rows, PSIM_EINVAL on a root listed
- * twice; otherwise psim_plumtree_broadcast per root, in order. */
+ * twice; otherwise psim_plumtree_broadcast per root, in order.  A SHARDED
+ * forest (psim_shard_init, world > 1) takes it as a collective: every rank
+ * passes the same roots (global ids), the owners run the origins and every
+ * lane's cross-shard pushes move in one exchange before it returns; then
+ * psim_shard_run / psim_shard_step drive all lanes (one launch per round,
+ * every lane's words in one all-to-all-v, counters all-reduced per chunk). */
 int  psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos_out);
 /* One heartbeat interval of one root: psim_plumtree_broadcast(root) then
  * psim_run(max_rounds) -- the same state, ids, per-round stats and codes --

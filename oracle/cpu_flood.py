@@ -29,3 +29,11 @@ def flood(job):
         pr += n * rounds
         orc.close()
     return pr, secs, rounds
+
+
+if __name__ == "__main__":
+    # bench.py runs each worker as a plain child process (no multiprocessing
+    # pool: its resource tracker outlived the bench) and reads
+    # the one JSON line it prints
+    import json
+    print(json.dumps(flood(tuple(int(x) for x in sys.argv[1:6]))), flush=True)

@@ -836,8 +836,24 @@ __device__ __forceinline__ int* hold_delta(const PtArgs& a) {
 // after another had flushed used to pick the flags while the others read the
 // list -- a listed vertex that gained rows this round was then visited again
 // as "due" and sent a second i_have (the 1M world-2 mismatch of round 2).
+// The group-flag mode of round R's senders from the counts of rounds R-1
+// (prev) and R-2 (prev2) -- round_counts and the sharded ingest of R's remote
+// words take it from the same numbers.  PSIM_FF_GROWING 1 would keep a round
+// after the peak (prev < prev2: a 10M flood's round 14, 2.45M words after
+// 19.3M) flagging, so that the round after it reads the flagged groups
+// instead of sweeping the whole inbox (round 15: 613k receivers): measured a
+// loss (the flag stores cost round 14 more than round 15 saves).
+#ifndef PSIM_FF_GROWING
+#define PSIM_FF_GROWING 0      // A/B knob: 1 = flag-free only while the count grows (measured: round 14 +15-20 us
+                               // of flag stores, round 15 -3..-8 us; profiles/r06/experiments/ab_group_shift.txt)
+#endif
+__device__ __forceinline__ uint32_t round_mark(const PtArgs& a, uint32_t prev, uint32_t prev2) {
+    if (prev >= a.dense && (prev >= prev2 || !PSIM_FF_GROWING)) return a.force_flags ? 1u : 0u;
+    return (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
+}
+
 __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint32_t* wl_off = nullptr) {
-    __shared__ uint32_t cnt2[5];
+    __shared__ uint32_t cnt2[6];
     m.mark = 1;
     m.all_in = m.list_in = false;
     if (!a.mcnt) {
@@ -852,6 +868,7 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
         cnt2[3] = uint32_t(hold);
         // an abandoned pipelined interval (PtArgs::spec), loaded with the counts
         cnt2[4] = a.spec ? a.spec[0] : 0u;
+        cnt2[5] = a.mcnt[kMcntFF + a.m_s];               // the last round wrote no group flags
     }
     if (t < 64) {
         uint32_t c1 = a.mcnt[a.m_s * 64 + t], c2 = a.mcnt[a.m_r * 64 + t];
@@ -877,25 +894,27 @@ __device__ __forceinline__ bool round_counts(const PtArgs& a, RoundMode& m, uint
     __syncthreads();
     // nothing of an abandoned interval runs, not even the rings' upkeep below
     if (cnt2[4]) return false;
+    const uint32_t prev = cnt2[0], prev2 = cnt2[1];
+    const uint32_t mark = round_mark(a, prev, prev2);
     if (blockIdx.x == 0) {        // (no workgroup of this launch reads these slots)
         if (t == 0) {
             a.mcnt[kMcntHold + a.m_s] = cnt2[3];          // = holders at the end of round R-1
             a.mcnt[kMcntHoldD + a.m_z] = 0u;              // the round after next adds into it
+            a.mcnt[kMcntFF + a.m_w] = mark == 0u ? 1u : 0u;   // a no-op round sends nothing: 0
         }
         if (t < 64) {                                     // the round after next starts empty
             a.mcnt[a.m_z * 64 + t] = 0;
             if (a.wl_cur) a.wlcnt[a.m_z * 64 + t] = 0;
         }
     }
-    const uint32_t prev = cnt2[0], prev2 = cnt2[1];
     const bool rows_due = a.tick && int(cnt2[3]) > 0;
     m.rows_due = rows_due;
     // nothing was sent last round and no row is due: every vertex is idle
     // (no inbox flag can be set), so the whole round is a no-op
     if (prev == 0 && !rows_due) return false;
-    // many senders expected: no group flags this round; few: flags + worklist
-    m.mark = prev >= a.dense ? (a.force_flags ? 1u : 0u) : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
-    m.all_in = prev2 >= a.dense;                       // the last round wrote none: every group is read
+    // many senders expected (and the flood still growing): no group flags this round; few: flags + worklist
+    m.mark = mark;
+    m.all_in = cnt2[5] != 0u;                          // the last round wrote none: every group is read
     // the last round's senders listed every group they flagged (the same
     // test on the same count) and no row is due: only the listed groups
     m.list_in = wl_off && a.wl_cur && prev2 < a.dense && prev2 < a.wl_thr && !cnt2[2] && !rows_due;
@@ -984,6 +1003,16 @@ constexpr uint32_t kEllChunk = 1024;   // 512 / 256 / 2048 measured slower (DESI
 constexpr uint32_t kVpt = kEllChunk / kBlock;
 static_assert(kVpt >= 1 && kVpt <= 8 && kEllChunk % 32 == 0 && (kEllChunk << 2) <= 65536,
               "ELL chunk: 1-8 vertices per thread, candidates fit 16 bits");
+
+// A chunk whose flagged groups are at least kFullQuarters / 4 of its groups
+// is read whole (the contiguous sweep below): the unflagged groups' words are
+// stale (a live word always has its group flagged), so reading them is only
+// bandwidth.  A/B knob PSIM_FULL_QUARTERS (4 = only chunks with every group
+// flagged).
+#ifndef PSIM_FULL_QUARTERS
+#define PSIM_FULL_QUARTERS 4
+#endif
+constexpr uint32_t kFullQuarters = PSIM_FULL_QUARTERS;
 
 // x / W for x < 2^13 and 1 <= W <= 8: x * ceil(2^18 / W) >> 18 (the rounding
 // error stays below 2^13 / 2^18 of one, under the 1/8 a fraction of x/W
@@ -1097,7 +1126,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         // LDS quad k, and which vertices hold live words is read back from LDS
         // by the candidate pass -- no per-word group lookup, division or LDS
         // atomic (the general sweep below spends ~100 VALU per quad on those).
-        const bool full = !list && ng == kGroups && nv == kEllChunk &&
+        const bool full = !list && ng * 4u >= kGroups * kFullQuarters && nv == kEllChunk &&
                           (reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0;   // uniform
         if (full) {
             constexpr uint32_t kSweepF = (kEllChunk * kCap / 4 + kBlock - 1) / kBlock;   // W <= kCap
@@ -1120,8 +1149,8 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
                 x.w = live_word(x.w, a.ctag) ? x.w : 0u;
                 reinterpret_cast<u32x4_t*>(wbuf)[q] = x;
             }
-        } else if ((reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0) {   // group g's words start at 64 W g bytes
-            // A group's 16 W words start on a 16-byte boundary: read them as
+        } else if ((reinterpret_cast<uintptr_t>(a.in_cur) & 15u) == 0) {   // group g's words start at 4 kGV W g bytes
+            // A group's kGV W words (kGV >= 4) start on a 16-byte boundary: read them as
             // quads, kSweepU quads per thread in flight before any is used (the
             // word-at-a-time loop waited out one load latency per word).
             constexpr uint32_t kSweepU = 8;   // a dense round's 5 quads per thread all in flight at once
@@ -1132,7 +1161,8 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
 #pragma unroll
                 for (uint32_t k = 0; k < kSweepU; k++) {
                     const uint32_t q = q0 + k * kBlock + t;
-                    const uint32_t i = div_w(q >> 2, wmag), r = (q - i * gq) * 4u;   // gq = 4 W
+                    // group slot i = q / gq, gq = kGV W / 4 quads: (4 q / kGV) / W
+                    const uint32_t i = div_w((q << 2) >> kGroupShift, wmag), r = (q - i * gq) * 4u;
                     li[k] = q < nq ? pos(i) * gw + r : 0xFFFFFFFFu;
                     gi[k] = q < nq ? gv(i) * W + r : nW;
                     if (gi[k] + 4 <= nW) {
@@ -1250,6 +1280,11 @@ __device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
         a.mcnt += size_t(lane) * kMcntLane;
         if (a.wlcnt) a.wlcnt = a.mcnt + 256;
     }
+    if (a.stage) a.stage += lane * f.s_stage;           // sharded forest: the lane's staged remote words
+    if (a.dly) {                                         // delay faults: the lane's inbox ring (s_in / s_pend
+        a.ring += lane * f.s_in;                         // are the ring strides then, forest_args)
+        a.pring += lane * f.s_pend;
+    }
     if (a.wl_cur) a.wl_cur = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_cur) + lane * f.s_pend);
     if (a.wl_nxt) a.wl_nxt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_nxt) + lane * f.s_pend);
     const uint2 li = f.info[lane];
@@ -1258,9 +1293,9 @@ __device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
     return a;
 }
 
-template <bool kFault, uint32_t kCap>
+template <bool kFault, uint32_t kCap, bool kLocal>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void pt_forest_ell_kernel(FoArgs f) {
-    pt_round_ell_body<kFault, kCap, true>(fo_lane(f, f.lane0 + blockIdx.y));   // one GPU, never sharded
+    pt_round_ell_body<kFault, kCap, kLocal>(fo_lane(f, f.lane0 + blockIdx.y));   // kLocal: one GPU
 }
 
 template <bool kFault>
@@ -1910,16 +1945,18 @@ __device__ __forceinline__ void ingest_count(const PtArgs& a, uint32_t c) {
 // listed.  Without counts: flags.  Uniform call (barrier).
 __device__ __forceinline__ uint32_t ingest_mark(const PtArgs& a) {
     if (!a.mcnt) return 1u;
-    __shared__ uint32_t pm;
+    __shared__ uint32_t pm[2];
     if (threadIdx.x < 64) {
-        uint32_t c = a.mcnt[a.m_s * 64 + threadIdx.x];
+        uint32_t c = a.mcnt[a.m_s * 64 + threadIdx.x], c2 = a.mcnt[a.m_r * 64 + threadIdx.x];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-        if (threadIdx.x == 0) pm = c;
+        for (int off = 32; off > 0; off >>= 1) {
+            c += __shfl_xor(c, off, 64);
+            c2 += __shfl_xor(c2, off, 64);
+        }
+        if (threadIdx.x == 0) { pm[0] = c; pm[1] = c2; }
     }
     __syncthreads();
-    const uint32_t prev = pm;
-    return prev >= a.dense ? (a.force_flags ? 1u : 0u) : (a.wl_nxt && prev < a.wl_thr) ? 2u : 1u;
+    return round_mark(a, pm[0], pm[1]);
 }
 
 __global__ __launch_bounds__(kBlock) void pt_ingest_kernel(PtArgs a, const uint2* __restrict__ rec, uint32_t nrec,
@@ -1958,6 +1995,61 @@ __global__ __launch_bounds__(kBlock) void pt_ingest_dense_kernel(PtArgs a, const
     uint32_t c = 0;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrecv; i += stride) {
         const uint32_t w = recv[i];
+        if (!w) continue;
+        const uint32_t ls = recv_map[i];
+        a.in_nxt[ls] = w;
+        mark_group(a, slot2v[ls] >> kGroupShift, mark, nullptr);
+        c++;
+    }
+    ingest_count(a, c);
+}
+
+// Sharded forest: every lane's dense regions in one
+// all-to-all-v.  Region d of the send buffer holds, lane after lane, each
+// lane's words for shard d in psim_shard_layout order: word i (region d of
+// the single-lane layout, base sb[d]) of lane L sits at
+// sb[d] nl + L (sb[d+1] - sb[d]) + i - sb[d]; the receive side the same over
+// the recv layout.  blockIdx.y = lane - f.lane0.
+__device__ __forceinline__ uint64_t fo_region_pos(const uint64_t* b, uint32_t world, uint32_t i, uint32_t lane,
+                                                  uint32_t nl) {
+    uint32_t d = 0;
+    while (d + 1 < world && b[d + 1] <= i) d++;       // world <= 64; regions in rank order
+    return b[d] * nl + uint64_t(lane) * (b[d + 1] - b[d]) + (i - b[d]);
+}
+
+__global__ __launch_bounds__(kBlock) void fo_pack_dense_kernel(FoArgs f, const uint32_t* __restrict__ rem,
+                                                               uint32_t nrem, const uint64_t* __restrict__ sb,
+                                                               uint32_t world, uint32_t* __restrict__ send) {
+    __shared__ uint64_t b[65];
+    if (threadIdx.x <= world) b[threadIdx.x] = sb[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = f.lane0 + blockIdx.y;
+    const PtArgs a = fo_lane(f, lane);
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrem; i += stride) {
+        const uint32_t e = rem[i];
+        const uint32_t w = a.stage[e];
+        send[fo_region_pos(b, world, i, lane, f.nl)] = w;
+        if (w) a.stage[e] = 0;
+    }
+}
+
+// fixed_mark >= 0: the group-flag mode of the words' round is given (the
+// origins' pushes: flags + list), else the ingest's own decision (ingest_mark)
+__global__ __launch_bounds__(kBlock) void fo_ingest_dense_kernel(FoArgs f, const uint32_t* __restrict__ recv,
+                                                                 const uint32_t* __restrict__ recv_map, uint32_t nrecv,
+                                                                 const uint64_t* __restrict__ rb, uint32_t world,
+                                                                 const uint32_t* __restrict__ slot2v, int fixed_mark) {
+    __shared__ uint64_t b[65];
+    if (threadIdx.x <= world) b[threadIdx.x] = rb[threadIdx.x];
+    const uint32_t lane = f.lane0 + blockIdx.y;
+    const PtArgs a = fo_lane(f, lane);
+    const uint32_t mark = fixed_mark >= 0 ? uint32_t(fixed_mark) : ingest_mark(a);   // (barrier inside)
+    __syncthreads();
+    const uint32_t stride = gridDim.x * kBlock;
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nrecv; i += stride) {
+        const uint32_t w = recv[fo_region_pos(b, world, i, lane, f.nl)];
         if (!w) continue;
         const uint32_t ls = recv_map[i];
         a.in_nxt[ls] = w;
@@ -2067,9 +2159,13 @@ hipError_t launch_fo_round(FoArgs f, uint32_t gx, hipStream_t s) {
             const uint32_t g = gx ? gx : std::max<uint32_t>(1u, (a0.ell_grid ? a0.ell_grid : 1536u) / ny);
             const dim3 grid(std::min(g, grid_ell(a0.n)), ny);
             const size_t lds = size_t(kEllChunk) * a0.ell * 4;
-            const auto k = a0.ell <= 4 ? (flt ? pt_forest_ell_kernel<true, 4> : pt_forest_ell_kernel<false, 4>)
-                         : a0.ell <= 6 ? (flt ? pt_forest_ell_kernel<true, 6> : pt_forest_ell_kernel<false, 6>)
-                                       : (flt ? pt_forest_ell_kernel<true, 8> : pt_forest_ell_kernel<false, 8>);
+            const bool loc = a0.stage == nullptr;        // sharded forests stage remote words per lane
+            const auto k = a0.ell <= 4 ? (flt ? pt_forest_ell_kernel<true, 4, false>
+                                              : loc ? pt_forest_ell_kernel<false, 4, true> : pt_forest_ell_kernel<false, 4, false>)
+                         : a0.ell <= 6 ? (flt ? pt_forest_ell_kernel<true, 6, false>
+                                              : loc ? pt_forest_ell_kernel<false, 6, true> : pt_forest_ell_kernel<false, 6, false>)
+                                       : (flt ? pt_forest_ell_kernel<true, 8, false>
+                                              : loc ? pt_forest_ell_kernel<false, 8, true> : pt_forest_ell_kernel<false, 8, false>);
             hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, f);
         } else {
             const dim3 grid(grid_chunks(a0.n), ny);
@@ -2158,6 +2254,35 @@ hipError_t launch_pt_pack_dense(const PtArgs& a, const uint32_t* rem, uint32_t n
     if (nrem == 0) return hipSuccess;
     hipLaunchKernelGGL(pt_pack_dense_kernel, dim3(grid_for(nrem)), dim3(kBlock), 0, s, a, rem, nrem, send);
     return hipGetLastError();
+}
+
+hipError_t launch_fo_pack_dense(FoArgs f, const uint32_t* rem, uint32_t nrem, const uint64_t* sb, uint32_t world,
+                                uint32_t* send, hipStream_t s) {
+    if (nrem == 0 || f.nl == 0) return hipSuccess;
+    const uint32_t gx = std::max<uint32_t>(1u, std::min<uint32_t>(grid_for(nrem), 4096u / std::min(f.nl, 4096u)));
+    for (uint32_t l0 = 0; l0 < f.nl; l0 += 65535u) {
+        f.lane0 = l0;
+        hipLaunchKernelGGL(fo_pack_dense_kernel, dim3(gx, std::min<uint32_t>(65535u, f.nl - l0)), dim3(kBlock), 0, s, f,
+                           rem, nrem, sb, world, send);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_fo_ingest_dense(FoArgs f, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,
+                                  const uint64_t* rb, uint32_t world, const uint32_t* slot2v, int fixed_mark,
+                                  hipStream_t s) {
+    if (nrecv == 0 || f.nl == 0) return hipSuccess;
+    const uint32_t gx = std::max<uint32_t>(1u, std::min<uint32_t>(grid_for(nrecv), 4096u / std::min(f.nl, 4096u)));
+    for (uint32_t l0 = 0; l0 < f.nl; l0 += 65535u) {
+        f.lane0 = l0;
+        hipLaunchKernelGGL(fo_ingest_dense_kernel, dim3(gx, std::min<uint32_t>(65535u, f.nl - l0)), dim3(kBlock), 0, s,
+                           f, recv, recv_map, nrecv, rb, world, slot2v, fixed_mark);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_pt_ingest_dense(const PtArgs& a, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,

@@ -101,6 +101,7 @@ struct psim_handle {
     size_t pend_bytes = 0, wl_off = 0;
     uint32_t wl_cap = 0;
     uint32_t wl_thr = 0;                     // 0: ng / 8 (PSIM_WL_THR test knob: list mode up to that count)
+    uint32_t dense_div = 4;                  // a round after >= n / dense_div messages is flag-free (PSIM_DENSE_DIV)
     uint32_t wl_gpc = 0;                     // listed groups per ELL chunk, 0: spread (PSIM_WL_GPC A/B knob)
     // list mode: the listed groups spread over at most wl_wgs workgroups (0:
     // the whole resident grid; PSIM_WL_WGS A/B knob).  A flood's rounds 5-7
@@ -173,6 +174,21 @@ struct psim_handle {
         uint32_t* d_list = nullptr;              // [cap] lane lists for the origin / busy / renorm kernels
         uint32_t* d_busy = nullptr;              // [cap]
         uint64_t s_in = 0, s_pend = 0, s_ost = 0;
+        // sharded forest (psim_shard_init, world > 1): each lane's staged remote
+        // words, every lane's dense regions in one all-to-all-v per round
+        uint32_t* stage = nullptr;               // [cap][s_stage]
+        uint32_t* xsend = nullptr;               // [cap * send_base[W]] region d = lane after lane
+        uint32_t* xrecv = nullptr;               // [cap * recv_base[W]]
+        uint64_t* sb_d = nullptr;                // [W + 1] send / recv layout bases (device)
+        uint64_t* rb_d = nullptr;
+        uint64_t s_stage = 0;
+        int64_t g_inflight = 0, g_live = 0;      // global totals after the last collective
+        // delay faults (psim_set_delays, one GPU): each lane's inbox is a ring of
+        // kRing word buffers (slot stride Ed) and flag buffers (stride ng), the
+        // single-lane ring layout (set_round_ring) lane after lane
+        uint32_t* ring = nullptr;                // [cap][s_ring]
+        uint8_t* pring = nullptr;                // [cap][s_pring]
+        uint64_t s_ring = 0, s_pring = 0;
         std::vector<uint2> h_info;
         std::vector<uint32_t> serial;            // lane -> heartbeats so far (the lane's tag source)
         std::vector<uint32_t> root_of;           // lane -> root
@@ -276,9 +292,16 @@ void free_forest(psim_handle* h) {
     h->pend[0] = h->pend[1] = nullptr;
     h->ost = nullptr;
     h->ost_total = h->ost_total_base;
-    void* fp[] = {f.vs, f.in[0], f.in[1], f.pend[0], f.pend[1], f.ost, f.ost_total, f.mcnt, f.info, f.d_list, f.d_busy};
+    void* fp[] = {f.vs, f.in[0], f.in[1], f.pend[0], f.pend[1], f.ost, f.ost_total, f.mcnt, f.info, f.d_list, f.d_busy,
+                  f.stage, f.xsend, f.xrecv, f.sb_d, f.rb_d, f.ring, f.pring};
     for (void* x : fp)
         if (x) (void)hipFree(x);
+    f.stage = f.xsend = f.xrecv = nullptr;
+    f.sb_d = f.rb_d = nullptr;
+    f.ring = nullptr;
+    f.pring = nullptr;
+    h->ring = nullptr;                          // aliased the focused lane's ring
+    h->pring = nullptr;
     f.vs = nullptr;
     f.in[0] = f.in[1] = nullptr;
     f.pend[0] = f.pend[1] = nullptr;
@@ -539,8 +562,8 @@ int to_window(psim_handle* h) {
 // seeds its first round's predecessor-but-one with it (flag mode, no list).
 uint32_t list_threshold(const psim_handle* h) {
     if (!h->wl_cap) return 0;
-    const uint32_t ng = (h->n + (1u << kGroupShift) - 1) >> kGroupShift;
-    return h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, ng / 8);
+    // n / 128 messages (ng / 8 of 16-vertex groups), whatever the group size
+    return h->wl_thr ? h->wl_thr : std::max<uint32_t>(1u, h->n / 128);
 }
 
 void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
@@ -553,7 +576,7 @@ void set_round_slots(const psim_handle* h, PtArgs& a, uint64_t R) {
     a.m_s = uint32_t((R + 3) % 4);
     a.m_r = uint32_t((R + 2) % 4);
     a.m_z = uint32_t((R + 1) % 4);
-    a.dense = std::max<uint32_t>(1u, h->n / 4);
+    a.dense = std::max<uint32_t>(1u, h->n / h->dense_div);
     const uint32_t thr = list_threshold(h);
     if (thr) {                // sparse rounds: the groups written are listed
         a.wlcnt = a.mcnt + 256;
@@ -1085,7 +1108,10 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
 // bytes one lane takes in the slabs
 uint64_t fo_lane_bytes(const psim_handle* h, uint64_t s_in) {
     const auto& f = h->fo;
-    return uint64_t(h->n) * 16 + 2 * s_in * 4 + 2 * f.s_pend + f.s_ost + 4 * sizeof(int) + kMcntLane * 4 + 8 + 8;
+    uint64_t b = uint64_t(h->n) * 16 + 2 * s_in * 4 + 2 * f.s_pend + f.s_ost + 4 * sizeof(int) + kMcntLane * 4 + 8 + 8;
+    if (h->sh.world > 1)        // staged words + the lane's share of the exchange buffers
+        b += s_in * 4 + 4 * (h->sh.send_base[h->sh.world] + h->sh.recv_base[h->sh.world]);
+    return b;
 }
 
 int forest_alloc(psim_handle* h) {
@@ -1111,6 +1137,21 @@ int forest_alloc(psim_handle* h) {
         free_forest(h);
         return fail(h, PSIM_ENOMEM, "forest slabs for %u roots (%.2f GB)", f.cap, double(total) / 1e9);
     }
+    if (h->sh.world > 1) {
+        const auto& sh = h->sh;
+        const size_t W = size_t(sh.world);
+        if (!alloc_zero((void**)&f.stage, C * s_in * 4) ||
+            !alloc_zero((void**)&f.xsend, std::max<uint64_t>(1, C * sh.send_base[W]) * 4) ||
+            !alloc_zero((void**)&f.xrecv, std::max<uint64_t>(1, C * sh.recv_base[W]) * 4) ||
+            !alloc_zero((void**)&f.sb_d, (W + 1) * 8) || !alloc_zero((void**)&f.rb_d, (W + 1) * 8)) {
+            free_forest(h);
+            return fail(h, PSIM_ENOMEM, "sharded forest exchange buffers for %u roots", f.cap);
+        }
+        HIPCHK(h, hipMemcpy(f.sb_d, sh.send_base.data(), (W + 1) * 8, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(f.rb_d, sh.recv_base.data(), (W + 1) * 8, hipMemcpyHostToDevice));
+        f.s_stage = s_in;
+    }
+    f.g_inflight = f.g_live = 0;
     f.s_in = s_in;
     f.nl = 0;
     f.focus = -1;
@@ -1123,7 +1164,8 @@ int forest_alloc(psim_handle* h) {
 
 // The arguments of round R (tags R, counts ring R mod 4) for every lane: lane
 // 0's slices here, the kernels shift them by the lane (fo_lane in plumtree.hip).
-FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats, uint64_t R) {
+FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned long long* stats, uint64_t R,
+                   bool origin = false) {
     const auto& f = h->fo;
     PtArgs a = make_args(h, par, tick, stats);
     a.vs = f.vs;
@@ -1139,7 +1181,7 @@ FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned l
     a.m_s = uint32_t((R + 3) % 4);
     a.m_r = uint32_t((R + 2) % 4);
     a.m_z = uint32_t((R + 1) % 4);
-    a.dense = std::max<uint32_t>(1u, h->n / 4);
+    a.dense = std::max<uint32_t>(1u, h->n / h->dense_div);
     const uint32_t thr = list_threshold(h);
     if (thr) {
         a.wlcnt = a.mcnt + 256;
@@ -1158,7 +1200,73 @@ FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned l
     fa.s_ost = f.s_ost;
     fa.info = f.info;
     fa.nl = f.nl;
+    fa.a.stage = f.stage;                      // null on one GPU
+    fa.s_stage = f.s_stage;
+    if (h->dly) {
+        // delay faults: round R reads ring slot R and writes slot R + 1 + d
+        // (set_round_ring's layout in each lane's ring); the origins emit as
+        // round R - 1.  No per-round counts (a word may arrive rounds later):
+        // flags only, every round runs.
+        const uint64_t Rr = origin ? R - 1 : R;
+        const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+        PtArgs& b = fa.a;
+        b.ring = f.ring;
+        b.pring = f.pring;
+        b.ed = uint32_t(h->Ed);
+        b.ngrp = uint32_t(ng);
+        b.rpos = uint32_t(Rr + 1) & (kRing - 1);
+        b.in_cur = f.ring + size_t(Rr & (kRing - 1)) * h->Ed;
+        b.in_nxt = f.ring + size_t(b.rpos) * h->Ed;
+        b.pend_cur = f.pring + size_t(Rr & (kRing - 1)) * ng;
+        b.pend_nxt = f.pring + size_t(b.rpos) * ng;
+        b.ctag = uint32_t(Rr) & 0xFFu;
+        b.wtag = uint32_t(Rr + 1) & 0xFFu;
+        b.mcnt = nullptr;
+        b.wlcnt = nullptr;
+        b.wl_cur = b.wl_nxt = nullptr;
+        b.wl_cap = b.wl_thr = 0;
+        fa.s_in = f.s_ring;                    // fo_lane shifts the ring with the lane
+        fa.s_pend = f.s_pring;
+    }
     return fa;
+}
+
+// Sharded forest: the round just run (its arguments fa) left every lane's
+// remote words staged; they travel as every lane's dense regions in ONE
+// all-to-all-v and land in each lane's inbox for the next round.
+// fixed_mark >= 0: the words are origins' pushes (flags + list).
+int forest_exchange(psim_handle* h, const FoArgs& fa, int fixed_mark) {
+    auto& f = h->fo;
+    auto& sh = h->sh;
+    if (sh.world == 1 || f.nl == 0) return PSIM_OK;
+    const uint32_t W = uint32_t(sh.world), nl = f.nl;
+    HIPCHK(h, launch_fo_pack_dense(fa, sh.rem, uint32_t(sh.send_base[W]), f.sb_d, W, f.xsend, h->stream));
+    std::vector<uint64_t> so(W + 1), ro(W + 1);
+    for (uint32_t d = 0; d <= W; d++) {
+        so[d] = sh.send_base[d] * nl;
+        ro[d] = sh.recv_base[d] * nl;
+    }
+    std::string err;
+    const int rc = sh.xport->alltoallv(f.xsend, so.data(), f.xrecv, ro.data(), sh.rank, int(W), h->stream, &err);
+    if (rc) return fail(h, rc, "forest exchange: %s", err.c_str());
+    HIPCHK(h, launch_fo_ingest_dense(fa, f.xrecv, sh.recv_map, uint32_t(sh.recv_base[W]), f.rb_d, W, sh.slot2v,
+                                     fixed_mark, h->stream));
+    return PSIM_OK;
+}
+
+// Sharded forest: the global in-flight messages and live rows (one all-reduce
+// of this shard's totals; every rank then takes the same stop decision).
+int forest_globals(psim_handle* h) {
+    auto& f = h->fo;
+    int64_t v[2] = {(int64_t)h->inflight, h->live_rows};
+    if (h->sh.world > 1) {
+        std::string err;
+        const int rc = h->sh.xport->allreduce(v, 2, h->stream, &err);
+        if (rc) return fail(h, rc, "forest all-reduce: %s", err.c_str());
+    }
+    f.g_inflight = v[0];
+    f.g_live = v[1];
+    return PSIM_OK;
 }
 
 // The getters' view: the handle's single-lane fields alias lane `lane`.
@@ -1172,6 +1280,10 @@ void forest_focus(psim_handle* h, int lane) {
     }
     h->ost = f.ost + l * f.s_ost;
     h->ost_total = f.ost_total + 4 * l;
+    if (f.ring) {                               // delay faults: the getters read the lane's ring
+        h->ring = f.ring + l * f.s_ring;
+        h->pring = f.pring + l * f.s_pring;
+    }
     h->serial = f.serial[lane];
     h->root = f.root_of[lane];
     h->have_root = true;
@@ -1216,8 +1328,10 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
     std::vector<uint32_t> lanes(k), old;
     std::unordered_map<uint32_t, int> seen;
     uint32_t fresh = 0;
+    const bool sharded = h->sh.world > 1;       // collective: every rank passes the same roots
+    if (sharded && !h->sh.xport) return fail(h, PSIM_ESTATE, "sharded forest without a transport");
     for (size_t i = 0; i < k; i++) {
-        if (roots[i] >= h->n) return fail(h, PSIM_EINVAL, "root %u >= n", roots[i]);
+        if (roots[i] >= h->sh.n_global) return fail(h, PSIM_EINVAL, "root %u >= n", roots[i]);
         if (!seen.emplace(roots[i], 1).second)
             return fail(h, PSIM_EINVAL, "root %u heartbeats twice in one call", roots[i]);
         const auto it = f.lane_of.find(roots[i]);
@@ -1233,19 +1347,36 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
     }
     if (uint64_t(f.nl) + fresh > f.cap)
         return fail(h, PSIM_ENOSPC, "%u roots hold trees, %u new ones exceed max_roots=%u", f.nl, fresh, f.cap);
-    if (!old.empty()) {                          // every heartbeating root's last one is done
+    if (!old.empty() && h->dly) {
+        // delay faults: no per-lane counts; a root heartbeats again once no
+        // delayed message is pending anywhere and its lane holds no rows
+        std::vector<int> tot(size_t(f.cap) * 4);
+        HIPCHK(h, hipMemcpyAsync(tot.data(), f.ost_total, tot.size() * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (uint32_t l : old)
+            if (h->inflight != 0 || tot[4 * size_t(l)] != 0)
+                return fail(h, PSIM_EBUSY, "root %u: messages are in flight or its lane holds rows (delay faults: a "
+                                           "forest root heartbeats again once nothing is pending)", f.root_of[l]);
+    } else if (!old.empty()) {                   // every heartbeating root's last one is done
         FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
         HIPCHK(h, hipMemcpyAsync(f.d_list, old.data(), old.size() * 4, hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, launch_fo_busy(fa, f.d_list, uint32_t(old.size()), uint32_t(h->round % 4), f.d_busy, h->stream));
         std::vector<uint32_t> busy(old.size());
         HIPCHK(h, hipMemcpyAsync(busy.data(), f.d_busy, old.size() * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (sharded) {                            // busy on any shard
+            std::vector<int64_t> b(busy.begin(), busy.end());
+            std::string err;
+            const int rc = h->sh.xport->allreduce(b.data(), b.size(), h->stream, &err);
+            if (rc) return fail(h, rc, "forest busy all-reduce: %s", err.c_str());
+            for (size_t i = 0; i < b.size(); i++) busy[i] = b[i] != 0;
+        }
         for (size_t i = 0; i < old.size(); i++)
             if (busy[i])
                 return fail(h, PSIM_EBUSY, "root %u: its last heartbeat is in flight or holds rows (a forest keeps one "
                                            "heartbeat per root)", f.root_of[old[i]]);
     }
-    std::vector<uint32_t> wrap;
+    std::vector<uint32_t> wrap, own;            // own: lanes whose root this shard holds (all on one GPU)
     for (size_t i = 0; i < k; i++) {
         if (lanes[i] == kNoPeer) {
             lanes[i] = f.nl++;
@@ -1255,7 +1386,9 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
         const uint32_t l = lanes[i];
         f.serial[l]++;
         if ((f.serial[l] & 0x7Fu) == 0) wrap.push_back(l);
-        f.h_info[l] = make_uint2(f.serial[l] & 0xFFu, roots[i]);
+        const uint32_t lr = roots[i] - h->sh.v_lo;  // the origin's local index on its owner
+        f.h_info[l] = make_uint2(f.serial[l] & 0xFFu, lr < h->n ? lr : kNoPeer);
+        if (lr < h->n) own.push_back(l);
         uint32_t mono = 0;
         (void)next_mono(h, roots[i], &mono, true);
         if (monos) monos[i] = mono;
@@ -1269,10 +1402,20 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
     }
     // the origins emit into the buffers the next round reads (broadcast_common)
     HIPCHK(h, hipMemsetAsync(h->stats, 0, kStatsRow * sizeof(unsigned long long), h->stream));
-    FoArgs fa = forest_args(h, h->par ^ 1u, 0, h->stats, h->round + 1);
+    FoArgs fa = forest_args(h, h->par ^ 1u, 0, h->stats, h->round + 1, true);
     fa.a.wtag = uint32_t(h->round + 1) & 0xFFu;
-    HIPCHK(h, hipMemcpyAsync(f.d_list, lanes.data(), k * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, launch_fo_origin(fa, f.d_list, uint32_t(k), h->stream));
+    if (!own.empty()) {
+        HIPCHK(h, hipMemcpyAsync(f.d_list, own.data(), own.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, launch_fo_origin(fa, f.d_list, uint32_t(own.size()), h->stream));
+    }
+    if (sharded) {
+        // the origins' remote pushes: counted as the round before the next
+        // one (the origin's count slot) and flagged + listed like its own
+        FoArgs fx = fa;
+        fx.a.m_w = fa.a.m_s;
+        const int rc2 = forest_exchange(h, fx, fa.a.wl_nxt ? 2 : 1);
+        if (rc2) return rc2;
+    }
     HIPCHK(h, hipMemcpyAsync(h->h_stats, h->stats, kStatsRow * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                              h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1284,12 +1427,16 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
     h->ost_cnt += (int64_t)r[S_OST_DELTA];
     h->live_rows += (int64_t)r[S_LIVE_DELTA];
     h->inflight += r[PSIM_MSG_BROADCAST];
-    return PSIM_OK;
+    // delay faults: the origins' pushes are pending until 1 + d rounds on
+    if (h->dly) h->inflight = add_due(h->due, h->round, h->h_stats + size_t(kStatShards) * kNStat);
+    return forest_globals(h);
 }
 
 int forest_scrub_if_needed(psim_handle* h, uint64_t last) {
     if (last + 1 < h->scrub + kTagSpan) return PSIM_OK;
     const uint32_t keep = uint32_t(h->round + 1) & 0xFFu;
+    if (h->fo.ring && h->fo.nl)                 // delay rings: keep the next kRing - 1 rounds' words
+        HIPCHK(h, launch_pt_scrub(h->fo.ring, uint64_t(h->fo.nl) * h->fo.s_ring, keep, kRing - 1, h->stream));
     for (int b = 0; b < 2 && h->fo.nl; b++)
         HIPCHK(h, launch_pt_scrub(h->fo.in[b], uint64_t(h->fo.nl) * h->fo.s_in, keep, 1, h->stream));
     h->scrub = h->round;
@@ -1311,10 +1458,18 @@ int forest_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, siz
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
     const uint32_t L = h->cfg.lazy_tick_rounds ? h->cfg.lazy_tick_rounds : 1;
     const bool per_round = !(h->cfg.flags & PSIM_CFG_CHUNK_TIMING);
-    auto quiet = [&]() { return h->inflight == 0 && h->live_rows == 0; };
-    {   // every lane's row-holder ring from its exact count (seed_hold_ring)
+    const bool sharded = h->sh.world > 1;       // collective: every rank drives the same rounds
+    // sharded: the stop rule reads the global totals (every rank decides alike)
+    auto quiet = [&]() {
+        return sharded ? (f.g_inflight == 0 && f.g_live == 0) : (h->inflight == 0 && h->live_rows == 0);
+    };
+    if (!h->dly) {   // every lane's row-holder ring from its exact count (seed_hold_ring; delays: no counts)
         FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
         HIPCHK(h, launch_fo_seed(fa, h->stream));
+    }
+    if (sharded) {
+        const int rc = forest_globals(h);
+        if (rc) return rc;
     }
     bool done = stop_q && quiet();
     while (!done && ran < max_rounds) {
@@ -1329,6 +1484,10 @@ int forest_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, siz
             if (per_round || i == 0) HIPCHK(h, hipEventRecord(h->ev[2 * i], h->stream));
             if (f.nl) HIPCHK(h, launch_fo_round(fa, f.gx, h->stream));
             if (per_round || i + 1 == k) HIPCHK(h, hipEventRecord(h->ev[per_round ? 2 * i + 1 : 1], h->stream));
+            if (sharded) {                            // every lane's remote words, one all-to-all-v
+                const int rc2 = forest_exchange(h, fa, -1);
+                if (rc2) return rc2;
+            }
             par ^= 1u;
         }
         h->par = par;
@@ -1337,32 +1496,78 @@ int forest_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, siz
         HIPCHK(h, chunk_wait(h));
         float chunk_ms = 0.f;
         if (!per_round) HIPCHK(h, hipEventElapsedTime(&chunk_ms, h->ev[0], h->ev[1]));
+        // sharded: the chunk's per-round counters summed over ranks in one
+        // all-reduce -- kinds, new deliveries, senders, degree sum, and this
+        // shard's live rows / row holders after each round (global stop rule)
+        constexpr int NK = 10;
+        std::vector<int64_t> glob(size_t(k) * NK, 0);
+        int overflow_rc = 0;
+        {
+            int64_t live = h->live_rows, ost = h->ost_cnt;
+            for (uint32_t i = 0; i < k; i++) {
+                unsigned long long r[kNStat];
+                reduce_row(h->h_stats + i * kStatsRow, r);
+                if (r[S_OVERFLOW] && !overflow_rc)
+                    overflow_rc = fail(h, PSIM_EOVERFLOW, "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: "
+                                       "Round > 4095, 4: outstanding rows of an older heartbeat)",
+                                       (unsigned long long)(h->round + 1 + i), r[S_OVERFLOW]);
+                live += (int64_t)r[S_LIVE_DELTA];
+                ost += (int64_t)r[S_OST_DELTA];
+                int64_t* g = glob.data() + size_t(i) * NK;
+                for (int t = 1; t <= 5; t++) g[t - 1] = (int64_t)r[t];
+                g[5] = (int64_t)r[S_DELIV];
+                g[6] = (int64_t)r[S_SENDERS];
+                g[7] = (int64_t)r[S_DEGSUM];
+                g[8] = live;
+                g[9] = ost;
+            }
+        }
+        if (sharded) {
+            // an overflow on one shard still joins the collective; every rank returns the common code
+            std::vector<int64_t> v(glob.size() + kNCodes);
+            std::copy(glob.begin(), glob.end(), v.begin());
+            put_code(v.data() + glob.size(), overflow_rc);
+            std::string err;
+            const int rc = h->sh.xport->allreduce(v.data(), v.size(), h->stream, &err);
+            if (rc) return fail(h, rc, "forest counter all-reduce: %s", err.c_str());
+            std::copy(v.begin(), v.begin() + glob.size(), glob.begin());
+            const int frc = finish_code(h, v.data() + glob.size(), overflow_rc, "forest round");
+            if (frc) return frc;
+        } else if (overflow_rc) {
+            return overflow_rc;
+        }
         for (uint32_t i = 0; i < k; i++) {
             float ms = chunk_ms / float(k);
             if (per_round) HIPCHK(h, hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
             unsigned long long r[kNStat];
             reduce_row(h->h_stats + i * kStatsRow, r);
-            if (r[S_OVERFLOW])
-                return fail(h, PSIM_EOVERFLOW, "round %llu: overflow flags 0x%llx (1: >4 msgs on one edge, 2: Round > "
-                            "4095, 4: outstanding rows of an older heartbeat)", (unsigned long long)(h->round + 1),
-                            r[S_OVERFLOW]);
+            const int64_t* g = glob.data() + size_t(i) * NK;
             uint64_t msgs = 0;
             for (int t = 1; t <= 5; t++) msgs += r[t];
             h->ost_cnt += (int64_t)r[S_OST_DELTA];
             h->live_rows += (int64_t)r[S_LIVE_DELTA];
             h->inflight = msgs;
+            if (h->dly) {   // round R consumed its arrivals; its sends are pending until R + 1 + d
+                const uint64_t R = h->round + 1;
+                h->due[R & (kRing - 1)] = 0;
+                h->inflight = add_due(h->due, R, h->h_stats + i * kStatsRow + size_t(kStatShards) * kNStat);
+            }
+            if (sharded) {
+                f.g_inflight = g[0] + g[1] + g[2] + g[3] + g[4];
+                f.g_live = g[8];
+            }
             h->round++;
             h->kernel_ms_total += ms;
             h->rounds_total++;
             if (out && ran < cap) {
                 psim_round_stats& o = out[ran];
                 memset(&o, 0, sizeof o);
-                for (int t = 1; t <= 5; t++) o.sent[t] = r[t];
-                o.delivered_new = r[S_DELIV];
-                o.active = r[S_ACTIVE];
-                o.senders = r[S_SENDERS];
-                o.sender_degree_sum = r[S_DEGSUM];
-                o.outstanding_vertices = (uint64_t)h->ost_cnt;
+                for (int t = 1; t <= 5; t++) o.sent[t] = (uint64_t)g[t - 1];   // global when sharded
+                o.delivered_new = (uint64_t)g[5];
+                o.active = r[S_ACTIVE];                                     // this shard's
+                o.senders = (uint64_t)g[6];
+                o.sender_degree_sum = (uint64_t)g[7];
+                o.outstanding_vertices = (uint64_t)g[9];
                 o.algo_bytes = 16ull * h->n * f.nl + 8ull * r[S_SENDERS] + 4ull * r[S_DEGSUM] + 32ull * msgs;
                 o.words_stored = r[S_WORDS];
                 o.kernel_ms = ms;
@@ -1736,7 +1941,6 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
         for (uint32_t f = 0; f <= bn.nf; f++) bn.h_fslot[f] = rpl[std::min<uint64_t>(nl, uint64_t(f) << bn.fv_shift)];
     }
     const bool forest = h->fo.on;       // the per-lane arrays live in the forest's slabs
-    if (forest && W > 1) return fail(h, PSIM_ESTATE, "max_roots > 16 (the forest) runs on one GPU");
     if (alloc((void**)&h->rowp, (size_t(nl) + 1) * 4) != hipSuccess || alloc((void**)&h->col, Ed * 4) != hipSuccess ||
         alloc((void**)&h->rev, Ed * 4) != hipSuccess || alloc((void**)&h->memb, size_t(nl + 1) * 4) != hipSuccess ||
         (!ep.empty() && alloc((void**)&h->ecol, Ed * 4) != hipSuccess) ||
@@ -1777,6 +1981,8 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     }
     h->pend_bytes = pend_bytes;
     h->wl_thr = getenv("PSIM_WL_THR") ? uint32_t(strtoul(getenv("PSIM_WL_THR"), nullptr, 10)) : 0u;
+    h->dense_div = std::max<uint32_t>(1u, getenv("PSIM_DENSE_DIV") ? uint32_t(strtoul(getenv("PSIM_DENSE_DIV"), nullptr, 10))
+                                                                   : 4u);
     h->wl_gpc = getenv("PSIM_WL_GPC") ? uint32_t(strtoul(getenv("PSIM_WL_GPC"), nullptr, 10)) : 0u;
     h->wl_wgs = getenv("PSIM_WL_WGS") ? uint32_t(strtoul(getenv("PSIM_WL_WGS"), nullptr, 10)) : 256u;
     h->wl_off = wl_off;
@@ -2338,9 +2544,9 @@ int psim_plumtree_broadcast(psim_handle* h, uint32_t root, uint32_t* mono_out) {
 
 int psim_plumtree_broadcast_many(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* monos_out) {
     if (!h) return PSIM_EINVAL;
-    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast_x per root");
     if (k && !roots) return PSIM_EINVAL;
-    if (h->fo.on) return forest_broadcast(h, roots, k, monos_out);
+    if (h->fo.on) return forest_broadcast(h, roots, k, monos_out);   // sharded: collective
+    if (h->sh.world > 1) return fail(h, PSIM_ESTATE, "sharded handle: use psim_shard_broadcast_x per root");
     for (size_t i = 0; i < k; i++) {
         unsigned long long r[kNStat];
         const int rc = broadcast_common(h, roots[i], monos_out ? monos_out + i : nullptr, r);
@@ -2377,7 +2583,6 @@ int psim_plumtree_broadcast_run_n(psim_handle* h, uint32_t root, uint32_t count,
 int psim_shard_init(psim_handle* h, int rank, int world) {
     if (!h || world < 1 || rank < 0 || rank >= world) return PSIM_EINVAL;
     if (h->n) return fail(h, PSIM_ESTATE, "psim_shard_init must precede psim_load_csr");
-    if (h->fo.on && world > 1) return fail(h, PSIM_ENOTSUP, "max_roots > 16 (the forest) runs on one GPU");
     h->sh.rank = rank;
     h->sh.world = world;
     return PSIM_OK;
@@ -2926,9 +3131,22 @@ int shard_drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size
     if (!h) return PSIM_EINVAL;
     if (!h->n) return fail(h, PSIM_ESTATE, "no overlay loaded");
     HIPCHK(h, hipSetDevice(h->device));
+    if (xs) memset(xs, 0, sizeof *xs);
+    if (h->fo.on) {             // every root's lane in one launch, every lane's words in one exchange
+        if (h->sh.world > 1 && !h->sh.xport) return fail(h, PSIM_ESTATE, "sharded forest without a transport");
+        const double k0 = h->kernel_ms_total;
+        const uint64_t r0 = h->rounds_total;
+        uint32_t ran = 0;
+        const int rc = forest_drive(h, max_rounds, out, cap, stop_q, &ran);
+        if (rounds_run) *rounds_run = ran;
+        if (xs) {
+            xs->rounds = h->rounds_total - r0;
+            xs->kernel_ms = h->kernel_ms_total - k0;
+        }
+        return rc;
+    }
     int rc = x_buffers(h);
     if (rc) return rc;
-    if (xs) memset(xs, 0, sizeof *xs);
     if (h->lanes.size() > 1 || h->win) {
         if (!h->sh.pending) HIPCHK(h, seed_hold_rings(h, h->round + 1));
         return shard_drive_lanes(h, max_rounds, out, cap, stop_q, rounds_run, xs);
@@ -3091,6 +3309,7 @@ extern "C" {
 
 int psim_shard_broadcast_x(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     if (!h) return PSIM_EINVAL;
+    if (h->fo.on) return forest_broadcast(h, &root, 1, mono_out);   // the forest's own exchange (collective)
     int rc = x_buffers(h);
     if (rc) return rc;
     if (h->sh.pending) return fail(h, PSIM_ESTATE, "collect the async rounds first");
@@ -3491,7 +3710,8 @@ int psim_set_omissions(psim_handle* h, const uint32_t* src, const uint32_t* dst,
 }
 
 int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, const uint8_t* rounds, size_t k) {
-    if (h && h->fo.on) return fail(h, PSIM_ENOTSUP, "delay faults are not supported on a forest (max_roots > 16)");
+    if (h && h->fo.on && h->sh.world > 1)
+        return fail(h, PSIM_ENOTSUP, "delay faults on a sharded forest (max_roots > 16 over several GPUs)");
     if (!h || !h->n || (k && (!src || !dst || !rounds))) return PSIM_EINVAL;
     if (h->bin.rec_c) return fail(h, PSIM_ENOTSUP, "delay faults need the slot-scatter engine (not the binned one)");
     if (h->sh.world > 1 && h->win)      // lane layouts are decided alike on every rank (global counts)
@@ -3509,6 +3729,7 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
         if (l.win && !lrc) lrc = fail(h, PSIM_ENOTSUP, "delay faults on a window lane (overlapping heartbeats)");
         busy += (int64_t)l.inflight;
     }
+    if (h->fo.on) busy = (int64_t)h->inflight;   // the forest: every lane's messages (delays: still pending)
     if (h->sh.world > 1) {
         // collective: every rank must return the same code, and a shard's own
         // in-flight count says nothing about the others' (ADVICE r3), so the
@@ -3555,8 +3776,30 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
             }
             for (auto& x : l.due) x = 0;
         }
-        if (h->lanes.empty() && h->sh.world > 1 && !alloc_zero((void**)&h->sh.srg, size_t(kRing) * h->Ed * 4))
+        if (h->lanes.empty() && h->sh.world > 1 && !h->fo.on &&
+            !alloc_zero((void**)&h->sh.srg, size_t(kRing) * h->Ed * 4))
             return fail(h, PSIM_ENOMEM, "staging ring of the delay faults");
+        if (h->fo.on) {
+            // every lane's inbox becomes a ring (nothing is in flight: no word moves)
+            auto& f = h->fo;
+            const size_t ng = (size_t(h->n) + (1u << kGroupShift) - 1) >> kGroupShift;
+            f.s_ring = (uint64_t(kRing) * h->Ed + 63) & ~uint64_t(63);
+            f.s_pring = (uint64_t(kRing) * ng + 255) & ~uint64_t(255);
+            size_t fr = 0, tot = 0;
+            HIPCHK(h, hipMemGetInfo(&fr, &tot));
+            const uint64_t need = uint64_t(f.cap) * (f.s_ring * 4 + f.s_pring);
+            if (need + (uint64_t(1) << 30) > fr ||
+                !alloc_zero((void**)&f.ring, uint64_t(f.cap) * f.s_ring * 4) ||
+                !alloc_zero((void**)&f.pring, uint64_t(f.cap) * f.s_pring)) {
+                if (f.ring) (void)hipFree(f.ring);
+                f.ring = nullptr;
+                (void)hipFree(h->dly);
+                h->dly = nullptr;
+                return fail(h, PSIM_ENOMEM, "forest delay rings: %.2f GB for %u roots", double(need) / 1e9, f.cap);
+            }
+            for (auto& x : h->due) x = 0;
+            if (f.focus >= 0) forest_focus(h, f.focus);
+        }
         if (!h->lanes.empty()) load_lane(h, focus);
     }
     HIPCHK(h, hipMemcpy(h->dly, dl.data(), h->Ed, hipMemcpyHostToDevice));

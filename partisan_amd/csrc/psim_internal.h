@@ -122,16 +122,23 @@ __device__ __forceinline__ void wq_flush(WaveQ<Rec> q, uint32_t* counter, Rec* _
 //   [512, 516)  row holders at the END of round k (k mod 4): round R writes
 //               slot R-1 once (block 0) -- a value no workgroup of R reads
 //   [516, 520)  change in row holders during round k (two's complement)
+//   [520, 524)  1 = round k (k mod 4) wrote no group flags (its senders were
+//               flag-free: the next round reads every group); written by block
+//               0 of round k, read by round k + 1 (0, the zeroed state, = flags)
 // Round R's "any row due" test reads holders(R-2) + delta(R-1): both written
 // by earlier launches, so every workgroup of a launch takes the same decision
 // (the running count PtArgs::ost_total moves while the launch runs).
 constexpr size_t kMcntHold = 512;
 constexpr size_t kMcntHoldD = 516;
-constexpr size_t kMcntLane = 520;
+constexpr size_t kMcntFF = 520;
+constexpr size_t kMcntLane = 524;
 constexpr int kMaxDeg = 32;          // peer slots per vertex (u32 masks)
 constexpr int kStatShards = 64;      // counter shards (blockIdx & 63) to spread atomics
 constexpr int kNStat = 16;           // counters per shard
-constexpr int kGroupShift = 4;       // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
+#ifndef PSIM_GROUP_SHIFT
+#define PSIM_GROUP_SHIFT 4               // A/B knob (-DPSIM_GROUP_SHIFT=2 / 3 builds, profiles/r06/experiments)
+#endif
+constexpr int kGroupShift = PSIM_GROUP_SHIFT;   // inbox flags cover 16-vertex groups (625 KB at 10M: L2-resident)
 static_assert(kGroupShift >= 2 && kGroupShift <= 8, "a group spans whole 4-vertex thread quads");
 constexpr uint32_t kChunkV = 1024;   // vertices owned by one round-kernel workgroup
 // binned engine (single GPU): messages travel as {receiver
@@ -279,6 +286,7 @@ struct PtArgs {
 struct FoArgs {
     PtArgs a;                              // this round's arguments at lane 0's slices
     uint64_t s_vs, s_in, s_pend, s_ost;    // per-lane strides: uint4 records, u32 words, bytes, bytes
+    uint64_t s_stage;                      // sharded forest: u32 staged words per lane (a.stage = lane 0's)
     const uint2* __restrict__ info;        // [lanes] {Monotonic tag (low 8 bits), local root}
     uint32_t lane0, nl;                    // this launch: lanes [lane0, lane0 + gridDim.y) of [0, nl)
 };
@@ -295,6 +303,15 @@ hipError_t launch_fo_seed(const FoArgs& f, hipStream_t s);
 hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s);
 // outstanding rows to live peers over every lane -> *out (added)
 hipError_t launch_fo_count_live(const FoArgs& f, unsigned long long* out, hipStream_t s);
+// sharded forest: every lane's staged remote words -> the dense send regions
+// (region d = lane after lane, psim_shard_layout order; sb = the layout's
+// [world + 1] bases on the device), and the received regions -> each lane's
+// inbox (rb = the recv layout's bases; fixed_mark >= 0 overrides ingest_mark)
+hipError_t launch_fo_pack_dense(FoArgs f, const uint32_t* rem, uint32_t nrem, const uint64_t* sb, uint32_t world,
+                                uint32_t* send, hipStream_t s);
+hipError_t launch_fo_ingest_dense(FoArgs f, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,
+                                  const uint64_t* rb, uint32_t world, const uint32_t* slot2v, int fixed_mark,
+                                  hipStream_t s);
 // a backend restart at local vertex v: v forgets every origin (each lane's delivered tag)
 hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s);
 

@@ -62,12 +62,14 @@ def gloo_transport():
 
 class ShardedPlumtree:
     def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None,
-                 csr=False, chunk_timing=False):
+                 csr=False, chunk_timing=False, max_roots=0):
         """csr: keep CSR slot rows (PSIM_CFG_CSR) instead of the ELL rows every
         shard uses when the overlay's widest row has <= 8 slots.  chunk_timing:
         psim_shard_run times each 4-round chunk with one event pair and puts no
         marker between its kernels (PSIM_CFG_CHUNK_TIMING; kernel_ms then
-        includes the exchange)."""
+        includes the exchange).  max_roots > 16: a sharded forest (every
+        root's trees kept; broadcast_many heartbeats many roots at once,
+        DESIGN.md 5.10)."""
         self.rank, self.world, self.backend = rank, world, backend
         self.transport = transport or ("rccl" if backend == "nccl" else "callback")
         self.dev = torch.device("cuda", device)
@@ -75,7 +77,7 @@ class ShardedPlumtree:
         # it finds no device (torch ships its own libamdhip64)
         torch.cuda.set_device(self.dev)
         self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world, csr=csr,
-                             chunk_timing=chunk_timing)
+                             chunk_timing=chunk_timing, max_roots=max_roots)
         self._h = self.sim._h
         self.last_exchange = {}
         self.exchange_total = {}      # psim_exchange_stats summed over runs (this rank)
@@ -207,6 +209,15 @@ class ShardedPlumtree:
               self._h)
         self._exchange_dense()
         return mono.value
+
+    def broadcast_many(self, roots):
+        """Heartbeats from many roots at once on a sharded forest (collective:
+        every rank passes the same global roots); returns their ids."""
+        return self.sim.broadcast_many(roots)
+
+    def focus(self, root):
+        """Point the getters at root's lane (this rank's vertex range)."""
+        self.sim.focus(root)
 
     KEYS = ["broadcast", "prune", "i_have", "ignored_i_have", "graft", "delivered_new", "senders",
             "sender_degree_sum", "algo_bytes"]

@@ -127,7 +127,7 @@ def test_bench_config_10m_oracle_parity():
         gst, gr = sim.run(as_dicts=False)
         omono = orc.heartbeat(0)
         ost, orr = orc.run()
-        res = bench.oracle_parity(sim, orc, 0, gst, gr, ost, orr, omono)
+        res = bench.oracle_parity(bench.local_state(sim), orc, 0, gst, gr, ost, orr, omono)
         print(hb, res, flush=True)
         assert res["ok"], (hb, res)
     orc.close()

@@ -239,3 +239,77 @@ def test_forest_config_field_in_abi():
     assert [f for f, _ in _lib.Config._fields_][5] == "max_roots"
     assert _lib.ERRORS[-9] == "PSIM_ENOSPC"
     assert _lib.PSIM_ABI_VERSION == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,dmax", [(1, 5), (2, 14)])
+def test_forest_delay_faults_lockstep(L, dmax):
+    """Delay faults on a forest (partisan_peer_service_client
+    egress / ingress delay, :148-176): 25 % of the directed edges deliver
+    1..dmax rounds late while 100 roots heartbeat at once; every lane's inbox
+    is a ring of kRing buffers.  Round by round against the oracle
+    (orc_pt_set_delays): counts by kind summed over roots every round, per-root
+    sets / delivered / Round, the rows over all roots and the next round's
+    in-flight messages every 3 rounds, until nothing is pending; then the
+    roots heartbeat again over their pruned trees.  A root whose messages may
+    still be on the wire cannot heartbeat again (PSIM_EBUSY)."""
+    pa, sim, orc = _forest(700, 31 + L, max_roots=128, L=L)
+    rng = np.random.default_rng(5 + L)
+    src = np.repeat(np.arange(sim.n), np.diff(sim.slot_row_ptr.astype(np.int64)))
+    pick = rng.random(len(src)) < 0.25
+    pairs = np.stack([src[pick], sim.slot_col[pick]], axis=1)
+    d = rng.integers(1, dmax + 1, len(pairs)).astype(np.uint8)
+    sim.set_delays(pairs, d)
+    orc.set_delays(pairs, d)
+    roots = sorted(rng.choice(sim.n, 100, replace=False).tolist())
+    monos = {}
+    for interval in range(2):
+        got = sim.broadcast_many(roots)
+        for r, m in zip(roots, got):
+            monos[r] = orc.heartbeat(r)
+            assert m == monos[r]
+        if interval == 0:
+            sim.step(1)
+            orc.step(1)
+            with pytest.raises(pa.PsimError) as ei:
+                sim.broadcast_many([roots[0]])
+            assert ei.value.name == "PSIM_EBUSY"
+        rounds = 0
+        while True:
+            gs, os_ = sim.step(1)[0], orc.step(1)[0]
+            rounds += 1
+            for k in KINDS:
+                assert gs[k] == os_[k], (interval, rounds, k, gs, os_)
+            assert gs["delivered_new"] == os_["delivered_new"], (interval, rounds)
+            if rounds % 3 == 0:
+                ost_all, oo = _compare_roots(sim, orc, monos, roots)
+                assert np.array_equal(ost_all, oo), ("rows", rounds)
+                inflight = []
+                for root in roots:
+                    sim.focus(root)
+                    inflight += sim.decode_inflight()
+                want = [(s_, d_, t, r if t in (1, 3) else 0) for (s_, d_, t, r) in orc.pending()]
+                assert sorted(inflight) == sorted(want), (interval, rounds)
+            if orc.inflight() == 0 and os_["outstanding_live"] == 0:
+                break
+            assert rounds < 400
+        ost_all, oo = _compare_roots(sim, orc, monos, roots)
+        assert np.array_equal(ost_all, oo)
+        for r in roots:
+            sim.focus(r)
+            assert sim.delivered().all(), (interval, r)
+    # healed while quiescent: next-round delivery again, psim_run to quiescence
+    sim.set_delays([], [])
+    orc.set_delays([], [])
+    got = sim.broadcast_many(roots[:10])
+    for r, m in zip(roots[:10], got):
+        monos[r] = orc.heartbeat(r)
+        assert m == monos[r]
+    gst, gr = sim.run()
+    ost, orr = orc.run()
+    assert gr == orr
+    for a, b in zip(gst, ost):
+        for k in KINDS:
+            assert a[k] == b[k], (k, a, b)
+    _compare_roots(sim, orc, monos, roots[:10])
+    sim.close()

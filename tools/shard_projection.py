@@ -27,6 +27,43 @@ import partisan_amd as pa  # noqa: E402
 from partisan_amd._lib import RoundStats, check, lib  # noqa: E402
 
 
+def rccl_latency(iters=2000):
+    """Per-call cost of what psim_shard_run adds per round on top of the
+    kernels, on a world-1 RCCL communicator: one grouped send/recv (to self,
+    4 KB: a sparse round's records) and the 11-value counter all-reduce every
+    4 rounds.  A floor for the latency term: at world 8 the calls also wait
+    for the slowest peer."""
+    import time
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29631")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    sb = torch.zeros(1024, dtype=torch.int32, device=dev)
+    rb = torch.zeros(1024, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(11, dtype=torch.int64, device=dev)
+
+    def sendrecv():
+        for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, sb, 0), dist.P2POp(dist.irecv, rb, 0)]):
+            q.wait()
+
+    res = {}
+    for name, fn in (("grouped_send_recv_us", sendrecv), ("allreduce_11_us", lambda: dist.all_reduce(cnt))):
+        for _ in range(50):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(dev)
+        res[name] = round((time.perf_counter() - t0) / iters * 1e6, 2)
+    dist.destroy_process_group()
+    res["per_round_us"] = round(res["grouped_send_recv_us"] + res["allreduce_11_us"] / 4, 2)
+    res["method"] = ("torch.distributed nccl (RCCL) world 1 on one MI355X, back-to-back calls with a sync at the "
+                     "ends; per round = one grouped send/recv + a quarter of the 4-round counter all-reduce")
+    return res
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=10_000_000)
@@ -36,6 +73,9 @@ def main():
     p.add_argument("--xgmi-gbps", type=float, default=7 * 153.0)
     p.add_argument("--floods", type=int, default=3)
     p.add_argument("--csr", action="store_true", help="CSR slot rows instead of the ELL rows shards load by default")
+    p.add_argument("--rccl-latency", action="store_true",
+                   help="also time a world-1 RCCL communicator's grouped send/recv + counter all-reduce per round "
+                        "(the latency floor of psim_shard_run's exchange; torch.distributed nccl, 127.0.0.1)")
     a = p.parse_args()
     W, n = a.world, a.n
     dev = torch.device("cuda", 0)
@@ -82,6 +122,7 @@ def main():
         per_round = []
         for rnd in range(200):
             ks = []
+            tb = []
             tot = 0
             live = 0
             hold = 0
@@ -93,11 +134,13 @@ def main():
                 check(lib().psim_shard_collect(s._h, st, 1, C.byref(got), lv), s._h)   # syncs: kernels run alone
                 d = st[0].as_dict()
                 ks.append(d["kernel_ms"])
+                # touched-state bytes of this shard's round (bench.py shard_touched_bytes)
+                tb.append(int(d["algo_bytes"]) - 16 * s.n + 16 * int(d["active"]))
                 tot += sum(d[k] for k in ("broadcast", "prune", "i_have", "ignored_i_have", "graft"))
                 live += int(lv[0])
                 hold += d["outstanding_vertices"]
             exchange()
-            per_round.append({"kernel_ms": ks, "msgs": tot, "holders": hold})
+            per_round.append({"kernel_ms": ks, "touched": tb, "msgs": tot, "holders": hold})
             if tot == 0 and live == 0:
                 break
         floods.append(per_round)
@@ -119,8 +162,29 @@ def main():
         if i % 4 == 3:                               # collective: actual counts
             bM, bH = float(r["msgs"]), float(r["holders"])
     xms_rec = sum(rec_fabric) / (a.xgmi_gbps * 1e6)
+    # touched-state roofline per shard over the flood (bench.py's model, each
+    # shard against its own GPU's 8 TB/s)
+    tbs = [sum(r["touched"][i] for r in last) for i in range(W)]
+    frac = [tbs[i] / (ksum[i] * 1e-3) / 1e9 / 8000.0 if ksum[i] > 0 else None for i in range(W)]
+    lat = rccl_latency() if a.rccl_latency else None
+    lat_ms = (len(last) * lat["per_round_us"] / 1e3) if lat else 0.0
+    step_ms = kmax + xms_rec + lat_ms
+    import hashlib
+    from partisan_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()
     out = {
         "n": n, "world": W, "rounds": len(last), "rows": "csr" if a.csr else "ell",
+        "lib_sha256": sha,
+        "per_round": [{"round": i + 1, "msgs_global": r["msgs"],
+                       "kernel_us_each_shard": [round(1e3 * x, 1) for x in r["kernel_ms"]],
+                       "format": "records" if rec_fabric[i] != max(fabric) else "dense",
+                       "fabric_bytes_per_shard": rec_fabric[i]} for i, r in enumerate(last)],
+        "touched_bytes_per_flood_each_shard": tbs,
+        "touched_frac_each_shard": [round(x, 4) if x is not None else None for x in frac],
+        "rccl_latency": lat,
+        "projected_step_ms_with_records_and_latency": round(step_ms, 4),
+        "projected_touched_frac_at_step": round(sum(tbs) / W / (step_ms * 1e-3) / 1e9 / 8000.0, 4),
         "per_shard_vertices": [s.n for s in sims],
         "kernel_ms_per_flood_max_over_shards": round(kmax, 4),
         "kernel_ms_per_flood_each_shard": [round(x, 4) for x in ksum],
