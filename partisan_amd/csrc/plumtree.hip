@@ -461,6 +461,13 @@ constexpr bool kNtRows = false;
 constexpr bool kNtSweep = true;
 constexpr bool kNtState = false;
 
+#ifndef PSIM_W5_CONST
+#define PSIM_W5_CONST 1        // A/B knob: 0 = the 5-slot kernel reads the row width at run time
+#endif
+#ifndef PSIM_VLOAD_ONE_REGION
+#define PSIM_VLOAD_ONE_REGION 1   // A/B knob: 0 = one predicated load per slot
+#endif
+
 template <uint32_t kCap>
 struct VLoad {
     uint4 st;
@@ -493,11 +500,24 @@ __device__ __forceinline__ void vload(const PtArgs& a, uint32_t v, uint32_t rs, 
     L.rows = rows;
     if (a.ecol) {                // ELL packed rows: half the row bytes
         const uint32_t W = a.ell;
+        uint32_t p[kCap];
+        if (PSIM_VLOAD_ONE_REGION) {
+            // one divergent region for the whole row (a region per slot cost
+            // an exec save / restore and a branch per slot)
+#pragma unroll
+            for (uint32_t s = 0; s < kCap; s++) p[s] = 0u;
+            if (rows) {
+#pragma unroll
+                for (uint32_t s = 0; s < kCap; s++) p[s] = s < deg ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t s = 0; s < kCap; s++) p[s] = (rows && s < deg) ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
+        }
 #pragma unroll
         for (uint32_t s = 0; s < kCap; s++) {
-            const uint32_t p = (rows && s < deg) ? ld_stream<kNtRows>(a.ecol + rs + s) : 0u;
-            L.cl[s] = p == kNoPeer ? kNoPeer : p >> 3;
-            L.rv[s] = p == kNoPeer ? 0u : (p >> 3) * W + (p & 7u);
+            L.cl[s] = p[s] == kNoPeer ? kNoPeer : p[s] >> 3;
+            L.rv[s] = p[s] == kNoPeer ? 0u : (p[s] >> 3) * W + (p[s] & 7u);
         }
         return;
     }
@@ -1035,7 +1055,10 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     const uint32_t t = threadIdx.x;
     RoundMode md;
     if (!round_counts(a, md, wl_off)) return;
-    const uint32_t W = a.ell;
+    // the 5-slot instantiation runs rows of exactly 5 slots (launch_pt_round):
+    // a compile-time row width folds every per-slot "s < deg" test, the row
+    // offsets v * W and the sweep's division
+    const uint32_t W = (kCap == 5 && PSIM_W5_CONST) ? 5u : a.ell;
     const bool list = md.list_in;
     // The grid is the chip's resident workgroups (PtArgs::ell_grid), each
     // looping over chunks c = blockIdx.x, + gridDim.x, ...: a chunk is 1024

@@ -681,6 +681,7 @@ hipError_t scrub_if_needed(psim_handle* h, uint64_t last) {
 
 // ---- heartbeat-root lanes ------------------------------------------------
 void save_lane(psim_handle* h) {
+    if (h->lanes.empty()) return;              // a forest keeps its lanes in slabs
     auto& l = h->lanes[h->cur_lane];
     l.vs = h->vs; l.in[0] = h->in[0]; l.in[1] = h->in[1]; l.pend[0] = h->pend[0]; l.pend[1] = h->pend[1];
     l.ost = h->ost; l.ost_total = h->ost_total; l.par = h->par; l.serial = h->serial; l.root = h->root;

@@ -36,6 +36,10 @@ for s in $STEPS; do
                    --timeout 300 --timeout-method thread ;;
         ab)    run ab 1100 bash tools/ab/gs_ab.sh ;;
         proj)  run shard_projection 600 python tools/shard_projection.py --rccl-latency ;;
+        c3prof)
+            export TMPDIR=/tmp
+            run c3prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c3prof -o run --output-format csv \
+                -- python3 tools/c3_wall.py 1000000 30 ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         benchq) run benchq 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity ;;
@@ -48,9 +52,9 @@ for s in $STEPS; do
         pmc)
             export TMPDIR=/tmp
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv \
-                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity
+                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --sustain-s 0
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv \
-                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity ;;
+                -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --sustain-s 0 ;;
         *) echo "unknown step $s" ;;
     esac
 done
