@@ -464,6 +464,12 @@ constexpr bool kNtState = false;
 #ifndef PSIM_W5_CONST
 #define PSIM_W5_CONST 1        // A/B knob: 0 = the 5-slot kernel reads the row width at run time
 #endif
+#ifndef PSIM_OUT_MASKS
+#define PSIM_OUT_MASKS 1       // A/B knob: 0 = the flood's output words through pt_out1 slot by slot
+#endif
+#ifndef PSIM_MARK1_LOOP
+#define PSIM_MARK1_LOOP 1      // A/B knob: 0 = flag rounds share the run-time-mark candidate loop with list rounds
+#endif
 #ifndef PSIM_VLOAD_ONE_REGION
 #define PSIM_VLOAD_ONE_REGION 1   // A/B knob: 0 = one predicated load per slot
 #endif
@@ -626,7 +632,7 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     // of a divergent per-slot FIFO walk.  Any other word: the general walk.
     constexpr uint32_t kBP = PSIM_MSG_BROADCAST | (PSIM_MSG_PRUNE << kKindBits);   // [broadcast, prune]
     constexpr uint32_t kPB = PSIM_MSG_PRUNE | (PSIM_MSG_BROADCAST << kKindBits);   // [prune, broadcast]
-    uint32_t bm = 0, pm = 0, om = 0;
+    uint32_t bm = 0, pm = 0, om = 0, rep = 0;        // rep: slots answering a broadcast with a prune
 #pragma unroll
     for (uint32_t s = 0; s < kCap; s++) {
         const uint32_t f = w[s] & kFifoMask;
@@ -638,7 +644,6 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
         om |= (f != 0u && !b && !p ? 1u : 0u) << s;
     }
     if (om == 0u) {
-        uint32_t rep = 0;                                // slots answering a broadcast with a prune
         if (!x.rcv && bm) {
             const uint32_t s0 = (uint32_t)__ffs(bm) - 1u, b0 = 1u << s0;
             uint32_t w0 = 0;
@@ -692,13 +697,40 @@ __device__ __forceinline__ int pt_vertex_core(const PtArgs& a, uint32_t v, uint3
     bool sent = false;
     uint32_t wo[kCap];
     uint32_t nstored = 0;
+    if (PSIM_OUT_MASKS && om == 0u) {
+        // The flood's words (every reply a prune): each slot's FIFO from the
+        // push / reply / i_have masks -- [push, prune] after the delivering
+        // slot, [prune, push] before it, then the i_have -- and the kinds
+        // counted once per vertex by popcount instead of per slot (pt_out1).
+        const uint32_t dm = deg >= 32u ? ~0u : (1u << deg) - 1u;
+        const uint32_t pu = x.push_mask & dm, re = rep & dm, ih = ihave & dm;
+        const uint32_t hi = x.push_pos >= 31u ? 0u : ~0u << (x.push_pos + 1u);   // slots after the delivering one
+        const uint32_t hdr = (x.myround << kRoundShift) | (a.wtag << kTagShift);
 #pragma unroll
-    for (uint32_t s = 0; s < kCap; s++) {
-        wo[s] = s >= deg ? 0u : r[s] < 8u ? pt_out1<true>(s, r[s], x, ihave, a.wtag, c)
-                                           : pt_out<true>(s, r[s], x, ihave, a.wtag, c);
-        sent |= wo[s] != 0u;
-        if (kFault && wo[s] && omitted(a, rs + s)) wo[s] = 0u;   // sent (counted) and lost
-        nstored += wo[s] != 0u ? 1u : 0u;
+        for (uint32_t s = 0; s < kCap; s++) {
+            const uint32_t b = 1u << s;
+            const bool p = (pu & b) != 0u, r1 = (re & b) != 0u, i1 = (ih & b) != 0u;
+            const uint32_t n = (p ? 1u : 0u) + (r1 ? 1u : 0u);
+            const uint32_t first = p && (!r1 || (hi & b)) ? (uint32_t)PSIM_MSG_BROADCAST
+                                 : r1 ? (uint32_t)PSIM_MSG_PRUNE : 0u;
+            const uint32_t second = p && r1 ? ((hi & b) ? (uint32_t)PSIM_MSG_PRUNE : (uint32_t)PSIM_MSG_BROADCAST) : 0u;
+            const uint32_t fifo = first | (second << kKindBits) | (i1 ? (uint32_t)PSIM_MSG_IHAVE << (kKindBits * n) : 0u);
+            wo[s] = fifo ? fifo | hdr : 0u;
+            sent |= fifo != 0u;
+            if (kFault && wo[s] && omitted(a, rs + s)) wo[s] = 0u;   // sent (counted) and lost
+            nstored += wo[s] != 0u ? 1u : 0u;
+        }
+        c.kinds += (unsigned long long)__popc(pu) + ((unsigned long long)__popc(re) << 12) +
+                   ((unsigned long long)__popc(ih) << 24);
+    } else {
+#pragma unroll
+        for (uint32_t s = 0; s < kCap; s++) {
+            wo[s] = s >= deg ? 0u : r[s] < 8u ? pt_out1<true>(s, r[s], x, ihave, a.wtag, c)
+                                               : pt_out<true>(s, r[s], x, ihave, a.wtag, c);
+            sent |= wo[s] != 0u;
+            if (kFault && wo[s] && omitted(a, rs + s)) wo[s] = 0u;   // sent (counted) and lost
+            nstored += wo[s] != 0u ? 1u : 0u;
+        }
     }
     c.words += nstored;
     if constexpr (kLocal && !kFault) {
@@ -1255,6 +1287,9 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
         };
         const uint32_t mark = __builtin_amdgcn_readfirstlane(md.mark);
         if (mark == 0) cand_loop(std::integral_constant<int, 0>{});
+#if PSIM_MARK1_LOOP
+        else if (mark == 1) cand_loop(std::integral_constant<int, 1>{});   // flags only: no claims, no list
+#endif
         else cand_loop(std::integral_constant<int, -1>{});
         __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
     }
