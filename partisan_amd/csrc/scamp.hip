@@ -41,7 +41,6 @@ struct Ctx {
     uint32_t dropped, ndraw, err, resub;
     uint32_t nev;      // update events recorded this round
     WaveQ<ScMsg> q;    // this wave's send buffer (LDS)
-    int32_t self_in;   // the manager's stop check (self in the partial view) since the row last changed; -1 unknown
 };
 
 // partisan_peer_service_events:update(Members) after a handler that changed
@@ -226,7 +225,6 @@ __device__ void do_periodic(Ctx& c) {
 // handle_message/2; returns false when the manager stops (:1791-1803)
 __device__ bool do_message(Ctx& c, const ScMsg& m) {
     const ScArgs& a = *c.a;
-    bool pvch = false;       // this handler edited the partial view (the stop check must rescan it)
     switch (m.type) {
     case SC_PING:                                             // v2 :224-229, v1 :219-227
         c.h.last_ping = (int32_t)a.round;
@@ -235,7 +233,6 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         const uint32_t node = m.a;
         const uint32_t r10 = 1u + (uint32_t)__umul64hi(draw64(c), 10ull);   // random_0_or_1: uniform(10) >= 5
         const bool keep = r10 < 5 && !in_pv(c, node);
-        pvch = keep;
         if (keep) {
             if (a.ver == 2) {
                 pv_push_front(c, node);
@@ -262,7 +259,6 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
         const uint32_t node = m.a;
         if (!in_pv(c, node)) break;
         if (a.ver == 1) { c.err |= 8u; return false; }       // Q17: the manager stops
-        pvch = true;
         const uint32_t n0 = c.h.npv;
         const uint32_t at = pv_del_first(c, node);
         if (!in_pv(c, node)) record_update(c, 0xFFFFFFFFu, node);   // a duplicate keeps it a member
@@ -274,7 +270,6 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
     }
     case SC_REPLACE: {                                        // v2 :275-294
         if (m.a == m.b || !in_pv(c, m.a)) break;
-        pvch = true;
         const bool had_b = in_pv(c, m.b);
         for (uint32_t i = 0; i < c.h.npv; i++)
             if (c.pv[i] == m.a) c.pv[i] = m.b;
@@ -283,7 +278,6 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
     }
     case SC_BOOT: {                                           // v2 :230-274
         if (m.a != c.v) break;
-        pvch = true;
         const int32_t L = (int32_t)c.h.niv, P = (int32_t)c.h.npv;
         const int32_t num = L - (int32_t)(a.c - 1), rem = L - num;
         bool crash = false;                                   // lists:nth/2 out of range (Q18)
@@ -303,10 +297,7 @@ __device__ bool do_message(Ctx& c, const ScMsg& m) {
     default:
         break;
     }
-    // the stop check scans the row only after a handler edited it: a ping
-    // round's ~80 pings per vertex rescanned an unchanged row 80 times
-    if (pvch || c.self_in < 0) c.self_in = in_pv(c, c.v) ? 1 : 0;
-    return c.self_in != 0;
+    return in_pv(c, c.v);
 }
 
 __device__ __forceinline__ bool msg_less(const ScMsg& x, const ScMsg& y) {
@@ -413,7 +404,6 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         for (int i = 0; i < 7; i++) c.sent[i] = 0;
         c.dropped = c.ndraw = c.err = c.resub = 0;
         c.nev = 0;
-        c.self_in = -1;
         c.q = q;
         const bool fresh = c.h.fresh != 0;
         c.h.fresh = 0;
@@ -433,13 +423,9 @@ __global__ __launch_bounds__(kBlock) void sc_process(ScArgs a) {
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         const uint32_t d1 = c.ndraw;
 #endif
-        // inbox in (src, seq) order; a restarted vertex drops what was sent to its old incarnation.
-        // A bucket of pings only needs no order: each ping sets last_ping to
-        // the round and edits nothing the stop check reads (v2 :224-229)
+        // inbox in (src, seq) order; a restarted vertex drops what was sent to its old incarnation
         const uint32_t lo = a.off[v], hi = a.off[v + 1];
-        bool all_ping = true;
-        for (uint32_t i = lo; i < hi && all_ping; i++) all_ping = a.in[a.idx[i]].type == SC_PING;
-        if (!fresh && hi > lo + 1 && !all_ping) {
+        if (!fresh && hi > lo) {
             for (uint32_t i = lo + 1; i < hi; i++) {
                 const uint32_t x = a.idx[i];
                 const ScMsg mx = a.in[x];
