@@ -1071,9 +1071,43 @@ constexpr uint32_t kFullQuarters = PSIM_FULL_QUARTERS;
 // leaves to the next integer)
 __device__ __forceinline__ uint32_t div_w(uint32_t x, uint32_t wmag) { return (x * wmag) >> 18; }
 
+// Diagnostic build (-DPSIM_PHASE_PROF=1, tools/phase_probe.py): workgroup 0
+// of every ELL round launch clocks its phases on the 100 MHz real-time
+// counter -- entry, counts read, first chunk's group list, sweep, candidates,
+// candidate loop, all chunks, counters flushed -- into g_phase[launch][8].
+#ifndef PSIM_PHASE_PROF
+#define PSIM_PHASE_PROF 0
+#endif
+#if PSIM_PHASE_PROF
+constexpr uint32_t kPhaseRecs = 4096;
+__device__ unsigned long long g_phase[kPhaseRecs][8];
+__device__ uint32_t g_phase_n;
+struct PhaseClock {
+    unsigned long long t[8] = {};
+    bool on;
+    __device__ PhaseClock() : on(blockIdx.x == 0 && threadIdx.x == 0) {}
+    __device__ __forceinline__ void mark(int i) { if (on) t[i] = (unsigned long long)wall_clock64(); }
+    __device__ __forceinline__ void flush() {
+        if (!on) return;
+        const uint32_t k = g_phase_n;
+        if (k < kPhaseRecs)
+            for (int i = 0; i < 8; i++) g_phase[k][i] = t[i];
+        g_phase_n = k + 1u;
+        on = false;
+    }
+};
+#else
+struct PhaseClock {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+};
+#endif
+
 template <bool kFault, uint32_t kCap, bool kLocal = false>
 __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     static_assert(kEllChunk * kEllMax <= (1u << 13), "div_w is exact below 2^13");
+    PhaseClock ph;
+    ph.mark(0);
     extern __shared__ __attribute__((aligned(16))) uint32_t wbuf[];   // [kEllChunk * W] the live words of the groups read
     __shared__ uint32_t actm[kEllChunk / 32];          // vertices with live words
     __shared__ uint32_t duem[kEllChunk / 32];          // vertices holding outstanding rows on a tick round
@@ -1086,7 +1120,11 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
     constexpr uint32_t kGroups = kEllChunk >> kGroupShift, kGV = 1u << kGroupShift;
     const uint32_t t = threadIdx.x;
     RoundMode md;
-    if (!round_counts(a, md, wl_off)) return;
+    if (!round_counts(a, md, wl_off)) {
+        ph.flush();
+        return;
+    }
+    ph.mark(1);
     // the 5-slot instantiation runs rows of exactly 5 slots (launch_pt_round):
     // a compile-time row width folds every per-slot "s < deg" test, the row
     // offsets v * W and the sweep's division
@@ -1109,7 +1147,10 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
                        : a.wl_gpc ? min(a.wl_gpc, kGroups)
                                   : max(1u, min(kGroups, (total + lwg - 1) / lwg));
     const uint32_t nchunks = list ? (total + gpc - 1) / gpc : (a.n + kEllChunk - 1) / kEllChunk;
-    if (blockIdx.x >= nchunks) return;                 // uniform
+    if (blockIdx.x >= nchunks) {                       // uniform
+        ph.flush();
+        return;
+    }
     if (t == 0) wl.n = 0;
     if (kFault && a.dly && t < kRing) delay_hist()[t] = 0;
     Ctr c;
@@ -1161,6 +1202,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             }
         }
         __syncthreads();
+        if (ch == blockIdx.x) ph.mark(2);
         const uint32_t ng = ngrp;
         // group slot i of this chunk: LDS words at pos(i) * gw, first vertex gv(i)
         auto pos = [&](uint32_t i) -> uint32_t { return list ? i : uint32_t(glist[i]); };
@@ -1248,6 +1290,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             }
         }
         __syncthreads();
+        if (ch == blockIdx.x) ph.mark(3);
         {
             constexpr uint32_t kMask = (1u << kVpt) - 1u;
             const uint32_t v4 = kVpt * t;
@@ -1273,6 +1316,7 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
             }
         }
         __syncthreads();
+        if (ch == blockIdx.x) ph.mark(4);
         const uint32_t nc = ncand;
         // the round's mark is uniform over the launch: the dense rounds' (mark 0,
         // no flags) get a candidate loop of their own
@@ -1292,11 +1336,15 @@ __device__ __forceinline__ void pt_round_ell_body(const PtArgs& a) {
 #endif
         else cand_loop(std::integral_constant<int, -1>{});
         __syncthreads();                               // LDS (cand, wbuf, gl) is reused by the next chunk
+        if (ch == blockIdx.x) ph.mark(5);
     }
+    ph.mark(6);
     if (md.mark == 2) wl_flush(a, &wl);
     flush_counters(c, a.stats, a.ost_total, a.mcnt ? a.mcnt + a.m_w * 64 + (blockIdx.x & 63) : nullptr,
                    hold_delta(a));
     flush_delays<kFault>(a);
+    ph.mark(7);
+    ph.flush();
 }
 
 template <bool kFault, uint32_t kCap, bool kLocal>
@@ -2380,3 +2428,20 @@ hipError_t launch_pt_renorm(const PtArgs& a, hipStream_t s) {
 }
 
 }  // namespace psim
+
+#if PSIM_PHASE_PROF
+// diagnostic build only (not in include/psim.h): the phase records so far,
+// [launch][8] real-time ticks (100 MHz); the record count restarts at zero
+extern "C" int psim_debug_phases(unsigned long long* out, uint32_t cap, uint32_t* n) {
+    uint32_t k = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&k, HIP_SYMBOL(psim::g_phase_n), 4) != hipSuccess) return -1;
+    k = k < psim::kPhaseRecs ? k : psim::kPhaseRecs;
+    const uint32_t c = k < cap ? k : cap;
+    if (c && hipMemcpyFromSymbol(out, HIP_SYMBOL(psim::g_phase), size_t(c) * 8 * 8) != hipSuccess) return -1;
+    const uint32_t z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(psim::g_phase_n), &z, 4) != hipSuccess) return -1;
+    *n = c;
+    return 0;
+}
+#endif
