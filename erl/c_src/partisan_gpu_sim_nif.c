@@ -77,9 +77,11 @@ static unsigned map_u32(ErlNifEnv* env, ERL_NIF_TERM m, const char* key, unsigne
     return dflt;
 }
 
-/* new(#{lazy_tick_rounds, exchange_tick_rounds, device, seed, max_roots}) -> {ok, Sim}
+/* new(#{lazy_tick_rounds, exchange_tick_rounds, device, seed, max_roots, forest_lanes}) -> {ok, Sim}
  * max_roots: heartbeat roots whose trees the handle keeps (every node of the
- * cluster heartbeats, partisan_plumtree_backend:341-368); 0 / absent = 16 */
+ * cluster heartbeats, partisan_plumtree_backend:341-368); 0 / absent = 16.
+ * forest_lanes (max_roots > 16): lanes for the heartbeats in flight at once,
+ * every root's records kept (psim_forest_set_lanes); 0 / absent = one per root */
 static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
     if (!enif_is_map(env, argv[0])) return enif_make_badarg(env);
@@ -100,6 +102,13 @@ static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[])
     memset(r, 0, sizeof *r);
     int rc = psim_create(&cfg, &r->h);
     if (rc != PSIM_OK) { enif_release_resource(r); return err(env, rc); }
+    const unsigned lanes = map_u32(env, argv[0], "forest_lanes", 0);
+    if (lanes && (rc = psim_forest_set_lanes(r->h, lanes)) != PSIM_OK) {
+        psim_destroy(r->h);
+        r->h = NULL;
+        enif_release_resource(r);
+        return err(env, rc);
+    }
     r->mu = enif_mutex_create("partisan_gpu_sim");
     ERL_NIF_TERM t = enif_make_resource(env, r);
     enif_release_resource(r);

@@ -37,7 +37,7 @@ init() ->
     erlang:load_nif(filename:join(Dir, "partisan_gpu_sim"), 0).
 
 -spec new(#{device => integer(), seed => non_neg_integer(), lazy_tick_rounds => pos_integer(),
-            max_roots => non_neg_integer(),
+            max_roots => non_neg_integer(), forest_lanes => non_neg_integer(),
             exchange_tick_rounds => pos_integer()}) -> {ok, sim()} | error().
 new(_Opts) -> erlang:nif_error(nif_not_loaded).
 

@@ -201,6 +201,22 @@ int  psim_plumtree_broadcast_run_n(psim_handle* h, uint32_t root, uint32_t count
  * _inflight, psim_trace_hash) read the focused root: the last broadcast one,
  * or the one chosen here (PSIM_EINVAL if it has no lane). */
 int  psim_plumtree_focus(psim_handle* h, uint32_t root);
+/* Forest capacity (max_roots > 16): the per-root records that outlive a
+ * heartbeat -- every vertex's eager / lazy / outstanding sets, accepted Round
+ * and delivered id for that root, the reference's eager_sets / lazy_sets
+ * entries kept for good (partisan_plumtree_broadcast.erl:1240-1248,
+ * 1278-1282) -- take 16 B per vertex and root; a heartbeat in flight also
+ * needs a lane (its inbox words, group flags, rows and counts: ~40 B per
+ * vertex).  With lanes < max_roots the handle keeps max_roots roots' records
+ * but only `lanes` lanes: a heartbeat takes the lane of a root whose own
+ * heartbeat is done (that root is parked: its records stay, nothing of it is
+ * in flight), and psim_plumtree_broadcast_many returns PSIM_ENOSPC when more
+ * heartbeats are in flight at once than there are lanes.  Results are those
+ * of lanes == max_roots.  0 (the default) = max_roots lanes.  Call before
+ * psim_load_csr: PSIM_ESTATE after it or on a handle that is no forest,
+ * PSIM_EINVAL for lanes > max_roots.  psim_plumtree_focus on a parked root
+ * shows its records with nothing in flight. */
+int  psim_forest_set_lanes(psim_handle* h, uint32_t lanes);
 /* Runs exactly `rounds` rounds.  stats may be NULL; otherwise stats[cap]. */
 int  psim_step(psim_handle* h, uint32_t rounds, psim_round_stats* stats, size_t cap);
 /* Runs until quiescent (nothing in flight and no outstanding i_have row to

@@ -189,6 +189,7 @@ SIGNATURES = {
     "psim_get_inflight": (C.c_int, [_H, _P(C.c_uint32), C.c_uint64]),
     "psim_trace_hash": (C.c_int, [_H, _P(C.c_uint64)]),
     "psim_plumtree_focus": (C.c_int, [_H, C.c_uint32]),
+    "psim_forest_set_lanes": (C.c_int, [_H, C.c_uint32]),
     "psim_set_omissions": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), C.c_size_t]),
     "psim_set_delays": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint8), C.c_size_t]),
     "psim_get_messages": (C.c_int, [_H, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),

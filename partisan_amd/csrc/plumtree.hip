@@ -1373,9 +1373,12 @@ __global__ __launch_bounds__(kBlock) void pt_round_ell_lanes_kernel(const PtArgs
 // The forest (FoArgs, psim_internal.h): lane L's arguments
 // are lane 0's shifted by L slices -- built in registers from one kernel
 // argument block, so a round over 10^4 roots uploads nothing per lane.
+__device__ __forceinline__ uint32_t fo_slot(const FoArgs& f, uint32_t lane) { return f.slot ? f.slot[lane] : lane; }
+
 __device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
     PtArgs a = f.a;
-    a.vs += lane * f.s_vs;
+    const uint32_t sl = fo_slot(f, lane);               // the lane's root's records (parked roots: FoArgs::slot)
+    a.vs += sl * f.s_vs;
     a.in_cur += lane * f.s_in;
     a.in_nxt += lane * f.s_in;
     a.pend_cur += lane * f.s_pend;
@@ -1393,7 +1396,7 @@ __device__ __forceinline__ PtArgs fo_lane(const FoArgs& f, uint32_t lane) {
     }
     if (a.wl_cur) a.wl_cur = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_cur) + lane * f.s_pend);
     if (a.wl_nxt) a.wl_nxt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.wl_nxt) + lane * f.s_pend);
-    const uint2 li = f.info[lane];
+    const uint2 li = f.info[sl];
     a.mono8 = li.x;
     a.root = li.y;
     return a;
@@ -1811,15 +1814,15 @@ __global__ __launch_bounds__(kBlock) void fo_seed_kernel(FoArgs f) {
     m[kMcntHoldD + f.a.m_s] = 0u;
 }
 
-// (lane, vertex) pairs, flattened: lane i of lanes[] (or lane i itself)
-__global__ __launch_bounds__(kBlock) void fo_renorm_kernel(FoArgs f, const uint32_t* __restrict__ lanes, uint32_t k) {
+// (state slot, vertex) pairs, flattened: slot i of slots[] (or slot i itself)
+__global__ __launch_bounds__(kBlock) void fo_renorm_kernel(FoArgs f, const uint32_t* __restrict__ slots, uint32_t k) {
     const unsigned long long total = (unsigned long long)k * f.a.n;
     const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
     for (unsigned long long x = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; x < total; x += stride) {
         const uint32_t i = uint32_t(x / f.a.n), v = uint32_t(x % f.a.n);
-        const uint32_t lane = lanes ? lanes[i] : i;
-        const uint32_t mono8 = f.info[lane].x;
-        uint4* vs = f.a.vs + lane * f.s_vs;
+        const uint32_t sl = slots ? slots[i] : i;
+        const uint32_t mono8 = f.info[sl].x;
+        uint4* vs = f.a.vs + sl * f.s_vs;
         uint4 st = vs[v];
         uint32_t rseq = (st.w >> 16) & 0xFFu, ep = st.w >> 24;
         if (rseq != mono8) rseq = (mono8 - 1u) & 0xFFu;
@@ -1837,7 +1840,7 @@ __global__ __launch_bounds__(kBlock) void fo_count_live_kernel(FoArgs f, unsigne
     for (unsigned long long x = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; x < total; x += stride) {
         const uint32_t lane = uint32_t(x / a.n), v = uint32_t(x % a.n);
         if (!a.ost[lane * f.s_ost + v] || !bit_alive(a.alive, a.v_lo + v)) continue;
-        uint32_t m = a.vs[lane * f.s_vs + v].z;
+        uint32_t m = a.vs[fo_slot(f, lane) * f.s_vs + v].z;
         const uint32_t rs = a.ell ? v * a.ell : a.rowp[v];
         while (m) {
             const uint32_t q = __ffs(m) - 1;
@@ -1850,11 +1853,11 @@ __global__ __launch_bounds__(kBlock) void fo_count_live_kernel(FoArgs f, unsigne
 }
 
 __global__ __launch_bounds__(kBlock) void fo_forget_kernel(FoArgs f, uint32_t v) {
-    const uint32_t lane = blockIdx.x * kBlock + threadIdx.x;
-    if (lane >= f.nl) return;
-    uint4* p = f.a.vs + lane * f.s_vs + v;
+    const uint32_t sl = blockIdx.x * kBlock + threadIdx.x;   // every root's records, parked or not
+    if (sl >= f.ns) return;
+    uint4* p = f.a.vs + sl * f.s_vs + v;
     uint4 st = *p;
-    st.w = (st.w & 0xFF00FFFFu) | (((f.info[lane].x - 1u) & 0xFFu) << 16);
+    st.w = (st.w & 0xFF00FFFFu) | (((f.info[sl].x - 1u) & 0xFFu) << 16);
     *p = st;
 }
 
@@ -2303,11 +2306,11 @@ hipError_t launch_fo_seed(const FoArgs& f, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s) {
+hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* slots, uint32_t k, hipStream_t s) {
     if (!k || !f.a.n) return hipSuccess;
     const unsigned long long total = (unsigned long long)k * f.a.n;
     const uint32_t g = uint32_t(std::min<unsigned long long>(65535ull * 8, (total + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(fo_renorm_kernel, dim3(g), dim3(kBlock), 0, s, f, lanes, k);
+    hipLaunchKernelGGL(fo_renorm_kernel, dim3(g), dim3(kBlock), 0, s, f, slots, k);
     return hipGetLastError();
 }
 
@@ -2320,8 +2323,8 @@ hipError_t launch_fo_count_live(const FoArgs& f, unsigned long long* out, hipStr
 }
 
 hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s) {
-    if (!f.nl) return hipSuccess;
-    hipLaunchKernelGGL(fo_forget_kernel, dim3((f.nl + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, v);
+    if (!f.ns) return hipSuccess;
+    hipLaunchKernelGGL(fo_forget_kernel, dim3((f.ns + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, v);
     return hipGetLastError();
 }
 

@@ -189,11 +189,28 @@ struct psim_handle {
         uint32_t* ring = nullptr;                // [cap][s_ring]
         uint8_t* pring = nullptr;                // [cap][s_pring]
         uint64_t s_ring = 0, s_pring = 0;
-        std::vector<uint2> h_info;
-        std::vector<uint32_t> serial;            // lane -> heartbeats so far (the lane's tag source)
-        std::vector<uint32_t> root_of;           // lane -> root
-        std::unordered_map<uint32_t, uint32_t> lane_of;
-        int focus = -1;
+        std::vector<uint2> h_info;               // slot -> {Monotonic tag, local root}
+        std::vector<uint32_t> serial;            // slot -> heartbeats so far (the root's tag source)
+        std::vector<uint32_t> root_of;           // lane -> root (kNoPeer: never used)
+        std::unordered_map<uint32_t, uint32_t> lane_of;   // root -> lane, while it holds one
+        // Parked roots (psim_forest_set_lanes, lanes < cap): a root's records
+        // live in its state slot for good (vs: cap slots of 16 n bytes), while
+        // the per-lane slabs (inbox, flags, rows, counts: ~40 n bytes) exist
+        // for `lanes` roots at a time; a heartbeat takes a lane from a root
+        // whose own heartbeat is done.  lanes == 0: one lane per root, slot =
+        // lane (no indirection).  The extra lane `lanes` stays empty: the
+        // getters' view of a parked root (nothing in flight, no rows).
+        uint32_t lanes = 0;
+        uint32_t ns = 0;                         // slots holding a root
+        uint32_t* d_slot = nullptr;              // [lanes + 1] lane -> slot (device; parking only)
+        std::vector<uint32_t> h_slot;            // lane -> slot
+        std::vector<uint32_t> slot_root;         // slot -> root
+        std::unordered_map<uint32_t, uint32_t> slot_of;   // root -> slot
+        bool parking() const { return lanes != 0 && lanes < cap; }
+        uint32_t nlanes() const { return parking() ? lanes : cap; }   // lanes that run roots
+        uint32_t slabs() const { return parking() ? lanes + 1 : cap; }
+        uint32_t slot(uint32_t lane) const { return parking() ? h_slot[lane] : lane; }
+        int focus = -1;                          // focused lane; <= -2: parked slot -2 - focus
         uint32_t gx = 0;                         // workgroups per lane (PSIM_FOREST_GX A/B knob; 0: auto)
     } fo;
     void* scratch_buf = nullptr;   // growable device scratch for batched host-buffer ops
@@ -293,7 +310,7 @@ void free_forest(psim_handle* h) {
     h->ost = nullptr;
     h->ost_total = h->ost_total_base;
     void* fp[] = {f.vs, f.in[0], f.in[1], f.pend[0], f.pend[1], f.ost, f.ost_total, f.mcnt, f.info, f.d_list, f.d_busy,
-                  f.stage, f.xsend, f.xrecv, f.sb_d, f.rb_d, f.ring, f.pring};
+                  f.stage, f.xsend, f.xrecv, f.sb_d, f.rb_d, f.ring, f.pring, f.d_slot};
     for (void* x : fp)
         if (x) (void)hipFree(x);
     f.stage = f.xsend = f.xrecv = nullptr;
@@ -310,10 +327,15 @@ void free_forest(psim_handle* h) {
     f.mcnt = nullptr;
     f.info = nullptr;
     f.d_list = f.d_busy = nullptr;
+    f.d_slot = nullptr;
     f.nl = 0;
+    f.ns = 0;
     f.h_info.clear();
     f.root_of.clear();
     f.lane_of.clear();
+    f.h_slot.clear();
+    f.slot_root.clear();
+    f.slot_of.clear();
     f.focus = -1;
 }
 
@@ -1106,10 +1128,11 @@ int drive(psim_handle* h, uint32_t max_rounds, psim_round_stats* out, size_t cap
 // round is one launch over every lane, and nothing per lane crosses PCIe
 // per round (the counters of all lanes add into the round's one stats row).
 
-// bytes one lane takes in the slabs
+// bytes one lane takes in the slabs besides its root's records (16 n, one
+// state slot per root)
 uint64_t fo_lane_bytes(const psim_handle* h, uint64_t s_in) {
     const auto& f = h->fo;
-    uint64_t b = uint64_t(h->n) * 16 + 2 * s_in * 4 + 2 * f.s_pend + f.s_ost + 4 * sizeof(int) + kMcntLane * 4 + 8 + 8;
+    uint64_t b = 2 * s_in * 4 + 2 * f.s_pend + f.s_ost + 4 * sizeof(int) + kMcntLane * 4 + 8 + 8;
     if (h->sh.world > 1)        // staged words + the lane's share of the exchange buffers
         b += s_in * 4 + 4 * (h->sh.send_base[h->sh.world] + h->sh.recv_base[h->sh.world]);
     return b;
@@ -1122,21 +1145,24 @@ int forest_alloc(psim_handle* h) {
     const uint64_t s_in = (h->Ed + 63) & ~uint64_t(63);
     f.s_pend = (h->pend_bytes + 255) & ~uint64_t(255);
     f.s_ost = (uint64_t(h->n) + 4 + 255) & ~uint64_t(255);
-    const uint64_t per = fo_lane_bytes(h, s_in), total = per * f.cap;
+    const uint64_t C = f.slabs(), R = f.cap;    // lane slabs, state slots
+    const uint64_t per = fo_lane_bytes(h, s_in), per_root = uint64_t(h->n) * 16, total = per * C + per_root * R;
     size_t fr = 0, tot = 0;
     HIPCHK(h, hipMemGetInfo(&fr, &tot));
     if (total + (uint64_t(1) << 30) > fr)
-        return fail(h, PSIM_ENOMEM, "max_roots=%u needs %.2f GB of slabs (%.2f MB per root); %.2f GB free", f.cap,
-                    double(total) / 1e9, double(per) / 1e6, double(fr) / 1e9);
-    const uint64_t C = f.cap;
-    if (!alloc_zero((void**)&f.vs, C * h->n * 16) || !alloc_zero((void**)&f.in[0], C * s_in * 4) ||
+        return fail(h, PSIM_ENOMEM, "max_roots=%u over %u lanes needs %.2f GB of slabs (%.2f MB per root, %.2f MB per "
+                                    "lane); %.2f GB free", f.cap, f.nlanes(), double(total) / 1e9,
+                    double(per_root) / 1e6, double(per) / 1e6, double(fr) / 1e9);
+    const uint64_t L = std::max(C, R);          // lane / slot lists
+    if (!alloc_zero((void**)&f.vs, R * h->n * 16) || !alloc_zero((void**)&f.in[0], C * s_in * 4) ||
         !alloc_zero((void**)&f.in[1], C * s_in * 4) || !alloc_zero((void**)&f.pend[0], C * f.s_pend) ||
         !alloc_zero((void**)&f.pend[1], C * f.s_pend) || !alloc_zero((void**)&f.ost, C * f.s_ost) ||
         !alloc_zero((void**)&f.ost_total, C * 4 * sizeof(int)) || !alloc_zero((void**)&f.mcnt, C * kMcntLane * 4) ||
-        !alloc_zero((void**)&f.info, C * 8) || !alloc_zero((void**)&f.d_list, C * 4) ||
-        !alloc_zero((void**)&f.d_busy, C * 4)) {
+        !alloc_zero((void**)&f.info, R * 8) || !alloc_zero((void**)&f.d_list, L * 4) ||
+        !alloc_zero((void**)&f.d_busy, L * 4) || (f.parking() && !alloc_zero((void**)&f.d_slot, C * 4))) {
         free_forest(h);
-        return fail(h, PSIM_ENOMEM, "forest slabs for %u roots (%.2f GB)", f.cap, double(total) / 1e9);
+        return fail(h, PSIM_ENOMEM, "forest slabs for %u roots over %u lanes (%.2f GB)", f.cap, f.nlanes(),
+                    double(total) / 1e9);
     }
     if (h->sh.world > 1) {
         const auto& sh = h->sh;
@@ -1155,11 +1181,15 @@ int forest_alloc(psim_handle* h) {
     f.g_inflight = f.g_live = 0;
     f.s_in = s_in;
     f.nl = 0;
+    f.ns = 0;
     f.focus = -1;
     f.h_info.assign(f.cap, make_uint2(0u, 0u));
     f.serial.assign(f.cap, 0u);
-    f.root_of.clear();
+    f.root_of.assign(C, kNoPeer);
     f.lane_of.clear();
+    f.h_slot.assign(C, 0u);
+    f.slot_root.clear();
+    f.slot_of.clear();
     return PSIM_OK;
 }
 
@@ -1201,6 +1231,8 @@ FoArgs forest_args(const psim_handle* h, uint32_t par, uint32_t tick, unsigned l
     fa.s_ost = f.s_ost;
     fa.info = f.info;
     fa.nl = f.nl;
+    fa.ns = f.ns;
+    fa.slot = f.parking() ? f.d_slot : nullptr;
     fa.a.stage = f.stage;                      // null on one GPU
     fa.s_stage = f.s_stage;
     if (h->dly) {
@@ -1270,11 +1302,12 @@ int forest_globals(psim_handle* h) {
     return PSIM_OK;
 }
 
-// The getters' view: the handle's single-lane fields alias lane `lane`.
-void forest_focus(psim_handle* h, int lane) {
+// The getters' view: the handle's single-lane fields alias lane `lane`
+// (its root's records in the root's state slot).
+void forest_view(psim_handle* h, uint32_t lane, uint32_t slot) {
     auto& f = h->fo;
     const uint64_t l = uint64_t(lane);
-    h->vs = f.vs + l * h->n;
+    h->vs = f.vs + uint64_t(slot) * h->n;
     for (int b = 0; b < 2; b++) {
         h->in[b] = f.in[b] + l * f.s_in;
         h->pend[b] = f.pend[b] + l * f.s_pend;
@@ -1285,15 +1318,36 @@ void forest_focus(psim_handle* h, int lane) {
         h->ring = f.ring + l * f.s_ring;
         h->pring = f.pring + l * f.s_pring;
     }
-    h->serial = f.serial[lane];
-    h->root = f.root_of[lane];
+    h->serial = f.serial[slot];
     h->have_root = true;
+}
+
+void forest_focus(psim_handle* h, int lane) {
+    auto& f = h->fo;
+    forest_view(h, uint32_t(lane), f.slot(uint32_t(lane)));
+    h->root = f.root_of[lane];
     f.focus = lane;
+}
+
+// A parked root: its records, and the empty lane's (nothing in flight, no rows).
+void forest_focus_parked(psim_handle* h, uint32_t slot) {
+    auto& f = h->fo;
+    forest_view(h, f.lanes, slot);
+    h->root = f.slot_root[slot];
+    f.focus = -2 - int(slot);
+}
+
+void forest_refocus(psim_handle* h) {
+    auto& f = h->fo;
+    if (f.focus >= 0) forest_focus(h, f.focus);
+    else if (f.focus <= -2) forest_focus_parked(h, uint32_t(-2 - f.focus));
 }
 
 int forest_upload_info(psim_handle* h) {
     auto& f = h->fo;
-    if (f.nl) HIPCHK(h, hipMemcpyAsync(f.info, f.h_info.data(), size_t(f.nl) * 8, hipMemcpyHostToDevice, h->stream));
+    if (f.ns) HIPCHK(h, hipMemcpyAsync(f.info, f.h_info.data(), size_t(f.ns) * 8, hipMemcpyHostToDevice, h->stream));
+    if (f.parking() && f.nl)
+        HIPCHK(h, hipMemcpyAsync(f.d_slot, f.h_slot.data(), size_t(f.nl) * 4, hipMemcpyHostToDevice, h->stream));
     return PSIM_OK;
 }
 
@@ -1326,19 +1380,22 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
     if (!k) return PSIM_OK;
     if (!roots) return PSIM_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
-    std::vector<uint32_t> lanes(k), old;
+    std::vector<uint32_t> lanes(k), slots(k), old;
     std::unordered_map<uint32_t, int> seen;
-    uint32_t fresh = 0;
+    uint32_t fresh = 0, need = 0;
     const bool sharded = h->sh.world > 1;       // collective: every rank passes the same roots
     if (sharded && !h->sh.xport) return fail(h, PSIM_ESTATE, "sharded forest without a transport");
     for (size_t i = 0; i < k; i++) {
         if (roots[i] >= h->sh.n_global) return fail(h, PSIM_EINVAL, "root %u >= n", roots[i]);
         if (!seen.emplace(roots[i], 1).second)
             return fail(h, PSIM_EINVAL, "root %u heartbeats twice in one call", roots[i]);
+        const auto is = f.slot_of.find(roots[i]);
+        slots[i] = is == f.slot_of.end() ? kNoPeer : is->second;
+        if (slots[i] == kNoPeer) fresh++;
         const auto it = f.lane_of.find(roots[i]);
         if (it == f.lane_of.end()) {
             lanes[i] = kNoPeer;
-            fresh++;
+            need++;
         } else {
             lanes[i] = it->second;
             old.push_back(it->second);
@@ -1346,24 +1403,26 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
         const int rc = next_mono(h, roots[i], nullptr, false);
         if (rc) return rc;
     }
-    if (uint64_t(f.nl) + fresh > f.cap)
-        return fail(h, PSIM_ENOSPC, "%u roots hold trees, %u new ones exceed max_roots=%u", f.nl, fresh, f.cap);
-    if (!old.empty() && h->dly) {
-        // delay faults: no per-lane counts; a root heartbeats again once no
-        // delayed message is pending anywhere and its lane holds no rows
-        std::vector<int> tot(size_t(f.cap) * 4);
-        HIPCHK(h, hipMemcpyAsync(tot.data(), f.ost_total, tot.size() * sizeof(int), hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        for (uint32_t l : old)
-            if (h->inflight != 0 || tot[4 * size_t(l)] != 0)
-                return fail(h, PSIM_EBUSY, "root %u: messages are in flight or its lane holds rows (delay faults: a "
-                                           "forest root heartbeats again once nothing is pending)", f.root_of[l]);
-    } else if (!old.empty()) {                   // every heartbeating root's last one is done
+    if (uint64_t(f.ns) + fresh > f.cap)
+        return fail(h, PSIM_ENOSPC, "%u roots hold trees, %u new ones exceed max_roots=%u", f.ns, fresh, f.cap);
+    // lanes busy with their root's heartbeat: messages of the last round (count
+    // slot round % 4, origins included) or rows held (delay faults: anything
+    // pending anywhere, or rows held)
+    auto busy_lanes = [&](const std::vector<uint32_t>& ls, std::vector<uint32_t>& busy) -> int {
+        busy.assign(ls.size(), 0u);
+        if (ls.empty()) return PSIM_OK;
+        if (h->dly) {
+            std::vector<int> tot(size_t(f.slabs()) * 4);
+            HIPCHK(h, hipMemcpyAsync(tot.data(), f.ost_total, tot.size() * sizeof(int), hipMemcpyDeviceToHost,
+                                     h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            for (size_t i = 0; i < ls.size(); i++) busy[i] = (h->inflight != 0 || tot[4 * size_t(ls[i])] != 0);
+            return PSIM_OK;
+        }
         FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
-        HIPCHK(h, hipMemcpyAsync(f.d_list, old.data(), old.size() * 4, hipMemcpyHostToDevice, h->stream));
-        HIPCHK(h, launch_fo_busy(fa, f.d_list, uint32_t(old.size()), uint32_t(h->round % 4), f.d_busy, h->stream));
-        std::vector<uint32_t> busy(old.size());
-        HIPCHK(h, hipMemcpyAsync(busy.data(), f.d_busy, old.size() * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(f.d_list, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, launch_fo_busy(fa, f.d_list, uint32_t(ls.size()), uint32_t(h->round % 4), f.d_busy, h->stream));
+        HIPCHK(h, hipMemcpyAsync(busy.data(), f.d_busy, ls.size() * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         if (sharded) {                            // busy on any shard
             std::vector<int64_t> b(busy.begin(), busy.end());
@@ -1372,23 +1431,58 @@ int forest_broadcast(psim_handle* h, const uint32_t* roots, size_t k, uint32_t* 
             if (rc) return fail(h, rc, "forest busy all-reduce: %s", err.c_str());
             for (size_t i = 0; i < b.size(); i++) busy[i] = b[i] != 0;
         }
+        return PSIM_OK;
+    };
+    {                                             // every heartbeating root's last one is done
+        std::vector<uint32_t> busy;
+        const int rc = busy_lanes(old, busy);
+        if (rc) return rc;
         for (size_t i = 0; i < old.size(); i++)
             if (busy[i])
-                return fail(h, PSIM_EBUSY, "root %u: its last heartbeat is in flight or holds rows (a forest keeps one "
-                                           "heartbeat per root)", f.root_of[old[i]]);
+                return fail(h, PSIM_EBUSY, h->dly ? "root %u: messages are in flight or its lane holds rows (delay "
+                                                    "faults: a forest root heartbeats again once nothing is pending)"
+                                                  : "root %u: its last heartbeat is in flight or holds rows (a forest "
+                                                    "keeps one heartbeat per root)", f.root_of[old[i]]);
     }
-    std::vector<uint32_t> wrap, own;            // own: lanes whose root this shard holds (all on one GPU)
+    // lanes for the roots without one: never-used lanes, then (parked roots)
+    // lanes whose root's heartbeat is done -- that root keeps its records in
+    // its slot and gives the lane up
+    std::vector<uint32_t> freel;
+    for (uint32_t l = f.nl; l < f.nlanes() && freel.size() < need; l++) freel.push_back(l);
+    if (freel.size() < need && f.parking()) {
+        std::vector<uint32_t> cand, busy;
+        for (uint32_t l = 0; l < f.nl; l++)
+            if (!seen.count(f.root_of[l])) cand.push_back(l);
+        const int rc = busy_lanes(cand, busy);
+        if (rc) return rc;
+        for (size_t i = 0; i < cand.size() && freel.size() < need; i++)
+            if (!busy[i]) freel.push_back(cand[i]);
+    }
+    if (freel.size() < need)
+        return fail(h, PSIM_ENOSPC, "%u heartbeats need a lane and %zu are free: %u lanes, the others' heartbeats are "
+                                    "in flight or hold rows (max_roots=%u)", need, freel.size(), f.nlanes(), f.cap);
+    std::vector<uint32_t> wrap, own;            // wrap: slots; own: lanes whose root this shard holds
+    size_t fi = 0;
     for (size_t i = 0; i < k; i++) {
-        if (lanes[i] == kNoPeer) {
-            lanes[i] = f.nl++;
-            f.root_of.push_back(roots[i]);
-            f.lane_of[roots[i]] = lanes[i];
+        if (slots[i] == kNoPeer) {
+            slots[i] = f.ns++;
+            f.slot_of[roots[i]] = slots[i];
+            f.slot_root.push_back(roots[i]);
         }
-        const uint32_t l = lanes[i];
-        f.serial[l]++;
-        if ((f.serial[l] & 0x7Fu) == 0) wrap.push_back(l);
+        if (lanes[i] == kNoPeer) {
+            const uint32_t l = freel[fi++];
+            if (l >= f.nl) f.nl = l + 1;
+            else f.lane_of.erase(f.root_of[l]);   // its root is parked from now on
+            lanes[i] = l;
+            f.root_of[l] = roots[i];
+            f.lane_of[roots[i]] = l;
+            f.h_slot[l] = slots[i];
+        }
+        const uint32_t l = lanes[i], sl = slots[i];
+        f.serial[sl]++;
+        if ((f.serial[sl] & 0x7Fu) == 0) wrap.push_back(sl);
         const uint32_t lr = roots[i] - h->sh.v_lo;  // the origin's local index on its owner
-        f.h_info[l] = make_uint2(f.serial[l] & 0xFFu, lr < h->n ? lr : kNoPeer);
+        f.h_info[sl] = make_uint2(f.serial[sl] & 0xFFu, lr < h->n ? lr : kNoPeer);
         if (lr < h->n) own.push_back(l);
         uint32_t mono = 0;
         (void)next_mono(h, roots[i], &mono, true);
@@ -1446,7 +1540,7 @@ int forest_scrub_if_needed(psim_handle* h, uint64_t last) {
 
 int forest_renorm_all(psim_handle* h) {
     FoArgs fa = forest_args(h, h->par, 0, h->stats, h->round + 1);
-    HIPCHK(h, launch_fo_renorm(fa, nullptr, h->fo.nl, h->stream));
+    HIPCHK(h, launch_fo_renorm(fa, nullptr, h->fo.ns, h->stream));   // every root's records, parked or not
     return PSIM_OK;
 }
 
@@ -3671,12 +3765,26 @@ int psim_vclock_get_counter(psim_handle* h, const uint32_t* a, const uint32_t* a
     return vc_op(h, 7, a, nullptr, actor, out, nullptr, n);
 }
 
+int psim_forest_set_lanes(psim_handle* h, uint32_t lanes) {
+    if (!h) return PSIM_EINVAL;
+    if (!h->fo.on) return fail(h, PSIM_ESTATE, "not a forest (psim_config.max_roots <= 16)");
+    if (h->n) return fail(h, PSIM_ESTATE, "set the forest's lanes before psim_load_csr");
+    if (lanes > h->fo.cap) return fail(h, PSIM_EINVAL, "lanes=%u > max_roots=%u", lanes, h->fo.cap);
+    h->fo.lanes = lanes;
+    return PSIM_OK;
+}
+
 int psim_plumtree_focus(psim_handle* h, uint32_t root) {
     if (!h || !h->n) return PSIM_ESTATE;
     if (h->fo.on) {
         const auto it = h->fo.lane_of.find(root);
-        if (it == h->fo.lane_of.end()) return fail(h, PSIM_EINVAL, "root %u has no heartbeat lane", root);
-        forest_focus(h, int(it->second));
+        if (it != h->fo.lane_of.end()) {
+            forest_focus(h, int(it->second));
+            return PSIM_OK;
+        }
+        const auto is = h->fo.slot_of.find(root);   // a parked root: its records, nothing in flight
+        if (is == h->fo.slot_of.end()) return fail(h, PSIM_EINVAL, "root %u has no heartbeat tree", root);
+        forest_focus_parked(h, is->second);
         return PSIM_OK;
     }
     if (!lanes_enabled(h)) return h->have_root && h->root == root ? PSIM_OK : PSIM_EINVAL;
@@ -3788,18 +3896,19 @@ int psim_set_delays(psim_handle* h, const uint32_t* src, const uint32_t* dst, co
             f.s_pring = (uint64_t(kRing) * ng + 255) & ~uint64_t(255);
             size_t fr = 0, tot = 0;
             HIPCHK(h, hipMemGetInfo(&fr, &tot));
-            const uint64_t need = uint64_t(f.cap) * (f.s_ring * 4 + f.s_pring);
+            const uint64_t need = uint64_t(f.slabs()) * (f.s_ring * 4 + f.s_pring);
             if (need + (uint64_t(1) << 30) > fr ||
-                !alloc_zero((void**)&f.ring, uint64_t(f.cap) * f.s_ring * 4) ||
-                !alloc_zero((void**)&f.pring, uint64_t(f.cap) * f.s_pring)) {
+                !alloc_zero((void**)&f.ring, uint64_t(f.slabs()) * f.s_ring * 4) ||
+                !alloc_zero((void**)&f.pring, uint64_t(f.slabs()) * f.s_pring)) {
                 if (f.ring) (void)hipFree(f.ring);
                 f.ring = nullptr;
                 (void)hipFree(h->dly);
                 h->dly = nullptr;
-                return fail(h, PSIM_ENOMEM, "forest delay rings: %.2f GB for %u roots", double(need) / 1e9, f.cap);
+                return fail(h, PSIM_ENOMEM, "forest delay rings: %.2f GB for %u lanes", double(need) / 1e9,
+                            f.slabs());
             }
             for (auto& x : h->due) x = 0;
-            if (f.focus >= 0) forest_focus(h, f.focus);
+            forest_refocus(h);
         }
         if (!h->lanes.empty()) load_lane(h, focus);
     }

@@ -287,8 +287,13 @@ struct FoArgs {
     PtArgs a;                              // this round's arguments at lane 0's slices
     uint64_t s_vs, s_in, s_pend, s_ost;    // per-lane strides: uint4 records, u32 words, bytes, bytes
     uint64_t s_stage;                      // sharded forest: u32 staged words per lane (a.stage = lane 0's)
-    const uint2* __restrict__ info;        // [lanes] {Monotonic tag (low 8 bits), local root}
+    const uint2* __restrict__ info;        // [slots] {Monotonic tag (low 8 bits), local root}
     uint32_t lane0, nl;                    // this launch: lanes [lane0, lane0 + gridDim.y) of [0, nl)
+    // parked roots (psim_forest_set_lanes): a root's per-root records (vs, its
+    // state slot) outlive its lane; lane L runs the root whose slot is
+    // slot[L].  Null: slot = lane (every root keeps its lane for good).
+    const uint32_t* __restrict__ slot;     // [lanes] state slot of each lane's root
+    uint32_t ns;                           // slots holding a root (= nl without parking)
 };
 // one round over lanes [0, f.nl): gx workgroups per lane (0: the round kernel's own choice)
 hipError_t launch_fo_round(FoArgs f, uint32_t gx, hipStream_t s);
@@ -299,8 +304,8 @@ hipError_t launch_fo_busy(const FoArgs& f, const uint32_t* lanes, uint32_t k, ui
                           hipStream_t s);
 // every lane's row-holder ring from its exact count (a.m_r, a.m_s as PtArgs)
 hipError_t launch_fo_seed(const FoArgs& f, hipStream_t s);
-// tag re-base of lanes[0, k) (lanes == null: all f.nl lanes)
-hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* lanes, uint32_t k, hipStream_t s);
+// tag re-base of state slots slots[0, k) (slots == null: slots [0, k))
+hipError_t launch_fo_renorm(const FoArgs& f, const uint32_t* slots, uint32_t k, hipStream_t s);
 // outstanding rows to live peers over every lane -> *out (added)
 hipError_t launch_fo_count_live(const FoArgs& f, unsigned long long* out, hipStream_t s);
 // sharded forest: every lane's staged remote words -> the dense send regions
@@ -312,7 +317,7 @@ hipError_t launch_fo_pack_dense(FoArgs f, const uint32_t* rem, uint32_t nrem, co
 hipError_t launch_fo_ingest_dense(FoArgs f, const uint32_t* recv, const uint32_t* recv_map, uint32_t nrecv,
                                   const uint64_t* rb, uint32_t world, const uint32_t* slot2v, int fixed_mark,
                                   hipStream_t s);
-// a backend restart at local vertex v: v forgets every origin (each lane's delivered tag)
+// a backend restart at local vertex v: v forgets every origin (each slot's delivered tag)
 hipError_t launch_fo_forget(const FoArgs& f, uint32_t v, hipStream_t s);
 
 // Demers rumor mongering + anti-entropy (demers.hip)

@@ -62,7 +62,7 @@ def gloo_transport():
 
 class ShardedPlumtree:
     def __init__(self, row_ptr, col, rank, world, device=0, backend="nccl", lazy_tick_rounds=1, transport=None,
-                 csr=False, chunk_timing=False, max_roots=0):
+                 csr=False, chunk_timing=False, max_roots=0, forest_lanes=0):
         """csr: keep CSR slot rows (PSIM_CFG_CSR) instead of the ELL rows every
         shard uses when the overlay's widest row has <= 8 slots.  chunk_timing:
         psim_shard_run times each 4-round chunk with one event pair and puts no
@@ -77,7 +77,7 @@ class ShardedPlumtree:
         # it finds no device (torch ships its own libamdhip64)
         torch.cuda.set_device(self.dev)
         self.sim = Simulator(lazy_tick_rounds=lazy_tick_rounds, device=device, rank=rank, world=world, csr=csr,
-                             chunk_timing=chunk_timing, max_roots=max_roots)
+                             chunk_timing=chunk_timing, max_roots=max_roots, forest_lanes=forest_lanes)
         self._h = self.sim._h
         self.last_exchange = {}
         self.exchange_total = {}      # psim_exchange_stats summed over runs (this rank)

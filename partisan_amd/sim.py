@@ -27,7 +27,7 @@ class Simulator:
     """Round-synchronous simulator of Partisan's gossip hot path."""
 
     def __init__(self, lazy_tick_rounds=1, exchange_tick_rounds=10, device=-1, seed=0, rank=0, world=1,
-                 binned=False, csr=False, chunk_timing=False, max_roots=0):
+                 binned=False, csr=False, chunk_timing=False, max_roots=0, forest_lanes=0):
         """binned: route Plumtree messages through receiver bins on a single
         GPU instead of scattering receiver-slot words (PSIM_CFG_BINNED; same
         results).  csr: keep CSR slot rows in the slot-scatter
@@ -37,7 +37,9 @@ class Simulator:
         max_roots: heartbeat roots whose per-root trees the handle keeps
         (psim_config.max_roots; 0 = 16 lanes).  Above 16 the roots live in one
         forest launched together; a root beyond max_roots is
-        PSIM_ENOSPC."""
+        PSIM_ENOSPC.  forest_lanes (< max_roots): lanes for heartbeats in
+        flight; every root's records are kept, a done root's lane is reused
+        (psim_forest_set_lanes; 0 = one lane per root)."""
         flags = ((PSIM_CFG_BINNED if binned else 0) | (PSIM_CFG_CSR if csr else 0)
                  | (PSIM_CFG_CHUNK_TIMING if chunk_timing else 0))
         cfg = Config(abi_version=PSIM_ABI_VERSION, device=device, lazy_tick_rounds=lazy_tick_rounds,
@@ -49,6 +51,8 @@ class Simulator:
         self.binned = binned
         self.lazy_tick_rounds = lazy_tick_rounds
         self.rank, self.world = rank, world
+        if forest_lanes:
+            check(lib().psim_forest_set_lanes(h, forest_lanes), h)
         if world > 1:
             check(lib().psim_shard_init(h, rank, world), h)
 

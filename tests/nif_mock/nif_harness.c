@@ -148,6 +148,26 @@ int main(int argc, char** argv) {
             want_ok_tuple("run", call("run", 2, A(fs, mock_uint(1000))));
             fprintf(g_out, ", \"forest\": {\"roots\": %u, \"rounds\": [%llu, %llu], \"delivered\": %llu}", n,
                     (unsigned long long)fr[0], (unsigned long long)fr[1], (unsigned long long)fdl);
+            /* parked roots: the same n roots' records through 16 lanes, 16 heartbeats at a time
+             * (forest_lanes => psim_forest_set_lanes); 17 at once is {error, enospc} */
+            const char* kp[] = {"seed", "lazy_tick_rounds", "device", "max_roots", "forest_lanes"};
+            const uint64_t vp[] = {0x5EED0002ull, 1, 0, n, 16};
+            ERL_NIF_TERM ps = mock_elem(want_ok_tuple("new", call("new", 1, A(mock_map(5, kp, vp)))), 1);
+            want_ok("load_csr", call("load_csr", 3, A(ps, mock_bin(rp, (n + 1) * 8), u32s(col, e))));
+            ERL_NIF_TERM over = call("broadcast_many", 2, A(ps, u32s(roots, 17)));
+            const int enospc = mock_tuple_arity(over) == 2 && mock_is_atom(mock_elem(over, 0), "error") &&
+                               mock_is_atom(mock_elem(over, 1), "enospc");
+            uint64_t pdl = 0;
+            for (uint32_t b = 0; b < n; b += 16) {
+                const uint32_t k16 = n - b < 16 ? n - b : 16;
+                want_ok_tuple("broadcast_many", call("broadcast_many", 2, A(ps, u32s(roots + b, k16))));
+                ERL_NIF_TERM pr = want_ok_tuple("run", call("run", 2, A(ps, mock_uint(1000))));
+                ERL_NIF_TERM pst = mock_elem(pr, 2);
+                for (size_t i = 0; i < mock_list_len(pst); i++)
+                    if (mock_map_get(mock_list_nth(pst, i), "delivered", &x)) pdl += x;
+            }
+            fprintf(g_out, ", \"parked\": {\"roots\": %u, \"lanes\": 16, \"delivered\": %llu, \"enospc\": %d}", n,
+                    (unsigned long long)pdl, enospc);
             free(roots);
         }
         {   /* window-lane-era getters on the static lane: every vertex delivered this Monotonic, nothing in flight */

@@ -27,7 +27,7 @@ from test_shard import ROOT, _init, run_world
 KINDS = ("broadcast", "prune", "i_have", "ignored_i_have", "graft")
 
 
-def _forest_worker(rank, world, port, n, seed, L, q):
+def _forest_worker(rank, world, port, n, seed, L, q, lanes=0):
     try:
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -37,7 +37,7 @@ def _forest_worker(rank, world, port, n, seed, L, q):
         import pyoracle as O
         rp, col = pa.overlay.random_regular(n, 5, seed)
         sp = ShardedPlumtree(rp, col, rank, world, device=0, backend="gloo", lazy_tick_rounds=L,
-                             transport="callback", max_roots=n)
+                             transport="callback", max_roots=n, forest_lanes=lanes)
         sim = sp.sim
         lo, hi = sim.v_lo, sim.v_lo + sim.n
         g = pa.Simulator(lazy_tick_rounds=L, device=0)      # the global slot layout (rows sorted by id)
@@ -86,6 +86,24 @@ def _forest_worker(rank, world, port, n, seed, L, q):
         assert ei.value.name == "PSIM_ENOTSUP"
         roots = list(range(n))
         monos = {}
+        if lanes:
+            # parked roots (psim_forest_set_lanes): every root through `lanes`
+            # lanes, a batch at a time, twice (the second interval in reverse
+            # order, from the records each root kept while parked)
+            for interval in range(2):
+                order = roots if interval == 0 else roots[::-1]
+                for b in range(0, n, lanes):
+                    batch = order[b:b + lanes]
+                    got = sp.broadcast_many(batch)
+                    for r, m in zip(batch, got):
+                        monos[r] = orc.heartbeat(r)
+                        assert m == monos[r]
+                    lockstep(monos, batch, full_every=6)
+                compare(monos, roots)
+            sp.close()
+            dist.destroy_process_group()
+            q.put((rank, "ok"))
+            return
         for interval in range(2):
             got = sp.broadcast_many(roots)
             for r in roots:
@@ -125,6 +143,21 @@ def _forest_worker(rank, world, port, n, seed, L, q):
 def test_sharded_forest_all_roots_lockstep(world, n, seed, L):
     res = run_world(_forest_worker, world, n, seed, L)
     for r in range(world):
+        assert res[r] == "ok", res[r]
+
+
+def _parked_worker(rank, world, port, n, seed, L, q):
+    _forest_worker(rank, world, port, n, seed, L, q, lanes=16)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_sharded_parked_forest_lockstep():
+    """Parked roots on a sharded forest (world 2, n = 600, 16 lanes): the
+    lanes' busy test and reuse agree on every rank (one all-reduce), and the
+    result is the oracle's round by round."""
+    res = run_world(_parked_worker, 2, 600, 3, 1)
+    for r in range(2):
         assert res[r] == "ok", res[r]
 
 

@@ -136,6 +136,8 @@ def test_nif_harness_on_gpu(tmp_path):
     # the forest through the NIF: every root of the C2 overlay heartbeats, twice
     assert rep["forest"]["roots"] == n and rep["forest"]["delivered"] == n * (n - 1), rep["forest"]
     assert all(r > 0 for r in rep["forest"]["rounds"])
+    # parked roots through the NIF (forest_lanes): every root's flood, 16 lanes at a time
+    assert rep["parked"]["delivered"] == n * (n - 1) and rep["parked"]["enospc"] == 1, rep["parked"]
 
     # the same C2 through the Python binding of the same ABI: bit-identical
     import partisan_amd as pa
