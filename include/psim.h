@@ -760,6 +760,16 @@ int  psim_c3_crash(psim_handle* h, const uint32_t* v, size_t k);
 /* heartbeat at `root` (backend :341-368 -> broadcast :565-569) */
 int  psim_c3_heartbeat(psim_handle* h, uint32_t root, uint32_t* mono_out);
 int  psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* stats, size_t cap);
+/* `rounds` rounds of churn in one call: round i is the heartbeat at hb_root
+ * when hb_every != 0 and i % hb_every == 0, then crash of
+ * crash_v[crash_off[i] .. crash_off[i+1]), join of join_v / join_c over
+ * [join_off[i], join_off[i+1]), then one psim_c3_step round -- the same
+ * calls and the same result as making them one by one, without the host
+ * waiting for the device between rounds (offsets: rounds + 1 entries each).
+ * stats[i] is round i's; the first failing round's error is returned. */
+int  psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, const uint32_t* crash_v,
+                 const uint32_t* join_off, const uint32_t* join_v, const uint32_t* join_c, uint32_t hb_every,
+                 uint32_t hb_root, psim_c3_stats* stats, size_t cap);
 /* vertex v's Plumtree state: all_eager_peers / all_lazy_peers / outstanding
  * rows (sorted ids, up to cap each), the heartbeat serial it delivered (0 =
  * none) and its pushed Round */

@@ -294,6 +294,8 @@ SIGNATURES = {
     "psim_c3_crash": (C.c_int, [_H, _P(C.c_uint32), C.c_size_t]),
     "psim_c3_heartbeat": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32)]),
     "psim_c3_step": (C.c_int, [_H, C.c_uint32, _P(C3Stats), C.c_size_t]),
+    "psim_c3_run": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32),
+                              _P(C.c_uint32), C.c_uint32, C.c_uint32, _P(C3Stats), C.c_size_t]),
     "psim_c3_get_plumtree": (C.c_int, [_H, C.c_uint32, _P(C.c_uint32), _P(C.c_size_t), _P(C.c_uint32),
                                        _P(C.c_size_t), _P(C.c_uint32), _P(C.c_size_t), C.c_size_t,
                                        _P(C.c_uint32), _P(C.c_uint32)]),

@@ -48,6 +48,31 @@ class C3Cluster:
         self._c(lib().psim_c3_step(self.sim._h, rounds, st, rounds))
         return [s.as_dict() for s in st]
 
+    def run(self, crashes, joins, heartbeat_every=0, root=0):
+        """Rounds of churn in one call (psim_c3_run): round i = heartbeat at
+        `root` when heartbeat_every and i % heartbeat_every == 0, crash of
+        crashes[i], join of joins[i] = (vertices, contacts), one step -- the
+        same as those calls one by one, with no host wait between rounds."""
+        rounds = len(crashes)
+        if len(joins) != rounds:
+            raise ValueError("one crash list and one join list per round")
+
+        def flat(parts):
+            off = np.zeros(rounds + 1, np.uint32)
+            off[1:] = np.cumsum([len(np.atleast_1d(x)) for x in parts])
+            v = np.concatenate([np.atleast_1d(x).astype(np.uint32) for x in parts] or [np.zeros(0, np.uint32)])
+            return off, np.ascontiguousarray(v, dtype=np.uint32)
+
+        co, cv = flat(crashes)
+        jo, jv = flat([j[0] for j in joins])
+        _, jc = flat([j[1] for j in joins])
+        u32 = _P(C.c_uint32)
+        st = (C3Stats * max(rounds, 1))()
+        self._c(lib().psim_c3_run(self.sim._h, rounds, co.ctypes.data_as(u32), cv.ctypes.data_as(u32),
+                                  jo.ctypes.data_as(u32), jv.ctypes.data_as(u32), jc.ctypes.data_as(u32),
+                                  heartbeat_every, root, st, rounds))
+        return [s.as_dict() for s in st[:rounds]]
+
     def plumtree(self, v, cap=128):
         """(eager, lazy, outstanding) sorted ids, delivered heartbeat serial, pushed Round."""
         e, l_, o = (C.c_uint32 * cap)(), (C.c_uint32 * cap)(), (C.c_uint32 * cap)()

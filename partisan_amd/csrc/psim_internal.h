@@ -587,6 +587,11 @@ int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k);
 // errors raised) -- psim_c3_step waits once for both engines' rounds
 int scamp_round_launch(psim_handle* h);
 int scamp_round_finish(psim_handle* h, psim_scamp_stats* out);
+// psim_c3_run: a round launched with its stats rows copied to `dst` (pinned,
+// kRoundStatShards * 16 u64) between events e0 / e1, the host's round count
+// advanced at once (*round = its number); reported later from those rows
+int scamp_round_launch_to(psim_handle* h, unsigned long long* dst, hipEvent_t e0, hipEvent_t e1, uint64_t* round);
+int scamp_round_report(psim_handle* h, const unsigned long long* rows, float ms, uint64_t round, psim_scamp_stats* out);
 hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);
 

@@ -564,11 +564,18 @@ struct PdState : ModuleState {
     uint32_t par = 0;
     uint64_t round = 0;
     unsigned long long* h_stats = nullptr;   // pinned: a round's stats rows
+    // psim_c3_run: pinned stats rows of every round of one call (heartbeat,
+    // SCAMP, Plumtree) and four timing events per round
+    unsigned long long* h_run = nullptr;
+    size_t h_run_rounds = 0;
+    std::vector<hipEvent_t> run_ev;
     ~PdState() override {
         void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum};
         for (void* x : p)
             if (x) (void)hipFree(x);
         if (h_stats) (void)hipHostFree(h_stats);
+        if (h_run) (void)hipHostFree(h_run);
+        for (hipEvent_t e : run_ev) (void)hipEventDestroy(e);
     }
 };
 
@@ -699,6 +706,23 @@ int psim_c3_heartbeat(psim_handle* h, uint32_t root, uint32_t* mono_out) {
     return pd_check(h, r[9], s->round);
 }
 
+// psim_c3_run: the per-round counters of a Plumtree round from its stats rows
+static void pd_fill(const PdState& s, const unsigned long long* r, float ms, psim_c3_stats* o) {
+    for (int k = 1; k <= 5; k++) o->pt_sent[k] = r[k];
+    o->pt_sent[0] = 0;
+    o->pt_dropped = r[6];
+    o->delivered_new = r[7];
+    o->active = r[8];
+    o->updates = r[10];
+    o->delivered_live = r[11];
+    o->live = r[12];
+    o->outstanding_live = r[13];
+    uint64_t msgs = 0;
+    for (int k = 1; k <= 5; k++) msgs += r[k];
+    o->pt_algo_bytes = 48ull * msgs + 24ull * msgs + 12ull * s.n + 64ull * r[12];
+    o->pt_kernel_ms = ms;
+}
+
 int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap) {
     if (!h) return PSIM_EINVAL;
     PdState* s = pd_of(h);
@@ -745,21 +769,113 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
         s->round++;
         rc = pd_check(h, r[9], s->round);
         if (rc) return rc;
-        if (o) {
-            for (int k = 1; k <= 5; k++) o->pt_sent[k] = r[k];
-            o->pt_sent[0] = 0;
-            o->pt_dropped = r[6];
-            o->delivered_new = r[7];
-            o->active = r[8];
-            o->updates = r[10];
-            o->delivered_live = r[11];
-            o->live = r[12];
-            o->outstanding_live = r[13];
-            uint64_t msgs = 0;
-            for (int k = 1; k <= 5; k++) msgs += r[k];
-            o->pt_algo_bytes = 48ull * msgs + 24ull * msgs + 12ull * s->n + 64ull * r[12];
-            o->pt_kernel_ms = ms;
+        if (o) pd_fill(*s, r, ms, o);
+    }
+    return PSIM_OK;
+}
+
+// Rounds of churn in one call (include/psim.h): round i is, in this order,
+// the heartbeat at hb_root when hb_every && i % hb_every == 0, the crash list
+// crash_v[crash_off[i], crash_off[i+1]), the joins join_v / join_c over
+// [join_off[i], join_off[i+1]), then one psim_c3_step round -- exactly the
+// calls psim_c3_heartbeat / crash / join / step would make, enqueued on the
+// handle's stream with no wait between rounds: each round's stats rows go to
+// a pinned row of their own and are read, checked and reported after one
+// wait at the end (the first failing round's error is returned, as the
+// per-round calls would have; the handle's C3 state is then spent).
+int psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, const uint32_t* crash_v,
+                const uint32_t* join_off, const uint32_t* join_v, const uint32_t* join_c, uint32_t hb_every,
+                uint32_t hb_root, psim_c3_stats* out, size_t cap) {
+    if (!h || (rounds && (!crash_off || !join_off))) return PSIM_EINVAL;
+    PdState* s = pd_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
+    if (hb_every && hb_root >= s->n) return handle_fail(h, PSIM_EINVAL, "heartbeat root %u >= n %u", hb_root, s->n);
+    for (uint32_t i = 0; i < rounds; i++) {
+        if (crash_off[i + 1] < crash_off[i] || join_off[i + 1] < join_off[i])
+            return handle_fail(h, PSIM_EINVAL, "round %u: decreasing list offsets", i);
+        if ((crash_off[i + 1] > crash_off[i] && !crash_v) || (join_off[i + 1] > join_off[i] && (!join_v || !join_c)))
+            return PSIM_EINVAL;
+    }
+    const hipStream_t st = handle_stream(h);
+    constexpr size_t kSc = kRoundStatShards * 16, kPd = kRoundStatShards * kPdNStat;   // u64 per stats row
+    constexpr size_t kRow = 2 * kPd + kSc;                                               // heartbeat, SCAMP, Plumtree
+    if (rounds > s->h_run_rounds) {
+        if (s->h_run) (void)hipHostFree(s->h_run);
+        s->h_run = nullptr;
+        s->h_run_rounds = 0;
+        if (hipHostMalloc((void**)&s->h_run, size_t(rounds) * kRow * 8) != hipSuccess) {
+            s->h_run = nullptr;
+            return handle_fail(h, PSIM_ENOMEM, "c3: pinned stats rows for %u rounds", rounds);
         }
+        s->h_run_rounds = rounds;
+    }
+    while (s->run_ev.size() < 4ull * rounds) {
+        hipEvent_t e;
+        PDCHK(h, hipEventCreate(&e));
+        s->run_ev.push_back(e);
+    }
+    std::vector<uint64_t> sc_round(rounds);
+    for (uint32_t i = 0; i < rounds; i++) {
+        unsigned long long* row = s->h_run + size_t(i) * kRow;
+        PdArgs a;
+        int rc;
+        if (hb_every && i % hb_every == 0) {      // psim_c3_heartbeat without its wait
+            s->mono++;
+            s->root = hb_root;
+            rc = pd_args(h, *s, a);
+            if (rc) return rc;
+            a.out = s->msg[s->par];
+            a.nout = s->nmsg + s->par;
+            PDCHK(h, hipMemsetAsync(s->stats, 0, kPd * 8, st));
+            PDCHK(h, launch_pd_origin(a, hb_root, st));
+            PDCHK(h, hipMemcpyAsync(row, s->stats, kPd * 8, hipMemcpyDeviceToHost, st));
+        } else {
+            row[0] = ~0ull;                        // no heartbeat this round
+        }
+        const size_t kc = crash_off[i + 1] - crash_off[i];
+        if (kc) {
+            rc = psim_c3_crash(h, crash_v + crash_off[i], kc);
+            if (rc) return rc;
+        }
+        const size_t kj = join_off[i + 1] - join_off[i];
+        if (kj) {
+            rc = psim_c3_join(h, join_v + join_off[i], join_c + join_off[i], kj);
+            if (rc) return rc;
+        }
+        hipEvent_t* ev = s->run_ev.data() + 4ull * i;
+        rc = scamp_round_launch_to(h, row + kPd, ev[0], ev[1], &sc_round[i]);
+        if (rc) return rc;
+        rc = pd_args(h, *s, a);
+        if (rc) return rc;
+        PDCHK(h, hipEventRecord(ev[2], st));
+        PDCHK(h, launch_pd_round(a, st));
+        PDCHK(h, hipEventRecord(ev[3], st));
+        PDCHK(h, hipMemcpyAsync(row + kPd + kSc, s->stats, kPd * 8, hipMemcpyDeviceToHost, st));
+        s->par ^= 1u;
+        s->round++;
+    }
+    PDCHK(h, handle_wait(h));
+    const uint64_t round0 = s->round - rounds;
+    for (uint32_t i = 0; i < rounds; i++) {
+        const unsigned long long* row = s->h_run + size_t(i) * kRow;
+        const hipEvent_t* ev = s->run_ev.data() + 4ull * i;
+        psim_c3_stats* o = out && i < cap ? &out[i] : nullptr;
+        unsigned long long r[kPdNStat];
+        int rc;
+        if (row[0] != ~0ull) {
+            fold_stat_shards(row, r, kPdNStat, 9);
+            rc = pd_check(h, r[9], round0 + i);
+            if (rc) return rc;
+        }
+        float ms = 0.f;
+        PDCHK(h, hipEventElapsedTime(&ms, ev[0], ev[1]));
+        rc = scamp_round_report(h, row + kPd, ms, sc_round[i], o ? &o->scamp : nullptr);
+        if (rc) return rc;
+        fold_stat_shards(row + kPd + kSc, r, kPdNStat, 9);
+        PDCHK(h, hipEventElapsedTime(&ms, ev[2], ev[3]));
+        rc = pd_check(h, r[9], round0 + i + 1);
+        if (rc) return rc;
+        if (o) pd_fill(*s, r, ms, o);
     }
     return PSIM_OK;
 }

@@ -660,7 +660,11 @@ uint32_t* sc_stage(psim_handle* h, ScState& s, size_t words) {
 // A round's first half: the calls made since the last round sorted and
 // uploaded, the round launched, its stats rows copied to the pinned mirror --
 // nothing waits; sc_round_finish reads them once the stream got there.
-int sc_round_launch(psim_handle* h, ScState& s) {
+// (dst, e0, e1): where the stats rows go and the events around the round's
+// kernels (null: the handle's pinned mirror and events 0 / 1; psim_c3_run
+// passes a row and events per round so that no round waits for the last)
+int sc_round_launch(psim_handle* h, ScState& s, unsigned long long* dst = nullptr, hipEvent_t e0 = nullptr,
+                    hipEvent_t e1 = nullptr) {
     const hipStream_t st = handle_stream(h);
     // calls sorted by vertex: leaves first, then joins, each in call order
     // (sc_prep indexes each vertex's first one on the device)
@@ -704,23 +708,54 @@ int sc_round_launch(psim_handle* h, ScState& s) {
     }
     s.cv.clear();
     s.cx.clear();
-    if (!s.h_stats && hipHostMalloc((void**)&s.h_stats, kRoundStatShards * 16 * 8) != hipSuccess) {
+    if (!dst && !s.h_stats && hipHostMalloc((void**)&s.h_stats, kRoundStatShards * 16 * 8) != hipSuccess) {
         s.h_stats = nullptr;
         return handle_fail(h, PSIM_ENOMEM, "scamp: pinned stats rows");
     }
+    if (!dst) dst = s.h_stats;
+    if (!e0) e0 = handle_event(h, 0);
+    if (!e1) e1 = handle_event(h, 1);
     ScArgs a = sc_args(h, s);
     a.ncalls = uint32_t(k);
-    SCCHK(h, hipEventRecord(handle_event(h, 0), st));
+    SCCHK(h, hipEventRecord(e0, st));
     SCCHK(h, launch_sc_round(a, st));
-    SCCHK(h, hipEventRecord(handle_event(h, 1), st));
-    SCCHK(h, hipMemcpyAsync(s.h_stats, s.stats, kRoundStatShards * 16 * 8, hipMemcpyDeviceToHost, st));
+    SCCHK(h, hipEventRecord(e1, st));
+    SCCHK(h, hipMemcpyAsync(dst, s.stats, kRoundStatShards * 16 * 8, hipMemcpyDeviceToHost, st));
+    return PSIM_OK;
+}
+
+// A round's report from its stats rows (`round` = its 1-based number): the
+// kernel time into the handle's totals, the error bits as PSIM codes, the
+// counters into `out`
+int sc_round_report(psim_handle* h, const ScState& s, const unsigned long long* rows, float ms, uint64_t round,
+                    psim_scamp_stats* out) {
+    unsigned long long r[16];
+    fold_stat_shards(rows, r, 16, 11);
+    handle_add_round(h, ms);
+    if (r[11] & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: message queue over %u records",
+                                         (unsigned long long)round, s.cap);
+    if (r[11] & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: a view exceeded %u / %u entries",
+                                         (unsigned long long)round, kScPv, kScIv);
+    if (r[11] & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: > %u membership updates at a vertex",
+                                          (unsigned long long)round, kScEv);
+    if (r[11] & 32ull) return handle_fail(h, PSIM_EHIP, "scamp round %llu: a message record addressed off the cluster",
+                                          (unsigned long long)round);
+    if (out) {
+        memset(out, 0, sizeof *out);
+        uint64_t emitted = 0;
+        for (int k = 1; k < 7; k++) { out->sent[k] = r[k]; emitted += r[k]; }
+        out->dropped = r[7]; out->processed = r[8]; out->draws = r[9]; out->stopped = r[10];
+        out->error = r[11]; out->pv_sum = r[12]; out->inview_sum = r[13]; out->resub = r[14];
+        // records read (bucket + handler) and written, bucket counts/offsets, and
+        // one pass over each live vertex's head and partial-view row
+        out->algo_bytes = 48ull * r[8] + 28ull * emitted + 12ull * s.n + 64ull * s.n + 4ull * r[12];
+        out->kernel_ms = ms;
+    }
     return PSIM_OK;
 }
 
 // A round's second half, after the stream passed sc_round_launch's copy
 int sc_round_finish(psim_handle* h, ScState& s, psim_scamp_stats* out) {
-    unsigned long long r[16];
-    fold_stat_shards(s.h_stats, r, 16, 11);
 #ifdef C3_PROF
     {
         static unsigned long long tot[kProfSlots];
@@ -735,29 +770,9 @@ int sc_round_finish(psim_handle* h, ScState& s, psim_scamp_stats* out) {
 #endif
     float ms = 0.f;
     SCCHK(h, hipEventElapsedTime(&ms, handle_event(h, 0), handle_event(h, 1)));
-    handle_add_round(h, ms);
     s.round++;
     s.par ^= 1u;
-    if (r[11] & 1ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: message queue over %u records",
-                                         (unsigned long long)s.round, s.cap);
-    if (r[11] & 2ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: a view exceeded %u / %u entries",
-                                         (unsigned long long)s.round, kScPv, kScIv);
-    if (r[11] & 16ull) return handle_fail(h, PSIM_EOVERFLOW, "scamp round %llu: > %u membership updates at a vertex",
-                                          (unsigned long long)s.round, kScEv);
-    if (r[11] & 32ull) return handle_fail(h, PSIM_EHIP, "scamp round %llu: a message record addressed off the cluster",
-                                          (unsigned long long)s.round);
-    if (out) {
-        memset(out, 0, sizeof *out);
-        uint64_t emitted = 0;
-        for (int k = 1; k < 7; k++) { out->sent[k] = r[k]; emitted += r[k]; }
-        out->dropped = r[7]; out->processed = r[8]; out->draws = r[9]; out->stopped = r[10];
-        out->error = r[11]; out->pv_sum = r[12]; out->inview_sum = r[13]; out->resub = r[14];
-        // records read (bucket + handler) and written, bucket counts/offsets, and
-        // one pass over each live vertex's head and partial-view row
-        out->algo_bytes = 48ull * r[8] + 28ull * emitted + 12ull * s.n + 64ull * s.n + 4ull * r[12];
-        out->kernel_ms = ms;
-    }
-    return PSIM_OK;
+    return sc_round_report(h, s, s.h_stats, ms, s.round, out);
 }
 
 int sc_round(psim_handle* h, ScState& s, psim_scamp_stats* out) {
@@ -820,6 +835,23 @@ int scamp_round_finish(psim_handle* h, psim_scamp_stats* out) {
     ScState* s = sc_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
     return sc_round_finish(h, *s, out);
+}
+
+int scamp_round_launch_to(psim_handle* h, unsigned long long* dst, hipEvent_t e0, hipEvent_t e1, uint64_t* round) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    const int rc = sc_round_launch(h, *s, dst, e0, e1);
+    if (rc) return rc;
+    s->round++;                                       // the next launch's arguments (sc_args) follow this round
+    s->par ^= 1u;
+    if (round) *round = s->round;
+    return PSIM_OK;
+}
+
+int scamp_round_report(psim_handle* h, const unsigned long long* rows, float ms, uint64_t round, psim_scamp_stats* out) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    return sc_round_report(h, *s, rows, ms, round, out);
 }
 
 int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k) { return psim_scamp_crash(h, v, k); }

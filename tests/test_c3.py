@@ -154,6 +154,64 @@ def test_gpu_c3_1m():
     assert all(x["live"] > 0.99 * n for x in st)
 
 
+def _strip(st):
+    out = []
+    for x in st:
+        x = dict(x)
+        x.pop("pt_kernel_ms")
+        x["scamp"] = {k: v for k, v in x["scamp"].items() if k != "kernel_ms"}
+        out.append(x)
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_c3_run_equals_per_round_calls():
+    """psim_c3_run (churn rounds enqueued with no host wait between them) is
+    the same as psim_c3_heartbeat / crash / join / step one by one: every
+    round's counters, then both protocols' state at every vertex.  Two run
+    calls of different lengths (the pinned rows are reused and grown)."""
+    import partisan_amd as pa
+    n, periodic = 3000, 10
+    gs = []
+    for _ in range(2):
+        sim = pa.Simulator(device=0, seed=SEED)
+        g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=periodic)
+        for v, cc in waves(n):
+            g.join(v, cc)
+            g.step(3)
+        g.step(5)
+        gs.append((sim, g))
+    plan = []
+    for i in range(17):
+        v, cc = churn(n, i)
+        keep = v != 0
+        plan.append((v[keep], v[keep], cc[keep]))
+    (sa, a), (sb, b) = gs
+    per_round = []
+    for i, (cr, jv, jc) in enumerate(plan):
+        if i % 5 == 0:
+            a.heartbeat(7)
+        a.crash(cr)
+        a.join(jv, jc)
+        per_round += a.step(1)
+
+    def run(lo, hi, **kw):
+        return b.run([p[0] for p in plan[lo:hi]], [(p[1], p[2]) for p in plan[lo:hi]], **kw)
+
+    # heartbeats at rounds 0, 5 (first call), none in 6..9, 10 and 15 (offsets 0 and 5 of the third)
+    out = run(0, 6, heartbeat_every=5, root=7) + run(6, 10) + run(10, 17, heartbeat_every=5, root=7)
+    assert len(out) == 17
+    assert _strip(out) == _strip(per_round)
+    pva, npva, _, _ = a.scamp.views()
+    pvb, npvb, _, _ = b.scamp.views()
+    assert (npva == npvb).all() and (pva == pvb).all()
+    for v in range(n):
+        assert a.plumtree(v) == b.plumtree(v), v
+    assert sum(x["pt_sent"]["graft"] + x["pt_sent"]["prune"] for x in out) > 0
+    sa.close()
+    sb.close()
+
+
 @pytest.mark.gpu
 def test_gpu_large_crash_list_resets_every_vertex():
     """A crash list larger than any before grows the device list buffer; the

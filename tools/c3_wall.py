@@ -2,7 +2,11 @@
 driver call (crash, join, step, heartbeat) against the device time of the
 round's SCAMP and Plumtree kernels -- where a C3 round's wall time goes.
 
-usage: python tools/c3_wall.py [n] [rounds]"""
+With a third argument "run" the churn rounds go through one psim_c3_run call
+(C3Cluster.run: no host wait between rounds; the churn is drawn beforehand
+and not timed).
+
+usage: python tools/c3_wall.py [n] [rounds] [run]"""
 import json
 import os
 import sys
@@ -23,6 +27,24 @@ def main():
         g.join(v, cc)
         g.step(3)
     g.step(5)
+    if len(sys.argv) > 3 and sys.argv[3] == "run":
+        plan = []
+        for i in range(rounds):
+            v, cc = churn_batch(n, seed, i)
+            keep = v != 0
+            plan.append((v[keep], cc[keep]))
+        g.step(1)                      # the pinned rows and events of a first call are not what is timed
+        t0 = time.perf_counter()
+        st = g.run([p[0] for p in plan], [(p[0], p[1]) for p in plan], heartbeat_every=10, root=0)
+        wall = time.perf_counter() - t0
+        print(json.dumps({"mode": "psim_c3_run", "n": n, "rounds": rounds,
+                          "wall_ms_per_round": round(1e3 * wall / rounds, 4),
+                          "scamp_kernel_ms": round(sum(s["scamp"]["kernel_ms"] for s in st) / rounds, 4),
+                          "plumtree_kernel_ms": round(sum(s["pt_kernel_ms"] for s in st) / rounds, 4),
+                          "delivered_live_last": st[-1]["delivered_live"], "live_last": st[-1]["live"]}),
+              flush=True)
+        sim.close()
+        return
     t = {"heartbeat": 0.0, "churn_draw": 0.0, "crash": 0.0, "join": 0.0, "step": 0.0}
     sc_ms = pt_ms = 0.0
     t0 = time.perf_counter()
