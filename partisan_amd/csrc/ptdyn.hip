@@ -53,13 +53,16 @@ struct Ctx {
 
 __device__ __forceinline__ bool connected(const Ctx& c, uint32_t t) { return t != c.v && row_has(c.pv, c.npv, t); }
 
-__device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
-    if (!connected(c, t)) { c.dropped++; return; }
+__device__ __forceinline__ void send_conn(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
     const PdArgs& a = *c.a;
     const uint32_t sh = 12u * (type - 1u);
     if (((c.sent >> sh) & 0xFFFull) == 0xFFFull) c.err |= 16u;   // a 13th bit would carry into the next kind
     else c.sent += 1ull << sh;
     wq_send(c.q, a.nout, a.out, a.out_cap, c.err, PdMsg{type, c.v, t, c.h.seq++, round, mono});
+}
+__device__ __forceinline__ void send(Ctx& c, uint32_t t, uint32_t type, uint32_t mono, uint32_t round) {
+    if (!connected(c, t)) { c.dropped++; return; }
+    send_conn(c, t, type, mono, round);
 }
 
 static_assert(kPdTab % 8 == 0, "row_find reads the peer table as quad pairs");
@@ -161,9 +164,32 @@ __device__ __forceinline__ void ack_rows(Ctx& c, uint32_t peer, uint32_t mono, u
 }
 
 // eager_push/7 (:962-970) to eager peers -- From, schedule_lazy_push/6 (:974-988)
+// The eager pushes test the connection rule on the member mask instead of
+// scanning the partial view: after this round's {update, Members} casts are
+// applied (pd_process step 1; pd_origin runs between rounds, after them),
+// S_MEM holds exactly the manager's members -- the partial view the send
+// rule reads (oracle/c3.c connected) -- so tab[i] is connected iff it is not
+// this vertex and bit i of S_MEM is set.  -DPD_CONN_CHECK builds compare the
+// two on every push and raise error bit 64 (PSIM_ESTATE) on a difference.
+#ifndef PD_CONN_MASK
+#define PD_CONN_MASK 1
+#endif
 __device__ __forceinline__ void push(Ctx& c, const PdBits& from_bit, uint32_t mono, uint32_t round) {
     PdBits e = eager_now(c) & ~from_bit;
+#if PD_CONN_MASK
+    while (e.any()) {
+        const int i = pop_low(e);
+        const uint32_t t = c.tab[i];
+        const bool conn = t != c.v && c.m[S_MEM].test((uint32_t)i);
+#ifdef PD_CONN_CHECK
+        if (conn != connected(c, t)) c.err |= 64u;
+#endif
+        if (!conn) c.dropped++;
+        else send_conn(c, t, PD_BROADCAST, mono, round);
+    }
+#else
     while (e.any()) send(c, c.tab[pop_low(e)], PD_BROADCAST, mono, round);
+#endif
     PdBits l = lazy_now(c) & ~from_bit;
     while (l.any()) add_row(c, c.tab[pop_low(l)], mono, round);
 }
@@ -620,6 +646,8 @@ int pd_check(psim_handle* h, unsigned long long err, uint64_t round) {
                                         (unsigned long long)round);
     if (err & 32ull) return handle_fail(h, PSIM_EHIP, "c3 round %llu: a message record addressed off the cluster",
                                         (unsigned long long)round);
+    if (err & 64ull) return handle_fail(h, PSIM_ESTATE, "c3 round %llu: member mask and partial view disagree "
+                                        "(PD_CONN_CHECK)", (unsigned long long)round);
     return PSIM_OK;
 }
 

@@ -6,6 +6,7 @@ usage: python tools/c3_run_gaps.py <dir with run_kernel_trace.csv> [R]"""
 import collections
 import csv
 import json
+import re
 import os
 import sys
 
@@ -17,7 +18,7 @@ def main():
     with open(os.path.join(d, "run_kernel_trace.csv")) as f:
         for r in csv.DictReader(f):
             n = r["Kernel_Name"]
-            n = n.split("(")[0].split("::")[-1][:40]
+            n = re.sub(r"\((psim::|unsigned).*", "", n).split("::")[-1][:40]
             ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), n))
     p = os.path.join(d, "run_memory_copy_trace.csv")
     if os.path.exists(p):
