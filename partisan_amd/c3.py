@@ -48,24 +48,35 @@ class C3Cluster:
         self._c(lib().psim_c3_step(self.sim._h, rounds, st, rounds))
         return [s.as_dict() for s in st]
 
-    def run(self, crashes, joins, heartbeat_every=0, root=0):
-        """Rounds of churn in one call (psim_c3_run): round i = heartbeat at
-        `root` when heartbeat_every and i % heartbeat_every == 0, crash of
-        crashes[i], join of joins[i] = (vertices, contacts), one step -- the
-        same as those calls one by one, with no host wait between rounds."""
+    @staticmethod
+    def plan(crashes, joins):
+        """Flat arrays for run(): (crash_off, crash_v, join_off, join_v,
+        join_c) from one crash list and one (vertices, contacts) join list per
+        round."""
         rounds = len(crashes)
         if len(joins) != rounds:
             raise ValueError("one crash list and one join list per round")
 
         def flat(parts):
+            parts = [np.atleast_1d(x).astype(np.uint32, copy=False) for x in parts]
             off = np.zeros(rounds + 1, np.uint32)
-            off[1:] = np.cumsum([len(np.atleast_1d(x)) for x in parts])
-            v = np.concatenate([np.atleast_1d(x).astype(np.uint32) for x in parts] or [np.zeros(0, np.uint32)])
+            off[1:] = np.cumsum([len(x) for x in parts])
+            v = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
             return off, np.ascontiguousarray(v, dtype=np.uint32)
 
         co, cv = flat(crashes)
         jo, jv = flat([j[0] for j in joins])
         _, jc = flat([j[1] for j in joins])
+        return co, cv, jo, jv, jc
+
+    def run(self, crashes=None, joins=None, heartbeat_every=0, root=0, plan=None):
+        """Rounds of churn in one call (psim_c3_run): round i = heartbeat at
+        `root` when heartbeat_every and i % heartbeat_every == 0, crash of
+        crashes[i], join of joins[i] = (vertices, contacts), one step -- the
+        same as those calls one by one, with no host wait between rounds.
+        `plan` (from C3Cluster.plan) replaces crashes / joins."""
+        co, cv, jo, jv, jc = plan if plan is not None else self.plan(crashes, joins)
+        rounds = len(co) - 1
         u32 = _P(C.c_uint32)
         st = (C3Stats * max(rounds, 1))()
         self._c(lib().psim_c3_run(self.sim._h, rounds, co.ctypes.data_as(u32), cv.ctypes.data_as(u32),

@@ -590,7 +590,20 @@ int scamp_round_finish(psim_handle* h, psim_scamp_stats* out);
 // psim_c3_run: a round launched with its stats rows copied to `dst` (pinned,
 // kRoundStatShards * 16 u64) between events e0 / e1, the host's round count
 // advanced at once (*round = its number); reported later from those rows
-int scamp_round_launch_to(psim_handle* h, unsigned long long* dst, hipEvent_t e0, hipEvent_t e1, uint64_t* round);
+struct ScLaunch {
+    unsigned long long* h_dst = nullptr;     // pinned row the stats rows are copied to (null: the handle's)
+    hipEvent_t e0 = nullptr, e1 = nullptr;   // around the round's kernels (null: handle events 0 / 1)
+    unsigned long long* d_stats = nullptr;   // device row the round's stats stay in (no copy; null: the handle's)
+    const uint32_t* d_calls = nullptr;       // the round's calls, sorted, on the device: vertices then targets
+    uint32_t d_ncalls = 0;
+};
+int scamp_round_launch_to(psim_handle* h, const ScLaunch& o, uint64_t* round);
+// psim_c3_run's pieces of psim_scamp_join / _crash: a call list checked and
+// sorted into `sorted` (k vertices then k targets); a crash list checked
+// (range, duplicates); the restart of a crash list already on the device
+int scamp_check_calls(psim_handle* h, const uint32_t* v, const uint32_t* x, size_t k, uint32_t* sorted);
+int scamp_check_crash(psim_handle* h, const uint32_t* v, size_t k);
+int scamp_crash_dev(psim_handle* h, const uint32_t* dv, size_t k);
 int scamp_round_report(psim_handle* h, const unsigned long long* rows, float ms, uint64_t round, psim_scamp_stats* out);
 hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);
 hipError_t launch_sc_round(const ScArgs& a, hipStream_t s);

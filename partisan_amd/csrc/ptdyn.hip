@@ -590,17 +590,23 @@ struct PdState : ModuleState {
     uint32_t par = 0;
     uint64_t round = 0;
     unsigned long long* h_stats = nullptr;   // pinned: a round's stats rows
-    // psim_c3_run: pinned stats rows of every round of one call (heartbeat,
-    // SCAMP, Plumtree) and four timing events per round
-    unsigned long long* h_run = nullptr;
-    size_t h_run_rounds = 0;
+    // psim_c3_run: the stats rows of every round of one call (heartbeat,
+    // SCAMP, Plumtree) on the device and their pinned mirror, the call's
+    // crash lists and sorted calls (pinned staging, one upload to d_in), and
+    // four timing events per round
+    unsigned long long *h_run = nullptr, *d_run = nullptr;
+    size_t run_rounds = 0;
+    uint32_t *h_in = nullptr, *d_in = nullptr;
+    size_t in_cap = 0;
+    bool run_pending = false;                // a run returned early: its copies may still be queued
     std::vector<hipEvent_t> run_ev;
     ~PdState() override {
-        void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum};
+        void* p[] = {head, tab, mask, rows, stats, msg[0], msg[1], nmsg, cnt, cur, off, idx, bsum, d_run, d_in};
         for (void* x : p)
             if (x) (void)hipFree(x);
         if (h_stats) (void)hipHostFree(h_stats);
         if (h_run) (void)hipHostFree(h_run);
+        if (h_in) (void)hipHostFree(h_in);
         for (hipEvent_t e : run_ev) (void)hipEventDestroy(e);
     }
 };
@@ -807,10 +813,13 @@ int psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* out, size_t cap
 // crash_v[crash_off[i], crash_off[i+1]), the joins join_v / join_c over
 // [join_off[i], join_off[i+1]), then one psim_c3_step round -- exactly the
 // calls psim_c3_heartbeat / crash / join / step would make, enqueued on the
-// handle's stream with no wait between rounds: each round's stats rows go to
-// a pinned row of their own and are read, checked and reported after one
-// wait at the end (the first failing round's error is returned, as the
-// per-round calls would have; the handle's C3 state is then spent).
+// handle's stream with no wait between rounds.  The crash lists and sorted
+// calls of every kC3Block rounds travel in one upload, each round's stats
+// rows stay in a device row of their own, and the rows come back in one copy
+// after the last round: the per-round work on the stream is the kernels
+// alone.  A bad list fails the call at its round (the rounds before it were
+// run); the first failing round's error is returned, as the per-round calls
+// would have (the handle's C3 state is then spent).
 int psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, const uint32_t* crash_v,
                 const uint32_t* join_off, const uint32_t* join_v, const uint32_t* join_c, uint32_t hb_every,
                 uint32_t hb_root, psim_c3_stats* out, size_t cap) {
@@ -818,71 +827,129 @@ int psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, cons
     PdState* s = pd_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
     if (hb_every && hb_root >= s->n) return handle_fail(h, PSIM_EINVAL, "heartbeat root %u >= n %u", hb_root, s->n);
+    if (!rounds) return PSIM_OK;
+    size_t words = 0;
     for (uint32_t i = 0; i < rounds; i++) {
         if (crash_off[i + 1] < crash_off[i] || join_off[i + 1] < join_off[i])
             return handle_fail(h, PSIM_EINVAL, "round %u: decreasing list offsets", i);
         if ((crash_off[i + 1] > crash_off[i] && !crash_v) || (join_off[i + 1] > join_off[i] && (!join_v || !join_c)))
             return PSIM_EINVAL;
     }
+    words = size_t(crash_off[rounds] - crash_off[0]) + 2ull * (join_off[rounds] - join_off[0]);
     const hipStream_t st = handle_stream(h);
+    if (s->run_pending) {                         // the staging below may be refilled or freed
+        PDCHK(h, hipStreamSynchronize(st));
+        s->run_pending = false;
+    }
     constexpr size_t kSc = kRoundStatShards * 16, kPd = kRoundStatShards * kPdNStat;   // u64 per stats row
     constexpr size_t kRow = 2 * kPd + kSc;                                               // heartbeat, SCAMP, Plumtree
-    if (rounds > s->h_run_rounds) {
+    if (rounds > s->run_rounds) {
         if (s->h_run) (void)hipHostFree(s->h_run);
-        s->h_run = nullptr;
-        s->h_run_rounds = 0;
+        if (s->d_run) (void)hipFree(s->d_run);
+        s->h_run = s->d_run = nullptr;
+        s->run_rounds = 0;
         if (hipHostMalloc((void**)&s->h_run, size_t(rounds) * kRow * 8) != hipSuccess) {
             s->h_run = nullptr;
             return handle_fail(h, PSIM_ENOMEM, "c3: pinned stats rows for %u rounds", rounds);
         }
-        s->h_run_rounds = rounds;
+        if (!pd_alloc((void**)&s->d_run, size_t(rounds) * kRow * 8))
+            return handle_fail(h, PSIM_ENOMEM, "c3: device stats rows for %u rounds", rounds);
+        s->run_rounds = rounds;
+    }
+    if (words > s->in_cap) {
+        if (s->h_in) (void)hipHostFree(s->h_in);
+        if (s->d_in) (void)hipFree(s->d_in);
+        s->h_in = s->d_in = nullptr;
+        s->in_cap = 0;
+        if (hipHostMalloc((void**)&s->h_in, words * 4) != hipSuccess) {
+            s->h_in = nullptr;
+            return handle_fail(h, PSIM_ENOMEM, "c3: pinned staging for %zu list words", words);
+        }
+        if (!pd_alloc((void**)&s->d_in, words * 4)) return handle_fail(h, PSIM_ENOMEM, "c3: %zu list words", words);
+        s->in_cap = words;
     }
     while (s->run_ev.size() < 4ull * rounds) {
         hipEvent_t e;
         PDCHK(h, hipEventCreate(&e));
         s->run_ev.push_back(e);
     }
+    // rounds go out in blocks of kC3Block: a block's lists are checked and
+    // staged (round i's crash list at cpos[i], its sorted calls -- vertices,
+    // then targets -- at jpos[i]) and uploaded in one copy, then its rounds
+    // are enqueued; the host stages the next block while the device runs
+    // this one.  Segments never overlap, so no upload waits for another.
+    constexpr uint32_t kC3Block = 4;
+    std::vector<size_t> cpos(rounds), jpos(rounds);
     std::vector<uint64_t> sc_round(rounds);
-    for (uint32_t i = 0; i < rounds; i++) {
-        unsigned long long* row = s->h_run + size_t(i) * kRow;
-        PdArgs a;
-        int rc;
-        if (hb_every && i % hb_every == 0) {      // psim_c3_heartbeat without its wait
-            s->mono++;
-            s->root = hb_root;
+    std::vector<uint8_t> beat(rounds, 0);
+    size_t w = 0;
+    s->run_pending = true;
+    PDCHK(h, hipMemsetAsync(s->d_run, 0, size_t(rounds) * kRow * 8, st));
+    for (uint32_t b0 = 0; b0 < rounds; b0 += kC3Block) {
+        const uint32_t b1 = std::min(rounds, b0 + kC3Block);
+        const size_t w0 = w;
+        for (uint32_t i = b0; i < b1; i++) {
+            const size_t kc = crash_off[i + 1] - crash_off[i], kj = join_off[i + 1] - join_off[i];
+            cpos[i] = w;
+            if (kc) {
+                int rc = scamp_check_crash(h, crash_v + crash_off[i], kc);
+                if (rc) return rc;
+                memcpy(s->h_in + w, crash_v + crash_off[i], kc * 4);
+                w += kc;
+            }
+            jpos[i] = w;
+            if (kj) {
+                int rc = scamp_check_calls(h, join_v + join_off[i], join_c + join_off[i], kj, s->h_in + w);
+                if (rc) return rc;
+                w += 2 * kj;
+            }
+        }
+        if (w > w0) PDCHK(h, hipMemcpyAsync(s->d_in + w0, s->h_in + w0, (w - w0) * 4, hipMemcpyHostToDevice, st));
+        for (uint32_t i = b0; i < b1; i++) {
+            unsigned long long* row = s->d_run + size_t(i) * kRow;
+            PdArgs a;
+            int rc;
+            if (hb_every && i % hb_every == 0) {      // psim_c3_heartbeat (its stats row was zeroed above)
+                s->mono++;
+                s->root = hb_root;
+                rc = pd_args(h, *s, a);
+                if (rc) return rc;
+                a.out = s->msg[s->par];
+                a.nout = s->nmsg + s->par;
+                a.stats = row;
+                PDCHK(h, launch_pd_origin(a, hb_root, st));
+                beat[i] = 1;
+            }
+            const size_t kc = crash_off[i + 1] - crash_off[i], kj = join_off[i + 1] - join_off[i];
+            if (kc) {                                 // psim_c3_crash: both processes restart
+                rc = scamp_crash_dev(h, s->d_in + cpos[i], kc);
+                if (rc) return rc;
+                rc = pd_args(h, *s, a);
+                if (rc) return rc;
+                PDCHK(h, launch_pd_init(a, s->d_in + cpos[i], (uint32_t)kc, st));
+            }
+            hipEvent_t* ev = s->run_ev.data() + 4ull * i;
+            ScLaunch o;
+            o.e0 = ev[0];
+            o.e1 = ev[1];
+            o.d_stats = row + kPd;
+            o.d_calls = kj ? s->d_in + jpos[i] : nullptr;
+            o.d_ncalls = (uint32_t)kj;
+            rc = scamp_round_launch_to(h, o, &sc_round[i]);
+            if (rc) return rc;
             rc = pd_args(h, *s, a);
             if (rc) return rc;
-            a.out = s->msg[s->par];
-            a.nout = s->nmsg + s->par;
-            PDCHK(h, hipMemsetAsync(s->stats, 0, kPd * 8, st));
-            PDCHK(h, launch_pd_origin(a, hb_root, st));
-            PDCHK(h, hipMemcpyAsync(row, s->stats, kPd * 8, hipMemcpyDeviceToHost, st));
-        } else {
-            row[0] = ~0ull;                        // no heartbeat this round
+            a.stats = row + kPd + kSc;
+            PDCHK(h, hipEventRecord(ev[2], st));
+            PDCHK(h, launch_pd_round(a, st));
+            PDCHK(h, hipEventRecord(ev[3], st));
+            s->par ^= 1u;
+            s->round++;
         }
-        const size_t kc = crash_off[i + 1] - crash_off[i];
-        if (kc) {
-            rc = psim_c3_crash(h, crash_v + crash_off[i], kc);
-            if (rc) return rc;
-        }
-        const size_t kj = join_off[i + 1] - join_off[i];
-        if (kj) {
-            rc = psim_c3_join(h, join_v + join_off[i], join_c + join_off[i], kj);
-            if (rc) return rc;
-        }
-        hipEvent_t* ev = s->run_ev.data() + 4ull * i;
-        rc = scamp_round_launch_to(h, row + kPd, ev[0], ev[1], &sc_round[i]);
-        if (rc) return rc;
-        rc = pd_args(h, *s, a);
-        if (rc) return rc;
-        PDCHK(h, hipEventRecord(ev[2], st));
-        PDCHK(h, launch_pd_round(a, st));
-        PDCHK(h, hipEventRecord(ev[3], st));
-        PDCHK(h, hipMemcpyAsync(row + kPd + kSc, s->stats, kPd * 8, hipMemcpyDeviceToHost, st));
-        s->par ^= 1u;
-        s->round++;
     }
+    PDCHK(h, hipMemcpyAsync(s->h_run, s->d_run, size_t(rounds) * kRow * 8, hipMemcpyDeviceToHost, st));
     PDCHK(h, handle_wait(h));
+    s->run_pending = false;
     const uint64_t round0 = s->round - rounds;
     for (uint32_t i = 0; i < rounds; i++) {
         const unsigned long long* row = s->h_run + size_t(i) * kRow;
@@ -890,7 +957,7 @@ int psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, cons
         psim_c3_stats* o = out && i < cap ? &out[i] : nullptr;
         unsigned long long r[kPdNStat];
         int rc;
-        if (row[0] != ~0ull) {
+        if (beat[i]) {
             fold_stat_shards(row, r, kPdNStat, 9);
             rc = pd_check(h, r[9], round0 + i);
             if (rc) return rc;

@@ -657,42 +657,49 @@ uint32_t* sc_stage(psim_handle* h, ScState& s, size_t words) {
     return s.h_up;
 }
 
+// Calls sorted by vertex: leaves first, then joins, each in call order
+// (sc_prep indexes each vertex's first one on the device), written to `up`
+// as k vertices then k targets.  An LSD radix sort of key 2 v + join, stable:
+// O(k) per 11-bit digit, where a comparison sort of 50k calls took
+// milliseconds of host time; calls already in key order -- a churn batch's
+// joins -- are copied as they are.
+void sc_sort_calls(uint32_t n, const uint32_t* cv, const uint32_t* cx, size_t k, uint32_t* up) {
+    auto key = [&](size_t i) -> uint64_t { return 2ull * cv[i] + ((cx[i] >> 31) ^ 1u); };   // leave first
+    bool sorted = true;
+    for (size_t i = 1; i < k && sorted; i++) sorted = key(i - 1) <= key(i);
+    if (sorted) {
+        memcpy(up, cv, k * 4);
+        memcpy(up + k, cx, k * 4);
+        return;
+    }
+    std::vector<uint32_t> ord(k), tmp(k);
+    for (size_t i = 0; i < k; i++) ord[i] = uint32_t(i);
+    for (uint32_t shift = 0; shift < 64 && (2ull * n) >> shift; shift += 11) {
+        uint32_t cnt[2049] = {0};
+        for (size_t i = 0; i < k; i++) cnt[((key(ord[i]) >> shift) & 2047u) + 1]++;
+        for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+        for (size_t i = 0; i < k; i++) tmp[cnt[(key(ord[i]) >> shift) & 2047u]++] = ord[i];
+        ord.swap(tmp);
+    }
+    for (size_t i = 0; i < k; i++) { up[i] = cv[ord[i]]; up[k + i] = cx[ord[i]]; }
+}
+
 // A round's first half: the calls made since the last round sorted and
 // uploaded, the round launched, its stats rows copied to the pinned mirror --
 // nothing waits; sc_round_finish reads them once the stream got there.
-// (dst, e0, e1): where the stats rows go and the events around the round's
-// kernels (null: the handle's pinned mirror and events 0 / 1; psim_c3_run
-// passes a row and events per round so that no round waits for the last)
-int sc_round_launch(psim_handle* h, ScState& s, unsigned long long* dst = nullptr, hipEvent_t e0 = nullptr,
-                    hipEvent_t e1 = nullptr) {
+// `o` (psim_c3_run; null: the handle's own buffers and events 0 / 1): the
+// events around the round's kernels, and either a pinned row the stats are
+// copied to or a device row they stay in (d_stats), and the round's calls
+// already sorted and on the device (d_calls: d_ncalls vertices then targets)
+int sc_round_launch(psim_handle* h, ScState& s, const ScLaunch* o = nullptr) {
     const hipStream_t st = handle_stream(h);
-    // calls sorted by vertex: leaves first, then joins, each in call order
-    // (sc_prep indexes each vertex's first one on the device)
-    // (an LSD radix sort of key 2 v + join, stable: O(k) per 11-bit digit,
-    // where a comparison sort of 50k calls took milliseconds of host time;
-    // calls already in key order -- a churn batch's joins -- skip it)
-    const size_t k = s.cv.size();
-    auto key = [&](uint32_t i) -> uint64_t { return 2ull * s.cv[i] + ((s.cx[i] >> 31) ^ 1u); };   // leave first
-    bool sorted = true;
-    for (size_t i = 1; i < k && sorted; i++) sorted = key(uint32_t(i - 1)) <= key(uint32_t(i));
-    uint32_t* up = k ? sc_stage(h, s, 2 * k) : nullptr;
-    if (k && !up) return handle_fail(h, PSIM_ENOMEM, "scamp: pinned staging for %zu calls", k);
-    if (k && sorted) {
-        memcpy(up, s.cv.data(), k * 4);
-        memcpy(up + k, s.cx.data(), k * 4);
-    } else if (k) {
-        std::vector<uint32_t> ord(k), tmp(k);
-        for (size_t i = 0; i < k; i++) ord[i] = uint32_t(i);
-        for (uint32_t shift = 0; shift < 64 && (2ull * s.n) >> shift; shift += 11) {
-            uint32_t cnt[2049] = {0};
-            for (size_t i = 0; i < k; i++) cnt[((key(ord[i]) >> shift) & 2047u) + 1]++;
-            for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
-            for (size_t i = 0; i < k; i++) tmp[cnt[(key(ord[i]) >> shift) & 2047u]++] = ord[i];
-            ord.swap(tmp);
-        }
-        for (size_t i = 0; i < k; i++) { up[i] = s.cv[ord[i]]; up[k + i] = s.cx[ord[i]]; }
-    }
-    if (k > s.calls_cap) {
+    const uint32_t* d_calls = o ? o->d_calls : nullptr;
+    const size_t k = d_calls ? o->d_ncalls : s.cv.size();
+    if (d_calls && !s.cv.empty()) return handle_fail(h, PSIM_ESTATE, "scamp: calls pending beside a run's call list");
+    uint32_t* up = k && !d_calls ? sc_stage(h, s, 2 * k) : nullptr;
+    if (k && !d_calls && !up) return handle_fail(h, PSIM_ENOMEM, "scamp: pinned staging for %zu calls", k);
+    if (k && !d_calls) sc_sort_calls(s.n, s.cv.data(), s.cx.data(), k, up);
+    if (k > s.calls_cap && !d_calls) {
         if (s.calls) (void)hipFree(s.calls);
         if (s.call_v) (void)hipFree(s.call_v);
         s.calls = s.call_v = nullptr;
@@ -700,7 +707,7 @@ int sc_round_launch(psim_handle* h, ScState& s, unsigned long long* dst = nullpt
         if (!sc_alloc((void**)&s.calls, s.calls_cap * 4) || !sc_alloc((void**)&s.call_v, s.calls_cap * 4))
             return handle_fail(h, PSIM_ENOMEM, "scamp: call list");
     }
-    if (k) {
+    if (k && !d_calls) {
         SCCHK(h, hipMemcpyAsync(s.call_v, up, k * 4, hipMemcpyHostToDevice, st));
         SCCHK(h, hipMemcpyAsync(s.calls, up + k, k * 4, hipMemcpyHostToDevice, st));
         SCCHK(h, hipEventRecord(s.up_ev, st));
@@ -708,19 +715,26 @@ int sc_round_launch(psim_handle* h, ScState& s, unsigned long long* dst = nullpt
     }
     s.cv.clear();
     s.cx.clear();
-    if (!dst && !s.h_stats && hipHostMalloc((void**)&s.h_stats, kRoundStatShards * 16 * 8) != hipSuccess) {
+    unsigned long long* dst = o ? o->h_dst : nullptr;
+    unsigned long long* d_stats = o ? o->d_stats : nullptr;
+    if (!dst && !d_stats && !s.h_stats && hipHostMalloc((void**)&s.h_stats, kRoundStatShards * 16 * 8) != hipSuccess) {
         s.h_stats = nullptr;
         return handle_fail(h, PSIM_ENOMEM, "scamp: pinned stats rows");
     }
     if (!dst) dst = s.h_stats;
-    if (!e0) e0 = handle_event(h, 0);
-    if (!e1) e1 = handle_event(h, 1);
+    const hipEvent_t e0 = o && o->e0 ? o->e0 : handle_event(h, 0);
+    const hipEvent_t e1 = o && o->e1 ? o->e1 : handle_event(h, 1);
     ScArgs a = sc_args(h, s);
     a.ncalls = uint32_t(k);
+    if (d_calls) {
+        a.call_v = d_calls;
+        a.calls = d_calls + k;
+    }
+    if (d_stats) a.stats = d_stats;
     SCCHK(h, hipEventRecord(e0, st));
     SCCHK(h, launch_sc_round(a, st));
     SCCHK(h, hipEventRecord(e1, st));
-    SCCHK(h, hipMemcpyAsync(dst, s.stats, kRoundStatShards * 16 * 8, hipMemcpyDeviceToHost, st));
+    if (!d_stats) SCCHK(h, hipMemcpyAsync(dst, s.stats, kRoundStatShards * 16 * 8, hipMemcpyDeviceToHost, st));
     return PSIM_OK;
 }
 
@@ -837,10 +851,10 @@ int scamp_round_finish(psim_handle* h, psim_scamp_stats* out) {
     return sc_round_finish(h, *s, out);
 }
 
-int scamp_round_launch_to(psim_handle* h, unsigned long long* dst, hipEvent_t e0, hipEvent_t e1, uint64_t* round) {
+int scamp_round_launch_to(psim_handle* h, const ScLaunch& o, uint64_t* round) {
     ScState* s = sc_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
-    const int rc = sc_round_launch(h, *s, dst, e0, e1);
+    const int rc = sc_round_launch(h, *s, &o);
     if (rc) return rc;
     s->round++;                                       // the next launch's arguments (sc_args) follow this round
     s->par ^= 1u;
@@ -855,6 +869,39 @@ int scamp_round_report(psim_handle* h, const unsigned long long* rows, float ms,
 }
 
 int scamp_crash_list(psim_handle* h, const uint32_t* v, size_t k) { return psim_scamp_crash(h, v, k); }
+
+int scamp_check_calls(psim_handle* h, const uint32_t* v, const uint32_t* x, size_t k, uint32_t* sorted) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    for (size_t i = 0; i < k; i++)
+        if (v[i] >= s->n || x[i] >= s->n) return handle_fail(h, PSIM_EINVAL, "call %zu: vertex out of range", i);
+    sc_sort_calls(s->n, v, x, k, sorted);
+    return PSIM_OK;
+}
+
+int scamp_check_crash(psim_handle* h, const uint32_t* v, size_t k) {
+    ScState* s = sc_of(h);
+    if (k && !v) return PSIM_EINVAL;
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    if (s->stamp.size() != s->n || ++s->stamp_gen == 0) {
+        s->stamp.assign(s->n, 0u);
+        s->stamp_gen = 1;
+    }
+    for (size_t i = 0; i < k; i++) {
+        if (v[i] >= s->n) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex out of range", i);
+        if (s->stamp[v[i]] == s->stamp_gen) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex %u listed twice", i, v[i]);
+        s->stamp[v[i]] = s->stamp_gen;
+    }
+    return PSIM_OK;
+}
+
+int scamp_crash_dev(psim_handle* h, const uint32_t* dv, size_t k) {
+    ScState* s = sc_of(h);
+    if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
+    if (!k) return PSIM_OK;
+    SCCHK(h, launch_sc_init(sc_args(h, *s), dv, (uint32_t)k, handle_stream(h)));
+    return PSIM_OK;
+}
 
 }  // namespace psim
 
@@ -930,17 +977,8 @@ int psim_scamp_crash(psim_handle* h, const uint32_t* v, size_t k) {
     if (!h || (k && !v)) return PSIM_EINVAL;
     ScState* s = sc_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_scamp_setup not called");
-    // duplicates by generation stamps (no O(n) clear per call)
-    if (s->stamp.size() != s->n || ++s->stamp_gen == 0) {
-        s->stamp.assign(s->n, 0u);
-        s->stamp_gen = 1;
-    }
-    for (size_t i = 0; i < k; i++) {
-        if (v[i] >= s->n) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex out of range", i);
-        if (s->stamp[v[i]] == s->stamp_gen) return handle_fail(h, PSIM_EINVAL, "crash %zu: vertex %u listed twice", i, v[i]);
-        s->stamp[v[i]] = s->stamp_gen;
-    }
-    if (!k) return PSIM_OK;
+    const int crc = scamp_check_crash(h, v, k);   // range, duplicates (generation stamps: no O(n) clear per call)
+    if (crc || !k) return crc;
     SCCHK(h, hipSetDevice(handle_device(h)));
     int rc = sc_upload_list(h, *s, v, k);
     if (rc) return rc;
