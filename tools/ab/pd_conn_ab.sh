@@ -11,7 +11,7 @@ step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" >
 export PYTHONUNBUFFERED=1
 T="python -u -m pytest tests/test_c3.py -m gpu -x -v --timeout 300 --timeout-method thread"
 PSIM_LIB_PATH=$PWD/partisan_amd/exp_pd_chk.so step pytest_c3_chk 400 $T
-PSIM_LIB_PATH=$PWD/partisan_amd/exp_pd_chk.so step c3_chk_1m 300 python tools/c3_wall.py 1000000 30
+PSIM_LIB_PATH=$PWD/partisan_amd/exp_pd_chk.so step c3_chk_1m 300 python tools/c3_wall.py 1000000 30 run
 step pytest_c3_mask 400 $T
 for rep in 1 2; do
   PSIM_LIB_PATH=$PWD/partisan_amd/exp_pd_off.so step c3_off_$rep 300 python tools/c3_wall.py 1000000 30 run
