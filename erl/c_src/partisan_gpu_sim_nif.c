@@ -1299,6 +1299,60 @@ static ERL_NIF_TERM nif_c3_heartbeat(ErlNifEnv* env, int argc, const ERL_NIF_TER
     return enif_make_tuple2(env, mk_atom(env, "ok"), enif_make_uint(env, mono));
 }
 
+/* {ok, [{PlumtreeMap, ScampMap}]} of k C3 rounds; maps: k scratch terms */
+static ERL_NIF_TERM c3_stats_ok(ErlNifEnv* env, const psim_c3_stats* st, ERL_NIF_TERM* maps, unsigned k) {
+    static const char* const names[] = {"broadcast", "prune", "i_have", "ignored_i_have", "graft", "pt_dropped",
+                                        "delivered_new", "updates", "delivered_live", "live", "outstanding_live",
+                                        "pt_kernel_us"};
+    for (unsigned i = 0; i < k; i++) {
+        const psim_c3_stats* x = &st[i];
+        const uint64_t v[12] = {x->pt_sent[1], x->pt_sent[2], x->pt_sent[3], x->pt_sent[4], x->pt_sent[5],
+                                x->pt_dropped, x->delivered_new, x->updates, x->delivered_live, x->live,
+                                x->outstanding_live, (uint64_t)(x->pt_kernel_ms * 1000.0)};
+        maps[i] = enif_make_tuple2(env, kv_map(env, names, v, 12), scamp_stats_term(env, &x->scamp));
+    }
+    return enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
+}
+
+/* c3_run(Sim, CrashOff, CrashV, JoinOff, JoinV, JoinC, HbEvery, Root) -> {ok, [Stats]}
+ * (psim_c3_run: R rounds of churn in one call; the offsets are <<u32>> of R + 1
+ * entries, the lists <<u32>> as in c3_crash / c3_join; Stats as c3_step's) */
+static ERL_NIF_TERM nif_c3_run(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    sim_res* r;
+    unsigned hb, root;
+    if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[6], &hb) || !enif_get_uint(env, argv[7], &root))
+        return enif_make_badarg(env);
+    size_t n[5] = {0, 0, 0, 0, 0};
+    uint32_t* b[5];
+    int ok = 1;
+    for (int i = 0; i < 5; i++) {
+        b[i] = u32_copy(env, argv[1 + i], &n[i]);
+        ok &= b[i] != NULL;
+    }
+    const size_t k = n[0] ? n[0] - 1 : 0;
+    ok = ok && n[0] >= 1 && n[2] == n[0] && n[4] == n[3] && k <= 1000000 && b[0][k] - b[0][0] <= n[1] &&
+         b[2][k] - b[2][0] <= n[3];
+    psim_c3_stats* st = ok && k ? (psim_c3_stats*)enif_alloc(k * sizeof(psim_c3_stats)) : NULL;
+    ERL_NIF_TERM* maps = ok && k ? (ERL_NIF_TERM*)enif_alloc(k * sizeof(ERL_NIF_TERM)) : NULL;
+    ERL_NIF_TERM out;
+    if (!ok) {
+        out = enif_make_badarg(env);
+    } else if (k && (!st || !maps)) {
+        out = err(env, PSIM_ENOMEM);
+    } else {
+        enif_mutex_lock(r->mu);
+        int rc = psim_c3_run(r->h, (uint32_t)k, b[0], b[1], b[2], b[3], b[4], hb, root, st, k);
+        enif_mutex_unlock(r->mu);
+        out = rc == PSIM_OK ? c3_stats_ok(env, st, maps, (unsigned)k) : err(env, rc);
+    }
+    for (int i = 0; i < 5; i++)
+        if (b[i]) enif_free(b[i]);
+    if (st) enif_free(st);
+    if (maps) enif_free(maps);
+    return out;
+}
+
 /* c3_step(Sim, Rounds) -> {ok, [StatsMap]} (both protocols' counters) */
 static ERL_NIF_TERM nif_c3_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     (void)argc;
@@ -1315,20 +1369,7 @@ static ERL_NIF_TERM nif_c3_step(ErlNifEnv* env, int argc, const ERL_NIF_TERM arg
     enif_mutex_lock(r->mu);
     int rc = psim_c3_step(r->h, k, st, k);
     enif_mutex_unlock(r->mu);
-    ERL_NIF_TERM out = err(env, rc);
-    if (rc == PSIM_OK) {
-        static const char* const names[] = {"broadcast", "prune", "i_have", "ignored_i_have", "graft", "pt_dropped",
-                                            "delivered_new", "updates", "delivered_live", "live", "outstanding_live",
-                                            "pt_kernel_us"};
-        for (unsigned i = 0; i < k; i++) {
-            const psim_c3_stats* x = &st[i];
-            const uint64_t v[12] = {x->pt_sent[1], x->pt_sent[2], x->pt_sent[3], x->pt_sent[4], x->pt_sent[5],
-                                    x->pt_dropped, x->delivered_new, x->updates, x->delivered_live, x->live,
-                                    x->outstanding_live, (uint64_t)(x->pt_kernel_ms * 1000.0)};
-            maps[i] = enif_make_tuple2(env, kv_map(env, names, v, 12), scamp_stats_term(env, &x->scamp));
-        }
-        out = enif_make_tuple2(env, mk_atom(env, "ok"), stats_list(env, maps, k));
-    }
+    ERL_NIF_TERM out = rc == PSIM_OK ? c3_stats_ok(env, st, maps, k) : err(env, rc);
     enif_free(st);
     enif_free(maps);
     return out;
@@ -1734,6 +1775,7 @@ static ErlNifFunc funcs[] = {
     {"c3_crash", 2, nif_c3_crash, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_heartbeat", 2, nif_c3_heartbeat, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"c3_step", 2, nif_c3_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"c3_run", 8, nif_c3_run, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"causal_setup", 6, nif_causal_setup, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"causal_step", 2, nif_causal_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"causal_clocks", 1, nif_causal_clocks, ERL_NIF_DIRTY_JOB_CPU_BOUND},

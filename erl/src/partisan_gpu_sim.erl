@@ -17,7 +17,7 @@
          scamp_messages/1, scamp_messages_from/2, scamp_take/2, scamp_put/2,
          fm_setup/4, fm_join/3, fm_leave/3, fm_step/2, fm_state/1, fm_tokens/1,
          fm_messages/1, fm_messages_from/2, fm_take/2, fm_put/2,
-         c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2,
+         c3_setup/4, c3_join/3, c3_crash/2, c3_heartbeat/2, c3_step/2, c3_run/8,
          causal_setup/6, causal_step/2, causal_clocks/1,
          rccl_unique_id/0, shard_init_rccl/4, shard_broadcast/2, shard_run/2,
          demers_shard_setup/7, demers_shard_run/2, causal_shard_setup/8, causal_shard_step/2]).
@@ -240,6 +240,10 @@ c3_crash(_Sim, _Vs) -> erlang:nif_error(nif_not_loaded).
 c3_heartbeat(_Sim, _Root) -> erlang:nif_error(nif_not_loaded).
 -spec c3_step(sim(), pos_integer()) -> {ok, [{map(), map()}]} | error().
 c3_step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+%% R churn rounds in one call (psim_c3_run): offsets are <<u32>> of R + 1 entries
+-spec c3_run(sim(), binary(), binary(), binary(), binary(), binary(), non_neg_integer(), non_neg_integer()) ->
+          {ok, [{map(), map()}]} | error().
+c3_run(_Sim, _CrashOff, _CrashV, _JoinOff, _JoinV, _JoinC, _HbEvery, _Root) -> erlang:nif_error(nif_not_loaded).
 
 %% ---- causal delivery (psim_causal_*) ------------------------------------------
 -spec causal_setup(sim(), pos_integer(), 1..64, pos_integer(), pos_integer(), pos_integer()) -> ok | error().

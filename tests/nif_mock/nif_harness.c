@@ -499,8 +499,17 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 20; i++) crash[i] = 100 + 17 * i;
         want_ok("c3_crash", call("c3_crash", 2, A(sim, u32s(crash, 20))));
         want_ok_tuple("c3_step", call("c3_step", 2, A(sim, mock_uint(2))));
-        fprintf(g_out, ", \"c3\": {\"n\": %u, \"delivered_live\": %llu, \"live\": %llu}", n, (unsigned long long)dl,
-               (unsigned long long)live);
+        /* c3_run: 3 rounds in one call -- round 0 a heartbeat and a crash list, round 1 those vertices rejoin */
+        uint32_t coff[4] = {0, 10, 10, 10}, joff[4] = {0, 0, 10, 10}, cv[10], jv[10], jc[10];
+        for (int i = 0; i < 10; i++) { cv[i] = jv[i] = 1000 + 31 * i; jc[i] = 7; }
+        ERL_NIF_TERM rs = mock_elem(want_ok_tuple("c3_run", call("c3_run", 8, A(sim, u32s(coff, 4), u32s(cv, 10),
+                                                                                 u32s(joff, 4), u32s(jv, 10), u32s(jc, 10),
+                                                                                 mock_uint(3), mock_uint(0)))), 1);
+        uint64_t run_live = 0;
+        mock_map_get(mock_elem(mock_list_nth(rs, 2), 0), "live", &run_live);
+        fprintf(g_out, ", \"c3\": {\"n\": %u, \"delivered_live\": %llu, \"live\": %llu, \"run_rounds\": %zu, "
+                "\"run_live\": %llu}", n, (unsigned long long)dl, (unsigned long long)live, mock_list_len(rs),
+                (unsigned long long)run_live);
     }
     /* ---- causal delivery ------------------------------------------------------ */
     {

@@ -130,6 +130,7 @@ def test_nif_harness_on_gpu(tmp_path):
     _check_scamp_wire(rep["scamp_wire"])
     _check_fm_wire(rep["fm_wire"])
     assert 0 < rep["c3"]["delivered_live"] <= rep["c3"]["live"]
+    assert rep["c3"]["run_rounds"] == 3 and rep["c3"]["run_live"] == rep["c3"]["n"]   # c3_run: crashed, then rejoined
     assert rep["causal"]["delivered"] > 0
     assert rep["causal_shard_rccl_world1"]["delivered"] == rep["causal"]["delivered"]
     assert rep["vclock_merge"] == [3, 1, 4]
