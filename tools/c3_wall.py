@@ -2,9 +2,10 @@
 driver call (crash, join, step, heartbeat) against the device time of the
 round's SCAMP and Plumtree kernels -- where a C3 round's wall time goes.
 
-With a third argument "run" the churn rounds go through one psim_c3_run call
-(C3Cluster.run: no host wait between rounds; the churn is drawn beforehand
-and not timed).
+Churn rounds 0 .. R-1 run untimed, rounds R .. 2R-1 are timed.  With a third
+argument "run" each R rounds go through one psim_c3_run call (C3Cluster.run:
+no host wait between rounds; the churn is drawn beforehand and not timed,
+the flat plan's build is reported apart).
 
 usage: python tools/c3_wall.py [n] [rounds] [run]"""
 import json
@@ -55,10 +56,18 @@ def main():
               flush=True)
         sim.close()
         return
+    for i in range(rounds):            # churn rounds 0 .. rounds-1 untimed, as the run mode's first call
+        if i % 10 == 0:
+            g.heartbeat(0)
+        v, cc = churn_batch(n, seed, i)
+        keep = v != 0
+        g.crash(v[keep])
+        g.join(v[keep], cc[keep])
+        g.step(1)
     t = {"heartbeat": 0.0, "churn_draw": 0.0, "crash": 0.0, "join": 0.0, "step": 0.0}
     sc_ms = pt_ms = 0.0
     t0 = time.perf_counter()
-    for i in range(rounds):
+    for i in range(rounds, 2 * rounds):
         a = time.perf_counter()
         if i % 10 == 0:
             g.heartbeat(0)
