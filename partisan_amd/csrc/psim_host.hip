@@ -2066,6 +2066,11 @@ int psim_load_csr(psim_handle* h, uint32_t n, const uint64_t* row_ptr, const uin
     h->Ed = Ed;
     h->ell = ell;
     h->ell_grid = ell ? ell_round_grid(ell, h->device) : 0u;
+#ifdef PSIM_ELL_GRID_ENV
+    // A/B builds only (make variant DEFS=-DPSIM_ELL_GRID_ENV): the round kernel's grid from the
+    // environment (0: one workgroup per chunk); the grid changes no result, only the schedule
+    if (ell && getenv("PSIM_ELL_GRID")) h->ell_grid = uint32_t(strtoul(getenv("PSIM_ELL_GRID"), nullptr, 10));
+#endif
     {
         uint64_t mx = 0;                               // the same on every shard: the whole overlay
         for (uint32_t v = 0; v < n; v++) mx = std::max<uint64_t>(mx, rp[v + 1] - rp[v]);
