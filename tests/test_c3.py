@@ -213,6 +213,32 @@ def test_gpu_c3_run_equals_per_round_calls():
 
 
 @pytest.mark.gpu
+def test_gpu_c3_run_rejects_bad_lists():
+    """psim_c3_run checks a round's lists before it enqueues that round:
+    offsets that go backwards and a crash list naming a vertex twice are
+    PSIM_EINVAL with nothing of that round run, and the handle stays usable."""
+    import partisan_amd as pa
+    from partisan_amd._lib import PsimError
+    n = 500
+    sim = pa.Simulator(device=0, seed=SEED)
+    g = pa.c3.C3Cluster(sim, n, c=5, periodic_rounds=10)
+    for v, cc in waves(n):
+        g.join(v, cc)
+        g.step(3)
+    co, cv, jo, jv, jc = g.plan([np.array([5, 6], np.uint32)], [(np.zeros(0, np.uint32), np.zeros(0, np.uint32))])
+    with pytest.raises(PsimError) as ei:
+        g.run(plan=(np.array([2, 1], np.uint32), cv, jo, jv, jc))
+    assert ei.value.name == "PSIM_EINVAL"
+    with pytest.raises(PsimError) as ei:
+        g.run([np.array([7, 9, 7], np.uint32)], [(np.zeros(0, np.uint32), np.zeros(0, np.uint32))])
+    assert ei.value.name == "PSIM_EINVAL"
+    st = g.run([np.array([7, 9], np.uint32)], [(np.array([7, 9], np.uint32), np.array([1, 2], np.uint32))],
+               heartbeat_every=1, root=0)
+    assert len(st) == 1 and st[0]["live"] == n
+    sim.close()
+
+
+@pytest.mark.gpu
 def test_gpu_large_crash_list_resets_every_vertex():
     """A crash list larger than any before grows the device list buffer; the
     upload must land after the buffer's zero fill (regression: the fill ran
