@@ -766,7 +766,9 @@ int  psim_c3_step(psim_handle* h, uint32_t rounds, psim_c3_stats* stats, size_t 
  * [join_off[i], join_off[i+1]), then one psim_c3_step round -- the same
  * calls and the same result as making them one by one, without the host
  * waiting for the device between rounds (offsets: rounds + 1 entries each).
- * stats[i] is round i's; the first failing round's error is returned. */
+ * stats[i] is round i's; the first failing round's error is returned.
+ * Joins made by psim_c3_join since the last round: PSIM_ESTATE (step first,
+ * or pass them in round 0's lists). */
 int  psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, const uint32_t* crash_v,
                  const uint32_t* join_off, const uint32_t* join_v, const uint32_t* join_c, uint32_t hb_every,
                  uint32_t hb_root, psim_c3_stats* stats, size_t cap);

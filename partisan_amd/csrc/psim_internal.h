@@ -603,6 +603,7 @@ int scamp_round_launch_to(psim_handle* h, const ScLaunch& o, uint64_t* round);
 // (range, duplicates); the restart of a crash list already on the device
 int scamp_check_calls(psim_handle* h, const uint32_t* v, const uint32_t* x, size_t k, uint32_t* sorted);
 int scamp_check_crash(psim_handle* h, const uint32_t* v, size_t k);
+size_t scamp_calls_pending(psim_handle* h);   // joins / leaves made since the last round
 int scamp_crash_dev(psim_handle* h, const uint32_t* dv, size_t k);
 int scamp_round_report(psim_handle* h, const unsigned long long* rows, float ms, uint64_t round, psim_scamp_stats* out);
 hipError_t launch_sc_init(const ScArgs& a, const uint32_t* list, uint32_t k, hipStream_t s);

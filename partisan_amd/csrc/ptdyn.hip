@@ -827,6 +827,9 @@ int psim_c3_run(psim_handle* h, uint32_t rounds, const uint32_t* crash_off, cons
     PdState* s = pd_of(h);
     if (!s) return handle_fail(h, PSIM_ESTATE, "psim_c3_setup not called");
     if (hb_every && hb_root >= s->n) return handle_fail(h, PSIM_EINVAL, "heartbeat root %u >= n %u", hb_root, s->n);
+    if (scamp_calls_pending(h))
+        return handle_fail(h, PSIM_ESTATE, "c3 run: %zu joins made since the last round (step first, or pass them "
+                           "in round 0's lists)", scamp_calls_pending(h));
     if (!rounds) return PSIM_OK;
     size_t words = 0;
     for (uint32_t i = 0; i < rounds; i++) {

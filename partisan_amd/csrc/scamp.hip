@@ -879,6 +879,11 @@ int scamp_check_calls(psim_handle* h, const uint32_t* v, const uint32_t* x, size
     return PSIM_OK;
 }
 
+size_t scamp_calls_pending(psim_handle* h) {
+    ScState* s = sc_of(h);
+    return s ? s->cv.size() : 0;
+}
+
 int scamp_check_crash(psim_handle* h, const uint32_t* v, size_t k) {
     ScState* s = sc_of(h);
     if (k && !v) return PSIM_EINVAL;

@@ -232,6 +232,11 @@ def test_gpu_c3_run_rejects_bad_lists():
     with pytest.raises(PsimError) as ei:
         g.run([np.array([7, 9, 7], np.uint32)], [(np.zeros(0, np.uint32), np.zeros(0, np.uint32))])
     assert ei.value.name == "PSIM_EINVAL"
+    g.join(np.array([11], np.uint32), np.array([3], np.uint32))      # a join not yet stepped
+    with pytest.raises(PsimError) as ei:
+        g.run([np.zeros(0, np.uint32)], [(np.zeros(0, np.uint32), np.zeros(0, np.uint32))])
+    assert ei.value.name == "PSIM_ESTATE"
+    g.step(1)
     st = g.run([np.array([7, 9], np.uint32)], [(np.array([7, 9], np.uint32), np.array([1, 2], np.uint32))],
                heartbeat_every=1, root=0)
     assert len(st) == 1 and st[0]["live"] == n
