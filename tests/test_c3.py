@@ -52,6 +52,21 @@ def test_c3_oracle_repair_and_churn():
     c.step(3)
 
 
+def test_c3_run_plan_layout():
+    """C3Cluster.plan: per-round lists flattened into psim_c3_run's arrays --
+    offsets of R + 1 entries from 0, lists concatenated in round order, join
+    vertices and contacts aligned; empty rounds are empty ranges."""
+    import partisan_amd as pa
+    crashes = [np.array([4, 2], np.uint32), np.zeros(0, np.uint32), np.array([9], np.int64)]
+    joins = [(np.array([4, 2]), np.array([1, 1])), (np.zeros(0), np.zeros(0)), (np.array([9]), np.array([3]))]
+    co, cv, jo, jv, jc = pa.c3.C3Cluster.plan(crashes, joins)
+    assert co.tolist() == [0, 2, 2, 3] and cv.tolist() == [4, 2, 9]
+    assert jo.tolist() == [0, 2, 2, 3] and jv.tolist() == [4, 2, 9] and jc.tolist() == [1, 1, 3]
+    assert all(x.dtype == np.uint32 and x.flags.c_contiguous for x in (co, cv, jo, jv, jc))
+    with pytest.raises(ValueError):
+        pa.c3.C3Cluster.plan(crashes, joins[:2])
+
+
 def _compare(g, o, n, root, mono):
     pv, npv, iv, niv = g.scamp.views()
     od = o.pt.delivered(root, mono) if mono else np.zeros(n, np.uint8)
